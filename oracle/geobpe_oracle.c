@@ -1,0 +1,594 @@
+/*
+ * geobpe_oracle.c -- CPU restatement of the reference GeoBPE merge loop.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load this library, and only as the checker /
+ * the timed CPU baseline.  The product path (pt-bpe_amd/) never links it.
+ *
+ * Parity: pinned against the tests/golden fixtures, which were produced by the
+ * reference itself (tests/golden/make_golden.py).
+ *
+ * What it restates (scoped mode: res_init=True, p_min_size=inf, glue_opt=False,
+ * bin_strategy=histogram, std_bonds=True, single bin grid):
+ *
+ *  - bin()   foldingdiff/bpe.py:1431-1474  full adjacent-pair histogram keyed by
+ *            the quantised CONTENT of the span (compute_geo_key, bpe.py:1192-1299);
+ *  - step()  foldingdiff/bpe.py:1792-2166  argmax = max count, ties -> smallest
+ *            json.dumps(sort_keys=True) key string (SortedDict priority
+ *            (True, -count, key), bpe.py:1469-1471 / 2126-2131); the new token id is
+ *            len(_tokens) (bpe.py:1857); occurrences are visited in sorted
+ *            (row, pos) order, skipping ones a previous merge of the same step
+ *            removed (the overlap check, bpe.py:1905-1916); per merge the left /
+ *            right neighbour pairs are removed and re-added (bpe.py:1924-2006);
+ *            touched keys get their priority refreshed once per step (diff_count,
+ *            bpe.py:2078-2138) and count-0 keys are dropped;
+ *  - tokenize()+quantize()  foldingdiff/tokenizer.py:379-392, bpe.py:918-956:
+ *            per token: id, then (if not last) K+B+omega, K+2B+phi, K+cnca.
+ *
+ * Content model.  A residue symbol is  tau*B^2 + cac1n*B + psi  (or B^3 + tau for
+ * the chain's last residue, whose token geometry has no CA:C:1N/psi, tokenizer.py
+ * token_geo with l=2); a junction symbol is  omega*B^2 + cnca*B + phi(next).  The
+ * content of a span of residues a..b is R_a G_a R_{a+1} ... G_{b-1} R_b, and two
+ * spans have equal reference key strings iff their contents are equal.
+ *
+ * Keys are interned exactly (hash + full symbol compare).  The JSON string used
+ * for the tie-break is rendered from the content (json_render below) exactly as
+ * json.dumps(geo, sort_keys=True) renders the reference's geo dict.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+typedef struct {
+  int32_t *a;
+  int64_t n, cap;
+} ivec;
+
+static void iv_push(ivec *v, int32_t x) {
+  if (v->n == v->cap) {
+    v->cap = v->cap ? v->cap * 2 : 4;
+    v->a = (int32_t *)realloc(v->a, (size_t)v->cap * sizeof(int32_t));
+  }
+  v->a[v->n++] = x;
+}
+
+#define PREFIX 64
+
+typedef struct {
+  /* corpus */
+  int64_t R, nrows;
+  int32_t B, B2, B3;
+  const int64_t *row_off;
+  int32_t *rsym, *gsym;
+  /* tokens, indexed by the start residue of the token */
+  int32_t *tid, *tlen, *tnext, *tprev;
+  int32_t *pair_key; /* key of the pair (token at g, next token) or -1 */
+  int32_t *occ_pos;  /* position of g in keys[pair_key[g]].occ */
+  /* vocab: id -> content (symbol sequence) */
+  ivec vsyms;
+  int64_t *voff;     /* content of id v = vsyms.a[voff[v] .. voff[v+1]) */
+  int32_t *vnres;
+  uint64_t *vhash;
+  int64_t K, Kcap;
+  /* keys */
+  int32_t *kL, *kG, *kR, *knres, *kcount;
+  uint64_t *khash;
+  char *kprefix;
+  ivec *kocc;
+  int64_t U, Ucap;
+  /* content hash table: slot -> key index + 1 (0 = empty) */
+  int32_t *ht;
+  int64_t htcap;
+  /* powers of the hash base */
+  uint64_t *pw;
+  int64_t pwn;
+  /* priority heap of (count, key) with lazy invalidation */
+  int32_t *hc, *hk;
+  int64_t hn, hcap;
+  /* per-step scratch */
+  int32_t *touched_flag;
+  ivec touched;
+  int64_t step;
+  /* json scratch */
+  char *jbufA, *jbufB;
+  int64_t jcap;
+  int error;
+} oracle_t;
+
+static const uint64_t HBASE = 0x9E3779B97F4A7C15ULL;
+
+/* ---------------- content accessors ---------------- */
+
+static inline int32_t vsym(const oracle_t *o, int32_t v, int64_t i) { return o->vsyms.a[o->voff[v] + i]; }
+
+/* symbol i of key k's content: content(L) g content(R) */
+static inline int32_t ksym(const oracle_t *o, int32_t k, int64_t i) {
+  int64_t nl = 2 * (int64_t)o->vnres[o->kL[k]] - 1;
+  if (i < nl) return vsym(o, o->kL[k], i);
+  if (i == nl) return o->kG[k];
+  return vsym(o, o->kR[k], i - nl - 1);
+}
+
+static inline uint64_t pair_hash(const oracle_t *o, int32_t L, int32_t g, int32_t Rr) {
+  int64_t nr = 2 * (int64_t)o->vnres[Rr] - 1;
+  return o->vhash[L] * o->pw[nr + 1] + (uint64_t)(g + 1) * o->pw[nr] + o->vhash[Rr];
+}
+
+/* ---------------- JSON rendering (json.dumps(geo, sort_keys=True)) ----------- */
+
+typedef struct {
+  char *p;
+  int64_t n, cap;
+} sbuf;
+
+static void sb_put(sbuf *s, const char *x, int64_t m) {
+  if (s->n + m + 1 > s->cap) {
+    while (s->n + m + 1 > s->cap) s->cap = s->cap ? s->cap * 2 : 256;
+    s->p = (char *)realloc(s->p, (size_t)s->cap);
+  }
+  memcpy(s->p + s->n, x, (size_t)m);
+  s->n += m;
+  s->p[s->n] = 0;
+}
+static void sb_int(sbuf *s, int32_t v) {
+  char t[16];
+  int m = snprintf(t, sizeof t, "%d", v);
+  sb_put(s, t, m);
+}
+
+typedef int32_t (*sym_fn)(const oracle_t *, int32_t, int64_t);
+
+/* Render the key string for a content of nres residues.  Field order is the
+ * sorted key order of the reference's geo dict:
+ * 0C:1N, C:1N:1CA, CA:C, CA:C:1N, N:CA, omega, phi, psi, tau. */
+static void json_render(const oracle_t *o, sym_fn f, int32_t obj, int32_t nres, sbuf *s, int64_t limit) {
+  const int32_t B = o->B, B2 = o->B2, B3 = o->B3;
+  int32_t last = f(o, obj, 2 * (int64_t)nres - 2);
+  int lam = last >= B3;
+  int32_t r = nres;
+  s->n = 0;
+#define STOP if (limit > 0 && s->n >= limit) return
+#define ZEROS(name, cnt)                         \
+  do {                                           \
+    sb_put(s, "\"" name "\": [", strlen(name) + 5); \
+    for (int32_t q = 0; q < (cnt); q++) {        \
+      if (q) sb_put(s, ", ", 2);                 \
+      sb_put(s, "0", 1);                         \
+    }                                            \
+    sb_put(s, "]", 1);                           \
+  } while (0)
+  sb_put(s, "{", 1);
+  ZEROS("0C:1N", r - lam);
+  STOP;
+  sb_put(s, ", \"C:1N:1CA\": [", 15);
+  for (int32_t j = 0; j < r - 1; j++) {
+    if (j) sb_put(s, ", ", 2);
+    sb_int(s, f(o, obj, 2 * (int64_t)j + 1) / B % B);
+    STOP;
+  }
+  sb_put(s, "], ", 3);
+  ZEROS("CA:C", r);
+  sb_put(s, ", \"CA:C:1N\": [", 14);
+  for (int32_t j = 0; j < r - lam; j++) {
+    if (j) sb_put(s, ", ", 2);
+    sb_int(s, f(o, obj, 2 * (int64_t)j) / B % B);
+    STOP;
+  }
+  sb_put(s, "], ", 3);
+  ZEROS("N:CA", r);
+  sb_put(s, ", \"omega\": [", 12);
+  for (int32_t j = 0; j < r - 1; j++) {
+    if (j) sb_put(s, ", ", 2);
+    sb_int(s, f(o, obj, 2 * (int64_t)j + 1) / B2);
+  }
+  sb_put(s, "], \"phi\": [", 11);
+  for (int32_t j = 0; j < r - 1; j++) {
+    if (j) sb_put(s, ", ", 2);
+    sb_int(s, f(o, obj, 2 * (int64_t)j + 1) % B);
+  }
+  sb_put(s, "], \"psi\": [", 11);
+  for (int32_t j = 0; j < r - lam; j++) {
+    if (j) sb_put(s, ", ", 2);
+    sb_int(s, f(o, obj, 2 * (int64_t)j) % B);
+  }
+  sb_put(s, "], \"tau\": [", 11);
+  for (int32_t j = 0; j < r; j++) {
+    if (j) sb_put(s, ", ", 2);
+    int32_t x = f(o, obj, 2 * (int64_t)j);
+    sb_int(s, x >= B3 ? x - B3 : x / B2);
+  }
+  sb_put(s, "]}", 2);
+#undef STOP
+#undef ZEROS
+}
+
+static sbuf g_sa, g_sb;
+
+static void key_prefix(oracle_t *o, int32_t k) {
+  json_render(o, ksym, k, o->knres[k], &g_sa, PREFIX);
+  char *dst = o->kprefix + (int64_t)k * PREFIX;
+  memset(dst, 0, PREFIX);
+  memcpy(dst, g_sa.p, (size_t)(g_sa.n < PREFIX ? g_sa.n : PREFIX));
+}
+
+/* strcmp of the two keys' JSON strings */
+static int key_json_cmp(oracle_t *o, int32_t a, int32_t b) {
+  int c = memcmp(o->kprefix + (int64_t)a * PREFIX, o->kprefix + (int64_t)b * PREFIX, PREFIX);
+  if (c) return c;
+  json_render(o, ksym, a, o->knres[a], &g_sa, 0);
+  json_render(o, ksym, b, o->knres[b], &g_sb, 0);
+  return strcmp(g_sa.p, g_sb.p);
+}
+
+/* priority order of the reference's SortedDict: larger count first, then the
+ * smaller key string */
+static int better(oracle_t *o, int32_t ca, int32_t ka, int32_t cb, int32_t kb) {
+  if (ca != cb) return ca > cb;
+  if (ka == kb) return 0;
+  return key_json_cmp(o, ka, kb) < 0;
+}
+
+static void heap_push(oracle_t *o, int32_t c, int32_t k) {
+  if (o->hn == o->hcap) {
+    o->hcap = o->hcap ? o->hcap * 2 : 1024;
+    o->hc = (int32_t *)realloc(o->hc, (size_t)o->hcap * 4);
+    o->hk = (int32_t *)realloc(o->hk, (size_t)o->hcap * 4);
+  }
+  int64_t i = o->hn++;
+  while (i > 0) {
+    int64_t p = (i - 1) / 2;
+    if (!better(o, c, k, o->hc[p], o->hk[p])) break;
+    o->hc[i] = o->hc[p];
+    o->hk[i] = o->hk[p];
+    i = p;
+  }
+  o->hc[i] = c;
+  o->hk[i] = k;
+}
+
+static void heap_pop(oracle_t *o) {
+  int32_t c = o->hc[o->hn - 1], k = o->hk[o->hn - 1];
+  o->hn--;
+  int64_t i = 0;
+  for (;;) {
+    int64_t l = 2 * i + 1, r = l + 1, m = i;
+    int32_t mc = c, mk = k;
+    if (l < o->hn && better(o, o->hc[l], o->hk[l], mc, mk)) { m = l; mc = o->hc[l]; mk = o->hk[l]; }
+    if (r < o->hn && better(o, o->hc[r], o->hk[r], mc, mk)) { m = r; }
+    if (m == i) break;
+    o->hc[i] = o->hc[m];
+    o->hk[i] = o->hk[m];
+    i = m;
+  }
+  if (o->hn > 0) {
+    o->hc[i] = c;
+    o->hk[i] = k;
+  }
+}
+
+/* ---------------- vocab / keys ---------------- */
+
+static void ensure_pw(oracle_t *o, int64_t n) {
+  if (n < o->pwn) return;
+  int64_t m = o->pwn ? o->pwn : 64;
+  while (m <= n) m *= 2;
+  o->pw = (uint64_t *)realloc(o->pw, (size_t)m * 8);
+  if (o->pwn == 0) o->pw[0] = 1;
+  for (int64_t i = (o->pwn ? o->pwn : 1); i < m; i++) o->pw[i] = o->pw[i - 1] * HBASE;
+  o->pwn = m;
+}
+
+static int32_t vocab_add_from(oracle_t *o, sym_fn f, int32_t obj, int32_t nres, uint64_t h) {
+  if (o->K + 1 >= o->Kcap) {
+    o->Kcap = o->Kcap ? o->Kcap * 2 : 256;
+    o->voff = (int64_t *)realloc(o->voff, (size_t)(o->Kcap + 1) * 8);
+    o->vnres = (int32_t *)realloc(o->vnres, (size_t)o->Kcap * 4);
+    o->vhash = (uint64_t *)realloc(o->vhash, (size_t)o->Kcap * 8);
+  }
+  int32_t v = (int32_t)o->K++;
+  o->voff[v] = o->vsyms.n;
+  for (int64_t i = 0; i < 2 * (int64_t)nres - 1; i++) iv_push(&o->vsyms, f(o, obj, i));
+  o->voff[v + 1] = o->vsyms.n;
+  o->vnres[v] = nres;
+  o->vhash[v] = h;
+  return v;
+}
+
+static int32_t rsym_fn(const oracle_t *o, int32_t g, int64_t i) { (void)i; return o->rsym[g]; }
+
+static int same_content(const oracle_t *o, int32_t k, int32_t L, int32_t g, int32_t Rr) {
+  int32_t nres = o->vnres[L] + o->vnres[Rr];
+  if (o->knres[k] != nres) return 0;
+  /* fast path: identical decomposition */
+  if (o->kL[k] == L && o->kG[k] == g && o->kR[k] == Rr) return 1;
+  int64_t nl = 2 * (int64_t)o->vnres[L] - 1;
+  int64_t ns = 2 * (int64_t)nres - 1;
+  for (int64_t i = 0; i < ns; i++) {
+    int32_t s = i < nl ? vsym(o, L, i) : (i == nl ? g : vsym(o, Rr, i - nl - 1));
+    if (s != ksym(o, k, i)) return 0;
+  }
+  return 1;
+}
+
+static void ht_grow(oracle_t *o) {
+  int64_t ncap = o->htcap ? o->htcap * 2 : 1 << 16;
+  int32_t *nt = (int32_t *)calloc((size_t)ncap, 4);
+  for (int64_t k = 0; k < o->U; k++) {
+    uint64_t s = (o->khash[k] * 0xD6E8FEB86659FD93ULL) >> 17;
+    for (;; s++) {
+      int64_t j = (int64_t)(s & (uint64_t)(ncap - 1));
+      if (!nt[j]) { nt[j] = (int32_t)k + 1; break; }
+    }
+  }
+  free(o->ht);
+  o->ht = nt;
+  o->htcap = ncap;
+}
+
+/* intern the content L g R, returning its key index */
+static int32_t key_get(oracle_t *o, int32_t L, int32_t g, int32_t Rr) {
+  uint64_t h = pair_hash(o, L, g, Rr);
+  if (2 * (o->U + 1) > o->htcap) ht_grow(o);
+  uint64_t s = (h * 0xD6E8FEB86659FD93ULL) >> 17;
+  for (;; s++) {
+    int64_t j = (int64_t)(s & (uint64_t)(o->htcap - 1));
+    int32_t e = o->ht[j];
+    if (!e) {
+      if (o->U == o->Ucap) {
+        o->Ucap = o->Ucap ? o->Ucap * 2 : 4096;
+        o->kL = (int32_t *)realloc(o->kL, (size_t)o->Ucap * 4);
+        o->kG = (int32_t *)realloc(o->kG, (size_t)o->Ucap * 4);
+        o->kR = (int32_t *)realloc(o->kR, (size_t)o->Ucap * 4);
+        o->knres = (int32_t *)realloc(o->knres, (size_t)o->Ucap * 4);
+        o->kcount = (int32_t *)realloc(o->kcount, (size_t)o->Ucap * 4);
+        o->khash = (uint64_t *)realloc(o->khash, (size_t)o->Ucap * 8);
+        o->kprefix = (char *)realloc(o->kprefix, (size_t)o->Ucap * PREFIX);
+        o->kocc = (ivec *)realloc(o->kocc, (size_t)o->Ucap * sizeof(ivec));
+        o->touched_flag = (int32_t *)realloc(o->touched_flag, (size_t)o->Ucap * 4);
+      }
+      int32_t k = (int32_t)o->U++;
+      o->kL[k] = L; o->kG[k] = g; o->kR[k] = Rr;
+      o->knres[k] = o->vnres[L] + o->vnres[Rr];
+      o->kcount[k] = 0;
+      o->khash[k] = h;
+      memset(&o->kocc[k], 0, sizeof(ivec));
+      o->touched_flag[k] = 0;
+      key_prefix(o, k);
+      o->ht[j] = k + 1;
+      return k;
+    }
+    int32_t k = e - 1;
+    if (o->khash[k] == h && same_content(o, k, L, g, Rr)) return k;
+  }
+}
+
+static void touch(oracle_t *o, int32_t k) {
+  if (!o->touched_flag[k]) { o->touched_flag[k] = 1; iv_push(&o->touched, k); }
+}
+
+/* add the pair (token at a, its next token) */
+static void pair_add(oracle_t *o, int32_t a) {
+  int32_t b = o->tnext[a];
+  int32_t g = o->gsym[a + o->tlen[a] - 1];
+  int32_t k = key_get(o, o->tid[a], g, o->tid[b]);
+  o->pair_key[a] = k;
+  o->occ_pos[a] = (int32_t)o->kocc[k].n;
+  iv_push(&o->kocc[k], a);
+  o->kcount[k]++;
+  touch(o, k);
+}
+
+static void pair_remove(oracle_t *o, int32_t a) {
+  int32_t k = o->pair_key[a];
+  ivec *v = &o->kocc[k];
+  int32_t p = o->occ_pos[a];
+  int32_t last = v->a[v->n - 1];
+  v->a[p] = last;
+  o->occ_pos[last] = p;
+  v->n--;
+  o->pair_key[a] = -1;
+  o->kcount[k]--;
+  touch(o, k);
+}
+
+static void flush_touched(oracle_t *o) {
+  for (int64_t i = 0; i < o->touched.n; i++) {
+    int32_t k = o->touched.a[i];
+    o->touched_flag[k] = 0;
+    if (o->kcount[k] > 0) heap_push(o, o->kcount[k], k);
+  }
+  o->touched.n = 0;
+}
+
+/* ---------------- public API ---------------- */
+
+oracle_t *oracle_create(int64_t nrows, const int64_t *row_off, const int32_t *rsym, const int32_t *gsym,
+                        const int32_t *init_labels, int32_t K0, int32_t B) {
+  oracle_t *o = (oracle_t *)calloc(1, sizeof(oracle_t));
+  o->nrows = nrows;
+  o->R = row_off[nrows];
+  o->B = B; o->B2 = B * B; o->B3 = B * B * B;
+  int64_t R = o->R;
+  o->row_off = (int64_t *)malloc((size_t)(nrows + 1) * 8);
+  memcpy((void *)o->row_off, row_off, (size_t)(nrows + 1) * 8);
+  o->rsym = (int32_t *)malloc((size_t)R * 4 + 4);
+  o->gsym = (int32_t *)malloc((size_t)R * 4 + 4);
+  memcpy(o->rsym, rsym, (size_t)R * 4);
+  memcpy(o->gsym, gsym, (size_t)R * 4);
+  o->tid = (int32_t *)malloc((size_t)R * 4 + 4);
+  o->tlen = (int32_t *)malloc((size_t)R * 4 + 4);
+  o->tnext = (int32_t *)malloc((size_t)R * 4 + 4);
+  o->tprev = (int32_t *)malloc((size_t)R * 4 + 4);
+  o->pair_key = (int32_t *)malloc((size_t)R * 4 + 4);
+  o->occ_pos = (int32_t *)malloc((size_t)R * 4 + 4);
+  int64_t maxlen = 1;
+  for (int64_t r = 0; r < nrows; r++) {
+    int64_t a = row_off[r], b = row_off[r + 1];
+    if (b - a > maxlen) maxlen = b - a;
+    for (int64_t g = a; g < b; g++) {
+      o->tid[g] = init_labels[g];
+      o->tlen[g] = 1;
+      o->tnext[g] = (g + 1 < b) ? (int32_t)(g + 1) : -1;
+      o->tprev[g] = (g > a) ? (int32_t)(g - 1) : -1;
+      o->pair_key[g] = -1;
+    }
+  }
+  ensure_pw(o, 2 * maxlen + 4);
+  /* initial vocab: label v -> the residue symbol of its first appearance
+     (bpe.py:231-261: labels are first-appearance indices of the residue key) */
+  int32_t *first = (int32_t *)malloc((size_t)K0 * 4);
+  for (int32_t v = 0; v < K0; v++) first[v] = -1;
+  for (int64_t g = 0; g < R; g++) {
+    int32_t v = init_labels[g];
+    if (v < 0 || v >= K0) { o->error = 1; continue; }
+    if (first[v] < 0) first[v] = (int32_t)g;
+  }
+  for (int32_t v = 0; v < K0; v++) {
+    if (first[v] < 0) { o->error = 2; vocab_add_from(o, rsym_fn, 0, 1, 0); continue; }
+    vocab_add_from(o, rsym_fn, first[v], 1, (uint64_t)(o->rsym[first[v]] + 1));
+  }
+  free(first);
+  return o;
+}
+
+int oracle_error(oracle_t *o) { return o->error; }
+
+/* BPE.bin(): full pair histogram (bpe.py:1431-1474) */
+void oracle_bin(oracle_t *o) {
+  for (int64_t r = 0; r < o->nrows; r++) {
+    for (int64_t g = o->row_off[r]; g < o->row_off[r + 1]; g = o->tnext[g] < 0 ? o->row_off[r + 1] : o->tnext[g])
+      if (o->tnext[g] >= 0) pair_add(o, (int32_t)g);
+  }
+  flush_touched(o);
+}
+
+/* BPE.step(): returns the new token id, or -1 when no pair is left.
+ * *count receives the winning count, *key the winning key index. */
+int32_t oracle_step(oracle_t *o, int32_t *count, int32_t *key) {
+  int32_t W = -1, c = 0;
+  while (o->hn > 0) {
+    int32_t hc = o->hc[0], hk = o->hk[0];
+    if (o->kcount[hk] == hc && hc > 0) { W = hk; c = hc; break; }
+    heap_pop(o);
+  }
+  if (W < 0) return -1;
+  heap_pop(o);
+  /* _tokens[n] = json.loads(key) (bpe.py:1857-1860) */
+  int32_t n = vocab_add_from(o, ksym, W, o->knres[W], o->khash[W]);
+  /* sorted occurrences (bpe.py:1888-1895): left-token start order == (row, pos) order */
+  ivec occ = {0, 0, 0};
+  for (int64_t i = 0; i < o->kocc[W].n; i++) iv_push(&occ, o->kocc[W].a[i]);
+  int cmp_i32(const void *x, const void *y);
+  qsort(occ.a, (size_t)occ.n, 4, cmp_i32);
+  for (int64_t i = 0; i < occ.n; i++) {
+    int32_t a = occ.a[i];
+    if (o->pair_key[a] != W) continue; /* overlapped by the previous merge (bpe.py:1909-1916) */
+    int32_t b = o->tnext[a];
+    int32_t p = o->tprev[a];
+    int32_t c2 = o->tnext[b];
+    pair_remove(o, a);                 /* step 1 */
+    if (p >= 0) pair_remove(o, p);     /* step 3: left neighbour pair */
+    if (c2 >= 0) pair_remove(o, b);    /* step 4: right neighbour pair */
+    o->tlen[a] += o->tlen[b];          /* step 2: token_pos / bond_to_token */
+    o->tid[a] = n;
+    o->tid[b] = -1;
+    o->tnext[a] = c2;
+    if (c2 >= 0) o->tprev[c2] = a;
+    if (p >= 0) pair_add(o, p);        /* step 5: new neighbour pairs */
+    if (c2 >= 0) pair_add(o, a);
+  }
+  free(occ.a);
+  flush_touched(o);
+  o->step++;
+  if (count) *count = c;
+  if (key) *key = W;
+  return n;
+}
+
+int cmp_i32(const void *x, const void *y) {
+  int32_t a = *(const int32_t *)x, b = *(const int32_t *)y;
+  return (a > b) - (a < b);
+}
+
+/* JSON key string of key k into buf (returns the full length; writes at most cap-1) */
+int64_t oracle_key_json(oracle_t *o, int32_t k, char *buf, int64_t cap) {
+  json_render(o, ksym, k, o->knres[k], &g_sa, 0);
+  if (buf && cap > 0) {
+    int64_t m = g_sa.n < cap - 1 ? g_sa.n : cap - 1;
+    memcpy(buf, g_sa.p, (size_t)m);
+    buf[m] = 0;
+  }
+  return g_sa.n;
+}
+
+int64_t oracle_num_keys(oracle_t *o) { return o->U; }
+int64_t oracle_vocab_size_tokens(oracle_t *o) { return o->K; }
+int32_t oracle_key_count(oracle_t *o, int32_t k) { return o->kcount[k]; }
+int32_t oracle_vocab_nres(oracle_t *o, int32_t v) { return o->vnres[v]; }
+
+/* content symbols of vocab id v (2*nres-1 ints) */
+int64_t oracle_vocab_content(oracle_t *o, int32_t v, int32_t *out) {
+  int64_t m = o->voff[v + 1] - o->voff[v];
+  if (out) memcpy(out, o->vsyms.a + o->voff[v], (size_t)m * 4);
+  return m;
+}
+
+/* segmentation: per row, token (start residue, id) in order; returns #tokens */
+int64_t oracle_segmentation(oracle_t *o, int32_t *start, int32_t *id, int64_t *row_tok_off) {
+  int64_t t = 0;
+  for (int64_t r = 0; r < o->nrows; r++) {
+    if (row_tok_off) row_tok_off[r] = t;
+    int64_t a = o->row_off[r], b = o->row_off[r + 1];
+    for (int64_t g = a; g < b;) {
+      if (start) start[t] = (int32_t)(g - a);
+      if (id) id[t] = o->tid[g];
+      t++;
+      g += o->tlen[g];
+    }
+  }
+  if (row_tok_off) row_tok_off[o->nrows] = t;
+  return t;
+}
+
+/* quantize(tokenize()) for every row (tokenizer.py:379-392, bpe.py:918-956) */
+int64_t oracle_encode(oracle_t *o, int32_t *ids, int64_t *row_id_off) {
+  int64_t t = 0;
+  int32_t K = (int32_t)o->K, B = o->B;
+  for (int64_t r = 0; r < o->nrows; r++) {
+    if (row_id_off) row_id_off[r] = t;
+    int64_t a = o->row_off[r], b = o->row_off[r + 1];
+    for (int64_t g = a; g < b;) {
+      int64_t e = g + o->tlen[g] - 1;
+      if (ids) ids[t] = o->tid[g];
+      t++;
+      if (e + 1 < b) {
+        int32_t gs = o->gsym[e];
+        if (ids) {
+          ids[t] = K + B + gs / o->B2;        /* omega */
+          ids[t + 1] = K + 2 * B + gs % B;    /* phi */
+          ids[t + 2] = K + gs / B % B;        /* C:1N:1CA */
+        }
+        t += 3;
+      }
+      g = e + 1;
+    }
+  }
+  if (row_id_off) row_id_off[o->nrows] = t;
+  return t;
+}
+
+int64_t oracle_steps_done(oracle_t *o) { return o->step; }
+
+void oracle_destroy(oracle_t *o) {
+  if (!o) return;
+  free((void *)o->row_off);
+  free(o->rsym); free(o->gsym); free(o->tid); free(o->tlen); free(o->tnext); free(o->tprev);
+  free(o->pair_key); free(o->occ_pos);
+  free(o->vsyms.a); free(o->voff); free(o->vnres); free(o->vhash);
+  for (int64_t k = 0; k < o->U; k++) free(o->kocc[k].a);
+  free(o->kL); free(o->kG); free(o->kR); free(o->knres); free(o->kcount); free(o->khash);
+  free(o->kprefix); free(o->kocc); free(o->ht); free(o->pw); free(o->hc); free(o->hk);
+  free(o->touched_flag); free(o->touched.a);
+  free(o);
+}
