@@ -1,0 +1,222 @@
+"""GeoBPE merge-loop benchmark (BASELINE.json metric: BPE merge iters/sec on a
+PDB-pretrain-scale corpus at 1/2/4/8 MI355X).
+
+A "step" is one BPE merge iteration (`BPE.step()`, foldingdiff/bpe.py:1792-2166)
+on the BASELINE configs[2] corpus: 100k synthetic chains, lengths U{40..560}
+(mean 300, ~30M residues), seed 0, bins {1: 5}; the default W + K = 10 + 990
+covers the config's 1000 merges.  The prologue (thresholds, quantisation,
+labels) and the initial histogram (BPE.bin) run before the timed region and are
+reported separately.  Inputs are resident in HBM when the timer starts.
+
+N > 1: launched by torch.distributed.run, one rank per GPU (RCCL); the corpus is
+row-sharded (same 100k chains in total: strong scaling), the ranks exchange count
+deltas once per iteration.
+
+rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "pt-bpe_amd"))
+sys.path.insert(0, REPO)
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    # name: (n_chains, len_lo, len_hi, bins, merges)
+    "c3": (100_000, 40, 560, 5, 1000),  # BASELINE configs[2]
+    "c2": (10_000, 256, None, 5, 500),  # BASELINE configs[1]
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=990)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=30.0)
+    ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    from geobpe import synth
+    from geobpe.dist import TorchGroup, shard_rows, slice_corpus
+    from geobpe.engine import GeoBPEEngine
+
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    n, lo, hi, B, merges = CONFIGS[args.config]
+    t0 = time.time()
+    lengths = synth.make_lengths(n, lo, hi, seed=0)
+    corpus = synth.make_corpus(lengths, seed=0)
+    R_total = int(corpus["row_off"][-1])
+    t_gen = time.time() - t0
+    shard = corpus
+    group = None
+    if world > 1:
+        lo_r, hi_r = shard_rows(corpus["row_off"], world)[rank]
+        shard = slice_corpus(corpus, lo_r, hi_r)
+        group = TorchGroup(int(shard["row_off"][-1]), device=local)
+    eng = GeoBPEEngine(shard, B, device=local, group=group, max_vocab=1 << 20)
+    torch.cuda.synchronize()
+    t0 = time.time()
+    eng.initialize()
+    torch.cuda.synchronize()
+    t_init = time.time() - t0
+    if not args.no_profile:
+        eng.set_profiling(True)
+    t0 = time.time()
+    eng.bin()
+    torch.cuda.synchronize()
+    t_bin = time.time() - t0
+    U0 = eng.num_keys
+    bin_ms = {k: eng.kernel_ms(k)[0] for k in ("pair_count", "assign", "finalize")}
+    if not args.no_profile:
+        eng.set_profiling(True)  # reset counters
+    for _ in range(args.warmup):
+        if eng.step(want_merged=False) is None:
+            break
+    if not args.no_profile:
+        eng.set_profiling(True)
+    # ---- timed region: exactly K merges
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    done = 0
+    for _ in range(args.steps):
+        if eng.step(want_merged=False) is None:
+            break
+        done += 1
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    T = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([T], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        T = float(tt.item())
+    kern = {}
+    if not args.no_profile:
+        for k in ("argmax", "mark", "apply", "assign", "finalize"):
+            ms, nl = eng.kernel_ms(k)
+            kern[k] = {"ms_total": round(ms, 4), "launches": nl, "avg_us": round(1000 * ms / max(nl, 1), 3)}
+    R_local = int(shard["row_off"][-1])
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    # ---- roofline of the dominant kernel of the loop (HIP events over the timed region)
+    roofline = None
+    if kern:
+        dom = max(kern, key=lambda k: kern[k]["ms_total"])
+        # algorithmic bytes per launch:
+        #   mark:  the pk scan, 4 B per residue slot (+ small run walks)
+        #   apply / assign / finalize / argmax: per-merge / per-key records
+        if dom == "mark":
+            bytes_per_launch = 4.0 * R_local
+            unit_note = "4 B x residue slots (pk scan)"
+        elif dom == "argmax":
+            bytes_per_launch = 2 * 4.0 * eng.num_keys
+            unit_note = "2 passes x 4 B x dense keys"
+        else:
+            bytes_per_launch = None
+            unit_note = "record-bound kernel; see DESIGN.md"
+        avg_s = kern[dom]["ms_total"] / 1000.0 / max(kern[dom]["launches"], 1)
+        if bytes_per_launch:
+            ach = bytes_per_launch / avg_s / 1e9
+            roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                        "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(avg_s * 1e6, 3),
+                        "algorithmic_bytes": unit_note}
+    # the full content-keyed pair-count pass (BPE.bin) at iteration 0: SURVEY §8(d)
+    # B_count = 20*T_live + 4*U_live with T = residues
+    pair_count = None
+    if bin_ms.get("pair_count"):
+        t_count = sum(bin_ms.values()) / 1000.0
+        bc = 20.0 * R_local + 4.0 * U0
+        pair_count = {"kernels": "k_pairs_all+k_assign+k_finalize", "bytes": bc, "time_us": round(t_count * 1e6, 2),
+                      "achieved_GBs": round(bc / t_count / 1e9, 1), "frac": round(bc / t_count / 1e9 / HBM_PEAK_GBS, 4),
+                      "ms": {k: round(v, 4) for k, v in bin_ms.items()}, "U0": U0, "T0": R_local}
+
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(corpus, B, args.warmup, args.steps, args.cpu_budget_s)
+
+    value = done / T if T > 0 else 0.0
+    out = {
+        "metric": "BPE merge iters/sec on PDB-pretrain-scale corpus",
+        "value": round(value, 2),
+        "unit": "merges/s",
+        "n_gpus": world,
+        "steps": done,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000 * T / max(done, 1), 4),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic",
+        "config": {"workload": f"BASELINE configs[2]: {n} synthetic chains, len U{{{lo}..{hi}}}, "
+                               f"{R_total} residues, bins {{1: {B}}}, merges {args.warmup + 1}..{args.warmup + done}"
+                   if args.config == "c3" else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
+                   "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}"},
+        "roofline": roofline,
+        "cpu_baseline": cpu,
+        "pair_count_pass": pair_count,
+        "kernels": kern,
+        "prologue_s": {"generate": round(t_gen, 3), "initialize": round(t_init, 3), "bin": round(t_bin, 3)},
+        "final": {"vocab": eng.vocab_count, "keys": eng.num_keys},
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(corpus, B, warmup, steps, budget_s):
+    """The CPU oracle (C restatement of the reference loop, 1 core) on the same
+    corpus and the same merge window, stopped after ``budget_s`` of timed work."""
+    try:
+        import oracle
+    except Exception as e:  # pragma: no cover
+        return {"error": repr(e)}
+    o = oracle.OracleBPE(corpus, B).initialize()
+    o.bin()
+    for _ in range(warmup):
+        o.step_fast()
+    t0 = time.perf_counter()
+    done = 0
+    while done < steps:
+        if o.step_fast() is None:
+            break
+        done += 1
+        if time.perf_counter() - t0 > budget_s:
+            break
+    T = time.perf_counter() - t0
+    return {"value": round(done / T, 2), "unit": "merges/s", "cores": 1, "kind": "port",
+            "sample": f"oracle/geobpe_oracle.c on the same corpus, merges {warmup + 1}..{warmup + done} "
+                      f"({T:.1f} s of single-core work)"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,134 @@
+/*
+ * geobpe.h -- C-ABI of the MI355X-native GeoBPE merge loop (libgeobpe.so).
+ *
+ * The reference has no FFI: its hot path is the Python object API of
+ * foldingdiff.bpe.BPE.  Each entry point below replaces one
+ * step of that API; the Python host mirror (pt-bpe_amd/geobpe/bpe.py) binds them
+ * with ctypes exactly where the reference calls the Python methods.
+ *
+ * Conventions: plain pointers and sizes, no torch types.  Host pointers are
+ * marked h_, device pointers d_.  Every call is ordered on the context's HIP
+ * stream (the stream given at create time, or a private one).  Every function
+ * returns 0 on success and a nonzero GEOBPE_E* code on failure; the message is
+ * in geobpe_last_error().  GEOBPE_EVALUE corresponds to the reference's
+ * ValueError from BPE.get_ind (foldingdiff/bpe.py:1180-1189).
+ */
+#ifndef GEOBPE_H
+#define GEOBPE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GEOBPE_OK 0
+#define GEOBPE_EARG 1      /* bad argument / call order */
+#define GEOBPE_EVALUE 2    /* a value outside the histogram range (reference ValueError) */
+#define GEOBPE_ECAPACITY 3 /* a device table is full */
+#define GEOBPE_EHIP 4      /* HIP runtime error */
+#define GEOBPE_EHASH 5     /* content-hash collision detected (never expected) */
+
+/* angle column order of the input table (= Tokenizer.init_structure,
+ * foldingdiff/tokenizer.py:393-405): */
+#define GEOBPE_COL_0C1N 0
+#define GEOBPE_COL_NCA 1
+#define GEOBPE_COL_CAC 2
+#define GEOBPE_COL_PHI 3
+#define GEOBPE_COL_PSI 4
+#define GEOBPE_COL_OMEGA 5
+#define GEOBPE_COL_TAU 6
+#define GEOBPE_COL_CAC1N 7
+#define GEOBPE_COL_C1NCA 8
+/* threshold type order (= BPE._init_thresholds keys, bpe.py:828):
+ * tau, CA:C:1N, C:1N:1CA, psi, omega, phi */
+#define GEOBPE_NTYPES 6
+
+typedef struct geobpe_ctx geobpe_ctx;
+
+/* Create a context on HIP device `device`.  `stream` is a hipStream_t (e.g.
+ * torch.cuda.current_stream().cuda_stream) or NULL for a private stream.
+ * `max_vocab` bounds len(_tokens) (K0 + merges). */
+int geobpe_create(geobpe_ctx **out, int device, void *stream, int64_t max_vocab);
+void geobpe_destroy(geobpe_ctx *ctx);
+const char *geobpe_last_error(geobpe_ctx *ctx);
+
+/* ---- prologue: BPE.__init__ + BPE.initialize() (bpe.py:33-103, 820-876, 138-394) ----
+ * Upload the corpus: n_rows chains, h_row_off[n_rows+1] residue offsets and the
+ * 9 float64 columns (each h_cols[c] has row_off[n_rows] values, NaN allowed). */
+int geobpe_load_angles(geobpe_ctx *ctx, int64_t n_rows, const int64_t *h_row_off, const double *const *h_cols);
+
+/* Per threshold type t (order above): min and max of the wrapped, non-NaN,
+ * non-zero column values (bpe.py:844 + plotting.py:309-310), and how many
+ * there were.  h_minmax[2t] = min, [2t+1] = max; h_count[t].  The tau init
+ * angle of bpe.py:845-846 is NOT included (the host adds it). */
+int geobpe_angle_range(geobpe_ctx *ctx, double *h_minmax, int64_t *h_count);
+
+/* Set the grid-1 histogram edges (np.histogram edges, B+1 per type, type-major)
+ * and quantise every residue / junction (get_ind semantics, bpe.py:1164-1189).
+ * `init_tau` is Tokenizer._init_bond_angle (tokenizer.py:74-77).
+ * Fails with GEOBPE_EVALUE if any used value falls outside its bins. */
+int geobpe_quantize(geobpe_ctx *ctx, int32_t B, const double *h_edges, double init_tau);
+
+/* First appearance of every residue symbol: h_first[s] = smallest residue index
+ * (+ row_base) holding symbol s, or INT64_MAX.  Symbols s < B^3 + B. */
+int geobpe_symbol_first(geobpe_ctx *ctx, int64_t row_base, int64_t *h_first);
+
+/* Install the initial residue tokens: label of symbol s = h_label_of_sym[s]
+ * (first-appearance rank, bpe.py:231-261); K0 labels. */
+int geobpe_init_tokens(geobpe_ctx *ctx, const int32_t *h_label_of_sym, int32_t K0);
+
+/* ---- BPE.bin(): full content-keyed adjacent-pair histogram (bpe.py:1431-1474) ---- */
+int geobpe_bin(geobpe_ctx *ctx);
+
+/* ---- BPE.step() (bpe.py:1792-2166) ----
+ * One merge iteration: device argmax (max count, ties -> smallest reference key
+ * string), greedy non-overlapping merge-apply, incremental count update.
+ * *new_id = the new token id (len(_tokens) before the step), *count = its
+ * occurrence count, *n_merged = merges applied; *new_id = -1 if no pair is left. */
+int geobpe_step(geobpe_ctx *ctx, int32_t *new_id, int32_t *count, int64_t *n_merged);
+
+/* The split step for row-sharded multi-GPU runs: select (argmax over the
+ * replicated global counts) + apply locally, recording count deltas; then the
+ * caller exchanges the delta records (geobpe_delta_export / _import). */
+int geobpe_step_select(geobpe_ctx *ctx, int32_t *new_id, int32_t *count);
+int geobpe_step_apply(geobpe_ctx *ctx, int64_t *n_merged);
+/* Delta records (40 bytes each) of every key whose local count changed since
+ * the last export; copies them to d_out (device, capacity cap records). */
+int geobpe_delta_export(geobpe_ctx *ctx, void *d_out, int64_t cap, int64_t *n_records);
+/* Add the records (from every rank, this one included) to the global counts. */
+int geobpe_delta_import(geobpe_ctx *ctx, const void *d_in, int64_t n_records);
+/* 1 = multi-rank mode (local changes go to the delta buffer), 0 = single.
+ * Must precede geobpe_bin(). */
+int geobpe_set_distributed(geobpe_ctx *ctx, int on);
+/* Residues of the whole (all-rank) corpus: sizes the replicated key table. */
+int geobpe_set_global_residues(geobpe_ctx *ctx, int64_t n);
+
+/* ---- introspection / exports ---- */
+/* Key string (json.dumps(geo, sort_keys=True)) of vocab id v's content. */
+int64_t geobpe_token_json(geobpe_ctx *ctx, int32_t v, char *buf, int64_t cap);
+/* Content (residue / junction symbols, 2*nres-1 values) of vocab id v. */
+int64_t geobpe_token_content(geobpe_ctx *ctx, int32_t v, int32_t *h_out, int64_t cap);
+int64_t geobpe_vocab_count(geobpe_ctx *ctx); /* len(_tokens) */
+int64_t geobpe_num_keys(geobpe_ctx *ctx);    /* distinct pair keys ever seen */
+int64_t geobpe_num_tokens(geobpe_ctx *ctx);  /* live tokens (sync) */
+/* Segmentation (bond_to_token order): per row the (start residue within the row,
+ * token id) of every token.  Call with NULL buffers to get the total count. */
+int64_t geobpe_segmentation(geobpe_ctx *ctx, int32_t *h_start, int32_t *h_id, int64_t *h_row_tok_off);
+/* quantize(tokenize()) of every row (tokenizer.py:379-392, bpe.py:918-956). */
+int64_t geobpe_encode(geobpe_ctx *ctx, int32_t *h_ids, int64_t *h_row_id_off);
+/* Full recount of the live pair histogram from the per-token key ids, compared
+ * with the incrementally maintained counts: returns the number of mismatching
+ * keys (0 = consistent), or -1 on error. */
+int64_t geobpe_verify_counts(geobpe_ctx *ctx);
+/* Time the last launch of each kernel (ms, HIP events on the context stream)
+ * when profiling is enabled.  names: "pair_count", "argmax", "mark", "apply",
+ * "assign", "finalize". */
+int geobpe_set_profiling(geobpe_ctx *ctx, int on);
+double geobpe_kernel_ms(geobpe_ctx *ctx, const char *name, int64_t *launches);
+int geobpe_synchronize(geobpe_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,92 @@
+"""ctypes binding of libgeobpe.so (the C-ABI in include/geobpe.h).
+
+The HIP library is the product: there is no CPU fallback.  Importing this
+module on a box without the built library raises immediately; calls into a
+context raise `GeoBPEError` (or `ValueError` for the reference's ValueError
+cases) with the library's message.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libgeobpe.so")
+
+E_OK, E_ARG, E_VALUE, E_CAPACITY, E_HIP, E_HASH = range(6)
+DELTA_RECORD_BYTES = 40
+
+
+class GeoBPEError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libgeobpe.so (built by __graft_entry__.build() / geobpe.build)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise GeoBPEError(
+            f"{LIB_PATH} is missing: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, D = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_double
+    pI32, pI64 = ctypes.POINTER(I32), ctypes.POINTER(I64)
+    sig = {
+        "geobpe_create": (ctypes.c_int, [ctypes.POINTER(P), ctypes.c_int, P, I64]),
+        "geobpe_destroy": (None, [P]),
+        "geobpe_last_error": (ctypes.c_char_p, [P]),
+        "geobpe_load_angles": (ctypes.c_int, [P, I64, P, P]),
+        "geobpe_angle_range": (ctypes.c_int, [P, P, P]),
+        "geobpe_quantize": (ctypes.c_int, [P, I32, P, D]),
+        "geobpe_symbol_first": (ctypes.c_int, [P, I64, P]),
+        "geobpe_init_tokens": (ctypes.c_int, [P, P, I32]),
+        "geobpe_bin": (ctypes.c_int, [P]),
+        "geobpe_step": (ctypes.c_int, [P, pI32, pI32, pI64]),
+        "geobpe_step_select": (ctypes.c_int, [P, pI32, pI32]),
+        "geobpe_step_apply": (ctypes.c_int, [P, pI64]),
+        "geobpe_delta_export": (ctypes.c_int, [P, P, I64, pI64]),
+        "geobpe_delta_import": (ctypes.c_int, [P, P, I64]),
+        "geobpe_set_distributed": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_set_global_residues": (ctypes.c_int, [P, I64]),
+        "geobpe_token_json": (I64, [P, I32, ctypes.c_char_p, I64]),
+        "geobpe_token_content": (I64, [P, I32, P, I64]),
+        "geobpe_vocab_count": (I64, [P]),
+        "geobpe_num_keys": (I64, [P]),
+        "geobpe_num_tokens": (I64, [P]),
+        "geobpe_segmentation": (I64, [P, P, P, P]),
+        "geobpe_encode": (I64, [P, P, P]),
+        "geobpe_verify_counts": (I64, [P]),
+        "geobpe_set_profiling": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_kernel_ms": (D, [P, ctypes.c_char_p, pI64]),
+        "geobpe_synchronize": (ctypes.c_int, [P]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+EXPORTED_SYMBOLS = [
+    "geobpe_create", "geobpe_destroy", "geobpe_last_error", "geobpe_load_angles", "geobpe_angle_range",
+    "geobpe_quantize", "geobpe_symbol_first", "geobpe_init_tokens", "geobpe_bin", "geobpe_step",
+    "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
+    "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",
+    "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
+    "geobpe_verify_counts", "geobpe_set_profiling", "geobpe_kernel_ms", "geobpe_synchronize",
+]
+
+
+def check(ctx, rc: int) -> None:
+    if rc == E_OK:
+        return
+    msg = lib().geobpe_last_error(ctx)
+    msg = msg.decode() if msg else f"error {rc}"
+    if rc == E_VALUE:
+        raise ValueError(msg)
+    raise GeoBPEError(f"libgeobpe: {msg} (code {rc})")

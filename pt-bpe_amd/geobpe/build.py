@@ -1,0 +1,42 @@
+"""Build libgeobpe.so (gfx950) in-tree with hipcc."""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(os.path.dirname(HERE), "csrc")
+OUT = os.path.join(HERE, "libgeobpe.so")
+SOURCES = [os.path.join(CSRC, "geobpe.hip")]
+DEPS = SOURCES + [os.path.join(CSRC, "keyjson.h"),
+                  os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "geobpe.h")]
+ARCH = os.environ.get("GEOBPE_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and os.path.exists(OUT):
+        t = os.path.getmtime(OUT)
+        if all(os.path.getmtime(d) <= t for d in DEPS if os.path.exists(d)):
+            return OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-fPIC", "-shared", "-std=c++17",
+           "-ffp-contract=off", "-Wall", "-Wno-unused-result", "-Wno-unused-value",
+           "-Wno-unused-function", *SOURCES, "-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed:\n{r.stderr[-4000:]}")
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

@@ -1,0 +1,274 @@
+"""GeoBPEEngine: the host driver of libgeobpe.so for one corpus shard.
+
+It runs the reference's scoped GeoBPE pipeline:
+
+  initialize()   BPE._init_thresholds + BPE._init_res_tokens (bpe.py:820-876, 138-394):
+                 device min/max of the wrapped angle columns -> np.histogram edges on
+                 the host (exactly the reference's edges, plotting.py:305-337) ->
+                 device quantisation of every residue / junction -> first-appearance
+                 labels (bpe.py:236-246).
+  bin()          BPE.bin (bpe.py:1431-1474) -- full content-keyed pair histogram.
+  step()         BPE.step (bpe.py:1792-2166) -- one merge.
+  encode()       quantize(tokenize()) for every chain (bpe.py:918-956).
+
+Multi-GPU: each rank holds a contiguous block of chains (row sharding,
+SURVEY.md §8(e)).  Thresholds and first appearances are all-reduced once;
+then every iteration the ranks select the same winner from replicated global
+counts, apply it locally and exchange their count deltas (one all-gather of
+40-byte records of the keys whose local count changed).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+from typing import Optional
+
+import numpy as np
+
+from . import _native
+from .synth import COLUMNS
+
+ANGLE_TYPES = ["tau", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"]
+TWO_PI = 2 * np.pi
+# nerf.py:22-24 -- Tokenizer._init_bond_angle (tokenizer.py:74-77, angles_and_coords.py:746-752)
+_N_INIT = np.array([17.047, 14.099, 3.625])
+_CA_INIT = np.array([16.967, 12.784, 4.338])
+_C_INIT = np.array([15.685, 12.755, 5.133])
+
+
+def init_bond_angle() -> float:
+    v1, v2 = _N_INIT - _CA_INIT, _C_INIT - _CA_INIT
+    u1 = v1 / np.linalg.norm(v1)
+    u2 = v2 / np.linalg.norm(v2)
+    return float(np.arccos(np.clip(np.dot(u1, u2), -1.0, 1.0)))
+
+
+def histogram_edges(mn: float, mx: float, count: int, B: int) -> np.ndarray:
+    """np.histogram(a, bins=B) edges given only min/max/len of ``a`` (numpy's
+    _get_outer_edges + linspace depend on nothing else)."""
+    a = np.array([mn, mx], dtype=np.float64) if count > 0 else np.zeros(0, dtype=np.float64)
+    return np.histogram_bin_edges(a, bins=B)
+
+
+def _p(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _stream_handle(device: int):
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+    except Exception:
+        pass
+    return None
+
+
+class GeoBPEEngine:
+    def __init__(self, corpus: dict, bins: int, device: int = 0, max_vocab: int = 1 << 20,
+                 group=None, stream=None, use_torch_stream: bool = True):
+        """``corpus``: ``{column: float64[R]}`` + ``row_off`` (geobpe.synth layout) for
+        THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs."""
+        self.L = _native.lib()
+        self.B = int(bins)
+        self.device = int(device)
+        self.group = group
+        self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
+        self.n_rows = len(self.row_off) - 1
+        self._cols = [np.ascontiguousarray(corpus[c], dtype=np.float64) for c in COLUMNS]
+        if stream is None and use_torch_stream:
+            stream = _stream_handle(self.device)
+        self._ctx = ctypes.c_void_p()
+        rc = self.L.geobpe_create(ctypes.byref(self._ctx), self.device, stream, int(max_vocab))
+        if rc:
+            msg = self.L.geobpe_last_error(self._ctx) if self._ctx else b"create failed"
+            raise _native.GeoBPEError(f"geobpe_create: {msg.decode() if msg else rc}")
+        self.K0 = 0
+        self.merges = []  # [(new_id, count, n_merged)]
+        self.thresholds = None
+        self._initialized = False
+        self._binned = False
+        self._delta_buf = None
+        self._done = False
+
+    # ------------------------------------------------------------ helpers
+    def _chk(self, rc):
+        _native.check(self._ctx, rc)
+
+    @property
+    def distributed(self) -> bool:
+        return self.group is not None and self.group.world_size > 1
+
+    def close(self):
+        if self._ctx:
+            self.L.geobpe_destroy(self._ctx)
+            self._ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------ prologue
+    def initialize(self):
+        arr = (ctypes.c_void_p * 9)(*[c.ctypes.data for c in self._cols])
+        self._chk(self.L.geobpe_load_angles(self._ctx, self.n_rows, _p(self.row_off), arr))
+        mm = np.zeros(12, dtype=np.float64)
+        cnt = np.zeros(6, dtype=np.int64)
+        self._chk(self.L.geobpe_angle_range(self._ctx, _p(mm), _p(cnt)))
+        n_rows_total = self.n_rows
+        if self.distributed:
+            mm, cnt, n_rows_total = self.group.reduce_ranges(mm, cnt, self.n_rows)
+        w0 = (init_bond_angle() + TWO_PI) % TWO_PI
+        edges = np.zeros((6, self.B + 1), dtype=np.float64)
+        self.thresholds = {}
+        for t, key in enumerate(ANGLE_TYPES):
+            mn, mx, c = float(mm[2 * t]), float(mm[2 * t + 1]), int(cnt[t])
+            if key == "tau" and n_rows_total > 0:  # bpe.py:845-846: + _bond_angle(0) per tokenizer
+                mn, mx, c = (min(mn, w0), max(mx, w0), c + n_rows_total) if c > 0 else (w0, w0, n_rows_total)
+            e = histogram_edges(mn, mx, c, self.B)
+            edges[t] = e
+            self.thresholds[key] = [(float(s), float(f)) for s, f in zip(e[:-1], e[1:])]
+        self._edges = edges
+        self._chk(self.L.geobpe_quantize(self._ctx, self.B, _p(edges), init_bond_angle()))
+        S = self.B ** 3 + self.B
+        first = np.zeros(S, dtype=np.int64)
+        row_base = 0 if not self.distributed else self.group.residue_base
+        self._chk(self.L.geobpe_symbol_first(self._ctx, row_base, _p(first)))
+        if self.distributed:
+            first = self.group.reduce_first(first)
+        present = np.nonzero(first != np.iinfo(np.int64).max)[0]
+        order = present[np.argsort(first[present], kind="stable")]
+        label_of_sym = np.full(S, -1, dtype=np.int32)
+        label_of_sym[order] = np.arange(len(order), dtype=np.int32)
+        self.K0 = int(len(order))
+        self.sym_of_label = order.astype(np.int32)
+        self._chk(self.L.geobpe_init_tokens(self._ctx, _p(label_of_sym), self.K0))
+        self._initialized = True
+        return self
+
+    # ------------------------------------------------------------ histogram / merges
+    def bin(self):
+        if not self._initialized:
+            raise RuntimeError("initialize() first")
+        if self.distributed:
+            self._chk(self.L.geobpe_set_distributed(self._ctx, 1))
+            self._chk(self.L.geobpe_set_global_residues(self._ctx, self.group.total_residues))
+        self._chk(self.L.geobpe_bin(self._ctx))
+        if self.distributed:
+            self._exchange()
+        self._binned = True
+
+    def _exchange(self):
+        """export local count deltas -> all-gather -> import on every rank."""
+        n = ctypes.c_int64(0)
+        cap, ptr = self.group.export_buffer(self)
+        self._chk(self.L.geobpe_delta_export(self._ctx, ptr, cap, ctypes.byref(n)))
+        d_in, total = self.group.all_gather_deltas(self, int(n.value))
+        self._chk(self.L.geobpe_delta_import(self._ctx, d_in, total))
+
+    def step(self, want_merged: bool = True):
+        """One merge. Returns (new_id, count, n_merged) or None if no pair is left."""
+        if not self._binned:
+            raise RuntimeError("bin() first")
+        nid, cnt = ctypes.c_int32(0), ctypes.c_int32(0)
+        nm = ctypes.c_int64(0)
+        if not self.distributed:
+            self._chk(self.L.geobpe_step(self._ctx, ctypes.byref(nid), ctypes.byref(cnt),
+                                         ctypes.byref(nm) if want_merged else None))
+            if nid.value < 0:
+                self._done = True
+                return None
+        else:
+            self._chk(self.L.geobpe_step_select(self._ctx, ctypes.byref(nid), ctypes.byref(cnt)))
+            if nid.value < 0:
+                self._done = True
+                return None
+            self._chk(self.L.geobpe_step_apply(self._ctx, ctypes.byref(nm) if want_merged else None))
+            self._exchange()
+        rec = (int(nid.value), int(cnt.value), int(nm.value) if want_merged else -1)
+        self.merges.append(rec)
+        return rec
+
+    def run(self, n_merges: int, want_merged: bool = False) -> int:
+        done = 0
+        for _ in range(n_merges):
+            if self.step(want_merged=want_merged) is None:
+                break
+            done += 1
+        return done
+
+    def synchronize(self):
+        self._chk(self.L.geobpe_synchronize(self._ctx))
+
+    # ------------------------------------------------------------ introspection
+    @property
+    def vocab_count(self) -> int:
+        return int(self.L.geobpe_vocab_count(self._ctx))
+
+    @property
+    def vocab_size(self) -> int:
+        return self.vocab_count + 3 * self.B
+
+    @property
+    def num_keys(self) -> int:
+        return int(self.L.geobpe_num_keys(self._ctx))
+
+    @property
+    def num_tokens(self) -> int:
+        return int(self.L.geobpe_num_tokens(self._ctx))
+
+    def token_json(self, v: int) -> str:
+        m = self.L.geobpe_token_json(self._ctx, v, None, 0)
+        if m < 0:
+            raise IndexError(v)
+        buf = ctypes.create_string_buffer(int(m) + 1)
+        self.L.geobpe_token_json(self._ctx, v, buf, m + 1)
+        return buf.value.decode()
+
+    def token_content(self, v: int) -> np.ndarray:
+        m = self.L.geobpe_token_content(self._ctx, v, None, 0)
+        if m < 0:
+            raise IndexError(v)
+        out = np.empty(m, dtype=np.int32)
+        self.L.geobpe_token_content(self._ctx, v, _p(out), m)
+        return out
+
+    def merge_keys(self):
+        """[(key_json, count)] of every merge so far -- the reference's merge list."""
+        return [(self.token_json(nid), c) for nid, c, _ in self.merges]
+
+    def segmentation(self):
+        T = self.L.geobpe_segmentation(self._ctx, None, None, None)
+        if T < 0:
+            raise _native.GeoBPEError("segmentation failed")
+        start = np.empty(T, np.int32)
+        ids = np.empty(T, np.int32)
+        off = np.empty(self.n_rows + 1, np.int64)
+        self.L.geobpe_segmentation(self._ctx, _p(start), _p(ids), _p(off))
+        return start, ids, off
+
+    def encode(self):
+        T = self.L.geobpe_encode(self._ctx, None, None)
+        if T < 0:
+            raise _native.GeoBPEError("encode failed")
+        ids = np.empty(T, np.int32)
+        off = np.empty(self.n_rows + 1, np.int64)
+        self.L.geobpe_encode(self._ctx, _p(ids), _p(off))
+        return ids, off
+
+    def verify_counts(self) -> int:
+        n = int(self.L.geobpe_verify_counts(self._ctx))
+        if n < 0:
+            raise _native.GeoBPEError(_native.lib().geobpe_last_error(self._ctx).decode())
+        return n
+
+    # ------------------------------------------------------------ profiling
+    def set_profiling(self, on: bool = True):
+        self._chk(self.L.geobpe_set_profiling(self._ctx, 1 if on else 0))
+
+    def kernel_ms(self, name: str):
+        n = ctypes.c_int64(0)
+        ms = self.L.geobpe_kernel_ms(self._ctx, name.encode(), ctypes.byref(n))
+        return float(ms), int(n.value)

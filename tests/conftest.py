@@ -1,0 +1,39 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (REPO, os.path.join(REPO, "pt-bpe_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
+
+
+def golden_names():
+    return sorted(f[:-5] for f in os.listdir(GOLDEN) if f.endswith(".json"))
+
+
+def load_golden(name):
+    import json
+
+    import numpy as np
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        meta = json.load(f)
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        arrs = {k: z[k] for k in z.files}
+    corpus = {k: arrs[k] for k in ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N",
+                                    "C:1N:1CA", "row_off"]}
+    return meta, corpus, arrs
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    import oracle
+    oracle.build()
+    return oracle

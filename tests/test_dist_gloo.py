@@ -1,0 +1,74 @@
+"""The multi-rank exchange layer on CPU: world_size 2 over gloo (127.0.0.1).
+
+Covers what the N>1 path does on the host between device calls: the
+threshold / first-appearance all-reduces and the variable-size all-gather of
+40-byte delta records.  The device side of the protocol is covered on the GPU
+by tests/test_gpu_parity.py (VirtualCluster, several shards on one device)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+REC = 40
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    import ctypes
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "pt-bpe_amd"))
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geobpe.dist import TorchGroup
+        R_local = 100 + 50 * rank
+        g = TorchGroup(R_local)
+        assert g.residue_base == (0 if rank == 0 else 100)
+        assert g.total_residues == 250
+        mm = np.array([rank + 0.5, rank + 2.0] * 6)
+        cnt = np.arange(6, dtype=np.int64) + rank
+        mm2, cnt2, nrows = g.reduce_ranges(mm, cnt, 10 + rank)
+        assert mm2[0] == 0.5 and mm2[1] == 3.0
+        assert list(cnt2) == [2 * i + 1 for i in range(6)] and nrows == 21
+        first = np.array([5, 7, np.iinfo(np.int64).max], dtype=np.int64) - rank
+        assert list(g.reduce_first(first)[:2]) == [4, 6]
+        # export buffer -> variable-length all-gather of records
+        cap, ptr = g.export_buffer(None)
+        n = 3 + 2 * rank
+        payload = np.arange(n * REC, dtype=np.uint8) % 251 + rank
+        ctypes.memmove(ptr.value, payload.ctypes.data, n * REC)
+        d, total = g.all_gather_deltas(None, n)
+        got = np.ctypeslib.as_array((ctypes.c_uint8 * (total * REC)).from_address(d.value)).copy()
+        exp = np.concatenate([np.arange((3 + 2 * r) * REC, dtype=np.uint8) % 251 + r for r in range(world)])
+        assert total == 8 and np.array_equal(got, exp)
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_torchgroup_gloo_world2():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=240) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}
