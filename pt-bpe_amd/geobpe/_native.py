@@ -29,6 +29,14 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # Share ONE HIP runtime with PyTorch: torch bundles its own libamdhip64
+    # (soname libamdhip64.so.7); loading torch first makes libgeobpe.so bind to
+    # that copy, so torch streams / device pointers are valid in our calls.  A
+    # second runtime instance in the process would not see the device.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover
+        pass
     if not os.path.exists(LIB_PATH):
         raise GeoBPEError(
             f"{LIB_PATH} is missing: build the HIP extension first (python -c 'import __graft_entry__ as g; g.build()')")
