@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=30.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
+    ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
+    ap.add_argument("--roofline-kernel", default="mark")
     return ap.parse_args()
 
 
@@ -80,31 +82,21 @@ def main():
     eng.initialize()
     torch.cuda.synchronize()
     t_init = time.time() - t0
-    if not args.no_profile:
-        eng.set_profiling(True)
+    eng.set_profiling(not args.no_profile)
     t0 = time.time()
     eng.bin()
     torch.cuda.synchronize()
     t_bin = time.time() - t0
     U0 = eng.num_keys
     bin_ms = {k: eng.kernel_ms(k)[0] for k in ("pair_count", "assign", "finalize")}
-    if not args.no_profile:
-        eng.set_profiling(True)  # reset counters
-    for _ in range(args.warmup):
-        if eng.step(want_merged=False) is None:
-            break
-    if not args.no_profile:
-        eng.set_profiling(True)
-    # ---- timed region: exactly K merges
+    eng.run(args.warmup)
+    # ---- timed region: exactly K merges; HIP events only around the roofline kernel
+    eng.set_profiling(not args.no_profile, only=args.roofline_kernel)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    done = 0
-    for _ in range(args.steps):
-        if eng.step(want_merged=False) is None:
-            break
-        done += 1
+    done = eng.run(args.steps)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -113,11 +105,8 @@ def main():
         tt = torch.tensor([T], dtype=torch.float64, device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
-    kern = {}
-    if not args.no_profile:
-        for k in ("argmax", "mark", "apply", "assign", "finalize"):
-            ms, nl = eng.kernel_ms(k)
-            kern[k] = {"ms_total": round(ms, 4), "launches": nl, "avg_us": round(1000 * ms / max(nl, 1), 3)}
+    live_ms, live_n = eng.kernel_ms(args.roofline_kernel) if not args.no_profile else (0.0, 0)
+    merges_log = list(eng.merges)
     R_local = int(shard["row_off"][-1])
     if rank != 0:
         if world > 1:
@@ -125,29 +114,36 @@ def main():
             dist.destroy_process_group()
         return
 
-    # ---- roofline of the dominant kernel of the loop (HIP events over the timed region)
+    # ---- per-kernel table: a replay of the same merges with every kernel timed
+    kern = {}
+    if not args.no_profile and world == 1 and not args.no_replay:
+        rep = GeoBPEEngine(shard, B, device=local, max_vocab=1 << 20)
+        rep.initialize()
+        rep.bin()
+        rep.run(args.warmup)
+        rep.set_profiling(True)
+        rep.run(done)
+        for k in ("argmax", "select", "mark", "apply", "assign", "finalize"):
+            ms, nl = rep.kernel_ms(k)
+            kern[k] = {"ms_total": round(ms, 4), "launches": nl, "avg_us": round(1000 * ms / max(nl, 1), 3)}
+        assert rep.merges == merges_log, "replay diverged"
+        rep.close()
+
+    # ---- roofline of the loop's scan kernel, from the live events of the timed region
     roofline = None
-    if kern:
-        dom = max(kern, key=lambda k: kern[k]["ms_total"])
-        # algorithmic bytes per launch:
-        #   mark:  the pk scan, 4 B per residue slot (+ small run walks)
-        #   apply / assign / finalize / argmax: per-merge / per-key records
-        if dom == "mark":
-            bytes_per_launch = 4.0 * R_local
-            unit_note = "4 B x residue slots (pk scan)"
-        elif dom == "argmax":
-            bytes_per_launch = 2 * 4.0 * eng.num_keys
-            unit_note = "2 passes x 4 B x dense keys"
+    if live_n:
+        avg_s = live_ms / 1000.0 / live_n
+        if args.roofline_kernel == "mark":
+            bytes_per_launch = 4.0 * R_local  # the pk scan: 4 B per residue slot
+            note = "4 B x residue slots (pk scan); run walks and merge records excluded"
         else:
-            bytes_per_launch = None
-            unit_note = "record-bound kernel; see DESIGN.md"
-        avg_s = kern[dom]["ms_total"] / 1000.0 / max(kern[dom]["launches"], 1)
-        if bytes_per_launch:
-            ach = bytes_per_launch / avg_s / 1e9
-            roofline = {"kernel": dom, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                        "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                        "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(avg_s * 1e6, 3),
-                        "algorithmic_bytes": unit_note}
+            bytes_per_launch = 4.0 * eng.num_keys
+            note = "4 B x dense keys"
+        ach = bytes_per_launch / avg_s / 1e9
+        roofline = {"kernel": args.roofline_kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                    "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(avg_s * 1e6, 3),
+                    "launches": live_n, "algorithmic_bytes": note}
     # the full content-keyed pair-count pass (BPE.bin) at iteration 0: SURVEY §8(d)
     # B_count = 20*T_live + 4*U_live with T = residues
     pair_count = None
@@ -155,7 +151,8 @@ def main():
         t_count = sum(bin_ms.values()) / 1000.0
         bc = 20.0 * R_local + 4.0 * U0
         pair_count = {"kernels": "k_pairs_all+k_assign+k_finalize", "bytes": bc, "time_us": round(t_count * 1e6, 2),
-                      "achieved_GBs": round(bc / t_count / 1e9, 1), "frac": round(bc / t_count / 1e9 / HBM_PEAK_GBS, 4),
+                      "achieved_GBs": round(bc / t_count / 1e9, 1),
+                      "frac": round(bc / t_count / 1e9 / HBM_PEAK_GBS, 4),
                       "ms": {k: round(v, 4) for k, v in bin_ms.items()}, "U0": U0, "T0": R_local}
 
     cpu = None

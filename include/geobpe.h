@@ -88,6 +88,14 @@ int geobpe_bin(geobpe_ctx *ctx);
  * occurrence count, *n_merged = merges applied; *new_id = -1 if no pair is left. */
 int geobpe_step(geobpe_ctx *ctx, int32_t *new_id, int32_t *count, int64_t *n_merged);
 
+/* Enqueue n_iters merge iterations back to back with no host synchronisation
+ * (the winner, tie-break and new token are resolved on the device), then wait;
+ * *n_done = merges actually made (fewer if the pairs ran out). */
+int geobpe_run(geobpe_ctx *ctx, int64_t n_iters, int64_t *n_done);
+/* The merge list so far: 3 int64 per merge (new id, count, merges applied);
+ * returns the number of merges (copies at most cap). */
+int64_t geobpe_merge_log(geobpe_ctx *ctx, int64_t *h_out, int64_t cap);
+
 /* The split step for row-sharded multi-GPU runs: select (argmax over the
  * replicated global counts) + apply locally, recording count deltas; then the
  * caller exchanges the delta records (geobpe_delta_export / _import). */
@@ -107,6 +115,11 @@ int geobpe_set_global_residues(geobpe_ctx *ctx, int64_t n);
 /* ---- introspection / exports ---- */
 /* Key string (json.dumps(geo, sort_keys=True)) of vocab id v's content. */
 int64_t geobpe_token_json(geobpe_ctx *ctx, int32_t v, char *buf, int64_t cap);
+/* Key string of dense pair key d (introspection / tests). */
+int64_t geobpe_key_json(geobpe_ctx *ctx, int32_t d, char *buf, int64_t cap);
+/* Device ordering of reference key strings: h_out[i] = key(h_pairs[2i]) <
+ * key(h_pairs[2i+1]) for dense key ids (tests the device tie-break). */
+int geobpe_debug_key_less(geobpe_ctx *ctx, const int32_t *h_pairs, int32_t n, int32_t *h_out);
 /* Content (residue / junction symbols, 2*nres-1 values) of vocab id v. */
 int64_t geobpe_token_content(geobpe_ctx *ctx, int32_t v, int32_t *h_out, int64_t cap);
 int64_t geobpe_vocab_count(geobpe_ctx *ctx); /* len(_tokens) */
@@ -121,10 +134,12 @@ int64_t geobpe_encode(geobpe_ctx *ctx, int32_t *h_ids, int64_t *h_row_id_off);
  * with the incrementally maintained counts: returns the number of mismatching
  * keys (0 = consistent), or -1 on error. */
 int64_t geobpe_verify_counts(geobpe_ctx *ctx);
-/* Time the last launch of each kernel (ms, HIP events on the context stream)
- * when profiling is enabled.  names: "pair_count", "argmax", "mark", "apply",
- * "assign", "finalize". */
+/* Per-kernel time (ms summed over launches, HIP events on the context stream)
+ * while profiling is enabled.  names: "pair_count", "argmax", "select",
+ * "mark", "apply", "assign", "finalize", "recount". */
 int geobpe_set_profiling(geobpe_ctx *ctx, int on);
+/* Restrict the timing to a comma-separated list of kernel names ("" = all). */
+int geobpe_set_profiling_filter(geobpe_ctx *ctx, const char *names);
 double geobpe_kernel_ms(geobpe_ctx *ctx, const char *name, int64_t *launches);
 int geobpe_synchronize(geobpe_ctx *ctx);
 

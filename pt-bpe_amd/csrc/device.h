@@ -1,0 +1,334 @@
+// device.h -- device-side data layout and helpers of the GeoBPE engine (gfx950).
+// Included once, by geobpe.hip.  See DESIGN.md §3 for the layout rationale.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/geobpe.h"
+
+typedef unsigned long long u64;
+
+namespace gb {
+
+constexpr u64 M61 = (1ULL << 61) - 1;
+constexpr u64 HP1 = 0x0A3B5C7D9E1F2437ULL % M61;  // content-hash bases (< M61)
+constexpr u64 HP2 = 0x13579BDF2468ACE1ULL % M61;
+constexpr u64 KMIX = 0x9E3779B97F4A7C15ULL;
+constexpr double TWO_PI = 6.283185307179586;  // 2*np.pi
+constexpr int BLOCK = 256;
+constexpr int AGG = 2048;      // LDS partial-count slots per workgroup
+constexpr int BLK_CANDS = 8;   // argmax candidates kept per workgroup
+
+// ------------------------------------------------------------------ records
+struct State {
+  // persistent
+  int64_t U;          // dense keys allocated
+  int64_t err_code;   // first error (GEOBPE_E*)
+  int64_t err_pos;
+  int64_t epoch;      // delta-touch epoch (multi-rank)
+  int64_t vsym_used;  // device vocab content pool cursor
+  int32_t K;          // len(_tokens) on the device
+  int32_t iter;       // merges selected so far
+  int32_t tag;        // role tag of the current merge (= iter)
+  int32_t done;       // 1 once no pair is left
+  int32_t W, nid, maxc, ncand;
+  // per-iteration, reset by k_select_final
+  int64_t L_ovf, np_ovf, ns_ovf, nnew_total;
+  int64_t ntouched, nmismatch;
+};
+
+struct LEntry {  // one merge: left token a (+ its prev p), right token b (+ next c)
+  int32_t a, p, b, c;
+};
+struct NewPair {
+  int32_t target;  // residue whose pk receives the key (-1: none)
+  int32_t slot;    // key-table slot
+  int32_t len;     // residues of the pair content
+  int32_t delta;   // count contribution
+  u64 h1, h2;
+};
+struct NewSlot {
+  int32_t slot, len;
+  int32_t idL, g, idR, pad;
+  u64 h1, h2;
+};
+struct DeltaRec {  // 40 bytes, exchanged between ranks
+  u64 h1, h2;
+  int32_t len, idL, g, idR, delta, pad;
+};
+static_assert(sizeof(DeltaRec) == 40, "delta record layout");
+struct BlkMax {
+  int32_t max, n;
+  int32_t c[BLK_CANDS];
+};
+struct LogRec {  // one merge of the run (the merge list, device side)
+  int32_t nid, count, W, idL, g, idR;
+  int64_t nmerged;
+};
+
+struct Dev {
+  // corpus
+  int64_t R, nrows;
+  int32_t B, B2, B3, pad0;
+  const int64_t* row_off;
+  int32_t *rsym, *gsym;
+  // tokens (residue indexed)
+  int32_t *tid, *tlen, *tprev, *pk, *role;
+  // vocab (token id indexed)
+  u64 *vh1, *vh2;
+  int32_t* vlen;
+  int64_t* voff;  // content of id v = vsym[voff[v] .. voff[v+1])
+  int32_t* vsym;
+  int64_t KC, VSC;
+  // hash powers
+  const u64 *pw1, *pw2;
+  int64_t pwn;
+  // key table
+  u64* ht_key;
+  int32_t* ht_dense;
+  int64_t HC;
+  int32_t ht_shift, pad1;
+  // dense keys
+  u64 *kh1, *kh2;
+  int32_t *klen, *krep, *count, *dcount, *touch, *touched, *scratch;
+  int64_t UC;
+  // per-workgroup output regions (no global returning atomics on the hot path)
+  int32_t NB;       // workgroups of the region kernels
+  int32_t pad2;
+  int64_t CH;       // int4 groups of pk per mark workgroup
+  int64_t LC;       // merge entries per workgroup region
+  int64_t RC;       // new pairs / new keys per workgroup region
+  LEntry* L;
+  int32_t* Lcnt;
+  LEntry* Lovf;
+  int64_t Lovf_cap;
+  NewPair* np;
+  int32_t* npcnt;
+  NewPair* npovf;
+  NewSlot* ns;
+  int32_t* nscnt;
+  NewSlot* nsovf;
+  int64_t ovf_cap;
+  // argmax
+  BlkMax* blk;
+  int32_t* cand;
+  int64_t candcap;
+  LogRec* log;
+  State* st;
+};
+
+// ------------------------------------------------------------------ arithmetic
+__host__ __device__ inline u64 mulmod61(u64 a, u64 b) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  u64 lo = a * b;
+  u64 hi = __umul64hi(a, b);
+#else
+  unsigned __int128 p = (unsigned __int128)a * b;
+  u64 lo = (u64)p, hi = (u64)(p >> 64);
+#endif
+  u64 r = (lo & M61) + ((lo >> 61) | (hi << 3));
+  r = (r & M61) + (r >> 61);
+  return r >= M61 ? r - M61 : r;
+}
+__host__ __device__ inline u64 addmod61(u64 a, u64 b) {
+  u64 r = a + b;
+  return r >= M61 ? r - M61 : r;
+}
+
+// content hash of X ++ [g] ++ Y from the hashes of X and Y and |Y| residues:
+// H(s_0..s_{n-1}) = sum (s_i + 1) P^(n-1-i)  mod 2^61-1, two bases
+__device__ inline void combine(const Dev& D, u64 x1, u64 x2, int32_t g, u64 y1, u64 y2, int32_t ylen, u64& o1,
+                               u64& o2) {
+  const int64_t ny = 2 * (int64_t)ylen - 1;
+  const u64 gg = (u64)(g + 1);
+  o1 = addmod61(addmod61(mulmod61(x1, D.pw1[ny + 1]), mulmod61(gg, D.pw1[ny])), y1);
+  o2 = addmod61(addmod61(mulmod61(x2, D.pw2[ny + 1]), mulmod61(gg, D.pw2[ny])), y2);
+}
+
+__device__ inline u64 probe_key(u64 h1, u64 h2, int32_t len) {
+  u64 k = (h1 * KMIX) ^ (h2 + ((u64)len << 40)) ^ (h2 >> 29);
+  return k ? k : 1;
+}
+
+__device__ inline void set_error(const Dev& D, int64_t code, int64_t pos) {
+  unsigned long long* p = (unsigned long long*)&D.st->err_code;
+  if (atomicCAS(p, 0ULL, (unsigned long long)code) == 0ULL) D.st->err_pos = pos;
+}
+
+// Python / numpy  (v + 2*pi) % (2*pi)  in float64 (float_rem / npy_divmod)
+__device__ inline double wrap2pi(double v) {
+  const double a = v + TWO_PI;
+  double m;
+  if (a >= 0.0 && a < TWO_PI)
+    m = a;
+  else if (a >= TWO_PI && a < 2.0 * TWO_PI)
+    m = a - TWO_PI;  // exact (Sterbenz)
+  else
+    m = fmod(a, TWO_PI);
+  if (m != 0.0) {
+    if (m < 0.0) m += TWO_PI;
+  } else {
+    m = 0.0;
+  }
+  return m;
+}
+
+// BPE.get_ind (bpe.py:1164-1189); -1 where the reference raises ValueError
+__device__ inline int32_t get_ind(const double* e, int32_t B, double v) {
+  int32_t lo = 0, hi = B;  // bisect_right over the B left edges e[0..B-1]
+  while (lo < hi) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (v < e[mid])
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  const int32_t ind = lo - 1;
+  if (ind < 0) return -1;
+  const double s = e[ind], t = e[ind + 1];
+  if (ind == B - 1 && v == t) return ind;
+  if (s <= v && v < t) return ind;
+  return -1;
+}
+
+// ------------------------------------------------------------------ wave / block helpers
+__device__ inline int wave_lane() { return threadIdx.x & 63; }
+
+__device__ inline int32_t wave_excl_scan(int32_t v, int32_t& total) {
+  int32_t x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int32_t y = __shfl_up(x, o, 64);
+    if (wave_lane() >= o) x += y;
+  }
+  total = __shfl(x, 63, 64);
+  return x - v;
+}
+
+__device__ inline int32_t wave_max(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide max (all threads get the result); scratch: BLOCK/64 ints
+__device__ inline int32_t block_max(int32_t v, int32_t* scratch) {
+  v = wave_max(v);
+  __syncthreads();
+  if (wave_lane() == 0) scratch[threadIdx.x >> 6] = v;
+  __syncthreads();
+  int32_t r = scratch[0];
+  for (int i = 1; i < (int)(blockDim.x >> 6); i++) r = max(r, scratch[i]);
+  return r;
+}
+
+// exclusive prefix of a[0..n) for element i computed cooperatively: every block
+// thread gets (prefix of a[0..lo)) into LDS sums; n <= BLOCK*32
+__device__ inline int64_t block_sum_before(const int32_t* a, int32_t n, int32_t i, int64_t* s) {
+  // s: BLOCK int64 scratch. returns sum a[0..i)
+  int64_t part = 0;
+  for (int32_t k = threadIdx.x; k < i; k += blockDim.x) part += a[k];
+  __syncthreads();
+  s[threadIdx.x] = part;
+  __syncthreads();
+  for (int o = BLOCK / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
+    __syncthreads();
+  }
+  const int64_t r = s[0];
+  __syncthreads();
+  return r;
+}
+
+// count update target: global counts, or the rank-local delta + touched list
+__device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_delta) {
+  if (!to_delta) {
+    atomicAdd(&D.count[d], v);
+    return;
+  }
+  atomicAdd(&D.dcount[d], v);
+  const int32_t ep = (int32_t)D.st->epoch;
+  if (atomicExch(&D.touch[d], ep) != ep) {
+    const int64_t j = atomicAdd((unsigned long long*)&D.st->ntouched, 1ULL);
+    D.touched[j] = d;
+  }
+}
+
+// LDS-staged per-workgroup partial counts, flushed with one global atomic per
+// distinct key per workgroup
+struct Agg {
+  int32_t key[AGG];
+  int32_t val[AGG];
+};
+__device__ inline void agg_init(Agg& s) {
+  for (int i = threadIdx.x; i < AGG; i += blockDim.x) {
+    s.key[i] = -1;
+    s.val[i] = 0;
+  }
+  __syncthreads();
+}
+__device__ inline void agg_add(Agg& s, const Dev& D, int32_t d, int32_t v, bool to_delta) {
+  uint32_t h = ((uint32_t)d * 2654435761u) >> 21;  // 11 bits
+#pragma unroll 1
+  for (int probe = 0; probe < 8; probe++) {
+    const int32_t k = s.key[h];
+    if (k == d) {
+      atomicAdd(&s.val[h], v);
+      return;
+    }
+    if (k == -1) {
+      const int32_t old = atomicCAS(&s.key[h], -1, d);
+      if (old == -1 || old == d) {
+        atomicAdd(&s.val[h], v);
+        return;
+      }
+    }
+    h = (h + 1) & (AGG - 1);
+  }
+  global_add(D, d, v, to_delta);
+}
+__device__ inline void agg_flush(Agg& s, const Dev& D, bool to_delta) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < AGG; i += blockDim.x) {
+    const int32_t k = s.key[i];
+    if (k >= 0 && s.val[i] != 0) global_add(D, k, s.val[i], to_delta);
+  }
+}
+
+// find-or-claim the key-table slot; returns slot, *claimed = 1 if this thread
+// inserted the key
+__device__ inline int32_t ht_insert(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
+  const u64 k = probe_key(h1, h2, len);
+  u64 s = (k * 0xD6E8FEB86659FD93ULL) >> D.ht_shift;
+  const u64 mask = (u64)D.HC - 1;
+  *claimed = false;
+  for (int64_t probe = 0; probe < D.HC; probe++) {
+    const u64 cur = D.ht_key[s];
+    if (cur == k) return (int32_t)s;
+    if (cur == 0) {
+      const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s], 0ULL, (unsigned long long)k);
+      if (old == 0) {
+        *claimed = true;
+        return (int32_t)s;
+      }
+      if (old == k) return (int32_t)s;
+    }
+    s = (s + 1) & mask;
+  }
+  set_error(D, GEOBPE_ECAPACITY, -2);
+  return -1;
+}
+
+// per-workgroup output region with an LDS cursor; spills to a global overflow list
+template <class T>
+struct Region {
+  T* base;       // this workgroup's region
+  int64_t cap;
+  int32_t* cnt;  // LDS cursor
+  T* ovf;
+  int64_t* ovf_n;
+  int64_t ovf_cap;
+};
+
+}  // namespace gb

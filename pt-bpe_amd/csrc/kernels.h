@@ -1,0 +1,842 @@
+// kernels.h -- the HIP kernels of the GeoBPE engine (gfx950).  Included once, by
+// geobpe.hip.  Reference behaviour cited per kernel; layout in DESIGN.md §3.
+#pragma once
+#include "device.h"
+
+namespace gb {
+
+// ====================================================================== prologue
+__constant__ int32_t c_type_col[GEOBPE_NTYPES] = {GEOBPE_COL_TAU, GEOBPE_COL_CAC1N, GEOBPE_COL_C1NCA,
+                                                  GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_PHI};
+struct Cols {
+  const double* c[9];
+};
+
+// per (workgroup, type) min / max / count of the wrapped non-NaN non-zero values
+// (the inputs of np.histogram in BPE._init_thresholds, bpe.py:840-850)
+__global__ __launch_bounds__(BLOCK) void k_range(Cols cols, int64_t R, double* part) {
+  const int t = blockIdx.y;
+  const double* x = cols.c[c_type_col[t]];
+  double mn = INFINITY, mx = -INFINITY;
+  int64_t cnt = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < R; i += (int64_t)gridDim.x * blockDim.x) {
+    const double v = x[i];
+    if (v == v && v != 0.0) {
+      const double w = wrap2pi(v);
+      mn = fmin(mn, w);
+      mx = fmax(mx, w);
+      cnt++;
+    }
+  }
+  __shared__ double smn[BLOCK], smx[BLOCK];
+  __shared__ int64_t scn[BLOCK];
+  smn[threadIdx.x] = mn;
+  smx[threadIdx.x] = mx;
+  scn[threadIdx.x] = cnt;
+  __syncthreads();
+  for (int o = BLOCK / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      smn[threadIdx.x] = fmin(smn[threadIdx.x], smn[threadIdx.x + o]);
+      smx[threadIdx.x] = fmax(smx[threadIdx.x], smx[threadIdx.x + o]);
+      scn[threadIdx.x] += scn[threadIdx.x + o];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    double* p = part + ((int64_t)t * gridDim.x + blockIdx.x) * 3;
+    p[0] = smn[0];
+    p[1] = smx[0];
+    p[2] = (double)scn[0];
+  }
+}
+
+// residue / junction symbols: SURVEY.md App. A with the Tokenizer index maps
+// (tokenizer.py:131-167) and get_ind (bpe.py:1164-1189)
+__global__ __launch_bounds__(64) void k_quantize(Dev D, Cols cols, const double* edges, double init_tau) {
+  const int32_t B = D.B;
+  const double* eT = edges + 0 * (B + 1);
+  const double* eA = edges + 1 * (B + 1);
+  const double* eC = edges + 2 * (B + 1);
+  const double* eP = edges + 3 * (B + 1);
+  const double* eO = edges + 4 * (B + 1);
+  const double* eF = edges + 5 * (B + 1);
+  const double* tau = cols.c[GEOBPE_COL_TAU];
+  const double* cac1n = cols.c[GEOBPE_COL_CAC1N];
+  const double* c1nca = cols.c[GEOBPE_COL_C1NCA];
+  const double* psi = cols.c[GEOBPE_COL_PSI];
+  const double* omega = cols.c[GEOBPE_COL_OMEGA];
+  const double* phi = cols.c[GEOBPE_COL_PHI];
+  for (int64_t r = blockIdx.x; r < D.nrows; r += gridDim.x) {
+    const int64_t a = D.row_off[r], b = D.row_off[r + 1];
+    for (int64_t g = a + threadIdx.x; g < b; g += blockDim.x) {
+      const bool last = (g == b - 1);
+      const double ts = (g == a) ? init_tau : tau[g - 1];  // tau_j = df.tau[j-1]
+      const int32_t tb = get_ind(eT, B, wrap2pi(ts));
+      int32_t rs, gs = -1;
+      bool bad = tb < 0;
+      if (!last) {
+        const int32_t ab = get_ind(eA, B, wrap2pi(cac1n[g]));
+        const int32_t pb = get_ind(eP, B, wrap2pi(psi[g]));
+        const int32_t ob = get_ind(eO, B, wrap2pi(omega[g]));
+        const int32_t cb = get_ind(eC, B, wrap2pi(c1nca[g]));
+        const int32_t fb = get_ind(eF, B, wrap2pi(phi[g + 1]));
+        bad = bad || ab < 0 || pb < 0 || ob < 0 || cb < 0 || fb < 0;
+        rs = tb * D.B2 + ab * B + pb;
+        gs = ob * D.B2 + cb * B + fb;
+      } else {
+        rs = D.B3 + tb;
+      }
+      if (bad) {
+        set_error(D, GEOBPE_EVALUE, g);
+        rs = last ? D.B3 : 0;
+        gs = last ? -1 : 0;
+      }
+      D.rsym[g] = rs;
+      D.gsym[g] = gs;
+    }
+  }
+}
+
+// first appearance of every residue symbol (label order of bpe.py:236-246)
+__global__ __launch_bounds__(BLOCK) void k_first(Dev D, int64_t row_base, u64* first, int32_t S, int use_lds) {
+  extern __shared__ u64 sfirst[];
+  if (use_lds) {
+    for (int i = threadIdx.x; i < S; i += blockDim.x) sfirst[i] = ~0ULL;
+    __syncthreads();
+  }
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t s = D.rsym[g];
+    if (use_lds)
+      atomicMin(&sfirst[s], (u64)(g + row_base));
+    else
+      atomicMin((unsigned long long*)&first[s], (unsigned long long)(g + row_base));
+  }
+  if (use_lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < S; i += blockDim.x)
+      if (sfirst[i] != ~0ULL) atomicMin((unsigned long long*)&first[i], (unsigned long long)sfirst[i]);
+  }
+}
+
+__global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_of_sym) {
+  for (int64_t r = blockIdx.x; r < D.nrows; r += gridDim.x) {
+    const int64_t a = D.row_off[r], b = D.row_off[r + 1];
+    for (int64_t g = a + threadIdx.x; g < b; g += blockDim.x) {
+      D.tid[g] = label_of_sym[D.rsym[g]];
+      D.tlen[g] = 1;
+      D.tprev[g] = (g == a) ? -1 : (int32_t)(g - 1);
+      D.pk[g] = -1;
+      D.role[g] = 0;
+    }
+  }
+}
+
+// ====================================================================== region emitters
+// new pair into this workgroup's region (LDS cursor), spilling to the overflow list
+__device__ inline void emit_pair(const Dev& D, int32_t* s_cnt, int32_t target, int32_t slot, int32_t len,
+                                 int32_t delta, u64 h1, u64 h2) {
+  NewPair e;
+  e.target = target;
+  e.slot = slot;
+  e.len = len;
+  e.delta = delta;
+  e.h1 = h1;
+  e.h2 = h2;
+  const int32_t j = atomicAdd(s_cnt, 1);
+  if (j < D.RC) {
+    D.np[(int64_t)blockIdx.x * D.RC + j] = e;
+  } else {
+    const int64_t k = atomicAdd((unsigned long long*)&D.st->np_ovf, 1ULL);
+    if (k < D.ovf_cap)
+      D.npovf[k] = e;
+    else
+      set_error(D, GEOBPE_ECAPACITY, -3);
+  }
+}
+
+__device__ inline void emit_slot(const Dev& D, int32_t* s_cnt, int32_t slot, int32_t len, int32_t idL, int32_t g,
+                                 int32_t idR, u64 h1, u64 h2) {
+  NewSlot e;
+  e.slot = slot;
+  e.len = len;
+  e.idL = idL;
+  e.g = g;
+  e.idR = idR;
+  e.pad = 0;
+  e.h1 = h1;
+  e.h2 = h2;
+  const int32_t j = atomicAdd(s_cnt, 1);
+  if (j < D.RC) {
+    D.ns[(int64_t)blockIdx.x * D.RC + j] = e;
+  } else {
+    const int64_t k = atomicAdd((unsigned long long*)&D.st->ns_ovf, 1ULL);
+    if (k < D.ovf_cap)
+      D.nsovf[k] = e;
+    else
+      set_error(D, GEOBPE_ECAPACITY, -4);
+  }
+}
+
+// insert (or find) a pair key and emit the pair
+__device__ inline void add_pair(const Dev& D, int32_t* s_np, int32_t* s_ns, int32_t target, u64 h1, u64 h2,
+                                int32_t len, int32_t idL, int32_t g, int32_t idR, int32_t delta) {
+  bool claimed;
+  const int32_t slot = ht_insert(D, h1, h2, len, &claimed);
+  if (slot < 0) return;
+  if (claimed) emit_slot(D, s_ns, slot, len, idL, g, idR, h1, h2);
+  emit_pair(D, s_np, target, slot, len, delta, h1, h2);
+}
+
+__device__ inline void close_regions(const Dev& D, int32_t* s_np, int32_t* s_ns) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    D.npcnt[blockIdx.x] = min(*s_np, (int32_t)D.RC);
+    D.nscnt[blockIdx.x] = min(*s_ns, (int32_t)D.RC);
+  }
+}
+
+// ====================================================================== histogram
+// BPE.bin (bpe.py:1431-1474): every live adjacent pair -> content hash -> key
+__global__ __launch_bounds__(BLOCK) void k_pairs_all(Dev D) {
+  __shared__ int32_t s_np, s_ns;
+  if (threadIdx.x == 0) s_np = s_ns = 0;
+  __syncthreads();
+  const int64_t SC = (D.R + D.NB - 1) / D.NB;
+  const int64_t lo = (int64_t)blockIdx.x * SC, hi = min(D.R, lo + SC);
+  for (int64_t g = lo + threadIdx.x; g < hi; g += blockDim.x) {
+    const int32_t L = D.tid[g];
+    if (L < 0) continue;
+    const int32_t e = (int32_t)g + D.tlen[g] - 1;
+    if (D.rsym[e] >= D.B3) continue;  // last token of its chain
+    const int32_t Rr = D.tid[e + 1];
+    const int32_t gl = D.gsym[e];
+    const int32_t ylen = D.vlen[Rr];
+    u64 h1, h2;
+    combine(D, D.vh1[L], D.vh2[L], gl, D.vh1[Rr], D.vh2[Rr], ylen, h1, h2);
+    add_pair(D, &s_np, &s_ns, (int32_t)g, h1, h2, D.vlen[L] + ylen, L, gl, Rr, 1);
+  }
+  close_regions(D, &s_np, &s_ns);
+}
+
+// dense ids for the keys claimed since the last commit: region r's claims get
+// U + (claims of regions < r) + i; overflow claims follow all regions
+__global__ __launch_bounds__(BLOCK) void k_assign(Dev D, int merge_iter) {
+  __shared__ int64_t s_sum[BLOCK];
+  if (merge_iter && D.st->done) return;
+  const int64_t U = D.st->U;
+  const int32_t per = (D.NB + gridDim.x - 1) / gridDim.x;
+  const int32_t r0 = min((int32_t)blockIdx.x * per, D.NB), r1 = min(r0 + per, D.NB);
+  int64_t base = block_sum_before(D.nscnt, D.NB, r0, s_sum);
+  const int64_t total = block_sum_before(D.nscnt, D.NB, D.NB, s_sum);
+  const int64_t novf = min(D.st->ns_ovf, D.ovf_cap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.st->nnew_total = total + novf;
+  if (merge_iter && blockIdx.x == 0) {  // merges applied this iteration -> merge log
+    const int64_t nm = block_sum_before(D.Lcnt, D.NB, D.NB, s_sum) + min(D.st->L_ovf, D.Lovf_cap);
+    if (threadIdx.x == 0) D.log[D.st->iter - 1].nmerged = nm;
+  }
+  for (int32_t r = r0; r < r1; r++) {
+    const int32_t n = D.nscnt[r];
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+      const NewSlot e = D.ns[(int64_t)r * D.RC + i];
+      const int64_t d = U + base + i;
+      if (d >= D.UC) {
+        set_error(D, GEOBPE_ECAPACITY, -5);
+        continue;
+      }
+      D.ht_dense[e.slot] = (int32_t)d;
+      D.kh1[d] = e.h1;
+      D.kh2[d] = e.h2;
+      D.klen[d] = e.len;
+      D.krep[3 * d + 0] = e.idL;
+      D.krep[3 * d + 1] = e.g;
+      D.krep[3 * d + 2] = e.idR;
+      D.count[d] = 0;
+      if (D.dcount) {
+        D.dcount[d] = 0;
+        D.touch[d] = -1;
+      }
+    }
+    base += n;
+  }
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x) {
+    const NewSlot e = D.nsovf[k];
+    const int64_t d = U + total + k;
+    if (d >= D.UC) {
+      set_error(D, GEOBPE_ECAPACITY, -6);
+      continue;
+    }
+    D.ht_dense[e.slot] = (int32_t)d;
+    D.kh1[d] = e.h1;
+    D.kh2[d] = e.h2;
+    D.klen[d] = e.len;
+    D.krep[3 * d + 0] = e.idL;
+    D.krep[3 * d + 1] = e.g;
+    D.krep[3 * d + 2] = e.idR;
+    D.count[d] = 0;
+    if (D.dcount) {
+      D.dcount[d] = 0;
+      D.touch[d] = -1;
+    }
+  }
+}
+
+// pair -> dense key id into pk, counts via LDS-staged partial counts
+__device__ inline void finalize_one(const Dev& D, Agg& agg, const NewPair& e, int64_t j, bool to_delta) {
+  const int32_t d = D.ht_dense[e.slot];
+  if (d < 0 || D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) {
+    set_error(D, GEOBPE_EHASH, j);
+    return;
+  }
+  if (e.target >= 0) D.pk[e.target] = d;
+  agg_add(agg, D, d, e.delta, to_delta);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_finalize(Dev D, int to_delta, int merge_iter) {
+  __shared__ Agg agg;
+  if (merge_iter && D.st->done) return;
+  agg_init(agg);
+  if (blockIdx.x == 0 && threadIdx.x == 0) D.st->U += D.st->nnew_total;
+  const int32_t n = D.npcnt[blockIdx.x];
+  const NewPair* reg = D.np + (int64_t)blockIdx.x * D.RC;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) finalize_one(D, agg, reg[i], i, to_delta != 0);
+  const int64_t novf = min(D.st->np_ovf, D.ovf_cap);
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x)
+    finalize_one(D, agg, D.npovf[k], k, to_delta != 0);
+  agg_flush(agg, D, to_delta != 0);
+}
+
+// ====================================================================== argmax + tie-break
+// the reference key string json.dumps(geo, sort_keys=True) of a content, char by
+// char (same rendering as keyjson.h::render_key)
+struct JGen {
+  const int32_t *A, *C;
+  int32_t nA, g, nC;
+  int32_t B, B2, B3, r, lam;
+  int32_t sec, item, len, pos;
+  char buf[24];
+
+  __device__ int32_t sym(int32_t k) const { return k < nA ? A[k] : (k == nA ? g : C[k - nA - 1]); }
+  __device__ void init(const int32_t* a, int32_t na, int32_t gg, const int32_t* c, int32_t nc, int32_t b) {
+    A = a;
+    nA = na;
+    g = gg;
+    C = c;
+    nC = nc;
+    B = b;
+    B2 = b * b;
+    B3 = B2 * b;
+    const int32_t n = na + 1 + nc;
+    r = (n + 1) / 2;
+    lam = sym(n - 1) >= B3 ? 1 : 0;
+    sec = -1;
+    item = len = pos = 0;
+  }
+  __device__ int32_t sec_len(int32_t s) const {
+    switch (s) {
+      case 0: case 3: case 7: return r - lam;
+      case 1: case 5: case 6: return r - 1;
+      default: return r;
+    }
+  }
+  __device__ int32_t value(int32_t s, int32_t i) const {
+    switch (s) {
+      case 1: return sym(2 * i + 1) / B % B;   // C:1N:1CA
+      case 3: return sym(2 * i) / B % B;       // CA:C:1N
+      case 5: return sym(2 * i + 1) / B2;      // omega
+      case 6: return sym(2 * i + 1) % B;       // phi
+      case 7: return sym(2 * i) % B;           // psi
+      case 8: {                                // tau
+        const int32_t x = sym(2 * i);
+        return x >= B3 ? x - B3 : x / B2;
+      }
+      default: return 0;                       // bond lists (std_bonds)
+    }
+  }
+  __device__ void put(const char* s) {
+    while (*s) buf[len++] = *s++;
+  }
+  __device__ void put_int(int32_t v) {
+    char t[12];
+    int n = 0;
+    do {
+      t[n++] = (char)('0' + v % 10);
+      v /= 10;
+    } while (v);
+    while (n) buf[len++] = t[--n];
+  }
+  __device__ bool refill() {
+    len = pos = 0;
+    if (sec == 9) return false;
+    if (sec == -1) {
+      put("{\"0C:1N\": [");
+      sec = 0;
+      item = 0;
+      return true;
+    }
+    if (item < sec_len(sec)) {
+      if (item > 0) put(", ");
+      put_int(value(sec, item));
+      item++;
+      return true;
+    }
+    if (sec == 8) {
+      put("]}");
+      sec = 9;
+      return true;
+    }
+    sec++;
+    item = 0;
+    put("], \"");
+    switch (sec) {
+      case 1: put("C:1N:1CA"); break;
+      case 2: put("CA:C"); break;
+      case 3: put("CA:C:1N"); break;
+      case 4: put("N:CA"); break;
+      case 5: put("omega"); break;
+      case 6: put("phi"); break;
+      case 7: put("psi"); break;
+      default: put("tau"); break;
+    }
+    put("\": [");
+    return true;
+  }
+  __device__ int next() {
+    while (pos >= len)
+      if (!refill()) return -1;
+    return (unsigned char)buf[pos++];
+  }
+};
+
+__device__ inline void key_src(const Dev& D, int32_t d, const int32_t** A, int32_t* nA, int32_t* g, const int32_t** C,
+                               int32_t* nC) {
+  const int32_t L = D.krep[3 * d], Rr = D.krep[3 * d + 2];
+  *g = D.krep[3 * d + 1];
+  *A = D.vsym + D.voff[L];
+  *nA = (int32_t)(D.voff[L + 1] - D.voff[L]);
+  *C = D.vsym + D.voff[Rr];
+  *nC = (int32_t)(D.voff[Rr + 1] - D.voff[Rr]);
+}
+
+// true iff key a's reference string < key b's (Python str order)
+__device__ inline bool key_less(const Dev& D, int32_t a, int32_t b) {
+  JGen x, y;
+  const int32_t *A, *C;
+  int32_t nA, g, nC;
+  key_src(D, a, &A, &nA, &g, &C, &nC);
+  x.init(A, nA, g, C, nC, D.B);
+  key_src(D, b, &A, &nA, &g, &C, &nC);
+  y.init(A, nA, g, C, nC, D.B);
+  for (;;) {
+    const int ca = x.next(), cb = y.next();
+    if (ca != cb) return ca < cb;
+    if (ca < 0) return false;
+  }
+}
+
+// per-workgroup max count over its dense-key range + up to BLK_CANDS keys at it
+__global__ __launch_bounds__(BLOCK) void k_argmax_blocks(Dev D) {
+  __shared__ int32_t s_red[BLOCK / 64];
+  __shared__ int32_t s_n;
+  __shared__ int32_t s_c[BLK_CANDS];
+  if (D.st->done) return;
+  const int64_t U = D.st->U;
+  const int64_t U4 = (U + 3) / 4;
+  const int64_t per = (U4 + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U4, lo + per);
+  const int4* c4 = reinterpret_cast<const int4*>(D.count);
+  int32_t m = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+    const int4 v = c4[i];
+    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+  }
+  m = block_max(m, s_red);
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  if (m > 0) {
+    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
+      const int4 v = c4[i];
+      const int32_t vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        if (vv[q] == m) {
+          const int32_t j = atomicAdd(&s_n, 1);
+          if (j < BLK_CANDS) s_c[j] = (int32_t)(4 * i + q);
+        }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    BlkMax r;
+    r.max = m;
+    r.n = s_n;
+    for (int q = 0; q < BLK_CANDS; q++) r.c[q] = q < s_n ? s_c[q] : -1;
+    D.blk[blockIdx.x] = r;
+  }
+}
+
+// one workgroup: global max, exact candidate set, reference tie-break, then the
+// new token (BPE.step, bpe.py:1796-1860): id, vocab hash / content, merge log
+__global__ __launch_bounds__(BLOCK) void k_select_final(Dev D, int32_t nblk) {
+  __shared__ int32_t s_red[BLOCK / 64];
+  __shared__ int32_t s_nc;
+  __shared__ int32_t s_nres;
+  __shared__ int32_t s_res[64];
+  __shared__ int32_t s_best[BLOCK];
+  if (D.st->done) return;
+  int32_t m = 0;
+  for (int32_t i = threadIdx.x; i < nblk; i += blockDim.x) m = max(m, D.blk[i].max);
+  m = block_max(m, s_red);
+  if (m <= 0) {
+    if (threadIdx.x == 0) {
+      D.st->done = 1;
+      D.st->maxc = 0;
+    }
+    return;
+  }
+  if (threadIdx.x == 0) {
+    s_nc = 0;
+    s_nres = 0;
+  }
+  __syncthreads();
+  // candidates: listed ones, or a rescan of workgroups that had more than BLK_CANDS
+  for (int32_t i = threadIdx.x; i < nblk; i += blockDim.x) {
+    const BlkMax& b = D.blk[i];
+    if (b.max != m) continue;
+    if (b.n <= BLK_CANDS) {
+      for (int q = 0; q < b.n; q++) {
+        const int32_t j = atomicAdd(&s_nc, 1);
+        if (j < D.candcap) D.cand[j] = b.c[q];
+      }
+    } else {
+      const int32_t j = atomicAdd(&s_nres, 1);
+      if (j < 64) s_res[j] = i;
+    }
+  }
+  __syncthreads();
+  const int64_t U = D.st->U;
+  const int64_t U4 = (U + 3) / 4;
+  const int64_t per = (U4 + nblk - 1) / nblk;
+  const int32_t nres = s_nres;
+  if (nres > 64) {  // many tied workgroups: rescan every key
+    __syncthreads();
+    if (threadIdx.x == 0) s_nc = 0;
+    __syncthreads();
+    for (int64_t d = threadIdx.x; d < U; d += blockDim.x)
+      if (D.count[d] == m) {
+        const int32_t j = atomicAdd(&s_nc, 1);
+        if (j < D.candcap) D.cand[j] = (int32_t)d;
+      }
+  } else {
+    for (int32_t q = 0; q < nres; q++) {
+      const int64_t lo = 4 * (int64_t)s_res[q] * per, hi = min(U, lo + 4 * per);
+      for (int64_t d = lo + threadIdx.x; d < hi; d += blockDim.x)
+        if (D.count[d] == m) {
+          const int32_t j = atomicAdd(&s_nc, 1);
+          if (j < D.candcap) D.cand[j] = (int32_t)d;
+        }
+    }
+  }
+  __syncthreads();
+  const int32_t nc = min(s_nc, (int32_t)D.candcap);
+  if (s_nc > D.candcap && threadIdx.x == 0) set_error(D, GEOBPE_ECAPACITY, -8);
+  // tie-break: smallest reference key string (SortedDict order, bpe.py:1469-1471)
+  int32_t best = -1;
+  for (int32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+    const int32_t d = D.cand[i];
+    if (best < 0 || key_less(D, d, best)) best = d;
+  }
+  s_best[threadIdx.x] = best;
+  __syncthreads();
+  for (int o = BLOCK / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const int32_t a = s_best[threadIdx.x], b = s_best[threadIdx.x + o];
+      if (a < 0 || (b >= 0 && key_less(D, b, a))) s_best[threadIdx.x] = b;
+    }
+    __syncthreads();
+  }
+  const int32_t W = s_best[0];
+  const int32_t nid = D.st->K;
+  const int32_t L = D.krep[3 * W], g = D.krep[3 * W + 1], Rr = D.krep[3 * W + 2];
+  const int64_t nL = D.voff[L + 1] - D.voff[L], nR = D.voff[Rr + 1] - D.voff[Rr];
+  const int64_t pos = D.st->vsym_used, ln = nL + 1 + nR;
+  if (nid >= D.KC || pos + ln > D.VSC) {
+    if (threadIdx.x == 0) {
+      set_error(D, GEOBPE_ECAPACITY, -9);
+      D.st->done = 1;
+    }
+    return;
+  }
+  // _tokens[n] = json.loads(key): content = content(L) ++ [g] ++ content(R)
+  for (int64_t i = threadIdx.x; i < ln; i += blockDim.x)
+    D.vsym[pos + i] = i < nL ? D.vsym[D.voff[L] + i] : (i == nL ? g : D.vsym[D.voff[Rr] + i - nL - 1]);
+  __syncthreads();  // every thread has read st->K / vsym_used before they move
+  if (threadIdx.x == 0) {
+    D.voff[nid + 1] = pos + ln;
+    D.vh1[nid] = D.kh1[W];
+    D.vh2[nid] = D.kh2[W];
+    D.vlen[nid] = D.klen[W];
+    State* st = D.st;
+    LogRec lr;
+    lr.nid = nid;
+    lr.count = m;
+    lr.W = W;
+    lr.idL = L;
+    lr.g = g;
+    lr.idR = Rr;
+    lr.nmerged = 0;
+    D.log[st->iter] = lr;
+    st->vsym_used = pos + ln;
+    st->K = nid + 1;
+    st->iter += 1;
+    st->tag = st->iter;
+    st->W = W;
+    st->nid = nid;
+    st->maxc = m;
+    st->ncand = nc;
+    st->L_ovf = st->np_ovf = st->ns_ovf = st->nnew_total = 0;
+  }
+}
+
+// ====================================================================== merge-apply
+// walk one maximal run of winner matches starting at token h: greedy left to
+// right (bpe.py:1888-1916) -- merge h, skip the next pair, merge the one after
+// if the run continues, ...
+__device__ inline void walk_run(const Dev& D, int32_t h, int32_t W, int32_t tag, int32_t* s_n) {
+  int32_t t = h, p = D.tprev[h];
+  for (;;) {
+    const int32_t b = t + D.tlen[t];
+    const int32_t pkb = D.pk[b];
+    const int32_t c = pkb >= 0 ? b + D.tlen[b] : -1;
+    LEntry e;
+    e.a = t;
+    e.p = p;
+    e.b = b;
+    e.c = c;
+    D.role[t] = (tag << 2) | 1;
+    D.role[b] = (tag << 2) | 2;
+    const int32_t j = atomicAdd(s_n, 1);
+    if (j < D.LC) {
+      D.L[(int64_t)blockIdx.x * D.LC + j] = e;
+    } else {
+      const int64_t k = atomicAdd((unsigned long long*)&D.st->L_ovf, 1ULL);
+      if (k < D.Lovf_cap)
+        D.Lovf[k] = e;
+      else
+        set_error(D, GEOBPE_ECAPACITY, -10);
+    }
+    if (pkb != W) break;
+    if (D.pk[c] != W) break;
+    p = b;
+    t = c;
+  }
+}
+
+// scan pk for the winner key (4 x int4 per lane in flight), start a walk at every
+// run start; each workgroup owns CH int4 groups and one output region
+__global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
+  __shared__ int32_t s_n;
+  if (D.st->done) return;
+  const int32_t W = D.st->W, tag = D.st->tag;
+  if (threadIdx.x == 0) s_n = 0;
+  __syncthreads();
+  const int64_t n4 = (D.R + 3) / 4;
+  const int64_t lo = (int64_t)blockIdx.x * D.CH, hi = min(n4, lo + D.CH);
+  const int4* pk4 = reinterpret_cast<const int4*>(D.pk);
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 4 * BLOCK) {
+    int4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int64_t i = i0 + u * BLOCK;
+      v[u] = i < hi ? pk4[i] : make_int4(-1, -1, -1, -1);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        if (vv[q] == W) {
+          const int32_t g = (int32_t)(4 * (i0 + u * BLOCK) + q);
+          const int32_t p = D.tprev[g];
+          if (p < 0 || D.pk[p] != W) walk_run(D, g, W, tag, &s_n);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = min(s_n, (int32_t)D.LC);
+}
+
+// rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014)
+__device__ inline void apply_one(const Dev& D, Agg& agg, int32_t* s_np, int32_t* s_ns, const LEntry& e, int32_t W,
+                                 int32_t nid, u64 w1, u64 w2, int32_t wl, int32_t tagL, int32_t tagR, bool to_delta) {
+  const int32_t pkb = D.pk[e.b];
+  agg_add(agg, D, W, -1, to_delta);                        // step 1: the merged pair
+  if (pkb >= 0) agg_add(agg, D, pkb, -1, to_delta);        // step 4: right neighbour pair
+  const bool pN = e.p >= 0 && D.role[e.p] != tagR;
+  if (pN) agg_add(agg, D, D.pk[e.p], -1, to_delta);        // step 3: left neighbour pair
+  D.tid[e.a] = nid;                                        // step 2: bond_to_token / token_pos
+  D.tlen[e.a] = wl;
+  D.tid[e.b] = -1;
+  D.pk[e.b] = -1;
+  if (e.c >= 0) D.tprev[e.c] = e.a;
+  if (pN) {                                                // step 5: new left pair
+    const int32_t L = D.tid[e.p];
+    const int32_t gl = D.gsym[e.a - 1];
+    u64 h1, h2;
+    combine(D, D.vh1[L], D.vh2[L], gl, w1, w2, wl, h1, h2);
+    add_pair(D, s_np, s_ns, e.p, h1, h2, D.vlen[L] + wl, L, gl, nid, 1);
+  }
+  if (e.c >= 0) {                                          // step 5: new right pair
+    const bool cL = D.role[e.c] == tagL;
+    const int32_t idr = cL ? nid : D.tid[e.c];
+    const u64 r1 = cL ? w1 : D.vh1[idr], r2 = cL ? w2 : D.vh2[idr];
+    const int32_t rl = cL ? wl : D.vlen[idr];
+    const int32_t gl = D.gsym[e.a + wl - 1];
+    u64 h1, h2;
+    combine(D, w1, w2, gl, r1, r2, rl, h1, h2);
+    add_pair(D, s_np, s_ns, e.a, h1, h2, wl + rl, nid, gl, idr, 1);
+  } else {
+    D.pk[e.a] = -1;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
+  __shared__ Agg agg;
+  __shared__ int32_t s_np, s_ns;
+  if (D.st->done) return;
+  agg_init(agg);
+  if (threadIdx.x == 0) s_np = s_ns = 0;
+  __syncthreads();
+  const int32_t W = D.st->W, nid = D.st->nid, tag = D.st->tag;
+  const u64 w1 = D.kh1[W], w2 = D.kh2[W];
+  const int32_t wl = D.klen[W];
+  const int32_t tagR = (tag << 2) | 2, tagL = (tag << 2) | 1;
+  const int32_t n = D.Lcnt[blockIdx.x];
+  const LEntry* reg = D.L + (int64_t)blockIdx.x * D.LC;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x)
+    apply_one(D, agg, &s_np, &s_ns, reg[i], W, nid, w1, w2, wl, tagL, tagR, to_delta != 0);
+  const int64_t novf = min(D.st->L_ovf, D.Lovf_cap);
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x)
+    apply_one(D, agg, &s_np, &s_ns, D.Lovf[k], W, nid, w1, w2, wl, tagL, tagR, to_delta != 0);
+  agg_flush(agg, D, to_delta != 0);
+  close_regions(D, &s_np, &s_ns);
+}
+
+// ====================================================================== multi-rank deltas
+__global__ __launch_bounds__(BLOCK) void k_export(Dev D, DeltaRec* out, int64_t n) {
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t d = D.touched[j];
+    DeltaRec r;
+    r.h1 = D.kh1[d];
+    r.h2 = D.kh2[d];
+    r.len = D.klen[d];
+    r.idL = D.krep[3 * d];
+    r.g = D.krep[3 * d + 1];
+    r.idR = D.krep[3 * d + 2];
+    r.delta = D.dcount[d];
+    r.pad = 0;
+    D.dcount[d] = 0;
+    out[j] = r;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_import(Dev D, const DeltaRec* in, int64_t n) {
+  __shared__ int32_t s_np, s_ns;
+  if (threadIdx.x == 0) s_np = s_ns = 0;
+  __syncthreads();
+  const int64_t E = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * E, hi = min(n, lo + E);
+  for (int64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+    const DeltaRec r = in[j];
+    if (r.delta == 0) continue;
+    add_pair(D, &s_np, &s_ns, -1, r.h1, r.h2, r.len, r.idL, r.g, r.idR, r.delta);
+  }
+  close_regions(D, &s_np, &s_ns);
+}
+
+// ====================================================================== exports / checks
+__global__ __launch_bounds__(BLOCK) void k_row_ntok(Dev D, int64_t* ntok) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = D.row_off[r], b = D.row_off[r + 1];
+    int64_t n = 0;
+    for (int64_t g = a; g < b; g += D.tlen[g]) n++;
+    ntok[r] = n;
+  }
+}
+
+__global__ __launch_bounds__(BLOCK) void k_row_seg(Dev D, const int64_t* tok_off, int32_t* start, int32_t* id) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = D.row_off[r], b = D.row_off[r + 1];
+    int64_t t = tok_off[r];
+    for (int64_t g = a; g < b; g += D.tlen[g]) {
+      start[t] = (int32_t)(g - a);
+      id[t] = D.tid[g];
+      t++;
+    }
+  }
+}
+
+// quantize(tokenize()) per chain: id, then K+B+omega, K+2B+phi, K+cnca
+// (tokenizer.py:379-392, bpe.py:918-956)
+__global__ __launch_bounds__(BLOCK) void k_row_encode(Dev D, const int64_t* id_off, int32_t* ids, int32_t K) {
+  const int32_t B = D.B;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.nrows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t a = D.row_off[r], b = D.row_off[r + 1];
+    int64_t t = id_off[r];
+    for (int64_t g = a; g < b;) {
+      const int64_t e = g + D.tlen[g] - 1;
+      ids[t++] = D.tid[g];
+      if (e + 1 < b) {
+        const int32_t gs = D.gsym[e];
+        ids[t++] = K + B + gs / D.B2;
+        ids[t++] = K + 2 * B + gs % B;
+        ids[t++] = K + gs / B % B;
+      }
+      g = e + 1;
+    }
+  }
+}
+
+// full recount of the live pair histogram from pk (verification)
+__global__ __launch_bounds__(BLOCK) void k_recount(Dev D) {
+  __shared__ Agg agg;
+  agg_init(agg);
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t d = D.pk[g];
+    if (d < 0) continue;
+    uint32_t h = ((uint32_t)d * 2654435761u) >> 21;
+    bool done = false;
+    for (int probe = 0; probe < 8 && !done; probe++) {
+      const int32_t k = agg.key[h];
+      if (k == d) {
+        atomicAdd(&agg.val[h], 1);
+        done = true;
+      } else if (k == -1) {
+        const int32_t old = atomicCAS(&agg.key[h], -1, d);
+        if (old == -1 || old == d) {
+          atomicAdd(&agg.val[h], 1);
+          done = true;
+        }
+      }
+      h = (h + 1) & (AGG - 1);
+    }
+    if (!done) atomicAdd(&D.scratch[d], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < AGG; i += blockDim.x)
+    if (agg.key[i] >= 0) atomicAdd(&D.scratch[agg.key[i]], agg.val[i]);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_compare(Dev D) {
+  const int64_t U = D.st->U;
+  for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < U; d += (int64_t)gridDim.x * blockDim.x)
+    if (D.scratch[d] != D.count[d]) atomicAdd((unsigned long long*)&D.st->nmismatch, 1ULL);
+}
+
+// debug: device key-string order of n (a, b) key pairs (tests the JSON generator)
+__global__ void k_debug_key_less(Dev D, const int32_t* pairs, int32_t* out, int32_t n) {
+  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = key_less(D, pairs[2 * i], pairs[2 * i + 1]) ? 1 : 0;
+}
+
+}  // namespace gb

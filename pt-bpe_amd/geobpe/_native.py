@@ -54,6 +54,10 @@ def lib():
         "geobpe_init_tokens": (ctypes.c_int, [P, P, I32]),
         "geobpe_bin": (ctypes.c_int, [P]),
         "geobpe_step": (ctypes.c_int, [P, pI32, pI32, pI64]),
+        "geobpe_run": (ctypes.c_int, [P, I64, pI64]),
+        "geobpe_merge_log": (I64, [P, P, I64]),
+        "geobpe_key_json": (I64, [P, I32, ctypes.c_char_p, I64]),
+        "geobpe_debug_key_less": (ctypes.c_int, [P, P, I32, P]),
         "geobpe_step_select": (ctypes.c_int, [P, pI32, pI32]),
         "geobpe_step_apply": (ctypes.c_int, [P, pI64]),
         "geobpe_delta_export": (ctypes.c_int, [P, P, I64, pI64]),
@@ -70,6 +74,7 @@ def lib():
         "geobpe_verify_counts": (I64, [P]),
         "geobpe_set_profiling": (ctypes.c_int, [P, ctypes.c_int]),
         "geobpe_kernel_ms": (D, [P, ctypes.c_char_p, pI64]),
+        "geobpe_set_profiling_filter": (ctypes.c_int, [P, ctypes.c_char_p]),
         "geobpe_synchronize": (ctypes.c_int, [P]),
     }
     for name, (res, args) in sig.items():
@@ -83,10 +88,11 @@ def lib():
 EXPORTED_SYMBOLS = [
     "geobpe_create", "geobpe_destroy", "geobpe_last_error", "geobpe_load_angles", "geobpe_angle_range",
     "geobpe_quantize", "geobpe_symbol_first", "geobpe_init_tokens", "geobpe_bin", "geobpe_step",
+    "geobpe_run", "geobpe_merge_log", "geobpe_key_json", "geobpe_debug_key_less",
     "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
-    "geobpe_verify_counts", "geobpe_set_profiling", "geobpe_kernel_ms", "geobpe_synchronize",
+    "geobpe_verify_counts", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_synchronize",
 ]
 
 

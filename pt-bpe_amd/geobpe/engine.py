@@ -175,8 +175,7 @@ class GeoBPEEngine:
         nid, cnt = ctypes.c_int32(0), ctypes.c_int32(0)
         nm = ctypes.c_int64(0)
         if not self.distributed:
-            self._chk(self.L.geobpe_step(self._ctx, ctypes.byref(nid), ctypes.byref(cnt),
-                                         ctypes.byref(nm) if want_merged else None))
+            self._chk(self.L.geobpe_step(self._ctx, ctypes.byref(nid), ctypes.byref(cnt), ctypes.byref(nm)))
             if nid.value < 0:
                 self._done = True
                 return None
@@ -187,17 +186,38 @@ class GeoBPEEngine:
                 return None
             self._chk(self.L.geobpe_step_apply(self._ctx, ctypes.byref(nm) if want_merged else None))
             self._exchange()
-        rec = (int(nid.value), int(cnt.value), int(nm.value) if want_merged else -1)
+        want = want_merged or not self.distributed
+        rec = (int(nid.value), int(cnt.value), int(nm.value) if want else -1)
         self.merges.append(rec)
         return rec
 
-    def run(self, n_merges: int, want_merged: bool = False) -> int:
-        done = 0
-        for _ in range(n_merges):
-            if self.step(want_merged=want_merged) is None:
-                break
-            done += 1
-        return done
+    def run(self, n_merges: int) -> int:
+        """Enqueue ``n_merges`` iterations with no host synchronisation in between
+        (device-side argmax + tie-break); returns the merges actually made."""
+        if not self._binned:
+            raise RuntimeError("bin() first")
+        if self.distributed:
+            done = 0
+            for _ in range(n_merges):
+                if self.step(want_merged=False) is None:
+                    break
+                done += 1
+            return done
+        n = ctypes.c_int64(0)
+        self._chk(self.L.geobpe_run(self._ctx, int(n_merges), ctypes.byref(n)))
+        self._refresh_log()
+        if n.value < n_merges:
+            self._done = True
+        return int(n.value)
+
+    def _refresh_log(self):
+        m = int(self.L.geobpe_merge_log(self._ctx, None, 0))
+        if m < 0:
+            raise _native.GeoBPEError("merge log unavailable")
+        if m > len(self.merges):
+            buf = np.zeros(3 * m, dtype=np.int64)
+            self.L.geobpe_merge_log(self._ctx, _p(buf), m)
+            self.merges = [tuple(int(x) for x in buf[3 * i:3 * i + 3]) for i in range(m)]
 
     def synchronize(self):
         self._chk(self.L.geobpe_synchronize(self._ctx))
@@ -237,7 +257,23 @@ class GeoBPEEngine:
 
     def merge_keys(self):
         """[(key_json, count)] of every merge so far -- the reference's merge list."""
+        if not self.distributed:
+            self._refresh_log()
         return [(self.token_json(nid), c) for nid, c, _ in self.merges]
+
+    def key_json(self, d: int) -> str:
+        m = self.L.geobpe_key_json(self._ctx, d, None, 0)
+        if m < 0:
+            raise IndexError(d)
+        buf = ctypes.create_string_buffer(int(m) + 1)
+        self.L.geobpe_key_json(self._ctx, d, buf, m + 1)
+        return buf.value.decode()
+
+    def debug_key_less(self, pairs: np.ndarray) -> np.ndarray:
+        pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
+        out = np.zeros(len(pairs), dtype=np.int32)
+        self._chk(self.L.geobpe_debug_key_less(self._ctx, _p(pairs), len(pairs), _p(out)))
+        return out.astype(bool)
 
     def segmentation(self):
         T = self.L.geobpe_segmentation(self._ctx, None, None, None)
@@ -265,7 +301,8 @@ class GeoBPEEngine:
         return n
 
     # ------------------------------------------------------------ profiling
-    def set_profiling(self, on: bool = True):
+    def set_profiling(self, on: bool = True, only: str = ""):
+        self._chk(self.L.geobpe_set_profiling_filter(self._ctx, only.encode()))
         self._chk(self.L.geobpe_set_profiling(self._ctx, 1 if on else 0))
 
     def kernel_ms(self, name: str):

@@ -28,15 +28,19 @@ def _check_against_golden(run, meta, arrs, thresholds=None):
     assert np.array_equal(e, arrs["ids"]) and np.array_equal(eoff, arrs["ids_off"])
 
 
+@pytest.mark.parametrize("mode", ["step", "run"])
 @pytest.mark.parametrize("name", golden_names())
-def test_engine_matches_reference_golden(name):
+def test_engine_matches_reference_golden(name, mode):
     meta, corpus, arrs = load_golden(name)
     B = meta["bins"]["1"]
     eng = _engine(corpus, B)
     assert eng.K0 == meta["K0"]
     eng.bin()
-    for _ in range(len(meta["merges"])):
-        assert eng.step() is not None
+    if mode == "step":
+        for _ in range(len(meta["merges"])):
+            assert eng.step() is not None
+    else:  # device-resident loop: no host sync between merges
+        assert eng.run(len(meta["merges"])) == len(meta["merges"])
     _check_against_golden(eng, meta, arrs, eng.thresholds)
     assert eng.vocab_size == meta["vocab_size"]
     # merged tokens of the reference vocab are json.loads(key)
@@ -84,9 +88,7 @@ def test_engine_matches_oracle_synthetic(cfg, oracle_lib):
     eng = _engine(corpus, cfg["B"])
     assert eng.thresholds == o.thresholds
     eng.bin()
-    for _ in range(cfg["merges"]):
-        if eng.step() is None:
-            break
+    eng.run(cfg["merges"])
     assert eng.merge_keys() == o.merges
     assert eng.verify_counts() == 0
     e, eo = eng.encode()
@@ -162,4 +164,41 @@ def test_c3_scale_properties():
     e, eo = eng.encode()
     assert np.array_equal(np.diff(eo), 4 * ntok - 3)
     assert ids.min() >= 0 and ids.max() < eng.vocab_count
+    eng.close()
+
+
+@pytest.mark.parametrize("name", ["g40x40-120_b12", "g30x40-120_b2", "g60x20-90_b5_rep"])
+def test_device_key_order_matches_python_strings(name):
+    """The device tie-break (JGen in kernels.h) orders keys exactly like Python
+    str comparison of the reference key strings (two-digit bins included)."""
+    meta, corpus, _ = load_golden(name)
+    eng = _engine(corpus, meta["bins"]["1"])
+    eng.bin()
+    eng.run(30)
+    U = eng.num_keys
+    rng = np.random.default_rng(0)
+    pairs = rng.integers(0, U, size=(3000, 2)).astype(np.int32)
+    # near-ties: keys sharing long prefixes are the interesting comparisons
+    keys = [eng.key_json(d) for d in range(U)]
+    order = np.argsort(np.array(keys, dtype=object), kind="stable")
+    adj = np.stack([order[:-1], order[1:]], axis=1)[: 3000].astype(np.int32)
+    pairs = np.concatenate([pairs, adj, adj[:, ::-1]])
+    got = eng.debug_key_less(pairs)
+    exp = np.array([keys[a] < keys[b] for a, b in pairs])
+    assert np.array_equal(got, exp)
+    eng.close()
+
+
+def test_run_to_exhaustion_device_loop(oracle_lib):
+    """run() past the point where no pair is left stops cleanly (device done flag)."""
+    from geobpe import synth
+    lengths = synth.make_lengths(20, 1, 12, seed=51)
+    corpus = synth.make_corpus(lengths, seed=51, repeat_frac=0.3)
+    o = _oracle_run(oracle_lib, corpus, 3, 100000)
+    eng = _engine(corpus, 3)
+    eng.bin()
+    n = eng.run(10000)
+    assert n == len(o.merges)
+    assert eng.merge_keys() == o.merges
+    assert eng.run(5) == 0
     eng.close()
