@@ -17,8 +17,11 @@ constexpr u64 HP2 = 0x13579BDF2468ACE1ULL % M61;
 constexpr u64 KMIX = 0x9E3779B97F4A7C15ULL;
 constexpr double TWO_PI = 6.283185307179586;  // 2*np.pi
 constexpr int BLOCK = 256;
-constexpr int AGG = 2048;      // LDS partial-count slots per workgroup
+constexpr int AGG = 512;       // LDS partial-count slots per workgroup
+constexpr int AGG_SHIFT = 23;  // 32 - log2(AGG)
+constexpr int RPB = 8;         // mark regions per apply workgroup (NB = RPB * NBA)
 constexpr int BLK_CANDS = 8;   // argmax candidates kept per workgroup
+constexpr int ID_CHUNK = 256;  // dense ids a workgroup reserves at a time
 
 // ------------------------------------------------------------------ records
 struct State {
@@ -33,8 +36,12 @@ struct State {
   int32_t tag;        // role tag of the current merge (= iter)
   int32_t done;       // 1 once no pair is left
   int32_t W, nid, maxc, ncand;
+  // the winner, precomputed by k_select_final for k_mark / k_apply
+  u64 w1, w2;                      // content hash of the merged token
+  u64 pwW1a, pwW1b, pwW2a, pwW2b;  // P^(|W|syms+1), P^|W|syms (both bases)
+  int32_t wl, wfp;                 // residues of W, key_fp(W)
   // per-iteration, reset by k_select_final
-  int64_t L_ovf, np_ovf, ns_ovf, nnew_total;
+  int64_t L_ovf, np_ovf, ns_ovf, nL_total;
   int64_t ntouched, nmismatch;
 };
 
@@ -75,6 +82,7 @@ struct Dev {
   int32_t *rsym, *gsym;
   // tokens (residue indexed)
   int32_t *tid, *tlen, *tprev, *pk, *role;
+  uint16_t* fp;  // 16-bit fingerprint of pk (0xFFFF = none): the mark scan reads these
   // vocab (token id indexed)
   u64 *vh1, *vh2;
   int32_t* vlen;
@@ -94,11 +102,11 @@ struct Dev {
   int32_t *klen, *krep, *count, *dcount, *touch, *touched, *scratch;
   int64_t UC;
   // per-workgroup output regions (no global returning atomics on the hot path)
-  int32_t NB;       // workgroups of the region kernels
-  int32_t pad2;
-  int64_t CH;       // int4 groups of pk per mark workgroup
-  int64_t LC;       // merge entries per workgroup region
-  int64_t RC;       // new pairs / new keys per workgroup region
+  int32_t NB;       // mark workgroups (one merge region each)
+  int32_t NBA;      // apply / finalize / bin / import workgroups (one pair region each), NB = RPB*NBA
+  int64_t CH8;      // 8-slot fingerprint groups per mark workgroup
+  int64_t LC;       // merge entries per mark region
+  int64_t RC;       // new pairs / new keys per apply region
   LEntry* L;
   int32_t* Lcnt;
   LEntry* Lovf;
@@ -106,11 +114,11 @@ struct Dev {
   NewPair* np;
   int32_t* npcnt;
   NewPair* npovf;
-  NewSlot* ns;
-  int32_t* nscnt;
-  NewSlot* nsovf;
+  NewSlot* ns;  // keys claimed per apply region (dense ids given at region close)
+  int64_t* chunk;  // per apply workgroup: [next, end) of its reserved dense-id chunk
   int64_t ovf_cap;
   // argmax
+  int32_t* bmax;  // per mark-workgroup max count (contiguous, for k_select_final)
   BlkMax* blk;
   int32_t* cand;
   int64_t candcap;
@@ -223,23 +231,24 @@ __device__ inline int32_t block_max(int32_t v, int32_t* scratch) {
   return r;
 }
 
-// exclusive prefix of a[0..n) for element i computed cooperatively: every block
-// thread gets (prefix of a[0..lo)) into LDS sums; n <= BLOCK*32
-__device__ inline int64_t block_sum_before(const int32_t* a, int32_t n, int32_t i, int64_t* s) {
-  // s: BLOCK int64 scratch. returns sum a[0..i)
-  int64_t part = 0;
-  for (int32_t k = threadIdx.x; k < i; k += blockDim.x) part += a[k];
+// block-wide exclusive scan of one int per thread; *total = block sum
+// scratch: BLOCK/64 ints
+__device__ inline int32_t block_excl_scan(int32_t v, int32_t* total, int32_t* scratch) {
+  int32_t wt;
+  const int32_t ex = wave_excl_scan(v, wt);
   __syncthreads();
-  s[threadIdx.x] = part;
+  if (wave_lane() == 0) scratch[threadIdx.x >> 6] = wt;
   __syncthreads();
-  for (int o = BLOCK / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) s[threadIdx.x] += s[threadIdx.x + o];
-    __syncthreads();
+  int32_t base = 0, tot = 0;
+  for (int i = 0; i < (int)(blockDim.x >> 6); i++) {
+    if (i < (int)(threadIdx.x >> 6)) base += scratch[i];
+    tot += scratch[i];
   }
-  const int64_t r = s[0];
-  __syncthreads();
-  return r;
+  *total = tot;
+  return base + ex;
 }
+
+__device__ inline uint16_t key_fp(int32_t d) { return (uint16_t)((uint32_t)d % 65535u); }
 
 // count update target: global counts, or the rank-local delta + touched list
 __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_delta) {
@@ -269,7 +278,7 @@ __device__ inline void agg_init(Agg& s) {
   __syncthreads();
 }
 __device__ inline void agg_add(Agg& s, const Dev& D, int32_t d, int32_t v, bool to_delta) {
-  uint32_t h = ((uint32_t)d * 2654435761u) >> 21;  // 11 bits
+  uint32_t h = ((uint32_t)d * 2654435761u) >> AGG_SHIFT;
 #pragma unroll 1
   for (int probe = 0; probe < 8; probe++) {
     const int32_t k = s.key[h];
@@ -296,15 +305,14 @@ __device__ inline void agg_flush(Agg& s, const Dev& D, bool to_delta) {
   }
 }
 
-// find-or-claim the key-table slot; returns slot, *claimed = 1 if this thread
-// inserted the key
-__device__ inline int32_t ht_insert(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
-  const u64 k = probe_key(h1, h2, len);
-  u64 s = (k * 0xD6E8FEB86659FD93ULL) >> D.ht_shift;
+// key-table probing: the first slot of a key and, given the value already read
+// there, find-or-claim (CAS) its slot; *claimed = true if this thread inserted it
+__device__ inline u64 ht_first_slot(const Dev& D, u64 k) { return (k * 0xD6E8FEB86659FD93ULL) >> D.ht_shift; }
+
+__device__ inline int32_t ht_resolve(const Dev& D, u64 k, u64 s, u64 cur, bool* claimed) {
   const u64 mask = (u64)D.HC - 1;
   *claimed = false;
   for (int64_t probe = 0; probe < D.HC; probe++) {
-    const u64 cur = D.ht_key[s];
     if (cur == k) return (int32_t)s;
     if (cur == 0) {
       const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s], 0ULL, (unsigned long long)k);
@@ -315,20 +323,24 @@ __device__ inline int32_t ht_insert(const Dev& D, u64 h1, u64 h2, int32_t len, b
       if (old == k) return (int32_t)s;
     }
     s = (s + 1) & mask;
+    cur = D.ht_key[s];
   }
   set_error(D, GEOBPE_ECAPACITY, -2);
   return -1;
 }
 
-// per-workgroup output region with an LDS cursor; spills to a global overflow list
-template <class T>
-struct Region {
-  T* base;       // this workgroup's region
-  int64_t cap;
-  int32_t* cnt;  // LDS cursor
-  T* ovf;
-  int64_t* ovf_n;
-  int64_t ovf_cap;
-};
+__device__ inline int32_t ht_insert(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
+  const u64 k = probe_key(h1, h2, len);
+  const u64 s = ht_first_slot(D, k);
+  return ht_resolve(D, k, s, D.ht_key[s], claimed);
+}
+
+// hash of X ++ [g] ++ Y with the powers P^(|Y|syms+1), P^|Y|syms given
+__device__ inline void combine_pw(u64 x1, u64 x2, int32_t g, u64 y1, u64 y2, u64 p1a, u64 p1b, u64 p2a, u64 p2b,
+                                  u64& o1, u64& o2) {
+  const u64 gg = (u64)(g + 1);
+  o1 = addmod61(addmod61(mulmod61(x1, p1a), mulmod61(gg, p1b)), y1);
+  o2 = addmod61(addmod61(mulmod61(x2, p2a), mulmod61(gg, p2b)), y2);
+}
 
 }  // namespace gb

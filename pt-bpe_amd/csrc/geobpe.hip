@@ -3,13 +3,15 @@
 //
 // Replaces the Python/dict hot path of foldingdiff/bpe.py (BPE.initialize /
 // bin / step / quantize).  Integer work only (no
-// MFMA).  One merge iteration is six stream-ordered launches with no host
+// MFMA).  One merge iteration is five stream-ordered launches with no host
 // synchronisation:
 //   k_argmax_blocks -> k_select_final   max count, exact candidate set, reference
 //                                       key-string tie-break, new token (device)
 //   k_mark                              scan pk for the winner, greedy run walks
-//   k_apply                             rewrite tokens, count deltas, new pairs
-//   k_assign -> k_finalize              dense ids for new keys, pk + counts
+//   k_apply                             rewrite tokens, count deltas, new pairs,
+//                                       dense ids for new keys (one reservation
+//                                       per workgroup)
+//   k_finalize                          pk + counts of the new pairs
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -49,7 +51,8 @@ struct geobpe_ctx {
   std::vector<std::vector<int32_t>> vocab;
   int32_t K0 = 0;
   int ncu = 256;
-  int nb = 2048;  // workgroups of the region kernels (= D.NB)
+  int nb = 2048;  // mark / argmax workgroups (= D.NB)
+  int nba = 256;  // apply / finalize / assign / bin / import workgroups (= D.NBA)
   // profiling
   bool prof = false;
   std::string prof_filter;  // ",name,name," or empty = every kernel
@@ -194,7 +197,7 @@ int alloc_keys(geobpe_ctx* c) {
   if (c->keys_ready) return 0;
   Dev& D = c->D;
   const int64_t base = c->distributed && c->global_residues > c->R ? c->global_residues : c->R;
-  D.UC = 3 * base + 65536;
+  D.UC = 3 * base + 65536 + (int64_t)c->nba * ID_CHUNK;  // + the unused chunk tails
   int64_t hc = 1 << 16;
   while (hc < 2 * D.UC) hc <<= 1;
   D.HC = hc;
@@ -204,7 +207,7 @@ int alloc_keys(geobpe_ctx* c) {
   int rc;
   if ((rc = dalloc(c, &D.ht_key, D.HC, 0)) || (rc = dalloc(c, &D.ht_dense, D.HC, 0xFF)) ||
       (rc = dalloc(c, &D.kh1, D.UC)) || (rc = dalloc(c, &D.kh2, D.UC)) || (rc = dalloc(c, &D.klen, D.UC)) ||
-      (rc = dalloc(c, &D.krep, 3 * D.UC)) || (rc = dalloc(c, &D.count, D.UC + 16, 0)) ||
+      (rc = dalloc(c, &D.krep, 3 * D.UC, 0xFF)) || (rc = dalloc(c, &D.count, D.UC + 16, 0)) ||
       (rc = dalloc(c, &D.scratch, D.UC + 16, 0)))
     return rc;
   if (c->distributed) {
@@ -213,7 +216,9 @@ int alloc_keys(geobpe_ctx* c) {
       return rc;
   }
   D.candcap = 1 << 20;
-  if ((rc = dalloc(c, &D.blk, c->nb)) || (rc = dalloc(c, &D.cand, D.candcap))) return rc;
+  if ((rc = dalloc(c, &D.blk, c->nb)) || (rc = dalloc(c, &D.bmax, c->nb + 4, 0)) ||
+      (rc = dalloc(c, &D.cand, D.candcap)))
+    return rc;
   c->keys_ready = true;
   return 0;
 }
@@ -232,12 +237,8 @@ void enqueue_select(geobpe_ctx* c) {
 
 void enqueue_commit(geobpe_ctx* c, bool to_delta, bool merge_iter) {
   {
-    Timed t(c, "assign");
-    hipLaunchKernelGGL(k_assign, dim3(std::max(1, c->nb / 8)), dim3(BLOCK), 0, c->stream, c->D, merge_iter ? 1 : 0);
-  }
-  {
     Timed t(c, "finalize");
-    hipLaunchKernelGGL(k_finalize, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, to_delta ? 1 : 0,
+    hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, to_delta ? 1 : 0,
                        merge_iter ? 1 : 0);
   }
 }
@@ -249,7 +250,7 @@ void enqueue_apply(geobpe_ctx* c) {
   }
   {
     Timed t(c, "apply");
-    hipLaunchKernelGGL(k_apply, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0);
+    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0);
   }
   enqueue_commit(c, c->distributed, true);
 }
@@ -279,8 +280,10 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->ncu = prop.multiProcessorCount;
-  c->nb = c->ncu * 8;
+  c->nba = std::min(c->ncu, BLOCK);
+  c->nb = RPB * c->nba;
   c->D.NB = c->nb;
+  c->D.NBA = c->nba;
   return 0;
 }
 
@@ -320,23 +323,24 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   const int64_t Rp = c->R + 8;  // int4 padding for the pk scan
   if ((rc = dalloc(c, &c->d_row_off, n_rows + 1)) || (rc = dalloc(c, &D.rsym, Rp, 0)) ||
       (rc = dalloc(c, &D.gsym, Rp, 0)) || (rc = dalloc(c, &D.tid, Rp, 0xFF)) || (rc = dalloc(c, &D.tlen, Rp, 0)) ||
-      (rc = dalloc(c, &D.tprev, Rp, 0xFF)) || (rc = dalloc(c, &D.pk, Rp, 0xFF)) || (rc = dalloc(c, &D.role, Rp, 0)))
+      (rc = dalloc(c, &D.tprev, Rp, 0xFF)) || (rc = dalloc(c, &D.pk, Rp, 0xFF)) || (rc = dalloc(c, &D.role, Rp, 0)) ||
+      (rc = dalloc(c, &D.fp, Rp + 16, 0xFF)))
     return rc;
   D.row_off = c->d_row_off;
   HIPCHK(c, hipMemcpyAsync(c->d_row_off, h_row_off, (n_rows + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  // per-workgroup regions: CH int4 groups of pk per mark workgroup; its merges
-  // (<= 2 per int4 group it owns, LC) and their new pairs / keys (<= 2 each, RC)
-  const int64_t n4 = (c->R + 3) / 4;
-  D.CH = std::max<int64_t>(1, (n4 + c->nb - 1) / c->nb);
-  D.LC = 2 * D.CH + 64;
-  D.RC = 4 * D.CH + 256;
+  // per-workgroup regions: a mark workgroup owns CH8 8-slot fingerprint groups
+  // (<= 4 merges per group it owns: LC); an apply workgroup handles RPB mark
+  // regions (<= 2 new pairs / keys per merge: RC)
+  const int64_t n8 = (c->R + 7) / 8;
+  D.CH8 = std::max<int64_t>(1, (n8 + c->nb - 1) / c->nb);
+  D.LC = 4 * D.CH8 + 64;
+  D.RC = 2 * RPB * D.LC + 256;
   D.Lovf_cap = c->R / 2 + 1024;
   D.ovf_cap = c->R + 1024;
   if ((rc = dalloc(c, &D.L, (int64_t)c->nb * D.LC)) || (rc = dalloc(c, &D.Lcnt, c->nb, 0)) ||
-      (rc = dalloc(c, &D.Lovf, D.Lovf_cap)) || (rc = dalloc(c, &D.np, (int64_t)c->nb * D.RC)) ||
-      (rc = dalloc(c, &D.npcnt, c->nb, 0)) || (rc = dalloc(c, &D.npovf, D.ovf_cap)) ||
-      (rc = dalloc(c, &D.ns, (int64_t)c->nb * D.RC)) || (rc = dalloc(c, &D.nscnt, c->nb, 0)) ||
-      (rc = dalloc(c, &D.nsovf, D.ovf_cap)))
+      (rc = dalloc(c, &D.Lovf, D.Lovf_cap)) || (rc = dalloc(c, &D.np, (int64_t)c->nba * D.RC)) ||
+      (rc = dalloc(c, &D.npcnt, c->nba, 0)) || (rc = dalloc(c, &D.npovf, D.ovf_cap)) ||
+      (rc = dalloc(c, &D.ns, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chunk, 2 * (int64_t)c->nba, 0)))
     return rc;
   const int need[6] = {GEOBPE_COL_PHI, GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_TAU, GEOBPE_COL_CAC1N,
                        GEOBPE_COL_C1NCA};
@@ -514,7 +518,7 @@ int geobpe_bin(geobpe_ctx* c) {
   if ((rc = reset_region_counters(c))) return rc;
   {
     Timed t(c, "pair_count");
-    hipLaunchKernelGGL(k_pairs_all, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+    hipLaunchKernelGGL(k_pairs_all, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D);
   }
   HIPCHK(c, hipGetLastError());
   enqueue_commit(c, c->distributed, false);
@@ -634,12 +638,12 @@ int geobpe_delta_export(geobpe_ctx* c, void* d_out, int64_t cap, int64_t* n_reco
 int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
   if (!c || !c->distributed) return GEOBPE_EARG;
   HIPCHK(c, hipSetDevice(c->device));
-  const int64_t chunk = (int64_t)c->nb * (c->D.RC - 256);
+  const int64_t chunk = (int64_t)c->nba * (c->D.RC - 256);
   int rc;
   for (int64_t off = 0; off < n_records; off += chunk) {
     const int64_t n = std::min(chunk, n_records - off);
     if ((rc = reset_region_counters(c))) return rc;
-    hipLaunchKernelGGL(k_import, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (const DeltaRec*)d_in + off, n);
+    hipLaunchKernelGGL(k_import, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, (const DeltaRec*)d_in + off, n);
     HIPCHK(c, hipGetLastError());
     enqueue_commit(c, false, false);
   }
@@ -791,6 +795,8 @@ int64_t geobpe_key_json(geobpe_ctx* c, int32_t d, char* buf, int64_t cap) {
   if (d >= c->h_state->U) return -1;
   int32_t rep[3];
   if (hipMemcpy(rep, c->D.krep + 3 * (int64_t)d, sizeof rep, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  const int32_t K = (int32_t)c->vocab.size();
+  if (rep[0] < 0 || rep[0] >= K || rep[2] < 0 || rep[2] >= K) return -1;  // an unused id of a chunk tail
   std::vector<int32_t> x(c->vocab[rep[0]]);
   x.push_back(rep[1]);
   x.insert(x.end(), c->vocab[rep[2]].begin(), c->vocab[rep[2]].end());
@@ -802,6 +808,39 @@ int64_t geobpe_key_json(geobpe_ctx* c, int32_t d, char* buf, int64_t cap) {
     buf[m] = 0;
   }
   return (int64_t)s.size();
+}
+
+int64_t geobpe_debug_counts(geobpe_ctx* c, int32_t* h_counts, int64_t cap) {
+  if (!c || !c->keys_ready) return -1;
+  if (sync_state(c)) return -1;
+  const int64_t U = c->h_state->U;
+  if (h_counts && cap > 0 &&
+      hipMemcpy(h_counts, c->D.count, sizeof(int32_t) * std::min(U, cap), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return U;
+}
+
+int geobpe_debug_key(geobpe_ctx* c, int32_t d, int64_t* out) {
+  if (!c || !c->keys_ready || d < 0 || !out) return GEOBPE_EARG;
+  int rc;
+  if ((rc = sync_state(c))) return rc;
+  int32_t rep[3], len, cnt, dense = -2;
+  u64 h1;
+  HIPCHK(c, hipMemcpy(rep, c->D.krep + 3 * (int64_t)d, sizeof rep, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(&len, c->D.klen + d, 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(&cnt, c->D.count + d, 4, hipMemcpyDeviceToHost));
+  HIPCHK(c, hipMemcpy(&h1, c->D.kh1 + d, 8, hipMemcpyDeviceToHost));
+  out[0] = rep[0];
+  out[1] = rep[1];
+  out[2] = rep[2];
+  out[3] = len;
+  out[4] = cnt;
+  out[5] = c->h_state->U;
+  out[6] = c->h_state->K;
+  out[7] = (int64_t)c->vocab.size();
+  out[8] = (int64_t)h1;
+  (void)dense;
+  return 0;
 }
 
 int geobpe_set_profiling(geobpe_ctx* c, int on) {

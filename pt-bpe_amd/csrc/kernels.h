@@ -126,6 +126,7 @@ __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_
       D.tlen[g] = 1;
       D.tprev[g] = (g == a) ? -1 : (int32_t)(g - 1);
       D.pk[g] = -1;
+      D.fp[g] = 0xFFFF;
       D.role[g] = 0;
     }
   }
@@ -154,6 +155,25 @@ __device__ inline void emit_pair(const Dev& D, int32_t* s_cnt, int32_t target, i
   }
 }
 
+__device__ inline void assign_one(const Dev& D, const NewSlot& e, int64_t d) {
+  if (d >= D.UC) {
+    set_error(D, GEOBPE_ECAPACITY, -5);
+    return;
+  }
+  D.ht_dense[e.slot] = (int32_t)d;
+  D.kh1[d] = e.h1;
+  D.kh2[d] = e.h2;
+  D.klen[d] = e.len;
+  D.krep[3 * d + 0] = e.idL;
+  D.krep[3 * d + 1] = e.g;
+  D.krep[3 * d + 2] = e.idR;
+  D.count[d] = 0;
+  if (D.dcount) {
+    D.dcount[d] = 0;
+    D.touch[d] = -1;
+  }
+}
+
 __device__ inline void emit_slot(const Dev& D, int32_t* s_cnt, int32_t slot, int32_t len, int32_t idL, int32_t g,
                                  int32_t idR, u64 h1, u64 h2) {
   NewSlot e;
@@ -168,12 +188,9 @@ __device__ inline void emit_slot(const Dev& D, int32_t* s_cnt, int32_t slot, int
   const int32_t j = atomicAdd(s_cnt, 1);
   if (j < D.RC) {
     D.ns[(int64_t)blockIdx.x * D.RC + j] = e;
-  } else {
-    const int64_t k = atomicAdd((unsigned long long*)&D.st->ns_ovf, 1ULL);
-    if (k < D.ovf_cap)
-      D.nsovf[k] = e;
-    else
-      set_error(D, GEOBPE_ECAPACITY, -4);
+  } else {  // rare: a dense id of its own right away
+    const int64_t d = (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL);
+    assign_one(D, e, d);
   }
 }
 
@@ -187,12 +204,36 @@ __device__ inline void add_pair(const Dev& D, int32_t* s_np, int32_t* s_ns, int3
   emit_pair(D, s_np, target, slot, len, delta, h1, h2);
 }
 
+// end of a region kernel: publish the pair count and give this workgroup's
+// claimed keys dense ids from its reserved chunk (a global reservation only when
+// the chunk runs out; the unused tail of a chunk stays count 0)
 __device__ inline void close_regions(const Dev& D, int32_t* s_np, int32_t* s_ns) {
+  __shared__ int64_t s_cur, s_n1, s_base2;
   __syncthreads();
+  const int32_t nsz = min(*s_ns, (int32_t)D.RC);
   if (threadIdx.x == 0) {
     D.npcnt[blockIdx.x] = min(*s_np, (int32_t)D.RC);
-    D.nscnt[blockIdx.x] = min(*s_ns, (int32_t)D.RC);
+    int64_t cur = D.chunk[2 * blockIdx.x], end = D.chunk[2 * blockIdx.x + 1];
+    s_cur = cur;
+    s_n1 = nsz;
+    if (nsz > end - cur) {  // old chunk's tail first, then a fresh chunk
+      const int64_t rest = nsz - (end - cur);
+      const int64_t sz = max(rest, (int64_t)ID_CHUNK);
+      const int64_t b2 = (int64_t)atomicAdd((unsigned long long*)&D.st->U, (unsigned long long)sz);
+      s_n1 = end - cur;
+      s_base2 = b2;
+      cur = b2 + rest;
+      end = b2 + sz;
+    } else {
+      cur += nsz;
+    }
+    D.chunk[2 * blockIdx.x] = cur;
+    D.chunk[2 * blockIdx.x + 1] = end;
   }
+  __syncthreads();
+  const NewSlot* reg = D.ns + (int64_t)blockIdx.x * D.RC;
+  for (int32_t i = threadIdx.x; i < nsz; i += blockDim.x)
+    assign_one(D, reg[i], i < s_n1 ? s_cur + i : s_base2 + (i - s_n1));
 }
 
 // ====================================================================== histogram
@@ -201,7 +242,7 @@ __global__ __launch_bounds__(BLOCK) void k_pairs_all(Dev D) {
   __shared__ int32_t s_np, s_ns;
   if (threadIdx.x == 0) s_np = s_ns = 0;
   __syncthreads();
-  const int64_t SC = (D.R + D.NB - 1) / D.NB;
+  const int64_t SC = (D.R + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * SC, hi = min(D.R, lo + SC);
   for (int64_t g = lo + threadIdx.x; g < hi; g += blockDim.x) {
     const int32_t L = D.tid[g];
@@ -218,68 +259,7 @@ __global__ __launch_bounds__(BLOCK) void k_pairs_all(Dev D) {
   close_regions(D, &s_np, &s_ns);
 }
 
-// dense ids for the keys claimed since the last commit: region r's claims get
-// U + (claims of regions < r) + i; overflow claims follow all regions
-__global__ __launch_bounds__(BLOCK) void k_assign(Dev D, int merge_iter) {
-  __shared__ int64_t s_sum[BLOCK];
-  if (merge_iter && D.st->done) return;
-  const int64_t U = D.st->U;
-  const int32_t per = (D.NB + gridDim.x - 1) / gridDim.x;
-  const int32_t r0 = min((int32_t)blockIdx.x * per, D.NB), r1 = min(r0 + per, D.NB);
-  int64_t base = block_sum_before(D.nscnt, D.NB, r0, s_sum);
-  const int64_t total = block_sum_before(D.nscnt, D.NB, D.NB, s_sum);
-  const int64_t novf = min(D.st->ns_ovf, D.ovf_cap);
-  if (blockIdx.x == 0 && threadIdx.x == 0) D.st->nnew_total = total + novf;
-  if (merge_iter && blockIdx.x == 0) {  // merges applied this iteration -> merge log
-    const int64_t nm = block_sum_before(D.Lcnt, D.NB, D.NB, s_sum) + min(D.st->L_ovf, D.Lovf_cap);
-    if (threadIdx.x == 0) D.log[D.st->iter - 1].nmerged = nm;
-  }
-  for (int32_t r = r0; r < r1; r++) {
-    const int32_t n = D.nscnt[r];
-    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
-      const NewSlot e = D.ns[(int64_t)r * D.RC + i];
-      const int64_t d = U + base + i;
-      if (d >= D.UC) {
-        set_error(D, GEOBPE_ECAPACITY, -5);
-        continue;
-      }
-      D.ht_dense[e.slot] = (int32_t)d;
-      D.kh1[d] = e.h1;
-      D.kh2[d] = e.h2;
-      D.klen[d] = e.len;
-      D.krep[3 * d + 0] = e.idL;
-      D.krep[3 * d + 1] = e.g;
-      D.krep[3 * d + 2] = e.idR;
-      D.count[d] = 0;
-      if (D.dcount) {
-        D.dcount[d] = 0;
-        D.touch[d] = -1;
-      }
-    }
-    base += n;
-  }
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x) {
-    const NewSlot e = D.nsovf[k];
-    const int64_t d = U + total + k;
-    if (d >= D.UC) {
-      set_error(D, GEOBPE_ECAPACITY, -6);
-      continue;
-    }
-    D.ht_dense[e.slot] = (int32_t)d;
-    D.kh1[d] = e.h1;
-    D.kh2[d] = e.h2;
-    D.klen[d] = e.len;
-    D.krep[3 * d + 0] = e.idL;
-    D.krep[3 * d + 1] = e.g;
-    D.krep[3 * d + 2] = e.idR;
-    D.count[d] = 0;
-    if (D.dcount) {
-      D.dcount[d] = 0;
-      D.touch[d] = -1;
-    }
-  }
-}
-
+// dense id of a key claimed in this launch (key arrays + table slot -> id)
 // pair -> dense key id into pk, counts via LDS-staged partial counts
 __device__ inline void finalize_one(const Dev& D, Agg& agg, const NewPair& e, int64_t j, bool to_delta) {
   const int32_t d = D.ht_dense[e.slot];
@@ -287,7 +267,10 @@ __device__ inline void finalize_one(const Dev& D, Agg& agg, const NewPair& e, in
     set_error(D, GEOBPE_EHASH, j);
     return;
   }
-  if (e.target >= 0) D.pk[e.target] = d;
+  if (e.target >= 0) {
+    D.pk[e.target] = d;
+    D.fp[e.target] = key_fp(d);
+  }
   agg_add(agg, D, d, e.delta, to_delta);
 }
 
@@ -295,7 +278,18 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(Dev D, int to_delta, int mer
   __shared__ Agg agg;
   if (merge_iter && D.st->done) return;
   agg_init(agg);
-  if (blockIdx.x == 0 && threadIdx.x == 0) D.st->U += D.st->nnew_total;
+  if (merge_iter && blockIdx.x == 0) {  // merges applied this iteration -> merge log
+    __shared__ int32_t s_red[BLOCK / 64];
+    int32_t nm = 0;
+    const int4* l4 = reinterpret_cast<const int4*>(D.Lcnt);  // NB % 4 == 0
+    for (int32_t i = threadIdx.x; i < D.NB / 4; i += blockDim.x) {
+      const int4 v = l4[i];
+      nm += v.x + v.y + v.z + v.w;
+    }
+    int32_t tot;
+    block_excl_scan(nm, &tot, s_red);
+    if (threadIdx.x == 0) D.log[D.st->iter - 1].nmerged = (int64_t)tot + min(D.st->L_ovf, D.Lovf_cap);
+  }
   const int32_t n = D.npcnt[blockIdx.x];
   const NewPair* reg = D.np + (int64_t)blockIdx.x * D.RC;
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) finalize_one(D, agg, reg[i], i, to_delta != 0);
@@ -471,6 +465,7 @@ __global__ __launch_bounds__(BLOCK) void k_argmax_blocks(Dev D) {
     r.n = s_n;
     for (int q = 0; q < BLK_CANDS; q++) r.c[q] = q < s_n ? s_c[q] : -1;
     D.blk[blockIdx.x] = r;
+    D.bmax[blockIdx.x] = m;
   }
 }
 
@@ -484,7 +479,11 @@ __global__ __launch_bounds__(BLOCK) void k_select_final(Dev D, int32_t nblk) {
   __shared__ int32_t s_best[BLOCK];
   if (D.st->done) return;
   int32_t m = 0;
-  for (int32_t i = threadIdx.x; i < nblk; i += blockDim.x) m = max(m, D.blk[i].max);
+  const int4* b4 = reinterpret_cast<const int4*>(D.bmax);  // nblk % 4 == 0
+  for (int32_t i = threadIdx.x; i < nblk / 4; i += blockDim.x) {
+    const int4 v = b4[i];
+    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+  }
   m = block_max(m, s_red);
   if (m <= 0) {
     if (threadIdx.x == 0) {
@@ -500,8 +499,8 @@ __global__ __launch_bounds__(BLOCK) void k_select_final(Dev D, int32_t nblk) {
   __syncthreads();
   // candidates: listed ones, or a rescan of workgroups that had more than BLK_CANDS
   for (int32_t i = threadIdx.x; i < nblk; i += blockDim.x) {
+    if (D.bmax[i] != m) continue;
     const BlkMax& b = D.blk[i];
-    if (b.max != m) continue;
     if (b.n <= BLK_CANDS) {
       for (int q = 0; q < b.n; q++) {
         const int32_t j = atomicAdd(&s_nc, 1);
@@ -593,7 +592,18 @@ __global__ __launch_bounds__(BLOCK) void k_select_final(Dev D, int32_t nblk) {
     st->nid = nid;
     st->maxc = m;
     st->ncand = nc;
-    st->L_ovf = st->np_ovf = st->ns_ovf = st->nnew_total = 0;
+    st->L_ovf = st->np_ovf = st->ns_ovf = st->nL_total = 0;
+    const u64 w1 = D.kh1[W], w2 = D.kh2[W];
+    const int32_t wl = D.klen[W];
+    const int64_t ny = 2 * (int64_t)wl - 1;
+    st->w1 = w1;
+    st->w2 = w2;
+    st->wl = wl;
+    st->wfp = key_fp(W);
+    st->pwW1a = D.pw1[ny + 1];
+    st->pwW1b = D.pw1[ny];
+    st->pwW2a = D.pw2[ny + 1];
+    st->pwW2b = D.pw2[ny];
   }
 }
 
@@ -631,33 +641,39 @@ __device__ inline void walk_run(const Dev& D, int32_t h, int32_t W, int32_t tag,
   }
 }
 
-// scan pk for the winner key (4 x int4 per lane in flight), start a walk at every
-// run start; each workgroup owns CH int4 groups and one output region
+// scan the 16-bit key fingerprints for the winner (4 x 16 B per lane in flight),
+// confirm on pk, start a walk at every run start; each workgroup owns CH8
+// 8-slot groups and one merge region
 __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
   __shared__ int32_t s_n;
   if (D.st->done) return;
   const int32_t W = D.st->W, tag = D.st->tag;
+  const uint32_t fW = (uint32_t)D.st->wfp;
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
-  const int64_t n4 = (D.R + 3) / 4;
-  const int64_t lo = (int64_t)blockIdx.x * D.CH, hi = min(n4, lo + D.CH);
-  const int4* pk4 = reinterpret_cast<const int4*>(D.pk);
-  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += 4 * BLOCK) {
-    int4 v[4];
+  const int64_t n8 = (D.R + 7) / 8;
+  const int64_t lo = (int64_t)blockIdx.x * D.CH8, hi = min(n8, lo + D.CH8);
+  const uint4* f4 = reinterpret_cast<const uint4*>(D.fp);
+  constexpr int UNR = 8;
+  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += UNR * BLOCK) {
+    uint4 v[UNR];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
+    for (int u = 0; u < UNR; u++) {
       const int64_t i = i0 + u * BLOCK;
-      v[u] = i < hi ? pk4[i] : make_int4(-1, -1, -1, -1);
+      v[u] = i < hi ? f4[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     }
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      const int32_t vv[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+    for (int u = 0; u < UNR; u++) {
+      const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        if (vv[q] == W) {
-          const int32_t g = (int32_t)(4 * (i0 + u * BLOCK) + q);
-          const int32_t p = D.tprev[g];
-          if (p < 0 || D.pk[p] != W) walk_run(D, g, W, tag, &s_n);
+      for (int q = 0; q < 8; q++) {
+        const uint32_t f = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
+        if (f == fW) {
+          const int32_t g = (int32_t)(8 * (i0 + u * BLOCK) + q);
+          if (D.pk[g] == W) {
+            const int32_t p = D.tprev[g];
+            if (p < 0 || D.pk[p] != W) walk_run(D, g, W, tag, &s_n);
+          }
         }
       }
     }
@@ -666,59 +682,144 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
   if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = min(s_n, (int32_t)D.LC);
 }
 
-// rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014)
-__device__ inline void apply_one(const Dev& D, Agg& agg, int32_t* s_np, int32_t* s_ns, const LEntry& e, int32_t W,
-                                 int32_t nid, u64 w1, u64 w2, int32_t wl, int32_t tagL, int32_t tagR, bool to_delta) {
+// rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014).
+// Latency-bound: every independent load is issued before any store.
+struct ApplyCtx {
+  int32_t W, nid, wl, tagL, tagR;
+  u64 w1, w2;
+  u64 pwL1a, pwL1b, pwL2a, pwL2b;  // powers for "X ++ g ++ W" (W on the right)
+  bool to_delta;
+};
+
+__device__ inline void apply_one(const Dev& D, Agg& agg, int32_t* s_np, int32_t* s_ns, const LEntry e,
+                                 const ApplyCtx& A) {
+  const bool hasP = e.p >= 0, hasC = e.c >= 0;
+  // round 1: everything that depends only on the entry
   const int32_t pkb = D.pk[e.b];
-  agg_add(agg, D, W, -1, to_delta);                        // step 1: the merged pair
-  if (pkb >= 0) agg_add(agg, D, pkb, -1, to_delta);        // step 4: right neighbour pair
-  const bool pN = e.p >= 0 && D.role[e.p] != tagR;
-  if (pN) agg_add(agg, D, D.pk[e.p], -1, to_delta);        // step 3: left neighbour pair
-  D.tid[e.a] = nid;                                        // step 2: bond_to_token / token_pos
-  D.tlen[e.a] = wl;
+  const int32_t rp = hasP ? D.role[e.p] : 0;
+  const int32_t pkp = hasP ? D.pk[e.p] : -1;
+  const int32_t L = hasP ? D.tid[e.p] : 0;
+  const int32_t glL = hasP ? D.gsym[e.a - 1] : 0;
+  const int32_t rc = hasC ? D.role[e.c] : 0;
+  const int32_t tc = hasC ? D.tid[e.c] : 0;
+  const int32_t glR = hasC ? D.gsym[e.a + A.wl - 1] : 0;
+  const bool pN = hasP && rp != A.tagR;  // p is never a left part; R or untouched
+  const bool cL = hasC && rc == A.tagL;
+  const int32_t idr = cL ? A.nid : tc;
+  // round 2: vocab hashes of the neighbours
+  u64 l1 = 0, l2 = 0, r1 = A.w1, r2 = A.w2;
+  int32_t ll = 0, rl = A.wl;
+  if (pN) {
+    l1 = D.vh1[L];
+    l2 = D.vh2[L];
+    ll = D.vlen[L];
+  }
+  if (hasC && !cL) {
+    r1 = D.vh1[idr];
+    r2 = D.vh2[idr];
+    rl = D.vlen[idr];
+  }
+  u64 pr1a = 0, pr1b = 0, pr2a = 0, pr2b = 0;
+  if (hasC) {
+    const int64_t ny = 2 * (int64_t)rl - 1;
+    pr1a = D.pw1[ny + 1];
+    pr1b = D.pw1[ny];
+    pr2a = D.pw2[ny + 1];
+    pr2b = D.pw2[ny];
+  }
+  // new pair keys and their first table probes (issued together)
+  u64 hL1 = 0, hL2 = 0, hR1 = 0, hR2 = 0, kL = 0, kR = 0, sL = 0, sR = 0, cLv = 0, cRv = 0;
+  if (pN) {
+    combine_pw(l1, l2, glL, A.w1, A.w2, A.pwL1a, A.pwL1b, A.pwL2a, A.pwL2b, hL1, hL2);
+    kL = probe_key(hL1, hL2, ll + A.wl);
+    sL = ht_first_slot(D, kL);
+    cLv = D.ht_key[sL];
+  }
+  if (hasC) {
+    combine_pw(A.w1, A.w2, glR, r1, r2, pr1a, pr1b, pr2a, pr2b, hR1, hR2);
+    kR = probe_key(hR1, hR2, A.wl + rl);
+    sR = ht_first_slot(D, kR);
+    cRv = D.ht_key[sR];
+  }
+  // count deltas: step 4 (right neighbour pair) and step 3 (left neighbour pair);
+  // step 1 (the merged pair, -1 on W) is counted once per workgroup by the caller
+  if (pkb >= 0) agg_add(agg, D, pkb, -1, A.to_delta);
+  if (pN) agg_add(agg, D, pkp, -1, A.to_delta);
+  // step 2: bond_to_token / token_pos
+  D.tid[e.a] = A.nid;
+  D.tlen[e.a] = A.wl;
   D.tid[e.b] = -1;
   D.pk[e.b] = -1;
-  if (e.c >= 0) D.tprev[e.c] = e.a;
-  if (pN) {                                                // step 5: new left pair
-    const int32_t L = D.tid[e.p];
-    const int32_t gl = D.gsym[e.a - 1];
-    u64 h1, h2;
-    combine(D, D.vh1[L], D.vh2[L], gl, w1, w2, wl, h1, h2);
-    add_pair(D, s_np, s_ns, e.p, h1, h2, D.vlen[L] + wl, L, gl, nid, 1);
+  D.fp[e.b] = 0xFFFF;
+  if (hasC) D.tprev[e.c] = e.a;
+  // step 5: the new neighbour pairs
+  if (pN) {
+    bool claimed;
+    const int32_t slot = ht_resolve(D, kL, sL, cLv, &claimed);
+    if (slot >= 0) {
+      if (claimed) emit_slot(D, s_ns, slot, ll + A.wl, L, glL, A.nid, hL1, hL2);
+      emit_pair(D, s_np, e.p, slot, ll + A.wl, 1, hL1, hL2);
+    }
   }
-  if (e.c >= 0) {                                          // step 5: new right pair
-    const bool cL = D.role[e.c] == tagL;
-    const int32_t idr = cL ? nid : D.tid[e.c];
-    const u64 r1 = cL ? w1 : D.vh1[idr], r2 = cL ? w2 : D.vh2[idr];
-    const int32_t rl = cL ? wl : D.vlen[idr];
-    const int32_t gl = D.gsym[e.a + wl - 1];
-    u64 h1, h2;
-    combine(D, w1, w2, gl, r1, r2, rl, h1, h2);
-    add_pair(D, s_np, s_ns, e.a, h1, h2, wl + rl, nid, gl, idr, 1);
+  if (hasC) {
+    bool claimed;
+    const int32_t slot = ht_resolve(D, kR, sR, cRv, &claimed);
+    if (slot >= 0) {
+      if (claimed) emit_slot(D, s_ns, slot, A.wl + rl, A.nid, glR, idr, hR1, hR2);
+      emit_pair(D, s_np, e.a, slot, A.wl + rl, 1, hR1, hR2);
+    }
   } else {
     D.pk[e.a] = -1;
+    D.fp[e.a] = 0xFFFF;
   }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
   __shared__ Agg agg;
   __shared__ int32_t s_np, s_ns;
+  __shared__ int32_t s_off[RPB + 1];
   if (D.st->done) return;
   agg_init(agg);
-  if (threadIdx.x == 0) s_np = s_ns = 0;
+  const State* st = D.st;
+  ApplyCtx A;
+  A.W = st->W;
+  A.nid = st->nid;
+  const int32_t tag = st->tag;
+  A.tagR = (tag << 2) | 2;
+  A.tagL = (tag << 2) | 1;
+  A.to_delta = to_delta != 0;
+  A.w1 = st->w1;
+  A.w2 = st->w2;
+  A.wl = st->wl;
+  A.pwL1a = st->pwW1a;
+  A.pwL1b = st->pwW1b;
+  A.pwL2a = st->pwW2a;
+  A.pwL2b = st->pwW2b;
+  if (threadIdx.x < 64) {  // this workgroup's RPB mark regions: offsets by a wave scan
+    const int32_t c = threadIdx.x < RPB ? D.Lcnt[blockIdx.x * RPB + threadIdx.x] : 0;
+    int32_t tot;
+    const int32_t ex = wave_excl_scan(c, tot);
+    if (threadIdx.x < RPB) s_off[threadIdx.x] = ex;
+    if (threadIdx.x == 0) {
+      s_off[RPB] = tot;
+      s_np = s_ns = 0;
+    }
+  }
   __syncthreads();
-  const int32_t W = D.st->W, nid = D.st->nid, tag = D.st->tag;
-  const u64 w1 = D.kh1[W], w2 = D.kh2[W];
-  const int32_t wl = D.klen[W];
-  const int32_t tagR = (tag << 2) | 2, tagL = (tag << 2) | 1;
-  const int32_t n = D.Lcnt[blockIdx.x];
-  const LEntry* reg = D.L + (int64_t)blockIdx.x * D.LC;
-  for (int32_t i = threadIdx.x; i < n; i += blockDim.x)
-    apply_one(D, agg, &s_np, &s_ns, reg[i], W, nid, w1, w2, wl, tagL, tagR, to_delta != 0);
-  const int64_t novf = min(D.st->L_ovf, D.Lovf_cap);
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x)
-    apply_one(D, agg, &s_np, &s_ns, D.Lovf[k], W, nid, w1, w2, wl, tagL, tagR, to_delta != 0);
-  agg_flush(agg, D, to_delta != 0);
+  const int32_t E = s_off[RPB];
+  for (int32_t j = threadIdx.x; j < E; j += blockDim.x) {
+    int r = 0;
+    while (j >= s_off[r + 1]) r++;
+    const LEntry e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + (j - s_off[r])];
+    apply_one(D, agg, &s_np, &s_ns, e, A);
+  }
+  const int64_t novf = min(st->L_ovf, D.Lovf_cap);
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x) {
+    apply_one(D, agg, &s_np, &s_ns, D.Lovf[k], A);
+    agg_add(agg, D, A.W, -1, A.to_delta);  // step 1 for an overflow entry
+  }
+  agg_flush(agg, D, A.to_delta);
+  if (threadIdx.x == 0 && E) global_add(D, A.W, -E, A.to_delta);  // step 1 for the region entries
   close_regions(D, &s_np, &s_ns);
 }
 
@@ -804,7 +905,7 @@ __global__ __launch_bounds__(BLOCK) void k_recount(Dev D) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = D.pk[g];
     if (d < 0) continue;
-    uint32_t h = ((uint32_t)d * 2654435761u) >> 21;
+    uint32_t h = ((uint32_t)d * 2654435761u) >> AGG_SHIFT;
     bool done = false;
     for (int probe = 0; probe < 8 && !done; probe++) {
       const int32_t k = agg.key[h];

@@ -117,6 +117,10 @@ class TorchGroup:
         parts = [out[r, : counts[r] * REC] for r in range(self.world_size)]
         flat = T.cat(parts).to(self.dev)
         self._keep = flat
+        # the engine runs on its own HIP stream: the records must be complete on
+        # torch's stream before the import kernels read them
+        if self.dev.type == "cuda":
+            T.cuda.current_stream(self.dev).synchronize()
         return ctypes.c_void_p(flat.data_ptr()), int(sum(counts))
 
 
@@ -203,6 +207,7 @@ class VirtualCluster:
             parts.append(buf[: n.value * REC])
         flat = T.cat(parts)
         total = flat.numel() // REC
+        T.cuda.current_stream(self.dev).synchronize()  # engines run on their own streams
         for e in self.engines:
             e._chk(L.geobpe_delta_import(e._ctx, ctypes.c_void_p(flat.data_ptr()), total))
 

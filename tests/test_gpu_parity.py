@@ -58,6 +58,9 @@ def test_sharded_matches_reference_golden(name, world):
     vc = VirtualCluster(corpus, meta["bins"]["1"], world=world).initialize()
     assert vc.thresholds == {k: [tuple(p) for p in v] for k, v in meta["thresholds"].items()}
     vc.bin()
+    ref = vc.engines[0].key_counts()  # replicated global counts agree on every rank
+    for e in vc.engines[1:]:
+        assert e.key_counts() == ref
     for _ in range(len(meta["merges"])):
         assert vc.step() is not None
     _check_against_golden(vc, meta, arrs)
@@ -175,16 +178,16 @@ def test_device_key_order_matches_python_strings(name):
     eng = _engine(corpus, meta["bins"]["1"])
     eng.bin()
     eng.run(30)
-    U = eng.num_keys
+    ids = eng.live_key_ids()
     rng = np.random.default_rng(0)
-    pairs = rng.integers(0, U, size=(3000, 2)).astype(np.int32)
+    pairs = ids[rng.integers(0, len(ids), size=(3000, 2))].astype(np.int32)
     # near-ties: keys sharing long prefixes are the interesting comparisons
-    keys = [eng.key_json(d) for d in range(U)]
-    order = np.argsort(np.array(keys, dtype=object), kind="stable")
-    adj = np.stack([order[:-1], order[1:]], axis=1)[: 3000].astype(np.int32)
+    keys = {int(d): eng.key_json(int(d)) for d in ids}
+    order = sorted(keys, key=lambda d: keys[d])
+    adj = np.array(list(zip(order[:-1], order[1:]))[:3000], dtype=np.int32)
     pairs = np.concatenate([pairs, adj, adj[:, ::-1]])
     got = eng.debug_key_less(pairs)
-    exp = np.array([keys[a] < keys[b] for a, b in pairs])
+    exp = np.array([keys[int(a)] < keys[int(b)] for a, b in pairs])
     assert np.array_equal(got, exp)
     eng.close()
 

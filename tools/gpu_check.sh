@@ -3,4 +3,4 @@ cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && echo SMOKE_OK && \
 timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1 && echo PYTEST_OK && \
-timeout -k 10 600 python bench.py --steps 990 --warmup 10 > gpurun_out/bench.log 2>&1 && echo BENCH_OK
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 && echo BENCH_OK

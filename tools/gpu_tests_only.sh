@@ -1,0 +1,3 @@
+cd $GRAFT_REPO_ROOT
+mkdir -p gpurun_out
+timeout -k 10 900 python -m pytest tests -q -m gpu "$@" > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?"
