@@ -76,14 +76,15 @@ def _ptr(a: np.ndarray):
 class OracleBPE:
     """Scoped-mode GeoBPE on the CPU: ``initialize()``, ``bin()``, ``step()``."""
 
-    def __init__(self, corpus: dict, bins: int):
+    def __init__(self, corpus: dict, bins: int, cover: bool = False):
         self.corpus = corpus
+        self.cover = cover
         self.B = int(bins)
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
         self._h = None
 
     def initialize(self):
-        self.thresholds = prologue.thresholds(self.corpus, self.B)
+        self.thresholds = prologue.thresholds(self.corpus, self.B, self.cover)
         self.rsym, self.gsym = prologue.symbols(self.corpus, self.thresholds, self.B)
         self.labels, self.sym_of_label = prologue.init_labels(self.rsym)
         self.K0 = len(self.sym_of_label)

@@ -39,7 +39,8 @@ def init_bond_angle() -> float:
     return float(np.arccos(np.clip(np.dot(u1, u2), -1.0, 1.0)))
 
 
-def thresholds(corpus: dict, B: int) -> dict:
+def thresholds(corpus: dict, B: int, cover: bool = False) -> dict:
+    """``cover``: bin_strategy "histogram-cover" -> range=(0, 2pi) (plotting.py:319)."""
     n_rows = len(corpus["row_off"]) - 1
     init = init_bond_angle()
     out = {}
@@ -49,7 +50,7 @@ def thresholds(corpus: dict, B: int) -> dict:
         if key == "tau":
             vals = np.concatenate([vals, np.full(n_rows, init)])
         a = (vals + 2 * np.pi) % (2 * np.pi)
-        _, edges = np.histogram(a, bins=B)
+        _, edges = np.histogram(a, bins=B, range=(0, 2 * np.pi) if cover else None)
         out[key] = [(float(s), float(e)) for s, e in zip(edges[:-1], edges[1:])]
     return out
 

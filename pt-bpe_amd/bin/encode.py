@@ -1,0 +1,199 @@
+#!/usr/bin/env python
+"""GeoBPE training driver on MI355X -- the caller side of the hot path,
+mirroring the reference's ``bin/encode.py`` (flags :106-167, loop :371-427).
+
+Differences (all outside SURVEY.md §8's hot path):
+  * ``--data-dir`` takes an internal-coordinate corpus (``.npz`` in the
+    geobpe.synth layout) or ``synthetic:N:LO:HI:SEED``; PDB featurisation is
+    §8(f) row 2.
+  * stats JSON carries K, L, bpr and the codebook utility (encode.py:408-420);
+    bb_rmsd / lddt need the coordinate stack (esm ProteinChain) and are omitted.
+  * checkpoints are ``bpe_iter={t}.json`` (merge list + counts + args); resume
+    replays the merges on the device and checks them against the file.  The
+    reference-compatible ``bpe_iter=*.pkl`` writer is §8(f) row 1.
+  * ``--run-chunk M`` (ours): merges issued per device call between host
+    syncs; the reference steps one at a time.  Outputs do not depend on it.
+
+Out-of-scope flag values (res-init false, free bonds, p-min-size < inf,
+glue-opt, uniform bins, multi-grid --bins) raise NotImplementedError from
+geobpe.bpe.BPE before any work starts.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import logging
+import os
+import re
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def str2bool(v):
+    if isinstance(v, bool):
+        return v
+    if v.lower() in ("yes", "true", "t", "y", "1"):
+        return True
+    if v.lower() in ("no", "false", "f", "n", "0"):
+        return False
+    raise argparse.ArgumentTypeError("Boolean value expected.")
+
+
+def str2dict(v):
+    if not re.match(r"\d+-\d+(?::\d+-\d+)*$", v):
+        raise argparse.ArgumentTypeError("Wrong format, see help.")
+    return {int(a): int(b) for a, b in re.findall(r"(\d+)-(\d+)", v)}
+
+
+def int_or_inf(x):
+    if x.lower() in ("inf", "infinity"):
+        return float("inf")
+    try:
+        return int(x)
+    except ValueError:
+        raise argparse.ArgumentTypeError(f"'{x}' is not an integer or 'inf'")
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(description="GeoBPE (MI355X) BPE script")
+    p.add_argument("--auto", action="store_true")
+    p.add_argument("--base-dir", type=str, default="./")
+    p.add_argument("--save-dir", type=str)
+    p.add_argument("--log-dir", type=str, default="logs")
+    p.add_argument("--data-dir", type=str, default="synthetic:1000:40:300:0",
+                   help="corpus .npz (geobpe.synth layout) or synthetic:N:LO:HI:SEED")
+    p.add_argument("--toy", type=int, default=0, help="number of chains; 0 for all")
+    p.add_argument("--res-init", type=str2bool, default=True)
+    p.add_argument("--free-bonds", type=str2bool, default=False)
+    p.add_argument("--bin-strategy", default="histogram", choices=["histogram", "histogram-cover", "uniform"])
+    p.add_argument("--bins", type=str2dict, default="1-10")
+    p.add_argument("--p-min-size", type=int_or_inf, default=float("inf"))
+    p.add_argument("--max-iter", type=int, default=10000)
+    p.add_argument("--glue-opt", type=str2bool, default=False)
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--save-every", type=int, default=10)
+    p.add_argument("--run-chunk", type=int, default=0, help="merges per device call (0: = save-every)")
+    p.add_argument("--device", type=int, default=0)
+    return p.parse_args(argv)
+
+
+def load_corpus(spec: str, toy: int = 0) -> dict:
+    from geobpe import synth
+    if spec.startswith("synthetic:"):
+        n, lo, hi, seed = (int(x) for x in spec.split(":")[1:5])
+        corpus = synth.make_corpus(synth.make_lengths(n, lo, hi, seed=seed), seed=seed)
+    else:
+        corpus = synth.load_corpus(spec)
+    if toy:
+        from geobpe.dist import slice_corpus
+        corpus = slice_corpus(corpus, 0, min(toy, len(corpus["row_off"]) - 1))
+    return corpus
+
+
+def stats(bpe) -> dict:
+    from geobpe.bpe import get_codebook_utility
+    ids, off = bpe.encode_all()
+    ntok = (np.diff(off) + 3) // 4
+    N = len(ntok)
+    L = float(np.mean(ntok)) if N else 0.0
+    K = len(bpe._tokens)
+    return {"K": K, "L": L, "bpr": bpe.capacity(tokenizer=True) / (N * L) if N else 0.0} | \
+        get_codebook_utility(ids, bpe.vocab_size)
+
+
+def latest_checkpoint(save_dir: str):
+    best, path = -1, None
+    for f in glob.glob(os.path.join(save_dir, "bpe_iter=*.json")):
+        m = re.match(r"bpe_iter=(\d+)\.json$", os.path.basename(f))
+        if not m:
+            continue
+        try:
+            with open(f) as fh:
+                json.load(fh)
+        except (OSError, ValueError):
+            continue  # incomplete write (encode.py:183-200 skips incomplete pickles)
+        if int(m.group(1)) > best:
+            best, path = int(m.group(1)), f
+    return best, path
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    if not args.save_dir:
+        if not args.auto:
+            raise SystemExit("--save-dir or --auto is required")
+        args.save_dir = os.path.join(args.base_dir, "ckpts", str(time.time()))
+    os.makedirs(args.save_dir, exist_ok=True)
+    args_path = os.path.join(args.save_dir, "args.txt")
+    skip = {"auto", "save_dir", "max_iter", "run_chunk", "device"}
+    if os.path.exists(args_path):  # validate_args_match (utils.py)
+        with open(args_path) as f:
+            loaded = dict(line.rstrip("\n").split(": ", 1) for line in f if ": " in line)
+        for k, v in sorted(vars(args).items()):
+            if k not in skip and k in loaded and loaded[k] != str(v):
+                raise SystemExit(f"argument mismatch for {k}: saved {loaded[k]!r} != current {v!r}")
+    else:
+        with open(args_path, "w") as f:
+            for k, v in sorted(vars(args).items()):
+                f.write(f"{k}: {v}\n")
+    os.makedirs(args.log_dir, exist_ok=True)
+    logging.basicConfig(filename=os.path.join(args.log_dir, "encode.log"), level=logging.INFO)
+    log = logging.getLogger("geobpe.encode")
+    log.info(args)
+
+    from geobpe.bpe import BPE
+    corpus = load_corpus(args.data_dir, args.toy)
+    bpe = BPE(corpus, bins=args.bins, bin_strategy=args.bin_strategy, save_dir=args.save_dir,
+              res_init=args.res_init, std_bonds=not args.free_bonds,
+              rmsd_partition_min_size=args.p_min_size, glue_opt=args.glue_opt, seed=args.seed,
+              device=args.device)
+    t0 = time.time()
+    bpe.initialize()
+    with open(os.path.join(args.save_dir, "initial_stats=-1.json"), "w") as f:
+        json.dump(stats(bpe), f)
+    bpe.bin()
+    log.info("initialize+bin %.3fs", time.time() - t0)
+
+    start, ck = latest_checkpoint(args.save_dir)
+    if ck is not None:  # resume: replay the merges, then check them against the file
+        with open(ck) as f:
+            saved = json.load(f)
+        done = bpe.run(len(saved["merges"]))
+        if [list(m) for m in bpe.merges] != saved["merges"] or done != len(saved["merges"]):
+            raise SystemExit(f"replay of {ck} diverged from the saved merge list")
+        log.info("resumed from %s at iter=%d", ck, start)
+
+    chunk = args.run_chunk or args.save_every
+    t = start + 1
+    while t < args.max_iter:
+        # next save point: t with t % save_every == 0 (encode.py:403)
+        nxt = min(args.max_iter - 1, t + (-t) % args.save_every, t + chunk - 1)
+        n = nxt - t + 1
+        got = bpe.run(n)
+        if got < n:
+            log.info("no pairs left after %d merges", bpe._step)
+            break
+        t = nxt
+        if t % args.save_every == 0:
+            with open(os.path.join(args.save_dir, f"stats={t}.json"), "w") as f:
+                json.dump(stats(bpe), f)
+            tmp = os.path.join(args.save_dir, f".bpe_iter={t}.json.tmp")
+            with open(tmp, "w") as f:
+                json.dump({"iter": t, "merges": [list(m) for m in bpe.merges],
+                           "args": {k: str(v) for k, v in vars(args).items()}}, f)
+            os.replace(tmp, os.path.join(args.save_dir, f"bpe_iter={t}.json"))
+        t += 1
+    log.info("done: %d merges, vocab_size %d", bpe._step, bpe.vocab_size)
+    print(json.dumps({"merges": bpe._step, "vocab_size": bpe.vocab_size,
+                      "seconds": time.time() - t0}))
+    bpe.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -136,7 +136,8 @@ class VirtualCluster:
     """k row shards in one process on one device, run in lockstep with the exact
     multi-rank protocol (replicated counts, delta exchange)."""
 
-    def __init__(self, corpus: dict, bins: int, world: int, device: int = 0, max_vocab: int = 1 << 20):
+    def __init__(self, corpus: dict, bins: int, world: int, device: int = 0, max_vocab: int = 1 << 20,
+                 cover: bool = False):
         import torch
         self.torch = torch
         self.world = world
@@ -146,6 +147,7 @@ class VirtualCluster:
         self.R = [int(s["row_off"][-1]) for s in self.shards]
         self.base = [int(sum(self.R[:r])) for r in range(world)]
         self.B = int(bins)
+        self.cover = bool(cover)
         self.dev = torch.device("cuda", device)
         self.merges = []
 
@@ -173,7 +175,7 @@ class VirtualCluster:
             mn, mx, c = float(mm[2 * t]), float(mm[2 * t + 1]), int(cnt[t])
             if key == "tau" and n_rows > 0:
                 mn, mx, c = (min(mn, w0), max(mx, w0), c + n_rows) if c > 0 else (w0, w0, n_rows)
-            e_ = histogram_edges(mn, mx, c, self.B)
+            e_ = histogram_edges(mn, mx, c, self.B, self.cover)
             edges[t] = e_
             thr[key] = [(float(s), float(f)) for s, f in zip(e_[:-1], e_[1:])]
         self.thresholds = thr

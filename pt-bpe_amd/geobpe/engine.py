@@ -43,11 +43,12 @@ def init_bond_angle() -> float:
     return float(np.arccos(np.clip(np.dot(u1, u2), -1.0, 1.0)))
 
 
-def histogram_edges(mn: float, mx: float, count: int, B: int) -> np.ndarray:
+def histogram_edges(mn: float, mx: float, count: int, B: int, cover: bool = False) -> np.ndarray:
     """np.histogram(a, bins=B) edges given only min/max/len of ``a`` (numpy's
-    _get_outer_edges + linspace depend on nothing else)."""
+    _get_outer_edges + linspace depend on nothing else).  ``cover``: the
+    "histogram-cover" strategy, range=(0, 2*pi) (plotting.py:319)."""
     a = np.array([mn, mx], dtype=np.float64) if count > 0 else np.zeros(0, dtype=np.float64)
-    return np.histogram_bin_edges(a, bins=B)
+    return np.histogram_bin_edges(a, bins=B, range=(0, TWO_PI) if cover else None)
 
 
 def _p(a: np.ndarray):
@@ -66,13 +67,14 @@ def _stream_handle(device: int):
 
 class GeoBPEEngine:
     def __init__(self, corpus: dict, bins: int, device: int = 0, max_vocab: int = 1 << 20,
-                 group=None, stream=None, use_torch_stream: bool = True):
+                 group=None, stream=None, use_torch_stream: bool = True, cover: bool = False):
         """``corpus``: ``{column: float64[R]}`` + ``row_off`` (geobpe.synth layout) for
         THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs."""
         self.L = _native.lib()
         self.B = int(bins)
         self.device = int(device)
         self.group = group
+        self.cover = bool(cover)
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
         self.n_rows = len(self.row_off) - 1
         self._cols = [np.ascontiguousarray(corpus[c], dtype=np.float64) for c in COLUMNS]
@@ -127,7 +129,7 @@ class GeoBPEEngine:
             mn, mx, c = float(mm[2 * t]), float(mm[2 * t + 1]), int(cnt[t])
             if key == "tau" and n_rows_total > 0:  # bpe.py:845-846: + _bond_angle(0) per tokenizer
                 mn, mx, c = (min(mn, w0), max(mx, w0), c + n_rows_total) if c > 0 else (w0, w0, n_rows_total)
-            e = histogram_edges(mn, mx, c, self.B)
+            e = histogram_edges(mn, mx, c, self.B, self.cover)
             edges[t] = e
             self.thresholds[key] = [(float(s), float(f)) for s, f in zip(e[:-1], e[1:])]
         self._edges = edges

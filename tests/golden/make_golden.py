@@ -39,6 +39,7 @@ FIXTURES = {
     "g25x1-12_b3_short": (25, 1, 12, 3, 40, 4, 0.0),
     "g300x60-200_b5": (300, 60, 200, 5, 40, 5, 0.0),
     "g80x40-160_b7_rep": (80, 40, 160, 7, 100, 6, 0.1),
+    "g50x30-110_b6_cover": (50, 30, 110, 6, 80, 7, 0.1, "histogram-cover"),
 }
 
 
@@ -74,7 +75,8 @@ def run_one(name: str) -> None:
     import numpy as np
     from geobpe import synth
 
-    n_seqs, lo, hi, bins, merges, seed, rep = FIXTURES[name]
+    n_seqs, lo, hi, bins, merges, seed, rep = FIXTURES[name][:7]
+    strategy = FIXTURES[name][7] if len(FIXTURES[name]) > 7 else "histogram"
     lengths = synth.make_lengths(n_seqs, lo, hi, seed=seed)
     corpus = synth.make_corpus(lengths, seed=seed, repeat_frac=rep)
 
@@ -93,7 +95,7 @@ def run_one(name: str) -> None:
         s["fname"] = f"synthetic_{i}"
         structs.append(s)
     t0 = time.time()
-    bpe = B.BPE(structs, bins={1: bins}, save_dir=tempfile.mkdtemp(prefix="geobpe_golden_"),
+    bpe = B.BPE(structs, bins={1: bins}, bin_strategy=strategy, save_dir=tempfile.mkdtemp(prefix="geobpe_golden_"),
                 rmsd_partition_min_size=float("inf"), res_init=True, std_bonds=True, seed=0)
     bpe.initialize()
     init_labels = np.concatenate([
@@ -121,10 +123,23 @@ def run_one(name: str) -> None:
         ids.extend(q)
         ids_off.append(len(ids))
     thresholds = {k: [list(p) for p in v] for k, v in bpe._thresholds[1].items()}
+    # object-API views for the host mirror (geobpe.bpe): first three chains
+    t0s = bpe.tokenizers[:3]
+    api = {
+        "tokenize": [[list(x) for x in t.tokenize()] for t in t0s],
+        "token_pos": [list(t.token_pos) for t in t0s],
+        "bond_to_token": [[list(v) for v in t.bond_to_token.values()] for t in t0s],
+        "dequantize": [[list(x) for x in bpe.dequantize(bpe.quantize(t))] for t in t0s],
+        "recover": [bpe.recover(t.tokenize()) for t in t0s],
+        "capacity": bpe.capacity(), "capacity_tokenizer": float(bpe.capacity(tokenizer=True)),
+        "bin_counts": {k: [int(c) for c in v] for k, v in bpe._bin_counts[1].items()},
+    }
     meta = {
         "name": name,
         "n_seqs": n_seqs, "len_lo": lo, "len_hi": hi, "seed": seed, "repeat_frac": rep,
         "bins": {"1": bins},
+        "bin_strategy": strategy,
+        "api": api,
         "merges_requested": merges,
         "K0": k0,
         "thresholds": thresholds,

@@ -1,0 +1,146 @@
+"""The drop-in object API (geobpe.bpe.BPE, mirror of foldingdiff.bpe.BPE) against
+the reference's own outputs for the same calls (tests/golden/*.json "api")."""
+import json
+
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+
+
+def _bpe(meta, corpus):
+    from geobpe.bpe import BPE
+    b = BPE(corpus, bins={1: meta["bins"]["1"]}, bin_strategy=meta.get("bin_strategy", "histogram"),
+            res_init=True, rmsd_partition_min_size=float("inf"), std_bonds=True, seed=0)
+    return b
+
+
+@pytest.mark.parametrize("kw, exc", [
+    (dict(res_init=False), NotImplementedError),
+    (dict(rmsd_partition_min_size=4), NotImplementedError),
+    (dict(glue_opt=True), NotImplementedError),
+    (dict(std_bonds=False), NotImplementedError),
+    (dict(bin_strategy="uniform"), NotImplementedError),
+    (dict(bins={1: 5, 10: 3}), NotImplementedError),
+    (dict(bins={2: 5}), KeyError),
+])
+def test_out_of_scope_configurations_are_rejected(kw, exc):
+    """Scope check happens before any device work (runs without a GPU)."""
+    from geobpe.bpe import BPE
+    args = dict(bins={1: 5}, res_init=True, rmsd_partition_min_size=float("inf"))
+    args.update(kw)
+    bins = args.pop("bins")
+    with pytest.raises(exc):
+        BPE({"row_off": np.zeros(1, dtype=np.int64)}, bins, **args)
+
+
+def test_codebook_utility_matches_definition():
+    from geobpe.bpe import get_codebook_utility
+    u = get_codebook_utility([0, 0, 1, 3], 4)
+    p = np.array([0.5, 0.25, 0, 0.25])
+    ent = -np.sum(p * np.log(p + 1e-8))
+    assert abs(u["entropy"] - ent) < 1e-6 and u["use_ratio"] == 0.75
+
+
+def test_threshold_dict_floor_lookup():
+    from geobpe.bpe import ThresholdDict
+    t = ThresholdDict({1: "a", 5: "b", "N:CA": "c"})
+    assert t[1] == "a" and t[4] == "a" and t[5] == "b" and t[99] == "b" and t["N:CA"] == "c"
+    with pytest.raises(KeyError):
+        t[0]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["step", "run"])
+@pytest.mark.parametrize("name", golden_names())
+def test_bpe_object_api_matches_reference(name, mode):
+    meta, corpus, arrs = load_golden(name)
+    api = meta["api"]
+    b = _bpe(meta, corpus)
+    b.initialize()
+    assert {k: [list(p) for p in v] for k, v in b._thresholds[1].items()} == meta["thresholds"]
+    assert b._bin_counts[1] == api["bin_counts"]
+    b.bin()
+    if mode == "step":
+        for _ in range(len(meta["merges"])):
+            b.step()
+    else:
+        assert b.run(len(meta["merges"])) == len(meta["merges"])
+    assert b._step == len(meta["merges"])
+    assert {str(k): v for k, v in b._tokens.items()} == meta["vocab"]
+    assert b.vocab_size == meta["vocab_size"]
+    assert {k: b.cum_bin_count(k) for k in meta["cum_bin_count"]} == meta["cum_bin_count"]
+    assert b.capacity() == api["capacity"]
+    assert abs(b.capacity(tokenizer=True) - api["capacity_tokenizer"]) <= 1e-9 * api["capacity_tokenizer"]
+    toks = b.tokenizers
+    q = b.quantize(toks)
+    flat = np.concatenate([np.asarray(x, dtype=np.int64) for x in q])
+    assert np.array_equal(flat, arrs["ids"])
+    for i, t in enumerate(toks[:3]):
+        assert [list(v) for v in t.bond_to_token.values()] == api["bond_to_token"][i]
+        assert t.token_pos == api["token_pos"][i]
+        tt = t.tokenize()
+        assert [list(x) for x in tt] == api["tokenize"][i]
+        assert b.quantize(tt) == b.quantize(t)  # tuple path == tokenizer path
+        assert [list(x) for x in b.dequantize(b.quantize(t))] == api["dequantize"][i]
+        assert json.loads(json.dumps(b.recover(tt))) == api["recover"][i]
+    b.close()
+
+
+@pytest.mark.gpu
+def test_step_past_exhaustion_raises():
+    from geobpe import synth
+    from geobpe.bpe import BPE
+    lengths = synth.make_lengths(6, 1, 6, seed=3)
+    b = BPE(synth.make_corpus(lengths, seed=3), {1: 2}, res_init=True,
+            rmsd_partition_min_size=float("inf"))
+    b.initialize()
+    b.bin()
+    b.run(10000)
+    with pytest.raises(IndexError):
+        b.step()
+    assert all(len(t.tokens) == 1 for t in b.tokenizers)
+    b.close()
+
+
+def _encode_cli():
+    import importlib.util
+    import os
+    from conftest import REPO
+    spec = importlib.util.spec_from_file_location("geobpe_encode_cli", os.path.join(REPO, "pt-bpe_amd", "bin", "encode.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_cli_flags_mirror_reference_parsers():
+    cli = _encode_cli()
+    a = cli.parse_args(["--save-dir", "x", "--bins", "1-5", "--p-min-size", "inf", "--res-init", "true"])
+    assert a.bins == {1: 5} and a.p_min_size == float("inf") and a.res_init is True
+    assert cli.str2dict("1-5:10-3") == {1: 5, 10: 3}
+    with pytest.raises(Exception):
+        cli.str2dict("1-5:")
+
+
+def test_cli_latest_checkpoint_skips_incomplete(tmp_path):
+    cli = _encode_cli()
+    (tmp_path / "bpe_iter=10.json").write_text(json.dumps({"merges": []}))
+    (tmp_path / "bpe_iter=20.json").write_text("{\"merges\": [")  # torn write
+    it, path = cli.latest_checkpoint(str(tmp_path))
+    assert it == 10 and path.endswith("bpe_iter=10.json")
+
+
+@pytest.mark.gpu
+def test_cli_resume_reproduces_one_shot(tmp_path):
+    cli = _encode_cli()
+    common = ["--data-dir", "synthetic:300:30:150:5", "--bins", "1-5", "--save-every", "10",
+              "--log-dir", str(tmp_path / "logs")]
+    one, two = tmp_path / "one", tmp_path / "two"
+    assert cli.main(common + ["--save-dir", str(one), "--max-iter", "61"]) == 0
+    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "31"]) == 0
+    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "61"]) == 0  # resumes at 30
+    a = json.loads((one / "bpe_iter=60.json").read_text())["merges"]
+    b = json.loads((two / "bpe_iter=60.json").read_text())["merges"]
+    assert a == b and len(a) == 61
+    sa = json.loads((one / "stats=60.json").read_text())
+    assert sa == json.loads((two / "stats=60.json").read_text()) and sa["K"] > 0

@@ -33,7 +33,7 @@ def _check_against_golden(run, meta, arrs, thresholds=None):
 def test_engine_matches_reference_golden(name, mode):
     meta, corpus, arrs = load_golden(name)
     B = meta["bins"]["1"]
-    eng = _engine(corpus, B)
+    eng = _engine(corpus, B, cover=meta.get("bin_strategy") == "histogram-cover")
     assert eng.K0 == meta["K0"]
     eng.bin()
     if mode == "step":
@@ -51,11 +51,13 @@ def test_engine_matches_reference_golden(name, mode):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-@pytest.mark.parametrize("name", ["g40x40-120_b12", "g60x20-90_b5_rep", "g25x1-12_b3_short"])
+@pytest.mark.parametrize("name", ["g40x40-120_b12", "g60x20-90_b5_rep", "g25x1-12_b3_short",
+                                  "g50x30-110_b6_cover"])
 def test_sharded_matches_reference_golden(name, world):
     from geobpe.dist import VirtualCluster
     meta, corpus, arrs = load_golden(name)
-    vc = VirtualCluster(corpus, meta["bins"]["1"], world=world).initialize()
+    vc = VirtualCluster(corpus, meta["bins"]["1"], world=world,
+                        cover=meta.get("bin_strategy") == "histogram-cover").initialize()
     assert vc.thresholds == {k: [tuple(p) for p in v] for k, v in meta["thresholds"].items()}
     vc.bin()
     ref = vc.engines[0].key_counts()  # replicated global counts agree on every rank

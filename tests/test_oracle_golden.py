@@ -12,7 +12,8 @@ from conftest import golden_names, load_golden
 def test_oracle_matches_reference(name, oracle_lib):
     meta, corpus, arrs = load_golden(name)
     B = meta["bins"]["1"]
-    o = oracle_lib.OracleBPE(corpus, B).initialize()
+    cover = meta.get("bin_strategy", "histogram") == "histogram-cover"
+    o = oracle_lib.OracleBPE(corpus, B, cover=cover).initialize()
     # thresholds (bpe.py:820-876) and first-appearance labels (bpe.py:231-261)
     assert o.thresholds == {k: [tuple(p) for p in v] for k, v in meta["thresholds"].items()}
     assert np.array_equal(o.labels, arrs["init_labels"])
