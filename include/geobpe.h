@@ -141,7 +141,9 @@ int64_t geobpe_encode(geobpe_ctx *ctx, int32_t *h_ids, int64_t *h_row_id_off);
 int64_t geobpe_verify_counts(geobpe_ctx *ctx);
 /* Per-kernel time (ms summed over launches, HIP events on the context stream)
  * while profiling is enabled.  names: "pair_count", "argmax", "select",
- * "mark", "apply", "assign", "finalize", "recount". */
+ * "mark", "apply", "assign", "finalize", "recount".  on = 0: off; on = 1: every
+ * launch; on = k > 1: every k-th launch of each kernel (sampling keeps the event
+ * packets from stretching the stream they measure). */
 int geobpe_set_profiling(geobpe_ctx *ctx, int on);
 /* Restrict the timing to a comma-separated list of kernel names ("" = all). */
 int geobpe_set_profiling_filter(geobpe_ctx *ctx, const char *names);

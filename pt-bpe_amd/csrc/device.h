@@ -20,7 +20,7 @@ constexpr int BLOCK = 256;
 constexpr int AGG = 512;       // LDS partial-count slots per workgroup
 constexpr int AGG_SHIFT = 23;  // 32 - log2(AGG)
 constexpr int RPB = 8;         // mark regions per apply workgroup (NB = RPB * NBA)
-constexpr int BLK_CANDS = 8;   // argmax candidates kept per workgroup
+constexpr int CL_MIN_SHRINK = 4096;  // hot-list length above which a 4x drop of theta re-scans
 constexpr int ID_CHUNK = 256;  // dense ids a workgroup reserves at a time
 
 // ------------------------------------------------------------------ records
@@ -40,9 +40,16 @@ struct State {
   u64 w1, w2;                      // content hash of the merged token
   u64 pwW1a, pwW1b, pwW2a, pwW2b;  // P^(|W|syms+1), P^|W|syms (both bases)
   int32_t wl, wfp;                 // residues of W, key_fp(W)
-  // per-iteration, reset by k_select_final
+  // per-iteration, reset by k_select
   int64_t L_ovf, np_ovf, ns_ovf, nL_total;
   int64_t ntouched, nmismatch;
+  // hot list (argmax): every key with count >= theta is in clist[0..ncl)
+  int64_t ncl;
+  int32_t theta;      // 0 = list not built yet
+  int32_t cl_valid;
+  int32_t skip;       // this iteration only rebuilds the hot list (no merge)
+  int32_t theta_new;  // threshold of that rebuild
+  int64_t nskip;      // rebuild iterations so far (stats)
 };
 
 struct LEntry {  // one merge: left token a (+ its prev p), right token b (+ next c)
@@ -65,10 +72,6 @@ struct DeltaRec {  // 40 bytes, exchanged between ranks
   int32_t len, idL, g, idR, delta, pad;
 };
 static_assert(sizeof(DeltaRec) == 40, "delta record layout");
-struct BlkMax {
-  int32_t max, n;
-  int32_t c[BLK_CANDS];
-};
 struct LogRec {  // one merge of the run (the merge list, device side)
   int32_t nid, count, W, idL, g, idR;
   int64_t nmerged;
@@ -118,9 +121,8 @@ struct Dev {
   int64_t* chunk;  // per apply workgroup: [next, end) of its reserved dense-id chunk
   int64_t ovf_cap;
   // argmax
-  int32_t* bmax;  // per mark-workgroup max count (contiguous, for k_select_final)
-  BlkMax* blk;
-  int32_t* cand;
+  int32_t* clist;  // hot list (capacity UC)
+  int32_t* cand;   // tied keys of the current maximum
   int64_t candcap;
   LogRec* log;
   State* st;
@@ -303,6 +305,82 @@ __device__ inline void agg_flush(Agg& s, const Dev& D, bool to_delta) {
     const int32_t k = s.key[i];
     if (k >= 0 && s.val[i] != 0) global_add(D, k, s.val[i], to_delta);
   }
+}
+
+// hot-list appends (argmax): a key whose count crosses theta from below joins
+// clist; LDS-buffered, one global reservation per workgroup
+constexpr int HOT_BUF = 256;
+struct HotApp {
+  int32_t n;
+  int32_t buf[HOT_BUF];
+};
+__device__ inline void hot_init(HotApp& h) {
+  if (threadIdx.x == 0) h.n = 0;
+}
+__device__ inline void hot_store(const Dev& D, int64_t k, int32_t d) {
+  if (k < D.UC)
+    D.clist[k] = d;
+  else
+    D.st->cl_valid = 0;  // list lost an entry: the next k_select rebuilds it
+}
+__device__ inline void hot_push(const Dev& D, HotApp& h, int32_t d) {
+  const int32_t j = atomicAdd(&h.n, 1);
+  if (j < HOT_BUF)
+    h.buf[j] = d;
+  else
+    hot_store(D, (int64_t)atomicAdd((unsigned long long*)&D.st->ncl, 1ULL), d);
+}
+__device__ inline void hot_flush(const Dev& D, HotApp& h) {
+  __shared__ int64_t s_base;
+  __syncthreads();
+  const int32_t n = min(h.n, HOT_BUF);
+  if (threadIdx.x == 0 && n > 0) s_base = (int64_t)atomicAdd((unsigned long long*)&D.st->ncl, (unsigned long long)n);
+  __syncthreads();
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) hot_store(D, s_base + i, h.buf[i]);
+}
+// global count update with the theta-crossing check (positive deltas only can cross)
+__device__ inline void count_add_hot(const Dev& D, HotApp& h, int32_t d, int32_t v, int32_t th) {
+  if (v > 0 && th > 0) {
+    const int32_t old = atomicAdd(&D.count[d], v);
+    if (old < th && old + v >= th) hot_push(D, h, d);
+  } else {
+    atomicAdd(&D.count[d], v);
+  }
+}
+__device__ inline void agg_add_hot(Agg& s, const Dev& D, HotApp& h, int32_t d, int32_t v, bool to_delta, int32_t th) {
+  uint32_t hh = ((uint32_t)d * 2654435761u) >> AGG_SHIFT;
+#pragma unroll 1
+  for (int probe = 0; probe < 8; probe++) {
+    const int32_t k = s.key[hh];
+    if (k == d) {
+      atomicAdd(&s.val[hh], v);
+      return;
+    }
+    if (k == -1) {
+      const int32_t old = atomicCAS(&s.key[hh], -1, d);
+      if (old == -1 || old == d) {
+        atomicAdd(&s.val[hh], v);
+        return;
+      }
+    }
+    hh = (hh + 1) & (AGG - 1);
+  }
+  if (to_delta)
+    global_add(D, d, v, true);
+  else
+    count_add_hot(D, h, d, v, th);
+}
+__device__ inline void agg_flush_hot(Agg& s, const Dev& D, HotApp& h, bool to_delta, int32_t th) {
+  __syncthreads();
+  for (int i = threadIdx.x; i < AGG; i += blockDim.x) {
+    const int32_t k = s.key[i];
+    if (k < 0 || s.val[i] == 0) continue;
+    if (to_delta)
+      global_add(D, k, s.val[i], true);
+    else
+      count_add_hot(D, h, k, s.val[i], th);
+  }
+  hot_flush(D, h);
 }
 
 // key-table probing: the first slot of a key and, given the value already read

@@ -3,9 +3,9 @@
 //
 // Replaces the Python/dict hot path of foldingdiff/bpe.py (BPE.initialize /
 // bin / step / quantize).  Integer work only (no
-// MFMA).  One merge iteration is five stream-ordered launches with no host
+// MFMA).  One merge iteration is four stream-ordered launches with no host
 // synchronisation:
-//   k_argmax_blocks -> k_select_final   max count, exact candidate set, reference
+//   k_select                            hot-list max count, tied keys, reference
 //                                       key-string tie-break, new token (device)
 //   k_mark                              scan pk for the winner, greedy run walks
 //   k_apply                             rewrite tokens, count deltas, new pairs,
@@ -55,7 +55,9 @@ struct geobpe_ctx {
   int nba = 256;  // apply / finalize / assign / bin / import workgroups (= D.NBA)
   // profiling
   bool prof = false;
+  int prof_stride = 1;      // time every prof_stride-th launch of each kernel
   std::string prof_filter;  // ",name,name," or empty = every kernel
+  std::map<std::string, int64_t> prof_seen;
   std::map<std::string, std::pair<double, int64_t>> ktime;
   struct Pend {
     std::string name;
@@ -121,6 +123,7 @@ struct Timed {
   Timed(geobpe_ctx* c_, const char* n) : c(c_), name(n) {
     if (!c->prof) return;
     if (!c->prof_filter.empty() && c->prof_filter.find("," + std::string(n) + ",") == std::string::npos) return;
+    if (c->prof_stride > 1 && (c->prof_seen[n]++ % c->prof_stride) != 0) return;
     a = take_event(c);
     b = take_event(c);
     hipEventRecord(a, c->stream);
@@ -216,23 +219,15 @@ int alloc_keys(geobpe_ctx* c) {
       return rc;
   }
   D.candcap = 1 << 20;
-  if ((rc = dalloc(c, &D.blk, c->nb)) || (rc = dalloc(c, &D.bmax, c->nb + 4, 0)) ||
-      (rc = dalloc(c, &D.cand, D.candcap)))
-    return rc;
+  if ((rc = dalloc(c, &D.clist, D.UC)) || (rc = dalloc(c, &D.cand, D.candcap))) return rc;
   c->keys_ready = true;
   return 0;
 }
 
 // the launches of one merge iteration (no host synchronisation)
 void enqueue_select(geobpe_ctx* c) {
-  {
-    Timed t(c, "argmax");
-    hipLaunchKernelGGL(k_argmax_blocks, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
-  }
-  {
-    Timed t(c, "select");
-    hipLaunchKernelGGL(k_select_final, dim3(1), dim3(BLOCK), 0, c->stream, c->D, c->nb);
-  }
+  Timed t(c, "select");
+  hipLaunchKernelGGL(k_select, dim3(1), dim3(BLOCK), 0, c->stream, c->D);
 }
 
 void enqueue_commit(geobpe_ctx* c, bool to_delta, bool merge_iter) {
@@ -529,10 +524,14 @@ int geobpe_bin(geobpe_ctx* c) {
 int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {
   if (!c || !c->keys_ready || !new_id) return GEOBPE_EARG;
   HIPCHK(c, hipSetDevice(c->device));
-  enqueue_select(c);
-  HIPCHK(c, hipGetLastError());
   int rc;
-  if ((rc = sync_state(c))) return rc;
+  for (;;) {
+    enqueue_select(c);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = sync_state(c))) return rc;
+    if (c->h_state->done || !c->h_state->skip) break;
+    enqueue_commit(c, false, true);  // hot-list rebuild (rank-local, same decision on every rank)
+  }
   if (c->h_state->done) {
     *new_id = -1;
     if (count) *count = 0;
@@ -564,11 +563,14 @@ int geobpe_step(geobpe_ctx* c, int32_t* new_id, int32_t* count, int64_t* n_merge
   if (c->distributed) return fail(c, GEOBPE_EARG, "geobpe_step in distributed mode: use step_select/apply + deltas");
   HIPCHK(c, hipSetDevice(c->device));
   const int32_t it0 = c->h_state->iter;
-  enqueue_select(c);
-  enqueue_apply(c);
-  HIPCHK(c, hipGetLastError());
   int rc;
-  if ((rc = sync_state(c))) return rc;
+  for (;;) {  // an iteration that only rebuilt the hot list merges nothing: go again
+    enqueue_select(c);
+    enqueue_apply(c);
+    HIPCHK(c, hipGetLastError());
+    if ((rc = sync_state(c))) return rc;
+    if (c->h_state->iter != it0 || c->h_state->done) break;
+  }
   if (c->h_state->iter == it0) {
     *new_id = -1;
     if (count) *count = 0;
@@ -589,13 +591,18 @@ int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) {
   if (c->distributed) return fail(c, GEOBPE_EARG, "geobpe_run in distributed mode");
   HIPCHK(c, hipSetDevice(c->device));
   const int32_t it0 = c->h_state->iter;
-  for (int64_t i = 0; i < n_iters; i++) {
-    enqueue_select(c);
-    enqueue_apply(c);
-  }
-  HIPCHK(c, hipGetLastError());
   int rc;
-  if ((rc = sync_state(c))) return rc;
+  // hot-list rebuild iterations merge nothing: top up until n merges or done
+  for (int64_t want = n_iters; want > 0;) {
+    for (int64_t i = 0; i < want; i++) {
+      enqueue_select(c);
+      enqueue_apply(c);
+    }
+    HIPCHK(c, hipGetLastError());
+    if ((rc = sync_state(c))) return rc;
+    if (c->h_state->done) break;
+    want = n_iters - (c->h_state->iter - it0);
+  }
   if (n_done) *n_done = c->h_state->iter - it0;
   return 0;
 }
@@ -846,7 +853,9 @@ int geobpe_debug_key(geobpe_ctx* c, int32_t d, int64_t* out) {
 int geobpe_set_profiling(geobpe_ctx* c, int on) {
   if (!c) return GEOBPE_EARG;
   collect_events(c);
-  c->prof = on != 0;
+  c->prof = on > 0;
+  c->prof_stride = on > 1 ? on : 1;
+  c->prof_seen.clear();
   c->ktime.clear();
   return 0;
 }

@@ -259,9 +259,10 @@ __global__ __launch_bounds__(BLOCK) void k_pairs_all(Dev D) {
   close_regions(D, &s_np, &s_ns);
 }
 
-// dense id of a key claimed in this launch (key arrays + table slot -> id)
-// pair -> dense key id into pk, counts via LDS-staged partial counts
-__device__ inline void finalize_one(const Dev& D, Agg& agg, const NewPair& e, int64_t j, bool to_delta) {
+// pair -> dense key id into pk, counts via LDS-staged partial counts (+ the
+// hot-list crossing check on the global counts)
+__device__ inline void finalize_one(const Dev& D, Agg& agg, HotApp& hot, const NewPair& e, int64_t j, bool to_delta,
+                                    int32_t th) {
   const int32_t d = D.ht_dense[e.slot];
   if (d < 0 || D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) {
     set_error(D, GEOBPE_EHASH, j);
@@ -271,13 +272,46 @@ __device__ inline void finalize_one(const Dev& D, Agg& agg, const NewPair& e, in
     D.pk[e.target] = d;
     D.fp[e.target] = key_fp(d);
   }
-  agg_add(agg, D, d, e.delta, to_delta);
+  agg_add_hot(agg, D, hot, d, e.delta, to_delta, th);
+}
+
+// a hot-list rebuild iteration (k_select set st->skip): clist = every key with
+// count >= theta_new.  Two coalesced passes over this workgroup's key range; one
+// global reservation per workgroup.
+__device__ void rebuild_hot_list(const Dev& D) {
+  __shared__ int32_t s_red[BLOCK / 64];
+  __shared__ int64_t s_base;
+  State* st = D.st;
+  const int32_t th = st->theta_new;
+  const int64_t U = st->U;
+  const int64_t per = (U + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
+  int32_t n = 0;
+  for (int64_t d = lo + threadIdx.x; d < hi; d += BLOCK) n += D.count[d] >= th;
+  int32_t tot;
+  const int32_t ex = block_excl_scan(n, &tot, s_red);
+  if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&st->ncl, (unsigned long long)tot) : 0;
+  __syncthreads();
+  int64_t j = s_base + ex;
+  for (int64_t d = lo + threadIdx.x; d < hi; d += BLOCK)
+    if (D.count[d] >= th) D.clist[j++] = (int32_t)d;  // j < U <= UC
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->theta = th;
+    st->cl_valid = 1;
+  }
 }
 
 __global__ __launch_bounds__(BLOCK) void k_finalize(Dev D, int to_delta, int merge_iter) {
   __shared__ Agg agg;
+  __shared__ HotApp hot;
   if (merge_iter && D.st->done) return;
+  if (merge_iter && D.st->skip) {
+    rebuild_hot_list(D);
+    return;
+  }
+  const int32_t th = D.st->theta;
   agg_init(agg);
+  hot_init(hot);
   if (merge_iter && blockIdx.x == 0) {  // merges applied this iteration -> merge log
     __shared__ int32_t s_red[BLOCK / 64];
     int32_t nm = 0;
@@ -292,11 +326,11 @@ __global__ __launch_bounds__(BLOCK) void k_finalize(Dev D, int to_delta, int mer
   }
   const int32_t n = D.npcnt[blockIdx.x];
   const NewPair* reg = D.np + (int64_t)blockIdx.x * D.RC;
-  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) finalize_one(D, agg, reg[i], i, to_delta != 0);
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) finalize_one(D, agg, hot, reg[i], i, to_delta != 0, th);
   const int64_t novf = min(D.st->np_ovf, D.ovf_cap);
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x)
-    finalize_one(D, agg, D.npovf[k], k, to_delta != 0);
-  agg_flush(agg, D, to_delta != 0);
+    finalize_one(D, agg, hot, D.npovf[k], k, to_delta != 0, th);
+  agg_flush_hot(agg, D, hot, to_delta != 0, th);
 }
 
 // ====================================================================== argmax + tie-break
@@ -307,10 +341,17 @@ struct JGen {
   int32_t nA, g, nC;
   int32_t B, B2, B3, r, lam;
   int32_t sec, item, len, pos;
-  char buf[24];
+  char* buf;  // 24 chars of LDS per generator (private arrays would put the kernel on scratch)
 
-  __device__ int32_t sym(int32_t k) const { return k < nA ? A[k] : (k == nA ? g : C[k - nA - 1]); }
-  __device__ void init(const int32_t* a, int32_t na, int32_t gg, const int32_t* c, int32_t nc, int32_t b) {
+  // (a select between two global pointers, then g by value: a pointer to g would
+  // put the generator on the scratch stack)
+  __device__ int32_t sym(int32_t k) const {
+    const int32_t* p = k < nA ? A + k : C + max(k - nA - 1, 0);
+    const int32_t v = *p;
+    return k == nA ? g : v;
+  }
+  __device__ void init(const int32_t* a, int32_t na, int32_t gg, const int32_t* c, int32_t nc, int32_t b, char* lds) {
+    buf = lds;
     A = a;
     nA = na;
     g = gg;
@@ -350,13 +391,13 @@ struct JGen {
     while (*s) buf[len++] = *s++;
   }
   __device__ void put_int(int32_t v) {
-    char t[12];
-    int n = 0;
-    do {
-      t[n++] = (char)('0' + v % 10);
+    int n = 1;
+    for (int32_t x = v; x >= 10; x /= 10) n++;
+    for (int k = n - 1; k >= 0; k--) {
+      buf[len + k] = (char)('0' + v % 10);
       v /= 10;
-    } while (v);
-    while (n) buf[len++] = t[--n];
+    }
+    len += n;
   }
   __device__ bool refill() {
     len = pos = 0;
@@ -401,25 +442,19 @@ struct JGen {
   }
 };
 
-__device__ inline void key_src(const Dev& D, int32_t d, const int32_t** A, int32_t* nA, int32_t* g, const int32_t** C,
-                               int32_t* nC) {
-  const int32_t L = D.krep[3 * d], Rr = D.krep[3 * d + 2];
-  *g = D.krep[3 * d + 1];
-  *A = D.vsym + D.voff[L];
-  *nA = (int32_t)(D.voff[L + 1] - D.voff[L]);
-  *C = D.vsym + D.voff[Rr];
-  *nC = (int32_t)(D.voff[Rr + 1] - D.voff[Rr]);
+// generator over key d's reference string: content(L) ++ [g] ++ content(R)
+__device__ inline void key_gen(const Dev& D, int32_t d, JGen& x, char* lds) {
+  const int32_t L = D.krep[3 * d], g = D.krep[3 * d + 1], Rr = D.krep[3 * d + 2];
+  const int64_t a0 = D.voff[L], a1 = D.voff[L + 1], c0 = D.voff[Rr], c1 = D.voff[Rr + 1];
+  x.init(D.vsym + a0, (int32_t)(a1 - a0), g, D.vsym + c0, (int32_t)(c1 - c0), D.B, lds);
 }
 
-// true iff key a's reference string < key b's (Python str order)
-__device__ inline bool key_less(const Dev& D, int32_t a, int32_t b) {
+// true iff key a's reference string < key b's (Python str order); lds: 48 chars
+// of this thread's LDS
+__device__ inline bool key_less(const Dev& D, int32_t a, int32_t b, char* lds) {
   JGen x, y;
-  const int32_t *A, *C;
-  int32_t nA, g, nC;
-  key_src(D, a, &A, &nA, &g, &C, &nC);
-  x.init(A, nA, g, C, nC, D.B);
-  key_src(D, b, &A, &nA, &g, &C, &nC);
-  y.init(A, nA, g, C, nC, D.B);
+  key_gen(D, a, x, lds);
+  key_gen(D, b, y, lds + 24);
   for (;;) {
     const int ca = x.next(), cb = y.next();
     if (ca != cb) return ca < cb;
@@ -427,157 +462,130 @@ __device__ inline bool key_less(const Dev& D, int32_t a, int32_t b) {
   }
 }
 
-// per-workgroup max count over its dense-key range + up to BLK_CANDS keys at it
-__global__ __launch_bounds__(BLOCK) void k_argmax_blocks(Dev D) {
-  __shared__ int32_t s_red[BLOCK / 64];
-  __shared__ int32_t s_n;
-  __shared__ int32_t s_c[BLK_CANDS];
-  if (D.st->done) return;
-  const int64_t U = D.st->U;
-  const int64_t U4 = (U + 3) / 4;
-  const int64_t per = (U4 + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U4, lo + per);
-  const int4* c4 = reinterpret_cast<const int4*>(D.count);
-  int32_t m = 0;
-  for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-    const int4 v = c4[i];
-    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
-  }
-  m = block_max(m, s_red);
-  if (threadIdx.x == 0) s_n = 0;
-  __syncthreads();
-  if (m > 0) {
-    for (int64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) {
-      const int4 v = c4[i];
-      const int32_t vv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int q = 0; q < 4; q++)
-        if (vv[q] == m) {
-          const int32_t j = atomicAdd(&s_n, 1);
-          if (j < BLK_CANDS) s_c[j] = (int32_t)(4 * i + q);
-        }
-    }
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    BlkMax r;
-    r.max = m;
-    r.n = s_n;
-    for (int q = 0; q < BLK_CANDS; q++) r.c[q] = q < s_n ? s_c[q] : -1;
-    D.blk[blockIdx.x] = r;
-    D.bmax[blockIdx.x] = m;
-  }
-}
-
-// one workgroup: global max, exact candidate set, reference tie-break, then the
-// new token (BPE.step, bpe.py:1796-1860): id, vocab hash / content, merge log
-__global__ __launch_bounds__(BLOCK) void k_select_final(Dev D, int32_t nblk) {
+// BPE.step's argmax (bpe.py:1796-1800, SortedDict peekitem(0)): ONE workgroup
+// over the hot list -- every key with count >= theta is in clist, so when the
+// list maximum m >= theta it is the global maximum and all keys tied at m are in
+// the list.  Otherwise (or when the list has grown long while m >= 4 theta) this
+// iteration is a rebuild: st->skip, theta_new = max(1, m/2) <= the true maximum,
+// and k_finalize re-scans the counts.  Then the reference tie-break (smallest key
+// string) and the new token (bpe.py:1857-1860): id, vocab hash / content, merge log.
+constexpr int SEL_TIES = 256;
+__global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
   __shared__ int32_t s_red[BLOCK / 64];
   __shared__ int32_t s_nc;
-  __shared__ int32_t s_nres;
-  __shared__ int32_t s_res[64];
+  __shared__ int32_t s_tie[SEL_TIES];
   __shared__ int32_t s_best[BLOCK];
-  if (D.st->done) return;
-  int32_t m = 0;
-  const int4* b4 = reinterpret_cast<const int4*>(D.bmax);  // nblk % 4 == 0
-  for (int32_t i = threadIdx.x; i < nblk / 4; i += blockDim.x) {
-    const int4 v = b4[i];
-    m = max(m, max(max(v.x, v.y), max(v.z, v.w)));
+  __shared__ char s_jbuf[48 * BLOCK];
+  State* st = D.st;
+  if (st->done) return;
+  const int64_t n = st->ncl;
+  const int32_t th = st->theta;
+  const bool valid = st->cl_valid != 0;
+  // pass over the list: 4 entries per thread in flight; keep this thread's best
+  int32_t m = 0, mkey = -1, mcnt = 0;
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {
+    int32_t d[4], c[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int64_t i = i0 + (int64_t)q * BLOCK;
+      d[q] = i < n ? D.clist[i] : -1;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) c[q] = d[q] >= 0 ? D.count[d[q]] : 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if (c[q] > m) {
+        m = c[q];
+        mkey = d[q];
+        mcnt = 1;
+      } else if (c[q] == m && d[q] >= 0 && c[q] > 0) {
+        mcnt++;
+      }
+    }
   }
-  m = block_max(m, s_red);
-  if (m <= 0) {
+  const int32_t gm = block_max(m, s_red);
+  if (!valid || gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th)) {
     if (threadIdx.x == 0) {
-      D.st->done = 1;
-      D.st->maxc = 0;
+      if (valid && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
+        st->done = 1;
+        st->maxc = 0;
+      } else {
+        st->skip = 1;
+        st->theta_new = max(1, gm / 2);
+        st->ncl = 0;
+        st->cl_valid = 0;
+        st->nskip += 1;
+      }
     }
     return;
   }
-  if (threadIdx.x == 0) {
-    s_nc = 0;
-    s_nres = 0;
-  }
+  if (threadIdx.x == 0) s_nc = 0;
   __syncthreads();
-  // candidates: listed ones, or a rescan of workgroups that had more than BLK_CANDS
-  for (int32_t i = threadIdx.x; i < nblk; i += blockDim.x) {
-    if (D.bmax[i] != m) continue;
-    const BlkMax& b = D.blk[i];
-    if (b.n <= BLK_CANDS) {
-      for (int q = 0; q < b.n; q++) {
-        const int32_t j = atomicAdd(&s_nc, 1);
-        if (j < D.candcap) D.cand[j] = b.c[q];
-      }
+  // keys tied at the maximum (a thread with several re-reads its own entries)
+  if (m == gm) {
+    if (mcnt == 1) {
+      const int32_t j = atomicAdd(&s_nc, 1);
+      if (j < SEL_TIES) s_tie[j] = mkey; else if (j < D.candcap) D.cand[j] = mkey;
     } else {
-      const int32_t j = atomicAdd(&s_nres, 1);
-      if (j < 64) s_res[j] = i;
-    }
-  }
-  __syncthreads();
-  const int64_t U = D.st->U;
-  const int64_t U4 = (U + 3) / 4;
-  const int64_t per = (U4 + nblk - 1) / nblk;
-  const int32_t nres = s_nres;
-  if (nres > 64) {  // many tied workgroups: rescan every key
-    __syncthreads();
-    if (threadIdx.x == 0) s_nc = 0;
-    __syncthreads();
-    for (int64_t d = threadIdx.x; d < U; d += blockDim.x)
-      if (D.count[d] == m) {
-        const int32_t j = atomicAdd(&s_nc, 1);
-        if (j < D.candcap) D.cand[j] = (int32_t)d;
-      }
-  } else {
-    for (int32_t q = 0; q < nres; q++) {
-      const int64_t lo = 4 * (int64_t)s_res[q] * per, hi = min(U, lo + 4 * per);
-      for (int64_t d = lo + threadIdx.x; d < hi; d += blockDim.x)
-        if (D.count[d] == m) {
+      for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
+        const int32_t d = D.clist[i];
+        if (D.count[d] == gm) {
           const int32_t j = atomicAdd(&s_nc, 1);
-          if (j < D.candcap) D.cand[j] = (int32_t)d;
+          if (j < SEL_TIES) s_tie[j] = d; else if (j < D.candcap) D.cand[j] = d;
         }
+      }
     }
   }
   __syncthreads();
   const int32_t nc = min(s_nc, (int32_t)D.candcap);
   if (s_nc > D.candcap && threadIdx.x == 0) set_error(D, GEOBPE_ECAPACITY, -8);
-  // tie-break: smallest reference key string (SortedDict order, bpe.py:1469-1471)
-  int32_t best = -1;
-  for (int32_t i = threadIdx.x; i < nc; i += blockDim.x) {
-    const int32_t d = D.cand[i];
-    if (best < 0 || key_less(D, d, best)) best = d;
-  }
-  s_best[threadIdx.x] = best;
-  __syncthreads();
-  for (int o = BLOCK / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      const int32_t a = s_best[threadIdx.x], b = s_best[threadIdx.x + o];
-      if (a < 0 || (b >= 0 && key_less(D, b, a))) s_best[threadIdx.x] = b;
+  int32_t W;
+  if (nc == 1) {
+    W = s_tie[0];
+  } else {  // tie-break: smallest reference key string (SortedDict order, bpe.py:1469-1471)
+    int32_t best = -1;
+    for (int32_t i = threadIdx.x; i < nc; i += blockDim.x) {
+      const int32_t d = i < SEL_TIES ? s_tie[i] : D.cand[i];
+      if (best < 0 || (d != best && key_less(D, d, best, s_jbuf + 48 * threadIdx.x))) best = d;
     }
+    s_best[threadIdx.x] = best;
     __syncthreads();
+    for (int o = BLOCK / 2; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) {
+        const int32_t a = s_best[threadIdx.x], b = s_best[threadIdx.x + o];
+        if (a < 0 || (b >= 0 && b != a && key_less(D, b, a, s_jbuf + 48 * threadIdx.x))) s_best[threadIdx.x] = b;
+      }
+      __syncthreads();
+    }
+    W = s_best[0];
   }
-  const int32_t W = s_best[0];
-  const int32_t nid = D.st->K;
+  const int32_t nid = st->K;
   const int32_t L = D.krep[3 * W], g = D.krep[3 * W + 1], Rr = D.krep[3 * W + 2];
-  const int64_t nL = D.voff[L + 1] - D.voff[L], nR = D.voff[Rr + 1] - D.voff[Rr];
-  const int64_t pos = D.st->vsym_used, ln = nL + 1 + nR;
+  const int64_t vL = D.voff[L], vR = D.voff[Rr];
+  const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
+  const int64_t pos = st->vsym_used, ln = nL + 1 + nR;
   if (nid >= D.KC || pos + ln > D.VSC) {
     if (threadIdx.x == 0) {
       set_error(D, GEOBPE_ECAPACITY, -9);
-      D.st->done = 1;
+      st->done = 1;
     }
     return;
   }
   // _tokens[n] = json.loads(key): content = content(L) ++ [g] ++ content(R)
   for (int64_t i = threadIdx.x; i < ln; i += blockDim.x)
-    D.vsym[pos + i] = i < nL ? D.vsym[D.voff[L] + i] : (i == nL ? g : D.vsym[D.voff[Rr] + i - nL - 1]);
+    D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
   __syncthreads();  // every thread has read st->K / vsym_used before they move
   if (threadIdx.x == 0) {
+    const u64 w1 = D.kh1[W], w2 = D.kh2[W];
+    const int32_t wl = D.klen[W];
+    const int64_t ny = 2 * (int64_t)wl - 1;
     D.voff[nid + 1] = pos + ln;
-    D.vh1[nid] = D.kh1[W];
-    D.vh2[nid] = D.kh2[W];
-    D.vlen[nid] = D.klen[W];
-    State* st = D.st;
+    D.vh1[nid] = w1;
+    D.vh2[nid] = w2;
+    D.vlen[nid] = wl;
     LogRec lr;
     lr.nid = nid;
-    lr.count = m;
+    lr.count = gm;
     lr.W = W;
     lr.idL = L;
     lr.g = g;
@@ -588,14 +596,12 @@ __global__ __launch_bounds__(BLOCK) void k_select_final(Dev D, int32_t nblk) {
     st->K = nid + 1;
     st->iter += 1;
     st->tag = st->iter;
+    st->skip = 0;
     st->W = W;
     st->nid = nid;
-    st->maxc = m;
+    st->maxc = gm;
     st->ncand = nc;
     st->L_ovf = st->np_ovf = st->ns_ovf = st->nL_total = 0;
-    const u64 w1 = D.kh1[W], w2 = D.kh2[W];
-    const int32_t wl = D.klen[W];
-    const int64_t ny = 2 * (int64_t)wl - 1;
     st->w1 = w1;
     st->w2 = w2;
     st->wl = wl;
@@ -646,7 +652,7 @@ __device__ inline void walk_run(const Dev& D, int32_t h, int32_t W, int32_t tag,
 // 8-slot groups and one merge region
 __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
   __shared__ int32_t s_n;
-  if (D.st->done) return;
+  if (D.st->done || D.st->skip) return;
   const int32_t W = D.st->W, tag = D.st->tag;
   const uint32_t fW = (uint32_t)D.st->wfp;
   if (threadIdx.x == 0) s_n = 0;
@@ -778,7 +784,7 @@ __global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
   __shared__ Agg agg;
   __shared__ int32_t s_np, s_ns;
   __shared__ int32_t s_off[RPB + 1];
-  if (D.st->done) return;
+  if (D.st->done || D.st->skip) return;
   agg_init(agg);
   const State* st = D.st;
   ApplyCtx A;
@@ -935,9 +941,10 @@ __global__ __launch_bounds__(BLOCK) void k_compare(Dev D) {
 }
 
 // debug: device key-string order of n (a, b) key pairs (tests the JSON generator)
-__global__ void k_debug_key_less(Dev D, const int32_t* pairs, int32_t* out, int32_t n) {
+__global__ __launch_bounds__(256) void k_debug_key_less(Dev D, const int32_t* pairs, int32_t* out, int32_t n) {
+  __shared__ char s_jbuf[48 * 256];
   const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = key_less(D, pairs[2 * i], pairs[2 * i + 1]) ? 1 : 0;
+  if (i < n) out[i] = key_less(D, pairs[2 * i], pairs[2 * i + 1], s_jbuf + 48 * threadIdx.x) ? 1 : 0;
 }
 
 }  // namespace gb

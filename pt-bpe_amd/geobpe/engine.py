@@ -315,9 +315,10 @@ class GeoBPEEngine:
         return n
 
     # ------------------------------------------------------------ profiling
-    def set_profiling(self, on: bool = True, only: str = ""):
+    def set_profiling(self, on: bool = True, only: str = "", stride: int = 1):
+        """HIP-event timing of the named kernels ("" = all), every ``stride``-th launch."""
         self._chk(self.L.geobpe_set_profiling_filter(self._ctx, only.encode()))
-        self._chk(self.L.geobpe_set_profiling(self._ctx, 1 if on else 0))
+        self._chk(self.L.geobpe_set_profiling(self._ctx, max(1, int(stride)) if on else 0))
 
     def kernel_ms(self, name: str):
         n = ctypes.c_int64(0)
