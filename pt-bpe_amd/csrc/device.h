@@ -50,6 +50,7 @@ struct State {
   int32_t skip;       // this iteration only rebuilds the hot list (no merge)
   int32_t theta_new;  // threshold of that rebuild
   int64_t nskip;      // rebuild iterations so far (stats)
+  int64_t nunchecked; // found-key records beyond the check regions (not verified)
 };
 
 struct LEntry {  // one merge: left token a (+ its prev p), right token b (+ next c)
@@ -118,6 +119,8 @@ struct Dev {
   int32_t* npcnt;
   NewPair* npovf;
   NewSlot* ns;  // keys claimed per apply region (dense ids given at region close)
+  NewPair* chk;     // per apply workgroup: keys found in the last merge (EHASH check)
+  int32_t* chkcnt;
   int64_t* chunk;  // per apply workgroup: [next, end) of its reserved dense-id chunk
   int64_t ovf_cap;
   // argmax

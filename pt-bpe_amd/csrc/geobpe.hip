@@ -230,12 +230,9 @@ void enqueue_select(geobpe_ctx* c) {
   hipLaunchKernelGGL(k_select, dim3(1), dim3(BLOCK), 0, c->stream, c->D);
 }
 
-void enqueue_commit(geobpe_ctx* c, bool to_delta, bool merge_iter) {
-  {
-    Timed t(c, "finalize");
-    hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, to_delta ? 1 : 0,
-                       merge_iter ? 1 : 0);
-  }
+void enqueue_commit(geobpe_ctx* c, bool to_delta) {
+  Timed t(c, "finalize");
+  hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, to_delta ? 1 : 0);
 }
 
 void enqueue_apply(geobpe_ctx* c) {
@@ -247,7 +244,6 @@ void enqueue_apply(geobpe_ctx* c) {
     Timed t(c, "apply");
     hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0);
   }
-  enqueue_commit(c, c->distributed, true);
 }
 
 }  // namespace
@@ -335,7 +331,8 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   if ((rc = dalloc(c, &D.L, (int64_t)c->nb * D.LC)) || (rc = dalloc(c, &D.Lcnt, c->nb, 0)) ||
       (rc = dalloc(c, &D.Lovf, D.Lovf_cap)) || (rc = dalloc(c, &D.np, (int64_t)c->nba * D.RC)) ||
       (rc = dalloc(c, &D.npcnt, c->nba, 0)) || (rc = dalloc(c, &D.npovf, D.ovf_cap)) ||
-      (rc = dalloc(c, &D.ns, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chunk, 2 * (int64_t)c->nba, 0)))
+      (rc = dalloc(c, &D.ns, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chunk, 2 * (int64_t)c->nba, 0)) ||
+      (rc = dalloc(c, &D.chk, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chkcnt, c->nba, 0)))
     return rc;
   const int need[6] = {GEOBPE_COL_PHI, GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_TAU, GEOBPE_COL_CAC1N,
                        GEOBPE_COL_C1NCA};
@@ -516,7 +513,7 @@ int geobpe_bin(geobpe_ctx* c) {
     hipLaunchKernelGGL(k_pairs_all, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D);
   }
   HIPCHK(c, hipGetLastError());
-  enqueue_commit(c, c->distributed, false);
+  enqueue_commit(c, c->distributed);
   HIPCHK(c, hipGetLastError());
   return sync_state(c);
 }
@@ -530,7 +527,7 @@ int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {
     HIPCHK(c, hipGetLastError());
     if ((rc = sync_state(c))) return rc;
     if (c->h_state->done || !c->h_state->skip) break;
-    enqueue_commit(c, false, true);  // hot-list rebuild (rank-local, same decision on every rank)
+    enqueue_apply(c);  // a hot-list rebuild iteration (rank-local, same decision on every rank)
   }
   if (c->h_state->done) {
     *new_id = -1;
@@ -652,7 +649,7 @@ int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
     if ((rc = reset_region_counters(c))) return rc;
     hipLaunchKernelGGL(k_import, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, (const DeltaRec*)d_in + off, n);
     HIPCHK(c, hipGetLastError());
-    enqueue_commit(c, false, false);
+    enqueue_commit(c, false);
   }
   return sync_state(c);
 }

@@ -275,9 +275,9 @@ __device__ inline void finalize_one(const Dev& D, Agg& agg, HotApp& hot, const N
   agg_add_hot(agg, D, hot, d, e.delta, to_delta, th);
 }
 
-// a hot-list rebuild iteration (k_select set st->skip): clist = every key with
-// count >= theta_new.  Two coalesced passes over this workgroup's key range; one
-// global reservation per workgroup.
+// a hot-list rebuild iteration (k_select set st->skip; run by k_apply's grid):
+// clist = every key with count >= theta_new.  Two coalesced passes over this
+// workgroup's key range; one global reservation per workgroup.
 __device__ void rebuild_hot_list(const Dev& D) {
   __shared__ int32_t s_red[BLOCK / 64];
   __shared__ int64_t s_base;
@@ -301,29 +301,13 @@ __device__ void rebuild_hot_list(const Dev& D) {
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_finalize(Dev D, int to_delta, int merge_iter) {
+// after BPE.bin / a delta import: pk + counts of the emitted pairs
+__global__ __launch_bounds__(BLOCK) void k_finalize(Dev D, int to_delta) {
   __shared__ Agg agg;
   __shared__ HotApp hot;
-  if (merge_iter && D.st->done) return;
-  if (merge_iter && D.st->skip) {
-    rebuild_hot_list(D);
-    return;
-  }
   const int32_t th = D.st->theta;
   agg_init(agg);
   hot_init(hot);
-  if (merge_iter && blockIdx.x == 0) {  // merges applied this iteration -> merge log
-    __shared__ int32_t s_red[BLOCK / 64];
-    int32_t nm = 0;
-    const int4* l4 = reinterpret_cast<const int4*>(D.Lcnt);  // NB % 4 == 0
-    for (int32_t i = threadIdx.x; i < D.NB / 4; i += blockDim.x) {
-      const int4 v = l4[i];
-      nm += v.x + v.y + v.z + v.w;
-    }
-    int32_t tot;
-    block_excl_scan(nm, &tot, s_red);
-    if (threadIdx.x == 0) D.log[D.st->iter - 1].nmerged = (int64_t)tot + min(D.st->L_ovf, D.Lovf_cap);
-  }
   const int32_t n = D.npcnt[blockIdx.x];
   const NewPair* reg = D.np + (int64_t)blockIdx.x * D.RC;
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) finalize_one(D, agg, hot, reg[i], i, to_delta != 0, th);
@@ -614,6 +598,19 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
 }
 
 // ====================================================================== merge-apply
+// EHASH check of the keys k_apply found (not claimed) in the previous merge
+// iteration: their content hashes must be the key's canonical ones
+__device__ inline void check_found(const Dev& D) {
+  if (blockIdx.x >= D.NBA) return;
+  const int32_t n = D.chkcnt[blockIdx.x];
+  const NewPair* reg = D.chk + (int64_t)blockIdx.x * D.RC;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const NewPair e = reg[i];
+    const int32_t d = e.target;
+    if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) set_error(D, GEOBPE_EHASH, i);
+  }
+}
+
 // walk one maximal run of winner matches starting at token h: greedy left to
 // right (bpe.py:1888-1916) -- merge h, skip the next pair, merge the one after
 // if the run continues, ...
@@ -652,6 +649,7 @@ __device__ inline void walk_run(const Dev& D, int32_t h, int32_t W, int32_t tag,
 // 8-slot groups and one merge region
 __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
   __shared__ int32_t s_n;
+  check_found(D);
   if (D.st->done || D.st->skip) return;
   const int32_t W = D.st->W, tag = D.st->tag;
   const uint32_t fW = (uint32_t)D.st->wfp;
@@ -689,15 +687,92 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
 }
 
 // rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014).
-// Latency-bound: every independent load is issued before any store.
+// Latency-bound: every independent load is issued before any store.  New pair
+// keys get their dense id here (a fresh key: from this workgroup's id chunk,
+// published in ht_dense with an agent-scope store; a key claimed by another
+// workgroup in this launch: spin on that store), so pk and the counts are final
+// when the kernel ends -- no separate finalize launch in the merge loop.
 struct ApplyCtx {
-  int32_t W, nid, wl, tagL, tagR;
+  int32_t W, nid, wl, tagL, tagR, theta;
   u64 w1, w2;
   u64 pwL1a, pwL1b, pwL2a, pwL2b;  // powers for "X ++ g ++ W" (W on the right)
   bool to_delta;
 };
 
-__device__ inline void apply_one(const Dev& D, Agg& agg, int32_t* s_np, int32_t* s_ns, const LEntry e,
+struct WgIds {  // this workgroup's dense-id chunk [next, end) (LDS)
+  int64_t next, end;
+};
+
+__device__ inline int64_t take_id(const Dev& D, WgIds& ids) {
+  const int64_t j = (int64_t)atomicAdd((unsigned long long*)&ids.next, 1ULL);
+  if (j < ids.end) return j;
+  return (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL);  // chunk exhausted
+}
+
+// record of a key found (not claimed) in this launch: k_mark of the next
+// iteration checks it against the key's canonical hashes (EHASH)
+__device__ inline void emit_check(const Dev& D, int32_t* s_np, int32_t d, int32_t len, u64 h1, u64 h2) {
+  NewPair e;
+  e.target = d;
+  e.slot = -1;
+  e.len = len;
+  e.delta = 0;
+  e.h1 = h1;
+  e.h2 = h2;
+  const int32_t j = atomicAdd(s_np, 1);
+  if (j < D.RC)
+    D.chk[(int64_t)blockIdx.x * D.RC + j] = e;
+  else
+    atomicAdd((unsigned long long*)&D.st->nunchecked, 1ULL);
+}
+
+__device__ inline int32_t key_id_now(const Dev& D, WgIds& ids, int32_t* s_chk, u64 k, u64 s, u64 cur, u64 h1, u64 h2,
+                                     int32_t len, int32_t idL, int32_t g, int32_t idR) {
+  bool claimed;
+  const int32_t slot = ht_resolve(D, k, s, cur, &claimed);
+  if (slot < 0) return -1;
+  int64_t id = -1;
+  if (claimed) {
+    id = take_id(D, ids);
+    if (id >= D.UC) {
+      set_error(D, GEOBPE_ECAPACITY, -5);
+      id = 0;  // still published below: other threads may be waiting on this slot
+    } else {
+      D.kh1[id] = h1;
+      D.kh2[id] = h2;
+      D.klen[id] = len;
+      D.krep[3 * id + 0] = idL;
+      D.krep[3 * id + 1] = g;
+      D.krep[3 * id + 2] = idR;
+    }
+  }
+  // One loop for the claimer's publication and the waiters' polling: a lane of
+  // the same wave may be waiting on this lane's claim, so the publishing store
+  // must not sit in a separate region the compiler could schedule after the
+  // polling loop (pub changes inside the loop, so it cannot be unswitched).
+  bool pub = claimed;
+  int32_t d = -1;
+  for (int32_t spin = 0;; spin++) {
+    if (pub) {
+      __hip_atomic_store(&D.ht_dense[slot], (int32_t)id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      d = (int32_t)id;
+      pub = false;
+    } else if (spin == 0) {
+      d = D.ht_dense[slot];  // ids are written once: a stale read can only be -1
+    } else {
+      d = __hip_atomic_load(&D.ht_dense[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (d >= 0) break;
+    if (spin > (1 << 20)) {  // never published: a failed claim elsewhere
+      set_error(D, GEOBPE_ECAPACITY, -11);
+      return -1;
+    }
+  }
+  if (!claimed) emit_check(D, s_chk, d, len, h1, h2);
+  return d;
+}
+
+__device__ inline void apply_one(const Dev& D, Agg& agg, HotApp& hot, WgIds& ids, int32_t* s_chk, const LEntry e,
                                  const ApplyCtx& A) {
   const bool hasP = e.p >= 0, hasC = e.c >= 0;
   // round 1: everything that depends only on the entry
@@ -749,8 +824,8 @@ __device__ inline void apply_one(const Dev& D, Agg& agg, int32_t* s_np, int32_t*
   }
   // count deltas: step 4 (right neighbour pair) and step 3 (left neighbour pair);
   // step 1 (the merged pair, -1 on W) is counted once per workgroup by the caller
-  if (pkb >= 0) agg_add(agg, D, pkb, -1, A.to_delta);
-  if (pN) agg_add(agg, D, pkp, -1, A.to_delta);
+  if (pkb >= 0) agg_add_hot(agg, D, hot, pkb, -1, A.to_delta, A.theta);
+  if (pN) agg_add_hot(agg, D, hot, pkp, -1, A.to_delta, A.theta);
   // step 2: bond_to_token / token_pos
   D.tid[e.a] = A.nid;
   D.tlen[e.a] = A.wl;
@@ -758,21 +833,21 @@ __device__ inline void apply_one(const Dev& D, Agg& agg, int32_t* s_np, int32_t*
   D.pk[e.b] = -1;
   D.fp[e.b] = 0xFFFF;
   if (hasC) D.tprev[e.c] = e.a;
-  // step 5: the new neighbour pairs
+  // step 5: the new neighbour pairs (dense ids now; pk + counts final)
   if (pN) {
-    bool claimed;
-    const int32_t slot = ht_resolve(D, kL, sL, cLv, &claimed);
-    if (slot >= 0) {
-      if (claimed) emit_slot(D, s_ns, slot, ll + A.wl, L, glL, A.nid, hL1, hL2);
-      emit_pair(D, s_np, e.p, slot, ll + A.wl, 1, hL1, hL2);
+    const int32_t d = key_id_now(D, ids, s_chk, kL, sL, cLv, hL1, hL2, ll + A.wl, L, glL, A.nid);
+    if (d >= 0) {
+      D.pk[e.p] = d;
+      D.fp[e.p] = key_fp(d);
+      agg_add_hot(agg, D, hot, d, 1, A.to_delta, A.theta);
     }
   }
   if (hasC) {
-    bool claimed;
-    const int32_t slot = ht_resolve(D, kR, sR, cRv, &claimed);
-    if (slot >= 0) {
-      if (claimed) emit_slot(D, s_ns, slot, A.wl + rl, A.nid, glR, idr, hR1, hR2);
-      emit_pair(D, s_np, e.a, slot, A.wl + rl, 1, hR1, hR2);
+    const int32_t d = key_id_now(D, ids, s_chk, kR, sR, cRv, hR1, hR2, A.wl + rl, A.nid, glR, idr);
+    if (d >= 0) {
+      D.pk[e.a] = d;
+      D.fp[e.a] = key_fp(d);
+      agg_add_hot(agg, D, hot, d, 1, A.to_delta, A.theta);
     }
   } else {
     D.pk[e.a] = -1;
@@ -782,17 +857,26 @@ __device__ inline void apply_one(const Dev& D, Agg& agg, int32_t* s_np, int32_t*
 
 __global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
   __shared__ Agg agg;
-  __shared__ int32_t s_np, s_ns;
+  __shared__ HotApp hot;
+  __shared__ WgIds ids;
+  __shared__ int32_t s_chk;
   __shared__ int32_t s_off[RPB + 1];
-  if (D.st->done || D.st->skip) return;
+  __shared__ int32_t s_red[BLOCK / 64];
+  if (D.st->done) return;
+  if (D.st->skip) {
+    rebuild_hot_list(D);
+    return;
+  }
   agg_init(agg);
-  const State* st = D.st;
+  hot_init(hot);
+  State* st = D.st;
   ApplyCtx A;
   A.W = st->W;
   A.nid = st->nid;
   const int32_t tag = st->tag;
   A.tagR = (tag << 2) | 2;
   A.tagL = (tag << 2) | 1;
+  A.theta = st->theta;
   A.to_delta = to_delta != 0;
   A.w1 = st->w1;
   A.w2 = st->w2;
@@ -808,7 +892,17 @@ __global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
     if (threadIdx.x < RPB) s_off[threadIdx.x] = ex;
     if (threadIdx.x == 0) {
       s_off[RPB] = tot;
-      s_np = s_ns = 0;
+      s_chk = 0;
+      ids.next = D.chunk[2 * blockIdx.x];
+      ids.end = D.chunk[2 * blockIdx.x + 1];
+    }
+  }
+  int32_t nm = 0;
+  if (blockIdx.x == 0) {  // merges applied this iteration -> merge log
+    const int4* l4 = reinterpret_cast<const int4*>(D.Lcnt);  // NB % 4 == 0
+    for (int32_t i = threadIdx.x; i < D.NB / 4; i += blockDim.x) {
+      const int4 v = l4[i];
+      nm += v.x + v.y + v.z + v.w;
     }
   }
   __syncthreads();
@@ -817,16 +911,31 @@ __global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
     int r = 0;
     while (j >= s_off[r + 1]) r++;
     const LEntry e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + (j - s_off[r])];
-    apply_one(D, agg, &s_np, &s_ns, e, A);
+    apply_one(D, agg, hot, ids, &s_chk, e, A);
   }
   const int64_t novf = min(st->L_ovf, D.Lovf_cap);
   for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x) {
-    apply_one(D, agg, &s_np, &s_ns, D.Lovf[k], A);
-    agg_add(agg, D, A.W, -1, A.to_delta);  // step 1 for an overflow entry
+    apply_one(D, agg, hot, ids, &s_chk, D.Lovf[k], A);
+    agg_add_hot(agg, D, hot, A.W, -1, A.to_delta, A.theta);  // step 1 for an overflow entry
   }
-  agg_flush(agg, D, A.to_delta);
-  if (threadIdx.x == 0 && E) global_add(D, A.W, -E, A.to_delta);  // step 1 for the region entries
-  close_regions(D, &s_np, &s_ns);
+  agg_flush_hot(agg, D, hot, A.to_delta, A.theta);  // (syncs the workgroup first)
+  if (threadIdx.x == 0) {
+    if (E) global_add(D, A.W, -E, A.to_delta);  // step 1 for the region entries
+    D.chkcnt[blockIdx.x] = min(s_chk, (int32_t)D.RC);
+    int64_t nx = ids.next, en = ids.end;
+    if (nx >= en) {  // chunk used up: reserve the next one, sized by this launch's demand
+      const int64_t sz = max((int64_t)ID_CHUNK, 2 * (nx - en + ID_CHUNK));
+      nx = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
+      en = nx + sz;
+    }
+    D.chunk[2 * blockIdx.x] = nx;
+    D.chunk[2 * blockIdx.x + 1] = en;
+  }
+  if (blockIdx.x == 0) {
+    int32_t tot;
+    block_excl_scan(nm, &tot, s_red);
+    if (threadIdx.x == 0) D.log[st->iter - 1].nmerged = (int64_t)tot + min(st->L_ovf, D.Lovf_cap);
+  }
 }
 
 // ====================================================================== multi-rank deltas
