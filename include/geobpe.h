@@ -145,6 +145,10 @@ int64_t geobpe_verify_counts(geobpe_ctx *ctx);
  * launch; on = k > 1: every k-th launch of each kernel (sampling keeps the event
  * packets from stretching the stream they measure). */
 int geobpe_set_profiling(geobpe_ctx *ctx, int on);
+/* Debug: per-workgroup phase timestamps (wall clock, 100 MHz) of k_apply.
+ * on = 1 enables and clears (returns the slot count); on = 0 copies up to cap
+ * stamps to h_out and disables. */
+int64_t geobpe_debug_timeline(geobpe_ctx *ctx, int on, int64_t *h_out, int64_t cap);
 /* Restrict the timing to a comma-separated list of kernel names ("" = all). */
 int geobpe_set_profiling_filter(geobpe_ctx *ctx, const char *names);
 double geobpe_kernel_ms(geobpe_ctx *ctx, const char *name, int64_t *launches);

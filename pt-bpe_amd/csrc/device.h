@@ -17,10 +17,13 @@ constexpr u64 HP2 = 0x13579BDF2468ACE1ULL % M61;
 constexpr u64 KMIX = 0x9E3779B97F4A7C15ULL;
 constexpr double TWO_PI = 6.283185307179586;  // 2*np.pi
 constexpr int BLOCK = 256;
-constexpr int AGG = 512;       // LDS partial-count slots per workgroup
-constexpr int AGG_SHIFT = 23;  // 32 - log2(AGG)
+constexpr int ABLOCK = 1024;  // region kernels (bin pairs, finalize, apply, import): 16 waves per CU
 constexpr int RPB = 8;         // mark regions per apply workgroup (NB = RPB * NBA)
 constexpr int CL_MIN_SHRINK = 4096;  // hot-list length above which a 4x drop of theta re-scans
+constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per region)
+constexpr int NBKT = 1 << NBKT_LOG2;
+constexpr int SKIP_HOT = 1, SKIP_POST = 2;  // what a rebuild iteration rebuilds
+constexpr int DBG_SLOTS = 64;
 constexpr int ID_CHUNK = 256;  // dense ids a workgroup reserves at a time
 
 // ------------------------------------------------------------------ records
@@ -51,6 +54,10 @@ struct State {
   int32_t theta_new;  // threshold of that rebuild
   int64_t nskip;      // rebuild iterations so far (stats)
   int64_t nunchecked; // found-key records beyond the check regions (not verified)
+  // posting index (k_mark): bucket-sorted (key, slot) per region + the log of
+  // pairs made since its last rebuild
+  int32_t post_valid, plog_ovf;
+  int64_t plog_total, npost;
 };
 
 struct LEntry {  // one merge: left token a (+ its prev p), right token b (+ next c)
@@ -121,6 +128,15 @@ struct Dev {
   NewSlot* ns;  // keys claimed per apply region (dense ids given at region close)
   NewPair* chk;     // per apply workgroup: keys found in the last merge (EHASH check)
   int32_t* chkcnt;
+  // posting index: region r = residue slots [r*PR, (r+1)*PR), one per apply workgroup
+  int2* post;       // (key, slot) of every live pair at the last rebuild, bucket-sorted per region
+  int32_t* poff;    // [NBA][NBKT+1] bucket offsets within a region
+  int64_t PR;
+  int2* plog;       // per apply workgroup: (key, slot) of the pairs it made since the rebuild
+  int32_t* plogn;
+  int64_t PLC, LOGMAX;
+  // optional phase timeline (geobpe_debug_timeline): DBG_SLOTS wall-clock stamps per workgroup
+  int64_t* dbg;
   int64_t* chunk;  // per apply workgroup: [next, end) of its reserved dense-id chunk
   int64_t ovf_cap;
   // argmax
@@ -253,6 +269,13 @@ __device__ inline int32_t block_excl_scan(int32_t v, int32_t* total, int32_t* sc
   return base + ex;
 }
 
+// phase stamp for the debug timeline (no-op unless enabled)
+__device__ inline void dbg_stamp(const Dev& D, int k) {
+  if (D.dbg && threadIdx.x == 0 && k < DBG_SLOTS) D.dbg[(int64_t)blockIdx.x * DBG_SLOTS + k] = (int64_t)wall_clock64();
+}
+
+__device__ inline uint32_t post_bkt(int32_t d) { return ((uint32_t)d * 2654435761u) >> (32 - NBKT_LOG2); }
+
 __device__ inline uint16_t key_fp(int32_t d) { return (uint16_t)((uint32_t)d % 65535u); }
 
 // count update target: global counts, or the rank-local delta + touched list
@@ -270,41 +293,55 @@ __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_de
 }
 
 // LDS-staged per-workgroup partial counts, flushed with one global atomic per
-// distinct key per workgroup
-struct Agg {
-  int32_t key[AGG];
-  int32_t val[AGG];
+// distinct key per workgroup (open addressing, 8 probes, then straight to global)
+template <int LOG2>
+struct AggT {
+  static constexpr int N = 1 << LOG2;
+  int32_t key[N];
+  int32_t val[N];
+  __device__ static uint32_t slot(int32_t d) { return ((uint32_t)d * 2654435761u) >> (32 - LOG2); }
 };
-__device__ inline void agg_init(Agg& s) {
-  for (int i = threadIdx.x; i < AGG; i += blockDim.x) {
+using Agg = AggT<9>;      // 4 KB: recount
+using AggBig = AggT<13>;  // 64 KB: bin / merge-apply / import (early merges touch ~10^4 keys per workgroup)
+
+template <class A>
+__device__ inline void agg_init(A& s) {
+  for (int i = threadIdx.x; i < A::N; i += blockDim.x) {
     s.key[i] = -1;
     s.val[i] = 0;
   }
   __syncthreads();
 }
-__device__ inline void agg_add(Agg& s, const Dev& D, int32_t d, int32_t v, bool to_delta) {
-  uint32_t h = ((uint32_t)d * 2654435761u) >> AGG_SHIFT;
+// true if staged in LDS
+template <class A>
+__device__ inline bool agg_stage(A& s, int32_t d, int32_t v) {
+  uint32_t h = A::slot(d);
 #pragma unroll 1
   for (int probe = 0; probe < 8; probe++) {
     const int32_t k = s.key[h];
     if (k == d) {
       atomicAdd(&s.val[h], v);
-      return;
+      return true;
     }
     if (k == -1) {
       const int32_t old = atomicCAS(&s.key[h], -1, d);
       if (old == -1 || old == d) {
         atomicAdd(&s.val[h], v);
-        return;
+        return true;
       }
     }
-    h = (h + 1) & (AGG - 1);
+    h = (h + 1) & (A::N - 1);
   }
-  global_add(D, d, v, to_delta);
+  return false;
 }
-__device__ inline void agg_flush(Agg& s, const Dev& D, bool to_delta) {
+template <class A>
+__device__ inline void agg_add(A& s, const Dev& D, int32_t d, int32_t v, bool to_delta) {
+  if (!agg_stage(s, d, v)) global_add(D, d, v, to_delta);
+}
+template <class A>
+__device__ inline void agg_flush(A& s, const Dev& D, bool to_delta) {
   __syncthreads();
-  for (int i = threadIdx.x; i < AGG; i += blockDim.x) {
+  for (int i = threadIdx.x; i < A::N; i += blockDim.x) {
     const int32_t k = s.key[i];
     if (k >= 0 && s.val[i] != 0) global_add(D, k, s.val[i], to_delta);
   }
@@ -350,32 +387,18 @@ __device__ inline void count_add_hot(const Dev& D, HotApp& h, int32_t d, int32_t
     atomicAdd(&D.count[d], v);
   }
 }
-__device__ inline void agg_add_hot(Agg& s, const Dev& D, HotApp& h, int32_t d, int32_t v, bool to_delta, int32_t th) {
-  uint32_t hh = ((uint32_t)d * 2654435761u) >> AGG_SHIFT;
-#pragma unroll 1
-  for (int probe = 0; probe < 8; probe++) {
-    const int32_t k = s.key[hh];
-    if (k == d) {
-      atomicAdd(&s.val[hh], v);
-      return;
-    }
-    if (k == -1) {
-      const int32_t old = atomicCAS(&s.key[hh], -1, d);
-      if (old == -1 || old == d) {
-        atomicAdd(&s.val[hh], v);
-        return;
-      }
-    }
-    hh = (hh + 1) & (AGG - 1);
-  }
+template <class A>
+__device__ inline void agg_add_hot(A& s, const Dev& D, HotApp& h, int32_t d, int32_t v, bool to_delta, int32_t th) {
+  if (agg_stage(s, d, v)) return;
   if (to_delta)
     global_add(D, d, v, true);
   else
     count_add_hot(D, h, d, v, th);
 }
-__device__ inline void agg_flush_hot(Agg& s, const Dev& D, HotApp& h, bool to_delta, int32_t th) {
+template <class A>
+__device__ inline void agg_flush_hot(A& s, const Dev& D, HotApp& h, bool to_delta, int32_t th) {
   __syncthreads();
-  for (int i = threadIdx.x; i < AGG; i += blockDim.x) {
+  for (int i = threadIdx.x; i < A::N; i += blockDim.x) {
     const int32_t k = s.key[i];
     if (k < 0 || s.val[i] == 0) continue;
     if (to_delta)
@@ -393,6 +416,10 @@ __device__ inline u64 ht_first_slot(const Dev& D, u64 k) { return (k * 0xD6E8FEB
 __device__ inline int32_t ht_resolve(const Dev& D, u64 k, u64 s, u64 cur, bool* claimed) {
   const u64 mask = (u64)D.HC - 1;
   *claimed = false;
+  // keep cur an opaque register value: otherwise the loop's phi of (cur, table
+  // load) can be folded into a load through a phi of pointers -- a flat load
+  // via the scratch stack when cur came from a caller's struct
+  asm volatile("" : "+v"(cur));
   for (int64_t probe = 0; probe < D.HC; probe++) {
     if (cur == k) return (int32_t)s;
     if (cur == 0) {

@@ -232,7 +232,7 @@ void enqueue_select(geobpe_ctx* c) {
 
 void enqueue_commit(geobpe_ctx* c, bool to_delta) {
   Timed t(c, "finalize");
-  hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, to_delta ? 1 : 0);
+  hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, to_delta ? 1 : 0);
 }
 
 void enqueue_apply(geobpe_ctx* c) {
@@ -242,7 +242,7 @@ void enqueue_apply(geobpe_ctx* c) {
   }
   {
     Timed t(c, "apply");
-    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0);
+    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0);
   }
 }
 
@@ -333,6 +333,14 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
       (rc = dalloc(c, &D.npcnt, c->nba, 0)) || (rc = dalloc(c, &D.npovf, D.ovf_cap)) ||
       (rc = dalloc(c, &D.ns, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chunk, 2 * (int64_t)c->nba, 0)) ||
       (rc = dalloc(c, &D.chk, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chkcnt, c->nba, 0)))
+    return rc;
+  // posting index: one residue region per apply workgroup; the log holds the pairs
+  // made since the last rebuild (k_select rebuilds when it passes LOGMAX)
+  D.PR = (c->R + c->nba - 1) / c->nba;
+  D.LOGMAX = std::max<int64_t>((int64_t)c->nba * 64, c->R / 32);
+  D.PLC = 4 * D.LOGMAX / c->nba + 64;
+  if ((rc = dalloc(c, &D.post, (int64_t)c->nba * D.PR)) || (rc = dalloc(c, &D.poff, (int64_t)c->nba * (NBKT + 1), 0)) ||
+      (rc = dalloc(c, &D.plog, (int64_t)c->nba * D.PLC)) || (rc = dalloc(c, &D.plogn, c->nba, 0)))
     return rc;
   const int need[6] = {GEOBPE_COL_PHI, GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_TAU, GEOBPE_COL_CAC1N,
                        GEOBPE_COL_C1NCA};
@@ -510,7 +518,7 @@ int geobpe_bin(geobpe_ctx* c) {
   if ((rc = reset_region_counters(c))) return rc;
   {
     Timed t(c, "pair_count");
-    hipLaunchKernelGGL(k_pairs_all, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D);
+    hipLaunchKernelGGL(k_pairs_all, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D);
   }
   HIPCHK(c, hipGetLastError());
   enqueue_commit(c, c->distributed);
@@ -647,7 +655,7 @@ int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
   for (int64_t off = 0; off < n_records; off += chunk) {
     const int64_t n = std::min(chunk, n_records - off);
     if ((rc = reset_region_counters(c))) return rc;
-    hipLaunchKernelGGL(k_import, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, (const DeltaRec*)d_in + off, n);
+    hipLaunchKernelGGL(k_import, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, (const DeltaRec*)d_in + off, n);
     HIPCHK(c, hipGetLastError());
     enqueue_commit(c, false);
   }
@@ -775,6 +783,22 @@ int64_t geobpe_verify_counts(geobpe_ctx* c) {
   hipLaunchKernelGGL(k_compare, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
   if (sync_state(c)) return -1;
   return c->h_state->nmismatch;
+}
+
+int64_t geobpe_debug_timeline(geobpe_ctx* c, int on, int64_t* h_out, int64_t cap) {
+  if (!c) return -1;
+  if (hipSetDevice(c->device) != hipSuccess) return -1;
+  const int64_t n = (int64_t)c->nb * DBG_SLOTS;
+  if (on) {
+    if (!c->D.dbg && dalloc(c, &c->D.dbg, n)) return -1;
+    hipMemsetAsync(c->D.dbg, 0, n * 8, c->stream);
+    return n;
+  }
+  if (!c->D.dbg) return 0;
+  hipStreamSynchronize(c->stream);
+  if (h_out && cap > 0) hipMemcpy(h_out, c->D.dbg, std::min(cap, n) * 8, hipMemcpyDeviceToHost);
+  c->D.dbg = nullptr;  // (the buffer stays allocated until destroy)
+  return n;
 }
 
 int geobpe_debug_key_less(geobpe_ctx* c, const int32_t* h_pairs, int32_t n, int32_t* h_out) {

@@ -238,7 +238,7 @@ __device__ inline void close_regions(const Dev& D, int32_t* s_np, int32_t* s_ns)
 
 // ====================================================================== histogram
 // BPE.bin (bpe.py:1431-1474): every live adjacent pair -> content hash -> key
-__global__ __launch_bounds__(BLOCK) void k_pairs_all(Dev D) {
+__global__ __launch_bounds__(ABLOCK) void k_pairs_all(Dev D) {
   __shared__ int32_t s_np, s_ns;
   if (threadIdx.x == 0) s_np = s_ns = 0;
   __syncthreads();
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(BLOCK) void k_pairs_all(Dev D) {
 
 // pair -> dense key id into pk, counts via LDS-staged partial counts (+ the
 // hot-list crossing check on the global counts)
-__device__ inline void finalize_one(const Dev& D, Agg& agg, HotApp& hot, const NewPair& e, int64_t j, bool to_delta,
+__device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, const NewPair& e, int64_t j, bool to_delta,
                                     int32_t th) {
   const int32_t d = D.ht_dense[e.slot];
   if (d < 0 || D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) {
@@ -279,22 +279,35 @@ __device__ inline void finalize_one(const Dev& D, Agg& agg, HotApp& hot, const N
 // clist = every key with count >= theta_new.  Two coalesced passes over this
 // workgroup's key range; one global reservation per workgroup.
 __device__ void rebuild_hot_list(const Dev& D) {
-  __shared__ int32_t s_red[BLOCK / 64];
+  __shared__ int32_t s_red[ABLOCK / 64];
   __shared__ int64_t s_base;
   State* st = D.st;
   const int32_t th = st->theta_new;
   const int64_t U = st->U;
   const int64_t per = (U + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
+  constexpr int UNR = 16;  // count loads in flight per thread
   int32_t n = 0;
-  for (int64_t d = lo + threadIdx.x; d < hi; d += BLOCK) n += D.count[d] >= th;
+  for (int64_t d = lo + threadIdx.x; d < hi; d += UNR * ABLOCK) {
+    int32_t c[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) c[u] = d + u * ABLOCK < hi ? D.count[d + u * ABLOCK] : 0;
+#pragma unroll
+    for (int u = 0; u < UNR; u++) n += c[u] >= th;
+  }
   int32_t tot;
   const int32_t ex = block_excl_scan(n, &tot, s_red);
   if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&st->ncl, (unsigned long long)tot) : 0;
   __syncthreads();
   int64_t j = s_base + ex;
-  for (int64_t d = lo + threadIdx.x; d < hi; d += BLOCK)
-    if (D.count[d] >= th) D.clist[j++] = (int32_t)d;  // j < U <= UC
+  for (int64_t d = lo + threadIdx.x; d < hi; d += UNR * ABLOCK) {
+    int32_t c[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) c[u] = d + u * ABLOCK < hi ? D.count[d + u * ABLOCK] : 0;
+#pragma unroll
+    for (int u = 0; u < UNR; u++)
+      if (c[u] >= th) D.clist[j++] = (int32_t)(d + u * ABLOCK);  // j < U <= UC
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->theta = th;
     st->cl_valid = 1;
@@ -302,8 +315,63 @@ __device__ void rebuild_hot_list(const Dev& D) {
 }
 
 // after BPE.bin / a delta import: pk + counts of the emitted pairs
-__global__ __launch_bounds__(BLOCK) void k_finalize(Dev D, int to_delta) {
-  __shared__ Agg agg;
+// posting-index rebuild (a rebuild iteration, run by k_apply's grid): workgroup r
+// counting-sorts the live pairs of residue region r by key bucket (LDS
+// histogram -> scan -> scatter), writes its bucket offsets and empties its log.
+// No cross-workgroup step: k_mark looks a bucket up in every region.
+__device__ void rebuild_postings(const Dev& D, int32_t* hist) {
+  __shared__ int32_t s_red[ABLOCK / 64];
+  constexpr int PER = NBKT / ABLOCK;
+  const int64_t r = blockIdx.x;
+  const int64_t g0 = r * D.PR, g1 = min(D.R, g0 + D.PR);
+  constexpr int UNR = 16;  // pk loads in flight per thread (the passes are latency-bound otherwise)
+  for (int i = threadIdx.x; i < NBKT; i += ABLOCK) hist[i] = 0;
+  __syncthreads();
+  for (int64_t g = g0 + threadIdx.x; g < g1; g += UNR * ABLOCK) {
+    int32_t d[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) d[u] = g + u * ABLOCK < g1 ? D.pk[g + u * ABLOCK] : -1;
+#pragma unroll
+    for (int u = 0; u < UNR; u++)
+      if (d[u] >= 0) atomicAdd(&hist[post_bkt(d[u])], 1);
+  }
+  __syncthreads();
+  int32_t sum = 0;
+  for (int k = 0; k < PER; k++) sum += hist[threadIdx.x * PER + k];
+  int32_t tot;
+  int32_t run = block_excl_scan(sum, &tot, s_red);
+  int32_t* off = D.poff + r * (NBKT + 1);
+  __syncthreads();
+  for (int k = 0; k < PER; k++) {
+    const int b = threadIdx.x * PER + k;
+    const int32_t c = hist[b];
+    hist[b] = run;
+    off[b] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) off[NBKT] = tot;
+  __syncthreads();
+  int2* out = D.post + r * D.PR;
+  for (int64_t g = g0 + threadIdx.x; g < g1; g += UNR * ABLOCK) {
+    int32_t d[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) d[u] = g + u * ABLOCK < g1 ? D.pk[g + u * ABLOCK] : -1;
+#pragma unroll
+    for (int u = 0; u < UNR; u++)
+      if (d[u] >= 0) out[atomicAdd(&hist[post_bkt(d[u])], 1)] = make_int2(d[u], (int32_t)(g + u * ABLOCK));
+  }
+  if (threadIdx.x == 0) D.plogn[r] = 0;
+  if (r == 0 && threadIdx.x == 0) {
+    State* st = D.st;
+    st->post_valid = 1;
+    st->plog_ovf = 0;
+    st->plog_total = 0;
+    st->npost += 1;
+  }
+}
+
+__global__ __launch_bounds__(ABLOCK) void k_finalize(Dev D, int to_delta) {
+  __shared__ AggBig agg;
   __shared__ HotApp hot;
   const int32_t th = D.st->theta;
   agg_init(agg);
@@ -488,18 +556,27 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
     }
   }
   const int32_t gm = block_max(m, s_red);
-  if (!valid || gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th)) {
+  const bool hot = !valid || gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th);
+  if (hot && valid && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
     if (threadIdx.x == 0) {
-      if (valid && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
-        st->done = 1;
-        st->maxc = 0;
-      } else {
-        st->skip = 1;
+      st->done = 1;
+      st->maxc = 0;
+    }
+    return;
+  }
+  // posting index stale (log full / overflowed / never built) and the merges are
+  // small enough that a rebuild lasts >= 64 iterations: rebuild it this iteration
+  const bool post = !hot && (st->post_valid == 0 || st->plog_ovf != 0 || st->plog_total > D.LOGMAX) &&
+                    (int64_t)gm * 64 <= D.LOGMAX;
+  if (hot || post) {
+    if (threadIdx.x == 0) {
+      if (hot) {
         st->theta_new = max(1, gm / 2);
         st->ncl = 0;
         st->cl_valid = 0;
-        st->nskip += 1;
       }
+      st->skip = (hot ? SKIP_HOT : 0) | (post ? SKIP_POST : 0);
+      st->nskip += 1;
     }
     return;
   }
@@ -600,10 +677,9 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
 // ====================================================================== merge-apply
 // EHASH check of the keys k_apply found (not claimed) in the previous merge
 // iteration: their content hashes must be the key's canonical ones
-__device__ inline void check_found(const Dev& D) {
-  if (blockIdx.x >= D.NBA) return;
-  const int32_t n = D.chkcnt[blockIdx.x];
-  const NewPair* reg = D.chk + (int64_t)blockIdx.x * D.RC;
+__device__ inline void check_found(const Dev& D, int32_t r) {
+  const int32_t n = D.chkcnt[r];
+  const NewPair* reg = D.chk + (int64_t)r * D.RC;
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
     const NewPair e = reg[i];
     const int32_t d = e.target;
@@ -644,17 +720,54 @@ __device__ inline void walk_run(const Dev& D, int32_t h, int32_t W, int32_t tag,
   }
 }
 
-// scan the 16-bit key fingerprints for the winner (4 x 16 B per lane in flight),
-// confirm on pk, start a walk at every run start; each workgroup owns CH8
-// 8-slot groups and one merge region
+// find the winner's occurrences and start a walk at every run start.  Posting
+// mode (index valid): O(bucket + log) reads.  Otherwise scan the 16-bit key
+// fingerprints (4 x 16 B per lane in flight; each workgroup owns CH8 8-slot
+// groups), confirm on pk.  Either way one merge region per workgroup.
 __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
   __shared__ int32_t s_n;
-  check_found(D);
-  if (D.st->done || D.st->skip) return;
+  const bool posting = D.st->post_valid && !D.st->plog_ovf;
+  if (!posting && blockIdx.x < D.NBA) check_found(D, blockIdx.x);
+  if (D.st->done || D.st->skip) {
+    if (posting && blockIdx.x % RPB == RPB - 1) check_found(D, blockIdx.x / RPB);
+    return;
+  }
   const int32_t W = D.st->W, tag = D.st->tag;
   const uint32_t fW = (uint32_t)D.st->wfp;
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
+  if (posting) {
+    // posting mode: the winner's bucket in region r (bucket-sorted at the last
+    // rebuild) + region r's log, split over RPB-1 workgroups of the region; the
+    // last one checks the hashes of the keys found in the previous merge
+    const int32_t r = blockIdx.x / RPB, q = blockIdx.x % RPB;
+    if (q == RPB - 1) {
+      check_found(D, r);
+      if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = 0;
+      return;
+    }
+    const int32_t* off = D.poff + (int64_t)r * (NBKT + 1);
+    const uint32_t b = post_bkt(W);
+    const int32_t lo = off[b], n1 = off[b + 1] - lo;
+    const int32_t ntot = n1 + D.plogn[r];
+    const int32_t per = (ntot + RPB - 2) / (RPB - 1);
+    const int32_t i1 = min(ntot, (q + 1) * per);
+    const int2* P = D.post + (int64_t)r * D.PR + lo;
+    const int2* Lg = D.plog + (int64_t)r * D.PLC - n1;
+    for (int32_t i = q * per + threadIdx.x; i < i1; i += BLOCK) {
+      const int2 e = i < n1 ? P[i] : Lg[i];
+      if (e.x == W) {
+        const int32_t g = e.y;
+        if (D.pk[g] == W) {
+          const int32_t p = D.tprev[g];
+          if (p < 0 || D.pk[p] != W) walk_run(D, g, W, tag, &s_n);
+        }
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = min(s_n, (int32_t)D.LC);
+    return;
+  }
   const int64_t n8 = (D.R + 7) / 8;
   const int64_t lo = (int64_t)blockIdx.x * D.CH8, hi = min(n8, lo + D.CH8);
   const uint4* f4 = reinterpret_cast<const uint4*>(D.fp);
@@ -702,6 +815,19 @@ struct ApplyCtx {
 struct WgIds {  // this workgroup's dense-id chunk [next, end) (LDS)
   int64_t next, end;
 };
+struct WgLog {  // this workgroup's posting log cursor (LDS)
+  int32_t n0, n, ovf;
+};
+
+// a pair made in this merge joins the posting log (k_mark finds it there until
+// the next posting rebuild)
+__device__ inline void log_pair(const Dev& D, WgLog& lg, int32_t d, int32_t slot) {
+  const int32_t j = atomicAdd(&lg.n, 1);
+  if (j < D.PLC)
+    D.plog[(int64_t)blockIdx.x * D.PLC + j] = make_int2(d, slot);
+  else
+    lg.ovf = 1;
+}
 
 __device__ inline int64_t take_id(const Dev& D, WgIds& ids) {
   const int64_t j = (int64_t)atomicAdd((unsigned long long*)&ids.next, 1ULL);
@@ -760,6 +886,7 @@ __device__ inline int32_t key_id_now(const Dev& D, WgIds& ids, int32_t* s_chk, u
     } else if (spin == 0) {
       d = D.ht_dense[slot];  // ids are written once: a stale read can only be -1
     } else {
+      __builtin_amdgcn_s_sleep(2);
       d = __hip_atomic_load(&D.ht_dense[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (d >= 0) break;
@@ -772,8 +899,54 @@ __device__ inline int32_t key_id_now(const Dev& D, WgIds& ids, int32_t* s_chk, u
   return d;
 }
 
-__device__ inline void apply_one(const Dev& D, Agg& agg, HotApp& hot, WgIds& ids, int32_t* s_chk, const LEntry e,
-                                 const ApplyCtx& A) {
+// per-workgroup key cache (LDS): the occurrences a workgroup handles often make
+// the same new pair key; one thread (the resolver) goes to the global table, the
+// others take its dense id from LDS after the round's barrier -- the global CAS /
+// polling traffic per key is one per workgroup, not one per occurrence
+constexpr int KC_SZ = 2048;
+struct KeyCache {
+  u64 key[KC_SZ];
+  u64 h1[KC_SZ];
+  int32_t id[KC_SZ];  // -2: the resolver failed (error already set)
+};
+__device__ inline void kc_init(KeyCache& kc) {
+  for (int i = threadIdx.x; i < KC_SZ; i += blockDim.x) kc.key[i] = 0;
+}
+// slot of k in the cache (*res: this thread inserted it), -1 if the cache is full there
+__device__ inline int32_t kc_find(KeyCache& kc, u64 k, bool* res) {
+  int32_t h = (int32_t)((k * 0x9E3779B97F4A7C15ULL) >> 53);  // log2(KC_SZ) bits
+#pragma unroll 1
+  for (int probe = 0; probe < 16; probe++, h = (h + 1) & (KC_SZ - 1)) {
+    const u64 c = kc.key[h];
+    if (c == k) {
+      *res = false;
+      return h;
+    }
+    if (c == 0) {
+      const u64 old = atomicCAS((unsigned long long*)&kc.key[h], 0ULL, (unsigned long long)k);
+      if (old == 0 || old == k) {
+        *res = old == 0;
+        return h;
+      }
+    }
+  }
+  *res = true;
+  return -1;
+}
+
+// one new neighbour pair of a merged occurrence, between its key computation
+// and its dense id
+struct Half {
+  u64 k, s, cur, h1, h2;
+  int32_t len, idL, g, idR, target, kcs, d;
+  bool res;
+};
+
+// rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014)
+// up to the keys of its new neighbour pairs (step 5 finishes in k_apply).
+// Latency-bound: every independent load is issued before any store.
+__device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const LEntry e, const ApplyCtx& A, Half& hl,
+                                   bool& vl, Half& hr, bool& vr, int dk) {
   const bool hasP = e.p >= 0, hasC = e.c >= 0;
   // round 1: everything that depends only on the entry
   const int32_t pkb = D.pk[e.b];
@@ -788,18 +961,16 @@ __device__ inline void apply_one(const Dev& D, Agg& agg, HotApp& hot, WgIds& ids
   const bool cL = hasC && rc == A.tagL;
   const int32_t idr = cL ? A.nid : tc;
   // round 2: vocab hashes of the neighbours
-  u64 l1 = 0, l2 = 0, r1 = A.w1, r2 = A.w2;
-  int32_t ll = 0, rl = A.wl;
-  if (pN) {
-    l1 = D.vh1[L];
-    l2 = D.vh2[L];
-    ll = D.vlen[L];
-  }
-  if (hasC && !cL) {
-    r1 = D.vh1[idr];
-    r2 = D.vh2[idr];
-    rl = D.vlen[idr];
-  }
+  // (loads from valid addresses, then selects by value: a conditional load with
+  // a fallback in ApplyCtx would become a flat load through the scratch stack)
+  const bool rN = hasC && !cL;
+  const int32_t iL = pN ? L : 0, iR = rN ? idr : 0;
+  const u64 vl1 = D.vh1[iL], vl2 = D.vh2[iL], vr1 = D.vh1[iR], vr2 = D.vh2[iR];
+  const int32_t vll = D.vlen[iL], vrl = D.vlen[iR];
+  const u64 l1 = vl1, l2 = vl2;
+  const int32_t ll = vll;
+  const u64 r1 = rN ? vr1 : A.w1, r2 = rN ? vr2 : A.w2;
+  const int32_t rl = rN ? vrl : A.wl;
   u64 pr1a = 0, pr1b = 0, pr2a = 0, pr2b = 0;
   if (hasC) {
     const int64_t ny = 2 * (int64_t)rl - 1;
@@ -809,66 +980,114 @@ __device__ inline void apply_one(const Dev& D, Agg& agg, HotApp& hot, WgIds& ids
     pr2b = D.pw2[ny];
   }
   // new pair keys and their first table probes (issued together)
-  u64 hL1 = 0, hL2 = 0, hR1 = 0, hR2 = 0, kL = 0, kR = 0, sL = 0, sR = 0, cLv = 0, cRv = 0;
+  vl = pN;
+  vr = hasC;
   if (pN) {
-    combine_pw(l1, l2, glL, A.w1, A.w2, A.pwL1a, A.pwL1b, A.pwL2a, A.pwL2b, hL1, hL2);
-    kL = probe_key(hL1, hL2, ll + A.wl);
-    sL = ht_first_slot(D, kL);
-    cLv = D.ht_key[sL];
+    combine_pw(l1, l2, glL, A.w1, A.w2, A.pwL1a, A.pwL1b, A.pwL2a, A.pwL2b, hl.h1, hl.h2);
+    hl.len = ll + A.wl;
+    hl.k = probe_key(hl.h1, hl.h2, hl.len);
+    hl.s = ht_first_slot(D, hl.k);
+    hl.cur = D.ht_key[hl.s];
+    hl.idL = L;
+    hl.g = glL;
+    hl.idR = A.nid;
+    hl.target = e.p;
   }
   if (hasC) {
-    combine_pw(A.w1, A.w2, glR, r1, r2, pr1a, pr1b, pr2a, pr2b, hR1, hR2);
-    kR = probe_key(hR1, hR2, A.wl + rl);
-    sR = ht_first_slot(D, kR);
-    cRv = D.ht_key[sR];
+    combine_pw(A.w1, A.w2, glR, r1, r2, pr1a, pr1b, pr2a, pr2b, hr.h1, hr.h2);
+    hr.len = A.wl + rl;
+    hr.k = probe_key(hr.h1, hr.h2, hr.len);
+    hr.s = ht_first_slot(D, hr.k);
+    hr.cur = D.ht_key[hr.s];
+    hr.idL = A.nid;
+    hr.g = glR;
+    hr.idR = idr;
+    hr.target = e.a;
   }
   // count deltas: step 4 (right neighbour pair) and step 3 (left neighbour pair);
   // step 1 (the merged pair, -1 on W) is counted once per workgroup by the caller
+  if (dk >= 0) dbg_stamp(D, dk);
   if (pkb >= 0) agg_add_hot(agg, D, hot, pkb, -1, A.to_delta, A.theta);
   if (pN) agg_add_hot(agg, D, hot, pkp, -1, A.to_delta, A.theta);
+  if (dk >= 0) dbg_stamp(D, dk + 1);
   // step 2: bond_to_token / token_pos
   D.tid[e.a] = A.nid;
   D.tlen[e.a] = A.wl;
   D.tid[e.b] = -1;
   D.pk[e.b] = -1;
   D.fp[e.b] = 0xFFFF;
-  if (hasC) D.tprev[e.c] = e.a;
-  // step 5: the new neighbour pairs (dense ids now; pk + counts final)
-  if (pN) {
-    const int32_t d = key_id_now(D, ids, s_chk, kL, sL, cLv, hL1, hL2, ll + A.wl, L, glL, A.nid);
-    if (d >= 0) {
-      D.pk[e.p] = d;
-      D.fp[e.p] = key_fp(d);
-      agg_add_hot(agg, D, hot, d, 1, A.to_delta, A.theta);
-    }
-  }
   if (hasC) {
-    const int32_t d = key_id_now(D, ids, s_chk, kR, sR, cRv, hR1, hR2, A.wl + rl, A.nid, glR, idr);
-    if (d >= 0) {
-      D.pk[e.a] = d;
-      D.fp[e.a] = key_fp(d);
-      agg_add_hot(agg, D, hot, d, 1, A.to_delta, A.theta);
-    }
+    D.tprev[e.c] = e.a;
   } else {
     D.pk[e.a] = -1;
     D.fp[e.a] = 0xFFFF;
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
-  __shared__ Agg agg;
+// before the round's barrier: look the key up in the workgroup cache; the
+// resolver (or an uncached thread) gets the dense id from the global table
+__device__ inline void half_resolve(const Dev& D, KeyCache& kc, WgIds& ids, int32_t* s_chk, Half& x) {
+  x.kcs = kc_find(kc, x.k, &x.res);
+  x.d = -1;
+  if (!x.res) return;
+  x.d = key_id_now(D, ids, s_chk, x.k, x.s, x.cur, x.h1, x.h2, x.len, x.idL, x.g, x.idR);
+  if (x.kcs >= 0) {
+    kc.h1[x.kcs] = x.h1;
+    kc.id[x.kcs] = x.d >= 0 ? x.d : -2;
+  }
+}
+
+// after the barrier: followers read the id; then pk / counts / posting log
+__device__ inline void half_finish(const Dev& D, AggBig& agg, HotApp& hot, KeyCache& kc, WgLog& lg, Half& x,
+                                   const ApplyCtx& A, int dk) {
+  if (!x.res) {
+    x.d = kc.id[x.kcs];
+    if (x.d >= 0 && kc.h1[x.kcs] != x.h1) {  // same probe key, other content
+      set_error(D, GEOBPE_EHASH, -13);
+      x.d = -1;
+    }
+  }
+  if (x.d < 0) return;
+  if (dk >= 0) dbg_stamp(D, dk);
+  D.pk[x.target] = x.d;
+  D.fp[x.target] = key_fp(x.d);
+  log_pair(D, lg, x.d, x.target);
+  if (dk >= 0) dbg_stamp(D, dk + 1);
+  agg_add_hot(agg, D, hot, x.d, 1, A.to_delta, A.theta);
+  if (dk >= 0) dbg_stamp(D, dk + 2);
+}
+
+// BPE.step's merge-apply (bpe.py:1888-2014) for this workgroup's RPB mark
+// regions (+ its share of the overflow list), in block-uniform rounds: front
+// half, key resolution, barrier, finish.  Also the merge log's n_merged, and
+// the rebuild iterations (hot list / posting index) k_select requests.
+__global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
+  // the posting rebuild's histogram and the merge's partial counts never live in
+  // the same launch: one 64 KB LDS buffer
+  __shared__ union {
+    AggBig agg;
+    int32_t hist[NBKT];
+  } u;
+  static_assert(sizeof(AggBig) == sizeof(int32_t) * NBKT, "LDS union layout");
+  AggBig& agg = u.agg;
   __shared__ HotApp hot;
   __shared__ WgIds ids;
+  __shared__ WgLog lg;
+  __shared__ KeyCache kc;
   __shared__ int32_t s_chk;
   __shared__ int32_t s_off[RPB + 1];
-  __shared__ int32_t s_red[BLOCK / 64];
+  __shared__ int32_t s_red[ABLOCK / 64];
   if (D.st->done) return;
   if (D.st->skip) {
-    rebuild_hot_list(D);
+    const int32_t sk = D.st->skip;
+    if (sk & SKIP_HOT) rebuild_hot_list(D);
+    if (sk & SKIP_POST) rebuild_postings(D, u.hist);
     return;
   }
+  dbg_stamp(D, 0);
   agg_init(agg);
   hot_init(hot);
+  kc_init(kc);
   State* st = D.st;
   ApplyCtx A;
   A.W = st->W;
@@ -895,6 +1114,8 @@ __global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
       s_chk = 0;
       ids.next = D.chunk[2 * blockIdx.x];
       ids.end = D.chunk[2 * blockIdx.x + 1];
+      lg.n0 = lg.n = D.plogn[blockIdx.x];
+      lg.ovf = 0;
     }
   }
   int32_t nm = 0;
@@ -907,21 +1128,57 @@ __global__ __launch_bounds__(BLOCK) void k_apply(Dev D, int to_delta) {
   }
   __syncthreads();
   const int32_t E = s_off[RPB];
-  for (int32_t j = threadIdx.x; j < E; j += blockDim.x) {
-    int r = 0;
-    while (j >= s_off[r + 1]) r++;
-    const LEntry e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + (j - s_off[r])];
-    apply_one(D, agg, hot, ids, &s_chk, e, A);
-  }
   const int64_t novf = min(st->L_ovf, D.Lovf_cap);
-  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < novf; k += (int64_t)gridDim.x * blockDim.x) {
-    apply_one(D, agg, hot, ids, &s_chk, D.Lovf[k], A);
-    agg_add_hot(agg, D, hot, A.W, -1, A.to_delta, A.theta);  // step 1 for an overflow entry
+  const int64_t oper = (novf + gridDim.x - 1) / gridDim.x;
+  const int64_t o_lo = (int64_t)blockIdx.x * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
+  const int64_t total = E + o_n;
+  // at most two new keys per merge: make the id chunk that large now, with one
+  // global reservation (refilling claim by claim would serialise every
+  // workgroup on one returning atomic)
+  if (threadIdx.x == 0 && ids.end - ids.next < 2 * total) {
+    const int64_t sz = max((int64_t)ID_CHUNK, 2 * total);
+    ids.next = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
+    ids.end = ids.next + sz;
   }
+  __syncthreads();
+  dbg_stamp(D, 1);
+  int dbk = 2;
+  for (int64_t j0 = 0; j0 < total; j0 += blockDim.x) {
+    const int64_t j = j0 + threadIdx.x;
+    Half hl, hr;
+    bool vl = false, vr = false;
+    if (j < total) {
+      LEntry e;
+      if (j < E) {
+        int r = 0;
+        while (j >= s_off[r + 1]) r++;
+        e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + (j - s_off[r])];
+      } else {
+        e = D.Lovf[o_lo + (j - E)];
+        agg_add_hot(agg, D, hot, A.W, -1, A.to_delta, A.theta);  // step 1 for an overflow entry
+      }
+      apply_front(D, agg, hot, e, A, hl, vl, hr, vr, j0 < 2 * ABLOCK ? 40 + 10 * (int)(j0 / ABLOCK) : -1);
+    }
+    dbg_stamp(D, dbk++);
+    if (vl) half_resolve(D, kc, ids, &s_chk, hl);
+    if (vr) half_resolve(D, kc, ids, &s_chk, hr);
+    dbg_stamp(D, dbk++);
+    __syncthreads();
+    dbg_stamp(D, dbk++);
+    if (vl) half_finish(D, agg, hot, kc, lg, hl, A, j0 < 2 * ABLOCK ? 42 + 10 * (int)(j0 / ABLOCK) : -1);
+    if (vr) half_finish(D, agg, hot, kc, lg, hr, A, j0 < 2 * ABLOCK ? 45 + 10 * (int)(j0 / ABLOCK) : -1);
+    dbg_stamp(D, dbk++);
+  }
+  dbg_stamp(D, 60);
   agg_flush_hot(agg, D, hot, A.to_delta, A.theta);  // (syncs the workgroup first)
+  dbg_stamp(D, 61);
   if (threadIdx.x == 0) {
     if (E) global_add(D, A.W, -E, A.to_delta);  // step 1 for the region entries
     D.chkcnt[blockIdx.x] = min(s_chk, (int32_t)D.RC);
+    const int32_t ln = min(lg.n, (int32_t)D.PLC);
+    D.plogn[blockIdx.x] = ln;
+    if (ln > lg.n0) atomicAdd((unsigned long long*)&st->plog_total, (unsigned long long)(ln - lg.n0));
+    if (lg.ovf) st->plog_ovf = 1;
     int64_t nx = ids.next, en = ids.end;
     if (nx >= en) {  // chunk used up: reserve the next one, sized by this launch's demand
       const int64_t sz = max((int64_t)ID_CHUNK, 2 * (nx - en + ID_CHUNK));
@@ -956,7 +1213,7 @@ __global__ __launch_bounds__(BLOCK) void k_export(Dev D, DeltaRec* out, int64_t 
   }
 }
 
-__global__ __launch_bounds__(BLOCK) void k_import(Dev D, const DeltaRec* in, int64_t n) {
+__global__ __launch_bounds__(ABLOCK) void k_import(Dev D, const DeltaRec* in, int64_t n) {
   __shared__ int32_t s_np, s_ns;
   if (threadIdx.x == 0) s_np = s_ns = 0;
   __syncthreads();
@@ -1019,27 +1276,10 @@ __global__ __launch_bounds__(BLOCK) void k_recount(Dev D) {
   agg_init(agg);
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = D.pk[g];
-    if (d < 0) continue;
-    uint32_t h = ((uint32_t)d * 2654435761u) >> AGG_SHIFT;
-    bool done = false;
-    for (int probe = 0; probe < 8 && !done; probe++) {
-      const int32_t k = agg.key[h];
-      if (k == d) {
-        atomicAdd(&agg.val[h], 1);
-        done = true;
-      } else if (k == -1) {
-        const int32_t old = atomicCAS(&agg.key[h], -1, d);
-        if (old == -1 || old == d) {
-          atomicAdd(&agg.val[h], 1);
-          done = true;
-        }
-      }
-      h = (h + 1) & (AGG - 1);
-    }
-    if (!done) atomicAdd(&D.scratch[d], 1);
+    if (d >= 0 && !agg_stage(agg, d, 1)) atomicAdd(&D.scratch[d], 1);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < AGG; i += blockDim.x)
+  for (int i = threadIdx.x; i < Agg::N; i += blockDim.x)
     if (agg.key[i] >= 0) atomicAdd(&D.scratch[agg.key[i]], agg.val[i]);
 }
 

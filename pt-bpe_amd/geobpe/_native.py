@@ -74,6 +74,7 @@ def lib():
         "geobpe_segmentation": (I64, [P, P, P, P]),
         "geobpe_encode": (I64, [P, P, P]),
         "geobpe_verify_counts": (I64, [P]),
+        "geobpe_debug_timeline": (I64, [P, ctypes.c_int, P, I64]),
         "geobpe_set_profiling": (ctypes.c_int, [P, ctypes.c_int]),
         "geobpe_kernel_ms": (D, [P, ctypes.c_char_p, pI64]),
         "geobpe_set_profiling_filter": (ctypes.c_int, [P, ctypes.c_char_p]),
@@ -94,7 +95,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
-    "geobpe_verify_counts", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_synchronize",
+    "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_synchronize",
 ]
 
 

@@ -1,0 +1,50 @@
+"""Phase timeline of k_apply for a few early merges on the C3 corpus
+(geobpe_debug_timeline): per-workgroup wall-clock stamps (100 MHz)."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "pt-bpe_amd"))
+import torch  # noqa: E402,F401
+from geobpe import _native, synth  # noqa: E402
+from geobpe.engine import GeoBPEEngine  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+iters = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,2,3,20,200,800").split(",")]
+corpus = synth.make_corpus(synth.make_lengths(n, 40, 560, seed=0), seed=0)
+eng = GeoBPEEngine(corpus, 5).initialize()
+eng.bin()
+L = _native.lib()
+done = 0
+for it in iters:
+    eng.run(it - done - 1)
+    done = it - 1
+    m = L.geobpe_debug_timeline(eng._ctx, 1, None, 0)
+    eng.run(1)
+    done += 1
+    buf = np.zeros(m, dtype=np.int64)
+    L.geobpe_debug_timeline(eng._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p), m)
+    t = buf.reshape(-1, 64)
+    t = t[t[:, 0] > 0]
+    if len(t) == 0:
+        print(f"merge {it}: (rebuild iteration / no stamps)")
+        continue
+    base = t[:, 0].min()
+    rel = (t - base) / 100.0  # us
+    rel[t == 0] = np.nan
+    last = eng.merges[-1]
+    print(f"merge {it}: count {last[1]} merged {last[2]}  workgroups {len(t)}")
+    names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end"}
+    for r in range(2):
+        for i, nm in enumerate(["front.loads", "front.agg", "finL.kc", "finL.store", "finL.agg", "finR.kc",
+                                "finR.store", "finR.agg"]):
+            names[40 + 10 * r + i] = f"r{r}.{nm}"
+    for k in sorted(range(62), key=lambda k: np.nanmedian(rel[:, k]) if not np.all(np.isnan(rel[:, k])) else 0):
+        col = rel[:, k]
+        if np.all(np.isnan(col)):
+            continue
+        name = names.get(k, f"r{(k - 2) // 4}." + ["front", "resolve", "barrier", "finish"][(k - 2) % 4])
+        print(f"  {name:14s} min {np.nanmin(col):8.1f}  med {np.nanmedian(col):8.1f}  max {np.nanmax(col):8.1f}")
+eng.close()
