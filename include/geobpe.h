@@ -120,9 +120,9 @@ int64_t geobpe_key_json(geobpe_ctx *ctx, int32_t d, char *buf, int64_t cap);
 /* Device ordering of reference key strings: h_out[i] = key(h_pairs[2i]) <
  * key(h_pairs[2i+1]) for dense key ids (tests the device tie-break). */
 int geobpe_debug_key_less(geobpe_ctx *ctx, const int32_t *h_pairs, int32_t n, int32_t *h_out);
-/* Global pair counts by dense key id (ids of unused chunk tails read 0);
- * returns U, copies at most cap. */
-int64_t geobpe_debug_counts(geobpe_ctx *ctx, int32_t *h_counts, int64_t cap);
+/* Every key (id = key-table slot, in claim order) and its global pair count;
+ * returns the number of keys U, copies at most cap of each. */
+int64_t geobpe_debug_counts(geobpe_ctx *ctx, int32_t *h_keys, int32_t *h_counts, int64_t cap);
 /* Debug record of dense key d: idL, g, idR, len, count, U, K(device), K(host), h1. */
 int geobpe_debug_key(geobpe_ctx *ctx, int32_t d, int64_t *h_out9);
 /* Content (residue / junction symbols, 2*nres-1 values) of vocab id v. */

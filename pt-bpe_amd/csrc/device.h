@@ -24,12 +24,11 @@ constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per re
 constexpr int NBKT = 1 << NBKT_LOG2;
 constexpr int SKIP_HOT = 1, SKIP_POST = 2;  // what a rebuild iteration rebuilds
 constexpr int DBG_SLOTS = 64;
-constexpr int ID_CHUNK = 256;  // dense ids a workgroup reserves at a time
 
 // ------------------------------------------------------------------ records
 struct State {
   // persistent
-  int64_t U;          // dense keys allocated
+  int64_t U;          // keys listed in klist
   int64_t err_code;   // first error (GEOBPE_E*)
   int64_t err_pos;
   int64_t epoch;      // delta-touch epoch (multi-rank)
@@ -70,11 +69,6 @@ struct NewPair {
   int32_t delta;   // count contribution
   u64 h1, h2;
 };
-struct NewSlot {
-  int32_t slot, len;
-  int32_t idL, g, idR, pad;
-  u64 h1, h2;
-};
 struct DeltaRec {  // 40 bytes, exchanged between ranks
   u64 h1, h2;
   int32_t len, idL, g, idR, delta, pad;
@@ -105,13 +99,12 @@ struct Dev {
   int64_t pwn;
   // key table
   u64* ht_key;
-  int32_t* ht_dense;
   int64_t HC;
   int32_t ht_shift, pad1;
   // dense keys
   u64 *kh1, *kh2;
   int32_t *klen, *krep, *count, *dcount, *touch, *touched, *scratch;
-  int64_t UC;
+  int64_t KCAP;     // klist capacity (keys)
   // per-workgroup output regions (no global returning atomics on the hot path)
   int32_t NB;       // mark workgroups (one merge region each)
   int32_t NBA;      // apply / finalize / bin / import workgroups (one pair region each), NB = RPB*NBA
@@ -125,7 +118,8 @@ struct Dev {
   NewPair* np;
   int32_t* npcnt;
   NewPair* npovf;
-  NewSlot* ns;  // keys claimed per apply region (dense ids given at region close)
+  int32_t* ns;  // per region workgroup: slots it claimed (listed in klist at region close)
+  int32_t* klist;  // every key id (= key-table slot), in claim order: U entries
   NewPair* chk;     // per apply workgroup: keys found in the last merge (EHASH check)
   int32_t* chkcnt;
   // posting index: region r = residue slots [r*PR, (r+1)*PR), one per apply workgroup
@@ -137,10 +131,9 @@ struct Dev {
   int64_t PLC, LOGMAX;
   // optional phase timeline (geobpe_debug_timeline): DBG_SLOTS wall-clock stamps per workgroup
   int64_t* dbg;
-  int64_t* chunk;  // per apply workgroup: [next, end) of its reserved dense-id chunk
   int64_t ovf_cap;
   // argmax
-  int32_t* clist;  // hot list (capacity UC)
+  int32_t* clist;  // hot list (capacity KCAP)
   int32_t* cand;   // tied keys of the current maximum
   int64_t candcap;
   LogRec* log;
@@ -358,7 +351,7 @@ __device__ inline void hot_init(HotApp& h) {
   if (threadIdx.x == 0) h.n = 0;
 }
 __device__ inline void hot_store(const Dev& D, int64_t k, int32_t d) {
-  if (k < D.UC)
+  if (k < D.KCAP)
     D.clist[k] = d;
   else
     D.st->cl_valid = 0;  // list lost an entry: the next k_select rebuilds it

@@ -200,26 +200,27 @@ int alloc_keys(geobpe_ctx* c) {
   if (c->keys_ready) return 0;
   Dev& D = c->D;
   const int64_t base = c->distributed && c->global_residues > c->R ? c->global_residues : c->R;
-  D.UC = 3 * base + 65536 + (int64_t)c->nba * ID_CHUNK;  // + the unused chunk tails
+  D.KCAP = 3 * base + 65536;  // keys: bin pairs + at most two new pairs per merge
   int64_t hc = 1 << 16;
-  while (hc < 2 * D.UC) hc <<= 1;
+  while (hc < 2 * D.KCAP) hc <<= 1;
   D.HC = hc;
   int sh = 0;
   while ((1LL << sh) < hc) sh++;
   D.ht_shift = 64 - sh;
   int rc;
-  if ((rc = dalloc(c, &D.ht_key, D.HC, 0)) || (rc = dalloc(c, &D.ht_dense, D.HC, 0xFF)) ||
-      (rc = dalloc(c, &D.kh1, D.UC)) || (rc = dalloc(c, &D.kh2, D.UC)) || (rc = dalloc(c, &D.klen, D.UC)) ||
-      (rc = dalloc(c, &D.krep, 3 * D.UC, 0xFF)) || (rc = dalloc(c, &D.count, D.UC + 16, 0)) ||
-      (rc = dalloc(c, &D.scratch, D.UC + 16, 0)))
+  // key arrays are indexed by the key id = key-table slot
+  if ((rc = dalloc(c, &D.ht_key, D.HC, 0)) || (rc = dalloc(c, &D.kh1, D.HC)) || (rc = dalloc(c, &D.kh2, D.HC)) ||
+      (rc = dalloc(c, &D.klen, D.HC)) || (rc = dalloc(c, &D.krep, 3 * D.HC, 0xFF)) ||
+      (rc = dalloc(c, &D.count, D.HC + 16, 0)) || (rc = dalloc(c, &D.scratch, D.HC + 16, 0)) ||
+      (rc = dalloc(c, &D.klist, D.KCAP, 0xFF)))
     return rc;
   if (c->distributed) {
-    if ((rc = dalloc(c, &D.dcount, D.UC, 0)) || (rc = dalloc(c, &D.touch, D.UC, 0xFF)) ||
-        (rc = dalloc(c, &D.touched, D.UC)))
+    if ((rc = dalloc(c, &D.dcount, D.HC, 0)) || (rc = dalloc(c, &D.touch, D.HC, 0xFF)) ||
+        (rc = dalloc(c, &D.touched, D.KCAP)))
       return rc;
   }
   D.candcap = 1 << 20;
-  if ((rc = dalloc(c, &D.clist, D.UC)) || (rc = dalloc(c, &D.cand, D.candcap))) return rc;
+  if ((rc = dalloc(c, &D.clist, D.KCAP)) || (rc = dalloc(c, &D.cand, D.candcap))) return rc;
   c->keys_ready = true;
   return 0;
 }
@@ -331,7 +332,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   if ((rc = dalloc(c, &D.L, (int64_t)c->nb * D.LC)) || (rc = dalloc(c, &D.Lcnt, c->nb, 0)) ||
       (rc = dalloc(c, &D.Lovf, D.Lovf_cap)) || (rc = dalloc(c, &D.np, (int64_t)c->nba * D.RC)) ||
       (rc = dalloc(c, &D.npcnt, c->nba, 0)) || (rc = dalloc(c, &D.npovf, D.ovf_cap)) ||
-      (rc = dalloc(c, &D.ns, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chunk, 2 * (int64_t)c->nba, 0)) ||
+      (rc = dalloc(c, &D.ns, (int64_t)c->nba * D.RC)) ||
       (rc = dalloc(c, &D.chk, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chkcnt, c->nba, 0)))
     return rc;
   // posting index: one residue region per apply workgroup; the log holds the pairs
@@ -773,8 +774,7 @@ int64_t geobpe_verify_counts(geobpe_ctx* c) {
   if (!c || !c->keys_ready || c->distributed) return -1;
   hipSetDevice(c->device);
   if (sync_state(c)) return -1;
-  const int64_t U = c->h_state->U;
-  hipMemsetAsync(c->D.scratch, 0, U * 4 + 4, c->stream);
+  hipMemsetAsync(c->D.scratch, 0, c->D.HC * 4, c->stream);
   hipMemsetAsync(&c->D.st->nmismatch, 0, 8, c->stream);
   {
     Timed t(c, "recount");
@@ -820,11 +820,11 @@ int geobpe_debug_key_less(geobpe_ctx* c, const int32_t* h_pairs, int32_t n, int3
 int64_t geobpe_key_json(geobpe_ctx* c, int32_t d, char* buf, int64_t cap) {
   if (!c || !c->keys_ready || d < 0) return -1;
   if (sync_vocab(c)) return -1;
-  if (d >= c->h_state->U) return -1;
+  if (d >= c->D.HC) return -1;
   int32_t rep[3];
   if (hipMemcpy(rep, c->D.krep + 3 * (int64_t)d, sizeof rep, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   const int32_t K = (int32_t)c->vocab.size();
-  if (rep[0] < 0 || rep[0] >= K || rep[2] < 0 || rep[2] >= K) return -1;  // an unused id of a chunk tail
+  if (rep[0] < 0 || rep[0] >= K || rep[2] < 0 || rep[2] >= K) return -1;  // not a key
   std::vector<int32_t> x(c->vocab[rep[0]]);
   x.push_back(rep[1]);
   x.insert(x.end(), c->vocab[rep[2]].begin(), c->vocab[rep[2]].end());
@@ -838,13 +838,21 @@ int64_t geobpe_key_json(geobpe_ctx* c, int32_t d, char* buf, int64_t cap) {
   return (int64_t)s.size();
 }
 
-int64_t geobpe_debug_counts(geobpe_ctx* c, int32_t* h_counts, int64_t cap) {
+int64_t geobpe_debug_counts(geobpe_ctx* c, int32_t* h_keys, int32_t* h_counts, int64_t cap) {
   if (!c || !c->keys_ready) return -1;
   if (sync_state(c)) return -1;
-  const int64_t U = c->h_state->U;
-  if (h_counts && cap > 0 &&
-      hipMemcpy(h_counts, c->D.count, sizeof(int32_t) * std::min(U, cap), hipMemcpyDeviceToHost) != hipSuccess)
-    return -1;
+  const int64_t U = std::min(c->h_state->U, c->D.KCAP);
+  const int64_t n = std::min(U, cap);
+  if (h_keys && h_counts && n > 0) {
+    int32_t *dk, *dc;
+    if (hipMalloc(&dk, n * 4) != hipSuccess || hipMalloc(&dc, n * 4) != hipSuccess) return -1;
+    hipLaunchKernelGGL(k_gather_counts, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, dk, dc, n);
+    hipMemcpyAsync(h_keys, dk, n * 4, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(h_counts, dc, n * 4, hipMemcpyDeviceToHost, c->stream);
+    hipStreamSynchronize(c->stream);
+    hipFree(dk);
+    hipFree(dc);
+  }
   return U;
 }
 

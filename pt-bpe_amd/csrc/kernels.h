@@ -155,43 +155,33 @@ __device__ inline void emit_pair(const Dev& D, int32_t* s_cnt, int32_t target, i
   }
 }
 
-__device__ inline void assign_one(const Dev& D, const NewSlot& e, int64_t d) {
-  if (d >= D.UC) {
-    set_error(D, GEOBPE_ECAPACITY, -5);
-    return;
-  }
-  D.ht_dense[e.slot] = (int32_t)d;
-  D.kh1[d] = e.h1;
-  D.kh2[d] = e.h2;
-  D.klen[d] = e.len;
-  D.krep[3 * d + 0] = e.idL;
-  D.krep[3 * d + 1] = e.g;
-  D.krep[3 * d + 2] = e.idR;
-  D.count[d] = 0;
-  if (D.dcount) {
-    D.dcount[d] = 0;
-    D.touch[d] = -1;
-  }
+// A pair key is named by its key-table slot (the key id): the thread whose CAS
+// claims the slot writes the key's payload there at once and lists the slot in
+// klist; a finder has the id as soon as its probe matches -- nothing to wait for.
+__device__ inline void claim_payload(const Dev& D, int32_t slot, u64 h1, u64 h2, int32_t len, int32_t idL, int32_t g,
+                                     int32_t idR) {
+  D.kh1[slot] = h1;
+  D.kh2[slot] = h2;
+  D.klen[slot] = len;
+  D.krep[3 * (int64_t)slot + 0] = idL;
+  D.krep[3 * (int64_t)slot + 1] = g;
+  D.krep[3 * (int64_t)slot + 2] = idR;
 }
 
-__device__ inline void emit_slot(const Dev& D, int32_t* s_cnt, int32_t slot, int32_t len, int32_t idL, int32_t g,
-                                 int32_t idR, u64 h1, u64 h2) {
-  NewSlot e;
-  e.slot = slot;
-  e.len = len;
-  e.idL = idL;
-  e.g = g;
-  e.idR = idR;
-  e.pad = 0;
-  e.h1 = h1;
-  e.h2 = h2;
-  const int32_t j = atomicAdd(s_cnt, 1);
-  if (j < D.RC) {
-    D.ns[(int64_t)blockIdx.x * D.RC + j] = e;
-  } else {  // rare: a dense id of its own right away
-    const int64_t d = (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL);
-    assign_one(D, e, d);
-  }
+__device__ inline void klist_put(const Dev& D, int64_t k, int32_t slot) {
+  if (k < D.KCAP)
+    D.klist[k] = slot;
+  else
+    set_error(D, GEOBPE_ECAPACITY, -5);
+}
+
+// a claimed slot joins this workgroup's claim region (klist entries at region close)
+__device__ inline void note_claim(const Dev& D, int32_t* s_ns, int32_t slot) {
+  const int32_t j = atomicAdd(s_ns, 1);
+  if (j < D.RC)
+    D.ns[(int64_t)blockIdx.x * D.RC + j] = slot;
+  else  // rare: listed right away
+    klist_put(D, (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL), slot);
 }
 
 // insert (or find) a pair key and emit the pair
@@ -200,40 +190,27 @@ __device__ inline void add_pair(const Dev& D, int32_t* s_np, int32_t* s_ns, int3
   bool claimed;
   const int32_t slot = ht_insert(D, h1, h2, len, &claimed);
   if (slot < 0) return;
-  if (claimed) emit_slot(D, s_ns, slot, len, idL, g, idR, h1, h2);
+  if (claimed) {
+    claim_payload(D, slot, h1, h2, len, idL, g, idR);
+    note_claim(D, s_ns, slot);
+  }
   emit_pair(D, s_np, target, slot, len, delta, h1, h2);
 }
 
-// end of a region kernel: publish the pair count and give this workgroup's
-// claimed keys dense ids from its reserved chunk (a global reservation only when
-// the chunk runs out; the unused tail of a chunk stays count 0)
+// end of a region kernel: this workgroup's claimed keys join klist (one global
+// reservation); the pair count of a bin / import region is published
+__device__ inline void close_claims(const Dev& D, int32_t* s_ns) {
+  __shared__ int64_t s_base;
+  __syncthreads();
+  const int32_t n = min(*s_ns, (int32_t)D.RC);
+  if (threadIdx.x == 0) s_base = n ? (int64_t)atomicAdd((unsigned long long*)&D.st->U, (unsigned long long)n) : 0;
+  __syncthreads();
+  const int32_t* reg = D.ns + (int64_t)blockIdx.x * D.RC;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) klist_put(D, s_base + i, reg[i]);
+}
 __device__ inline void close_regions(const Dev& D, int32_t* s_np, int32_t* s_ns) {
-  __shared__ int64_t s_cur, s_n1, s_base2;
-  __syncthreads();
-  const int32_t nsz = min(*s_ns, (int32_t)D.RC);
-  if (threadIdx.x == 0) {
-    D.npcnt[blockIdx.x] = min(*s_np, (int32_t)D.RC);
-    int64_t cur = D.chunk[2 * blockIdx.x], end = D.chunk[2 * blockIdx.x + 1];
-    s_cur = cur;
-    s_n1 = nsz;
-    if (nsz > end - cur) {  // old chunk's tail first, then a fresh chunk
-      const int64_t rest = nsz - (end - cur);
-      const int64_t sz = max(rest, (int64_t)ID_CHUNK);
-      const int64_t b2 = (int64_t)atomicAdd((unsigned long long*)&D.st->U, (unsigned long long)sz);
-      s_n1 = end - cur;
-      s_base2 = b2;
-      cur = b2 + rest;
-      end = b2 + sz;
-    } else {
-      cur += nsz;
-    }
-    D.chunk[2 * blockIdx.x] = cur;
-    D.chunk[2 * blockIdx.x + 1] = end;
-  }
-  __syncthreads();
-  const NewSlot* reg = D.ns + (int64_t)blockIdx.x * D.RC;
-  for (int32_t i = threadIdx.x; i < nsz; i += blockDim.x)
-    assign_one(D, reg[i], i < s_n1 ? s_cur + i : s_base2 + (i - s_n1));
+  close_claims(D, s_ns);
+  if (threadIdx.x == 0) D.npcnt[blockIdx.x] = min(*s_np, (int32_t)D.RC);
 }
 
 // ====================================================================== histogram
@@ -259,12 +236,12 @@ __global__ __launch_bounds__(ABLOCK) void k_pairs_all(Dev D) {
   close_regions(D, &s_np, &s_ns);
 }
 
-// pair -> dense key id into pk, counts via LDS-staged partial counts (+ the
-// hot-list crossing check on the global counts)
+// pair -> key id into pk, counts via LDS-staged partial counts (+ the hot-list
+// crossing check on the global counts); the key's payload must be this content
 __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, const NewPair& e, int64_t j, bool to_delta,
                                     int32_t th) {
-  const int32_t d = D.ht_dense[e.slot];
-  if (d < 0 || D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) {
+  const int32_t d = e.slot;
+  if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) {
     set_error(D, GEOBPE_EHASH, j);
     return;
   }
@@ -277,36 +254,36 @@ __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, cons
 
 // a hot-list rebuild iteration (k_select set st->skip; run by k_apply's grid):
 // clist = every key with count >= theta_new.  Two coalesced passes over this
-// workgroup's key range; one global reservation per workgroup.
+// workgroup's share of klist; one global reservation per workgroup.
 __device__ void rebuild_hot_list(const Dev& D) {
   __shared__ int32_t s_red[ABLOCK / 64];
   __shared__ int64_t s_base;
   State* st = D.st;
   const int32_t th = st->theta_new;
-  const int64_t U = st->U;
+  const int64_t U = min(st->U, D.KCAP);
   const int64_t per = (U + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
-  constexpr int UNR = 16;  // count loads in flight per thread
+  constexpr int UNR = 16;  // loads in flight per thread
   int32_t n = 0;
-  for (int64_t d = lo + threadIdx.x; d < hi; d += UNR * ABLOCK) {
-    int32_t c[UNR];
+  for (int64_t i = lo + threadIdx.x; i < hi; i += UNR * ABLOCK) {
+    int32_t d[UNR];
 #pragma unroll
-    for (int u = 0; u < UNR; u++) c[u] = d + u * ABLOCK < hi ? D.count[d + u * ABLOCK] : 0;
+    for (int u = 0; u < UNR; u++) d[u] = i + u * ABLOCK < hi ? D.klist[i + u * ABLOCK] : -1;
 #pragma unroll
-    for (int u = 0; u < UNR; u++) n += c[u] >= th;
+    for (int u = 0; u < UNR; u++) n += d[u] >= 0 && D.count[d[u]] >= th;
   }
   int32_t tot;
   const int32_t ex = block_excl_scan(n, &tot, s_red);
   if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&st->ncl, (unsigned long long)tot) : 0;
   __syncthreads();
   int64_t j = s_base + ex;
-  for (int64_t d = lo + threadIdx.x; d < hi; d += UNR * ABLOCK) {
-    int32_t c[UNR];
+  for (int64_t i = lo + threadIdx.x; i < hi; i += UNR * ABLOCK) {
+    int32_t d[UNR];
 #pragma unroll
-    for (int u = 0; u < UNR; u++) c[u] = d + u * ABLOCK < hi ? D.count[d + u * ABLOCK] : 0;
+    for (int u = 0; u < UNR; u++) d[u] = i + u * ABLOCK < hi ? D.klist[i + u * ABLOCK] : -1;
 #pragma unroll
     for (int u = 0; u < UNR; u++)
-      if (c[u] >= th) D.clist[j++] = (int32_t)(d + u * ABLOCK);  // j < U <= UC
+      if (d[u] >= 0 && D.count[d[u]] >= th) D.clist[j++] = d[u];  // j < U <= KCAP
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->theta = th;
@@ -314,7 +291,6 @@ __device__ void rebuild_hot_list(const Dev& D) {
   }
 }
 
-// after BPE.bin / a delta import: pk + counts of the emitted pairs
 // posting-index rebuild (a rebuild iteration, run by k_apply's grid): workgroup r
 // counting-sorts the live pairs of residue region r by key bucket (LDS
 // histogram -> scan -> scatter), writes its bucket offsets and empties its log.
@@ -801,10 +777,8 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
 
 // rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014).
 // Latency-bound: every independent load is issued before any store.  New pair
-// keys get their dense id here (a fresh key: from this workgroup's id chunk,
-// published in ht_dense with an agent-scope store; a key claimed by another
-// workgroup in this launch: spin on that store), so pk and the counts are final
-// when the kernel ends -- no separate finalize launch in the merge loop.
+// keys get their id (key-table slot) here, so pk and the counts are final when the
+// kernel ends -- no separate finalize launch in the merge loop.
 struct ApplyCtx {
   int32_t W, nid, wl, tagL, tagR, theta;
   u64 w1, w2;
@@ -812,9 +786,6 @@ struct ApplyCtx {
   bool to_delta;
 };
 
-struct WgIds {  // this workgroup's dense-id chunk [next, end) (LDS)
-  int64_t next, end;
-};
 struct WgLog {  // this workgroup's posting log cursor (LDS)
   int32_t n0, n, ovf;
 };
@@ -827,12 +798,6 @@ __device__ inline void log_pair(const Dev& D, WgLog& lg, int32_t d, int32_t slot
     D.plog[(int64_t)blockIdx.x * D.PLC + j] = make_int2(d, slot);
   else
     lg.ovf = 1;
-}
-
-__device__ inline int64_t take_id(const Dev& D, WgIds& ids) {
-  const int64_t j = (int64_t)atomicAdd((unsigned long long*)&ids.next, 1ULL);
-  if (j < ids.end) return j;
-  return (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL);  // chunk exhausted
 }
 
 // record of a key found (not claimed) in this launch: k_mark of the next
@@ -852,51 +817,18 @@ __device__ inline void emit_check(const Dev& D, int32_t* s_np, int32_t d, int32_
     atomicAdd((unsigned long long*)&D.st->nunchecked, 1ULL);
 }
 
-__device__ inline int32_t key_id_now(const Dev& D, WgIds& ids, int32_t* s_chk, u64 k, u64 s, u64 cur, u64 h1, u64 h2,
+__device__ inline int32_t key_id_now(const Dev& D, int32_t* s_ns, int32_t* s_chk, u64 k, u64 s, u64 cur, u64 h1, u64 h2,
                                      int32_t len, int32_t idL, int32_t g, int32_t idR) {
   bool claimed;
   const int32_t slot = ht_resolve(D, k, s, cur, &claimed);
   if (slot < 0) return -1;
-  int64_t id = -1;
   if (claimed) {
-    id = take_id(D, ids);
-    if (id >= D.UC) {
-      set_error(D, GEOBPE_ECAPACITY, -5);
-      id = 0;  // still published below: other threads may be waiting on this slot
-    } else {
-      D.kh1[id] = h1;
-      D.kh2[id] = h2;
-      D.klen[id] = len;
-      D.krep[3 * id + 0] = idL;
-      D.krep[3 * id + 1] = g;
-      D.krep[3 * id + 2] = idR;
-    }
+    claim_payload(D, slot, h1, h2, len, idL, g, idR);
+    note_claim(D, s_ns, slot);
+  } else {
+    emit_check(D, s_chk, slot, len, h1, h2);
   }
-  // One loop for the claimer's publication and the waiters' polling: a lane of
-  // the same wave may be waiting on this lane's claim, so the publishing store
-  // must not sit in a separate region the compiler could schedule after the
-  // polling loop (pub changes inside the loop, so it cannot be unswitched).
-  bool pub = claimed;
-  int32_t d = -1;
-  for (int32_t spin = 0;; spin++) {
-    if (pub) {
-      __hip_atomic_store(&D.ht_dense[slot], (int32_t)id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      d = (int32_t)id;
-      pub = false;
-    } else if (spin == 0) {
-      d = D.ht_dense[slot];  // ids are written once: a stale read can only be -1
-    } else {
-      __builtin_amdgcn_s_sleep(2);
-      d = __hip_atomic_load(&D.ht_dense[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (d >= 0) break;
-    if (spin > (1 << 20)) {  // never published: a failed claim elsewhere
-      set_error(D, GEOBPE_ECAPACITY, -11);
-      return -1;
-    }
-  }
-  if (!claimed) emit_check(D, s_chk, d, len, h1, h2);
-  return d;
+  return slot;
 }
 
 // per-workgroup key cache (LDS): the occurrences a workgroup handles often make
@@ -1026,11 +958,11 @@ __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const
 
 // before the round's barrier: look the key up in the workgroup cache; the
 // resolver (or an uncached thread) gets the dense id from the global table
-__device__ inline void half_resolve(const Dev& D, KeyCache& kc, WgIds& ids, int32_t* s_chk, Half& x) {
+__device__ inline void half_resolve(const Dev& D, KeyCache& kc, int32_t* s_ns, int32_t* s_chk, Half& x) {
   x.kcs = kc_find(kc, x.k, &x.res);
   x.d = -1;
   if (!x.res) return;
-  x.d = key_id_now(D, ids, s_chk, x.k, x.s, x.cur, x.h1, x.h2, x.len, x.idL, x.g, x.idR);
+  x.d = key_id_now(D, s_ns, s_chk, x.k, x.s, x.cur, x.h1, x.h2, x.len, x.idL, x.g, x.idR);
   if (x.kcs >= 0) {
     kc.h1[x.kcs] = x.h1;
     kc.id[x.kcs] = x.d >= 0 ? x.d : -2;
@@ -1071,10 +1003,9 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   static_assert(sizeof(AggBig) == sizeof(int32_t) * NBKT, "LDS union layout");
   AggBig& agg = u.agg;
   __shared__ HotApp hot;
-  __shared__ WgIds ids;
   __shared__ WgLog lg;
   __shared__ KeyCache kc;
-  __shared__ int32_t s_chk;
+  __shared__ int32_t s_chk, s_ns;
   __shared__ int32_t s_off[RPB + 1];
   __shared__ int32_t s_red[ABLOCK / 64];
   if (D.st->done) return;
@@ -1112,8 +1043,7 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
     if (threadIdx.x == 0) {
       s_off[RPB] = tot;
       s_chk = 0;
-      ids.next = D.chunk[2 * blockIdx.x];
-      ids.end = D.chunk[2 * blockIdx.x + 1];
+      s_ns = 0;
       lg.n0 = lg.n = D.plogn[blockIdx.x];
       lg.ovf = 0;
     }
@@ -1132,15 +1062,6 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   const int64_t oper = (novf + gridDim.x - 1) / gridDim.x;
   const int64_t o_lo = (int64_t)blockIdx.x * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
   const int64_t total = E + o_n;
-  // at most two new keys per merge: make the id chunk that large now, with one
-  // global reservation (refilling claim by claim would serialise every
-  // workgroup on one returning atomic)
-  if (threadIdx.x == 0 && ids.end - ids.next < 2 * total) {
-    const int64_t sz = max((int64_t)ID_CHUNK, 2 * total);
-    ids.next = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
-    ids.end = ids.next + sz;
-  }
-  __syncthreads();
   dbg_stamp(D, 1);
   int dbk = 2;
   for (int64_t j0 = 0; j0 < total; j0 += blockDim.x) {
@@ -1160,8 +1081,8 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
       apply_front(D, agg, hot, e, A, hl, vl, hr, vr, j0 < 2 * ABLOCK ? 40 + 10 * (int)(j0 / ABLOCK) : -1);
     }
     dbg_stamp(D, dbk++);
-    if (vl) half_resolve(D, kc, ids, &s_chk, hl);
-    if (vr) half_resolve(D, kc, ids, &s_chk, hr);
+    if (vl) half_resolve(D, kc, &s_ns, &s_chk, hl);
+    if (vr) half_resolve(D, kc, &s_ns, &s_chk, hr);
     dbg_stamp(D, dbk++);
     __syncthreads();
     dbg_stamp(D, dbk++);
@@ -1179,15 +1100,8 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
     D.plogn[blockIdx.x] = ln;
     if (ln > lg.n0) atomicAdd((unsigned long long*)&st->plog_total, (unsigned long long)(ln - lg.n0));
     if (lg.ovf) st->plog_ovf = 1;
-    int64_t nx = ids.next, en = ids.end;
-    if (nx >= en) {  // chunk used up: reserve the next one, sized by this launch's demand
-      const int64_t sz = max((int64_t)ID_CHUNK, 2 * (nx - en + ID_CHUNK));
-      nx = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
-      en = nx + sz;
-    }
-    D.chunk[2 * blockIdx.x] = nx;
-    D.chunk[2 * blockIdx.x + 1] = en;
   }
+  close_claims(D, &s_ns);
   if (blockIdx.x == 0) {
     int32_t tot;
     block_excl_scan(nm, &tot, s_red);
@@ -1284,9 +1198,20 @@ __global__ __launch_bounds__(BLOCK) void k_recount(Dev D) {
 }
 
 __global__ __launch_bounds__(BLOCK) void k_compare(Dev D) {
-  const int64_t U = D.st->U;
-  for (int64_t d = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; d < U; d += (int64_t)gridDim.x * blockDim.x)
+  const int64_t U = min(D.st->U, D.KCAP);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t d = D.klist[i];
     if (D.scratch[d] != D.count[d]) atomicAdd((unsigned long long*)&D.st->nmismatch, 1ULL);
+  }
+}
+
+// debug: (key id, count) of every listed key
+__global__ __launch_bounds__(BLOCK) void k_gather_counts(Dev D, int32_t* keys, int32_t* counts, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t d = D.klist[i];
+    keys[i] = d;
+    counts[i] = D.count[d];
+  }
 }
 
 // debug: device key-string order of n (a, b) key pairs (tests the JSON generator)

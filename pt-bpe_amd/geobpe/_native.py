@@ -58,7 +58,7 @@ def lib():
         "geobpe_merge_log": (I64, [P, P, I64]),
         "geobpe_key_json": (I64, [P, I32, ctypes.c_char_p, I64]),
         "geobpe_debug_key_less": (ctypes.c_int, [P, P, I32, P]),
-        "geobpe_debug_counts": (I64, [P, P, I64]),
+        "geobpe_debug_counts": (I64, [P, P, P, I64]),
         "geobpe_debug_key": (ctypes.c_int, [P, I32, P]),
         "geobpe_step_select": (ctypes.c_int, [P, pI32, pI32]),
         "geobpe_step_apply": (ctypes.c_int, [P, pI64]),

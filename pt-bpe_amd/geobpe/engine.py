@@ -271,17 +271,21 @@ class GeoBPEEngine:
         self.L.geobpe_key_json(self._ctx, d, buf, m + 1)
         return buf.value.decode()
 
+    def _keys_and_counts(self):
+        U = int(self.L.geobpe_debug_counts(self._ctx, None, None, 0))
+        keys = np.zeros(max(U, 1), dtype=np.int32)
+        cnt = np.zeros(max(U, 1), dtype=np.int32)
+        self.L.geobpe_debug_counts(self._ctx, _p(keys), _p(cnt), U)
+        return keys[:U], cnt[:U]
+
     def key_counts(self) -> dict:
         """{key string: global count} of every key with a positive count."""
-        U = int(self.L.geobpe_debug_counts(self._ctx, None, 0))
-        cnt = np.zeros(max(U, 1), dtype=np.int32)
-        self.L.geobpe_debug_counts(self._ctx, _p(cnt), U)
-        return {self.key_json(int(d)): int(cnt[d]) for d in np.nonzero(cnt[:U] > 0)[0]}
+        keys, cnt = self._keys_and_counts()
+        return {self.key_json(int(d)): int(c) for d, c in zip(keys, cnt) if c > 0}
 
     def live_key_ids(self) -> np.ndarray:
-        """dense ids that name a key (chunk-tail ids that were never used excluded)"""
-        U = int(self.L.geobpe_debug_counts(self._ctx, None, 0))
-        return np.array([d for d in range(U) if self.L.geobpe_key_json(self._ctx, d, None, 0) >= 0], dtype=np.int32)
+        """ids (key-table slots) of every key"""
+        return self._keys_and_counts()[0].copy()
 
     def debug_key_less(self, pairs: np.ndarray) -> np.ndarray:
         pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
