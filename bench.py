@@ -34,6 +34,20 @@ CONFIGS = {
     "c2": (10_000, 256, None, 5, 500),  # BASELINE configs[1]
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+APPLY_BYTES_PER_MERGE = 156  # algorithmic bytes of one merged occurrence in k_apply
+PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_latest.json")
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of k_<kernel> from the committed rocprofv3 PMC summary
+    of this bench command (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), or None."""
+    try:
+        with open(PMC_SUMMARY) as f:
+            d = json.load(f)
+        k = d["kernels"][f"k_{kernel}"]
+        return round(k["hbm_bytes_per_launch"], 1), os.path.relpath(d.get("source", PMC_SUMMARY), REPO)
+    except Exception:
+        return None, None
 
 
 def parse():
@@ -46,7 +60,7 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=30.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
-    ap.add_argument("--roofline-kernel", default="mark")
+    ap.add_argument("--roofline-kernel", default="apply")
     ap.add_argument("--event-stride", type=int, default=8,
                     help="time every k-th launch of the roofline kernel in the timed region")
     return ap.parse_args()
@@ -90,7 +104,7 @@ def main():
     torch.cuda.synchronize()
     t_bin = time.time() - t0
     U0 = eng.num_keys
-    bin_ms = {k: eng.kernel_ms(k)[0] for k in ("pair_count", "assign", "finalize")}
+    bin_ms = {k: eng.kernel_ms(k)[0] for k in ("pair_count", "finalize")}
     eng.run(args.warmup)
     # ---- timed region: exactly K merges; HIP events only around the roofline kernel
     eng.set_profiling(not args.no_profile, only=args.roofline_kernel, stride=args.event_stride)
@@ -131,28 +145,35 @@ def main():
         assert rep.merges == merges_log, "replay diverged"
         rep.close()
 
-    # ---- roofline of the loop's scan kernel, from the live events of the timed region
+    # ---- roofline of the loop's dominant kernel, from the live events of the timed region
     roofline = None
     if live_n:
         avg_s = live_ms / 1000.0 / live_n
-        if args.roofline_kernel == "mark":
-            bytes_per_launch = 4.0 * R_local  # the pk scan: 4 B per residue slot
-            note = "4 B x residue slots (pk scan); run walks and merge records excluded"
-        else:
-            bytes_per_launch = 4.0 * eng.num_keys
-            note = "4 B x dense keys"
+        window = merges_log[-done:] if done else []
+        n_merged = sum(m[2] for m in window)
+        if args.roofline_kernel == "apply":
+            # 156 B per merged occurrence (token records of p, a, b, c; two
+            # glue symbols; neighbour content hashes; two key-table probes; the rewritten
+            # token fields; five count read-modify-writes)
+            bytes_per_launch = APPLY_BYTES_PER_MERGE * n_merged / max(done, 1)
+            note = f"{APPLY_BYTES_PER_MERGE} B x merged occurrences (avg {n_merged / max(done, 1):.0f} per launch)"
+        else:  # mark, fingerprint-scan mode: the 2 B/slot scan
+            bytes_per_launch = 2.0 * R_local
+            note = "2 B x residue slots (fingerprint scan)"
         ach = bytes_per_launch / avg_s / 1e9
-        roofline = {"kernel": args.roofline_kernel, "bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                    "bytes_per_launch": bytes_per_launch, "avg_launch_us": round(avg_s * 1e6, 3),
-                    "launches": live_n, "algorithmic_bytes": note}
+        traffic, tsrc = pmc_traffic(args.roofline_kernel)
+        roofline = {"kernel": f"k_{args.roofline_kernel}", "bound": "hbm", "achieved": round(ach, 2),
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
+                    "traffic_source": tsrc, "bytes_per_launch": round(bytes_per_launch, 1),
+                    "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": live_n,
+                    "event_stride": args.event_stride, "algorithmic_bytes": note}
     # the full content-keyed pair-count pass (BPE.bin) at iteration 0: SURVEY §8(d)
     # B_count = 20*T_live + 4*U_live with T = residues
     pair_count = None
     if bin_ms.get("pair_count"):
         t_count = sum(bin_ms.values()) / 1000.0
         bc = 20.0 * R_local + 4.0 * U0
-        pair_count = {"kernels": "k_pairs_all+k_assign+k_finalize", "bytes": bc, "time_us": round(t_count * 1e6, 2),
+        pair_count = {"kernels": "k_pairs_all+k_finalize", "bytes": bc, "time_us": round(t_count * 1e6, 2),
                       "achieved_GBs": round(bc / t_count / 1e9, 1),
                       "frac": round(bc / t_count / 1e9 / HBM_PEAK_GBS, 4),
                       "ms": {k: round(v, 4) for k, v in bin_ms.items()}, "U0": U0, "T0": R_local}

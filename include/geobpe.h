@@ -83,7 +83,9 @@ int geobpe_bin(geobpe_ctx *ctx);
 
 /* ---- BPE.step() (bpe.py:1792-2166) ----
  * One merge iteration: device argmax (max count, ties -> smallest reference key
- * string), greedy non-overlapping merge-apply, incremental count update.
+ * string: SortedDict.peekitem(0), bpe.py:1796-1800), greedy non-overlapping
+ * merge-apply (bpe.py:1888-2014), incremental count update, new token
+ * _tokens[n] = json.loads(key) (bpe.py:1857-1860).
  * *new_id = the new token id (len(_tokens) before the step), *count = its
  * occurrence count, *n_merged = merges applied; *new_id = -1 if no pair is left. */
 int geobpe_step(geobpe_ctx *ctx, int32_t *new_id, int32_t *count, int64_t *n_merged);
@@ -115,23 +117,24 @@ int geobpe_set_global_residues(geobpe_ctx *ctx, int64_t n);
 /* ---- introspection / exports ---- */
 /* Key string (json.dumps(geo, sort_keys=True)) of vocab id v's content. */
 int64_t geobpe_token_json(geobpe_ctx *ctx, int32_t v, char *buf, int64_t cap);
-/* Key string of dense pair key d (introspection / tests). */
+/* Key string of pair key d (key id = key-table slot; introspection / tests). */
 int64_t geobpe_key_json(geobpe_ctx *ctx, int32_t d, char *buf, int64_t cap);
 /* Device ordering of reference key strings: h_out[i] = key(h_pairs[2i]) <
- * key(h_pairs[2i+1]) for dense key ids (tests the device tie-break). */
+ * key(h_pairs[2i+1]) for key ids (tests the device tie-break of the
+ * SortedDict order, bpe.py:1469-1471). */
 int geobpe_debug_key_less(geobpe_ctx *ctx, const int32_t *h_pairs, int32_t n, int32_t *h_out);
 /* Every key (id = key-table slot, in claim order) and its global pair count;
  * returns the number of keys U, copies at most cap of each. */
 int64_t geobpe_debug_counts(geobpe_ctx *ctx, int32_t *h_keys, int32_t *h_counts, int64_t cap);
-/* Debug record of dense key d: idL, g, idR, len, count, U, K(device), K(host), h1. */
+/* Debug record of key d: idL, g, idR, len, count, U, K(device), K(host), h1. */
 int geobpe_debug_key(geobpe_ctx *ctx, int32_t d, int64_t *h_out9);
 /* Content (residue / junction symbols, 2*nres-1 values) of vocab id v. */
 int64_t geobpe_token_content(geobpe_ctx *ctx, int32_t v, int32_t *h_out, int64_t cap);
 int64_t geobpe_vocab_count(geobpe_ctx *ctx); /* len(_tokens) */
-int64_t geobpe_num_keys(geobpe_ctx *ctx);    /* distinct pair keys ever seen */
+int64_t geobpe_num_keys(geobpe_ctx *ctx);    /* distinct pair keys ever seen (len of the reference's _geo_dict history) */
 int64_t geobpe_num_tokens(geobpe_ctx *ctx);  /* live tokens (sync) */
-/* Segmentation (bond_to_token order): per row the (start residue within the row,
- * token id) of every token.  Call with NULL buffers to get the total count. */
+/* Segmentation (Tokenizer.bond_to_token order, tokenizer.py:24-61): per row the
+ * (start residue within the row, token id) of every token.  Call with NULL buffers to get the total count. */
 int64_t geobpe_segmentation(geobpe_ctx *ctx, int32_t *h_start, int32_t *h_id, int64_t *h_row_tok_off);
 /* quantize(tokenize()) of every row (tokenizer.py:379-392, bpe.py:918-956). */
 int64_t geobpe_encode(geobpe_ctx *ctx, int32_t *h_ids, int64_t *h_row_id_off);
@@ -140,8 +143,8 @@ int64_t geobpe_encode(geobpe_ctx *ctx, int32_t *h_ids, int64_t *h_row_id_off);
  * keys (0 = consistent), or -1 on error. */
 int64_t geobpe_verify_counts(geobpe_ctx *ctx);
 /* Per-kernel time (ms summed over launches, HIP events on the context stream)
- * while profiling is enabled.  names: "pair_count", "argmax", "select",
- * "mark", "apply", "assign", "finalize", "recount".  on = 0: off; on = 1: every
+ * while profiling is enabled.  names: "pair_count", "finalize" (bin), "select",
+ * "mark", "apply" (merge loop), "recount".  on = 0: off; on = 1: every
  * launch; on = k > 1: every k-th launch of each kernel (sampling keeps the event
  * packets from stretching the stream they measure). */
 int geobpe_set_profiling(geobpe_ctx *ctx, int on);

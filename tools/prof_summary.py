@@ -36,9 +36,19 @@ def main(d):
         for k, v in agg.items():
             if k.startswith("k_"):
                 out["pmc"].setdefault(k, {})[c + "_KB_avg"] = round(sum(v) / len(v), 1)
+    # HBM bytes per launch: FETCH_SIZE (KB) counts half of wide streaming reads on gfx950 -> x2
+    for k, v in out["pmc"].items():
+        if "fetch_KB_avg" in v and "write_KB_avg" in v:
+            v["hbm_bytes_per_launch"] = 1024.0 * (2 * v["fetch_KB_avg"] + v["write_KB_avg"])
     return out
 
 
 if __name__ == "__main__":
     r = main(sys.argv[1])
+    if len(sys.argv) > 2:  # write the bench's traffic source (profiles/pmc_latest.json)
+        with open(sys.argv[2], "w") as f:
+            json.dump({"source": sys.argv[3] if len(sys.argv) > 3 else sys.argv[1],
+                       "note": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of the bench command; "
+                               "hbm_bytes_per_launch = 1024 * (2 * FETCH_SIZE + WRITE_SIZE)",
+                       "kernels": r["pmc"]}, f, indent=1)
     print(json.dumps(r, indent=1))
