@@ -123,8 +123,9 @@ int64_t geobpe_key_json(geobpe_ctx *ctx, int32_t d, char *buf, int64_t cap);
  * key(h_pairs[2i+1]) for key ids (tests the device tie-break of the
  * SortedDict order, bpe.py:1469-1471). */
 int geobpe_debug_key_less(geobpe_ctx *ctx, const int32_t *h_pairs, int32_t n, int32_t *h_out);
-/* Every key (id = key-table slot, in claim order) and its global pair count;
- * returns the number of keys U, copies at most cap of each. */
+/* Every klist entry (key id = key-table slot, in claim order; -1 = an unused
+ * chunk entry) and its global pair count; returns the number of entries,
+ * copies at most cap of each. */
 int64_t geobpe_debug_counts(geobpe_ctx *ctx, int32_t *h_keys, int32_t *h_counts, int64_t cap);
 /* Debug record of key d: idL, g, idR, len, count, U, K(device), K(host), h1. */
 int geobpe_debug_key(geobpe_ctx *ctx, int32_t d, int64_t *h_out9);

@@ -24,24 +24,26 @@ constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per re
 constexpr int NBKT = 1 << NBKT_LOG2;
 constexpr int SKIP_HOT = 1, SKIP_POST = 2;  // what a rebuild iteration rebuilds
 constexpr int DBG_SLOTS = 64;
+constexpr int PW_LDS = 2048;    // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
+constexpr int KL_CHUNK = 4096;  // klist entries an apply workgroup reserves at a time
 
 // ------------------------------------------------------------------ records
 struct State {
   // persistent
-  int64_t U;          // keys listed in klist
+  int64_t U;          // klist entries reserved (keys + unused chunk tails)
+  int64_t nkeys;      // keys
   int64_t err_code;   // first error (GEOBPE_E*)
   int64_t err_pos;
   int64_t epoch;      // delta-touch epoch (multi-rank)
-  int64_t vsym_used;  // device vocab content pool cursor
   int32_t K;          // len(_tokens) on the device
   int32_t iter;       // merges selected so far
   int32_t tag;        // role tag of the current merge (= iter)
   int32_t done;       // 1 once no pair is left
   int32_t W, nid, maxc, ncand;
-  // the winner, precomputed by k_select_final for k_mark / k_apply
+  // the winner, set by k_select for k_mark / k_apply
   u64 w1, w2;                      // content hash of the merged token
-  u64 pwW1a, pwW1b, pwW2a, pwW2b;  // P^(|W|syms+1), P^|W|syms (both bases)
   int32_t wl, wfp;                 // residues of W, key_fp(W)
+  int32_t widL, wg, widR;          // W's representative: the new token's content parts
   // per-iteration, reset by k_select
   int64_t L_ovf, np_ovf, ns_ovf, nL_total;
   int64_t ntouched, nmismatch;
@@ -87,6 +89,7 @@ struct Dev {
   int32_t *rsym, *gsym;
   // tokens (residue indexed)
   int32_t *tid, *tlen, *tprev, *pk, *role;
+  u64 *th1, *th2;  // content hash of the token starting at a slot (= vh of its id; saves the vocab lookup)
   uint16_t* fp;  // 16-bit fingerprint of pk (0xFFFF = none): the mark scan reads these
   // vocab (token id indexed)
   u64 *vh1, *vh2;
@@ -119,7 +122,8 @@ struct Dev {
   int32_t* npcnt;
   NewPair* npovf;
   int32_t* ns;  // per region workgroup: slots it claimed (listed in klist at region close)
-  int32_t* klist;  // every key id (= key-table slot), in claim order: U entries
+  int32_t* klist;  // every key id (= key-table slot), in claim order; U = reserved length (-1 = unused)
+  int64_t* kchunk; // per apply workgroup: [next, end) of its reserved klist chunk
   NewPair* chk;     // per apply workgroup: keys found in the last merge (EHASH check)
   int32_t* chkcnt;
   // posting index: region r = residue slots [r*PR, (r+1)*PR), one per apply workgroup
@@ -401,6 +405,7 @@ __device__ inline void agg_flush_hot(A& s, const Dev& D, HotApp& h, bool to_delt
   }
   hot_flush(D, h);
 }
+
 
 // key-table probing: the first slot of a key and, given the value already read
 // there, find-or-claim (CAS) its slot; *claimed = true if this thread inserted it

@@ -200,7 +200,7 @@ int alloc_keys(geobpe_ctx* c) {
   if (c->keys_ready) return 0;
   Dev& D = c->D;
   const int64_t base = c->distributed && c->global_residues > c->R ? c->global_residues : c->R;
-  D.KCAP = 3 * base + 65536;  // keys: bin pairs + at most two new pairs per merge
+  D.KCAP = 3 * base + 65536 + (int64_t)c->nba * KL_CHUNK;  // bin pairs + 2 new pairs per merge + chunk tails
   int64_t hc = 1 << 16;
   while (hc < 2 * D.KCAP) hc <<= 1;
   D.HC = hc;
@@ -212,7 +212,7 @@ int alloc_keys(geobpe_ctx* c) {
   if ((rc = dalloc(c, &D.ht_key, D.HC, 0)) || (rc = dalloc(c, &D.kh1, D.HC)) || (rc = dalloc(c, &D.kh2, D.HC)) ||
       (rc = dalloc(c, &D.klen, D.HC)) || (rc = dalloc(c, &D.krep, 3 * D.HC, 0xFF)) ||
       (rc = dalloc(c, &D.count, D.HC + 16, 0)) || (rc = dalloc(c, &D.scratch, D.HC + 16, 0)) ||
-      (rc = dalloc(c, &D.klist, D.KCAP, 0xFF)))
+      (rc = dalloc(c, &D.klist, D.KCAP, 0xFF)) || (rc = dalloc(c, &D.kchunk, 2 * (int64_t)c->nba, 0)))
     return rc;
   if (c->distributed) {
     if ((rc = dalloc(c, &D.dcount, D.HC, 0)) || (rc = dalloc(c, &D.touch, D.HC, 0xFF)) ||
@@ -316,6 +316,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   if ((rc = dalloc(c, &c->d_row_off, n_rows + 1)) || (rc = dalloc(c, &D.rsym, Rp, 0)) ||
       (rc = dalloc(c, &D.gsym, Rp, 0)) || (rc = dalloc(c, &D.tid, Rp, 0xFF)) || (rc = dalloc(c, &D.tlen, Rp, 0)) ||
       (rc = dalloc(c, &D.tprev, Rp, 0xFF)) || (rc = dalloc(c, &D.pk, Rp, 0xFF)) || (rc = dalloc(c, &D.role, Rp, 0)) ||
+      (rc = dalloc(c, &D.th1, Rp, 0)) || (rc = dalloc(c, &D.th2, Rp, 0)) ||
       (rc = dalloc(c, &D.fp, Rp + 16, 0xFF)))
     return rc;
   D.row_off = c->d_row_off;
@@ -487,8 +488,6 @@ int geobpe_init_tokens(geobpe_ctx* c, const int32_t* h_label_of_sym, int32_t K0)
   }
   HIPCHK(c, hipMemcpyAsync(c->D.voff, vo.data(), (K0 + 1) * 8, hipMemcpyHostToDevice, c->stream));
   c->h_state->K = K0;
-  c->h_state->vsym_used = K0;
-  HIPCHK(c, hipMemcpyAsync(&c->D.st->vsym_used, &c->h_state->vsym_used, 8, hipMemcpyHostToDevice, c->stream));
   HIPCHK(c, hipMemcpyAsync(&c->D.st->K, &c->h_state->K, 4, hipMemcpyHostToDevice, c->stream));
   const int nb = (int)std::min<int64_t>(c->nrows, 65536);
   hipLaunchKernelGGL(k_init_tokens, dim3(std::max(nb, 1)), dim3(64), 0, c->stream, c->D, (const int32_t*)dl);
@@ -696,7 +695,7 @@ int64_t geobpe_vocab_count(geobpe_ctx* c) {
 int64_t geobpe_num_keys(geobpe_ctx* c) {
   if (!c || !c->keys_ready) return 0;
   if (sync_state(c)) return -1;
-  return c->h_state->U;
+  return c->h_state->nkeys;
 }
 
 static int row_token_offsets(geobpe_ctx* c, std::vector<int64_t>& off, int64_t** d_off) {

@@ -122,8 +122,10 @@ __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_
   for (int64_t r = blockIdx.x; r < D.nrows; r += gridDim.x) {
     const int64_t a = D.row_off[r], b = D.row_off[r + 1];
     for (int64_t g = a + threadIdx.x; g < b; g += blockDim.x) {
-      D.tid[g] = label_of_sym[D.rsym[g]];
+      const int32_t sy = D.rsym[g];
+      D.tid[g] = label_of_sym[sy];
       D.tlen[g] = 1;
+      D.th1[g] = D.th2[g] = (u64)(sy + 1);  // = vh of the residue token (geobpe_init_tokens)
       D.tprev[g] = (g == a) ? -1 : (int32_t)(g - 1);
       D.pk[g] = -1;
       D.fp[g] = 0xFFFF;
@@ -180,8 +182,10 @@ __device__ inline void note_claim(const Dev& D, int32_t* s_ns, int32_t slot) {
   const int32_t j = atomicAdd(s_ns, 1);
   if (j < D.RC)
     D.ns[(int64_t)blockIdx.x * D.RC + j] = slot;
-  else  // rare: listed right away
+  else {  // rare: listed right away
     klist_put(D, (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL), slot);
+    atomicAdd((unsigned long long*)&D.st->nkeys, 1ULL);
+  }
 }
 
 // insert (or find) a pair key and emit the pair
@@ -203,7 +207,10 @@ __device__ inline void close_claims(const Dev& D, int32_t* s_ns) {
   __shared__ int64_t s_base;
   __syncthreads();
   const int32_t n = min(*s_ns, (int32_t)D.RC);
-  if (threadIdx.x == 0) s_base = n ? (int64_t)atomicAdd((unsigned long long*)&D.st->U, (unsigned long long)n) : 0;
+  if (threadIdx.x == 0) {
+    s_base = n ? (int64_t)atomicAdd((unsigned long long*)&D.st->U, (unsigned long long)n) : 0;
+    if (n) atomicAdd((unsigned long long*)&D.st->nkeys, (unsigned long long)n);
+  }
   __syncthreads();
   const int32_t* reg = D.ns + (int64_t)blockIdx.x * D.RC;
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) klist_put(D, s_base + i, reg[i]);
@@ -224,14 +231,15 @@ __global__ __launch_bounds__(ABLOCK) void k_pairs_all(Dev D) {
   for (int64_t g = lo + threadIdx.x; g < hi; g += blockDim.x) {
     const int32_t L = D.tid[g];
     if (L < 0) continue;
-    const int32_t e = (int32_t)g + D.tlen[g] - 1;
+    const int32_t xlen = D.tlen[g];
+    const int32_t e = (int32_t)g + xlen - 1;
     if (D.rsym[e] >= D.B3) continue;  // last token of its chain
     const int32_t Rr = D.tid[e + 1];
     const int32_t gl = D.gsym[e];
-    const int32_t ylen = D.vlen[Rr];
+    const int32_t ylen = D.tlen[e + 1];
     u64 h1, h2;
-    combine(D, D.vh1[L], D.vh2[L], gl, D.vh1[Rr], D.vh2[Rr], ylen, h1, h2);
-    add_pair(D, &s_np, &s_ns, (int32_t)g, h1, h2, D.vlen[L] + ylen, L, gl, Rr, 1);
+    combine(D, D.th1[g], D.th2[g], gl, D.th1[e + 1], D.th2[e + 1], ylen, h1, h2);
+    add_pair(D, &s_np, &s_ns, (int32_t)g, h1, h2, xlen + ylen, L, gl, Rr, 1);
   }
   close_regions(D, &s_np, &s_ns);
 }
@@ -505,6 +513,11 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
   __shared__ int32_t s_best[BLOCK];
   __shared__ char s_jbuf[48 * BLOCK];
   State* st = D.st;
+  // the first 4*BLOCK list entries are loaded together with the state (clist has
+  // KCAP >= 4*BLOCK entries; entries past ncl are masked below)
+  int32_t d0[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) d0[q] = D.clist[threadIdx.x + q * BLOCK];
   if (st->done) return;
   const int64_t n = st->ncl;
   const int32_t th = st->theta;
@@ -516,7 +529,7 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const int64_t i = i0 + (int64_t)q * BLOCK;
-      d[q] = i < n ? D.clist[i] : -1;
+      d[q] = i < n ? (i0 < BLOCK ? d0[q] : D.clist[i]) : -1;
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) c[q] = d[q] >= 0 ? D.count[d[q]] : 0;
@@ -597,26 +610,17 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
     W = s_best[0];
   }
   const int32_t nid = st->K;
-  const int32_t L = D.krep[3 * W], g = D.krep[3 * W + 1], Rr = D.krep[3 * W + 2];
-  const int64_t vL = D.voff[L], vR = D.voff[Rr];
-  const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
-  const int64_t pos = st->vsym_used, ln = nL + 1 + nR;
-  if (nid >= D.KC || pos + ln > D.VSC) {
+  if (nid >= D.KC) {
     if (threadIdx.x == 0) {
       set_error(D, GEOBPE_ECAPACITY, -9);
       st->done = 1;
     }
     return;
   }
-  // _tokens[n] = json.loads(key): content = content(L) ++ [g] ++ content(R)
-  for (int64_t i = threadIdx.x; i < ln; i += blockDim.x)
-    D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
-  __syncthreads();  // every thread has read st->K / vsym_used before they move
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0) {  // (the new token's content is written by k_apply's workgroup 0)
+    const int32_t L = D.krep[3 * (int64_t)W], g = D.krep[3 * (int64_t)W + 1], Rr = D.krep[3 * (int64_t)W + 2];
     const u64 w1 = D.kh1[W], w2 = D.kh2[W];
     const int32_t wl = D.klen[W];
-    const int64_t ny = 2 * (int64_t)wl - 1;
-    D.voff[nid + 1] = pos + ln;
     D.vh1[nid] = w1;
     D.vh2[nid] = w2;
     D.vlen[nid] = wl;
@@ -629,7 +633,6 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
     lr.idR = Rr;
     lr.nmerged = 0;
     D.log[st->iter] = lr;
-    st->vsym_used = pos + ln;
     st->K = nid + 1;
     st->iter += 1;
     st->tag = st->iter;
@@ -643,10 +646,9 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
     st->w2 = w2;
     st->wl = wl;
     st->wfp = key_fp(W);
-    st->pwW1a = D.pw1[ny + 1];
-    st->pwW1b = D.pw1[ny];
-    st->pwW2a = D.pw2[ny + 1];
-    st->pwW2b = D.pw2[ny];
+    st->widL = L;
+    st->wg = g;
+    st->widR = Rr;
   }
 }
 
@@ -663,36 +665,51 @@ __device__ inline void check_found(const Dev& D, int32_t r) {
   }
 }
 
-// walk one maximal run of winner matches starting at token h: greedy left to
-// right (bpe.py:1888-1916) -- merge h, skip the next pair, merge the one after
-// if the run continues, ...
-__device__ inline void walk_run(const Dev& D, int32_t h, int32_t W, int32_t tag, int32_t* s_n) {
-  int32_t t = h, p = D.tprev[h];
+// a candidate occurrence g of the winner W: confirm it, and if g starts a run
+// of W pairs walk the run greedily left to right (bpe.py:1888-1916) -- merge
+// (t, b), skip the pair (b, c), merge (c, d) if it is W too, ...  Independent
+// loads are issued together: two dependent rounds per hit, two per run step.
+__device__ inline void emit_merge(const Dev& D, int32_t* s_n, int32_t t, int32_t p, int32_t b, int32_t c,
+                                  int32_t tag) {
+  LEntry e;
+  e.a = t;
+  e.p = p;
+  e.b = b;
+  e.c = c;
+  D.role[t] = (tag << 2) | 1;
+  D.role[b] = (tag << 2) | 2;
+  const int32_t j = atomicAdd(s_n, 1);
+  if (j < D.LC) {
+    D.L[(int64_t)blockIdx.x * D.LC + j] = e;
+  } else {
+    const int64_t k = atomicAdd((unsigned long long*)&D.st->L_ovf, 1ULL);
+    if (k < D.Lovf_cap)
+      D.Lovf[k] = e;
+    else
+      set_error(D, GEOBPE_ECAPACITY, -10);
+  }
+}
+
+__device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag, int32_t* s_n) {
+  const int32_t pkg = D.pk[g], p = D.tprev[g], lg = D.tlen[g];
+  if (pkg != W) return;
+  int32_t b = g + lg;
+  const int32_t pkp = D.pk[p >= 0 ? p : g];
+  int32_t pkb = D.pk[b], lb = D.tlen[b];
+  if (p >= 0 && pkp == W) return;  // not a run start: the run's head walks it
+  int32_t t = g, pp = p;
   for (;;) {
-    const int32_t b = t + D.tlen[t];
-    const int32_t pkb = D.pk[b];
-    const int32_t c = pkb >= 0 ? b + D.tlen[b] : -1;
-    LEntry e;
-    e.a = t;
-    e.p = p;
-    e.b = b;
-    e.c = c;
-    D.role[t] = (tag << 2) | 1;
-    D.role[b] = (tag << 2) | 2;
-    const int32_t j = atomicAdd(s_n, 1);
-    if (j < D.LC) {
-      D.L[(int64_t)blockIdx.x * D.LC + j] = e;
-    } else {
-      const int64_t k = atomicAdd((unsigned long long*)&D.st->L_ovf, 1ULL);
-      if (k < D.Lovf_cap)
-        D.Lovf[k] = e;
-      else
-        set_error(D, GEOBPE_ECAPACITY, -10);
-    }
+    const int32_t c = pkb >= 0 ? b + lb : -1;
+    emit_merge(D, s_n, t, pp, b, c, tag);
     if (pkb != W) break;
-    if (D.pk[c] != W) break;
-    p = b;
+    const int32_t pkc = D.pk[c], lc = D.tlen[c];
+    if (pkc != W) break;
+    const int32_t d = c + lc;
+    pp = b;
     t = c;
+    b = d;
+    pkb = D.pk[d];
+    lb = D.tlen[d];
   }
 }
 
@@ -734,10 +751,7 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
       const int2 e = i < n1 ? P[i] : Lg[i];
       if (e.x == W) {
         const int32_t g = e.y;
-        if (D.pk[g] == W) {
-          const int32_t p = D.tprev[g];
-          if (p < 0 || D.pk[p] != W) walk_run(D, g, W, tag, &s_n);
-        }
+        mark_hit(D, g, W, tag, &s_n);
       }
     }
     __syncthreads();
@@ -763,10 +777,7 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
         const uint32_t f = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
         if (f == fW) {
           const int32_t g = (int32_t)(8 * (i0 + u * BLOCK) + q);
-          if (D.pk[g] == W) {
-            const int32_t p = D.tprev[g];
-            if (p < 0 || D.pk[p] != W) walk_run(D, g, W, tag, &s_n);
-          }
+          mark_hit(D, g, W, tag, &s_n);
         }
       }
     }
@@ -782,9 +793,20 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
 struct ApplyCtx {
   int32_t W, nid, wl, tagL, tagR, theta;
   u64 w1, w2;
-  u64 pwL1a, pwL1b, pwL2a, pwL2b;  // powers for "X ++ g ++ W" (W on the right)
+  const u64* spw;                   // hash powers in LDS: base 1 at [0, PW_LDS), base 2 at [PW_LDS, 2 PW_LDS)
+  int32_t spwn;                     // entries staged per base
   bool to_delta;
 };
+// P^k of both bases: LDS when staged, else global
+__device__ inline void pw_pair(const Dev& D, const ApplyCtx& A, int64_t k, u64& p1, u64& p2) {
+  if (k < A.spwn) {
+    p1 = A.spw[k];
+    p2 = A.spw[PW_LDS + k];
+  } else {
+    p1 = D.pw1[k];
+    p2 = D.pw2[k];
+  }
+}
 
 struct WgLog {  // this workgroup's posting log cursor (LDS)
   int32_t n0, n, ovf;
@@ -880,42 +902,42 @@ struct Half {
 __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const LEntry e, const ApplyCtx& A, Half& hl,
                                    bool& vl, Half& hr, bool& vr, int dk) {
   const bool hasP = e.p >= 0, hasC = e.c >= 0;
-  // round 1: everything that depends only on the entry
+  // one round: everything that depends only on the entry, the neighbours' content
+  // hashes included (the per-slot token-hash cache th1/th2 + tlen).  Loads from
+  // valid addresses, then selects by value: a conditional load with a fallback
+  // in ApplyCtx would become a flat load through the scratch stack.
+  const int32_t ip = hasP ? e.p : e.a, ic = hasC ? e.c : e.a;
   const int32_t pkb = D.pk[e.b];
-  const int32_t rp = hasP ? D.role[e.p] : 0;
-  const int32_t pkp = hasP ? D.pk[e.p] : -1;
-  const int32_t L = hasP ? D.tid[e.p] : 0;
+  const int32_t rp = D.role[ip], pkp0 = D.pk[ip], L0 = D.tid[ip], ll0 = D.tlen[ip];
+  const u64 l1 = D.th1[ip], l2 = D.th2[ip];
   const int32_t glL = hasP ? D.gsym[e.a - 1] : 0;
-  const int32_t rc = hasC ? D.role[e.c] : 0;
-  const int32_t tc = hasC ? D.tid[e.c] : 0;
+  const int32_t rc0 = D.role[ic], tc = D.tid[ic], rl0 = D.tlen[ic];
+  const u64 c1 = D.th1[ic], c2 = D.th2[ic];
   const int32_t glR = hasC ? D.gsym[e.a + A.wl - 1] : 0;
+  const int32_t pkp = hasP ? pkp0 : -1;
+  const int32_t L = hasP ? L0 : 0;
+  const int32_t ll = ll0;
   const bool pN = hasP && rp != A.tagR;  // p is never a left part; R or untouched
-  const bool cL = hasC && rc == A.tagL;
+  const bool cL = hasC && rc0 == A.tagL;
   const int32_t idr = cL ? A.nid : tc;
-  // round 2: vocab hashes of the neighbours
-  // (loads from valid addresses, then selects by value: a conditional load with
-  // a fallback in ApplyCtx would become a flat load through the scratch stack)
   const bool rN = hasC && !cL;
-  const int32_t iL = pN ? L : 0, iR = rN ? idr : 0;
-  const u64 vl1 = D.vh1[iL], vl2 = D.vh2[iL], vr1 = D.vh1[iR], vr2 = D.vh2[iR];
-  const int32_t vll = D.vlen[iL], vrl = D.vlen[iR];
-  const u64 l1 = vl1, l2 = vl2;
-  const int32_t ll = vll;
-  const u64 r1 = rN ? vr1 : A.w1, r2 = rN ? vr2 : A.w2;
-  const int32_t rl = rN ? vrl : A.wl;
+  const u64 r1 = rN ? c1 : A.w1, r2 = rN ? c2 : A.w2;
+  const int32_t rl = rN ? rl0 : A.wl;
   u64 pr1a = 0, pr1b = 0, pr2a = 0, pr2b = 0;
   if (hasC) {
     const int64_t ny = 2 * (int64_t)rl - 1;
-    pr1a = D.pw1[ny + 1];
-    pr1b = D.pw1[ny];
-    pr2a = D.pw2[ny + 1];
-    pr2b = D.pw2[ny];
+    pw_pair(D, A, ny + 1, pr1a, pr2a);
+    pw_pair(D, A, ny, pr1b, pr2b);
   }
   // new pair keys and their first table probes (issued together)
   vl = pN;
   vr = hasC;
-  if (pN) {
-    combine_pw(l1, l2, glL, A.w1, A.w2, A.pwL1a, A.pwL1b, A.pwL2a, A.pwL2b, hl.h1, hl.h2);
+  if (pN) {  // X ++ g ++ W: powers of W's length
+    u64 pa1, pa2, pb1, pb2;
+    const int64_t nw = 2 * (int64_t)A.wl - 1;
+    pw_pair(D, A, nw + 1, pa1, pa2);
+    pw_pair(D, A, nw, pb1, pb2);
+    combine_pw(l1, l2, glL, A.w1, A.w2, pa1, pb1, pa2, pb2, hl.h1, hl.h2);
     hl.len = ll + A.wl;
     hl.k = probe_key(hl.h1, hl.h2, hl.len);
     hl.s = ht_first_slot(D, hl.k);
@@ -945,6 +967,8 @@ __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const
   // step 2: bond_to_token / token_pos
   D.tid[e.a] = A.nid;
   D.tlen[e.a] = A.wl;
+  D.th1[e.a] = A.w1;
+  D.th2[e.a] = A.w2;
   D.tid[e.b] = -1;
   D.pk[e.b] = -1;
   D.fp[e.b] = 0xFFFF;
@@ -1008,6 +1032,8 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   __shared__ int32_t s_chk, s_ns;
   __shared__ int32_t s_off[RPB + 1];
   __shared__ int32_t s_red[ABLOCK / 64];
+  __shared__ u64 s_pw[2 * PW_LDS];
+  __shared__ int64_t s_kl[2];
   if (D.st->done) return;
   if (D.st->skip) {
     const int32_t sk = D.st->skip;
@@ -1031,10 +1057,25 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   A.w1 = st->w1;
   A.w2 = st->w2;
   A.wl = st->wl;
-  A.pwL1a = st->pwW1a;
-  A.pwL1b = st->pwW1b;
-  A.pwL2a = st->pwW2a;
-  A.pwL2b = st->pwW2b;
+  A.spw = s_pw;
+  A.spwn = (int32_t)min(D.pwn, (int64_t)PW_LDS);
+  for (int i = threadIdx.x; i < A.spwn; i += blockDim.x) {
+    s_pw[i] = D.pw1[i];
+    s_pw[PW_LDS + i] = D.pw2[i];
+  }
+  if (blockIdx.x == 0) {  // _tokens[n] = json.loads(key): content(L) ++ [g] ++ content(R)
+    const int32_t L = st->widL, g = st->wg, Rr = st->widR;
+    const int64_t vL = D.voff[L], vR = D.voff[Rr];
+    const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
+    const int64_t pos = D.voff[A.nid], ln = nL + 1 + nR;
+    if (pos + ln > D.VSC) {
+      if (threadIdx.x == 0) set_error(D, GEOBPE_ECAPACITY, -9);
+    } else {
+      for (int64_t i = threadIdx.x; i < ln; i += blockDim.x)
+        D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
+      if (threadIdx.x == 0) D.voff[A.nid + 1] = pos + ln;
+    }
+  }
   if (threadIdx.x < 64) {  // this workgroup's RPB mark regions: offsets by a wave scan
     const int32_t c = threadIdx.x < RPB ? D.Lcnt[blockIdx.x * RPB + threadIdx.x] : 0;
     int32_t tot;
@@ -1046,8 +1087,16 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
       s_ns = 0;
       lg.n0 = lg.n = D.plogn[blockIdx.x];
       lg.ovf = 0;
+      s_kl[0] = D.kchunk[2 * blockIdx.x];
+      s_kl[1] = D.kchunk[2 * blockIdx.x + 1];
     }
   }
+  // speculative load of the first PRE entries of each of the RPB mark regions, in
+  // the same round as the state (late merges have a few entries per region)
+  constexpr int PRE = ABLOCK / RPB;
+  const int pr = threadIdx.x / PRE, pi = threadIdx.x % PRE;
+  LEntry pre;
+  if (pi < D.LC) pre = D.L[(int64_t)(blockIdx.x * RPB + pr) * D.LC + pi];
   int32_t nm = 0;
   if (blockIdx.x == 0) {  // merges applied this iteration -> merge log
     const int4* l4 = reinterpret_cast<const int4*>(D.Lcnt);  // NB % 4 == 0
@@ -1061,23 +1110,14 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   const int64_t novf = min(st->L_ovf, D.Lovf_cap);
   const int64_t oper = (novf + gridDim.x - 1) / gridDim.x;
   const int64_t o_lo = (int64_t)blockIdx.x * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
-  const int64_t total = E + o_n;
   dbg_stamp(D, 1);
   int dbk = 2;
-  for (int64_t j0 = 0; j0 < total; j0 += blockDim.x) {
-    const int64_t j = j0 + threadIdx.x;
+  // one block-uniform round: front half, key resolution, barrier, finish
+  auto round = [&](bool act, const LEntry& e, bool ovf, int64_t j0) {
     Half hl, hr;
     bool vl = false, vr = false;
-    if (j < total) {
-      LEntry e;
-      if (j < E) {
-        int r = 0;
-        while (j >= s_off[r + 1]) r++;
-        e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + (j - s_off[r])];
-      } else {
-        e = D.Lovf[o_lo + (j - E)];
-        agg_add_hot(agg, D, hot, A.W, -1, A.to_delta, A.theta);  // step 1 for an overflow entry
-      }
+    if (act) {
+      if (ovf) agg_add_hot(agg, D, hot, A.W, -1, A.to_delta, A.theta);  // step 1 for an overflow entry
       apply_front(D, agg, hot, e, A, hl, vl, hr, vr, j0 < 2 * ABLOCK ? 40 + 10 * (int)(j0 / ABLOCK) : -1);
     }
     dbg_stamp(D, dbk++);
@@ -1089,6 +1129,36 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
     if (vl) half_finish(D, agg, hot, kc, lg, hl, A, j0 < 2 * ABLOCK ? 42 + 10 * (int)(j0 / ABLOCK) : -1);
     if (vr) half_finish(D, agg, hot, kc, lg, hr, A, j0 < 2 * ABLOCK ? 45 + 10 * (int)(j0 / ABLOCK) : -1);
     dbg_stamp(D, dbk++);
+  };
+  // round 0: the prefetched entries
+  const int32_t cnt_r = s_off[pr + 1] - s_off[pr];
+  round(pi < cnt_r && pi < D.LC, pre, false, 0);
+  // then the rest of each region (entries >= PRE) and this workgroup's overflow share
+  __shared__ int32_t s_off2[RPB + 1];
+  if (threadIdx.x == 0) {
+    int32_t acc = 0;
+    for (int r = 0; r < RPB; r++) {
+      s_off2[r] = acc;
+      acc += max(0, s_off[r + 1] - s_off[r] - PRE);
+    }
+    s_off2[RPB] = acc;
+  }
+  __syncthreads();
+  const int32_t E2 = s_off2[RPB];
+  const int64_t total = E2 + o_n;
+  for (int64_t j0 = 0; j0 < total; j0 += blockDim.x) {
+    const int64_t j = j0 + threadIdx.x;
+    LEntry e;
+    bool ovf = false;
+    if (j < E2) {
+      int r = 0;
+      while (j >= s_off2[r + 1]) r++;
+      e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + PRE + (j - s_off2[r])];
+    } else if (j < total) {
+      e = D.Lovf[o_lo + (j - E2)];
+      ovf = true;
+    }
+    round(j < total, e, ovf, j0 + ABLOCK);
   }
   dbg_stamp(D, 60);
   agg_flush_hot(agg, D, hot, A.to_delta, A.theta);  // (syncs the workgroup first)
@@ -1101,12 +1171,32 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
     if (ln > lg.n0) atomicAdd((unsigned long long*)&st->plog_total, (unsigned long long)(ln - lg.n0));
     if (lg.ovf) st->plog_ovf = 1;
   }
-  close_claims(D, &s_ns);
+  // this workgroup's claims join klist from its chunk (a reservation only when
+  // the chunk runs out; the chunk state was read at kernel start)
+  __syncthreads();
+  {
+    const int32_t n = min(s_ns, (int32_t)D.RC);
+    if (threadIdx.x == 0 && n) {
+      if (s_kl[1] - s_kl[0] < n) {
+        const int64_t sz = max((int64_t)KL_CHUNK, (int64_t)n);
+        s_kl[0] = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
+        s_kl[1] = s_kl[0] + sz;
+      }
+      D.kchunk[2 * blockIdx.x] = s_kl[0] + n;
+      D.kchunk[2 * blockIdx.x + 1] = s_kl[1];
+      atomicAdd((unsigned long long*)&st->nkeys, (unsigned long long)n);
+    }
+    __syncthreads();
+    const int32_t* reg = D.ns + (int64_t)blockIdx.x * D.RC;
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) klist_put(D, s_kl[0] + i, reg[i]);
+  }
+  dbg_stamp(D, 62);
   if (blockIdx.x == 0) {
     int32_t tot;
     block_excl_scan(nm, &tot, s_red);
     if (threadIdx.x == 0) D.log[st->iter - 1].nmerged = (int64_t)tot + min(st->L_ovf, D.Lovf_cap);
   }
+  dbg_stamp(D, 63);
 }
 
 // ====================================================================== multi-rank deltas
@@ -1201,7 +1291,7 @@ __global__ __launch_bounds__(BLOCK) void k_compare(Dev D) {
   const int64_t U = min(D.st->U, D.KCAP);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = D.klist[i];
-    if (D.scratch[d] != D.count[d]) atomicAdd((unsigned long long*)&D.st->nmismatch, 1ULL);
+    if (d >= 0 && D.scratch[d] != D.count[d]) atomicAdd((unsigned long long*)&D.st->nmismatch, 1ULL);
   }
 }
 
@@ -1210,7 +1300,7 @@ __global__ __launch_bounds__(BLOCK) void k_gather_counts(Dev D, int32_t* keys, i
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = D.klist[i];
     keys[i] = d;
-    counts[i] = D.count[d];
+    counts[i] = d >= 0 ? D.count[d] : 0;
   }
 }
 

@@ -276,7 +276,8 @@ class GeoBPEEngine:
         keys = np.zeros(max(U, 1), dtype=np.int32)
         cnt = np.zeros(max(U, 1), dtype=np.int32)
         self.L.geobpe_debug_counts(self._ctx, _p(keys), _p(cnt), U)
-        return keys[:U], cnt[:U]
+        live = keys[:U] >= 0
+        return keys[:U][live], cnt[:U][live]
 
     def key_counts(self) -> dict:
         """{key string: global count} of every key with a positive count."""

@@ -33,15 +33,16 @@ for it in iters:
         continue
     base = t[:, 0].min()
     rel = (t - base) / 100.0  # us
+    rel[:, 63][t[:, 63] == 0] = np.nan
     rel[t == 0] = np.nan
     last = eng.merges[-1]
     print(f"merge {it}: count {last[1]} merged {last[2]}  workgroups {len(t)}")
-    names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end"}
+    names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end", 62: "klist_end", 63: "end"}
     for r in range(2):
         for i, nm in enumerate(["front.loads", "front.agg", "finL.kc", "finL.store", "finL.agg", "finR.kc",
                                 "finR.store", "finR.agg"]):
             names[40 + 10 * r + i] = f"r{r}.{nm}"
-    for k in sorted(range(62), key=lambda k: np.nanmedian(rel[:, k]) if not np.all(np.isnan(rel[:, k])) else 0):
+    for k in sorted(range(64), key=lambda k: np.nanmedian(rel[:, k]) if not np.all(np.isnan(rel[:, k])) else 0):
         col = rel[:, k]
         if np.all(np.isnan(col)):
             continue
