@@ -411,6 +411,13 @@ __device__ inline void agg_flush_hot(A& s, const Dev& D, HotApp& h, bool to_delt
 // there, find-or-claim (CAS) its slot; *claimed = true if this thread inserted it
 __device__ inline u64 ht_first_slot(const Dev& D, u64 k) { return (k * 0xD6E8FEB86659FD93ULL) >> D.ht_shift; }
 
+// a key-table probe that sees claims other workgroups made during this launch
+// (agent scope: skips this CU's stale L1), so late arrivals find the key instead
+// of queueing a CAS on the same slot
+__device__ inline u64 ht_probe(const Dev& D, u64 s) {
+  return __hip_atomic_load(&D.ht_key[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ inline int32_t ht_resolve(const Dev& D, u64 k, u64 s, u64 cur, bool* claimed) {
   const u64 mask = (u64)D.HC - 1;
   *claimed = false;
@@ -429,7 +436,7 @@ __device__ inline int32_t ht_resolve(const Dev& D, u64 k, u64 s, u64 cur, bool* 
       if (old == k) return (int32_t)s;
     }
     s = (s + 1) & mask;
-    cur = D.ht_key[s];
+    cur = ht_probe(D, s);
   }
   set_error(D, GEOBPE_ECAPACITY, -2);
   return -1;
@@ -438,7 +445,7 @@ __device__ inline int32_t ht_resolve(const Dev& D, u64 k, u64 s, u64 cur, bool* 
 __device__ inline int32_t ht_insert(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
   const u64 k = probe_key(h1, h2, len);
   const u64 s = ht_first_slot(D, k);
-  return ht_resolve(D, k, s, D.ht_key[s], claimed);
+  return ht_resolve(D, k, s, ht_probe(D, s), claimed);
 }
 
 // hash of X ++ [g] ++ Y with the powers P^(|Y|syms+1), P^|Y|syms given

@@ -941,7 +941,7 @@ __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const
     hl.len = ll + A.wl;
     hl.k = probe_key(hl.h1, hl.h2, hl.len);
     hl.s = ht_first_slot(D, hl.k);
-    hl.cur = D.ht_key[hl.s];
+    hl.cur = ht_probe(D, hl.s);
     hl.idL = L;
     hl.g = glL;
     hl.idR = A.nid;
@@ -952,7 +952,7 @@ __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const
     hr.len = A.wl + rl;
     hr.k = probe_key(hr.h1, hr.h2, hr.len);
     hr.s = ht_first_slot(D, hr.k);
-    hr.cur = D.ht_key[hr.s];
+    hr.cur = ht_probe(D, hr.s);
     hr.idL = A.nid;
     hr.g = glR;
     hr.idR = idr;
@@ -982,14 +982,73 @@ __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const
 
 // before the round's barrier: look the key up in the workgroup cache; the
 // resolver (or an uncached thread) gets the dense id from the global table
-__device__ inline void half_resolve(const Dev& D, KeyCache& kc, int32_t* s_ns, int32_t* s_chk, Half& x) {
-  x.kcs = kc_find(kc, x.k, &x.res);
-  x.d = -1;
-  if (!x.res) return;
-  x.d = key_id_now(D, s_ns, s_chk, x.k, x.s, x.cur, x.h1, x.h2, x.len, x.idL, x.g, x.idR);
-  if (x.kcs >= 0) {
-    kc.h1[x.kcs] = x.h1;
-    kc.id[x.kcs] = x.d >= 0 ? x.d : -2;
+// after a claimed/found slot: payload + klist note, or the EHASH check record
+__device__ inline int32_t key_done(const Dev& D, int32_t* s_ns, int32_t* s_chk, const Half& x, int32_t slot,
+                                   bool claimed) {
+  if (slot < 0) return -1;
+  if (claimed) {
+    claim_payload(D, slot, x.h1, x.h2, x.len, x.idL, x.g, x.idR);
+    note_claim(D, s_ns, slot);
+  } else {
+    emit_check(D, s_chk, slot, x.len, x.h1, x.h2);
+  }
+  return slot;
+}
+
+// Before the round's barrier: look both halves up in the workgroup cache; the
+// resolvers go to the global table.  A key first seen in this launch is probed
+// by up to one resolver per workgroup at about the same time: a CAS each would
+// queue ~256 same-address atomics (~70 ns apiece).  So a resolver that finds the
+// slot empty waits a workgroup-dependent moment and probes again (agent scope),
+// and CASes only if it is still empty; the L and R halves' first CASes are
+// issued back to back.
+__device__ inline void halves_resolve(const Dev& D, KeyCache& kc, int32_t* s_ns, int32_t* s_chk, Half& a, bool va,
+                                      Half& b, bool vb) {
+  if (va) a.kcs = kc_find(kc, a.k, &a.res);
+  if (vb) b.kcs = kc_find(kc, b.k, &b.res);
+  a.d = b.d = -1;
+  const bool ra = va && a.res, rb = vb && b.res;
+  u64 ca = ra ? a.cur : 1, cb = rb ? b.cur : 1;  // (1: no slot work for that half)
+  if ((ra && ca == 0) || (rb && cb == 0)) {
+    for (int i = 0; i < 1 + (int)(blockIdx.x & 15); i++) __builtin_amdgcn_s_sleep(2);
+    if (ra && ca == 0) ca = ht_probe(D, a.s);
+    if (rb && cb == 0) cb = ht_probe(D, b.s);
+  }
+  u64 oa = ca, ob = cb;
+  bool cla = false, clb = false;
+  if (ra && ca == 0) oa = atomicCAS((unsigned long long*)&D.ht_key[a.s], 0ULL, (unsigned long long)a.k);
+  if (rb && cb == 0) ob = atomicCAS((unsigned long long*)&D.ht_key[b.s], 0ULL, (unsigned long long)b.k);
+  if (ra) {
+    int32_t slot;
+    if (ca == 0 && oa == 0) {
+      cla = true;
+      slot = (int32_t)a.s;
+    } else if (oa == a.k) {
+      slot = (int32_t)a.s;
+    } else {  // another key here: probe on
+      slot = ht_resolve(D, a.k, (a.s + 1) & ((u64)D.HC - 1), ht_probe(D, (a.s + 1) & ((u64)D.HC - 1)), &cla);
+    }
+    a.d = key_done(D, s_ns, s_chk, a, slot, cla);
+  }
+  if (rb) {
+    int32_t slot;
+    if (cb == 0 && ob == 0) {
+      clb = true;
+      slot = (int32_t)b.s;
+    } else if (ob == b.k) {
+      slot = (int32_t)b.s;
+    } else {
+      slot = ht_resolve(D, b.k, (b.s + 1) & ((u64)D.HC - 1), ht_probe(D, (b.s + 1) & ((u64)D.HC - 1)), &clb);
+    }
+    b.d = key_done(D, s_ns, s_chk, b, slot, clb);
+  }
+  if (va && a.res && a.kcs >= 0) {
+    kc.h1[a.kcs] = a.h1;
+    kc.id[a.kcs] = a.d >= 0 ? a.d : -2;
+  }
+  if (vb && b.res && b.kcs >= 0) {
+    kc.h1[b.kcs] = b.h1;
+    kc.id[b.kcs] = b.d >= 0 ? b.d : -2;
   }
 }
 
@@ -1121,8 +1180,7 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
       apply_front(D, agg, hot, e, A, hl, vl, hr, vr, j0 < 2 * ABLOCK ? 40 + 10 * (int)(j0 / ABLOCK) : -1);
     }
     dbg_stamp(D, dbk++);
-    if (vl) half_resolve(D, kc, &s_ns, &s_chk, hl);
-    if (vr) half_resolve(D, kc, &s_ns, &s_chk, hr);
+    if (vl || vr) halves_resolve(D, kc, &s_ns, &s_chk, hl, vl, hr, vr);
     dbg_stamp(D, dbk++);
     __syncthreads();
     dbg_stamp(D, dbk++);

@@ -38,6 +38,7 @@ for it in iters:
     last = eng.merges[-1]
     print(f"merge {it}: count {last[1]} merged {last[2]}  workgroups {len(t)}")
     names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end", 62: "klist_end", 63: "end"}
+    names.update({30: "r0.kcL", 31: "r0.globalL", 32: "r0.kcR", 33: "r0.globalR"})
     for r in range(2):
         for i, nm in enumerate(["front.loads", "front.agg", "finL.kc", "finL.store", "finL.agg", "finR.kc",
                                 "finR.store", "finR.agg"]):
