@@ -22,12 +22,15 @@ constexpr int RPB = 8;         // mark regions per apply workgroup (NB = RPB * N
 constexpr int CL_MIN_SHRINK = 4096;  // hot-list length above which a 4x drop of theta re-scans
 constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per region)
 constexpr int NBKT = 1 << NBKT_LOG2;
-constexpr int SKIP_HOT = 1, SKIP_POST = 2;  // what a rebuild iteration rebuilds
+constexpr int SKIP_HOT = 1, SKIP_POST = 2, SKIP_MEASURE = 4;  // what a rebuild iteration does
 constexpr int DBG_SLOTS = 64;
 constexpr int PW_LDS = 2048;    // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
 constexpr int KL_CHUNK = 4096;  // klist entries an apply workgroup reserves at a time
 
 // ------------------------------------------------------------------ records
+// Kernel-to-kernel state.  No field is written by a kernel that other
+// workgroups of the same kernel read: k_mark reads State and writes only Sel
+// (its workgroup 0); k_apply reads Sel and its workgroup 0 writes State.
 struct State {
   // persistent
   int64_t U;          // klist entries reserved (keys + unused chunk tails)
@@ -36,29 +39,42 @@ struct State {
   int64_t err_pos;
   int64_t epoch;      // delta-touch epoch (multi-rank)
   int32_t K;          // len(_tokens) on the device
-  int32_t iter;       // merges selected so far
-  int32_t tag;        // role tag of the current merge (= iter)
+  int32_t iter;       // merges made so far
   int32_t done;       // 1 once no pair is left
-  int32_t W, nid, maxc, ncand;
-  // the winner, set by k_select for k_mark / k_apply
-  u64 w1, w2;                      // content hash of the merged token
-  int32_t wl, wfp;                 // residues of W, key_fp(W)
-  int32_t widL, wg, widR;          // W's representative: the new token's content parts
-  // per-iteration, reset by k_select
-  int64_t L_ovf, np_ovf, ns_ovf, nL_total;
+  int32_t maxc, ncand;  // the last merge's count and tied keys (stats)
+  int32_t pad0;
+  // per launch pair: merge entries past the mark regions, by launch parity
+  int64_t L_ovf2[2];
+  // per bin / import launch
+  int64_t np_ovf, ns_ovf, nL_total;
   int64_t ntouched, nmismatch;
-  // hot list (argmax): every key with count >= theta is in clist[0..ncl)
-  int64_t ncl;
-  int32_t theta;      // 0 = list not built yet
+  // hot list (argmax): every key with count >= theta is in clist[0..ncl2[cl_act])
+  int64_t ncl2[2];
+  int32_t cl_act;      // active list counter
+  int32_t theta;       // 0 = list not built yet
   int32_t cl_valid;
-  int32_t skip;       // this iteration only rebuilds the hot list (no merge)
-  int32_t theta_new;  // threshold of that rebuild
-  int64_t nskip;      // rebuild iterations so far (stats)
-  int64_t nunchecked; // found-key records beyond the check regions (not verified)
+  int32_t pad1;
+  int64_t cl_measured; // max count found by a measure iteration
+  int64_t nskip;       // rebuild iterations so far (stats)
+  int64_t nunchecked;  // found-key records beyond the check regions (not verified)
   // posting index (k_mark): bucket-sorted (key, slot) per region + the log of
   // pairs made since its last rebuild
   int32_t post_valid, plog_ovf;
   int64_t plog_total, npost;
+};
+
+// The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
+// and the host read it).  Every mark workgroup computes the same decision.
+constexpr int SEL_MERGE = 0, SEL_SKIP = 1, SEL_DONE = 2;
+struct Sel {
+  int32_t decision;
+  int32_t skip;       // SKIP_* bits of a rebuild iteration
+  int32_t theta_new;  // hot-list rebuild threshold
+  int32_t build;      // hot-list counter the rebuild fills
+  int32_t W, nid, iter, tag;
+  int32_t maxc, ncand, wl, wfp;
+  int32_t widL, wg, widR, pad;
+  u64 w1, w2;         // content hash of the new token
 };
 
 struct LEntry {  // one merge: left token a (+ its prev p), right token b (+ next c)
@@ -142,6 +158,7 @@ struct Dev {
   int64_t candcap;
   LogRec* log;
   State* st;
+  Sel* sel;  // [2], by launch parity
 };
 
 // ------------------------------------------------------------------ arithmetic
@@ -358,20 +375,21 @@ __device__ inline void hot_store(const Dev& D, int64_t k, int32_t d) {
   if (k < D.KCAP)
     D.clist[k] = d;
   else
-    D.st->cl_valid = 0;  // list lost an entry: the next k_select rebuilds it
+    D.st->cl_valid = 0;  // list lost an entry: the next k_mark has it rebuilt
 }
 __device__ inline void hot_push(const Dev& D, HotApp& h, int32_t d) {
   const int32_t j = atomicAdd(&h.n, 1);
   if (j < HOT_BUF)
     h.buf[j] = d;
   else
-    hot_store(D, (int64_t)atomicAdd((unsigned long long*)&D.st->ncl, 1ULL), d);
+    hot_store(D, (int64_t)atomicAdd((unsigned long long*)&D.st->ncl2[D.st->cl_act], 1ULL), d);
 }
 __device__ inline void hot_flush(const Dev& D, HotApp& h) {
   __shared__ int64_t s_base;
   __syncthreads();
   const int32_t n = min(h.n, HOT_BUF);
-  if (threadIdx.x == 0 && n > 0) s_base = (int64_t)atomicAdd((unsigned long long*)&D.st->ncl, (unsigned long long)n);
+  if (threadIdx.x == 0 && n > 0)
+    s_base = (int64_t)atomicAdd((unsigned long long*)&D.st->ncl2[D.st->cl_act], (unsigned long long)n);
   __syncthreads();
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) hot_store(D, s_base + i, h.buf[i]);
 }

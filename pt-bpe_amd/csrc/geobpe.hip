@@ -3,15 +3,16 @@
 //
 // Replaces the Python/dict hot path of foldingdiff/bpe.py (BPE.initialize /
 // bin / step / quantize).  Integer work only (no
-// MFMA).  One merge iteration is four stream-ordered launches with no host
+// MFMA).  One merge iteration is three stream-ordered launches with no host
 // synchronisation:
-//   k_select                            hot-list max count, tied keys, reference
-//                                       key-string tie-break, new token (device)
-//   k_mark                              scan pk for the winner, greedy run walks
-//   k_apply                             rewrite tokens, count deltas, new pairs,
-//                                       dense ids for new keys (one reservation
-//                                       per workgroup)
-//   k_finalize                          pk + counts of the new pairs
+//   k_select  one workgroup: hot-list argmax + reference key-string tie-break,
+//             the decision record (Sel) and merge-log entry
+//   k_mark    the winner's occurrences (posting index or fingerprint scan) and
+//             greedy run walks
+//   k_apply   rewrite tokens, count deltas, new pair keys (claimed in place),
+//             posting log; rebuild iterations (hot list / posting index)
+// The bin pass is k_pairs_all + k_finalize.
+
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -51,7 +52,9 @@ struct geobpe_ctx {
   std::vector<std::vector<int32_t>> vocab;
   int32_t K0 = 0;
   int ncu = 256;
-  int nb = 2048;  // mark / argmax workgroups (= D.NB)
+  int nb = 2048;  // mark workgroups (= D.NB)
+  int64_t gen = 0;            // merge-loop launch pairs so far (parity selects Sel / overflow buffers)
+  bool mark_pending = false;  // step_select decided a merge whose mark/apply are due
   int nba = 256;  // apply / finalize / assign / bin / import workgroups (= D.NBA)
   // profiling
   bool prof = false;
@@ -174,7 +177,7 @@ int sync_state(geobpe_ctx* c) {
 
 // zero the overflow / new-key counters before a bin() or an import chunk
 int reset_region_counters(geobpe_ctx* c) {
-  HIPCHK(c, hipMemsetAsync(&c->D.st->L_ovf, 0, 4 * sizeof(int64_t), c->stream));
+  HIPCHK(c, hipMemsetAsync(&c->D.st->np_ovf, 0, 3 * sizeof(int64_t), c->stream));
   return 0;
 }
 
@@ -226,25 +229,40 @@ int alloc_keys(geobpe_ctx* c) {
 }
 
 // the launches of one merge iteration (no host synchronisation)
-void enqueue_select(geobpe_ctx* c) {
-  Timed t(c, "select");
-  hipLaunchKernelGGL(k_select, dim3(1), dim3(BLOCK), 0, c->stream, c->D);
-}
-
 void enqueue_commit(geobpe_ctx* c, bool to_delta) {
   Timed t(c, "finalize");
   hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, to_delta ? 1 : 0);
 }
 
+// one merge iteration = k_select (argmax, decision) -> k_mark (occurrences) ->
+// k_apply, on launch parity gen & 1 (the double-buffered Sel record and
+// merge-overflow counter)
+void enqueue_select(geobpe_ctx* c) {
+  Timed t(c, "select");
+  hipLaunchKernelGGL(k_select, dim3(1), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
+}
+void enqueue_mark(geobpe_ctx* c) {
+  Timed t(c, "mark");
+  hipLaunchKernelGGL(k_mark, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
+}
 void enqueue_apply(geobpe_ctx* c) {
   {
-    Timed t(c, "mark");
-    hipLaunchKernelGGL(k_mark, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
-  }
-  {
     Timed t(c, "apply");
-    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0);
+    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0,
+                       (int)(c->gen & 1));
   }
+  c->gen++;
+}
+void enqueue_iteration(geobpe_ctx* c) {
+  enqueue_select(c);
+  enqueue_mark(c);
+  enqueue_apply(c);
+}
+
+// the Sel record of the last mark launch (after a sync)
+int read_sel(geobpe_ctx* c, Sel* out) {
+  HIPCHK(c, hipMemcpy(out, c->D.sel + (c->gen & 1), sizeof(Sel), hipMemcpyDeviceToHost));
+  return 0;
 }
 
 }  // namespace
@@ -268,7 +286,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   HIPCHK(c, hipHostMalloc((void**)&c->h_state, sizeof(State), hipHostMallocDefault));
   memset(c->h_state, 0, sizeof(State));
   int rc;
-  if ((rc = dalloc(c, &c->D.st, 1, 0))) return rc;
+  if ((rc = dalloc(c, &c->D.st, 1, 0)) || (rc = dalloc(c, &c->D.sel, 2, 0))) return rc;
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->ncu = prop.multiProcessorCount;
@@ -337,7 +355,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
       (rc = dalloc(c, &D.chk, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chkcnt, c->nba, 0)))
     return rc;
   // posting index: one residue region per apply workgroup; the log holds the pairs
-  // made since the last rebuild (k_select rebuilds when it passes LOGMAX)
+  // made since the last rebuild (k_mark has it rebuilt when it passes LOGMAX)
   D.PR = (c->R + c->nba - 1) / c->nba;
   D.LOGMAX = std::max<int64_t>((int64_t)c->nba * 64, c->R / 32);
   D.PLC = 4 * D.LOGMAX / c->nba + 64;
@@ -528,29 +546,36 @@ int geobpe_bin(geobpe_ctx* c) {
 
 int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {
   if (!c || !c->keys_ready || !new_id) return GEOBPE_EARG;
+  if (c->mark_pending) return fail(c, GEOBPE_EARG, "step_select twice without step_apply");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  Sel sel;
   for (;;) {
     enqueue_select(c);
     HIPCHK(c, hipGetLastError());
-    if ((rc = sync_state(c))) return rc;
-    if (c->h_state->done || !c->h_state->skip) break;
-    enqueue_apply(c);  // a hot-list rebuild iteration (rank-local, same decision on every rank)
+    if ((rc = sync_state(c)) || (rc = read_sel(c, &sel))) return rc;
+    if (sel.decision == SEL_MERGE) break;
+    enqueue_apply(c);  // a rebuild iteration (rank-local: every rank then selects the same winner) or done
+    if (sel.decision == SEL_DONE) {
+      if ((rc = sync_state(c))) return rc;
+      *new_id = -1;
+      if (count) *count = 0;
+      return 0;
+    }
   }
-  if (c->h_state->done) {
-    *new_id = -1;
-    if (count) *count = 0;
-    return 0;
-  }
-  *new_id = c->h_state->nid;
-  if (count) *count = c->h_state->maxc;
+  c->mark_pending = true;
+  *new_id = sel.nid;
+  if (count) *count = sel.maxc;
   return 0;
 }
 
 int geobpe_step_apply(geobpe_ctx* c, int64_t* n_merged) {
   if (!c || !c->keys_ready) return GEOBPE_EARG;
+  if (!c->mark_pending) return fail(c, GEOBPE_EARG, "step_apply without step_select");
   HIPCHK(c, hipSetDevice(c->device));
+  enqueue_mark(c);
   enqueue_apply(c);
+  c->mark_pending = false;
   HIPCHK(c, hipGetLastError());
   if (n_merged) {
     int rc;
@@ -569,9 +594,8 @@ int geobpe_step(geobpe_ctx* c, int32_t* new_id, int32_t* count, int64_t* n_merge
   HIPCHK(c, hipSetDevice(c->device));
   const int32_t it0 = c->h_state->iter;
   int rc;
-  for (;;) {  // an iteration that only rebuilt the hot list merges nothing: go again
-    enqueue_select(c);
-    enqueue_apply(c);
+  for (;;) {  // a rebuild iteration merges nothing: go again
+    enqueue_iteration(c);
     HIPCHK(c, hipGetLastError());
     if ((rc = sync_state(c))) return rc;
     if (c->h_state->iter != it0 || c->h_state->done) break;
@@ -599,10 +623,7 @@ int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) {
   int rc;
   // hot-list rebuild iterations merge nothing: top up until n merges or done
   for (int64_t want = n_iters; want > 0;) {
-    for (int64_t i = 0; i < want; i++) {
-      enqueue_select(c);
-      enqueue_apply(c);
-    }
+    for (int64_t i = 0; i < want; i++) enqueue_iteration(c);
     HIPCHK(c, hipGetLastError());
     if ((rc = sync_state(c))) return rc;
     if (c->h_state->done) break;

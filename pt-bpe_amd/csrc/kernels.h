@@ -260,14 +260,14 @@ __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, cons
   agg_add_hot(agg, D, hot, d, e.delta, to_delta, th);
 }
 
-// a hot-list rebuild iteration (k_select set st->skip; run by k_apply's grid):
-// clist = every key with count >= theta_new.  Two coalesced passes over this
-// workgroup's share of klist; one global reservation per workgroup.
-__device__ void rebuild_hot_list(const Dev& D) {
+// a hot-list rebuild iteration (k_mark chose it; run by k_apply's grid):
+// counter `build` (zeroed by k_mark) and clist = every key with count >= th.
+// Two coalesced passes over this workgroup's share of klist; one global
+// reservation per workgroup.
+__device__ void rebuild_hot_list(const Dev& D, int32_t th, int32_t build) {
   __shared__ int32_t s_red[ABLOCK / 64];
   __shared__ int64_t s_base;
   State* st = D.st;
-  const int32_t th = st->theta_new;
   const int64_t U = min(st->U, D.KCAP);
   const int64_t per = (U + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
@@ -282,7 +282,8 @@ __device__ void rebuild_hot_list(const Dev& D) {
   }
   int32_t tot;
   const int32_t ex = block_excl_scan(n, &tot, s_red);
-  if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&st->ncl, (unsigned long long)tot) : 0;
+  if (threadIdx.x == 0)
+    s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&st->ncl2[build], (unsigned long long)tot) : 0;
   __syncthreads();
   int64_t j = s_base + ex;
   for (int64_t i = lo + threadIdx.x; i < hi; i += UNR * ABLOCK) {
@@ -294,9 +295,32 @@ __device__ void rebuild_hot_list(const Dev& D) {
       if (d[u] >= 0 && D.count[d[u]] >= th) D.clist[j++] = d[u];  // j < U <= KCAP
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->cl_act = build;
     st->theta = th;
     st->cl_valid = 1;
+    st->cl_measured = 0;
   }
+}
+
+// a measure iteration: the global maximum count (the hot list must be rebuilt
+// from scratch and its threshold needs it)
+__device__ void measure_max(const Dev& D) {
+  __shared__ int32_t s_red[ABLOCK / 64];
+  const int64_t U = min(D.st->U, D.KCAP);
+  const int64_t per = (U + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
+  constexpr int UNR = 16;
+  int32_t m = 0;
+  for (int64_t i = lo + threadIdx.x; i < hi; i += UNR * ABLOCK) {
+    int32_t d[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) d[u] = i + u * ABLOCK < hi ? D.klist[i + u * ABLOCK] : -1;
+#pragma unroll
+    for (int u = 0; u < UNR; u++)
+      if (d[u] >= 0) m = max(m, D.count[d[u]]);
+  }
+  m = block_max(m, s_red);
+  if (threadIdx.x == 0 && m > 0) atomicMax((unsigned long long*)&D.st->cl_measured, (unsigned long long)m);
 }
 
 // posting-index rebuild (a rebuild iteration, run by k_apply's grid): workgroup r
@@ -498,30 +522,55 @@ __device__ inline bool key_less(const Dev& D, int32_t a, int32_t b, char* lds) {
   }
 }
 
-// BPE.step's argmax (bpe.py:1796-1800, SortedDict peekitem(0)): ONE workgroup
-// over the hot list -- every key with count >= theta is in clist, so when the
-// list maximum m >= theta it is the global maximum and all keys tied at m are in
-// the list.  Otherwise (or when the list has grown long while m >= 4 theta) this
-// iteration is a rebuild: st->skip, theta_new = max(1, m/2) <= the true maximum,
-// and k_finalize re-scans the counts.  Then the reference tie-break (smallest key
-// string) and the new token (bpe.py:1857-1860): id, vocab hash / content, merge log.
-constexpr int SEL_TIES = 256;
-__global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
+// BPE.step's argmax (bpe.py:1796-1800, SortedDict peekitem(0)), by one
+// workgroup (k_select): every key with
+// count >= theta is in clist[0..n), so when the list maximum m >= theta it is the
+// global maximum and every key tied at m is in the list.  Otherwise (or when the
+// list has grown long while m >= 4 theta) the launch pair is a rebuild
+// iteration with theta_new = max(1, m/2) <= the true maximum; an invalid list
+// is first re-measured.  Ties: the smallest reference key string
+// (bpe.py:1469-1471) via the device JSON generator.  It records the decision
+// in Sel[par], the merge log entry and the new token's hash
+// (_tokens[n] = json.loads(key), bpe.py:1857-1860; its content is written by
+// k_apply's workgroup 0).
+__device__ int32_t mark_select(const Dev& D, int par, int32_t* W_out) {
   __shared__ int32_t s_red[BLOCK / 64];
-  __shared__ int32_t s_nc;
-  __shared__ int32_t s_tie[SEL_TIES];
   __shared__ int32_t s_best[BLOCK];
   __shared__ char s_jbuf[48 * BLOCK];
   State* st = D.st;
-  // the first 4*BLOCK list entries are loaded together with the state (clist has
-  // KCAP >= 4*BLOCK entries; entries past ncl are masked below)
+  Sel* out = D.sel + par;
+  const bool rec = blockIdx.x == 0 && threadIdx.x == 0;
+  const int32_t act = st->cl_act;
+  // the first 4*BLOCK list entries are loaded with the state (clist has KCAP >=
+  // 4*BLOCK entries; entries past n are masked below)
   int32_t d0[4];
 #pragma unroll
   for (int q = 0; q < 4; q++) d0[q] = D.clist[threadIdx.x + q * BLOCK];
-  if (st->done) return;
-  const int64_t n = st->ncl;
-  const int32_t th = st->theta;
+  const int64_t n = st->ncl2[act];
+  const int32_t th = st->theta, iter = st->iter, K = st->K;
   const bool valid = st->cl_valid != 0;
+  if (st->done) {
+    if (rec) out->decision = SEL_DONE;
+    return SEL_DONE;
+  }
+  if (!valid) {  // no usable list: measure the maximum, then rebuild at half of it
+    const Sel& prev = D.sel[par ^ 1];
+    const bool measured = prev.decision == SEL_SKIP && (prev.skip & SKIP_MEASURE);
+    const int64_t ms = measured ? st->cl_measured : 0;
+    if (rec) {
+      if (measured && ms == 0) {
+        out->decision = SEL_DONE;
+        out->maxc = 0;
+      } else {
+        out->decision = SEL_SKIP;
+        out->skip = measured ? SKIP_HOT : SKIP_MEASURE;
+        out->theta_new = (int32_t)max((int64_t)1, ms / 2);
+        out->build = act ^ 1;
+        st->ncl2[act ^ 1] = 0;  // (no mark workgroup reads the idle counter)
+      }
+    }
+    return measured && ms == 0 ? SEL_DONE : SEL_SKIP;
+  }
   // pass over the list: 4 entries per thread in flight; keep this thread's best
   int32_t m = 0, mkey = -1, mcnt = 0;
   for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {
@@ -545,111 +594,98 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D) {
     }
   }
   const int32_t gm = block_max(m, s_red);
-  const bool hot = !valid || gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th);
-  if (hot && valid && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
-    if (threadIdx.x == 0) {
-      st->done = 1;
-      st->maxc = 0;
+  const bool hot = gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th);
+  if (hot && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
+    if (rec) {
+      out->decision = SEL_DONE;
+      out->maxc = 0;
     }
-    return;
+    return SEL_DONE;
   }
   // posting index stale (log full / overflowed / never built) and the merges are
   // small enough that a rebuild lasts >= 64 iterations: rebuild it this iteration
   const bool post = !hot && (st->post_valid == 0 || st->plog_ovf != 0 || st->plog_total > D.LOGMAX) &&
                     (int64_t)gm * 64 <= D.LOGMAX;
   if (hot || post) {
-    if (threadIdx.x == 0) {
-      if (hot) {
-        st->theta_new = max(1, gm / 2);
-        st->ncl = 0;
-        st->cl_valid = 0;
-      }
-      st->skip = (hot ? SKIP_HOT : 0) | (post ? SKIP_POST : 0);
-      st->nskip += 1;
+    if (rec) {
+      out->decision = SEL_SKIP;
+      out->skip = (hot ? SKIP_HOT : 0) | (post ? SKIP_POST : 0);
+      out->theta_new = max(1, gm / 2);
+      out->build = act ^ 1;
+      if (hot) st->ncl2[act ^ 1] = 0;
     }
-    return;
+    return SEL_SKIP;
   }
-  if (threadIdx.x == 0) s_nc = 0;
-  __syncthreads();
-  // keys tied at the maximum (a thread with several re-reads its own entries)
+  // each thread's smallest tied key (a thread with several re-reads its own entries)
+  int32_t best = -1, ntie = 0;
+  char* jb = s_jbuf + 48 * threadIdx.x;
   if (m == gm) {
     if (mcnt == 1) {
-      const int32_t j = atomicAdd(&s_nc, 1);
-      if (j < SEL_TIES) s_tie[j] = mkey; else if (j < D.candcap) D.cand[j] = mkey;
+      best = mkey;
+      ntie = 1;
     } else {
       for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
         const int32_t d = D.clist[i];
         if (D.count[d] == gm) {
-          const int32_t j = atomicAdd(&s_nc, 1);
-          if (j < SEL_TIES) s_tie[j] = d; else if (j < D.candcap) D.cand[j] = d;
+          ntie++;
+          if (best < 0 || (d != best && key_less(D, d, best, jb))) best = d;
         }
       }
     }
   }
+  int32_t nt;
+  block_excl_scan(ntie, &nt, s_red);
+  s_best[threadIdx.x] = best;
   __syncthreads();
-  const int32_t nc = min(s_nc, (int32_t)D.candcap);
-  if (s_nc > D.candcap && threadIdx.x == 0) set_error(D, GEOBPE_ECAPACITY, -8);
-  int32_t W;
-  if (nc == 1) {
-    W = s_tie[0];
-  } else {  // tie-break: smallest reference key string (SortedDict order, bpe.py:1469-1471)
-    int32_t best = -1;
-    for (int32_t i = threadIdx.x; i < nc; i += blockDim.x) {
-      const int32_t d = i < SEL_TIES ? s_tie[i] : D.cand[i];
-      if (best < 0 || (d != best && key_less(D, d, best, s_jbuf + 48 * threadIdx.x))) best = d;
+  for (int o = BLOCK / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const int32_t a = s_best[threadIdx.x], b = s_best[threadIdx.x + o];
+      if (a < 0 || (b >= 0 && b != a && key_less(D, b, a, jb))) s_best[threadIdx.x] = b;
     }
-    s_best[threadIdx.x] = best;
     __syncthreads();
-    for (int o = BLOCK / 2; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) {
-        const int32_t a = s_best[threadIdx.x], b = s_best[threadIdx.x + o];
-        if (a < 0 || (b >= 0 && b != a && key_less(D, b, a, s_jbuf + 48 * threadIdx.x))) s_best[threadIdx.x] = b;
-      }
-      __syncthreads();
-    }
-    W = s_best[0];
   }
-  const int32_t nid = st->K;
-  if (nid >= D.KC) {
-    if (threadIdx.x == 0) {
+  const int32_t W = s_best[0];
+  *W_out = W;
+  if (K >= D.KC) {
+    if (rec) {
       set_error(D, GEOBPE_ECAPACITY, -9);
-      st->done = 1;
+      out->decision = SEL_DONE;
     }
-    return;
+    return SEL_DONE;
   }
-  if (threadIdx.x == 0) {  // (the new token's content is written by k_apply's workgroup 0)
+  if (rec) {
     const int32_t L = D.krep[3 * (int64_t)W], g = D.krep[3 * (int64_t)W + 1], Rr = D.krep[3 * (int64_t)W + 2];
     const u64 w1 = D.kh1[W], w2 = D.kh2[W];
     const int32_t wl = D.klen[W];
-    D.vh1[nid] = w1;
-    D.vh2[nid] = w2;
-    D.vlen[nid] = wl;
+    D.vh1[K] = w1;
+    D.vh2[K] = w2;
+    D.vlen[K] = wl;
     LogRec lr;
-    lr.nid = nid;
+    lr.nid = K;
     lr.count = gm;
     lr.W = W;
     lr.idL = L;
     lr.g = g;
     lr.idR = Rr;
     lr.nmerged = 0;
-    D.log[st->iter] = lr;
-    st->K = nid + 1;
-    st->iter += 1;
-    st->tag = st->iter;
-    st->skip = 0;
-    st->W = W;
-    st->nid = nid;
-    st->maxc = gm;
-    st->ncand = nc;
-    st->L_ovf = st->np_ovf = st->ns_ovf = st->nL_total = 0;
-    st->w1 = w1;
-    st->w2 = w2;
-    st->wl = wl;
-    st->wfp = key_fp(W);
-    st->widL = L;
-    st->wg = g;
-    st->widR = Rr;
+    D.log[iter] = lr;
+    out->decision = SEL_MERGE;
+    out->skip = 0;
+    out->W = W;
+    out->nid = K;
+    out->iter = iter;
+    out->tag = iter + 1;
+    out->maxc = gm;
+    out->ncand = nt;
+    out->w1 = w1;
+    out->w2 = w2;
+    out->wl = wl;
+    out->wfp = key_fp(W);
+    out->widL = L;
+    out->wg = g;
+    out->widR = Rr;
   }
+  return SEL_MERGE;
 }
 
 // ====================================================================== merge-apply
@@ -670,7 +706,7 @@ __device__ inline void check_found(const Dev& D, int32_t r) {
 // (t, b), skip the pair (b, c), merge (c, d) if it is W too, ...  Independent
 // loads are issued together: two dependent rounds per hit, two per run step.
 __device__ inline void emit_merge(const Dev& D, int32_t* s_n, int32_t t, int32_t p, int32_t b, int32_t c,
-                                  int32_t tag) {
+                                  int32_t tag, int64_t* lovf) {
   LEntry e;
   e.a = t;
   e.p = p;
@@ -682,7 +718,7 @@ __device__ inline void emit_merge(const Dev& D, int32_t* s_n, int32_t t, int32_t
   if (j < D.LC) {
     D.L[(int64_t)blockIdx.x * D.LC + j] = e;
   } else {
-    const int64_t k = atomicAdd((unsigned long long*)&D.st->L_ovf, 1ULL);
+    const int64_t k = atomicAdd((unsigned long long*)lovf, 1ULL);
     if (k < D.Lovf_cap)
       D.Lovf[k] = e;
     else
@@ -690,7 +726,7 @@ __device__ inline void emit_merge(const Dev& D, int32_t* s_n, int32_t t, int32_t
   }
 }
 
-__device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag, int32_t* s_n) {
+__device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag, int32_t* s_n, int64_t* lovf) {
   const int32_t pkg = D.pk[g], p = D.tprev[g], lg = D.tlen[g];
   if (pkg != W) return;
   int32_t b = g + lg;
@@ -700,7 +736,7 @@ __device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag,
   int32_t t = g, pp = p;
   for (;;) {
     const int32_t c = pkb >= 0 ? b + lb : -1;
-    emit_merge(D, s_n, t, pp, b, c, tag);
+    emit_merge(D, s_n, t, pp, b, c, tag, lovf);
     if (pkb != W) break;
     const int32_t pkc = D.pk[c], lc = D.tlen[c];
     if (pkc != W) break;
@@ -713,20 +749,28 @@ __device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag,
   }
 }
 
-// find the winner's occurrences and start a walk at every run start.  Posting
+// The winner's occurrences, starting a walk at every run start.  Posting
 // mode (index valid): O(bucket + log) reads.  Otherwise scan the 16-bit key
 // fingerprints (4 x 16 B per lane in flight; each workgroup owns CH8 8-slot
 // groups), confirm on pk.  Either way one merge region per workgroup.
-__global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
+// one workgroup: the decision of this launch triple (Sel[par])
+__global__ __launch_bounds__(BLOCK) void k_select(Dev D, int par) {
+  int32_t W;
+  mark_select(D, par, &W);
+}
+
+__global__ __launch_bounds__(BLOCK) void k_mark(Dev D, int par) {
   __shared__ int32_t s_n;
   const bool posting = D.st->post_valid && !D.st->plog_ovf;
+  const Sel& sel = D.sel[par];
   if (!posting && blockIdx.x < D.NBA) check_found(D, blockIdx.x);
-  if (D.st->done || D.st->skip) {
+  if (sel.decision != SEL_MERGE) {
     if (posting && blockIdx.x % RPB == RPB - 1) check_found(D, blockIdx.x / RPB);
     return;
   }
-  const int32_t W = D.st->W, tag = D.st->tag;
-  const uint32_t fW = (uint32_t)D.st->wfp;
+  const int32_t W = sel.W, tag = sel.tag;
+  const uint32_t fW = (uint32_t)sel.wfp;
+  int64_t* lovf = &D.st->L_ovf2[par];
   if (threadIdx.x == 0) s_n = 0;
   __syncthreads();
   if (posting) {
@@ -751,7 +795,7 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
       const int2 e = i < n1 ? P[i] : Lg[i];
       if (e.x == W) {
         const int32_t g = e.y;
-        mark_hit(D, g, W, tag, &s_n);
+        mark_hit(D, g, W, tag, &s_n, lovf);
       }
     }
     __syncthreads();
@@ -777,7 +821,7 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D) {
         const uint32_t f = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
         if (f == fW) {
           const int32_t g = (int32_t)(8 * (i0 + u * BLOCK) + q);
-          mark_hit(D, g, W, tag, &s_n);
+          mark_hit(D, g, W, tag, &s_n, lovf);
         }
       }
     }
@@ -1076,7 +1120,7 @@ __device__ inline void half_finish(const Dev& D, AggBig& agg, HotApp& hot, KeyCa
 // regions (+ its share of the overflow list), in block-uniform rounds: front
 // half, key resolution, barrier, finish.  Also the merge log's n_merged, and
 // the rebuild iterations (hot list / posting index) k_select requests.
-__global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
+__global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta, int par) {
   // the posting rebuild's histogram and the merge's partial counts never live in
   // the same launch: one 64 KB LDS buffer
   __shared__ union {
@@ -1093,29 +1137,39 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   __shared__ int32_t s_red[ABLOCK / 64];
   __shared__ u64 s_pw[2 * PW_LDS];
   __shared__ int64_t s_kl[2];
-  if (D.st->done) return;
-  if (D.st->skip) {
-    const int32_t sk = D.st->skip;
-    if (sk & SKIP_HOT) rebuild_hot_list(D);
-    if (sk & SKIP_POST) rebuild_postings(D, u.hist);
+  State* st = D.st;
+  const Sel sel = D.sel[par];  // this launch pair's decision (k_mark)
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st->L_ovf2[par ^ 1] = 0;  // the next mark's overflow counter (idle since the last pair)
+    if (sel.decision == SEL_DONE) {
+      st->done = 1;
+      st->maxc = 0;
+    } else if (sel.decision == SEL_SKIP) {
+      st->nskip += 1;
+    }
+  }
+  if (sel.decision == SEL_DONE) return;
+  if (sel.decision == SEL_SKIP) {
+    if (sel.skip & SKIP_MEASURE) measure_max(D);
+    if (sel.skip & SKIP_HOT) rebuild_hot_list(D, sel.theta_new, sel.build);
+    if (sel.skip & SKIP_POST) rebuild_postings(D, u.hist);
     return;
   }
   dbg_stamp(D, 0);
   agg_init(agg);
   hot_init(hot);
   kc_init(kc);
-  State* st = D.st;
   ApplyCtx A;
-  A.W = st->W;
-  A.nid = st->nid;
-  const int32_t tag = st->tag;
+  A.W = sel.W;
+  A.nid = sel.nid;
+  const int32_t tag = sel.tag;
   A.tagR = (tag << 2) | 2;
   A.tagL = (tag << 2) | 1;
   A.theta = st->theta;
   A.to_delta = to_delta != 0;
-  A.w1 = st->w1;
-  A.w2 = st->w2;
-  A.wl = st->wl;
+  A.w1 = sel.w1;
+  A.w2 = sel.w2;
+  A.wl = sel.wl;
   A.spw = s_pw;
   A.spwn = (int32_t)min(D.pwn, (int64_t)PW_LDS);
   for (int i = threadIdx.x; i < A.spwn; i += blockDim.x) {
@@ -1123,7 +1177,7 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
     s_pw[PW_LDS + i] = D.pw2[i];
   }
   if (blockIdx.x == 0) {  // _tokens[n] = json.loads(key): content(L) ++ [g] ++ content(R)
-    const int32_t L = st->widL, g = st->wg, Rr = st->widR;
+    const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
     const int64_t vL = D.voff[L], vR = D.voff[Rr];
     const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
     const int64_t pos = D.voff[A.nid], ln = nL + 1 + nR;
@@ -1166,7 +1220,7 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   }
   __syncthreads();
   const int32_t E = s_off[RPB];
-  const int64_t novf = min(st->L_ovf, D.Lovf_cap);
+  const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
   const int64_t oper = (novf + gridDim.x - 1) / gridDim.x;
   const int64_t o_lo = (int64_t)blockIdx.x * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
   dbg_stamp(D, 1);
@@ -1252,7 +1306,13 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta) {
   if (blockIdx.x == 0) {
     int32_t tot;
     block_excl_scan(nm, &tot, s_red);
-    if (threadIdx.x == 0) D.log[st->iter - 1].nmerged = (int64_t)tot + min(st->L_ovf, D.Lovf_cap);
+    if (threadIdx.x == 0) {
+      D.log[sel.iter].nmerged = (int64_t)tot + novf;
+      st->iter = sel.iter + 1;
+      st->K = sel.nid + 1;
+      st->maxc = sel.maxc;
+      st->ncand = sel.ncand;
+    }
   }
   dbg_stamp(D, 63);
 }
