@@ -80,6 +80,10 @@ int geobpe_init_tokens(geobpe_ctx *ctx, const int32_t *h_label_of_sym, int32_t K
 
 /* ---- BPE.bin(): full content-keyed adjacent-pair histogram (bpe.py:1431-1474) ---- */
 int geobpe_bin(geobpe_ctx *ctx);
+/* Bin-pass form: 1 (default) = dense symbol-triple histogram when the corpus
+ * is at its initial state and K0*B^3*K0 <= 2^26; 0 = per-pair key probing.
+ * Both produce the same keys, counts and pk; must precede geobpe_bin(). */
+int geobpe_set_bin_dense(geobpe_ctx *ctx, int on);
 
 /* ---- BPE.step() (bpe.py:1792-2166) ----
  * One merge iteration: device argmax (max count, ties -> smallest reference key

@@ -21,6 +21,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "device.h"
@@ -47,6 +48,8 @@ struct geobpe_ctx {
   State* h_state = nullptr;  // pinned mirror
   bool keys_ready = false;
   bool distributed = false;
+  bool bin_dense = true;
+  int32_t bin_cube[2] = {0, 0};  // cube shape (CL, CG) of the last dense bin
   int64_t global_residues = 0;
   // host vocab mirror (content per token id), synced lazily from the device log
   std::vector<std::vector<int32_t>> vocab;
@@ -528,11 +531,100 @@ int geobpe_set_global_residues(geobpe_ctx* c, int64_t n) {
   return 0;
 }
 
+int geobpe_set_bin_dense(geobpe_ctx* c, int on) {
+  if (!c) return GEOBPE_EARG;
+  if (c->keys_ready) return fail(c, GEOBPE_EARG, "set_bin_dense must precede bin()");
+  c->bin_dense = on != 0;
+  return 0;
+}
+
 int geobpe_bin(geobpe_ctx* c) {
   if (!c || !c->K0) return GEOBPE_EARG;
+  if (c->keys_ready) return fail(c, GEOBPE_EARG, "bin() twice");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   if ((rc = alloc_keys(c))) return rc;
+  const int64_t K0 = c->K0, G = c->D.B3;
+  if (c->bin_dense && K0 <= BIN_MAXSYM && G <= BIN_MAXSYM && K0 * G * K0 < (1LL << 31)) {
+    // bin_dense.h: sample -> cube shape -> pre-claimed cube keys -> count -> reduce / lists
+    const int nbc = c->ncu;  // count / list workgroups (144 KB of LDS each)
+    BinWork W{};
+    W.K0 = (int32_t)K0;
+    W.G = (int32_t)G;
+    W.nbc = nbc;
+    const int64_t NV = c->R / BIN_VEC;
+    W.ool_cap = ((NV + nbc - 1) / nbc) * BIN_VEC + BIN_VEC;
+    std::vector<void*> tmp;
+    auto tmalloc = [&](auto** p, int64_t n) -> hipError_t {
+      void* q = nullptr;
+      hipError_t e = hipMalloc(&q, (size_t)std::max<int64_t>(n, 1) * sizeof(**p));
+      if (e == hipSuccess) tmp.push_back(q);
+      *p = (std::remove_reference_t<decltype(*p)>)q;
+      return e;
+    };
+    hipError_t e = hipSuccess;
+    if ((e = tmalloc(&W.hist, K0 + G)) || (e = tmalloc(&W.shape, 2)) || (e = tmalloc(&W.cl_of, K0)) ||
+        (e = tmalloc(&W.cg_of, G)) || (e = tmalloc(&W.l_at, K0)) || (e = tmalloc(&W.g_at, G)) ||
+        (e = tmalloc(&W.flag, BIN_NC)) || (e = tmalloc(&W.cubemap, BIN_NC)) ||
+        (e = tmalloc(&W.partial, (int64_t)nbc * BIN_NC)) || (e = tmalloc(&W.ool, (int64_t)nbc * W.ool_cap)) ||
+        (e = tmalloc(&W.ooln, nbc)) || (e = tmalloc(&W.found, (int64_t)nbc * AggOol::N)) ||
+        (e = tmalloc(&W.foundn, nbc))) {
+      for (void* q : tmp) hipFree(q);
+      return fail(c, GEOBPE_EHIP, "bin scratch: %s", hipGetErrorString(e));
+    }
+    HIPCHK(c, hipMemsetAsync(W.hist, 0, (size_t)(K0 + G) * 4, c->stream));
+    HIPCHK(c, hipMemsetAsync(W.flag, 0, (size_t)BIN_NC * 4, c->stream));
+    const int64_t DS = K0 * G * K0;
+    const bool dense_lists = DS <= (1LL << 26);
+    if (dense_lists) {
+      W.DS = DS;
+      W.newcap = std::min<int64_t>(DS, c->R + 1);
+      if ((e = tmalloc(&W.dcnt, DS)) || (e = tmalloc(&W.newl, W.newcap)) || (e = tmalloc(&W.nnew, 1))) {
+        for (void* q : tmp) hipFree(q);
+        return fail(c, GEOBPE_EHIP, "bin scratch: %s", hipGetErrorString(e));
+      }
+      HIPCHK(c, hipMemsetAsync(W.dcnt, 0, (size_t)DS * 4, c->stream));
+      HIPCHK(c, hipMemsetAsync(W.nnew, 0, 8, c->stream));
+    }
+    {
+      Timed t(c, "bin_sample");
+      hipLaunchKernelGGL(k_bin_sample, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+      hipLaunchKernelGGL(k_bin_rank, dim3(1), dim3(ABLOCK), 0, c->stream, c->D, W);
+      hipLaunchKernelGGL(k_bin_flag, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+      hipLaunchKernelGGL(k_bin_precube, dim3(BIN_NC / BLOCK), dim3(BLOCK), 0, c->stream, c->D, W);
+    }
+    {
+      Timed t(c, "pair_count");
+      hipLaunchKernelGGL(k_bin_count, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+    }
+    {
+      Timed t(c, "bin_claim");
+      hipLaunchKernelGGL(k_bin_reduce, dim3(BIN_NC / ABLOCK, (nbc + BIN_RROWS - 1) / BIN_RROWS), dim3(ABLOCK), 0,
+                         c->stream, c->D, W, c->distributed ? 1 : 0);
+    }
+    {
+      Timed t(c, "bin_assign");
+      if (dense_lists) {
+        hipLaunchKernelGGL(k_bin_ool_stage, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+        hipLaunchKernelGGL(k_bin_ool_claim, dim3(4 * c->ncu), dim3(BLOCK), 0, c->stream, c->D, W,
+                           c->distributed ? 1 : 0);
+        hipLaunchKernelGGL(k_bin_ool_fix, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+      } else {
+        hipLaunchKernelGGL(k_bin_ool, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W, c->distributed ? 1 : 0);
+        hipLaunchKernelGGL(k_bin_verify, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+      }
+    }
+    HIPCHK(c, hipGetLastError());
+    rc = sync_state(c);
+    if (!rc) {
+      int32_t shape[2];
+      HIPCHK(c, hipMemcpy(shape, W.shape, sizeof shape, hipMemcpyDeviceToHost));
+      c->bin_cube[0] = shape[0];
+      c->bin_cube[1] = shape[1];
+    }
+    for (void* q : tmp) hipFree(q);
+    return rc;
+  }
   if ((rc = reset_region_counters(c))) return rc;
   {
     Timed t(c, "pair_count");

@@ -244,6 +244,8 @@ __global__ __launch_bounds__(ABLOCK) void k_pairs_all(Dev D) {
   close_regions(D, &s_np, &s_ns);
 }
 
+#include "bin_dense.h"
+
 // pair -> key id into pk, counts via LDS-staged partial counts (+ the hot-list
 // crossing check on the global counts); the key's payload must be this content
 __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, const NewPair& e, int64_t j, bool to_delta,

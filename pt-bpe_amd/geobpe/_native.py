@@ -11,7 +11,7 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libgeobpe.so")
+LIB_PATH = os.environ.get("GEOBPE_LIB") or os.path.join(HERE, "libgeobpe.so")  # override: kernel A/B builds
 
 E_OK, E_ARG, E_VALUE, E_CAPACITY, E_HIP, E_HASH = range(6)
 DELTA_RECORD_BYTES = 40
@@ -53,6 +53,7 @@ def lib():
         "geobpe_symbol_first": (ctypes.c_int, [P, I64, P]),
         "geobpe_init_tokens": (ctypes.c_int, [P, P, I32]),
         "geobpe_bin": (ctypes.c_int, [P]),
+        "geobpe_set_bin_dense": (ctypes.c_int, [P, ctypes.c_int]),
         "geobpe_step": (ctypes.c_int, [P, pI32, pI32, pI64]),
         "geobpe_run": (ctypes.c_int, [P, I64, pI64]),
         "geobpe_merge_log": (I64, [P, P, I64]),
@@ -90,7 +91,7 @@ def lib():
 
 EXPORTED_SYMBOLS = [
     "geobpe_create", "geobpe_destroy", "geobpe_last_error", "geobpe_load_angles", "geobpe_angle_range",
-    "geobpe_quantize", "geobpe_symbol_first", "geobpe_init_tokens", "geobpe_bin", "geobpe_step",
+    "geobpe_quantize", "geobpe_symbol_first", "geobpe_init_tokens", "geobpe_bin", "geobpe_set_bin_dense", "geobpe_step",
     "geobpe_run", "geobpe_merge_log", "geobpe_key_json", "geobpe_debug_key_less", "geobpe_debug_counts", "geobpe_debug_key",
     "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",

@@ -67,7 +67,8 @@ def _stream_handle(device: int):
 
 class GeoBPEEngine:
     def __init__(self, corpus: dict, bins: int, device: int = 0, max_vocab: int = 1 << 20,
-                 group=None, stream=None, use_torch_stream: bool = True, cover: bool = False):
+                 group=None, stream=None, use_torch_stream: bool = True, cover: bool = False,
+                 bin_dense: bool = True):
         """``corpus``: ``{column: float64[R]}`` + ``row_off`` (geobpe.synth layout) for
         THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs."""
         self.L = _native.lib()
@@ -75,6 +76,7 @@ class GeoBPEEngine:
         self.device = int(device)
         self.group = group
         self.cover = bool(cover)
+        self.bin_dense = bool(bin_dense)
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
         self.n_rows = len(self.row_off) - 1
         self._cols = [np.ascontiguousarray(corpus[c], dtype=np.float64) for c in COLUMNS]
@@ -157,6 +159,7 @@ class GeoBPEEngine:
         if self.distributed:
             self._chk(self.L.geobpe_set_distributed(self._ctx, 1))
             self._chk(self.L.geobpe_set_global_residues(self._ctx, self.group.total_residues))
+        self._chk(self.L.geobpe_set_bin_dense(self._ctx, 1 if self.bin_dense else 0))
         self._chk(self.L.geobpe_bin(self._ctx))
         if self.distributed:
             self._exchange()

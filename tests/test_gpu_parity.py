@@ -207,3 +207,29 @@ def test_run_to_exhaustion_device_loop(oracle_lib):
     assert eng.merge_keys() == o.merges
     assert eng.run(5) == 0
     eng.close()
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(n=2000, lo=40, hi=300, B=5, seed=61, rep=0.05),
+    dict(n=300, lo=1, hi=40, B=3, seed=62, rep=0.2),
+    dict(n=400, lo=30, hi=200, B=7, seed=63, rep=0.0),
+    dict(n=100_000, lo=40, hi=560, B=5, seed=0, rep=0.0),  # BASELINE configs[2] (C3)
+])
+def test_dense_bin_equals_probe_bin(cfg):
+    """The dense symbol-triple bin pass (k_bin_count/claim/assign) and the per-pair
+    probing pass (k_pairs_all/k_finalize) give the same key strings and counts,
+    and the merges that follow are identical."""
+    from geobpe import synth
+    lengths = synth.make_lengths(cfg["n"], cfg["lo"], cfg["hi"], seed=cfg["seed"])
+    corpus = synth.make_corpus(lengths, seed=cfg["seed"], repeat_frac=cfg["rep"])
+    runs = []
+    for dense in (True, False):
+        eng = _engine(corpus, cfg["B"], bin_dense=dense)
+        eng.bin()
+        counts = eng.key_counts()
+        assert eng.verify_counts() == 0
+        eng.run(40)
+        runs.append((counts, eng.merge_keys()))
+        eng.close()
+    assert runs[0][0] == runs[1][0]
+    assert runs[0][1] == runs[1][1]
