@@ -160,6 +160,15 @@ int64_t geobpe_debug_timeline(geobpe_ctx *ctx, int on, int64_t *h_out, int64_t c
 /* Restrict the timing to a comma-separated list of kernel names ("" = all). */
 int geobpe_set_profiling_filter(geobpe_ctx *ctx, const char *names);
 double geobpe_kernel_ms(geobpe_ctx *ctx, const char *name, int64_t *launches);
+/* ---- merge events: the checkpoint's merge tree (TokenHierarchy.__setitem__ ->
+ * BinaryTreeBuilder.combine, data_structures.py:32-60,217-226) ----
+ * on=1 before the first merge: every merged occurrence of every later merge is
+ * logged on the device.  geobpe_events copies (merge index, left token start
+ * slot, right token start slot) of all logged events (any order within a merge)
+ * and returns their number (-1: not recording / error); NULL buffers: count only. */
+int geobpe_set_record_events(geobpe_ctx *ctx, int on);
+int64_t geobpe_events(geobpe_ctx *ctx, int32_t *h_merge, int32_t *h_a, int32_t *h_b);
+
 int geobpe_synchronize(geobpe_ctx *ctx);
 
 #ifdef __cplusplus

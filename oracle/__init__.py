@@ -146,6 +146,20 @@ class OracleBPE:
         L.oracle_encode(self._h, _ptr(ids), _ptr(off))
         return ids, off
 
+    def events(self):
+        """Merge events in iteration order: (a, b, iter_off) -- left / right token
+        start slots of every merged occurrence; events of merge t are
+        [iter_off[t], iter_off[t+1])."""
+        L = lib()
+        L.oracle_events.restype = ctypes.c_int64
+        L.oracle_events.argtypes = [ctypes.c_void_p] * 4
+        n = L.oracle_events(self._h, None, None, None)
+        a = np.empty(n, np.int32)
+        b = np.empty(n, np.int32)
+        off = np.empty(len(self.merges) + 1, np.int64)
+        L.oracle_events(self._h, _ptr(a), _ptr(b), _ptr(off))
+        return a, b, off
+
     def vocab_content(self, v: int) -> np.ndarray:
         L = lib()
         m = L.oracle_vocab_content(self._h, v, None)

@@ -90,6 +90,8 @@ typedef struct {
   int32_t *touched_flag;
   ivec touched;
   int64_t step;
+  ivec ev_a, ev_b;  /* merge events (left / right token start slots), iteration order */
+  ivec ev_iter;     /* events before each iteration (ev_iter[t] = first event of merge t) */
   /* json scratch */
   char *jbufA, *jbufB;
   int64_t jcap;
@@ -481,10 +483,13 @@ int32_t oracle_step(oracle_t *o, int32_t *count, int32_t *key) {
   for (int64_t i = 0; i < o->kocc[W].n; i++) iv_push(&occ, o->kocc[W].a[i]);
   int cmp_i32(const void *x, const void *y);
   qsort(occ.a, (size_t)occ.n, 4, cmp_i32);
+  iv_push(&o->ev_iter, (int32_t)o->ev_a.n);
   for (int64_t i = 0; i < occ.n; i++) {
     int32_t a = occ.a[i];
     if (o->pair_key[a] != W) continue; /* overlapped by the previous merge (bpe.py:1909-1916) */
     int32_t b = o->tnext[a];
+    iv_push(&o->ev_a, a); /* the merge tree event (TokenHierarchy.__setitem__, data_structures.py:217-226) */
+    iv_push(&o->ev_b, b);
     int32_t p = o->tprev[a];
     int32_t c2 = o->tnext[b];
     pair_remove(o, a);                 /* step 1 */
@@ -580,8 +585,25 @@ int64_t oracle_encode(oracle_t *o, int32_t *ids, int64_t *row_id_off) {
 
 int64_t oracle_steps_done(oracle_t *o) { return o->step; }
 
+/* merge events: a[i], b[i] = left / right token start slots of the i-th merged
+ * occurrence; iter_off[t] = first event of merge t (iter_off[steps] = total). */
+int64_t oracle_events(oracle_t *o, int32_t *a, int32_t *b, int64_t *iter_off) {
+  if (a && b) {
+    for (int64_t i = 0; i < o->ev_a.n; i++) {
+      a[i] = o->ev_a.a[i];
+      b[i] = o->ev_b.a[i];
+    }
+  }
+  if (iter_off) {
+    for (int64_t t = 0; t < o->ev_iter.n; t++) iter_off[t] = o->ev_iter.a[t];
+    iter_off[o->ev_iter.n] = o->ev_a.n;
+  }
+  return o->ev_a.n;
+}
+
 void oracle_destroy(oracle_t *o) {
   if (!o) return;
+  free(o->ev_a.a); free(o->ev_b.a); free(o->ev_iter.a);
   free((void *)o->row_off);
   free(o->rsym); free(o->gsym); free(o->tid); free(o->tlen); free(o->tnext); free(o->tprev);
   free(o->pair_key); free(o->occ_pos);

@@ -8,9 +8,12 @@ Differences (all outside SURVEY.md §8's hot path):
     §8(f) row 2.
   * stats JSON carries K, L, bpr and the codebook utility (encode.py:408-420);
     bb_rmsd / lddt need the coordinate stack (esm ProteinChain) and are omitted.
-  * checkpoints are ``bpe_iter={t}.json`` (merge list + counts + args); resume
-    replays the merges on the device and checks them against the file.  The
-    reference-compatible ``bpe_iter=*.pkl`` writer is §8(f) row 1.
+  * checkpoints are ``bpe_iter={t}.pkl`` in the reference's pickle format
+    (geobpe.refpickle: a foldingdiff.bpe.BPE object that bin/train.py,
+    bin/predict.py, bin/induce.py and the reference's resume load unchanged);
+    ``--ckpt-format json`` writes the bare merge list instead.  Resume (either
+    format, the reference's own pkl files included) reads the merge list, re-runs
+    that many merges on the device and checks them against it.
   * ``--run-chunk M`` (ours): merges issued per device call between host
     syncs; the reference steps one at a time.  Outputs do not depend on it.
 
@@ -79,6 +82,7 @@ def parse_args(argv=None):
     p.add_argument("--save-every", type=int, default=10)
     p.add_argument("--run-chunk", type=int, default=0, help="merges per device call (0: = save-every)")
     p.add_argument("--device", type=int, default=0)
+    p.add_argument("--ckpt-format", choices=["pkl", "json"], default="pkl")
     return p.parse_args(argv)
 
 
@@ -106,20 +110,30 @@ def stats(bpe) -> dict:
         get_codebook_utility(ids, bpe.vocab_size)
 
 
-def latest_checkpoint(save_dir: str):
-    best, path = -1, None
-    for f in glob.glob(os.path.join(save_dir, "bpe_iter=*.json")):
-        m = re.match(r"bpe_iter=(\d+)\.json$", os.path.basename(f))
-        if not m:
-            continue
+def _saved_keys(path: str):
+    """Merge key strings of a checkpoint, or None if it is incomplete."""
+    if path.endswith(".json"):
         try:
-            with open(f) as fh:
-                json.load(fh)
-        except (OSError, ValueError):
-            continue  # incomplete write (encode.py:183-200 skips incomplete pickles)
-        if int(m.group(1)) > best:
-            best, path = int(m.group(1)), f
-    return best, path
+            with open(path) as fh:
+                return [m[0] for m in json.load(fh)["merges"]]
+        except (OSError, ValueError, KeyError):
+            return None
+    from geobpe import refpickle
+    if not refpickle.is_complete(path):  # encode.py:183-200 skips incomplete pickles
+        return None
+    return refpickle.merge_keys(refpickle.load(path))
+
+
+def latest_checkpoint(save_dir: str):
+    best, path, keys = -1, None, None
+    for f in glob.glob(os.path.join(save_dir, "bpe_iter=*")):
+        m = re.match(r"bpe_iter=(\d+)\.(pkl|json)$", os.path.basename(f))
+        if not m or int(m.group(1)) <= best:
+            continue
+        k = _saved_keys(f)
+        if k is not None:
+            best, path, keys = int(m.group(1)), f, k
+    return best, path, keys
 
 
 def main(argv=None) -> int:
@@ -130,7 +144,7 @@ def main(argv=None) -> int:
         args.save_dir = os.path.join(args.base_dir, "ckpts", str(time.time()))
     os.makedirs(args.save_dir, exist_ok=True)
     args_path = os.path.join(args.save_dir, "args.txt")
-    skip = {"auto", "save_dir", "max_iter", "run_chunk", "device"}
+    skip = {"auto", "save_dir", "max_iter", "run_chunk", "device", "ckpt_format"}
     if os.path.exists(args_path):  # validate_args_match (utils.py)
         with open(args_path) as f:
             loaded = dict(line.rstrip("\n").split(": ", 1) for line in f if ": " in line)
@@ -151,7 +165,7 @@ def main(argv=None) -> int:
     bpe = BPE(corpus, bins=args.bins, bin_strategy=args.bin_strategy, save_dir=args.save_dir,
               res_init=args.res_init, std_bonds=not args.free_bonds,
               rmsd_partition_min_size=args.p_min_size, glue_opt=args.glue_opt, seed=args.seed,
-              device=args.device)
+              device=args.device, record_tree=args.ckpt_format == "pkl")
     t0 = time.time()
     bpe.initialize()
     with open(os.path.join(args.save_dir, "initial_stats=-1.json"), "w") as f:
@@ -159,12 +173,10 @@ def main(argv=None) -> int:
     bpe.bin()
     log.info("initialize+bin %.3fs", time.time() - t0)
 
-    start, ck = latest_checkpoint(args.save_dir)
-    if ck is not None:  # resume: replay the merges, then check them against the file
-        with open(ck) as f:
-            saved = json.load(f)
-        done = bpe.run(len(saved["merges"]))
-        if [list(m) for m in bpe.merges] != saved["merges"] or done != len(saved["merges"]):
+    start, ck, keys = latest_checkpoint(args.save_dir)
+    if ck is not None:  # resume: re-run the saved number of merges, then check them against the file
+        done = bpe.run(len(keys))
+        if [m[0] for m in bpe.merges] != keys or done != len(keys):
             raise SystemExit(f"replay of {ck} diverged from the saved merge list")
         log.info("resumed from %s at iter=%d", ck, start)
 
@@ -182,11 +194,14 @@ def main(argv=None) -> int:
         if t % args.save_every == 0:
             with open(os.path.join(args.save_dir, f"stats={t}.json"), "w") as f:
                 json.dump(stats(bpe), f)
-            tmp = os.path.join(args.save_dir, f".bpe_iter={t}.json.tmp")
-            with open(tmp, "w") as f:
-                json.dump({"iter": t, "merges": [list(m) for m in bpe.merges],
-                           "args": {k: str(v) for k, v in vars(args).items()}}, f)
-            os.replace(tmp, os.path.join(args.save_dir, f"bpe_iter={t}.json"))
+            if args.ckpt_format == "pkl":
+                bpe.save_checkpoint(os.path.join(args.save_dir, f"bpe_iter={t}.pkl"))
+            else:
+                tmp = os.path.join(args.save_dir, f".bpe_iter={t}.json.tmp")
+                with open(tmp, "w") as f:
+                    json.dump({"iter": t, "merges": [list(m) for m in bpe.merges],
+                               "args": {k: str(v) for k, v in vars(args).items()}}, f)
+                os.replace(tmp, os.path.join(args.save_dir, f"bpe_iter={t}.json"))
         t += 1
     log.info("done: %d merges, vocab_size %d", bpe._step, bpe.vocab_size)
     print(json.dumps({"merges": bpe._step, "vocab_size": bpe.vocab_size,

@@ -49,6 +49,10 @@ struct geobpe_ctx {
   bool keys_ready = false;
   bool distributed = false;
   bool bin_dense = true;
+  // merge-event log (geobpe_set_record_events): int4 {merge, left start, right start, 0}
+  int4* ev = nullptr;
+  int64_t ev_cap = 0;
+  unsigned long long* ev_n = nullptr;
   int32_t bin_cube[2] = {0, 0};  // cube shape (CL, CG) of the last dense bin
   int64_t global_residues = 0;
   // host vocab mirror (content per token id), synced lazily from the device log
@@ -254,6 +258,9 @@ void enqueue_apply(geobpe_ctx* c) {
     hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0,
                        (int)(c->gen & 1));
   }
+  if (c->ev)
+    hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1), c->ev, c->ev_cap,
+                       c->ev_n);
   c->gen++;
 }
 void enqueue_iteration(geobpe_ctx* c) {
@@ -305,6 +312,8 @@ void geobpe_destroy(geobpe_ctx* c) {
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
   for (void* p : c->allocs) hipFree(p);
+  if (c->ev) hipFree(c->ev);
+  if (c->ev_n) hipFree(c->ev_n);
   for (int i = 0; i < 9; i++)
     if (c->d_cols[i]) hipFree(c->d_cols[i]);
   if (c->h_state) hipHostFree(c->h_state);
@@ -1017,6 +1026,50 @@ double geobpe_kernel_ms(geobpe_ctx* c, const char* name, int64_t* launches) {
   }
   if (launches) *launches = it->second.second;
   return it->second.first;
+}
+
+int geobpe_set_record_events(geobpe_ctx* c, int on) {
+  if (!c) return GEOBPE_EARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  if (!on) {
+    if (c->ev) {
+      HIPCHK(c, hipStreamSynchronize(c->stream));
+      hipFree(c->ev);
+      hipFree(c->ev_n);
+    }
+    c->ev = nullptr;
+    c->ev_n = nullptr;
+    c->ev_cap = 0;
+    return 0;
+  }
+  if (c->ev) return 0;
+  if (c->h_state && c->h_state->iter > 0) return fail(c, GEOBPE_EARG, "record events before the first merge");
+  c->ev_cap = std::max<int64_t>(c->R, 1);  // every merge removes one token: < R events in all
+  HIPCHK(c, hipMalloc(&c->ev, (size_t)c->ev_cap * sizeof(int4)));
+  HIPCHK(c, hipMalloc(&c->ev_n, sizeof(unsigned long long)));
+  HIPCHK(c, hipMemsetAsync(c->ev_n, 0, sizeof(unsigned long long), c->stream));
+  return 0;
+}
+
+int64_t geobpe_events(geobpe_ctx* c, int32_t* h_merge, int32_t* h_a, int32_t* h_b) {
+  if (!c || !c->ev) return -1;
+  if (sync_state(c)) return -1;
+  unsigned long long n = 0;
+  if (hipMemcpy(&n, c->ev_n, sizeof n, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if ((int64_t)n > c->ev_cap) {
+    fail(c, GEOBPE_ECAPACITY, "merge-event log overflow (%llu > %lld)", n, (long long)c->ev_cap);
+    return -1;
+  }
+  if (h_merge && h_a && h_b && n) {
+    std::vector<int4> ev(n);
+    if (hipMemcpy(ev.data(), c->ev, n * sizeof(int4), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    for (size_t i = 0; i < n; i++) {
+      h_merge[i] = ev[i].x;
+      h_a[i] = ev[i].y;
+      h_b[i] = ev[i].z;
+    }
+  }
+  return (int64_t)n;
 }
 
 int geobpe_synchronize(geobpe_ctx* c) {

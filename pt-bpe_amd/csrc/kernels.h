@@ -1320,6 +1320,44 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta, int par) 
 }
 
 // ====================================================================== multi-rank deltas
+// merge events for the checkpoint's merge tree (TokenHierarchy / BinaryTreeBuilder.
+// combine, data_structures.py:32-60, 217-226): after a merge iteration's k_apply,
+// (merge index, left token start, right token start) of every merged occurrence
+// from the mark regions and the overflow list.  Record mode only (one launch per
+// iteration); the hot kernels are unchanged.
+__global__ __launch_bounds__(BLOCK) void k_events(Dev D, int par, int4* ev, int64_t cap, unsigned long long* ev_n) {
+  __shared__ int32_t s_off[RPB + 1];
+  __shared__ int64_t s_base;
+  const Sel sel = D.sel[par];
+  if (sel.decision != SEL_MERGE) return;
+  const int64_t novf = min(D.st->L_ovf2[par], D.Lovf_cap);
+  const int64_t per = (novf + gridDim.x - 1) / gridDim.x;
+  const int64_t o_lo = min(novf, (int64_t)blockIdx.x * per), o_hi = min(novf, o_lo + per);
+  if (threadIdx.x == 0) {
+    int32_t acc = 0;
+    for (int r = 0; r < RPB; r++) {
+      s_off[r] = acc;
+      acc += D.Lcnt[blockIdx.x * RPB + r];
+    }
+    s_off[RPB] = acc;
+    const int64_t n = acc + (o_hi - o_lo);
+    s_base = n ? (int64_t)atomicAdd(ev_n, (unsigned long long)n) : 0;
+  }
+  __syncthreads();
+  const int32_t nreg = s_off[RPB];
+  for (int32_t j = threadIdx.x; j < nreg; j += BLOCK) {
+    int r = 0;
+    while (j >= s_off[r + 1]) r++;
+    const LEntry e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + (j - s_off[r])];
+    if (s_base + j < cap) ev[s_base + j] = make_int4(sel.iter, e.a, e.b, 0);
+  }
+  for (int64_t k = o_lo + threadIdx.x; k < o_hi; k += BLOCK) {
+    const LEntry e = D.Lovf[k];
+    const int64_t at = s_base + nreg + (k - o_lo);
+    if (at < cap) ev[at] = make_int4(sel.iter, e.a, e.b, 0);
+  }
+}
+
 __global__ __launch_bounds__(BLOCK) void k_export(Dev D, DeltaRec* out, int64_t n) {
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = D.touched[j];

@@ -80,6 +80,8 @@ def lib():
         "geobpe_kernel_ms": (D, [P, ctypes.c_char_p, pI64]),
         "geobpe_set_profiling_filter": (ctypes.c_int, [P, ctypes.c_char_p]),
         "geobpe_synchronize": (ctypes.c_int, [P]),
+        "geobpe_set_record_events": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_events": (I64, [P, P, P, P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -97,6 +99,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
     "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_synchronize",
+    "geobpe_set_record_events", "geobpe_events",
 ]
 
 

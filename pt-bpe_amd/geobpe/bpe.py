@@ -165,7 +165,8 @@ class BPE:
                  compute_sec_structs=False, plot_iou_with_sec_structs=False, res_init=False, std_bonds=True,
                  rmsd_partition_min_size=4, rmsd_super_res=False, rmsd_only=False, num_partitions=3,
                  max_num_strucs=500, glue_opt=False, glue_opt_prior=0.0, glue_opt_every=10,
-                 glue_opt_method="all", seed=None, device: int = 0, max_vocab: int = 1 << 20, group=None):
+                 glue_opt_method="all", seed=None, device: int = 0, max_vocab: int = 1 << 20, group=None,
+                 record_tree: bool = True):
         _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_size, glue_opt, compute_sec_structs)
         if isinstance(structures, dict) and "row_off" in structures:
             corpus = structures
@@ -202,6 +203,7 @@ class BPE:
         self._engine = GeoBPEEngine(corpus, self.B, device=device, max_vocab=max_vocab, group=group,
                                     cover=bin_strategy == "histogram-cover")
         self._tok_cache = None
+        self._record_tree = bool(record_tree) and group is None
 
     # ------------------------------------------------------------ BPE.initialize
     def initialize(self, path=None):
@@ -249,6 +251,8 @@ class BPE:
     # ------------------------------------------------------------ bin / step
     def bin(self):
         self._engine.bin()
+        if self._record_tree:  # merge events for the checkpoint's merge tree (refpickle)
+            self._engine.record_events(True)
         self._tok_cache = None
 
     def step(self):
@@ -393,6 +397,35 @@ class BPE:
                 total += mbits * m
                 total += 3 * (m - 1) * bbits
         return total
+
+    # ------------------------------------------------------------ checkpoints
+    def checkpoint_state(self) -> dict:
+        """The run state geobpe.refpickle turns into the reference's BPE object."""
+        if not self._record_tree:
+            raise RuntimeError("checkpoints need record_tree=True (the merge tree)")
+        e = self._engine
+        start, ids, off = e.segmentation()
+        a, b, eoff = e.events()
+        ro = self._corpus["row_off"]
+        return {
+            "corpus": self._corpus, "fnames": self._fnames or [None] * (len(ro) - 1),
+            "B": self.B, "bins": dict(self.bins), "bin_strategy": self.bin_strategy,
+            "thresholds": {k: list(v) for k, v in self._thresholds[1].items()},
+            "bin_counts": self._bin_counts[1], "K0": e.K0, "tokens": dict(self._tokens),
+            "seg_start": start, "seg_id": ids, "seg_off": off, "ev_a": a, "ev_b": b, "ev_off": eoff,
+            "step": self._step, "times": list(self._times),
+            "args": {k: getattr(self, k) for k in ("compute_sec_structs", "plot_iou_with_sec_structs",
+                                                  "rmsd_partition_min_size", "rmsd_super_res", "rmsd_only",
+                                                  "glue_opt", "glue_opt_every", "glue_opt_prior", "glue_opt_method",
+                                                  "num_partitions", "max_num_strucs", "seed", "save_dir")},
+        }
+
+    def save_checkpoint(self, path: str) -> None:
+        """``bpe_iter=t.pkl`` in the reference's format (bin/encode.py:427): a
+        pickle of foldingdiff.bpe.BPE that train.py / predict.py / induce.py and
+        the reference's own resume load unchanged (geobpe.refpickle)."""
+        from . import refpickle
+        refpickle.save(self.checkpoint_state(), path)
 
     def visualize(self, key, output_path):  # plotting only in the reference (bpe.py:1583-1627)
         return None

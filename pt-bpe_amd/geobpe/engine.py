@@ -316,6 +316,27 @@ class GeoBPEEngine:
         self.L.geobpe_encode(self._ctx, _p(ids), _p(off))
         return ids, off
 
+    def record_events(self, on: bool = True):
+        """Log every merged occurrence from now on (before the first merge): the
+        checkpoint's merge tree (geobpe.refpickle)."""
+        self._chk(self.L.geobpe_set_record_events(self._ctx, 1 if on else 0))
+
+    def events(self):
+        """(a, b, off): left / right token start slots of the merged occurrences,
+        merge t's events in [off[t], off[t+1]), ascending slot within a merge."""
+        n = self.L.geobpe_events(self._ctx, None, None, None)
+        if n < 0:
+            raise _native.GeoBPEError(f"geobpe_events: {self.L.geobpe_last_error(self._ctx).decode()}")
+        t = np.empty(n, np.int32)
+        a = np.empty(n, np.int32)
+        b = np.empty(n, np.int32)
+        if n:
+            self.L.geobpe_events(self._ctx, _p(t), _p(a), _p(b))
+        order = np.lexsort((a, t))
+        t, a, b = t[order], a[order], b[order]
+        off = np.searchsorted(t, np.arange(len(self.merges) + 1), side="left").astype(np.int64)
+        return a, b, off
+
     def verify_counts(self) -> int:
         n = int(self.L.geobpe_verify_counts(self._ctx))
         if n < 0:

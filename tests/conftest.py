@@ -16,7 +16,11 @@ def pytest_configure(config):
 
 
 def golden_names():
-    return sorted(f[:-5] for f in os.listdir(GOLDEN) if f.endswith(".json"))
+    return sorted(f[:-5] for f in os.listdir(GOLDEN) if f.endswith(".json") and not f.endswith(".pkl.json"))
+
+
+def pickle_golden_names():
+    return sorted(f[:-9] for f in os.listdir(GOLDEN) if f.endswith(".pkl.json"))
 
 
 def load_golden(name):

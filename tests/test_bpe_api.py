@@ -122,12 +122,20 @@ def test_cli_flags_mirror_reference_parsers():
         cli.str2dict("1-5:")
 
 
-def test_cli_latest_checkpoint_skips_incomplete(tmp_path):
+def test_cli_latest_checkpoint_skips_incomplete(tmp_path, oracle_lib):
+    from test_refpickle import oracle_run
+    from geobpe import refpickle
     cli = _encode_cli()
-    (tmp_path / "bpe_iter=10.json").write_text(json.dumps({"merges": []}))
+    (tmp_path / "bpe_iter=10.json").write_text(json.dumps({"merges": [["k", 1]]}))
     (tmp_path / "bpe_iter=20.json").write_text("{\"merges\": [")  # torn write
-    it, path = cli.latest_checkpoint(str(tmp_path))
-    assert it == 10 and path.endswith("bpe_iter=10.json")
+    it, path, keys = cli.latest_checkpoint(str(tmp_path))
+    assert it == 10 and path.endswith("bpe_iter=10.json") and keys == ["k"]
+    o, run = oracle_run(oracle_lib, "g25x1-12_b3_short", 12)
+    refpickle.save(run, str(tmp_path / "bpe_iter=12.pkl"))
+    data = (tmp_path / "bpe_iter=12.pkl").read_bytes()
+    (tmp_path / "bpe_iter=30.pkl").write_bytes(data[: len(data) - 7])  # torn pickle
+    it, path, keys = cli.latest_checkpoint(str(tmp_path))
+    assert it == 12 and path.endswith("bpe_iter=12.pkl") and keys == [k for k, _ in o.merges]
 
 
 @pytest.mark.gpu
@@ -139,8 +147,31 @@ def test_cli_resume_reproduces_one_shot(tmp_path):
     assert cli.main(common + ["--save-dir", str(one), "--max-iter", "61"]) == 0
     assert cli.main(common + ["--save-dir", str(two), "--max-iter", "31"]) == 0
     assert cli.main(common + ["--save-dir", str(two), "--max-iter", "61"]) == 0  # resumes at 30
-    a = json.loads((one / "bpe_iter=60.json").read_text())["merges"]
-    b = json.loads((two / "bpe_iter=60.json").read_text())["merges"]
+    from geobpe import refpickle
+    a = refpickle.merge_keys(refpickle.load(str(one / "bpe_iter=60.pkl")))
+    b = refpickle.merge_keys(refpickle.load(str(two / "bpe_iter=60.pkl")))
     assert a == b and len(a) == 61
     sa = json.loads((one / "stats=60.json").read_text())
     assert sa == json.loads((two / "stats=60.json").read_text()) and sa["K"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["g40x50_b5", "g25x1-12_b3_short"])
+def test_checkpoint_from_device_matches_reference_pickle(name):
+    """BPE.save_checkpoint on the HIP path (device merge-event log for the merge
+    tree) against the digest of the reference's own pickled BPE."""
+    import os
+    from conftest import GOLDEN
+    from test_refpickle import check_against_digest
+    from geobpe import refpickle
+    with open(os.path.join(GOLDEN, name + ".pkl.json")) as f:
+        d = json.load(f)
+    meta, corpus, _ = load_golden(name)
+    from geobpe.bpe import BPE
+    b = BPE(corpus, bins={1: meta["bins"]["1"]}, res_init=True, rmsd_partition_min_size=float("inf"), seed=0)
+    b._fnames = [f"synthetic_{i}" for i in range(len(corpus["row_off"]) - 1)]
+    b.initialize()
+    b.bin()
+    assert b.run(d["merges"]) == d["merges"]
+    check_against_digest(refpickle.build(b.checkpoint_state()), d, [k for k, _ in meta["merges"][: d["merges"]]])
+    b.close()

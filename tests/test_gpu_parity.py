@@ -233,3 +233,25 @@ def test_dense_bin_equals_probe_bin(cfg):
         eng.close()
     assert runs[0][0] == runs[1][0]
     assert runs[0][1] == runs[1][1]
+
+
+def test_merge_events_match_oracle(oracle_lib):
+    """The device merge-event log (k_events: the checkpoint's merge tree) equals
+    the oracle's per-occurrence merge sequence."""
+    from geobpe import synth
+    lengths = synth.make_lengths(2000, 20, 200, seed=71)
+    corpus = synth.make_corpus(lengths, seed=71, repeat_frac=0.1)
+    o = _oracle_run(oracle_lib, corpus, 5, 300)
+    eng = _engine(corpus, 5)
+    eng.bin()
+    eng.record_events(True)
+    eng.run(300)
+    assert eng.merge_keys() == o.merges
+    a, b, off = eng.events()
+    oa, ob, ooff = o.events()
+    assert np.array_equal(off, ooff)
+    for t in range(len(off) - 1):  # within a merge the device order is free; the oracle's is ascending
+        s = slice(off[t], off[t + 1])
+        oo = np.argsort(oa[s], kind="stable")
+        assert np.array_equal(a[s], oa[s][oo]) and np.array_equal(b[s], ob[s][oo])
+    eng.close()
