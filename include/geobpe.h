@@ -160,6 +160,18 @@ int64_t geobpe_debug_timeline(geobpe_ctx *ctx, int on, int64_t *h_out, int64_t c
 /* Restrict the timing to a comma-separated list of kernel names ("" = all). */
 int geobpe_set_profiling_filter(geobpe_ctx *ctx, const char *names);
 double geobpe_kernel_ms(geobpe_ctx *ctx, const char *name, int64_t *launches);
+/* ---- merge replay (bin/induce.py: encode new chains with a trained vocabulary;
+ * SURVEY.md §8(f) row 1) ----
+ * After bin() and before any merge: merge t of geobpe_run / geobpe_step becomes
+ * the trained token K0 + t -- content hash (h1, h2) of len residues and one split
+ * L ++ [g] ++ R into earlier token ids -- instead of the argmax.  Every occurrence
+ * is merged greedily left to right as in training; a content with no occurrence
+ * merges nothing but keeps its token id.  geobpe_run stops after n merges (done).
+ * The context must have been initialised with the trained grid and labels
+ * (geobpe_quantize edges, geobpe_init_tokens label map). */
+int geobpe_replay_load(geobpe_ctx *ctx, const uint64_t *h_h1, const uint64_t *h_h2, const int32_t *h_len,
+                       const int32_t *h_idL, const int32_t *h_g, const int32_t *h_idR, int64_t n);
+
 /* ---- merge events: the checkpoint's merge tree (TokenHierarchy.__setitem__ ->
  * BinaryTreeBuilder.combine, data_structures.py:32-60,217-226) ----
  * on=1 before the first merge: every merged occurrence of every later merge is

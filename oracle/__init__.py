@@ -76,22 +76,42 @@ def _ptr(a: np.ndarray):
 class OracleBPE:
     """Scoped-mode GeoBPE on the CPU: ``initialize()``, ``bin()``, ``step()``."""
 
-    def __init__(self, corpus: dict, bins: int, cover: bool = False):
+    def __init__(self, corpus: dict, bins: int, cover: bool = False, thresholds=None, sym_of_label=None):
+        """``thresholds`` / ``sym_of_label``: a trained vocabulary's grid and
+        residue labels (merge replay on new chains); default: from this corpus."""
         self.corpus = corpus
         self.cover = cover
+        self._given = (thresholds, sym_of_label)
         self.B = int(bins)
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
         self._h = None
 
     def initialize(self):
-        self.thresholds = prologue.thresholds(self.corpus, self.B, self.cover)
+        thr, sol = self._given
+        self.thresholds = thr if thr is not None else prologue.thresholds(self.corpus, self.B, self.cover)
         self.rsym, self.gsym = prologue.symbols(self.corpus, self.thresholds, self.B)
-        self.labels, self.sym_of_label = prologue.init_labels(self.rsym)
+        if sol is None:
+            self.labels, self.sym_of_label = prologue.init_labels(self.rsym)
+        else:
+            self.sym_of_label = np.asarray(sol, dtype=np.int32)
+            lab = {int(s): i for i, s in enumerate(self.sym_of_label)}
+            missing = sorted(set(int(x) for x in np.unique(self.rsym)) - set(lab))
+            if missing:
+                raise ValueError(f"residue symbols {missing[:5]} are not in the trained vocabulary")
+            self.labels = np.array([lab[int(x)] for x in self.rsym], dtype=np.int32)
         self.K0 = len(self.sym_of_label)
         self._keep = (self.row_off, self.rsym, self.gsym, self.labels)
         L = lib()
-        self._h = L.oracle_create(len(self.row_off) - 1, _ptr(self.row_off), _ptr(self.rsym),
-                                  _ptr(self.gsym), _ptr(self.labels), self.K0, self.B)
+        if self._given[1] is None:
+            self._h = L.oracle_create(len(self.row_off) - 1, _ptr(self.row_off), _ptr(self.rsym),
+                                      _ptr(self.gsym), _ptr(self.labels), self.K0, self.B)
+        else:
+            L.oracle_create_vocab.restype = ctypes.c_void_p
+            L.oracle_create_vocab.argtypes = [ctypes.c_int64] + [ctypes.c_void_p] * 4 + [ctypes.c_int32] * 2 + \
+                [ctypes.c_void_p]
+            self._h = L.oracle_create_vocab(len(self.row_off) - 1, _ptr(self.row_off), _ptr(self.rsym),
+                                            _ptr(self.gsym), _ptr(self.labels), self.K0, self.B,
+                                            _ptr(self.sym_of_label))
         if L.oracle_error(self._h):
             raise RuntimeError("oracle: inconsistent initial labels")
         self.merges = []  # [(key_json, count)]
@@ -107,6 +127,18 @@ class OracleBPE:
             return None
         self.merges.append((self.key_json(k.value), c.value))
         return n
+
+    def step_forced(self, L: int, g: int, R: int):
+        """Merge replay: merge the content L ++ [g] ++ R next (its token id is
+        consumed even if it does not occur).  Returns (new id, count)."""
+        Lb = lib()
+        Lb.oracle_step_forced.restype = ctypes.c_int32
+        Lb.oracle_step_forced.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                          ctypes.POINTER(ctypes.c_int32)]
+        c = ctypes.c_int32(0)
+        n = Lb.oracle_step_forced(self._h, int(L), int(g), int(R), ctypes.byref(c))
+        self.merges.append((None, c.value))
+        return n, c.value
 
     def step_fast(self):
         """step() without rendering the key string (for timing)."""

@@ -92,6 +92,7 @@ typedef struct {
   int64_t step;
   ivec ev_a, ev_b;  /* merge events (left / right token start slots), iteration order */
   ivec ev_iter;     /* events before each iteration (ev_iter[t] = first event of merge t) */
+  const int32_t *given_sym; /* trained residue symbols per label (create only) */
   /* json scratch */
   char *jbufA, *jbufB;
   int64_t jcap;
@@ -298,6 +299,8 @@ static int32_t vocab_add_from(oracle_t *o, sym_fn f, int32_t obj, int32_t nres, 
 }
 
 static int32_t rsym_fn(const oracle_t *o, int32_t g, int64_t i) { (void)i; return o->rsym[g]; }
+static int32_t sym_self_fn(const oracle_t *o, int32_t s, int64_t i) { (void)o; (void)i; return s; }
+static const int32_t *given_sym_next = NULL; /* oracle_create_vocab -> oracle_create */
 
 static int same_content(const oracle_t *o, int32_t k, int32_t L, int32_t g, int32_t Rr) {
   int32_t nres = o->vnres[L] + o->vnres[Rr];
@@ -408,6 +411,7 @@ static void flush_touched(oracle_t *o) {
 oracle_t *oracle_create(int64_t nrows, const int64_t *row_off, const int32_t *rsym, const int32_t *gsym,
                         const int32_t *init_labels, int32_t K0, int32_t B) {
   oracle_t *o = (oracle_t *)calloc(1, sizeof(oracle_t));
+  o->given_sym = given_sym_next;
   o->nrows = nrows;
   o->R = row_off[nrows];
   o->B = B; o->B2 = B * B; o->B3 = B * B * B;
@@ -447,10 +451,24 @@ oracle_t *oracle_create(int64_t nrows, const int64_t *row_off, const int32_t *rs
     if (first[v] < 0) first[v] = (int32_t)g;
   }
   for (int32_t v = 0; v < K0; v++) {
+    if (o->given_sym) { /* a trained vocabulary (merge replay): label v is this symbol */
+      vocab_add_from(o, sym_self_fn, o->given_sym[v], 1, (uint64_t)(o->given_sym[v] + 1));
+      continue;
+    }
     if (first[v] < 0) { o->error = 2; vocab_add_from(o, rsym_fn, 0, 1, 0); continue; }
     vocab_add_from(o, rsym_fn, first[v], 1, (uint64_t)(o->rsym[first[v]] + 1));
   }
   free(first);
+  return o;
+}
+
+/* oracle_create with the residue labels of a trained vocabulary: label v is the
+ * residue symbol sym_of_label[v] whether or not it occurs in this corpus */
+oracle_t *oracle_create_vocab(int64_t nrows, const int64_t *row_off, const int32_t *rsym, const int32_t *gsym,
+                              const int32_t *init_labels, int32_t K0, int32_t B, const int32_t *sym_of_label) {
+  given_sym_next = sym_of_label;
+  oracle_t *o = oracle_create(nrows, row_off, rsym, gsym, init_labels, K0, B);
+  given_sym_next = NULL;
   return o;
 }
 
@@ -465,23 +483,14 @@ void oracle_bin(oracle_t *o) {
   flush_touched(o);
 }
 
-/* BPE.step(): returns the new token id, or -1 when no pair is left.
- * *count receives the winning count, *key the winning key index. */
-int32_t oracle_step(oracle_t *o, int32_t *count, int32_t *key) {
-  int32_t W = -1, c = 0;
-  while (o->hn > 0) {
-    int32_t hc = o->hc[0], hk = o->hk[0];
-    if (o->kcount[hk] == hc && hc > 0) { W = hk; c = hc; break; }
-    heap_pop(o);
-  }
-  if (W < 0) return -1;
-  heap_pop(o);
-  /* _tokens[n] = json.loads(key) (bpe.py:1857-1860) */
-  int32_t n = vocab_add_from(o, ksym, W, o->knres[W], o->khash[W]);
+int cmp_i32(const void *x, const void *y);
+
+/* merge every current occurrence of key W into token n, greedy left to right
+ * (bpe.py:1888-2014), logging the merge-tree events */
+static void apply_key(oracle_t *o, int32_t W, int32_t n) {
   /* sorted occurrences (bpe.py:1888-1895): left-token start order == (row, pos) order */
   ivec occ = {0, 0, 0};
   for (int64_t i = 0; i < o->kocc[W].n; i++) iv_push(&occ, o->kocc[W].a[i]);
-  int cmp_i32(const void *x, const void *y);
   qsort(occ.a, (size_t)occ.n, 4, cmp_i32);
   iv_push(&o->ev_iter, (int32_t)o->ev_a.n);
   for (int64_t i = 0; i < occ.n; i++) {
@@ -506,8 +515,36 @@ int32_t oracle_step(oracle_t *o, int32_t *count, int32_t *key) {
   free(occ.a);
   flush_touched(o);
   o->step++;
+}
+
+/* BPE.step(): returns the new token id, or -1 when no pair is left.
+ * *count receives the winning count, *key the winning key index. */
+int32_t oracle_step(oracle_t *o, int32_t *count, int32_t *key) {
+  int32_t W = -1, c = 0;
+  while (o->hn > 0) {
+    int32_t hc = o->hc[0], hk = o->hk[0];
+    if (o->kcount[hk] == hc && hc > 0) { W = hk; c = hc; break; }
+    heap_pop(o);
+  }
+  if (W < 0) return -1;
+  heap_pop(o);
+  /* _tokens[n] = json.loads(key) (bpe.py:1857-1860) */
+  int32_t n = vocab_add_from(o, ksym, W, o->knres[W], o->khash[W]);
+  apply_key(o, W, n);
   if (count) *count = c;
   if (key) *key = W;
+  return n;
+}
+
+/* merge replay (induce): the next merge is the given
+ * content L ++ [g] ++ R (token ids of the trained vocabulary), not the argmax;
+ * its token id is consumed even when the content does not occur. */
+int32_t oracle_step_forced(oracle_t *o, int32_t L, int32_t g, int32_t Rr, int32_t *count) {
+  int32_t W = key_get(o, L, g, Rr);
+  int32_t c = o->kcount[W];
+  int32_t n = vocab_add_from(o, ksym, W, o->knres[W], o->khash[W]);
+  apply_key(o, W, n);
+  if (count) *count = c;
   return n;
 }
 

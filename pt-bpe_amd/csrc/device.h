@@ -92,6 +92,11 @@ struct DeltaRec {  // 40 bytes, exchanged between ranks
   int32_t len, idL, g, idR, delta, pad;
 };
 static_assert(sizeof(DeltaRec) == 40, "delta record layout");
+struct ReplayRec {  // merge replay: the content of trained token K0 + t and one split of it
+  u64 h1, h2;
+  int32_t len, idL, g, idR;
+};
+static_assert(sizeof(ReplayRec) == 32, "replay record layout");
 struct LogRec {  // one merge of the run (the merge list, device side)
   int32_t nid, count, W, idL, g, idR;
   int64_t nmerged;

@@ -49,6 +49,9 @@ struct geobpe_ctx {
   bool keys_ready = false;
   bool distributed = false;
   bool bin_dense = true;
+  // merge replay (geobpe_replay_load): the trained tokens K0.. as forced merges
+  ReplayRec* replay = nullptr;
+  int64_t replay_n = 0;
   // merge-event log (geobpe_set_record_events): int4 {merge, left start, right start, 0}
   int4* ev = nullptr;
   int64_t ev_cap = 0;
@@ -246,7 +249,11 @@ void enqueue_commit(geobpe_ctx* c, bool to_delta) {
 // merge-overflow counter)
 void enqueue_select(geobpe_ctx* c) {
   Timed t(c, "select");
-  hipLaunchKernelGGL(k_select, dim3(1), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
+  if (c->replay)
+    hipLaunchKernelGGL(k_select_replay, dim3(1), dim3(64), 0, c->stream, c->D, (int)(c->gen & 1),
+                       (const ReplayRec*)c->replay, c->replay_n);
+  else
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
 }
 void enqueue_mark(geobpe_ctx* c) {
   Timed t(c, "mark");
@@ -314,6 +321,7 @@ void geobpe_destroy(geobpe_ctx* c) {
   for (void* p : c->allocs) hipFree(p);
   if (c->ev) hipFree(c->ev);
   if (c->ev_n) hipFree(c->ev_n);
+  if (c->replay) hipFree(c->replay);
   for (int i = 0; i < 9; i++)
     if (c->d_cols[i]) hipFree(c->d_cols[i]);
   if (c->h_state) hipHostFree(c->h_state);
@@ -1026,6 +1034,34 @@ double geobpe_kernel_ms(geobpe_ctx* c, const char* name, int64_t* launches) {
   }
   if (launches) *launches = it->second.second;
   return it->second.first;
+}
+
+int geobpe_replay_load(geobpe_ctx* c, const uint64_t* h_h1, const uint64_t* h_h2, const int32_t* h_len,
+                       const int32_t* h_idL, const int32_t* h_g, const int32_t* h_idR, int64_t n) {
+  if (!c || n < 0 || (n && (!h_h1 || !h_h2 || !h_len || !h_idL || !h_g || !h_idR))) return GEOBPE_EARG;
+  if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
+  if (c->distributed) return fail(c, GEOBPE_EARG, "merge replay is single-rank");
+  if (c->h_state->iter > 0) return fail(c, GEOBPE_EARG, "merge replay must start before the first merge");
+  if (c->K0 + n > c->max_vocab) return fail(c, GEOBPE_ECAPACITY, "K0 + %lld merges exceed max_vocab", (long long)n);
+  std::vector<ReplayRec> r((size_t)n);
+  for (int64_t t = 0; t < n; t++) {
+    const int32_t v = c->K0 + (int32_t)t;
+    if (h_idL[t] < 0 || h_idL[t] >= v || h_idR[t] < 0 || h_idR[t] >= v || h_len[t] < 2)
+      return fail(c, GEOBPE_EARG, "replay record %lld: split (%d, %d) is not of earlier tokens", (long long)t,
+                  h_idL[t], h_idR[t]);
+    r[t] = ReplayRec{h_h1[t], h_h2[t], h_len[t], h_idL[t], h_g[t], h_idR[t]};
+  }
+  HIPCHK(c, hipSetDevice(c->device));
+  if (c->replay) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(c->replay);
+    c->replay = nullptr;
+  }
+  HIPCHK(c, hipMalloc(&c->replay, std::max<size_t>(1, (size_t)n) * sizeof(ReplayRec)));
+  if (n)
+    HIPCHK(c, hipMemcpyAsync(c->replay, r.data(), (size_t)n * sizeof(ReplayRec), hipMemcpyHostToDevice, c->stream));
+  c->replay_n = n;
+  return 0;
 }
 
 int geobpe_set_record_events(geobpe_ctx* c, int on) {

@@ -761,6 +761,85 @@ __global__ __launch_bounds__(BLOCK) void k_select(Dev D, int par) {
   mark_select(D, par, &W);
 }
 
+// merge replay (bin/induce.py): merge t is the trained
+// token K0 + t, not the argmax.  Its key is looked up by content hash (find
+// only); absent or at count 0 it merges nothing but still takes its token id.
+// The posting index is rebuilt by the training rule (a rebuild iteration
+// consumes no merge).  One thread: a few loads.
+__global__ __launch_bounds__(64) void k_select_replay(Dev D, int par, const ReplayRec* fk, int64_t M) {
+  if (threadIdx.x != 0) return;
+  State* st = D.st;
+  Sel* out = D.sel + par;
+  const int32_t iter = st->iter, K = st->K;
+  if (st->done || iter >= M) {
+    out->decision = SEL_DONE;
+    out->maxc = 0;
+    return;
+  }
+  if (K >= D.KC) {
+    set_error(D, GEOBPE_ECAPACITY, -9);
+    out->decision = SEL_DONE;
+    return;
+  }
+  const ReplayRec r = fk[iter];
+  const u64 k = probe_key(r.h1, r.h2, r.len);
+  const u64 mask = (u64)D.HC - 1;
+  u64 s = ht_first_slot(D, k);
+  int32_t W = -1;
+  for (int64_t probe = 0; probe < D.HC; probe++) {
+    const u64 cur = D.ht_key[s];
+    if (cur == k) {
+      W = (int32_t)s;
+      break;
+    }
+    if (cur == 0) break;
+    s = (s + 1) & mask;
+  }
+  if (W >= 0 && (D.kh1[W] != r.h1 || D.kh2[W] != r.h2 || D.klen[W] != r.len)) {
+    set_error(D, GEOBPE_EHASH, iter);
+    out->decision = SEL_DONE;
+    return;
+  }
+  const int32_t c = W >= 0 ? D.count[W] : 0;
+  if (c <= 0) W = -1;
+  const bool post = c > 0 && (st->post_valid == 0 || st->plog_ovf != 0 || st->plog_total > D.LOGMAX) &&
+                    (int64_t)c * 64 <= D.LOGMAX;
+  if (post) {
+    out->decision = SEL_SKIP;
+    out->skip = SKIP_POST;
+    out->theta_new = max(1, st->theta);
+    out->build = st->cl_act;
+    return;
+  }
+  D.vh1[K] = r.h1;
+  D.vh2[K] = r.h2;
+  D.vlen[K] = r.len;
+  LogRec lr;
+  lr.nid = K;
+  lr.count = c;
+  lr.W = W;
+  lr.idL = r.idL;
+  lr.g = r.g;
+  lr.idR = r.idR;
+  lr.nmerged = 0;
+  D.log[iter] = lr;
+  out->decision = SEL_MERGE;
+  out->skip = 0;
+  out->W = W;
+  out->nid = K;
+  out->iter = iter;
+  out->tag = iter + 1;
+  out->maxc = c;
+  out->ncand = 1;
+  out->w1 = r.h1;
+  out->w2 = r.h2;
+  out->wl = r.len;
+  out->wfp = W >= 0 ? key_fp(W) : 0;
+  out->widL = r.idL;
+  out->wg = r.g;
+  out->widR = r.idR;
+}
+
 __global__ __launch_bounds__(BLOCK) void k_mark(Dev D, int par) {
   __shared__ int32_t s_n;
   const bool posting = D.st->post_valid && !D.st->plog_ovf;
@@ -768,6 +847,11 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D, int par) {
   if (!posting && blockIdx.x < D.NBA) check_found(D, blockIdx.x);
   if (sel.decision != SEL_MERGE) {
     if (posting && blockIdx.x % RPB == RPB - 1) check_found(D, blockIdx.x / RPB);
+    return;
+  }
+  if (sel.W < 0) {  // merge replay of a content with no occurrence: empty regions
+    if (posting && blockIdx.x % RPB == RPB - 1) check_found(D, blockIdx.x / RPB);
+    if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = 0;
     return;
   }
   const int32_t W = sel.W, tag = sel.tag;

@@ -81,6 +81,7 @@ def lib():
         "geobpe_set_profiling_filter": (ctypes.c_int, [P, ctypes.c_char_p]),
         "geobpe_synchronize": (ctypes.c_int, [P]),
         "geobpe_set_record_events": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_replay_load": (ctypes.c_int, [P, P, P, P, P, P, P, I64]),
         "geobpe_events": (I64, [P, P, P, P]),
     }
     for name, (res, args) in sig.items():
@@ -99,7 +100,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
     "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_synchronize",
-    "geobpe_set_record_events", "geobpe_events",
+    "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",
 ]
 
 

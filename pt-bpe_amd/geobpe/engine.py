@@ -115,25 +115,37 @@ class GeoBPEEngine:
             pass
 
     # ------------------------------------------------------------ prologue
-    def initialize(self):
+    def initialize(self, thresholds: Optional[dict] = None, sym_of_label=None):
+        """Thresholds (bpe.py:820-876), residue symbols and first-appearance labels.
+        ``thresholds`` ({type: [(start, end)]}) and ``sym_of_label`` fix a trained
+        vocabulary's grid and residue labels instead (merge replay on new chains)."""
         arr = (ctypes.c_void_p * 9)(*[c.ctypes.data for c in self._cols])
         self._chk(self.L.geobpe_load_angles(self._ctx, self.n_rows, _p(self.row_off), arr))
-        mm = np.zeros(12, dtype=np.float64)
-        cnt = np.zeros(6, dtype=np.int64)
-        self._chk(self.L.geobpe_angle_range(self._ctx, _p(mm), _p(cnt)))
-        n_rows_total = self.n_rows
-        if self.distributed:
-            mm, cnt, n_rows_total = self.group.reduce_ranges(mm, cnt, self.n_rows)
-        w0 = (init_bond_angle() + TWO_PI) % TWO_PI
         edges = np.zeros((6, self.B + 1), dtype=np.float64)
-        self.thresholds = {}
-        for t, key in enumerate(ANGLE_TYPES):
-            mn, mx, c = float(mm[2 * t]), float(mm[2 * t + 1]), int(cnt[t])
-            if key == "tau" and n_rows_total > 0:  # bpe.py:845-846: + _bond_angle(0) per tokenizer
-                mn, mx, c = (min(mn, w0), max(mx, w0), c + n_rows_total) if c > 0 else (w0, w0, n_rows_total)
-            e = histogram_edges(mn, mx, c, self.B, self.cover)
-            edges[t] = e
-            self.thresholds[key] = [(float(s), float(f)) for s, f in zip(e[:-1], e[1:])]
+        if thresholds is not None:
+            self.thresholds = {}
+            for t, key in enumerate(ANGLE_TYPES):
+                v = [(float(a), float(b)) for a, b in thresholds[key]]
+                if len(v) != self.B:
+                    raise ValueError(f"thresholds[{key!r}] has {len(v)} bins, expected {self.B}")
+                edges[t] = [a for a, _ in v] + [v[-1][1]]
+                self.thresholds[key] = v
+        else:
+            mm = np.zeros(12, dtype=np.float64)
+            cnt = np.zeros(6, dtype=np.int64)
+            self._chk(self.L.geobpe_angle_range(self._ctx, _p(mm), _p(cnt)))
+            n_rows_total = self.n_rows
+            if self.distributed:
+                mm, cnt, n_rows_total = self.group.reduce_ranges(mm, cnt, self.n_rows)
+            w0 = (init_bond_angle() + TWO_PI) % TWO_PI
+            self.thresholds = {}
+            for t, key in enumerate(ANGLE_TYPES):
+                mn, mx, c = float(mm[2 * t]), float(mm[2 * t + 1]), int(cnt[t])
+                if key == "tau" and n_rows_total > 0:  # bpe.py:845-846: + _bond_angle(0) per tokenizer
+                    mn, mx, c = (min(mn, w0), max(mx, w0), c + n_rows_total) if c > 0 else (w0, w0, n_rows_total)
+                e = histogram_edges(mn, mx, c, self.B, self.cover)
+                edges[t] = e
+                self.thresholds[key] = [(float(s), float(f)) for s, f in zip(e[:-1], e[1:])]
         self._edges = edges
         self._chk(self.L.geobpe_quantize(self._ctx, self.B, _p(edges), init_bond_angle()))
         S = self.B ** 3 + self.B
@@ -143,14 +155,33 @@ class GeoBPEEngine:
         if self.distributed:
             first = self.group.reduce_first(first)
         present = np.nonzero(first != np.iinfo(np.int64).max)[0]
-        order = present[np.argsort(first[present], kind="stable")]
         label_of_sym = np.full(S, -1, dtype=np.int32)
-        label_of_sym[order] = np.arange(len(order), dtype=np.int32)
+        if sym_of_label is not None:
+            order = np.asarray(sym_of_label, dtype=np.int64)
+            label_of_sym[order] = np.arange(len(order), dtype=np.int32)
+            unknown = present[label_of_sym[present] < 0]
+            if len(unknown):
+                raise ValueError(f"{len(unknown)} residue geometries (symbols {unknown[:5].tolist()}) are not in "
+                                 "the trained vocabulary")
+        else:
+            order = present[np.argsort(first[present], kind="stable")]
+            label_of_sym[order] = np.arange(len(order), dtype=np.int32)
         self.K0 = int(len(order))
         self.sym_of_label = order.astype(np.int32)
         self._chk(self.L.geobpe_init_tokens(self._ctx, _p(label_of_sym), self.K0))
         self._initialized = True
         return self
+
+    def replay_load(self, rec: dict):
+        """Merge replay: merge t becomes the trained token K0 + t (geobpe.induce
+        builds ``rec``: h1, h2, len, idL, g, idR arrays)."""
+        if not self._binned:
+            raise RuntimeError("bin() first")
+        h1 = np.ascontiguousarray(rec["h1"], dtype=np.uint64)
+        h2 = np.ascontiguousarray(rec["h2"], dtype=np.uint64)
+        ln, a, g, b = (np.ascontiguousarray(rec[k], dtype=np.int32) for k in ("len", "idL", "g", "idR"))
+        self._chk(self.L.geobpe_replay_load(self._ctx, _p(h1), _p(h2), _p(ln), _p(a), _p(g), _p(b), len(h1)))
+        self._replay_n = len(h1)
 
     # ------------------------------------------------------------ histogram / merges
     def bin(self):

@@ -237,20 +237,14 @@ def symbols(cols: dict, thr: dict, B: int):
 
 
 # ------------------------------------------------------------------ the checkpoint object
-def build(run: dict):
-    """The reference BPE object graph of a GeoBPE run.
-
-    ``run``: corpus (columns + row_off), fnames, B, bins, bin_strategy,
-    thresholds (grid-1 {type: [(start, end)]}), bin_counts ({type: [count]}),
-    K0, tokens (BPE._tokens), seg_start / seg_id / seg_off (final segmentation,
-    chain-local residue starts), ev_a / ev_b / ev_off (merge events: global
-    left / right token start slots, events of merge t in [ev_off[t],
-    ev_off[t+1])), step, times, the constructor arguments in ``args``."""
+def build_tokenizers(run: dict, C=None):
+    """Tokenizer records of a run's chains (frames, bond_to_token with the merge
+    tree, token_pos, tokens, fixed attributes) and its pair index
+    (``_geo_dict`` / ``_geo_step``).  ``run["sym_of_label"]`` fixes the residue
+    labels of a trained vocabulary (merge replay); default: first appearance."""
     import pandas as pd
-    import torch
-    from sortedcontainers import SortedDict
 
-    C = _real_or_local()
+    C = C or _real_or_local()
     corpus = run["corpus"]
     ro = np.asarray(corpus["row_off"], dtype=np.int64)
     B = int(run["B"])
@@ -268,11 +262,14 @@ def build(run: dict):
         rs, gs = symbols(cols, thr1, B)
         rsyms.append(rs)
         gsyms.append(gs)
-    allr = np.concatenate(rsyms) if nrows else np.zeros(0, np.int64)
-    uniq, first = np.unique(allr, return_index=True)
-    label_of_sym = {int(s): i for i, s in enumerate(uniq[np.argsort(first, kind="stable")])}
+    if run.get("sym_of_label") is not None:
+        label_of_sym = {int(sy): i for i, sy in enumerate(run["sym_of_label"])}
+    else:
+        allr = np.concatenate(rsyms) if nrows else np.zeros(0, np.int64)
+        uniq, first = np.unique(allr, return_index=True)
+        label_of_sym = {int(sy): i for i, sy in enumerate(uniq[np.argsort(first, kind="stable")])}
     if len(label_of_sym) != K0:
-        raise ValueError(f"corpus has {len(label_of_sym)} residue symbols, run says K0={K0}")
+        raise ValueError(f"{len(label_of_sym)} residue labels, run says K0={K0}")
     chain_of = np.searchsorted(ro, np.arange(int(ro[-1])), side="right") - 1 if nrows else np.zeros(0, np.int64)
 
     trees = []
@@ -308,23 +305,6 @@ def build(run: dict):
         for k in range(len(st) - 2):
             key = span_key(rsyms[r], gsyms[r], st[k], st[k + 2] - 1, st[k + 2] == n, B)
             geo[key].add((r, 3 * st[k + 1]))
-    prio = SortedDict()
-    k2p = {}
-    for key, occ in geo.items():
-        p = (True, -len(occ), key)
-        prio[p] = None
-        k2p[key] = p
-
-    # grid-1 state (bpe.py:856-876)
-    thresholds = _new_dict(C["ThresholdDict"], [(1, {k: list(v) for k, v in thr1.items()})]
-                           + [(bt, [(BOND_LENGTHS[bt], BOND_LENGTHS[bt])]) for bt in BOND_TYPES], {})
-    thresholds.__dict__["_int_keys"] = [1]
-    counts = {k: [np.int64(c) for c in run["bin_counts"][k]] for k in ANGLE_KEYS}
-    bin_counts = _new_dict(C["ThresholdDict"], [(1, counts)], {"_int_keys": [1]})
-    centers = _new_dict(C["ThresholdDict"], [(1, {k: torch.tensor(v, dtype=torch.float32).mean(axis=-1)
-                                                  for k, v in thr1.items()})], {"_int_keys": [1]})
-    weights = _new_dict(C["ThresholdDict"], [(1, {k: torch.tensor(v, dtype=torch.float32) / sum(v)
-                                                  for k, v in counts.items()})], {"_int_keys": [1]})
 
     tiba = thr1["tau"]
     init_tau = _centre(tiba, _get_ind(tiba, _wrap(init_bond_angle())))
@@ -336,9 +316,9 @@ def build(run: dict):
         st = [int(x) for x in seg_start[seg_off[r]:seg_off[r + 1]]]
         ids = [int(x) for x in seg_id[seg_off[r]:seg_off[r + 1]]]
         btt = []
-        for k, (s, v) in enumerate(zip(st, ids)):
+        for k, (s0, v) in enumerate(zip(st, ids)):
             e = st[k + 1] if k + 1 < len(st) else n
-            btt.append((3 * s, (3 * s, v, 3 * (e - s) - (1 if e == n else 0))))
+            btt.append((3 * s0, (3 * s0, v, 3 * (e - s0) - (1 if e == n else 0))))
         token_pos = []
         for _, (s3, _, nb) in btt:
             token_pos.extend([s3] * nb)
@@ -360,6 +340,44 @@ def build(run: dict):
             "_init_bond_angle": init_tau, "token_pos": token_pos, "tokens": init_tokens,
         })
         tokenizers.append(tok)
+    return tokenizers, {"geo": geo, "geo_step": geo_step, "rsyms": rsyms, "thr1": thr1}
+
+
+def build(run: dict):
+    """The reference BPE object graph of a GeoBPE run.
+
+    ``run``: corpus (columns + row_off), fnames, B, bins, bin_strategy,
+    thresholds (grid-1 {type: [(start, end)]}), bin_counts ({type: [count]}),
+    K0, tokens (BPE._tokens), seg_start / seg_id / seg_off (final segmentation,
+    chain-local residue starts), ev_a / ev_b / ev_off (merge events: global
+    left / right token start slots, events of merge t in [ev_off[t],
+    ev_off[t+1])), step, times, the constructor arguments in ``args``."""
+    import pandas as pd
+    import torch
+    from sortedcontainers import SortedDict
+
+    C = _real_or_local()
+    tokenizers, extra = build_tokenizers(run, C)
+    geo, geo_step, rsyms = extra["geo"], extra["geo_step"], extra["rsyms"]
+    nrows = len(tokenizers)
+    thr1 = extra["thr1"]
+    prio = SortedDict()
+    k2p = {}
+    for key, occ in geo.items():
+        p = (True, -len(occ), key)
+        prio[p] = None
+        k2p[key] = p
+
+    # grid-1 state (bpe.py:856-876)
+    thresholds = _new_dict(C["ThresholdDict"], [(1, {k: list(v) for k, v in thr1.items()})]
+                           + [(bt, [(BOND_LENGTHS[bt], BOND_LENGTHS[bt])]) for bt in BOND_TYPES], {})
+    thresholds.__dict__["_int_keys"] = [1]
+    counts = {k: [np.int64(c) for c in run["bin_counts"][k]] for k in ANGLE_KEYS}
+    bin_counts = _new_dict(C["ThresholdDict"], [(1, counts)], {"_int_keys": [1]})
+    centers = _new_dict(C["ThresholdDict"], [(1, {k: torch.tensor(v, dtype=torch.float32).mean(axis=-1)
+                                                  for k, v in thr1.items()})], {"_int_keys": [1]})
+    weights = _new_dict(C["ThresholdDict"], [(1, {k: torch.tensor(v, dtype=torch.float32) / sum(v)
+                                                  for k, v in counts.items()})], {"_int_keys": [1]})
 
     a = run.get("args", {})
     seed = a.get("seed")
