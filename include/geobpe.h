@@ -112,6 +112,11 @@ int geobpe_step_apply(geobpe_ctx *ctx, int64_t *n_merged);
 int geobpe_delta_export(geobpe_ctx *ctx, void *d_out, int64_t cap, int64_t *n_records);
 /* Add the records (from every rank, this one included) to the global counts. */
 int geobpe_delta_import(geobpe_ctx *ctx, const void *d_in, int64_t n_records);
+/* Stream-ordered variants (no host synchronisation): the export writes its
+ * record count to d_count (device int64; GEOBPE_ECAPACITY at the next sync if it
+ * exceeds cap); the import of n_records is only enqueued. */
+int geobpe_delta_export_async(geobpe_ctx *ctx, void *d_out, int64_t cap, void *d_count);
+int geobpe_delta_import_async(geobpe_ctx *ctx, const void *d_in, int64_t n_records);
 /* 1 = multi-rank mode (local changes go to the delta buffer), 0 = single.
  * Must precede geobpe_bin(). */
 int geobpe_set_distributed(geobpe_ctx *ctx, int on);

@@ -777,8 +777,7 @@ int geobpe_delta_export(geobpe_ctx* c, void* d_out, int64_t cap, int64_t* n_reco
   return 0;
 }
 
-int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
-  if (!c || !c->distributed) return GEOBPE_EARG;
+static int delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
   HIPCHK(c, hipSetDevice(c->device));
   const int64_t chunk = (int64_t)c->nba * (c->D.RC - 256);
   int rc;
@@ -789,7 +788,28 @@ int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
     HIPCHK(c, hipGetLastError());
     enqueue_commit(c, false);
   }
+  return 0;
+}
+
+int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
+  if (!c || !c->distributed) return GEOBPE_EARG;
+  int rc;
+  if ((rc = delta_import(c, d_in, n_records))) return rc;
   return sync_state(c);
+}
+
+int geobpe_delta_export_async(geobpe_ctx* c, void* d_out, int64_t cap, void* d_count) {
+  if (!c || !c->distributed || !d_out || !d_count) return GEOBPE_EARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (DeltaRec*)d_out, cap);
+  hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_count, cap);
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int geobpe_delta_import_async(geobpe_ctx* c, const void* d_in, int64_t n_records) {
+  if (!c || !c->distributed) return GEOBPE_EARG;
+  return delta_import(c, d_in, n_records);
 }
 
 int64_t geobpe_token_json(geobpe_ctx* c, int32_t v, char* buf, int64_t cap) {

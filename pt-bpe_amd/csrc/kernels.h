@@ -1459,6 +1459,34 @@ __global__ __launch_bounds__(BLOCK) void k_export(Dev D, DeltaRec* out, int64_t 
   }
 }
 
+// device-counted export (no host round trip): every touched key's record, up to
+// cap; k_export_fin then publishes the count and opens the next epoch
+__global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int64_t cap) {
+  const int64_t n = min(D.st->ntouched, cap);
+  for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t d = D.touched[j];
+    DeltaRec r;
+    r.h1 = D.kh1[d];
+    r.h2 = D.kh2[d];
+    r.len = D.klen[d];
+    r.idL = D.krep[3 * d];
+    r.g = D.krep[3 * d + 1];
+    r.idR = D.krep[3 * d + 2];
+    r.delta = D.dcount[d];
+    r.pad = 0;
+    D.dcount[d] = 0;
+    out[j] = r;
+  }
+}
+__global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap) {
+  State* st = D.st;
+  const int64_t n = st->ntouched;
+  d_count[0] = n;
+  if (n > cap) set_error(D, GEOBPE_ECAPACITY, -30);
+  st->ntouched = 0;
+  st->epoch += 1;  // every key may be touched again
+}
+
 __global__ __launch_bounds__(ABLOCK) void k_import(Dev D, const DeltaRec* in, int64_t n) {
   __shared__ int32_t s_np, s_ns;
   if (threadIdx.x == 0) s_np = s_ns = 0;

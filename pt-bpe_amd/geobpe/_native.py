@@ -82,6 +82,8 @@ def lib():
         "geobpe_synchronize": (ctypes.c_int, [P]),
         "geobpe_set_record_events": (ctypes.c_int, [P, ctypes.c_int]),
         "geobpe_replay_load": (ctypes.c_int, [P, P, P, P, P, P, P, I64]),
+        "geobpe_delta_export_async": (ctypes.c_int, [P, P, I64, P]),
+        "geobpe_delta_import_async": (ctypes.c_int, [P, P, I64]),
         "geobpe_events": (I64, [P, P, P, P]),
     }
     for name, (res, args) in sig.items():
@@ -101,6 +103,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
     "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_synchronize",
     "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",
+    "geobpe_delta_export_async", "geobpe_delta_import_async",
 ]
 
 

@@ -97,7 +97,7 @@ class TorchGroup:
 
     def export_buffer(self, engine):
         if self._buf is None:
-            cap = self.R_local + 65536
+            cap = 3 * self.R_local + 65536  # keys touched by one merge: <= 5 per occurrence, <= R/2 occurrences
             self._buf = self.torch.empty(cap * REC, dtype=self.torch.uint8, device=self.dev)
             self._cap = cap
         return self._cap, ctypes.c_void_p(self._buf.data_ptr())
@@ -122,6 +122,43 @@ class TorchGroup:
         if self.dev.type == "cuda":
             T.cuda.current_stream(self.dev).synchronize()
         return ctypes.c_void_p(flat.data_ptr()), int(sum(counts))
+
+
+    def exchange_async(self, engine):
+        """One merge's exchange with two host waits in all: the export count is
+        written on the device and all-gathered, the host reads the counts (the
+        only sync), then the records are all-gathered and imported stream-ordered
+        (ProcessGroupNCCL orders the collectives after / before the engine's
+        kernels on the current stream; gloo goes through host copies)."""
+        T = self.torch
+        with T.cuda.stream(engine.torch_stream):
+            self._exchange_on_stream(engine)
+
+    def _exchange_on_stream(self, engine):
+        T = self.torch
+        cap, ptr = self.export_buffer(engine)
+        if getattr(self, "_cnt", None) is None:
+            self._cnt = T.zeros(1, dtype=T.int64, device=self.dev)
+        engine._chk(engine.L.geobpe_delta_export_async(engine._ctx, ptr, cap, ctypes.c_void_p(self._cnt.data_ptr())))
+        src = self._cnt if self.on_gpu else self._cnt.cpu()
+        outs = [T.zeros_like(src) for _ in range(self.world_size)]
+        self.dist.all_gather(outs, src, group=self.pg)
+        counts = [int(x) for x in T.cat(outs).cpu().tolist()]
+        if max(counts) > cap:
+            raise _native.GeoBPEError(f"delta export needs {max(counts)} records (cap {cap})")
+        m = max(counts)
+        if m == 0:
+            return
+        src = self._buf[: m * REC]
+        if not self.on_gpu:
+            src = src.cpu()
+        out = T.empty(self.world_size * m * REC, dtype=T.uint8, device=src.device)
+        self.dist.all_gather_into_tensor(out, src, group=self.pg)
+        out = out.view(self.world_size, m * REC)
+        flat = T.cat([out[r, : counts[r] * REC] for r in range(self.world_size)]).to(self.dev)
+        self._keep = flat
+        engine._chk(engine.L.geobpe_delta_import_async(engine._ctx, ctypes.c_void_p(flat.data_ptr()),
+                                                       int(sum(counts))))
 
 
 class _VirtualGroup:

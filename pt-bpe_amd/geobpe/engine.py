@@ -80,6 +80,13 @@ class GeoBPEEngine:
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
         self.n_rows = len(self.row_off) - 1
         self._cols = [np.ascontiguousarray(corpus[c], dtype=np.float64) for c in COLUMNS]
+        self.torch_stream = None
+        if stream is None and group is not None and getattr(group, "world_size", 1) > 1:
+            # multi-rank: the engine's kernels and the exchange's torch ops (copies,
+            # collectives) must be ordered on ONE stream -- a torch stream of our own
+            import torch
+            self.torch_stream = torch.cuda.Stream(device=self.device)
+            stream = ctypes.c_void_p(self.torch_stream.cuda_stream)
         if stream is None and use_torch_stream:
             stream = _stream_handle(self.device)
         self._ctx = ctypes.c_void_p()
@@ -221,7 +228,7 @@ class GeoBPEEngine:
                 self._done = True
                 return None
             self._chk(self.L.geobpe_step_apply(self._ctx, ctypes.byref(nm) if want_merged else None))
-            self._exchange()
+            self.group.exchange_async(self)
         want = want_merged or not self.distributed
         rec = (int(nid.value), int(cnt.value), int(nm.value) if want else -1)
         self.merges.append(rec)

@@ -72,3 +72,60 @@ def test_torchgroup_gloo_world2():
     for p in ps:
         p.join(timeout=60)
     assert res == {0: "ok", 1: "ok"}
+
+
+def _engine_worker(rank, world, port, q):
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "pt-bpe_amd"))
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from geobpe import synth
+        from geobpe.dist import TorchGroup, shard_rows, slice_corpus
+        from geobpe.engine import GeoBPEEngine
+        corpus = synth.make_corpus(synth.make_lengths(2000, 20, 300, seed=91), seed=91, repeat_frac=0.05)
+        lo, hi = shard_rows(corpus["row_off"], world)[rank]
+        shard = slice_corpus(corpus, lo, hi)
+        g = TorchGroup(int(shard["row_off"][-1]), device=0)
+        e = GeoBPEEngine(shard, 5, device=0, group=g).initialize()
+        e.bin()
+        done = e.run(150)
+        s, ids, off = e.segmentation()
+        q.put((rank, done, e.merge_keys(), ids.tolist()))
+    except Exception as ex:  # pragma: no cover
+        q.put((rank, -1, repr(ex), None))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 3])
+def test_multirank_engine_on_one_gpu_matches_single(world, oracle_lib):
+    """The full N>1 path (TorchGroup exchange, stream-ordered export/import, one
+    process per rank) with gloo on one device: merge list and segmentation equal
+    the single-engine run and the oracle."""
+    import multiprocessing as mp
+    from geobpe import synth
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_engine_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert all(r[1] == 150 for r in res), res[0][2] if res[0][1] < 0 else None
+    corpus = synth.make_corpus(synth.make_lengths(2000, 20, 300, seed=91), seed=91, repeat_frac=0.05)
+    o = oracle_lib.OracleBPE(corpus, 5).initialize()
+    o.bin()
+    for _ in range(150):
+        o.step()
+    assert all(r[2] == o.merges for r in res)
+    _, ids, _ = o.segmentation()
+    assert sum((r[3] for r in res), []) == ids.tolist()
