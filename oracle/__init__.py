@@ -76,11 +76,13 @@ def _ptr(a: np.ndarray):
 class OracleBPE:
     """Scoped-mode GeoBPE on the CPU: ``initialize()``, ``bin()``, ``step()``."""
 
-    def __init__(self, corpus: dict, bins: int, cover: bool = False, thresholds=None, sym_of_label=None):
+    def __init__(self, corpus: dict, bins: int, cover: bool = False, thresholds=None, sym_of_label=None,
+                 strategy: str = None):
         """``thresholds`` / ``sym_of_label``: a trained vocabulary's grid and
         residue labels (merge replay on new chains); default: from this corpus."""
         self.corpus = corpus
         self.cover = cover
+        self.strategy = strategy
         self._given = (thresholds, sym_of_label)
         self.B = int(bins)
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
@@ -88,7 +90,7 @@ class OracleBPE:
 
     def initialize(self):
         thr, sol = self._given
-        self.thresholds = thr if thr is not None else prologue.thresholds(self.corpus, self.B, self.cover)
+        self.thresholds = thr if thr is not None else prologue.thresholds(self.corpus, self.B, self.cover, self.strategy)
         self.rsym, self.gsym = prologue.symbols(self.corpus, self.thresholds, self.B)
         if sol is None:
             self.labels, self.sym_of_label = prologue.init_labels(self.rsym)

@@ -39,8 +39,10 @@ def init_bond_angle() -> float:
     return float(np.arccos(np.clip(np.dot(u1, u2), -1.0, 1.0)))
 
 
-def thresholds(corpus: dict, B: int, cover: bool = False) -> dict:
-    """``cover``: bin_strategy "histogram-cover" -> range=(0, 2pi) (plotting.py:319)."""
+def thresholds(corpus: dict, B: int, cover: bool = False, strategy: str = None) -> dict:
+    """``cover``: bin_strategy "histogram-cover" -> range=(0, 2pi) (plotting.py:319);
+    ``strategy="uniform"``: equal-count edges, np.quantile of the sorted values
+    (save_histogram_equal_counts / equal_count_bin_edges, plotting.py:256-302)."""
     n_rows = len(corpus["row_off"]) - 1
     init = init_bond_angle()
     out = {}
@@ -50,7 +52,10 @@ def thresholds(corpus: dict, B: int, cover: bool = False) -> dict:
         if key == "tau":
             vals = np.concatenate([vals, np.full(n_rows, init)])
         a = (vals + 2 * np.pi) % (2 * np.pi)
-        _, edges = np.histogram(a, bins=B, range=(0, 2 * np.pi) if cover else None)
+        if strategy == "uniform":
+            edges = np.quantile(np.sort(a), np.linspace(0, 1, B + 1))
+        else:
+            _, edges = np.histogram(a, bins=B, range=(0, 2 * np.pi) if cover else None)
         out[key] = [(float(s), float(e)) for s, e in zip(edges[:-1], edges[1:])]
     return out
 

@@ -18,7 +18,7 @@ mode uses, so a caller of the reference (bin/encode.py, train.py) can switch:
 
 Scope: res_init=True, rmsd_partition_min_size=inf (no RMSD
 partitioning), glue_opt=False, std_bonds=True, bins={1: B},
-bin_strategy "histogram" or "histogram-cover".  Any other configuration raises
+bin_strategy "histogram", "histogram-cover" or "uniform".  Any other configuration raises
 NotImplementedError up front (the reference would run its float-geometry RMSD /
 LBFGS paths there).
 
@@ -146,8 +146,8 @@ def _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_siz
         raise KeyError("bins must be a dict with key 1 (quantize/capacity need bins[1], bpe.py:896,909,952)")
     if len(bins) != 1:
         raise NotImplementedError("multi-grid bin schedules (--bins 1-a:s-b) are not in this build (SURVEY §8(f) row 3)")
-    if bin_strategy not in ("histogram", "histogram-cover"):
-        raise NotImplementedError(f"bin_strategy={bin_strategy!r} (only histogram / histogram-cover)")
+    if bin_strategy not in ("histogram", "histogram-cover", "uniform"):
+        raise NotImplementedError(f"bin_strategy={bin_strategy!r} (histogram / histogram-cover / uniform)")
     if not res_init:
         raise NotImplementedError("res_init=False cannot quantize in the reference either (SURVEY App. A)")
     if not std_bonds:
@@ -201,7 +201,7 @@ class BPE:
         self._ious = []
         self._tokens = {}
         self._engine = GeoBPEEngine(corpus, self.B, device=device, max_vocab=max_vocab, group=group,
-                                    cover=bin_strategy == "histogram-cover")
+                                    strategy=bin_strategy)
         self._tok_cache = None
         self._record_tree = bool(record_tree) and group is None
 

@@ -51,6 +51,20 @@ def histogram_edges(mn: float, mx: float, count: int, B: int, cover: bool = Fals
     return np.histogram_bin_edges(a, bins=B, range=(0, TWO_PI) if cover else None)
 
 
+def equal_count_edges(col: np.ndarray, n_rows: int, key: str, B: int) -> np.ndarray:
+    """bin_strategy "uniform": np.quantile of the sorted wrapped values at
+    linspace(0, 1, B+1) (equal_count_bin_edges / save_histogram_equal_counts,
+    plotting.py:256-302), over the values _init_thresholds collects (non-NaN,
+    non-zero; tau + the init angle per chain, bpe.py:842-846).  An order
+    statistic of the whole column: computed on the host copy of the input (the
+    prologue; the histogram strategies need only the device min / max)."""
+    vals = col[np.nan_to_num(col, nan=0.0) != 0.0]
+    if key == "tau":
+        vals = np.concatenate([vals, np.full(n_rows, init_bond_angle())])
+    a = (vals + TWO_PI) % TWO_PI
+    return np.quantile(np.sort(a), np.linspace(0, 1, B + 1))
+
+
 def _p(a: np.ndarray):
     return a.ctypes.data_as(ctypes.c_void_p)
 
@@ -68,7 +82,7 @@ def _stream_handle(device: int):
 class GeoBPEEngine:
     def __init__(self, corpus: dict, bins: int, device: int = 0, max_vocab: int = 1 << 20,
                  group=None, stream=None, use_torch_stream: bool = True, cover: bool = False,
-                 bin_dense: bool = True):
+                 bin_dense: bool = True, strategy: Optional[str] = None):
         """``corpus``: ``{column: float64[R]}`` + ``row_off`` (geobpe.synth layout) for
         THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs."""
         self.L = _native.lib()
@@ -76,6 +90,10 @@ class GeoBPEEngine:
         self.device = int(device)
         self.group = group
         self.cover = bool(cover)
+        self.strategy = strategy or ("histogram-cover" if cover else "histogram")
+        if self.strategy not in ("histogram", "histogram-cover", "uniform"):
+            raise NotImplementedError(f"bin_strategy={self.strategy!r}")
+        self.cover = self.strategy == "histogram-cover"
         self.bin_dense = bool(bin_dense)
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
         self.n_rows = len(self.row_off) - 1
@@ -137,6 +155,14 @@ class GeoBPEEngine:
                     raise ValueError(f"thresholds[{key!r}] has {len(v)} bins, expected {self.B}")
                 edges[t] = [a for a, _ in v] + [v[-1][1]]
                 self.thresholds[key] = v
+        elif self.strategy == "uniform":
+            if self.distributed:
+                raise NotImplementedError("uniform bins need the global quantiles: single rank only")
+            self.thresholds = {}
+            for t, key in enumerate(ANGLE_TYPES):
+                e = equal_count_edges(self._cols[COLUMNS.index(key)], self.n_rows, key, self.B)
+                edges[t] = e
+                self.thresholds[key] = [(float(s), float(f)) for s, f in zip(e[:-1], e[1:])]
         else:
             mm = np.zeros(12, dtype=np.float64)
             cnt = np.zeros(6, dtype=np.int64)

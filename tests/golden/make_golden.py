@@ -40,6 +40,7 @@ FIXTURES = {
     "g300x60-200_b5": (300, 60, 200, 5, 40, 5, 0.0),
     "g80x40-160_b7_rep": (80, 40, 160, 7, 100, 6, 0.1),
     "g50x30-110_b6_cover": (50, 30, 110, 6, 80, 7, 0.1, "histogram-cover"),
+    "g50x30-110_b5_uniform": (50, 30, 110, 5, 80, 8, 0.1, "uniform"),
 }
 
 

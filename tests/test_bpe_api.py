@@ -20,7 +20,7 @@ def _bpe(meta, corpus):
     (dict(rmsd_partition_min_size=4), NotImplementedError),
     (dict(glue_opt=True), NotImplementedError),
     (dict(std_bonds=False), NotImplementedError),
-    (dict(bin_strategy="uniform"), NotImplementedError),
+    (dict(bin_strategy="quantile"), NotImplementedError),
     (dict(bins={1: 5, 10: 3}), NotImplementedError),
     (dict(bins={2: 5}), KeyError),
 ])

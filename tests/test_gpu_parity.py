@@ -33,7 +33,7 @@ def _check_against_golden(run, meta, arrs, thresholds=None):
 def test_engine_matches_reference_golden(name, mode):
     meta, corpus, arrs = load_golden(name)
     B = meta["bins"]["1"]
-    eng = _engine(corpus, B, cover=meta.get("bin_strategy") == "histogram-cover")
+    eng = _engine(corpus, B, strategy=meta.get("bin_strategy"))
     assert eng.K0 == meta["K0"]
     eng.bin()
     if mode == "step":

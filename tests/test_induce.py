@@ -20,7 +20,8 @@ def test_vocabulary_decodes_reference_tokens(name, oracle_lib):
     B = meta["bins"]["1"]
     thr = {k: [tuple(p) for p in v] for k, v in meta["thresholds"].items()}
     sol, K0, contents = induce.vocabulary(induce.tokens_from_json(meta["vocab"]), thr, B)
-    o = oracle_lib.OracleBPE(corpus, B, cover=meta.get("bin_strategy") == "histogram-cover").initialize()
+    o = oracle_lib.OracleBPE(corpus, B, cover=meta.get("bin_strategy") == "histogram-cover",
+                             strategy=meta.get("bin_strategy")).initialize()
     assert K0 == meta["K0"] and np.array_equal(sol, o.sym_of_label)
     assert induce.merge_keys_of(contents, K0, B) == [k for k, _ in meta["merges"]]
     rec = induce.replay_records(contents, K0)

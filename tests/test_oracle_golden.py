@@ -13,7 +13,7 @@ def test_oracle_matches_reference(name, oracle_lib):
     meta, corpus, arrs = load_golden(name)
     B = meta["bins"]["1"]
     cover = meta.get("bin_strategy", "histogram") == "histogram-cover"
-    o = oracle_lib.OracleBPE(corpus, B, cover=cover).initialize()
+    o = oracle_lib.OracleBPE(corpus, B, cover=cover, strategy=meta.get("bin_strategy")).initialize()
     # thresholds (bpe.py:820-876) and first-appearance labels (bpe.py:231-261)
     assert o.thresholds == {k: [tuple(p) for p in v] for k, v in meta["thresholds"].items()}
     assert np.array_equal(o.labels, arrs["init_labels"])

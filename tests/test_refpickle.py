@@ -26,7 +26,8 @@ def _digest(name):
 def oracle_run(oracle_lib, name, merges):
     meta, corpus, _ = load_golden(name)
     B = meta["bins"]["1"]
-    o = oracle_lib.OracleBPE(corpus, B, cover=meta.get("bin_strategy") == "histogram-cover").initialize()
+    o = oracle_lib.OracleBPE(corpus, B, cover=meta.get("bin_strategy") == "histogram-cover",
+                             strategy=meta.get("bin_strategy")).initialize()
     o.bin()
     for _ in range(merges):
         assert o.step() is not None
