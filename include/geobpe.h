@@ -165,6 +165,19 @@ int64_t geobpe_debug_timeline(geobpe_ctx *ctx, int on, int64_t *h_out, int64_t c
 /* Restrict the timing to a comma-separated list of kernel names ("" = all). */
 int geobpe_set_profiling_filter(geobpe_ctx *ctx, const char *names);
 double geobpe_kernel_ms(geobpe_ctx *ctx, const char *name, int64_t *launches);
+/* ---- PDB -> internal coordinates (the reference's
+ * canonical_distances_and_dihedrals, foldingdiff/angles_and_coords.py:69-154) ----
+ * geobpe_pdb_backbone: N, CA, C (x, y, z) of every amino-acid residue of the
+ * first model, 9 doubles per residue; returns the residues (h_xyz NULL: count
+ * only) or -GEOBPE_E* (-GEOBPE_EVALUE: a residue lacks a backbone atom, the
+ * reference's BadStructureError); geobpe_pdb_error() has the message.
+ * geobpe_featurize: on the device, the nine columns (GEOBPE_COL_* order, R values
+ * each) of chains given by row_off[n_rows+1] over the residues of h_xyz. */
+int64_t geobpe_pdb_backbone(const char *path, double *h_xyz, int64_t cap_residues);
+const char *geobpe_pdb_error(void);
+int geobpe_featurize(int device, int64_t n_rows, const int64_t *h_row_off, const double *h_xyz,
+                     double *const *h_cols);
+
 /* ---- merge replay (bin/induce.py: encode new chains with a trained vocabulary;
  * SURVEY.md §8(f) row 1) ----
  * After bin() and before any merge: merge t of geobpe_run / geobpe_step becomes

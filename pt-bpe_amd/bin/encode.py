@@ -3,9 +3,10 @@
 mirroring the reference's ``bin/encode.py`` (flags :106-167, loop :371-427).
 
 Differences (all outside SURVEY.md §8's hot path):
-  * ``--data-dir`` takes an internal-coordinate corpus (``.npz`` in the
-    geobpe.synth layout) or ``synthetic:N:LO:HI:SEED``; PDB featurisation is
-    §8(f) row 2.
+  * ``--data-dir`` takes a directory of PDB files (geobpe.pdb: C++ backbone
+    reader + HIP featurisation, the dataset's filters and shuffle), an
+    internal-coordinate corpus (``.npz`` in the geobpe.synth layout) or
+    ``synthetic:N:LO:HI:SEED``.
   * stats JSON carries K, L, bpr and the codebook utility (encode.py:408-420);
     bb_rmsd / lddt need the coordinate stack (esm ProteinChain) and are omitted.
   * checkpoints are ``bpe_iter={t}.pkl`` in the reference's pickle format
@@ -69,7 +70,7 @@ def parse_args(argv=None):
     p.add_argument("--save-dir", type=str)
     p.add_argument("--log-dir", type=str, default="logs")
     p.add_argument("--data-dir", type=str, default="synthetic:1000:40:300:0",
-                   help="corpus .npz (geobpe.synth layout) or synthetic:N:LO:HI:SEED")
+                   help="a directory of PDB files, a corpus .npz (geobpe.synth layout) or synthetic:N:LO:HI:SEED")
     p.add_argument("--toy", type=int, default=0, help="number of chains; 0 for all")
     p.add_argument("--res-init", type=str2bool, default=True)
     p.add_argument("--free-bonds", type=str2bool, default=False)
@@ -91,6 +92,11 @@ def load_corpus(spec: str, toy: int = 0) -> dict:
     if spec.startswith("synthetic:"):
         n, lo, hi, seed = (int(x) for x in spec.split(":")[1:5])
         corpus = synth.make_corpus(synth.make_lengths(n, lo, hi, seed=seed), seed=seed)
+    elif os.path.isdir(spec):  # a directory of PDB files (scripts/encode.sh, config 1)
+        from geobpe import pdb
+        corpus, fnames = pdb.load_pdb_dir(spec, toy=toy)
+        corpus["fnames"] = fnames
+        return corpus
     else:
         corpus = synth.load_corpus(spec)
     if toy:

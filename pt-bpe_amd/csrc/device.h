@@ -26,6 +26,12 @@ constexpr int SKIP_HOT = 1, SKIP_POST = 2, SKIP_MEASURE = 4;  // what a rebuild 
 constexpr int DBG_SLOTS = 64;
 constexpr int PW_LDS = 2048;    // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
 constexpr int KL_CHUNK = 4096;  // klist entries an apply workgroup reserves at a time
+#ifndef POST_SPAN_DEF
+#define POST_SPAN_DEF 64
+#endif
+// the posting index is rebuilt only when the winner's count is small enough that
+// the log lasts >= POST_SPAN / 2 merges (2 new pairs per occurrence)
+constexpr int POST_SPAN = POST_SPAN_DEF;
 
 // ------------------------------------------------------------------ records
 // Kernel-to-kernel state.  No field is written by a kernel that other

@@ -27,6 +27,7 @@
 #include "device.h"
 #include "keyjson.h"
 #include "kernels.h"
+#include "featurize.h"
 
 using namespace gb;
 
@@ -1082,6 +1083,60 @@ int geobpe_replay_load(geobpe_ctx* c, const uint64_t* h_h1, const uint64_t* h_h2
     HIPCHK(c, hipMemcpyAsync(c->replay, r.data(), (size_t)n * sizeof(ReplayRec), hipMemcpyHostToDevice, c->stream));
   c->replay_n = n;
   return 0;
+}
+
+// ---- PDB -> internal coordinates (featurize.h)
+static thread_local std::string g_pdb_err;
+
+const char* geobpe_pdb_error(void) { return g_pdb_err.c_str(); }
+
+int64_t geobpe_pdb_backbone(const char* path, double* h_xyz, int64_t cap_residues) {
+  if (!path) return GEOBPE_EARG;
+  std::vector<double> xyz;
+  g_pdb_err.clear();
+  const int n = pdb_backbone(path, xyz, g_pdb_err);
+  if (n < 0) return n == -2 ? -(int64_t)GEOBPE_EVALUE : -(int64_t)GEOBPE_EARG;
+  if (h_xyz) {
+    if (n > cap_residues) {
+      g_pdb_err = "buffer too small";
+      return -(int64_t)GEOBPE_ECAPACITY;
+    }
+    std::memcpy(h_xyz, xyz.data(), xyz.size() * sizeof(double));
+  }
+  return n;
+}
+
+int geobpe_featurize(int device, int64_t n_rows, const int64_t* h_row_off, const double* h_xyz,
+                     double* const* h_cols) {
+  if (n_rows < 0 || !h_row_off || !h_cols) return GEOBPE_EARG;
+  const int64_t R = h_row_off[n_rows];
+  if (R == 0) return 0;
+  if (!h_xyz) return GEOBPE_EARG;
+  if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GEOBPE_EHIP;
+  int64_t* d_off = nullptr;
+  double *d_xyz = nullptr, *d_out = nullptr;
+  int rc = 0;
+  if (hipMalloc(&d_off, (n_rows + 1) * 8) != hipSuccess || hipMalloc(&d_xyz, R * 9 * 8) != hipSuccess ||
+      hipMalloc(&d_out, R * 9 * 8) != hipSuccess) {
+    rc = GEOBPE_EHIP;
+  } else {
+    hipMemcpyAsync(d_off, h_row_off, (n_rows + 1) * 8, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_xyz, h_xyz, R * 9 * 8, hipMemcpyHostToDevice, s);
+    const int nb = (int)std::min<int64_t>(std::max<int64_t>(n_rows, 1), 65536);
+    hipLaunchKernelGGL(k_featurize, dim3(nb), dim3(BLOCK), 0, s, n_rows, (const int64_t*)d_off,
+                       (const double*)d_xyz, d_out, R);
+    if (hipGetLastError() != hipSuccess) rc = GEOBPE_EHIP;
+    for (int col = 0; col < 9 && !rc; col++)
+      if (hipMemcpyAsync(h_cols[col], d_out + col * R, R * 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = GEOBPE_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess) rc = GEOBPE_EHIP;
+  }
+  hipFree(d_off);
+  hipFree(d_xyz);
+  hipFree(d_out);
+  hipStreamDestroy(s);
+  return rc;
 }
 
 int geobpe_set_record_events(geobpe_ctx* c, int on) {

@@ -607,7 +607,7 @@ __device__ int32_t mark_select(const Dev& D, int par, int32_t* W_out) {
   // posting index stale (log full / overflowed / never built) and the merges are
   // small enough that a rebuild lasts >= 64 iterations: rebuild it this iteration
   const bool post = !hot && (st->post_valid == 0 || st->plog_ovf != 0 || st->plog_total > D.LOGMAX) &&
-                    (int64_t)gm * 64 <= D.LOGMAX;
+                    (int64_t)gm * POST_SPAN <= D.LOGMAX;
   if (hot || post) {
     if (rec) {
       out->decision = SEL_SKIP;
@@ -803,7 +803,7 @@ __global__ __launch_bounds__(64) void k_select_replay(Dev D, int par, const Repl
   const int32_t c = W >= 0 ? D.count[W] : 0;
   if (c <= 0) W = -1;
   const bool post = c > 0 && (st->post_valid == 0 || st->plog_ovf != 0 || st->plog_total > D.LOGMAX) &&
-                    (int64_t)c * 64 <= D.LOGMAX;
+                    (int64_t)c * POST_SPAN <= D.LOGMAX;
   if (post) {
     out->decision = SEL_SKIP;
     out->skip = SKIP_POST;

@@ -170,7 +170,7 @@ class BPE:
         _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_size, glue_opt, compute_sec_structs)
         if isinstance(structures, dict) and "row_off" in structures:
             corpus = structures
-            self._fnames = None
+            self._fnames = list(structures["fnames"]) if structures.get("fnames") is not None else None
         else:
             structures = list(structures)
             corpus = structures_to_corpus(structures)

@@ -29,6 +29,7 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, "pt-bpe_amd"))
+sys.path.insert(0, HERE)
 
 # name: (n_seqs, len_lo, len_hi, bins, merges, seed, repeat_frac)
 FIXTURES = {
@@ -41,6 +42,9 @@ FIXTURES = {
     "g80x40-160_b7_rep": (80, 40, 160, 7, 100, 6, 0.1),
     "g50x30-110_b6_cover": (50, 30, 110, 6, 80, 7, 0.1, "histogram-cover"),
     "g50x30-110_b5_uniform": (50, 30, 110, 5, 80, 8, 0.1, "uniform"),
+    # config 1 shape: the bundled PDB subset (tests/golden/pdb, from the reference's
+    # data/vqvae_pretrain/train) featurised by pdb_angles.py, 5 bins, 50 merges
+    "c1_pdb12_b5": ("pdb", None, None, 5, 50, 0, 0.0),
 }
 
 
@@ -78,8 +82,13 @@ def run_one(name: str) -> None:
 
     n_seqs, lo, hi, bins, merges, seed, rep = FIXTURES[name][:7]
     strategy = FIXTURES[name][7] if len(FIXTURES[name]) > 7 else "histogram"
-    lengths = synth.make_lengths(n_seqs, lo, hi, seed=seed)
-    corpus = synth.make_corpus(lengths, seed=seed, repeat_frac=rep)
+    if n_seqs == "pdb":
+        import pdb_angles
+        corpus, _ = pdb_angles.pdb_dir_corpus(os.path.join(HERE, "pdb"))
+        n_seqs = len(corpus["row_off"]) - 1
+    else:
+        lengths = synth.make_lengths(n_seqs, lo, hi, seed=seed)
+        corpus = synth.make_corpus(lengths, seed=seed, repeat_frac=rep)
 
     _stub_optional_deps()
     sys.path.insert(0, "/root/reference")
