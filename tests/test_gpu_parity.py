@@ -255,3 +255,22 @@ def test_merge_events_match_oracle(oracle_lib):
         oo = np.argsort(oa[s], kind="stable")
         assert np.array_equal(a[s], oa[s][oo]) and np.array_equal(b[s], ob[s][oo])
     eng.close()
+
+
+@pytest.mark.parametrize("cfg", [
+    dict(lengths=[5000, 3000, 4500], B=3, merges=400, seed=101, rep=0.3),   # long chains: hash powers past LDS
+    dict(lengths=[1] * 50 + [2] * 50 + [3], B=2, merges=100, seed=102, rep=0.0),  # tiny chains
+    dict(lengths=[700] * 40, B=12, merges=150, seed=103, rep=0.5),          # long repeats, two-digit bins
+])
+def test_edge_shapes_match_oracle(cfg, oracle_lib):
+    from geobpe import synth
+    corpus = synth.make_corpus(np.array(cfg["lengths"], dtype=np.int64), seed=cfg["seed"], repeat_frac=cfg["rep"])
+    o = _oracle_run(oracle_lib, corpus, cfg["B"], cfg["merges"])
+    eng = _engine(corpus, cfg["B"])
+    eng.bin()
+    eng.run(cfg["merges"])
+    assert eng.merge_keys() == o.merges
+    assert eng.verify_counts() == 0
+    for x, y in zip(eng.encode(), o.encode()):
+        assert np.array_equal(x, y)
+    eng.close()
