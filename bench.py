@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-exchange", action="store_true",
+                    help="run the multi-rank exchange (RCCL) even at world size 1: a 1-GPU rehearsal of the N>1 path")
     ap.add_argument("--cpu-budget-s", type=float, default=30.0)
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
@@ -68,6 +70,8 @@ def parse():
 
 def main():
     args = parse()
+    if args.force_exchange:  # rehearsal of the exchange only: no tables that need per-merge counts
+        args.no_profile = args.no_replay = args.no_cpu_baseline = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -78,8 +82,13 @@ def main():
     from geobpe.engine import GeoBPEEngine
 
     torch.cuda.set_device(local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if world > 1 or args.force_exchange:
+        if args.force_exchange and world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     n, lo, hi, B, merges = CONFIGS[args.config]
     t0 = time.time()
     lengths = synth.make_lengths(n, lo, hi, seed=0)
@@ -88,10 +97,11 @@ def main():
     t_gen = time.time() - t0
     shard = corpus
     group = None
-    if world > 1:
+    if world > 1 or args.force_exchange:
         lo_r, hi_r = shard_rows(corpus["row_off"], world)[rank]
         shard = slice_corpus(corpus, lo_r, hi_r)
         group = TorchGroup(int(shard["row_off"][-1]), device=local)
+        group.force = args.force_exchange
     eng = GeoBPEEngine(shard, B, device=local, group=group, max_vocab=1 << 20)
     torch.cuda.synchronize()
     t0 = time.time()
@@ -221,6 +231,7 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
+    if world > 1 or args.force_exchange:
         dist.destroy_process_group()
 
 

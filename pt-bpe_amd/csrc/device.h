@@ -303,18 +303,33 @@ __device__ inline uint32_t post_bkt(int32_t d) { return ((uint32_t)d * 265443576
 
 __device__ inline uint16_t key_fp(int32_t d) { return (uint16_t)((uint32_t)d % 65535u); }
 
-// count update target: global counts, or the rank-local delta + touched list
+// a key whose rank-local delta left 0 joins the touched list: one reservation per
+// wave instruction (the lanes calling this are exactly the active ones)
+__device__ inline void touched_append(const Dev& D, int32_t d) {
+  const u64 m = __ballot(1);
+  const int lane = wave_lane();
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd((unsigned long long*)&D.st->ntouched, (unsigned long long)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const unsigned long long j = base + __popcll(m & ((1ULL << lane) - 1));
+  if ((int64_t)j < D.KCAP)
+    D.touched[j] = d;
+  else
+    set_error(D, GEOBPE_ECAPACITY, -31);
+}
+
+// count update target: global counts, or the rank-local delta + touched list.
+// A key joins the touched list when its delta leaves 0 (the add that returns 0);
+// a key whose delta came back to 0 and left again is listed twice -- the export
+// takes each delta with an exchange, so the later copy carries 0 and the import
+// skips it.  No per-key epoch table, no returning exchange on a second array.
 __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_delta) {
   if (!to_delta) {
     atomicAdd(&D.count[d], v);
     return;
   }
-  atomicAdd(&D.dcount[d], v);
-  const int32_t ep = (int32_t)D.st->epoch;
-  if (atomicExch(&D.touch[d], ep) != ep) {
-    const int64_t j = atomicAdd((unsigned long long*)&D.st->ntouched, 1ULL);
-    D.touched[j] = d;
-  }
+  if (atomicAdd(&D.dcount[d], v) == 0) touched_append(D, d);
 }
 
 // LDS-staged per-workgroup partial counts, flushed with one global atomic per
@@ -424,13 +439,50 @@ __device__ inline void agg_add_hot(A& s, const Dev& D, HotApp& h, int32_t d, int
 template <class A>
 __device__ inline void agg_flush_hot(A& s, const Dev& D, HotApp& h, bool to_delta, int32_t th) {
   __syncthreads();
-  for (int i = threadIdx.x; i < A::N; i += blockDim.x) {
-    const int32_t k = s.key[i];
-    if (k < 0 || s.val[i] == 0) continue;
-    if (to_delta)
-      global_add(D, k, s.val[i], true);
-    else
+  if (to_delta) {
+    // all of a thread's returning adds in flight together; the keys whose delta
+    // left 0 join the touched list with ONE reservation per workgroup (a single
+    // global counter serialises at the memory side: one add per wave cost ~70 us)
+    constexpr int U = A::N / 1024 > 0 ? A::N / 1024 : 1;  // slots per thread at 1024 threads
+    __shared__ int32_t s_red_t[32];
+    __shared__ unsigned long long s_base_t;
+    int32_t k[U];
+    int32_t nt = 0;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int i = threadIdx.x + u * (int)blockDim.x;
+      k[u] = i < A::N ? s.key[i] : -1;
+      const int32_t v = k[u] >= 0 ? s.val[i] : 0;
+      if (v == 0) k[u] = -1;
+      const int32_t old = k[u] >= 0 ? atomicAdd(&D.dcount[k[u]], v) : 1;
+      if (old != 0) k[u] = -1;
+      nt += k[u] >= 0;
+    }
+    for (int i = threadIdx.x + U * (int)blockDim.x; i < A::N; i += blockDim.x) {  // blockDim < 1024
+      const int32_t kk = s.key[i];
+      if (kk >= 0 && s.val[i] != 0) global_add(D, kk, s.val[i], true);
+    }
+    int32_t tot;
+    const int32_t ex = block_excl_scan(nt, &tot, s_red_t);
+    if (threadIdx.x == 0)
+      s_base_t = tot ? atomicAdd((unsigned long long*)&D.st->ntouched, (unsigned long long)tot) : 0ULL;
+    __syncthreads();
+    int64_t j = (int64_t)s_base_t + ex;
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      if (k[u] < 0) continue;
+      if (j < D.KCAP)
+        D.touched[j] = k[u];
+      else
+        set_error(D, GEOBPE_ECAPACITY, -31);
+      j++;
+    }
+  } else {
+    for (int i = threadIdx.x; i < A::N; i += blockDim.x) {
+      const int32_t k = s.key[i];
+      if (k < 0 || s.val[i] == 0) continue;
       count_add_hot(D, h, k, s.val[i], th);
+    }
   }
   hot_flush(D, h);
 }

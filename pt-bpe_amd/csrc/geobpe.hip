@@ -47,6 +47,7 @@ struct geobpe_ctx {
   Dev D{};
   std::vector<void*> allocs;
   State* h_state = nullptr;  // pinned mirror
+  Sel* h_sel = nullptr;      // pinned copy of the last decision (step_select)
   bool keys_ready = false;
   bool distributed = false;
   bool bin_dense = true;
@@ -229,7 +230,7 @@ int alloc_keys(geobpe_ctx* c) {
       (rc = dalloc(c, &D.klist, D.KCAP, 0xFF)) || (rc = dalloc(c, &D.kchunk, 2 * (int64_t)c->nba, 0)))
     return rc;
   if (c->distributed) {
-    if ((rc = dalloc(c, &D.dcount, D.HC, 0)) || (rc = dalloc(c, &D.touch, D.HC, 0xFF)) ||
+    if ((rc = dalloc(c, &D.dcount, D.HC, 0)) ||
         (rc = dalloc(c, &D.touched, D.KCAP)))
       return rc;
   }
@@ -283,6 +284,16 @@ int read_sel(geobpe_ctx* c, Sel* out) {
   return 0;
 }
 
+// the state and the decision of the last select in one wait: two async copies
+// into pinned memory, one stream synchronisation
+int sync_state_sel(geobpe_ctx* c, Sel* out) {
+  HIPCHK(c, hipMemcpyAsync(c->h_state, c->D.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->h_sel, c->D.sel + (c->gen & 1), sizeof(Sel), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *out = *c->h_sel;
+  return check_device_error(c);
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------- C ABI
@@ -302,6 +313,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
     c->own_stream = true;
   }
   HIPCHK(c, hipHostMalloc((void**)&c->h_state, sizeof(State), hipHostMallocDefault));
+  HIPCHK(c, hipHostMalloc((void**)&c->h_sel, sizeof(Sel), hipHostMallocDefault));
   memset(c->h_state, 0, sizeof(State));
   int rc;
   if ((rc = dalloc(c, &c->D.st, 1, 0)) || (rc = dalloc(c, &c->D.sel, 2, 0))) return rc;
@@ -326,6 +338,7 @@ void geobpe_destroy(geobpe_ctx* c) {
   for (int i = 0; i < 9; i++)
     if (c->d_cols[i]) hipFree(c->d_cols[i]);
   if (c->h_state) hipHostFree(c->h_state);
+  if (c->h_sel) hipHostFree(c->h_sel);
   for (auto e : c->evall) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
@@ -663,7 +676,7 @@ int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {
   for (;;) {
     enqueue_select(c);
     HIPCHK(c, hipGetLastError());
-    if ((rc = sync_state(c)) || (rc = read_sel(c, &sel))) return rc;
+    if ((rc = sync_state_sel(c, &sel))) return rc;
     if (sel.decision == SEL_MERGE) break;
     enqueue_apply(c);  // a rebuild iteration (rank-local: every rank then selects the same winner) or done
     if (sel.decision == SEL_DONE) {

@@ -1452,9 +1452,8 @@ __global__ __launch_bounds__(BLOCK) void k_export(Dev D, DeltaRec* out, int64_t 
     r.idL = D.krep[3 * d];
     r.g = D.krep[3 * d + 1];
     r.idR = D.krep[3 * d + 2];
-    r.delta = D.dcount[d];
+    r.delta = atomicExch(&D.dcount[d], 0);  // a key listed twice: the later copy carries 0
     r.pad = 0;
-    D.dcount[d] = 0;
     out[j] = r;
   }
 }
@@ -1472,9 +1471,8 @@ __global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int6
     r.idL = D.krep[3 * d];
     r.g = D.krep[3 * d + 1];
     r.idR = D.krep[3 * d + 2];
-    r.delta = D.dcount[d];
+    r.delta = atomicExch(&D.dcount[d], 0);  // a key listed twice: the later copy carries 0
     r.pad = 0;
-    D.dcount[d] = 0;
     out[j] = r;
   }
 }

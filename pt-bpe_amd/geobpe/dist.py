@@ -141,9 +141,9 @@ class TorchGroup:
             self._cnt = T.zeros(1, dtype=T.int64, device=self.dev)
         engine._chk(engine.L.geobpe_delta_export_async(engine._ctx, ptr, cap, ctypes.c_void_p(self._cnt.data_ptr())))
         src = self._cnt if self.on_gpu else self._cnt.cpu()
-        outs = [T.zeros_like(src) for _ in range(self.world_size)]
-        self.dist.all_gather(outs, src, group=self.pg)
-        counts = [int(x) for x in T.cat(outs).cpu().tolist()]
+        allc = T.empty(self.world_size, dtype=T.int64, device=src.device)
+        self.dist.all_gather_into_tensor(allc, src, group=self.pg)
+        counts = [int(x) for x in allc.cpu().tolist()]  # the merge's one host wait on the exchange
         if max(counts) > cap:
             raise _native.GeoBPEError(f"delta export needs {max(counts)} records (cap {cap})")
         m = max(counts)

@@ -99,7 +99,7 @@ class GeoBPEEngine:
         self.n_rows = len(self.row_off) - 1
         self._cols = [np.ascontiguousarray(corpus[c], dtype=np.float64) for c in COLUMNS]
         self.torch_stream = None
-        if stream is None and group is not None and getattr(group, "world_size", 1) > 1:
+        if stream is None and group is not None and (getattr(group, "world_size", 1) > 1 or getattr(group, "force", False)):
             # multi-rank: the engine's kernels and the exchange's torch ops (copies,
             # collectives) must be ordered on ONE stream -- a torch stream of our own
             import torch
@@ -126,7 +126,7 @@ class GeoBPEEngine:
 
     @property
     def distributed(self) -> bool:
-        return self.group is not None and self.group.world_size > 1
+        return self.group is not None and (self.group.world_size > 1 or getattr(self.group, "force", False))
 
     def close(self):
         if self._ctx:
