@@ -32,6 +32,10 @@ CONFIGS = {
     # name: (n_chains, len_lo, len_hi, bins, merges)
     "c3": (100_000, 40, 560, 5, 1000),  # BASELINE configs[2]
     "c2": (10_000, 256, None, 5, 500),  # BASELINE configs[1]
+    # BASELINE configs[4] as SURVEY §8(d) allows it: the C3 corpus, bins {1: 5}, 5000
+    # merges (the multi-grid schedule cannot run in the reference's scoped mode);
+    # run with --steps 4990
+    "c5": (100_000, 40, 560, 5, 5000),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 APPLY_BYTES_PER_MERGE = 156  # algorithmic bytes of one merged occurrence in k_apply
@@ -217,9 +221,11 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic",
-        "config": {"workload": f"BASELINE configs[2]: {n} synthetic chains, len U{{{lo}..{hi}}}, "
-                               f"{R_total} residues, bins {{1: {B}}}, merges {args.warmup + 1}..{args.warmup + done}"
-                   if args.config == "c3" else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
+        "config": {"workload": (f"BASELINE configs[{ {'c3': 2, 'c5': 4}[args.config]}]"
+                                + (" (bins {1: 5} form, SURVEY 8(d))" if args.config == "c5" else "")
+                                + f": {n} synthetic chains, len U{{{lo}..{hi}}}, {R_total} residues, "
+                                f"bins {{1: {B}}}, merges {args.warmup + 1}..{args.warmup + done}")
+                   if args.config in ("c3", "c5") else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
                    "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}"},
         "roofline": roofline,
         "cpu_baseline": cpu,

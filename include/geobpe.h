@@ -136,6 +136,10 @@ int geobpe_debug_key_less(geobpe_ctx *ctx, const int32_t *h_pairs, int32_t n, in
  * chunk entry) and its global pair count; returns the number of entries,
  * copies at most cap of each. */
 int64_t geobpe_debug_counts(geobpe_ctx *ctx, int32_t *h_keys, int32_t *h_counts, int64_t cap);
+/* debug: argmax state after a sync -- {hot-list length, theta, tied keys of the last
+   merge, its count, rebuild iterations, list valid, merges, vocab, posting index valid,
+   posting log length}; returns 10 (cap >= 10) */
+int64_t geobpe_debug_state(geobpe_ctx *ctx, int64_t *h_out, int64_t cap);
 /* Debug record of key d: idL, g, idR, len, count, U, K(device), K(host), h1. */
 int geobpe_debug_key(geobpe_ctx *ctx, int32_t d, int64_t *h_out9);
 /* Content (residue / junction symbols, 2*nres-1 values) of vocab id v. */

@@ -5,7 +5,8 @@
 // bin / step / quantize).  Integer work only (no
 // MFMA).  One merge iteration is three stream-ordered launches with no host
 // synchronisation:
-//   k_select  one workgroup: hot-list argmax + reference key-string tie-break,
+//   k_select  one 1024-thread workgroup: hot-list argmax + reference key-string
+//             tie-break (wave-parallel comparisons on LDS copies of the tied keys),
 //             the decision record (Sel) and merge-log entry
 //   k_mark    the winner's occurrences (posting index or fingerprint scan) and
 //             greedy run walks
@@ -255,7 +256,7 @@ void enqueue_select(geobpe_ctx* c) {
     hipLaunchKernelGGL(k_select_replay, dim3(1), dim3(64), 0, c->stream, c->D, (int)(c->gen & 1),
                        (const ReplayRec*)c->replay, c->replay_n);
   else
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SBLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
 }
 void enqueue_mark(geobpe_ctx* c) {
   Timed t(c, "mark");
@@ -877,6 +878,16 @@ static int row_token_offsets(geobpe_ctx* c, std::vector<int64_t>& off, int64_t**
   return 0;
 }
 
+int64_t geobpe_debug_state(geobpe_ctx* c, int64_t* h_out, int64_t cap) {
+  if (!c || !h_out || cap < 10) return GEOBPE_EARG;
+  if (int rc = sync_state(c)) return rc;
+  const State& s = *c->h_state;
+  const int64_t v[10] = {s.ncl2[s.cl_act], s.theta, s.ncand, s.maxc, s.nskip, s.cl_valid,
+                         s.iter, s.K, s.post_valid, s.plog_total};
+  for (int i = 0; i < 10; i++) h_out[i] = v[i];
+  return 10;
+}
+
 int64_t geobpe_num_tokens(geobpe_ctx* c) {
   if (!c || !c->R) return -1;
   std::vector<int64_t> off;
@@ -971,7 +982,7 @@ int geobpe_debug_key_less(geobpe_ctx* c, const int32_t* h_pairs, int32_t n, int3
   HIPCHK(c, hipMalloc(&dp, 8 * (size_t)n + 8));
   HIPCHK(c, hipMalloc(&dout, 4 * (size_t)n + 4));
   HIPCHK(c, hipMemcpyAsync(dp, h_pairs, 8 * (size_t)n, hipMemcpyHostToDevice, c->stream));
-  hipLaunchKernelGGL(k_debug_key_less, dim3((n + 255) / 256 + 1), dim3(256), 0, c->stream, c->D, (const int32_t*)dp,
+  hipLaunchKernelGGL(k_debug_key_less, dim3((64 * (int64_t)n + 255) / 256 + 1), dim3(256), 0, c->stream, c->D, (const int32_t*)dp,
                      dout, n);
   HIPCHK(c, hipMemcpyAsync(h_out, dout, 4 * (size_t)n, hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));

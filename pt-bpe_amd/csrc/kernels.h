@@ -524,63 +524,221 @@ __device__ inline bool key_less(const Dev& D, int32_t a, int32_t b, char* lds) {
   }
 }
 
-// BPE.step's argmax (bpe.py:1796-1800, SortedDict peekitem(0)), by one
-// workgroup (k_select): every key with
+// The same order, compared item by item by a whole wave (the char generator
+// above costs ~100 instructions per character on one lane: 30-250 us for the
+// long tied keys of late merges).  The key string is nine lists
+// '{"0C:1N": [I0], "C:1N:1CA": [I1], ... "tau": [I8]}' with Is = ", ".join(str(v)).
+// Two strings first differ inside the first list s that differs, at its first
+// differing item i:
+//   * one list ended at i: its ']' sorts after the other's ',' or digit -> it is larger;
+//   * items x != y: decimal strings compared char-wise; when one is a prefix of
+//     the other the shorter one's terminator decides (',' < digit < ']').
+struct KSeq {  // content(L) ++ [g] ++ content(R)
+  const int32_t *A, *C;
+  int32_t nA, g, nC;
+};
+__device__ inline int32_t kseq_sym(const KSeq& q, int32_t k) {
+  const int32_t* p = k < q.nA ? q.A + k : q.C + max(k - q.nA - 1, 0);
+  const int32_t v = *p;
+  return k == q.nA ? q.g : v;
+}
+__device__ inline int32_t ksec_len(int s, int32_t r, int32_t lam) {
+  switch (s) {
+    case 0: case 3: case 7: return r - lam;
+    case 1: case 5: case 6: return r - 1;
+    default: return r;
+  }
+}
+__device__ inline int32_t ksec_val(const KSeq& q, int s, int32_t i, int32_t B, int32_t B2, int32_t B3) {
+  switch (s) {
+    case 1: return kseq_sym(q, 2 * i + 1) / B % B;  // C:1N:1CA
+    case 3: return kseq_sym(q, 2 * i) / B % B;      // CA:C:1N
+    case 5: return kseq_sym(q, 2 * i + 1) / B2;     // omega
+    case 6: return kseq_sym(q, 2 * i + 1) % B;      // phi
+    case 7: return kseq_sym(q, 2 * i) % B;          // psi
+    case 8: {                                       // tau
+      const int32_t x = kseq_sym(q, 2 * i);
+      return x >= B3 ? x - B3 : x / B2;
+    }
+    default: return 0;  // bond lists (std_bonds)
+  }
+}
+__device__ inline int ndigits(int32_t v) {
+  int n = 1;
+  for (; v >= 10; v /= 10) n++;
+  return n;
+}
+// str(x) + (']' if xlast else ',') < str(y) + (']' if ylast else ',') for x != y
+__device__ inline bool item_less(int32_t x, bool xlast, int32_t y, bool ylast) {
+  const int dx = ndigits(x), dy = ndigits(y);
+  if (dx == dy) return x < y;
+  if (dx < dy) {
+    int32_t yp = y;
+    for (int k = dx; k < dy; k++) yp /= 10;
+    return yp != x ? x < yp : !xlast;  // x a prefix of y: x's terminator against a digit
+  }
+  int32_t xp = x;
+  for (int k = dy; k < dx; k++) xp /= 10;
+  return xp != y ? xp < y : ylast;
+}
+// key string of a < key string of b; every lane of the wave calls it with the
+// same arguments and gets the same answer
+__device__ inline bool wave_key_less(const KSeq& a, const KSeq& b, int32_t B) {
+  const int32_t B2 = B * B, B3 = B2 * B;
+  const int lane = (int)(threadIdx.x & 63);
+  const int32_t na = a.nA + 1 + a.nC, nb = b.nA + 1 + b.nC;
+  const int32_t ra = (na + 1) / 2, rb = (nb + 1) / 2;
+  const int32_t lama = kseq_sym(a, na - 1) >= B3 ? 1 : 0, lamb = kseq_sym(b, nb - 1) >= B3 ? 1 : 0;
+  for (int s = 0; s < 9; s++) {
+    const int32_t la = ksec_len(s, ra, lama), lb = ksec_len(s, rb, lamb);
+    if (s == 0 || s == 2 || s == 4) {  // lists of zeros: the shorter one is larger
+      if (la != lb) return la > lb;
+      continue;
+    }
+    const int32_t m = max(la, lb);
+    for (int32_t i0 = 0; i0 < m; i0 += 64) {
+      const int32_t i = i0 + lane;
+      const bool ia = i < la, ib = i < lb;
+      int32_t va = 0, vb = 0;
+      bool diff = false;
+      if (ia && ib) {
+        va = ksec_val(a, s, i, B, B2, B3);
+        vb = ksec_val(b, s, i, B, B2, B3);
+        diff = va != vb;
+      } else {
+        diff = ia != ib;
+      }
+      const unsigned long long mask = __ballot(diff);
+      if (mask) {
+        const int first = __ffsll((long long)mask) - 1;
+        const int res = !ia ? 0 : (!ib ? 1 : (item_less(va, i == la - 1, vb, i == lb - 1) ? 1 : 0));
+        return __shfl(res, first, 64) != 0;
+      }
+    }
+  }
+  return false;
+}
+
+__device__ inline KSeq key_seq(const Dev& D, int32_t d) {
+  const int32_t L = D.krep[3 * (int64_t)d], g = D.krep[3 * (int64_t)d + 1], Rr = D.krep[3 * (int64_t)d + 2];
+  const int64_t a0 = D.voff[L], a1 = D.voff[L + 1], c0 = D.voff[Rr], c1 = D.voff[Rr + 1];
+  return KSeq{D.vsym + a0, D.vsym + c0, (int32_t)(a1 - a0), g, (int32_t)(c1 - c0)};
+}
+
+// BPE.step's argmax (bpe.py:1796-1800, SortedDict peekitem(0)): every key with
 // count >= theta is in clist[0..n), so when the list maximum m >= theta it is the
 // global maximum and every key tied at m is in the list.  Otherwise (or when the
-// list has grown long while m >= 4 theta) the launch pair is a rebuild
+// list has grown long while m >= 4 theta) the launch triple is a rebuild
 // iteration with theta_new = max(1, m/2) <= the true maximum; an invalid list
 // is first re-measured.  Ties: the smallest reference key string
-// (bpe.py:1469-1471) via the device JSON generator.  It records the decision
-// in Sel[par], the merge log entry and the new token's hash
-// (_tokens[n] = json.loads(key), bpe.py:1857-1860; its content is written by
-// k_apply's workgroup 0).
-__device__ int32_t mark_select(const Dev& D, int par, int32_t* W_out) {
-  __shared__ int32_t s_red[BLOCK / 64];
-  __shared__ int32_t s_best[BLOCK];
-  __shared__ char s_jbuf[48 * BLOCK];
+// (bpe.py:1469-1471) via the device JSON generator.
+//
+// k_select: one workgroup of SBLOCK threads (16 waves).  Every thread keeps 4
+// list entries in flight (one round covers 4096 entries: the lists of a C3/C5
+// run hold <= ~5 k), so the scan is one or two rounds of dependent list -> count
+// gathers.  The keys tied at the maximum are collected in LDS, their contents
+// staged in LDS, and a wave-per-comparison tournament (wave_key_less) picks the
+// smallest reference string.  It records the decision in Sel[par], the
+// merge-log entry and the new token's hash (_tokens[n] = json.loads(key),
+// bpe.py:1857-1860; its content is written by k_apply's workgroup 0).  More than
+// SEL_TMAX tied keys (runs to exhaustion) fall back to the char generator.
+// (Measured: the char-generator tie tree cost 30-250 us a merge for the 10-30 tied
+// long keys of late merges; a 64-workgroup scan with a last-arriver reduction
+// paid ~6 us of release/acquire fences and tickets for nothing at these lengths.)
+constexpr int SBLOCK = 1024;
+constexpr int SEL_TMAX = SBLOCK;  // staged candidates
+constexpr int SEL_SYMS = 6144;    // staged content symbols (24 KB)
+
+// block-wide smallest reference key string among the threads' candidates (-1 = none)
+__device__ inline int32_t block_min_key(const Dev& D, int32_t best, int32_t* s_best, char* jb) {
+  s_best[threadIdx.x] = best;
+  __syncthreads();
+  for (int o = blockDim.x / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) {
+      const int32_t a = s_best[threadIdx.x], b = s_best[threadIdx.x + o];
+      if (a < 0 || (b >= 0 && b != a && key_less(D, b, a, jb))) s_best[threadIdx.x] = b;
+    }
+    __syncthreads();
+  }
+  const int32_t r = s_best[0];
+  __syncthreads();
+  return r;
+}
+
+struct SelStage {  // the tied keys and LDS copies of their contents
+  int32_t key[SEL_TMAX];
+  int32_t off[SEL_TMAX];
+  int32_t idx[SEL_TMAX];
+  KSeq seq[SEL_TMAX];
+  int32_t sym[SEL_SYMS];
+  int32_t nt;
+};
+
+// tournament over the tied keys (indices 0..nt-1 into S.seq), one wave per
+// comparison; returns the index of the smallest key string
+__device__ inline int32_t wave_tournament(SelStage& S, int32_t nt, int32_t B) {
+  const int wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  if ((int)threadIdx.x < nt) S.idx[threadIdx.x] = threadIdx.x;
+  __syncthreads();
+  for (int32_t cnt = nt; cnt > 1;) {
+    const int32_t up = (cnt + 1) / 2;
+    for (int32_t p = wave; p < cnt - up; p += nw) {
+      const int32_t ia = S.idx[p], ib = S.idx[p + up];
+      const bool bl = S.key[ia] != S.key[ib] && wave_key_less(S.seq[ib], S.seq[ia], B);
+      if ((threadIdx.x & 63) == 0 && bl) S.idx[p] = ib;
+    }
+    __syncthreads();
+    cnt = up;
+  }
+  const int32_t r = S.idx[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
+  __shared__ int32_t s_red[SBLOCK / 64];
+  __shared__ SelStage S;
   State* st = D.st;
   Sel* out = D.sel + par;
-  const bool rec = blockIdx.x == 0 && threadIdx.x == 0;
+  const bool rec = threadIdx.x == 0;
   const int32_t act = st->cl_act;
-  // the first 4*BLOCK list entries are loaded with the state (clist has KCAP >=
-  // 4*BLOCK entries; entries past n are masked below)
+  // the first 4 * SBLOCK list entries are loaded with the state (clist capacity
+  // KCAP >= 4 * SBLOCK; entries past n are masked below)
   int32_t d0[4];
 #pragma unroll
-  for (int q = 0; q < 4; q++) d0[q] = D.clist[threadIdx.x + q * BLOCK];
+  for (int q = 0; q < 4; q++) d0[q] = D.clist[threadIdx.x + q * SBLOCK];
   const int64_t n = st->ncl2[act];
   const int32_t th = st->theta, iter = st->iter, K = st->K;
   const bool valid = st->cl_valid != 0;
   if (st->done) {
     if (rec) out->decision = SEL_DONE;
-    return SEL_DONE;
+    return;
   }
   if (!valid) {  // no usable list: measure the maximum, then rebuild at half of it
+    if (!rec) return;
     const Sel& prev = D.sel[par ^ 1];
     const bool measured = prev.decision == SEL_SKIP && (prev.skip & SKIP_MEASURE);
     const int64_t ms = measured ? st->cl_measured : 0;
-    if (rec) {
-      if (measured && ms == 0) {
-        out->decision = SEL_DONE;
-        out->maxc = 0;
-      } else {
-        out->decision = SEL_SKIP;
-        out->skip = measured ? SKIP_HOT : SKIP_MEASURE;
-        out->theta_new = (int32_t)max((int64_t)1, ms / 2);
-        out->build = act ^ 1;
-        st->ncl2[act ^ 1] = 0;  // (no mark workgroup reads the idle counter)
-      }
+    if (measured && ms == 0) {
+      out->decision = SEL_DONE;
+      out->maxc = 0;
+    } else {
+      out->decision = SEL_SKIP;
+      out->skip = measured ? SKIP_HOT : SKIP_MEASURE;
+      out->theta_new = (int32_t)max((int64_t)1, ms / 2);
+      out->build = act ^ 1;
+      st->ncl2[act ^ 1] = 0;  // (no mark workgroup reads the idle counter)
     }
-    return measured && ms == 0 ? SEL_DONE : SEL_SKIP;
+    return;
   }
-  // pass over the list: 4 entries per thread in flight; keep this thread's best
+  // ---- pass over the list: 4 entries per thread in flight; keep this thread's maximum
   int32_t m = 0, mkey = -1, mcnt = 0;
-  for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * BLOCK) {
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * SBLOCK) {
     int32_t d[4], c[4];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const int64_t i = i0 + (int64_t)q * BLOCK;
-      d[q] = i < n ? (i0 < BLOCK ? d0[q] : D.clist[i]) : -1;
+      const int64_t i = i0 + (int64_t)q * SBLOCK;
+      d[q] = i < n ? (i0 < SBLOCK ? d0[q] : D.clist[i]) : -1;
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) c[q] = d[q] >= 0 ? D.count[d[q]] : 0;
@@ -595,6 +753,7 @@ __device__ int32_t mark_select(const Dev& D, int par, int32_t* W_out) {
       }
     }
   }
+  if (rec) S.nt = 0;
   const int32_t gm = block_max(m, s_red);
   const bool hot = gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th);
   if (hot && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
@@ -602,7 +761,7 @@ __device__ int32_t mark_select(const Dev& D, int par, int32_t* W_out) {
       out->decision = SEL_DONE;
       out->maxc = 0;
     }
-    return SEL_DONE;
+    return;
   }
   // posting index stale (log full / overflowed / never built) and the merges are
   // small enough that a rebuild lasts >= 64 iterations: rebuild it this iteration
@@ -616,44 +775,74 @@ __device__ int32_t mark_select(const Dev& D, int par, int32_t* W_out) {
       out->build = act ^ 1;
       if (hot) st->ncl2[act ^ 1] = 0;
     }
-    return SEL_SKIP;
+    return;
   }
-  // each thread's smallest tied key (a thread with several re-reads its own entries)
-  int32_t best = -1, ntie = 0;
-  char* jb = s_jbuf + 48 * threadIdx.x;
-  if (m == gm) {
-    if (mcnt == 1) {
-      best = mkey;
-      ntie = 1;
-    } else {
-      for (int64_t i = threadIdx.x; i < n; i += BLOCK) {
-        const int32_t d = D.clist[i];
-        if (D.count[d] == gm) {
-          ntie++;
-          if (best < 0 || (d != best && key_less(D, d, best, jb))) best = d;
-        }
-      }
-    }
-  }
-  int32_t nt;
-  block_excl_scan(ntie, &nt, s_red);
-  s_best[threadIdx.x] = best;
-  __syncthreads();
-  for (int o = BLOCK / 2; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) {
-      const int32_t a = s_best[threadIdx.x], b = s_best[threadIdx.x + o];
-      if (a < 0 || (b >= 0 && b != a && key_less(D, b, a, jb))) s_best[threadIdx.x] = b;
-    }
-    __syncthreads();
-  }
-  const int32_t W = s_best[0];
-  *W_out = W;
   if (K >= D.KC) {
     if (rec) {
       set_error(D, GEOBPE_ECAPACITY, -9);
       out->decision = SEL_DONE;
     }
-    return SEL_DONE;
+    return;
+  }
+  // ---- the keys tied at the maximum (a thread with several re-reads its entries;
+  // a key listed twice is one candidate twice, harmless)
+  if (m == gm) {
+    if (mcnt == 1) {
+      const int32_t j = atomicAdd(&S.nt, 1);
+      if (j < SEL_TMAX) S.key[j] = mkey;
+    } else {
+      for (int64_t i = threadIdx.x; i < n; i += SBLOCK) {
+        const int32_t d = D.clist[i];
+        if (D.count[d] == gm) {
+          const int32_t j = atomicAdd(&S.nt, 1);
+          if (j < SEL_TMAX) S.key[j] = d;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  const int32_t nt = S.nt;
+  const int32_t t = threadIdx.x;
+  int32_t W;
+  if (nt == 1) {
+    W = S.key[0];
+  } else if (nt <= SEL_TMAX) {
+    // the candidates' contents (global), their staging offsets (one candidate per thread)
+    int32_t len = 0;
+    if (t < nt) {
+      S.seq[t] = key_seq(D, S.key[t]);
+      len = S.seq[t].nA + S.seq[t].nC;
+    }
+    int32_t tot;
+    const int32_t o = block_excl_scan(len, &tot, s_red);
+    if (t < nt) S.off[t] = o;
+    __syncthreads();
+    if (tot <= SEL_SYMS) {  // copy into LDS, one candidate per wave, 64 symbols a step
+      for (int32_t c = t >> 6; c < nt; c += SBLOCK / 64) {
+        const KSeq q = S.seq[c];
+        int32_t* dst = S.sym + S.off[c];
+        for (int32_t k = t & 63; k < q.nA; k += 64) dst[k] = q.A[k];
+        for (int32_t k = t & 63; k < q.nC; k += 64) dst[q.nA + k] = q.C[k];
+      }
+      __syncthreads();
+      if (t < nt) {
+        S.seq[t].A = S.sym + S.off[t];
+        S.seq[t].C = S.sym + S.off[t] + S.seq[t].nA;
+      }
+      __syncthreads();
+    }  // else: the tournament compares in global memory
+    W = S.key[wave_tournament(S, nt, D.B)];
+  } else {
+    // more tied keys than the staging holds (runs to exhaustion): the char
+    // generator over the list, 256 threads (48 chars of LDS each, in S.sym)
+    char* jb = (char*)S.sym + 48 * (t & 255);
+    int32_t best = -1;
+    if (t < 256)
+      for (int64_t i = t; i < n; i += 256) {
+        const int32_t d = D.clist[i];
+        if (D.count[d] == gm && (best < 0 || (d != best && key_less(D, d, best, jb)))) best = d;
+      }
+    W = block_min_key(D, best, S.idx, jb);
   }
   if (rec) {
     const int32_t L = D.krep[3 * (int64_t)W], g = D.krep[3 * (int64_t)W + 1], Rr = D.krep[3 * (int64_t)W + 2];
@@ -687,7 +876,6 @@ __device__ int32_t mark_select(const Dev& D, int par, int32_t* W_out) {
     out->wg = g;
     out->widR = Rr;
   }
-  return SEL_MERGE;
 }
 
 // ====================================================================== merge-apply
@@ -755,11 +943,6 @@ __device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag,
 // mode (index valid): O(bucket + log) reads.  Otherwise scan the 16-bit key
 // fingerprints (4 x 16 B per lane in flight; each workgroup owns CH8 8-slot
 // groups), confirm on pk.  Either way one merge region per workgroup.
-// one workgroup: the decision of this launch triple (Sel[par])
-__global__ __launch_bounds__(BLOCK) void k_select(Dev D, int par) {
-  int32_t W;
-  mark_select(D, par, &W);
-}
 
 // merge replay (bin/induce.py): merge t is the trained
 // token K0 + t, not the argmax.  Its key is looked up by content hash (find
@@ -1572,11 +1755,18 @@ __global__ __launch_bounds__(BLOCK) void k_gather_counts(Dev D, int32_t* keys, i
   }
 }
 
-// debug: device key-string order of n (a, b) key pairs (tests the JSON generator)
+// debug: device key-string order of n (a, b) key pairs, one wave per pair: the
+// char generator (key_less) and the wave comparator; 2 = they disagree
 __global__ __launch_bounds__(256) void k_debug_key_less(Dev D, const int32_t* pairs, int32_t* out, int32_t n) {
   __shared__ char s_jbuf[48 * 256];
-  const int32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = key_less(D, pairs[2 * i], pairs[2 * i + 1], s_jbuf + 48 * threadIdx.x) ? 1 : 0;
+  const int32_t i = (int32_t)((blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  if (i >= n) return;  // wave-uniform
+  const int32_t a = pairs[2 * i], b = pairs[2 * i + 1];
+  const bool w = wave_key_less(key_seq(D, a), key_seq(D, b), D.B);
+  if ((threadIdx.x & 63) == 0) {
+    const bool j = key_less(D, a, b, s_jbuf + 48 * threadIdx.x);
+    out[i] = j != w ? 2 : (j ? 1 : 0);
+  }
 }
 
 }  // namespace gb

@@ -60,6 +60,7 @@ def lib():
         "geobpe_key_json": (I64, [P, I32, ctypes.c_char_p, I64]),
         "geobpe_debug_key_less": (ctypes.c_int, [P, P, I32, P]),
         "geobpe_debug_counts": (I64, [P, P, P, I64]),
+        "geobpe_debug_state": (I64, [P, P, I64]),
         "geobpe_debug_key": (ctypes.c_int, [P, I32, P]),
         "geobpe_step_select": (ctypes.c_int, [P, pI32, pI32]),
         "geobpe_step_apply": (ctypes.c_int, [P, pI64]),
@@ -100,7 +101,7 @@ def lib():
 EXPORTED_SYMBOLS = [
     "geobpe_create", "geobpe_destroy", "geobpe_last_error", "geobpe_load_angles", "geobpe_angle_range",
     "geobpe_quantize", "geobpe_symbol_first", "geobpe_init_tokens", "geobpe_bin", "geobpe_set_bin_dense", "geobpe_step",
-    "geobpe_run", "geobpe_merge_log", "geobpe_key_json", "geobpe_debug_key_less", "geobpe_debug_counts", "geobpe_debug_key",
+    "geobpe_run", "geobpe_merge_log", "geobpe_key_json", "geobpe_debug_key_less", "geobpe_debug_counts", "geobpe_debug_state", "geobpe_debug_key",
     "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",

@@ -145,13 +145,22 @@ def _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_siz
     if not isinstance(bins, dict) or 1 not in bins:
         raise KeyError("bins must be a dict with key 1 (quantize/capacity need bins[1], bpe.py:896,909,952)")
     if len(bins) != 1:
-        raise NotImplementedError("multi-grid bin schedules (--bins 1-a:s-b) are not in this build (SURVEY §8(f) row 3)")
+        # the reference's step computes the new neighbour keys (bpe.py:1990-2006) before it
+        # re-snaps the merged span to grid(|token|) (bpe.py:2010-2013): with several grids the
+        # stored keys go stale and step() reaches breakpoint() at bpe.py:1917-1920
+        # (tests/golden/multigrid_reference.json)
+        raise NotImplementedError("multi-grid bin schedules (--bins 1-a:s-b): the reference's step() is inconsistent "
+                                  "for them (stale neighbour keys -> breakpoint at bpe.py:1919); see DESIGN.md §7")
     if bin_strategy not in ("histogram", "histogram-cover", "uniform"):
         raise NotImplementedError(f"bin_strategy={bin_strategy!r} (histogram / histogram-cover / uniform)")
     if not res_init:
         raise NotImplementedError("res_init=False cannot quantize in the reference either (SURVEY App. A)")
     if not std_bonds:
-        raise NotImplementedError("free bonds (std_bonds=False) are not in this build")
+        # the reference's res_init quant_geo bins bond lengths through _thresholds[bond]
+        # (bpe.py:1518-1519), which only std_bonds creates (bpe.py:874-876): its
+        # initialize() raises KeyError('N:CA') (tests/golden/multigrid_reference.json,
+        # "free-bonds"); this build raises the same error before any device work
+        raise KeyError("N:CA")
     if rmsd_partition_min_size != float("inf") and rmsd_partition_min_size < 10 ** 9:
         raise NotImplementedError("RMSD partitioning (p_min_size < inf) is float geometry, SURVEY §8(f) row 4")
     if glue_opt:

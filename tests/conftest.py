@@ -16,7 +16,8 @@ def pytest_configure(config):
 
 
 def golden_names():
-    return sorted(f[:-5] for f in os.listdir(GOLDEN) if f.endswith(".json") and not f.endswith(".pkl.json"))
+    return sorted(f[:-5] for f in os.listdir(GOLDEN)
+                  if f.endswith(".json") and os.path.exists(os.path.join(GOLDEN, f[:-5] + ".npz")))
 
 
 def pickle_golden_names():

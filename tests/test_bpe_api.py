@@ -19,7 +19,7 @@ def _bpe(meta, corpus):
     (dict(res_init=False), NotImplementedError),
     (dict(rmsd_partition_min_size=4), NotImplementedError),
     (dict(glue_opt=True), NotImplementedError),
-    (dict(std_bonds=False), NotImplementedError),
+    (dict(std_bonds=False), KeyError),  # as the reference's initialize() (free-bonds probe)
     (dict(bin_strategy="quantile"), NotImplementedError),
     (dict(bins={1: 5, 10: 3}), NotImplementedError),
     (dict(bins={2: 5}), KeyError),
@@ -32,6 +32,24 @@ def test_out_of_scope_configurations_are_rejected(kw, exc):
     bins = args.pop("bins")
     with pytest.raises(exc):
         BPE({"row_off": np.zeros(1, dtype=np.int64)}, bins, **args)
+
+
+def test_reference_probe_of_multigrid_and_free_bonds():
+    """Evidence behind the two rejections above (tests/golden/probe_multigrid.py ran
+    the reference): with a multi-grid schedule its step() finds a stale neighbour key
+    at step 1 (bpe.py:1917-1920) and, with breakpoints disabled, re-selects the same
+    key forever without merging; free bonds raise KeyError('N:CA') in initialize()."""
+    import os
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "multigrid_reference.json")) as f:
+        d = json.load(f)
+    dbg = d["debugger"]
+    assert dbg["stopped"] == "breakpoint at step 1" and dbg["breakpoints"][0]["line"] == 1919
+    assert dbg["breakpoints"][0]["differs"]  # stored key != recomputed key
+    loop = d["PYTHONBREAKPOINT=0"]["merges"]
+    assert len({m["key"] for m in loop[1:]}) == 1  # the same key every step
+    assert len({m["live_tokens_before"] for m in loop[1:]}) == 1  # and nothing merges
+    assert d["free-bonds"]["raised"] == "KeyError" and d["free-bonds"]["args"] == ["N:CA"]
 
 
 def test_codebook_utility_matches_definition():

@@ -102,6 +102,42 @@ def test_engine_matches_oracle_synthetic(cfg, oracle_lib):
     eng.close()
 
 
+def test_5000_merges_match_oracle(oracle_lib):
+    """Config 5 in its bins={1: 5} form is 5000 merges: a long run on a
+    C3-shaped corpus (U{40..560}) at an oracle-sized scale, bit-exact merge list and
+    encoding."""
+    from geobpe import synth
+    lengths = synth.make_lengths(3000, 40, 560, seed=51)
+    corpus = synth.make_corpus(lengths, seed=51, repeat_frac=0.05)
+    o = _oracle_run(oracle_lib, corpus, 5, 5000)
+    eng = _engine(corpus, 5)
+    eng.bin()
+    eng.run(5000)
+    assert len(o.merges) == 5000 and eng.merge_keys() == o.merges
+    assert eng.verify_counts() == 0
+    e, eo = eng.encode()
+    oe, oo = o.encode()
+    assert np.array_equal(e, oe) and np.array_equal(eo, oo)
+    eng.close()
+
+
+def test_c5_scale_properties():
+    """The C3 corpus (100k chains) through 5000 merges: incremental counts equal a
+    full recount and the segmentation tiles every chain."""
+    from geobpe import synth
+    lengths = synth.make_lengths(100_000, 40, 560, seed=0)
+    corpus = synth.make_corpus(lengths, seed=0)
+    eng = _engine(corpus, 5)
+    eng.bin()
+    assert eng.run(5000) == 5000
+    assert eng.verify_counts() == 0
+    s, ids, off = eng.segmentation()
+    e, eo = eng.encode()
+    assert np.array_equal(np.diff(eo), 4 * np.diff(off) - 3)
+    assert ids.min() >= 0 and ids.max() < eng.vocab_count
+    eng.close()
+
+
 def test_sharded_matches_oracle_synthetic(oracle_lib):
     from geobpe import synth
     from geobpe.dist import VirtualCluster
