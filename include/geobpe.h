@@ -120,6 +120,23 @@ int geobpe_delta_import_async(geobpe_ctx *ctx, const void *d_in, int64_t n_recor
 /* 1 = multi-rank mode (local changes go to the delta buffer), 0 = single.
  * Must precede geobpe_bin(). */
 int geobpe_set_distributed(geobpe_ctx *ctx, int on);
+/* Pipelined multi-rank loop (no host wait per merge).  The
+   reference has no distributed step (BPE.step, bpe.py:1792-2166, is serial); this
+   replaces a host-synchronised step_select / step_apply / delta exchange per merge.
+   Per iteration: geobpe_pipeline_iter enqueues select / mark / apply and the export
+   into d_buf = [header record: int64 count][records ... cap_total]; the caller
+   all-gathers the first (1 + cap_fixed) records of every rank's d_buf; then
+   geobpe_pipeline_import consumes the gathered slots.  A rank whose count exceeds
+   cap_fixed stalls every pipelined kernel; geobpe_pipeline_poll reports
+   {stalled, merges, done, largest slot count of the last import} (the same on every
+   rank: it sizes the next slots); after a stall the caller gathers the full records
+   of that merge and calls geobpe_pipeline_resolve. */
+int geobpe_pipeline_begin(geobpe_ctx *ctx);
+int geobpe_pipeline_iter(geobpe_ctx *ctx, void *d_buf, int64_t cap_total);
+int geobpe_pipeline_import(geobpe_ctx *ctx, const void *d_slots, int32_t world, int64_t cap_fixed);
+int geobpe_pipeline_poll(geobpe_ctx *ctx, int64_t *h_out4);
+int geobpe_pipeline_resolve(geobpe_ctx *ctx, const void *d_in, int64_t n_records);
+int geobpe_pipeline_end(geobpe_ctx *ctx);
 /* Residues of the whole (all-rank) corpus: sizes the replicated key table. */
 int geobpe_set_global_residues(geobpe_ctx *ctx, int64_t n);
 

@@ -19,7 +19,8 @@ constexpr double TWO_PI = 6.283185307179586;  // 2*np.pi
 constexpr int BLOCK = 256;
 constexpr int ABLOCK = 1024;  // region kernels (bin pairs, finalize, apply, import): 16 waves per CU
 constexpr int RPB = 8;         // mark regions per apply workgroup (NB = RPB * NBA)
-constexpr int CL_MIN_SHRINK = 4096;  // hot-list length above which a 4x drop of theta re-scans
+constexpr int CL_MIN_SHRINK = 4096;
+constexpr int PIPE_MAX_WORLD = 64;   // ranks of a pipelined exchange  // hot-list length above which a 4x drop of theta re-scans
 constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per region)
 constexpr int NBKT = 1 << NBKT_LOG2;
 constexpr int SKIP_HOT = 1, SKIP_POST = 2, SKIP_MEASURE = 4;  // what a rebuild iteration does
@@ -48,7 +49,7 @@ struct State {
   int32_t iter;       // merges made so far
   int32_t done;       // 1 once no pair is left
   int32_t maxc, ncand;  // the last merge's count and tied keys (stats)
-  int32_t pad0;
+  int32_t stall;      // pipelined exchange: a rank's deltas overflowed the fixed slot; every pipelined kernel no-ops
   // per launch pair: merge entries past the mark regions, by launch parity
   int64_t L_ovf2[2];
   // per bin / import launch
@@ -59,7 +60,7 @@ struct State {
   int32_t cl_act;      // active list counter
   int32_t theta;       // 0 = list not built yet
   int32_t cl_valid;
-  int32_t pad1;
+  int32_t dgen;        // pipelined exchange: iterations begun (launch parity = dgen & 1)
   int64_t cl_measured; // max count found by a measure iteration
   int64_t nskip;       // rebuild iterations so far (stats)
   int64_t nunchecked;  // found-key records beyond the check regions (not verified)
@@ -67,6 +68,7 @@ struct State {
   // pairs made since its last rebuild
   int32_t post_valid, plog_ovf;
   int64_t plog_total, npost;
+  int64_t slot_max;    // pipelined exchange: the largest slot count of the last import (every rank)
 };
 
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply

@@ -68,6 +68,7 @@ struct geobpe_ctx {
   int nb = 2048;  // mark workgroups (= D.NB)
   int64_t gen = 0;            // merge-loop launch pairs so far (parity selects Sel / overflow buffers)
   bool mark_pending = false;  // step_select decided a merge whose mark/apply are due
+  bool pipelined = false;     // between geobpe_pipeline_begin and _end (device-side parity)
   int nba = 256;  // apply / finalize / assign / bin / import workgroups (= D.NBA)
   // profiling
   bool prof = false;
@@ -671,6 +672,7 @@ int geobpe_bin(geobpe_ctx* c) {
 int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {
   if (!c || !c->keys_ready || !new_id) return GEOBPE_EARG;
   if (c->mark_pending) return fail(c, GEOBPE_EARG, "step_select twice without step_apply");
+  if (c->pipelined) return fail(c, GEOBPE_EARG, "step_select inside a pipelined exchange");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   Sel sel;
@@ -816,9 +818,103 @@ int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
 int geobpe_delta_export_async(geobpe_ctx* c, void* d_out, int64_t cap, void* d_count) {
   if (!c || !c->distributed || !d_out || !d_count) return GEOBPE_EARG;
   HIPCHK(c, hipSetDevice(c->device));
-  hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (DeltaRec*)d_out, cap);
-  hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_count, cap);
+  hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (DeltaRec*)d_out, cap, 0);
+  hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_count, cap, 0);
   HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+// ---------------------------------------------------------------- pipelined exchange
+// N > 1 without host waits: per iteration the select / mark / apply triple (launch
+// parity kept on the device, State.dgen), the export into a fixed slot (header +
+// records), a collective by the caller, and the import of the gathered slots.
+// A slot that overflowed stalls every pipelined kernel until the host resolves
+// that merge with a sized exchange; the host polls every few iterations.
+int geobpe_pipeline_begin(geobpe_ctx* c) {
+  if (!c || !c->distributed || !c->keys_ready) return GEOBPE_EARG;
+  if (c->mark_pending) return fail(c, GEOBPE_EARG, "pipeline_begin between step_select and step_apply");
+  if (c->ev) return fail(c, GEOBPE_EARG, "pipelined exchange with merge-event recording");
+  HIPCHK(c, hipSetDevice(c->device));
+  int rc;
+  if ((rc = sync_state(c))) return rc;
+  c->h_state->dgen = (int32_t)c->gen - 1;  // the next device iteration takes parity gen & 1
+  c->h_state->stall = 0;
+  HIPCHK(c, hipMemcpyAsync(&c->D.st->dgen, &c->h_state->dgen, 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(&c->D.st->stall, &c->h_state->stall, 4, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->pipelined = true;
+  return 0;
+}
+
+int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
+  if (!c || !c->pipelined || !d_buf) return GEOBPE_EARG;
+  {
+    Timed t(c, "select");
+    hipLaunchKernelGGL(k_select, dim3(1), dim3(SBLOCK), 0, c->stream, c->D, -1);
+  }
+  {
+    Timed t(c, "mark");
+    hipLaunchKernelGGL(k_mark, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, -1);
+  }
+  {
+    Timed t(c, "apply");
+    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
+  }
+  {
+    Timed t(c, "export");
+    DeltaRec* out = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
+    hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, out, cap_total, 1);
+    hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_buf, cap_total, 1);
+  }
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+int geobpe_pipeline_import(geobpe_ctx* c, const void* d_slots, int32_t world, int64_t cap_fixed) {
+  if (!c || !c->pipelined || !d_slots || world < 1 || world > PIPE_MAX_WORLD || cap_fixed < 0) return GEOBPE_EARG;
+  if (world * cap_fixed > (int64_t)c->nba * (c->D.RC - 256))
+    return fail(c, GEOBPE_EARG, "pipelined slots exceed one import launch (%d x %lld)", world, (long long)cap_fixed);
+  int rc;
+  if ((rc = reset_region_counters(c))) return rc;
+  {
+    Timed t(c, "import");
+    hipLaunchKernelGGL(k_import_fixed, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, (const uint8_t*)d_slots, world,
+                       cap_fixed);
+    hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, -1);
+  }
+  HIPCHK(c, hipGetLastError());
+  return 0;
+}
+
+// {stalled, merges made, done, largest slot count of the last import}: one wait
+int geobpe_pipeline_poll(geobpe_ctx* c, int64_t* h_out4) {
+  if (!c || !c->pipelined || !h_out4) return GEOBPE_EARG;
+  int rc;
+  if ((rc = sync_state(c))) return rc;
+  h_out4[0] = c->h_state->stall;
+  h_out4[1] = c->h_state->iter;
+  h_out4[2] = c->h_state->done;
+  h_out4[3] = c->h_state->slot_max;
+  return 0;
+}
+
+// the stalled merge's deltas of every rank (gathered by the caller from the
+// slots' full buffers): import them and release the pipeline
+int geobpe_pipeline_resolve(geobpe_ctx* c, const void* d_in, int64_t n_records) {
+  if (!c || !c->pipelined) return GEOBPE_EARG;
+  int rc;
+  if ((rc = delta_import(c, d_in, n_records))) return rc;
+  HIPCHK(c, hipMemsetAsync(&c->D.st->stall, 0, 4, c->stream));
+  return sync_state(c);
+}
+
+int geobpe_pipeline_end(geobpe_ctx* c) {
+  if (!c || !c->pipelined) return GEOBPE_EARG;
+  int rc;
+  if ((rc = sync_state(c))) return rc;
+  if (c->h_state->stall) return fail(c, GEOBPE_EARG, "pipeline_end while stalled");
+  c->gen = (int64_t)c->h_state->dgen + 1;  // host parity continues the device's
+  c->pipelined = false;
   return 0;
 }
 

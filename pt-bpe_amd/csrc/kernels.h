@@ -383,6 +383,10 @@ __device__ void rebuild_postings(const Dev& D, int32_t* hist) {
 __global__ __launch_bounds__(ABLOCK) void k_finalize(Dev D, int to_delta) {
   __shared__ AggBig agg;
   __shared__ HotApp hot;
+  if (to_delta < 0) {  // after a pipelined import: no-op while stalled
+    if (D.st->stall) return;
+    to_delta = 0;
+  }
   const int32_t th = D.st->theta;
   agg_init(agg);
   hot_init(hot);
@@ -699,6 +703,13 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
   State* st = D.st;
+  if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
+    if (st->stall) return;
+    const int32_t g = st->dgen + 1;
+    par = g & 1;
+    __syncthreads();  // every thread has read dgen
+    if (threadIdx.x == 0) st->dgen = g;
+  }
   Sel* out = D.sel + par;
   const bool rec = threadIdx.x == 0;
   const int32_t act = st->cl_act;
@@ -1025,6 +1036,10 @@ __global__ __launch_bounds__(64) void k_select_replay(Dev D, int par, const Repl
 
 __global__ __launch_bounds__(BLOCK) void k_mark(Dev D, int par) {
   __shared__ int32_t s_n;
+  if (par < 0) {  // pipelined exchange (k_select set dgen)
+    if (D.st->stall) return;
+    par = D.st->dgen & 1;
+  }
   const bool posting = D.st->post_valid && !D.st->plog_ovf;
   const Sel& sel = D.sel[par];
   if (!posting && blockIdx.x < D.NBA) check_found(D, blockIdx.x);
@@ -1407,6 +1422,10 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta, int par) 
   __shared__ u64 s_pw[2 * PW_LDS];
   __shared__ int64_t s_kl[2];
   State* st = D.st;
+  if (par < 0) {  // pipelined exchange (k_select set dgen)
+    if (st->stall) return;
+    par = st->dgen & 1;
+  }
   const Sel sel = D.sel[par];  // this launch pair's decision (k_mark)
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     st->L_ovf2[par ^ 1] = 0;  // the next mark's overflow counter (idle since the last pair)
@@ -1643,7 +1662,8 @@ __global__ __launch_bounds__(BLOCK) void k_export(Dev D, DeltaRec* out, int64_t 
 
 // device-counted export (no host round trip): every touched key's record, up to
 // cap; k_export_fin then publishes the count and opens the next epoch
-__global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int64_t cap) {
+__global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int64_t cap, int chk_stall) {
+  if (chk_stall && D.st->stall) return;  // pipelined: keep the stalled merge's records
   const int64_t n = min(D.st->ntouched, cap);
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = D.touched[j];
@@ -1659,8 +1679,9 @@ __global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int6
     out[j] = r;
   }
 }
-__global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap) {
+__global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap, int chk_stall) {
   State* st = D.st;
+  if (chk_stall && st->stall) return;
   const int64_t n = st->ntouched;
   d_count[0] = n;
   if (n > cap) set_error(D, GEOBPE_ECAPACITY, -30);
@@ -1678,6 +1699,49 @@ __global__ __launch_bounds__(ABLOCK) void k_import(Dev D, const DeltaRec* in, in
     const DeltaRec r = in[j];
     if (r.delta == 0) continue;
     add_pair(D, &s_np, &s_ns, -1, r.h1, r.h2, r.len, r.idL, r.g, r.idR, r.delta);
+  }
+  close_regions(D, &s_np, &s_ns);
+}
+
+// pipelined exchange: the all-gathered fixed slots of `world` ranks, each
+// {int64 count, pad to 40 B} + capf records.  A count above capf (that rank's
+// records did not fit) stalls the pipeline instead: nothing is imported, and the
+// host re-exchanges that merge's deltas in full (geobpe_pipeline_resolve).
+__global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* in, int world, int64_t capf) {
+  __shared__ int32_t s_np, s_ns, s_bad;
+  __shared__ int64_t s_cnt[PIPE_MAX_WORLD + 1];
+  if (D.st->stall) return;
+  const int64_t slot = (1 + capf) * (int64_t)sizeof(DeltaRec);
+  if (threadIdx.x == 0) {
+    int64_t acc = 0, mx = 0;
+    int bad = 0;
+    for (int r = 0; r < world; r++) {
+      const int64_t c = *reinterpret_cast<const int64_t*>(in + r * slot);
+      s_cnt[r] = acc;
+      acc += min(c, capf);
+      mx = max(mx, c);
+      bad |= c > capf;
+    }
+    s_cnt[world] = acc;
+    s_bad = bad;
+    s_np = s_ns = 0;
+    if (blockIdx.x == 0) D.st->slot_max = mx;  // sizes the host's next slots
+  }
+  __syncthreads();
+  if (s_bad) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) D.st->stall = 1;
+    return;
+  }
+  const int64_t n = s_cnt[world];
+  const int64_t E = (n + gridDim.x - 1) / gridDim.x;
+  const int64_t lo = (int64_t)blockIdx.x * E, hi = min(n, lo + E);
+  for (int64_t j = lo + threadIdx.x; j < hi; j += blockDim.x) {
+    int r = 0;
+    while (j >= s_cnt[r + 1]) r++;
+    const DeltaRec* recs = reinterpret_cast<const DeltaRec*>(in + r * slot + sizeof(DeltaRec));
+    const DeltaRec rr = recs[j - s_cnt[r]];
+    if (rr.delta == 0) continue;
+    add_pair(D, &s_np, &s_ns, -1, rr.h1, rr.h2, rr.len, rr.idL, rr.g, rr.idR, rr.delta);
   }
   close_regions(D, &s_np, &s_ns);
 }

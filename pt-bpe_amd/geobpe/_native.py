@@ -85,6 +85,12 @@ def lib():
         "geobpe_replay_load": (ctypes.c_int, [P, P, P, P, P, P, P, I64]),
         "geobpe_delta_export_async": (ctypes.c_int, [P, P, I64, P]),
         "geobpe_delta_import_async": (ctypes.c_int, [P, P, I64]),
+        "geobpe_pipeline_begin": (ctypes.c_int, [P]),
+        "geobpe_pipeline_iter": (ctypes.c_int, [P, P, I64]),
+        "geobpe_pipeline_import": (ctypes.c_int, [P, P, ctypes.c_int32, I64]),
+        "geobpe_pipeline_poll": (ctypes.c_int, [P, P]),
+        "geobpe_pipeline_resolve": (ctypes.c_int, [P, P, I64]),
+        "geobpe_pipeline_end": (ctypes.c_int, [P]),
         "geobpe_pdb_backbone": (I64, [ctypes.c_char_p, P, I64]),
         "geobpe_pdb_error": (ctypes.c_char_p, []),
         "geobpe_featurize": (ctypes.c_int, [ctypes.c_int, I64, P, P, P]),
@@ -107,7 +113,8 @@ EXPORTED_SYMBOLS = [
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
     "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_synchronize",
     "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",
-    "geobpe_delta_export_async", "geobpe_delta_import_async", "geobpe_pdb_backbone", "geobpe_pdb_error",
+    "geobpe_delta_export_async", "geobpe_delta_import_async", "geobpe_pipeline_begin", "geobpe_pipeline_iter",
+    "geobpe_pipeline_import", "geobpe_pipeline_poll", "geobpe_pipeline_resolve", "geobpe_pipeline_end", "geobpe_pdb_backbone", "geobpe_pdb_error",
     "geobpe_featurize",
 ]
 

@@ -124,6 +124,88 @@ class TorchGroup:
         return ctypes.c_void_p(flat.data_ptr()), int(sum(counts))
 
 
+    # ---------------------------------------------------------------- pipelined exchange
+    PIPE_CAP_MIN, PIPE_CAP_MAX = 1024, 65536  # records per rank slot (40 B each)
+    PIPE_AHEAD = 64      # iterations enqueued between polls (doubling from 1 after a stall)
+
+    def run_pipelined(self, engine, n_merges: int) -> int:
+        """``n_merges`` merges with no host wait per merge (include/geobpe.h,
+        geobpe_pipeline_*): per iteration the engine enqueues select / mark / apply
+        and its export into a fixed slot, one all-gather of the slots follows on the
+        engine's stream, then the import.  The host polls every few iterations; a
+        merge whose records overflowed a slot stalls the device until it is
+        re-exchanged in full (`_resolve`).  Slots are sized per poll window from the
+        largest count of the last import (2x, a power of two, clamped): the merges'
+        counts shrink as training goes on, and so do the collectives.  Every rank
+        sees the same poll results, so every rank issues the same collectives."""
+        T, L, ctx = self.torch, engine.L, engine._ctx
+        W = self.world_size
+        fixed = getattr(self, "pipe_cap", None)  # tests: a fixed slot size
+        if getattr(self, "_pbuf", None) is None:
+            self._pcap = 3 * self.R_local + 65536
+            self._pbuf = T.zeros((1 + self._pcap) * REC, dtype=T.uint8, device=self.dev)
+            top = int(fixed) if fixed else self.PIPE_CAP_MAX
+            self._gath = T.empty(W * (1 + top) * REC, dtype=T.uint8, device=self.comm_dev)
+        pbuf = ctypes.c_void_p(self._pbuf.data_ptr())
+        out = (ctypes.c_int64 * 4)()
+        engine._chk(L.geobpe_pipeline_begin(ctx))
+        try:
+            engine._chk(L.geobpe_pipeline_poll(ctx, out))
+            it0, done, ahead = int(out[1]), 0, 1
+            capf = int(fixed) if fixed else self.PIPE_CAP_MIN
+            with T.cuda.stream(engine.torch_stream):
+                while done < n_merges:
+                    slot = (1 + capf) * REC
+                    gath = self._gath[: W * slot]
+                    for _ in range(min(ahead, n_merges - done)):  # an iteration merges at most once
+                        engine._chk(L.geobpe_pipeline_iter(ctx, pbuf, self._pcap))
+                        src = self._pbuf[:slot]
+                        if self.on_gpu:
+                            self.dist.all_gather_into_tensor(gath, src, group=self.pg)
+                            g = gath
+                        else:  # gloo: through host copies
+                            self.dist.all_gather_into_tensor(gath, src.cpu(), group=self.pg)
+                            g = gath.to(self.dev)
+                            self._keep = g
+                        engine._chk(L.geobpe_pipeline_import(ctx, ctypes.c_void_p(g.data_ptr()), W, capf))
+                    engine._chk(L.geobpe_pipeline_poll(ctx, out))
+                    stalled, it, fin, smax = (int(x) for x in out)
+                    if stalled:
+                        self._resolve(engine)
+                        ahead = 1
+                    else:
+                        ahead = min(2 * ahead, self.PIPE_AHEAD)
+                    if not fixed:
+                        capf = min(self.PIPE_CAP_MAX, max(self.PIPE_CAP_MIN, 1 << (2 * max(smax, 1) - 1).bit_length()))
+                    done = it - it0
+                    if fin:
+                        break
+        finally:
+            engine._chk(L.geobpe_pipeline_end(ctx))
+        return done
+
+    def _resolve(self, engine):
+        """The stalled merge's full records: counts from the slot headers, then the
+        records (sized by the largest count), imported on every rank."""
+        T = self.torch
+        cnt = self._pbuf[:8].view(T.int64)
+        src = cnt if self.on_gpu else cnt.cpu()
+        allc = T.empty(self.world_size, dtype=T.int64, device=src.device)
+        self.dist.all_gather_into_tensor(allc, src, group=self.pg)
+        counts = [int(x) for x in allc.cpu().tolist()]
+        m = max(counts)
+        if m > self._pcap:
+            raise _native.GeoBPEError(f"delta export needs {m} records (cap {self._pcap})")
+        src = self._pbuf[REC: REC + m * REC]
+        if not self.on_gpu:
+            src = src.cpu()
+        out = T.empty(self.world_size * m * REC, dtype=T.uint8, device=src.device)
+        self.dist.all_gather_into_tensor(out, src, group=self.pg)
+        out = out.view(self.world_size, m * REC)
+        flat = T.cat([out[r, : counts[r] * REC] for r in range(self.world_size)]).to(self.dev)
+        engine._chk(engine.L.geobpe_pipeline_resolve(engine._ctx, ctypes.c_void_p(flat.data_ptr()),
+                                                      int(sum(counts))))
+
     def exchange_async(self, engine):
         """One merge's exchange with two host waits in all: the export count is
         written on the device and all-gathered, the host reads the counts (the

@@ -95,6 +95,9 @@ class GeoBPEEngine:
             raise NotImplementedError(f"bin_strategy={self.strategy!r}")
         self.cover = self.strategy == "histogram-cover"
         self.bin_dense = bool(bin_dense)
+        # multi-rank run(): the pipelined exchange (no host wait per merge, geobpe.dist)
+        self.pipelined = True
+        self._events_on = False
         self.row_off = np.ascontiguousarray(corpus["row_off"], dtype=np.int64)
         self.n_rows = len(self.row_off) - 1
         self._cols = [np.ascontiguousarray(corpus[c], dtype=np.float64) for c in COLUMNS]
@@ -266,6 +269,12 @@ class GeoBPEEngine:
         if not self._binned:
             raise RuntimeError("bin() first")
         if self.distributed:
+            if self.pipelined and not self._events_on and hasattr(self.group, "run_pipelined"):
+                done = self.group.run_pipelined(self, int(n_merges))
+                self._refresh_log()
+                if done < n_merges:
+                    self._done = True
+                return done
             done = 0
             for _ in range(n_merges):
                 if self.step(want_merged=False) is None:
@@ -384,6 +393,7 @@ class GeoBPEEngine:
         """Log every merged occurrence from now on (before the first merge): the
         checkpoint's merge tree (geobpe.refpickle)."""
         self._chk(self.L.geobpe_set_record_events(self._ctx, 1 if on else 0))
+        self._events_on = bool(on)
 
     def events(self):
         """(a, b, off): left / right token start slots of the merged occurrences,

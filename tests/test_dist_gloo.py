@@ -74,7 +74,7 @@ def test_torchgroup_gloo_world2():
     assert res == {0: "ok", 1: "ok"}
 
 
-def _engine_worker(rank, world, port, q):
+def _engine_worker(rank, world, port, q, mode="pipelined"):
     import sys
     here = os.path.dirname(os.path.abspath(__file__))
     sys.path.insert(0, os.path.join(os.path.dirname(here), "pt-bpe_amd"))
@@ -92,9 +92,13 @@ def _engine_worker(rank, world, port, q):
         lo, hi = shard_rows(corpus["row_off"], world)[rank]
         shard = slice_corpus(corpus, lo, hi)
         g = TorchGroup(int(shard["row_off"][-1]), device=0)
+        if mode == "small-slots":  # most merges overflow the fixed slots: the stall / resolve path
+            g.pipe_cap = 16
         e = GeoBPEEngine(shard, 5, device=0, group=g).initialize()
+        e.pipelined = mode != "stepwise"
         e.bin()
-        done = e.run(150)
+        done = e.run(70)
+        done += e.run(80)  # a second pipelined run continues the device parity
         s, ids, off = e.segmentation()
         q.put((rank, done, e.merge_keys(), ids.tolist()))
     except Exception as ex:  # pragma: no cover
@@ -104,17 +108,18 @@ def _engine_worker(rank, world, port, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_multirank_engine_on_one_gpu_matches_single(world, oracle_lib):
-    """The full N>1 path (TorchGroup exchange, stream-ordered export/import, one
-    process per rank) with gloo on one device: merge list and segmentation equal
-    the single-engine run and the oracle."""
+@pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise")])
+def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
+    """The full N>1 path (TorchGroup exchange, one process per rank) with gloo on
+    one device: the pipelined exchange (fixed slots, stall + full re-exchange of an
+    overflowing merge), the same with tiny slots, and the host-synchronised
+    per-merge exchange; merge list and segmentation equal the oracle's."""
     import multiprocessing as mp
     from geobpe import synth
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_engine_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_engine_worker, args=(r, world, port, q, mode)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted(q.get(timeout=300) for _ in ps)
