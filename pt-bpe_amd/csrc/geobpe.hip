@@ -818,7 +818,8 @@ int geobpe_delta_import(geobpe_ctx* c, const void* d_in, int64_t n_records) {
 int geobpe_delta_export_async(geobpe_ctx* c, void* d_out, int64_t cap, void* d_count) {
   if (!c || !c->distributed || !d_out || !d_count) return GEOBPE_EARG;
   HIPCHK(c, hipSetDevice(c->device));
-  hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (DeltaRec*)d_out, cap, 0);
+  hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (DeltaRec*)d_out, cap, 0,
+                     (int64_t*)nullptr);
   hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_count, cap, 0);
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -863,8 +864,7 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   {
     Timed t(c, "export");
     DeltaRec* out = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
-    hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, out, cap_total, 1);
-    hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_buf, cap_total, 1);
+    hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, out, cap_total, 1, (int64_t*)d_buf);
   }
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -872,15 +872,10 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
 
 int geobpe_pipeline_import(geobpe_ctx* c, const void* d_slots, int32_t world, int64_t cap_fixed) {
   if (!c || !c->pipelined || !d_slots || world < 1 || world > PIPE_MAX_WORLD || cap_fixed < 0) return GEOBPE_EARG;
-  if (world * cap_fixed > (int64_t)c->nba * (c->D.RC - 256))
-    return fail(c, GEOBPE_EARG, "pipelined slots exceed one import launch (%d x %lld)", world, (long long)cap_fixed);
-  int rc;
-  if ((rc = reset_region_counters(c))) return rc;
   {
     Timed t(c, "import");
     hipLaunchKernelGGL(k_import_fixed, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, (const uint8_t*)d_slots, world,
                        cap_fixed);
-    hipLaunchKernelGGL(k_finalize, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, -1);
   }
   HIPCHK(c, hipGetLastError());
   return 0;

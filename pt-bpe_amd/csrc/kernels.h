@@ -383,10 +383,6 @@ __device__ void rebuild_postings(const Dev& D, int32_t* hist) {
 __global__ __launch_bounds__(ABLOCK) void k_finalize(Dev D, int to_delta) {
   __shared__ AggBig agg;
   __shared__ HotApp hot;
-  if (to_delta < 0) {  // after a pipelined import: no-op while stalled
-    if (D.st->stall) return;
-    to_delta = 0;
-  }
   const int32_t th = D.st->theta;
   agg_init(agg);
   hot_init(hot);
@@ -1662,9 +1658,15 @@ __global__ __launch_bounds__(BLOCK) void k_export(Dev D, DeltaRec* out, int64_t 
 
 // device-counted export (no host round trip): every touched key's record, up to
 // cap; k_export_fin then publishes the count and opens the next epoch
-__global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int64_t cap, int chk_stall) {
+__global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int64_t cap, int chk_stall,
+                                                     int64_t* d_count) {
   if (chk_stall && D.st->stall) return;  // pipelined: keep the stalled merge's records
-  const int64_t n = min(D.st->ntouched, cap);
+  const int64_t nt = D.st->ntouched;
+  const int64_t n = min(nt, cap);
+  if (d_count && blockIdx.x == 0 && threadIdx.x == 0) {  // pipelined: the slot header (k_import_fixed resets ntouched)
+    d_count[0] = nt;
+    if (nt > cap) set_error(D, GEOBPE_ECAPACITY, -30);
+  }
   for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = D.touched[j];
     DeltaRec r;
@@ -1707,10 +1709,17 @@ __global__ __launch_bounds__(ABLOCK) void k_import(Dev D, const DeltaRec* in, in
 // {int64 count, pad to 40 B} + capf records.  A count above capf (that rank's
 // records did not fit) stalls the pipeline instead: nothing is imported, and the
 // host re-exchanges that merge's deltas in full (geobpe_pipeline_resolve).
+// Import and finalize in one pass: every record's key is found or claimed and its
+// delta added to the global count at once (the ranks' deltas are per key already;
+// no LDS aggregation to gain), with the hot-list crossing check; a found key's
+// content joins this workgroup's check region (verified by the next k_mark, as
+// k_apply's finds are).  Also opens the next delta epoch (the export consumed it).
 __global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* in, int world, int64_t capf) {
-  __shared__ int32_t s_np, s_ns, s_bad;
+  __shared__ int32_t s_ns, s_chk, s_bad;
   __shared__ int64_t s_cnt[PIPE_MAX_WORLD + 1];
-  if (D.st->stall) return;
+  __shared__ HotApp hot;
+  State* st = D.st;
+  if (st->stall) return;
   const int64_t slot = (1 + capf) * (int64_t)sizeof(DeltaRec);
   if (threadIdx.x == 0) {
     int64_t acc = 0, mx = 0;
@@ -1724,14 +1733,21 @@ __global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* i
     }
     s_cnt[world] = acc;
     s_bad = bad;
-    s_np = s_ns = 0;
-    if (blockIdx.x == 0) D.st->slot_max = mx;  // sizes the host's next slots
+    s_ns = 0;
+    s_chk = min(D.chkcnt[blockIdx.x], (int32_t)D.RC);  // after k_apply's finds
+    if (blockIdx.x == 0) {
+      st->slot_max = mx;  // sizes the host's next slots
+      st->ntouched = 0;   // the export of this merge consumed the touched list
+      st->epoch += 1;
+    }
   }
+  hot_init(hot);
   __syncthreads();
   if (s_bad) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) D.st->stall = 1;
+    if (blockIdx.x == 0 && threadIdx.x == 0) st->stall = 1;
     return;
   }
+  const int32_t th = st->theta;
   const int64_t n = s_cnt[world];
   const int64_t E = (n + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * E, hi = min(n, lo + E);
@@ -1741,9 +1757,20 @@ __global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* i
     const DeltaRec* recs = reinterpret_cast<const DeltaRec*>(in + r * slot + sizeof(DeltaRec));
     const DeltaRec rr = recs[j - s_cnt[r]];
     if (rr.delta == 0) continue;
-    add_pair(D, &s_np, &s_ns, -1, rr.h1, rr.h2, rr.len, rr.idL, rr.g, rr.idR, rr.delta);
+    bool claimed;
+    const int32_t d = ht_insert(D, rr.h1, rr.h2, rr.len, &claimed);
+    if (d < 0) continue;
+    if (claimed) {
+      claim_payload(D, d, rr.h1, rr.h2, rr.len, rr.idL, rr.g, rr.idR);
+      note_claim(D, &s_ns, d);
+    } else {
+      emit_check(D, &s_chk, d, rr.len, rr.h1, rr.h2);
+    }
+    count_add_hot(D, hot, d, rr.delta, th);
   }
-  close_regions(D, &s_np, &s_ns);
+  hot_flush(D, hot);
+  close_claims(D, &s_ns);
+  if (threadIdx.x == 0) D.chkcnt[blockIdx.x] = min(s_chk, (int32_t)D.RC);
 }
 
 // ====================================================================== exports / checks
