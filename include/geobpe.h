@@ -217,6 +217,15 @@ int geobpe_replay_load(geobpe_ctx *ctx, const uint64_t *h_h1, const uint64_t *h_
  * logged on the device.  geobpe_events copies (merge index, left token start
  * slot, right token start slot) of all logged events (any order within a merge)
  * and returns their number (-1: not recording / error); NULL buffers: count only. */
+/* Kabsch RMSD of structure pairs (no context needed).
+   h_a: n_a structures x n_atoms x 3 float64; h_b likewise (ignored when symmetric);
+   h_out[i * n_b + j] = compute_rmsd(A_i, B_j) of foldingdiff/algo.py:48-65 (Q = B_j
+   aligned onto P = A_i by kabsch, algo.py:8-46).  symmetric: B = A, the upper
+   triangle is computed and mirrored (k_medoids' distance matrix, algo.py:179-189).
+   Replaces the joblib-threaded compute_rmsd loops of k_medoids and the medoid
+   assignment (bpe.py:645-657, 1764-1777). */
+int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const double *h_a, const double *h_b,
+                int symmetric, double *h_out);
 int geobpe_set_record_events(geobpe_ctx *ctx, int on);
 int64_t geobpe_events(geobpe_ctx *ctx, int32_t *h_merge, int32_t *h_a, int32_t *h_b);
 

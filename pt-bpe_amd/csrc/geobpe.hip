@@ -29,6 +29,7 @@
 #include "keyjson.h"
 #include "kernels.h"
 #include "featurize.h"
+#include "rmsd.h"
 
 using namespace gb;
 
@@ -1249,6 +1250,44 @@ int geobpe_featurize(int device, int64_t n_rows, const int64_t* h_row_off, const
   }
   hipFree(d_off);
   hipFree(d_xyz);
+  hipFree(d_out);
+  hipStreamDestroy(s);
+  return rc;
+}
+
+int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const double* h_a, const double* h_b,
+                int symmetric, double* h_out) {
+  if (n_a < 0 || n_atoms <= 0 || !h_a || !h_out) return GEOBPE_EARG;
+  if (symmetric) {
+    h_b = h_a;
+    n_b = n_a;
+  }
+  if (n_b < 0 || !h_b) return GEOBPE_EARG;
+  if ((int64_t)n_a * n_b == 0) return 0;
+  if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GEOBPE_EHIP;
+  const int64_t la = (int64_t)n_a * n_atoms * 3, lb = (int64_t)n_b * n_atoms * 3, no = (int64_t)n_a * n_b;
+  double *d_a = nullptr, *d_b = nullptr, *d_out = nullptr;
+  int rc = 0;
+  if (hipMalloc(&d_a, la * 8) != hipSuccess || (!symmetric && hipMalloc(&d_b, lb * 8) != hipSuccess) ||
+      hipMalloc(&d_out, no * 8) != hipSuccess) {
+    rc = GEOBPE_EHIP;
+  } else {
+    hipMemcpyAsync(d_a, h_a, la * 8, hipMemcpyHostToDevice, s);
+    hipLaunchKernelGGL(k_rmsd_center, dim3((n_a + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d_a, n_a, n_atoms);
+    if (!symmetric) {
+      hipMemcpyAsync(d_b, h_b, lb * 8, hipMemcpyHostToDevice, s);
+      hipLaunchKernelGGL(k_rmsd_center, dim3((n_b + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d_b, n_b, n_atoms);
+    }
+    hipLaunchKernelGGL(k_rmsd_pairs, dim3((unsigned)((no + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, (const double*)d_a,
+                       (const double*)(symmetric ? d_a : d_b), n_a, n_b, n_atoms, symmetric, d_out);
+    if (hipGetLastError() != hipSuccess) rc = GEOBPE_EHIP;
+    if (!rc && hipMemcpyAsync(h_out, d_out, no * 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = GEOBPE_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess) rc = GEOBPE_EHIP;
+  }
+  hipFree(d_a);
+  hipFree(d_b);
   hipFree(d_out);
   hipStreamDestroy(s);
   return rc;
