@@ -149,6 +149,7 @@ class TorchGroup:
         pbuf = ctypes.c_void_p(self._pbuf.data_ptr())
         out = (ctypes.c_int64 * 4)()
         engine._chk(L.geobpe_pipeline_begin(ctx))
+        ok = False
         try:
             engine._chk(L.geobpe_pipeline_poll(ctx, out))
             it0, done, ahead = int(out[1]), 0, 1
@@ -180,8 +181,11 @@ class TorchGroup:
                     done = it - it0
                     if fin:
                         break
+            ok = True
         finally:
-            engine._chk(L.geobpe_pipeline_end(ctx))
+            rc = L.geobpe_pipeline_end(ctx)
+            if ok:  # (an error in flight is the one to report)
+                engine._chk(rc)
         return done
 
     def _resolve(self, engine):

@@ -98,7 +98,12 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
         e.pipelined = mode != "stepwise"
         e.bin()
         done = e.run(70)
-        done += e.run(80)  # a second pipelined run continues the device parity
+        if mode == "mixed":  # pipelined -> host-synchronised step() -> pipelined: the parity hand-offs
+            for _ in range(20):
+                done += e.step(want_merged=False) is not None
+            done += e.run(60)
+        else:
+            done += e.run(80)  # a second pipelined run continues the device parity
         s, ids, off = e.segmentation()
         q.put((rank, done, e.merge_keys(), ids.tolist()))
     except Exception as ex:  # pragma: no cover
@@ -108,7 +113,8 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise")])
+@pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise"),
+                                         (3, "mixed")])
 def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
     """The full N>1 path (TorchGroup exchange, one process per rank) with gloo on
     one device: the pipelined exchange (fixed slots, stall + full re-exchange of an
