@@ -245,6 +245,24 @@ def test_run_to_exhaustion_device_loop(oracle_lib):
     eng.close()
 
 
+def test_exhaustion_with_large_tie_sets(oracle_lib):
+    """Merged until nothing is left on a corpus whose last merges tie thousands of
+    count-1 keys with long contents: exercises k_select's fallbacks (more tied keys
+    than the LDS staging holds -> char-generator scan; staged contents past the LDS
+    budget -> wave comparisons in global memory)."""
+    from geobpe import synth
+    lengths = synth.make_lengths(150, 20, 60, seed=71)
+    corpus = synth.make_corpus(lengths, seed=71, repeat_frac=0.1)
+    o = _oracle_run(oracle_lib, corpus, 5, 10 ** 6)
+    eng = _engine(corpus, 5)
+    eng.bin()
+    n = eng.run(10 ** 6)
+    assert n == len(o.merges)
+    assert eng.merge_keys() == o.merges
+    assert max(m[1] for m in eng.merges[-200:]) == 1
+    eng.close()
+
+
 @pytest.mark.parametrize("cfg", [
     dict(n=2000, lo=40, hi=300, B=5, seed=61, rep=0.05),
     dict(n=300, lo=1, hi=40, B=3, seed=62, rep=0.2),
