@@ -25,7 +25,10 @@ constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per re
 constexpr int NBKT = 1 << NBKT_LOG2;
 constexpr int SKIP_HOT = 1, SKIP_POST = 2, SKIP_MEASURE = 4;  // what a rebuild iteration does
 constexpr int DBG_SLOTS = 64;
-constexpr int PW_LDS = 2048;    // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
+#ifndef PW_LDS_DEF
+#define PW_LDS_DEF 2048
+#endif
+constexpr int PW_LDS = PW_LDS_DEF;  // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
 constexpr int KL_CHUNK = 4096;  // klist entries an apply workgroup reserves at a time
 #ifndef POST_SPAN_DEF
 #define POST_SPAN_DEF 64
