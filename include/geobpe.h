@@ -226,6 +226,14 @@ int geobpe_replay_load(geobpe_ctx *ctx, const uint64_t *h_h1, const uint64_t *h_
    assignment (bpe.py:645-657, 1764-1777). */
 int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const double *h_a, const double *h_b,
                 int symmetric, double *h_out);
+/* NeRF: token coordinates from internal coordinates (Tokenizer.geo_nerf,
+   tokenizer.py:317-344, NERFBuilder / place_dihedral, nerf.py:85-211, the first
+   residue by update_backbone_positions, angles_and_coords.py:238-316), one span of
+   whole residues per thread.  h_res_off[n_spans + 1]: residue offsets; h_geo: 9
+   float64 per residue {N:CA, CA:C, tau, 0C:1N, CA:C:1N, C:1N:1CA, psi, omega, phi}
+   (the last six: the junction to the next residue of the span); h_xyz: N, CA, C of
+   every residue (9 float64 per residue). */
+int geobpe_nerf(int device, int64_t n_spans, const int64_t *h_res_off, const double *h_geo, double *h_xyz);
 int geobpe_set_record_events(geobpe_ctx *ctx, int on);
 int64_t geobpe_events(geobpe_ctx *ctx, int32_t *h_merge, int32_t *h_a, int32_t *h_b);
 

@@ -35,3 +35,44 @@ def rmsd_matrix(S) -> np.ndarray:
         for j in range(i, N):
             D[i, j] = D[j, i] = rmsd(S[i], S[j])
     return D
+
+
+# NeRF (nerf.py:85-211 place_dihedral / NERFBuilder.cartesian_coords;
+# angles_and_coords.py:232-316 update_backbone_positions), restated with numpy
+N_INIT = np.array([17.047, 14.099, 3.625])
+CA_INIT = np.array([16.967, 12.784, 4.338])
+C_INIT = np.array([15.685, 12.755, 5.133])
+
+
+def _unit(x):
+    return x / np.linalg.norm(x)
+
+
+def place(a, b, c, angle, length, torsion):
+    bc = _unit(c - b)
+    n = _unit(np.cross(b - a, bc))
+    m = np.stack([bc, np.cross(n, bc), n], axis=-1)
+    d = np.array([-length * np.cos(angle), length * np.cos(torsion) * np.sin(angle),
+                  length * np.sin(torsion) * np.sin(angle)])
+    return m @ d + c
+
+
+def start(l_ca_c, l_n_ca, theta):
+    ca = C_INIT + l_ca_c * _unit(CA_INIT - C_INIT)
+    vn, vc = N_INIT - ca, C_INIT - ca
+    cur = np.arccos(np.clip(np.dot(vn, vc) / (np.linalg.norm(vn) * np.linalg.norm(vc)), -1.0, 1.0))
+    k = _unit(np.cross(vn, vc))
+    ang = -(theta - cur)
+    rv = vn * np.cos(ang) + np.cross(k, vn) * np.sin(ang) + k * np.dot(k, vn) * (1 - np.cos(ang))
+    return ca + rv / np.linalg.norm(rv) * l_n_ca, ca, C_INIT.copy()
+
+
+def nerf(geo: dict) -> np.ndarray:
+    """Tokenizer.geo_nerf(geo).cartesian_coords (3r - 1 bonds -> 3r atoms)."""
+    r = len(geo["N:CA"])
+    out = list(start(geo["CA:C"][0], geo["N:CA"][0], geo["tau"][0]))
+    for i in range(r - 1):
+        out.append(place(out[-3], out[-2], out[-1], geo["CA:C:1N"][i], geo["0C:1N"][i], geo["psi"][i]))
+        out.append(place(out[-3], out[-2], out[-1], geo["C:1N:1CA"][i], geo["N:CA"][i + 1], geo["omega"][i]))
+        out.append(place(out[-3], out[-2], out[-1], geo["tau"][i + 1], geo["CA:C"][i + 1], geo["phi"][i]))
+    return np.array(out)

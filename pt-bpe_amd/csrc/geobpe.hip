@@ -1293,6 +1293,36 @@ int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const dou
   return rc;
 }
 
+int geobpe_nerf(int device, int64_t n_spans, const int64_t* h_res_off, const double* h_geo, double* h_xyz) {
+  if (n_spans < 0 || !h_res_off) return GEOBPE_EARG;
+  const int64_t R = h_res_off[n_spans];
+  if (R == 0) return 0;
+  if (!h_geo || !h_xyz) return GEOBPE_EARG;
+  if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GEOBPE_EHIP;
+  int64_t* d_off = nullptr;
+  double *d_geo = nullptr, *d_out = nullptr;
+  int rc = 0;
+  if (hipMalloc(&d_off, (n_spans + 1) * 8) != hipSuccess || hipMalloc(&d_geo, R * 9 * 8) != hipSuccess ||
+      hipMalloc(&d_out, R * 9 * 8) != hipSuccess) {
+    rc = GEOBPE_EHIP;
+  } else {
+    hipMemcpyAsync(d_off, h_res_off, (n_spans + 1) * 8, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_geo, h_geo, R * 9 * 8, hipMemcpyHostToDevice, s);
+    hipLaunchKernelGGL(k_nerf, dim3((unsigned)((n_spans + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, n_spans,
+                       (const int64_t*)d_off, (const double*)d_geo, d_out);
+    if (hipGetLastError() != hipSuccess) rc = GEOBPE_EHIP;
+    if (!rc && hipMemcpyAsync(h_xyz, d_out, R * 9 * 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = GEOBPE_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess) rc = GEOBPE_EHIP;
+  }
+  hipFree(d_off);
+  hipFree(d_geo);
+  hipFree(d_out);
+  hipStreamDestroy(s);
+  return rc;
+}
+
 int geobpe_set_record_events(geobpe_ctx* c, int on) {
   if (!c) return GEOBPE_EARG;
   HIPCHK(c, hipSetDevice(c->device));

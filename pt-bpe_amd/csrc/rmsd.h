@@ -18,10 +18,6 @@
 
 namespace gb {
 
-struct M3 {
-  double a[3][3];
-};
-
 __device__ inline void jacobi3(double A[3][3], double V[3][3]) {
   for (int i = 0; i < 3; i++)
     for (int j = 0; j < 3; j++) V[i][j] = i == j ? 1.0 : 0.0;
@@ -167,6 +163,93 @@ __global__ __launch_bounds__(BLOCK) void k_rmsd_pairs(const double* A, const dou
   const double r = sqrt(ss / L);
   out[t] = r;
   if (symmetric && j != i) out[(int64_t)j * nb + i] = r;
+}
+
+}  // namespace gb
+
+namespace gb {
+
+// ------------------------------------------------------------------ NeRF
+// Token coordinates from internal coordinates (Tokenizer.compute_coords ->
+// Tokenizer.geo_nerf, tokenizer.py:317-363; NERFBuilder.cartesian_coords and
+// place_dihedral, nerf.py:85-211; the first residue by update_backbone_positions,
+// angles_and_coords.py:238-316).  One thread per span (a span = whole residues,
+// 3r - 1 bonds).  geo: 9 float64 per residue k of a span,
+//   {N:CA_k, CA:C_k, tau_k, 0C:1N_k, CA:C:1N_k, C:1N:1CA_k, psi_k, omega_k, phi_k}
+// (the last six are the junction to residue k + 1, unused for the span's last
+// residue); out: N, CA, C of every residue (9 float64).
+__device__ inline V3 v_unit(V3 a) { return v_scale(a, 1.0 / v_norm(a)); }
+__device__ inline V3 v_add(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+
+__device__ inline V3 place_dihedral(V3 a, V3 b, V3 c, double angle, double len, double torsion) {
+  const V3 ab = v_sub(b, a);
+  const V3 bc = v_unit(v_sub(c, b));
+  const V3 n = v_unit(v_cross(ab, bc));
+  const V3 nbc = v_cross(n, bc);
+  const double d0 = -len * cos(angle), d1 = len * cos(torsion) * sin(angle), d2 = len * sin(torsion) * sin(angle);
+  // m = [bc | nbc | n] (columns), m . d + c
+  return {bc.x * d0 + nbc.x * d1 + n.x * d2 + c.x, bc.y * d0 + nbc.y * d1 + n.y * d2 + c.y,
+          bc.z * d0 + nbc.z * d1 + n.z * d2 + c.z};
+}
+
+// Rodrigues: v cos + (k x v) sin + k (k . v)(1 - cos)
+__device__ inline V3 rotate_vec(V3 v, V3 k, double ang) {
+  const double c = cos(ang), s = sin(ang);
+  const V3 kv = v_cross(k, v);
+  const double kd = v_dot(k, v) * (1.0 - c);
+  return {v.x * c + kv.x * s + k.x * kd, v.y * c + kv.y * s + k.y * kd, v.z * c + kv.z * s + k.z * kd};
+}
+
+// the first residue: C fixed, CA on the C->CA line at L_CA_C, N rotated in the
+// N-CA-C plane to the angle theta and rescaled to L_N_CA
+__device__ inline void backbone_start(double l_ca_c, double l_n_ca, double theta, V3& N, V3& CA, V3& C) {
+  const V3 n0 = {17.047, 14.099, 3.625}, ca0 = {16.967, 12.784, 4.338}, c0 = {15.685, 12.755, 5.133};  // nerf.py N/CA/C_INIT (1CRN)
+  const V3 v = v_unit(v_sub(ca0, c0));
+  CA = v_add(c0, v_scale(v, l_ca_c));
+  const V3 vn = v_sub(n0, CA), vc = v_sub(c0, CA);
+  double ct = v_dot(vn, vc) / (v_norm(vn) * v_norm(vc));
+  ct = fmin(fmax(ct, -1.0), 1.0);
+  const double dtheta = theta - acos(ct);
+  const V3 axis = v_unit(v_cross(vn, vc));
+  V3 r = rotate_vec(vn, axis, -dtheta);
+  r = v_scale(r, l_n_ca / v_norm(r));
+  N = v_add(CA, r);
+  C = c0;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_nerf(int64_t n_spans, const int64_t* res_off, const double* geo,
+                                                double* out) {
+  const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n_spans) return;
+  const int64_t a = res_off[s], r = res_off[s + 1] - a;
+  if (r <= 0) return;
+  const double* g = geo + 9 * a;
+  double* o = out + 9 * a;
+  V3 p3, p2, p1;  // the last three atoms placed: ..., p3, p2, p1
+  backbone_start(g[1], g[0], g[2], p3, p2, p1);
+  auto put = [&](int64_t atom, V3 v) {
+    o[3 * atom] = v.x;
+    o[3 * atom + 1] = v.y;
+    o[3 * atom + 2] = v.z;
+  };
+  put(0, p3);
+  put(1, p2);
+  put(2, p1);
+  for (int64_t k = 0; k + 1 < r; k++) {
+    const double* gk = g + 9 * k;
+    const double* gn = g + 9 * (k + 1);
+    // (C, N): CA:C:1N_k, 0C:1N_k, psi_k; (N, CA): C:1N:1CA_k, N:CA_{k+1}, omega_k;
+    // (CA, C): tau_{k+1}, CA:C_{k+1}, phi_k
+    const V3 nN = place_dihedral(p3, p2, p1, gk[4], gk[3], gk[6]);
+    const V3 nCA = place_dihedral(p2, p1, nN, gk[5], gn[0], gk[7]);
+    const V3 nC = place_dihedral(p1, nN, nCA, gn[2], gn[1], gk[8]);
+    put(3 * (k + 1), nN);
+    put(3 * (k + 1) + 1, nCA);
+    put(3 * (k + 1) + 2, nC);
+    p3 = nN;
+    p2 = nCA;
+    p1 = nC;
+  }
 }
 
 }  // namespace gb

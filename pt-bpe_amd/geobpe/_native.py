@@ -95,6 +95,7 @@ def lib():
         "geobpe_pdb_error": (ctypes.c_char_p, []),
         "geobpe_featurize": (ctypes.c_int, [ctypes.c_int, I64, P, P, P]),
         "geobpe_events": (I64, [P, P, P, P]),
+        "geobpe_nerf": (ctypes.c_int, [ctypes.c_int, I64, P, P, P]),
         "geobpe_rmsd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P, P,
                                        ctypes.c_int, P]),
     }
@@ -117,7 +118,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",
     "geobpe_delta_export_async", "geobpe_delta_import_async", "geobpe_pipeline_begin", "geobpe_pipeline_iter",
     "geobpe_pipeline_import", "geobpe_pipeline_poll", "geobpe_pipeline_resolve", "geobpe_pipeline_end", "geobpe_pdb_backbone", "geobpe_pdb_error",
-    "geobpe_featurize", "geobpe_rmsd",
+    "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf",
 ]
 
 

@@ -10,6 +10,8 @@ occurrence to its nearest medoid:
   algo.k_medoids(strucs, k, ..., rng)         k_medoids(...)        (same rng draws)
   nearest medoid per occurrence               assign(coords, medoids)
     bpe.py:645-657, 1764-1777
+  Tokenizer.compute_coords(index, length)     compute_coords(cols, spans)  (device NeRF)
+    tokenizer.py:347-363, nerf.py:85-211
 
 The distances come from ``geobpe_rmsd`` (csrc/rmsd.h: one thread per pair,
 float64, Jacobi SVD of the 3x3 covariance, explicit residuals); the k-medoids
@@ -106,3 +108,82 @@ def assign(coords, medoid_coords, device: int = 0) -> np.ndarray:
     """Nearest medoid of every occurrence: argmin_j compute_rmsd(coords_i, medoid_j)
     (bpe.py:645-657, 1764-1777: P = the occurrence, Q = the medoid)."""
     return np.argmin(rmsd_cross(coords, medoid_coords, device=device), axis=1)
+
+
+# ---------------------------------------------------------------- coordinates (NeRF)
+BOND_TYPES = ["N:CA", "CA:C", "0C:1N"]        # tokenizer.py:19-22
+BOND_ANGLES = ["tau", "CA:C:1N", "C:1N:1CA"]
+DIHEDRALS = ["psi", "omega", "phi"]
+N_INIT = np.array([17.047, 14.099, 3.625])     # nerf.py:21-23 (1CRN)
+CA_INIT = np.array([16.967, 12.784, 4.338])
+C_INIT = np.array([15.685, 12.755, 5.133])
+
+
+def init_geometry():
+    """(N-CA, CA-C, N-CA-C angle) of the initial residue (Tokenizer._init_coords,
+    tokenizer.py:74-77)."""
+    a, b = N_INIT - CA_INIT, C_INIT - CA_INIT
+    ang = float(np.arccos(np.clip(np.dot(a / np.linalg.norm(a), b / np.linalg.norm(b)), -1.0, 1.0)))
+    return float(np.linalg.norm(N_INIT - CA_INIT)), float(np.linalg.norm(CA_INIT - C_INIT)), ang
+
+
+def token_geo(cols: dict, idx: int, l: int, init=None) -> dict:
+    """Tokenizer.token_geo(idx, l) (tokenizer.py:131-202) of one chain given its
+    nine columns: bond b -> init N:CA / CA:C for b = 0, 1, else column
+    BOND_TYPES[b % 3] row (b - 2) // 3; angle a -> init tau for a = 0, else
+    BOND_ANGLES[a % 3] row (a - 1) // 3; dihedral d -> DIHEDRALS[d % 3] row (d + 1) // 3."""
+    n_ca, ca_c, tau0 = init if init is not None else init_geometry()
+    out = {}
+    for j in range(idx, idx + l):
+        v = n_ca if j == 0 else (ca_c if j == 1 else float(cols[BOND_TYPES[j % 3]][(j - 2) // 3]))
+        out.setdefault(BOND_TYPES[j % 3], []).append(v)
+    for j in range(idx, idx + l - 1):
+        v = tau0 if j == 0 else float(cols[BOND_ANGLES[j % 3]][(j - 1) // 3])
+        out.setdefault(BOND_ANGLES[j % 3], []).append(v)
+    for j in range(idx, idx + l - 2):
+        out.setdefault(DIHEDRALS[j % 3], []).append(float(cols[DIHEDRALS[j % 3]][(j + 1) // 3]))
+    return out
+
+
+def geo_coords(geos, device: int = 0):
+    """Tokenizer.geo_nerf(geo).cartesian_coords for a batch of whole-residue geometry
+    dicts (3r - 1 bonds each), on the device (csrc/rmsd.h k_nerf): [(3r, 3)]."""
+    L = _native.lib()
+    rs = []
+    for g in geos:
+        nb = sum(len(g.get(k, [])) for k in BOND_TYPES)
+        if nb % 3 != 2:
+            raise ValueError(f"geo_nerf needs 3r - 1 bonds, got {nb}")
+        rs.append((nb + 1) // 3)
+    off = np.zeros(len(geos) + 1, dtype=np.int64)
+    np.cumsum(rs, out=off[1:])
+    R = int(off[-1])
+    packed = np.zeros((max(R, 1), 9), dtype=np.float64)
+    for g, a, r in zip(geos, off[:-1], rs):
+        blk = packed[a:a + r]
+        blk[:, 0], blk[:, 1], blk[:, 2] = g["N:CA"], g["CA:C"], g["tau"]
+        if r > 1:
+            for c, k in enumerate(["0C:1N", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"], start=3):
+                blk[:r - 1, c] = g[k]
+    xyz = np.empty((max(R, 1), 3, 3), dtype=np.float64)
+    if R:
+        rc = L.geobpe_nerf(int(device), len(geos), off.ctypes.data_as(ctypes.c_void_p),
+                           packed.ctypes.data_as(ctypes.c_void_p), xyz.ctypes.data_as(ctypes.c_void_p))
+        if rc:
+            raise _native.GeoBPEError(f"geobpe_nerf failed (code {rc})")
+    return [xyz[a:a + r].reshape(3 * r, 3) for a, r in zip(off[:-1], rs)]
+
+
+def compute_coords(cols: dict, spans, init=None, device: int = 0):
+    """Tokenizer.compute_coords(index, length) (tokenizer.py:347-363) of one chain for
+    every (index, length) in spans: the geometry rounded out to whole residues, NeRF,
+    then the requested atoms."""
+    n = len(cols["phi"])
+    geos, cuts = [], []
+    for index, length in spans:
+        length = min(length, 3 * n - 1 - index)
+        start = 3 * (index // 3)
+        end = 3 * (((index + length - 1) + 1) // 3) + 1
+        geos.append(token_geo(cols, start, end - start + 1, init))
+        cuts.append((index - start, end - (index + length - 1)))
+    return [c[a:len(c) - b] for c, (a, b) in zip(geo_coords(geos, device=device), cuts)]

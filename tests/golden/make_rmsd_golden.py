@@ -10,6 +10,10 @@ Writes ``tests/golden/rmsd_ref.npz``:
   medoids_ref (5,)    algo.k_medoids(A, 5, rng=default_rng(3))
   A3 (30, 3, 3), D3_ref, medoids3_ref (4,)   three-atom structures (one residue's
                       N, CA, C), k = 4, rng=default_rng(5)
+  nerf_*              Tokenizer.compute_coords(index, length) (tokenizer.py:347-363,
+                      NeRF) of spans of five synthetic chains (1..30 residues):
+                      the chains' nine columns + row_off, spans (chain, index,
+                      length), the coordinates concatenated + their offsets
 Usage:  python tests/golden/make_rmsd_golden.py
 """
 from __future__ import annotations
@@ -45,6 +49,36 @@ def rotation(rng):
                      [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
 
 
+def nerf_fixture() -> dict:
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(HERE)), "pt-bpe_amd"))
+    sys.path.insert(0, HERE)
+    import make_golden
+    from geobpe import synth
+    make_golden._stub_optional_deps()
+    from foldingdiff.tokenizer import Tokenizer
+
+    lengths = np.array([1, 2, 7, 15, 30])
+    corpus = synth.make_corpus(lengths, seed=12)
+    spans, coords, coff = [], [], [0]
+    for ci, row in enumerate(synth.corpus_rows(corpus)):
+        n = len(row["phi"])
+        s = Tokenizer.init_structure(n)
+        for c in synth.COLUMNS:
+            s["angles"][c] = row[c].astype(np.float64)
+        s["fname"] = f"synthetic_{ci}"
+        t = Tokenizer(s)
+        cand = [(0, 3 * n - 1), (0, 3), (0, 2), (3, 6), (3 * (n - 1), 2), (3, 3 * (n - 2)), (6, 9), (4, 5)]
+        for index, length in cand:
+            if index < 0 or length <= 0 or index + length > 3 * n - 1:
+                continue
+            xyz = np.asarray(t.compute_coords(index, length), dtype=np.float64)
+            spans.append((ci, index, length))
+            coords.append(xyz)
+            coff.append(coff[-1] + len(xyz))
+    return {**{f"nerf_{k}": v for k, v in corpus.items()}, "nerf_spans": np.array(spans, dtype=np.int64),
+            "nerf_coords": np.concatenate(coords), "nerf_coff": np.array(coff, dtype=np.int64)}
+
+
 def main():
     sys.path.insert(0, "/root/reference")
     from foldingdiff import algo
@@ -75,9 +109,10 @@ def main():
     with redirect_stdout(io.StringIO()):
         med = algo.k_medoids(list(A), 5, rng=np.random.default_rng(3))
         med3 = algo.k_medoids(list(A3), 4, rng=np.random.default_rng(5))
+    nerf = nerf_fixture()
     np.savez_compressed(os.path.join(HERE, "rmsd_ref.npz"), A=A, B=B, D_ref=D_ref, cross_ref=cross_ref,
                         medoids_ref=np.array(med, dtype=np.int64), A3=A3, D3_ref=D3_ref,
-                        medoids3_ref=np.array(med3, dtype=np.int64))
+                        medoids3_ref=np.array(med3, dtype=np.int64), **nerf)
     print("medoids", list(map(int, med)), "medoids3", list(map(int, med3)))
 
 

@@ -76,3 +76,68 @@ def test_device_rmsd_at_max_num_strucs():
     X = rmsd.rmsd_cross(S[:20], S[:20] @ Rz.T + 3.0)
     assert np.all(np.abs(np.diag(X)) < 1e-9)
     assert np.max(np.abs(X - D[:20, :20].astype(np.float64))) <= TOL32 * 10
+
+
+def _nerf_cases(ref):
+    from geobpe.synth import COLUMNS
+    ro = ref["nerf_row_off"]
+    chains = [{c: ref[f"nerf_{c}"][ro[i]:ro[i + 1]] for c in COLUMNS} for i in range(len(ro) - 1)]
+    want = [ref["nerf_coords"][a:b] for a, b in zip(ref["nerf_coff"][:-1], ref["nerf_coff"][1:])]
+    return chains, ref["nerf_spans"], want
+
+
+def test_oracle_nerf_matches_reference(ref):
+    """The numpy NeRF restatement on token_geo spans equals the reference's
+    Tokenizer.compute_coords (tokenizer.py:347-363) to 1e-9."""
+    from geobpe.rmsd import token_geo
+    from oracle import rmsd as orm
+    chains, spans, want = _nerf_cases(ref)
+    for (ci, index, length), w in zip(spans, want):
+        cols = chains[ci]
+        n = len(cols["phi"])
+        length = min(int(length), 3 * n - 1 - int(index))
+        start = 3 * (int(index) // 3)
+        end = 3 * (((int(index) + length - 1) + 1) // 3) + 1
+        c = orm.nerf(token_geo(cols, start, end - start + 1))
+        c = c[int(index) - start: len(c) - (end - (int(index) + length - 1))]
+        assert c.shape == w.shape and np.max(np.abs(c - w)) <= TOL64
+
+
+@pytest.mark.gpu
+def test_device_nerf_matches_reference(ref):
+    """geobpe.rmsd.compute_coords (device k_nerf) equals the reference's
+    Tokenizer.compute_coords for whole chains, single residues, the 2-bond last
+    residue and spans that start or end inside a residue."""
+    from geobpe import rmsd
+    chains, spans, want = _nerf_cases(ref)
+    for ci in range(len(chains)):
+        sel = [k for k in range(len(spans)) if spans[k][0] == ci]
+        got = rmsd.compute_coords(chains[ci], [(int(spans[k][1]), int(spans[k][2])) for k in sel])
+        for k, g in zip(sel, got):
+            assert g.shape == want[k].shape and np.max(np.abs(g - want[k])) <= TOL64
+
+
+@pytest.mark.gpu
+def test_device_nerf_featurize_round_trip():
+    """NeRF then featurisation (csrc/featurize.h) recovers the internal coordinates:
+    the device's two geometry directions are inverse to each other on 2000 chains."""
+    from geobpe import pdb, rmsd, synth
+    corpus = synth.make_corpus(synth.make_lengths(2000, 5, 80, seed=13), seed=13)
+    ro = corpus["row_off"]
+    geos = []
+    for i in range(len(ro) - 1):
+        cols = {c: corpus[c][ro[i]:ro[i + 1]] for c in synth.COLUMNS}
+        n = ro[i + 1] - ro[i]
+        g = rmsd.token_geo(cols, 0, 3 * n - 1)
+        g["N:CA"] = [1.46] * n  # featurisation measures the placed bonds; init bonds are the first residue's
+        g["CA:C"] = [1.54] * n
+        geos.append(g)
+    xyz = rmsd.geo_coords(geos)
+    feat = pdb.featurize([x.reshape(-1, 3, 3) for x in xyz])
+    for i in range(0, len(ro) - 1, 97):
+        a, b = ro[i], ro[i + 1]
+        for c in ("phi", "psi", "omega", "CA:C:1N", "C:1N:1CA"):
+            v, w = feat[c][feat["row_off"][i]:feat["row_off"][i + 1]], corpus[c][a:b]
+            m = ~np.isnan(w)
+            d = np.angle(np.exp(1j * (v[m] - w[m])))
+            assert np.max(np.abs(d)) < 1e-9, c
