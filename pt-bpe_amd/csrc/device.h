@@ -170,8 +170,6 @@ struct Dev {
   int64_t ovf_cap;
   // argmax
   int32_t* clist;  // hot list (capacity KCAP)
-  int32_t* cand;   // tied keys of the current maximum
-  int64_t candcap;
   LogRec* log;
   State* st;
   Sel* sel;  // [2], by launch parity

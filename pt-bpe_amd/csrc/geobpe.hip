@@ -237,8 +237,7 @@ int alloc_keys(geobpe_ctx* c) {
         (rc = dalloc(c, &D.touched, D.KCAP)))
       return rc;
   }
-  D.candcap = 1 << 20;
-  if ((rc = dalloc(c, &D.clist, D.KCAP)) || (rc = dalloc(c, &D.cand, D.candcap))) return rc;
+  if ((rc = dalloc(c, &D.clist, D.KCAP))) return rc;
   c->keys_ready = true;
   return 0;
 }
