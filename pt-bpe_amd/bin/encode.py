@@ -84,6 +84,8 @@ def parse_args(argv=None):
     p.add_argument("--run-chunk", type=int, default=0, help="merges per device call (0: = save-every)")
     p.add_argument("--device", type=int, default=0)
     p.add_argument("--ckpt-format", choices=["pkl", "json"], default="pkl")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="under torchrun (WORLD_SIZE > 1): rows sharded over the ranks, RCCL by default")
     return p.parse_args(argv)
 
 
@@ -105,14 +107,19 @@ def load_corpus(spec: str, toy: int = 0) -> dict:
     return corpus
 
 
-def stats(bpe) -> dict:
+def stats(bpe):
+    """The stats json (encode.py:364,417); multi-GPU: None on ranks other than 0."""
     from geobpe.bpe import get_codebook_utility
-    ids, off = bpe.encode_all()
+    enc = bpe.encode_all()
+    cap = bpe.capacity(tokenizer=True)
+    if enc is None:
+        return None
+    ids, off = enc
     ntok = (np.diff(off) + 3) // 4
     N = len(ntok)
     L = float(np.mean(ntok)) if N else 0.0
     K = len(bpe._tokens)
-    return {"K": K, "L": L, "bpr": bpe.capacity(tokenizer=True) / (N * L) if N else 0.0} | \
+    return {"K": K, "L": L, "bpr": cap / (N * L) if N else 0.0} | \
         get_codebook_utility(ids, bpe.vocab_size)
 
 
@@ -150,7 +157,7 @@ def main(argv=None) -> int:
         args.save_dir = os.path.join(args.base_dir, "ckpts", str(time.time()))
     os.makedirs(args.save_dir, exist_ok=True)
     args_path = os.path.join(args.save_dir, "args.txt")
-    skip = {"auto", "save_dir", "max_iter", "run_chunk", "device", "ckpt_format"}
+    skip = {"auto", "save_dir", "max_iter", "run_chunk", "device", "ckpt_format", "dist_backend"}
     if os.path.exists(args_path):  # validate_args_match (utils.py)
         with open(args_path) as f:
             loaded = dict(line.rstrip("\n").split(": ", 1) for line in f if ": " in line)
@@ -168,14 +175,33 @@ def main(argv=None) -> int:
 
     from geobpe.bpe import BPE
     corpus = load_corpus(args.data_dir, args.toy)
-    bpe = BPE(corpus, bins=args.bins, bin_strategy=args.bin_strategy, save_dir=args.save_dir,
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    group, rank, shard, device = None, 0, corpus, args.device
+    if world > 1:  # one process per GPU (torchrun): contiguous row blocks, deltas exchanged per merge
+        import torch
+        import torch.distributed as dist
+        from geobpe.dist import TorchGroup, shard_rows, slice_corpus
+        rank = int(os.environ["RANK"])
+        device = int(os.environ.get("LOCAL_RANK", "0")) if args.dist_backend == "nccl" else args.device
+        torch.cuda.set_device(device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
+        lo, hi = shard_rows(corpus["row_off"], world)[rank]
+        shard = slice_corpus({k: v for k, v in corpus.items() if k != "fnames"}, lo, hi)
+        group = TorchGroup(int(shard["row_off"][-1]), device=device)
+    bpe = BPE(shard, bins=args.bins, bin_strategy=args.bin_strategy, save_dir=args.save_dir,
               res_init=args.res_init, std_bonds=not args.free_bonds,
               rmsd_partition_min_size=args.p_min_size, glue_opt=args.glue_opt, seed=args.seed,
-              device=args.device, record_tree=args.ckpt_format == "pkl")
+              device=device, record_tree=args.ckpt_format == "pkl", group=group,
+              global_corpus=corpus if group is not None else None)
     t0 = time.time()
     bpe.initialize()
-    with open(os.path.join(args.save_dir, "initial_stats=-1.json"), "w") as f:
-        json.dump(stats(bpe), f)
+    st = stats(bpe)  # (every rank takes part in the gather; rank 0 writes)
+    if rank == 0:
+        with open(os.path.join(args.save_dir, "initial_stats=-1.json"), "w") as f:
+            json.dump(st, f)
     bpe.bin()
     log.info("initialize+bin %.3fs", time.time() - t0)
 
@@ -198,11 +224,13 @@ def main(argv=None) -> int:
             break
         t = nxt
         if t % args.save_every == 0:
-            with open(os.path.join(args.save_dir, f"stats={t}.json"), "w") as f:
-                json.dump(stats(bpe), f)
+            st = stats(bpe)
+            if rank == 0:
+                with open(os.path.join(args.save_dir, f"stats={t}.json"), "w") as f:
+                    json.dump(st, f)
             if args.ckpt_format == "pkl":
                 bpe.save_checkpoint(os.path.join(args.save_dir, f"bpe_iter={t}.pkl"))
-            else:
+            elif rank == 0:
                 tmp = os.path.join(args.save_dir, f".bpe_iter={t}.json.tmp")
                 with open(tmp, "w") as f:
                     json.dump({"iter": t, "merges": [list(m) for m in bpe.merges],
@@ -210,9 +238,14 @@ def main(argv=None) -> int:
                 os.replace(tmp, os.path.join(args.save_dir, f"bpe_iter={t}.json"))
         t += 1
     log.info("done: %d merges, vocab_size %d", bpe._step, bpe.vocab_size)
-    print(json.dumps({"merges": bpe._step, "vocab_size": bpe.vocab_size,
-                      "seconds": time.time() - t0}))
+    if rank == 0:
+        print(json.dumps({"merges": bpe._step, "vocab_size": bpe.vocab_size, "ranks": world,
+                          "seconds": time.time() - t0}))
     bpe.close()
+    if group is not None:
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
     return 0
 
 

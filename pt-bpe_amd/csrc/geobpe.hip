@@ -834,7 +834,6 @@ int geobpe_delta_export_async(geobpe_ctx* c, void* d_out, int64_t cap, void* d_c
 int geobpe_pipeline_begin(geobpe_ctx* c) {
   if (!c || !c->distributed || !c->keys_ready) return GEOBPE_EARG;
   if (c->mark_pending) return fail(c, GEOBPE_EARG, "pipeline_begin between step_select and step_apply");
-  if (c->ev) return fail(c, GEOBPE_EARG, "pipelined exchange with merge-event recording");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
   if ((rc = sync_state(c))) return rc;
@@ -861,6 +860,8 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     Timed t(c, "apply");
     hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
   }
+  if (c->ev)
+    hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
   {
     Timed t(c, "export");
     DeltaRec* out = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header

@@ -1610,6 +1610,10 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta, int par) 
 __global__ __launch_bounds__(BLOCK) void k_events(Dev D, int par, int4* ev, int64_t cap, unsigned long long* ev_n) {
   __shared__ int32_t s_off[RPB + 1];
   __shared__ int64_t s_base;
+  if (par < 0) {  // pipelined exchange (k_select set dgen)
+    if (D.st->stall) return;
+    par = D.st->dgen & 1;
+  }
   const Sel sel = D.sel[par];
   if (sel.decision != SEL_MERGE) return;
   const int64_t novf = min(D.st->L_ovf2[par], D.Lovf_cap);

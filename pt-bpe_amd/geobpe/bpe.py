@@ -175,7 +175,11 @@ class BPE:
                  rmsd_partition_min_size=4, rmsd_super_res=False, rmsd_only=False, num_partitions=3,
                  max_num_strucs=500, glue_opt=False, glue_opt_prior=0.0, glue_opt_every=10,
                  glue_opt_method="all", seed=None, device: int = 0, max_vocab: int = 1 << 20, group=None,
-                 record_tree: bool = True):
+                 record_tree: bool = True, global_corpus=None):
+        """``group`` (geobpe.dist.TorchGroup): this process holds one row shard
+        (``structures``) of a multi-GPU run; ``global_corpus`` (the whole corpus,
+        needed on rank 0 for checkpoints) -- encode_all / capacity / checkpoints
+        then gather every rank's chains to rank 0 (None on the other ranks)."""
         _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_size, glue_opt, compute_sec_structs)
         if isinstance(structures, dict) and "row_off" in structures:
             corpus = structures
@@ -212,7 +216,9 @@ class BPE:
         self._engine = GeoBPEEngine(corpus, self.B, device=device, max_vocab=max_vocab, group=group,
                                     strategy=bin_strategy)
         self._tok_cache = None
-        self._record_tree = bool(record_tree) and group is None
+        self._record_tree = bool(record_tree)
+        self._group = group
+        self._global_corpus = global_corpus
 
     # ------------------------------------------------------------ BPE.initialize
     def initialize(self, path=None):
@@ -244,10 +250,11 @@ class BPE:
         """np.histogram counts per grid-1 type (bpe.py:864-866), computed on demand."""
         out = ThresholdDict()
         counts = {}
-        ro = self._corpus["row_off"]
+        corpus = self._global_corpus if self._global_corpus is not None else self._corpus
+        ro = corpus["row_off"]
         from .engine import init_bond_angle
         for key in ANGLE_TYPES:
-            col = np.asarray(self._corpus[key])
+            col = np.asarray(corpus[key])
             vals = col[np.nan_to_num(col, nan=0.0) != 0.0]
             if key == "tau":
                 vals = np.concatenate([vals, np.full(len(ro) - 1, init_bond_angle())])
@@ -325,9 +332,34 @@ class BPE:
             self._tok_cache = (toks, enc, eoff)
         return self._tok_cache[0]
 
+    def _gather(self, part: dict):
+        """Every rank's ``part`` on rank 0 (rank order), None elsewhere; [part] alone."""
+        g = self._group
+        if g is None:
+            return [part]
+        parts = [None] * g.world_size if g.rank == 0 else None
+        g.dist.gather_object(part, parts, dst=0, group=g.pg)
+        return parts
+
+    @staticmethod
+    def _cat_offsets(offs):
+        out = [np.zeros(1, dtype=np.int64)]
+        base = 0
+        for o in offs:
+            out.append(np.asarray(o[1:], dtype=np.int64) + base)
+            base += int(o[-1])
+        return np.concatenate(out)
+
     def encode_all(self):
-        """quantize(tokenize()) of every chain as (ids, row offsets), one device pass."""
-        return self._engine.encode()
+        """quantize(tokenize()) of every chain as (ids, row offsets), one device pass
+        (multi-GPU: every rank's chains in global order on rank 0, None elsewhere)."""
+        ids, off = self._engine.encode()
+        if self._group is None:
+            return ids, off
+        parts = self._gather({"ids": ids, "off": off})
+        if parts is None:
+            return None
+        return np.concatenate([p["ids"] for p in parts]), self._cat_offsets([p["off"] for p in parts])
 
     def quantize(self, tokenized):
         """bpe.py:918-956: a Tokenizer, a list of Tokenizers (one device encode
@@ -400,7 +432,10 @@ class BPE:
         if tokenizer:
             mbits = np.log2(len(self._tokens))
             bbits = np.log2(self.bins[1])
-            _, eoff = self._engine.encode()
+            enc = self.encode_all()
+            if enc is None:  # multi-GPU: rank 0 answers
+                return None
+            eoff = enc[1]
             for L in np.diff(eoff):
                 m = (int(L) + 3) // 4
                 total += mbits * m
@@ -415,9 +450,29 @@ class BPE:
         e = self._engine
         start, ids, off = e.segmentation()
         a, b, eoff = e.events()
-        ro = self._corpus["row_off"]
+        corpus, fnames = self._corpus, self._fnames
+        if self._group is not None:  # every rank's chains and merge events, in global order, on rank 0
+            parts = self._gather({"start": start, "ids": ids, "off": off, "a": a, "b": b, "eoff": eoff,
+                                  "base": self._group.residue_base})
+            if parts is None:
+                return None
+            if self._global_corpus is None:
+                raise RuntimeError("multi-GPU checkpoints need global_corpus on rank 0")
+            start = np.concatenate([p["start"] for p in parts])
+            ids = np.concatenate([p["ids"] for p in parts])
+            off = self._cat_offsets([p["off"] for p in parts])
+            M = len(parts[0]["eoff"]) - 1
+            t = np.concatenate([np.repeat(np.arange(M), np.diff(p["eoff"])) for p in parts])
+            ga = np.concatenate([np.asarray(p["a"], np.int64) + p["base"] for p in parts])
+            gb_ = np.concatenate([np.asarray(p["b"], np.int64) + p["base"] for p in parts])
+            order = np.argsort(t, kind="stable")  # rank order (= ascending slot) within a merge
+            a, b = ga[order], gb_[order]
+            eoff = np.searchsorted(t[order], np.arange(M + 1), side="left").astype(np.int64)
+            corpus = self._global_corpus
+            fnames = list(corpus["fnames"]) if corpus.get("fnames") is not None else None
+        ro = corpus["row_off"]
         return {
-            "corpus": self._corpus, "fnames": self._fnames or [None] * (len(ro) - 1),
+            "corpus": corpus, "fnames": fnames or [None] * (len(ro) - 1),
             "B": self.B, "bins": dict(self.bins), "bin_strategy": self.bin_strategy,
             "thresholds": {k: list(v) for k, v in self._thresholds[1].items()},
             "bin_counts": self._bin_counts[1], "K0": e.K0, "tokens": dict(self._tokens),
@@ -434,7 +489,9 @@ class BPE:
         pickle of foldingdiff.bpe.BPE that train.py / predict.py / induce.py and
         the reference's own resume load unchanged (geobpe.refpickle)."""
         from . import refpickle
-        refpickle.save(self.checkpoint_state(), path)
+        state = self.checkpoint_state()  # (multi-GPU: every rank gathers, rank 0 writes)
+        if state is not None:
+            refpickle.save(state, path)
 
     def visualize(self, key, output_path):  # plotting only in the reference (bpe.py:1583-1627)
         return None

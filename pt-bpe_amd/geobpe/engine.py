@@ -269,7 +269,7 @@ class GeoBPEEngine:
         if not self._binned:
             raise RuntimeError("bin() first")
         if self.distributed:
-            if self.pipelined and not self._events_on and hasattr(self.group, "run_pipelined"):
+            if self.pipelined and hasattr(self.group, "run_pipelined"):
                 done = self.group.run_pipelined(self, int(n_merges))
                 self._refresh_log()
                 if done < n_merges:

@@ -193,3 +193,73 @@ def test_checkpoint_from_device_matches_reference_pickle(name):
     assert b.run(d["merges"]) == d["merges"]
     check_against_digest(refpickle.build(b.checkpoint_state()), d, [k for k, _ in meta["merges"][: d["merges"]]])
     b.close()
+
+
+def _canon(x, seen=None, skip=("_times", "save_dir", "parent", "rng")):
+    """Structural form of a loaded checkpoint (refpickle records), cycles cut, timing fields dropped."""
+    import math
+    import numpy as np
+    seen = set() if seen is None else seen
+    if isinstance(x, float):
+        return "nan" if math.isnan(x) else round(x, 12)
+    if isinstance(x, (str, int, bool)) or x is None:
+        return x
+    if hasattr(x, "to_numpy") and hasattr(x, "columns"):  # a pandas frame
+        return [list(x.columns), _canon(x.to_numpy().tolist(), seen)]
+    if isinstance(x, np.ndarray):
+        return _canon(x.tolist(), seen)
+    if id(x) in seen:
+        return "<cycle>"
+    seen.add(id(x))
+    if isinstance(x, dict):
+        items = {str(k): _canon(v, seen) for k, v in x.items() if k not in skip}
+        attrs = {k: _canon(v, seen) for k, v in getattr(x, "__dict__", {}).items() if k not in skip}
+        return [type(x).__name__, sorted(items.items()), sorted(attrs.items())]
+    if isinstance(x, (list, tuple)):
+        return [_canon(v, seen) for v in x]
+    if hasattr(x, "__dict__"):
+        return [type(x).__name__, sorted((k, _canon(v, seen)) for k, v in vars(x).items() if k not in skip)]
+    return repr(x)
+
+
+@pytest.mark.gpu
+def test_cli_two_ranks_write_the_single_gpu_checkpoint(tmp_path):
+    """bin/encode.py under torchrun (2 ranks, gloo, sharing the one GPU): rows
+    sharded, deltas exchanged per merge (pipelined), stats and the merge tree
+    gathered to rank 0 -- the bpe_iter=*.pkl and stats equal the 1-GPU run's."""
+    import os
+    import socket
+    import subprocess
+    import sys
+    from geobpe import refpickle
+    cli = _encode_cli()
+    common = ["--data-dir", "synthetic:300:30:150:5", "--bins", "1-5", "--save-every", "10", "--max-iter", "31"]
+    one, two = tmp_path / "one", tmp_path / "two"
+    assert cli.main(common + ["--save-dir", str(one), "--log-dir", str(tmp_path / "l1")]) == 0
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    here = os.path.dirname(os.path.abspath(__file__))
+    enc = os.path.join(os.path.dirname(here), "pt-bpe_amd", "bin", "encode.py")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), enc] + common + \
+        ["--save-dir", str(two), "--log-dir", str(tmp_path / "l2"), "--dist-backend", "gloo"]
+    out = open(tmp_path / "ranks.out", "w")
+    p = subprocess.Popen(cmd, stdout=out, stderr=subprocess.STDOUT, start_new_session=True)
+    try:
+        rc = p.wait(timeout=150)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, 9)  # torchrun and its workers (their own session)
+        p.wait()
+        rc = None
+    out.close()
+    log = (tmp_path / "ranks.out").read_text()[-3000:]
+    elog = tmp_path / "l2" / "encode.log"
+    assert rc == 0, log + (elog.read_text()[-2000:] if elog.exists() else "")
+    for t in (10, 20, 30):
+        a = refpickle.load(str(one / f"bpe_iter={t}.pkl"))
+        b = refpickle.load(str(two / f"bpe_iter={t}.pkl"))
+        assert refpickle.merge_keys(a) == refpickle.merge_keys(b) and len(refpickle.merge_keys(a)) == t + 1
+        assert _canon(a) == _canon(b)
+        assert json.loads((one / f"stats={t}.json").read_text()) == json.loads((two / f"stats={t}.json").read_text())
