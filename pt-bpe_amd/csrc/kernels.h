@@ -633,9 +633,9 @@ __device__ inline KSeq key_seq(const Dev& D, int32_t d) {
 // is first re-measured.  Ties: the smallest reference key string
 // (bpe.py:1469-1471) via the device JSON generator.
 //
-// k_select: one workgroup of SBLOCK threads (16 waves).  Every thread keeps 4
-// list entries in flight (one round covers 4096 entries: the lists of a C3/C5
-// run hold <= ~5 k), so the scan is one or two rounds of dependent list -> count
+// k_select: one workgroup of SBLOCK threads (16 waves).  Every thread keeps
+// SEL_UNR list entries in flight (one round covers 4096 entries: the lists of a
+// C3/C5 run hold <= ~5 k), so the scan is one or two rounds of dependent list -> count
 // gathers.  The keys tied at the maximum are collected in LDS, their contents
 // staged in LDS, and a wave-per-comparison tournament (wave_key_less) picks the
 // smallest reference string.  It records the decision in Sel[par], the
@@ -646,6 +646,10 @@ __device__ inline KSeq key_seq(const Dev& D, int32_t d) {
 // long keys of late merges; a 64-workgroup scan with a last-arriver reduction
 // paid ~6 us of release/acquire fences and tickets for nothing at these lengths.)
 constexpr int SBLOCK = 1024;
+#ifndef SEL_UNR_DEF
+#define SEL_UNR_DEF 4
+#endif
+constexpr int SEL_UNR = SEL_UNR_DEF;  // list entries in flight per thread (A/B: 8 is no faster)
 constexpr int SEL_TMAX = SBLOCK;  // staged candidates
 constexpr int SEL_SYMS = 6144;    // staged content symbols (24 KB)
 
@@ -709,11 +713,11 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
   Sel* out = D.sel + par;
   const bool rec = threadIdx.x == 0;
   const int32_t act = st->cl_act;
-  // the first 4 * SBLOCK list entries are loaded with the state (clist capacity
-  // KCAP >= 4 * SBLOCK; entries past n are masked below)
-  int32_t d0[4];
+  // the first SEL_UNR * SBLOCK list entries are loaded with the state (clist
+  // capacity KCAP >= SEL_UNR * SBLOCK; entries past n are masked below)
+  int32_t d0[SEL_UNR];
 #pragma unroll
-  for (int q = 0; q < 4; q++) d0[q] = D.clist[threadIdx.x + q * SBLOCK];
+  for (int q = 0; q < SEL_UNR; q++) d0[q] = D.clist[threadIdx.x + q * SBLOCK];
   const int64_t n = st->ncl2[act];
   const int32_t th = st->theta, iter = st->iter, K = st->K;
   const bool valid = st->cl_valid != 0;
@@ -738,19 +742,19 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     }
     return;
   }
-  // ---- pass over the list: 4 entries per thread in flight; keep this thread's maximum
+  // ---- pass over the list: SEL_UNR entries per thread in flight; keep this thread's maximum
   int32_t m = 0, mkey = -1, mcnt = 0;
-  for (int64_t i0 = threadIdx.x; i0 < n; i0 += 4 * SBLOCK) {
-    int32_t d[4], c[4];
+  for (int64_t i0 = threadIdx.x; i0 < n; i0 += SEL_UNR * SBLOCK) {
+    int32_t d[SEL_UNR], c[SEL_UNR];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < SEL_UNR; q++) {
       const int64_t i = i0 + (int64_t)q * SBLOCK;
       d[q] = i < n ? (i0 < SBLOCK ? d0[q] : D.clist[i]) : -1;
     }
 #pragma unroll
-    for (int q = 0; q < 4; q++) c[q] = d[q] >= 0 ? D.count[d[q]] : 0;
+    for (int q = 0; q < SEL_UNR; q++) c[q] = d[q] >= 0 ? D.count[d[q]] : 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
+    for (int q = 0; q < SEL_UNR; q++) {
       if (c[q] > m) {
         m = c[q];
         mkey = d[q];
