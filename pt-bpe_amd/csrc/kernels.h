@@ -712,6 +712,7 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
   }
   Sel* out = D.sel + par;
   const bool rec = threadIdx.x == 0;
+  dbg_stamp(D, 20);  // (debug timeline slots 20-26: k_select phases)
   const int32_t act = st->cl_act;
   // the first SEL_UNR * SBLOCK list entries are loaded with the state (clist
   // capacity KCAP >= SEL_UNR * SBLOCK; entries past n are masked below)
@@ -765,7 +766,9 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     }
   }
   if (rec) S.nt = 0;
+  dbg_stamp(D, 21);
   const int32_t gm = block_max(m, s_red);
+  dbg_stamp(D, 22);
   const bool hot = gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th);
   if (hot && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
     if (rec) {
@@ -812,6 +815,7 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     }
   }
   __syncthreads();
+  dbg_stamp(D, 23);
   const int32_t nt = S.nt;
   const int32_t t = threadIdx.x;
   int32_t W;
@@ -842,7 +846,9 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
       }
       __syncthreads();
     }  // else: the tournament compares in global memory
+    dbg_stamp(D, 24);
     W = S.key[wave_tournament(S, nt, D.B)];
+    dbg_stamp(D, 25);
   } else {
     // more tied keys than the staging holds (runs to exhaustion): the char
     // generator over the list, 256 threads (48 chars of LDS each, in S.sym)
@@ -887,6 +893,7 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     out->wg = g;
     out->widR = Rr;
   }
+  dbg_stamp(D, 26);
 }
 
 // ====================================================================== merge-apply

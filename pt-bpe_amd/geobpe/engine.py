@@ -368,6 +368,10 @@ class GeoBPEEngine:
         pairs = np.ascontiguousarray(pairs, dtype=np.int32).reshape(-1, 2)
         out = np.zeros(len(pairs), dtype=np.int32)
         self._chk(self.L.geobpe_debug_key_less(self._ctx, _p(pairs), len(pairs), _p(out)))
+        bad = np.flatnonzero(out >= 2)  # 2: the two device comparators disagree
+        if len(bad):
+            raise _native.GeoBPEError(f"device key order inconsistent on {len(bad)} pairs, first {pairs[bad[0]]} "
+                                      f"(code {out[bad[0]]})")
         return out.astype(bool)
 
     def segmentation(self):

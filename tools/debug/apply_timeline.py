@@ -37,7 +37,9 @@ for it in iters:
     rel[t == 0] = np.nan
     last = eng.merges[-1]
     print(f"merge {it}: count {last[1]} merged {last[2]}  workgroups {len(t)}")
-    names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end", 62: "klist_end", 63: "end"}
+    names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end", 62: "klist_end", 63: "end",
+             20: "SEL.start", 21: "SEL.scanned", 22: "SEL.max", 23: "SEL.ties", 24: "SEL.staged", 25: "SEL.tourn",
+             26: "SEL.end"}
     names.update({30: "r0.kcL", 31: "r0.globalL", 32: "r0.kcR", 33: "r0.globalR"})
     for r in range(2):
         for i, nm in enumerate(["front.loads", "front.agg", "finL.kc", "finL.store", "finL.agg", "finR.kc",
