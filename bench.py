@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the multi-rank exchange (RCCL) even at world size 1: a 1-GPU rehearsal of the N>1 path")
     ap.add_argument("--cpu-budget-s", type=float, default=30.0)
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: RCCL (default); gloo puts every rank on GPU 0 (a one-GPU rehearsal of the N > 1 path)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
     ap.add_argument("--roofline-kernel", default="apply")
@@ -78,7 +80,7 @@ def main():
         args.no_profile = args.no_replay = args.no_cpu_baseline = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if args.dist_backend == "nccl" else 0
     import torch
     import torch.distributed as dist
     from geobpe import synth
@@ -92,7 +94,10 @@ def main():
             os.environ.setdefault("MASTER_PORT", "29533")
             dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", local))
         else:
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            if args.dist_backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group("gloo")
     n, lo, hi, B, merges = CONFIGS[args.config]
     t0 = time.time()
     lengths = synth.make_lengths(n, lo, hi, seed=0)
@@ -133,7 +138,7 @@ def main():
         dist.barrier()
     T = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([T], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([T], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
     live_ms, live_n = eng.kernel_ms(args.roofline_kernel) if not args.no_profile else (0.0, 0)
