@@ -27,11 +27,11 @@ for it in iters:
     buf = np.zeros(m, dtype=np.int64)
     L.geobpe_debug_timeline(eng._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p), m)
     t = buf.reshape(-1, 64)
-    t = t[t[:, 0] > 0]
+    t = t[(t > 0).any(axis=1)]
     if len(t) == 0:
         print(f"merge {it}: (rebuild iteration / no stamps)")
         continue
-    base = t[:, 0].min()
+    base = t[:, 0][t[:, 0] > 0].min()
     rel = (t - base) / 100.0  # us
     rel[:, 63][t[:, 63] == 0] = np.nan
     rel[t == 0] = np.nan
@@ -39,7 +39,7 @@ for it in iters:
     print(f"merge {it}: count {last[1]} merged {last[2]}  workgroups {len(t)}")
     names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end", 62: "klist_end", 63: "end",
              20: "SEL.start", 21: "SEL.scanned", 22: "SEL.max", 23: "SEL.ties", 24: "SEL.staged", 25: "SEL.tourn",
-             26: "SEL.end"}
+             26: "SEL.end", 10: "MARK.start", 11: "MARK.state", 12: "MARK.bucket", 13: "MARK.hits"}
     names.update({30: "r0.kcL", 31: "r0.globalL", 32: "r0.kcR", 33: "r0.globalR"})
     for r in range(2):
         for i, nm in enumerate(["front.loads", "front.agg", "finL.kc", "finL.store", "finL.agg", "finR.kc",
