@@ -45,6 +45,10 @@ for it in iters:
         for i, nm in enumerate(["front.loads", "front.agg", "finL.kc", "finL.store", "finL.agg", "finR.kc",
                                 "finR.store", "finR.agg"]):
             names[40 + 10 * r + i] = f"r{r}.{nm}"
+    if not np.all(np.isnan(rel[:, 63])):
+        order = np.argsort(-np.nan_to_num(rel[:, 63], nan=-1))[:5]
+        print("  slowest workgroups (end):", [(int(np.flatnonzero((t > 0).any(axis=1))[i]) if False else int(i),
+                                              round(float(rel[i, 63]), 1)) for i in order])
     for k in sorted(range(64), key=lambda k: np.nanmedian(rel[:, k]) if not np.all(np.isnan(rel[:, k])) else 0):
         col = rel[:, k]
         if np.all(np.isnan(col)):
