@@ -820,7 +820,7 @@ int geobpe_delta_export_async(geobpe_ctx* c, void* d_out, int64_t cap, void* d_c
   HIPCHK(c, hipSetDevice(c->device));
   hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (DeltaRec*)d_out, cap, 0,
                      (int64_t*)nullptr);
-  hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_count, cap, 0);
+  hipLaunchKernelGGL(k_export_fin, dim3(1), dim3(1), 0, c->stream, c->D, (int64_t*)d_count, cap);
   HIPCHK(c, hipGetLastError());
   return 0;
 }

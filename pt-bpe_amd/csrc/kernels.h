@@ -1696,9 +1696,8 @@ __global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int6
     out[j] = r;
   }
 }
-__global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap, int chk_stall) {
+__global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap) {
   State* st = D.st;
-  if (chk_stall && st->stall) return;
   const int64_t n = st->ntouched;
   d_count[0] = n;
   if (n > cap) set_error(D, GEOBPE_ECAPACITY, -30);
