@@ -199,7 +199,7 @@ def _canon(x, seen=None, skip=("_times", "save_dir", "parent", "rng")):
     """Structural form of a loaded checkpoint (refpickle records), cycles cut, timing fields dropped."""
     import math
     import numpy as np
-    seen = set() if seen is None else seen
+    seen = {} if seen is None else seen  # id -> object: held, so no id is reused during the walk
     if isinstance(x, float):
         return "nan" if math.isnan(x) else round(x, 12)
     if isinstance(x, (str, int, bool)) or x is None:
@@ -210,7 +210,7 @@ def _canon(x, seen=None, skip=("_times", "save_dir", "parent", "rng")):
         return _canon(x.tolist(), seen)
     if id(x) in seen:
         return "<cycle>"
-    seen.add(id(x))
+    seen[id(x)] = x
     if isinstance(x, dict):
         items = {str(k): _canon(v, seen) for k, v in x.items() if k not in skip}
         attrs = {k: _canon(v, seen) for k, v in getattr(x, "__dict__", {}).items() if k not in skip}
@@ -220,6 +220,18 @@ def _canon(x, seen=None, skip=("_times", "save_dir", "parent", "rng")):
     if hasattr(x, "__dict__"):
         return [type(x).__name__, sorted((k, _canon(v, seen)) for k, v in vars(x).items() if k not in skip)]
     return repr(x)
+
+
+def _first_diff(x, y, path="") -> str:
+    if type(x) != type(y):
+        return f"{path}: {type(x).__name__} != {type(y).__name__}"
+    if isinstance(x, (list, tuple)):
+        if len(x) != len(y):
+            return f"{path}: len {len(x)} != {len(y)}"
+        for i, (u, v) in enumerate(zip(x, y)):
+            if u != v:
+                return _first_diff(u, v, f"{path}/{u[0] if isinstance(u, tuple) and isinstance(u[0], str) else i}")
+    return f"{path}: {str(x)[:300]} != {str(y)[:300]}"
 
 
 @pytest.mark.gpu
@@ -261,5 +273,6 @@ def test_cli_two_ranks_write_the_single_gpu_checkpoint(tmp_path):
         a = refpickle.load(str(one / f"bpe_iter={t}.pkl"))
         b = refpickle.load(str(two / f"bpe_iter={t}.pkl"))
         assert refpickle.merge_keys(a) == refpickle.merge_keys(b) and len(refpickle.merge_keys(a)) == t + 1
-        assert _canon(a) == _canon(b)
+        ca, cb = _canon(a), _canon(b)
+        assert ca == cb, _first_diff(ca, cb)
         assert json.loads((one / f"stats={t}.json").read_text()) == json.loads((two / f"stats={t}.json").read_text())
