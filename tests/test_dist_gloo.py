@@ -114,7 +114,7 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise"),
-                                         (3, "mixed")])
+                                         (3, "mixed"), (4, "small-slots")])
 def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
     """The full N>1 path (TorchGroup exchange, one process per rank) with gloo on
     one device: the pipelined exchange (fixed slots, stall + full re-exchange of an
