@@ -350,6 +350,18 @@ class BPE:
             base += int(o[-1])
         return np.concatenate(out)
 
+    @staticmethod
+    def _merge_rank_events(parts):
+        """Every rank's merge events (rank-local slots, merge t's in [eoff[t],
+        eoff[t+1])) as global slots (+ the rank's residue base), merge by merge in
+        rank order -- ascending slot within a merge, as a 1-GPU run logs them."""
+        M = len(parts[0]["eoff"]) - 1
+        t = np.concatenate([np.repeat(np.arange(M), np.diff(p["eoff"])) for p in parts])
+        ga = np.concatenate([np.asarray(p["a"], np.int64) + p["base"] for p in parts])
+        gb = np.concatenate([np.asarray(p["b"], np.int64) + p["base"] for p in parts])
+        order = np.argsort(t, kind="stable")
+        return ga[order], gb[order], np.searchsorted(t[order], np.arange(M + 1), side="left").astype(np.int64)
+
     def encode_all(self):
         """quantize(tokenize()) of every chain as (ids, row offsets), one device pass
         (multi-GPU: every rank's chains in global order on rank 0, None elsewhere)."""
@@ -461,13 +473,7 @@ class BPE:
             start = np.concatenate([p["start"] for p in parts])
             ids = np.concatenate([p["ids"] for p in parts])
             off = self._cat_offsets([p["off"] for p in parts])
-            M = len(parts[0]["eoff"]) - 1
-            t = np.concatenate([np.repeat(np.arange(M), np.diff(p["eoff"])) for p in parts])
-            ga = np.concatenate([np.asarray(p["a"], np.int64) + p["base"] for p in parts])
-            gb_ = np.concatenate([np.asarray(p["b"], np.int64) + p["base"] for p in parts])
-            order = np.argsort(t, kind="stable")  # rank order (= ascending slot) within a merge
-            a, b = ga[order], gb_[order]
-            eoff = np.searchsorted(t[order], np.arange(M + 1), side="left").astype(np.int64)
+            a, b, eoff = self._merge_rank_events(parts)
             corpus = self._global_corpus
             fnames = list(corpus["fnames"]) if corpus.get("fnames") is not None else None
         ro = corpus["row_off"]

@@ -276,3 +276,18 @@ def test_cli_two_ranks_write_the_single_gpu_checkpoint(tmp_path):
         ca, cb = _canon(a), _canon(b)
         assert ca == cb, _first_diff(ca, cb)
         assert json.loads((one / f"stats={t}.json").read_text()) == json.loads((two / f"stats={t}.json").read_text())
+
+
+def test_rank_gather_helpers():
+    """Host logic of the multi-GPU checkpoint gather (no GPU): offsets concatenate,
+    and per-rank merge events interleave merge by merge in rank (= slot) order."""
+    import numpy as np
+    from geobpe.bpe import BPE
+    off = BPE._cat_offsets([np.array([0, 2, 5]), np.array([0, 1]), np.array([0, 3, 4, 6])])
+    assert off.tolist() == [0, 2, 5, 6, 9, 10, 12]
+    parts = [  # merge 0: rank 0 has slots 3, 7; rank 1 slot 2 (+ base 10); merge 1: rank 1 only
+        {"a": np.array([3, 7]), "b": np.array([4, 8]), "eoff": np.array([0, 2, 2]), "base": 0},
+        {"a": np.array([2, 5]), "b": np.array([3, 6]), "eoff": np.array([0, 1, 2]), "base": 10},
+    ]
+    a, b, eoff = BPE._merge_rank_events(parts)
+    assert a.tolist() == [3, 7, 12, 15] and b.tolist() == [4, 8, 13, 16] and eoff.tolist() == [0, 3, 4]
