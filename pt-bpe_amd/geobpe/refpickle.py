@@ -449,14 +449,24 @@ _SAFE = {
     ("pandas.core.indexes.base", "Index"), ("pandas.core.indexes.base", "_new_Index"),
     ("pandas.core.indexes.range", "RangeIndex"), ("pandas.core.internals.managers", "BlockManager"),
     ("pandas.core.internals.managers", "SingleBlockManager"),
-    ("torch._utils", "_rebuild_tensor_v2"), ("torch.storage", "_load_from_bytes"),
+    ("torch._utils", "_rebuild_tensor_v2"),
 }
+
+
+def _storage_from_bytes(b):
+    """Stand-in for ``torch.storage._load_from_bytes``: torch's own version
+    unpickles ``b`` with ``weights_only=False`` (arbitrary code); this one only
+    accepts tensor/storage payloads."""
+    import torch
+    return torch.load(io.BytesIO(b), weights_only=True)
 
 
 class _Reader(pickle.Unpickler):
     def find_class(self, module, name):
         if REF_MODULES.get(name) == module:
             return _LOCAL[name]
+        if (module, name) == ("torch.storage", "_load_from_bytes"):
+            return _storage_from_bytes
         if (module, name) in _SAFE:
             if module.startswith("torch"):
                 import torch  # noqa: F401

@@ -123,6 +123,25 @@ def test_reader_rejects_unlisted_globals():
         refpickle.load(pickle.dumps(Evil()))
 
 
+def test_reader_runs_no_code_nested_in_storage_bytes(tmp_path):
+    """torch.storage._load_from_bytes unpickles its argument with weights_only=False;
+    the reader must not hand a nested payload to it."""
+    from geobpe import refpickle
+    marker = tmp_path / "ran"
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, (f"touch {marker}",))
+
+    class Nest:
+        def __reduce__(self):
+            import torch.storage
+            return (torch.storage._load_from_bytes, (pickle.dumps(Evil()),))
+    with pytest.raises(Exception):
+        refpickle.load(pickle.dumps(Nest()))
+    assert not marker.exists(), "a payload nested in _load_from_bytes ran"
+
+
 def test_save_is_atomic_and_complete(tmp_path, oracle_lib):
     from geobpe import refpickle
     _, run = oracle_run(oracle_lib, "g25x1-12_b3_short", 10)
