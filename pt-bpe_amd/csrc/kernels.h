@@ -1093,31 +1093,63 @@ __global__ __launch_bounds__(BLOCK) void k_mark(Dev D, int par) {
     if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = min(s_n, (int32_t)D.LC);
     return;
   }
+  // Fingerprint scan in chunks of UNR x BLOCK 8-slot groups.  The hits of a chunk
+  // are compacted into an LDS queue (per-lane hit counts -> wave prefix sum -> one
+  // LDS reservation per wave), then confirmed and walked one candidate per thread:
+  // the dependent loads of every hit are in flight together.  (Walking each hit
+  // where the scan finds it serialises the wave over its lanes' hits: ~17 hits per
+  // wave and chunk in the heavy merges, 3 dependent round trips each.)
   const int64_t n8 = (D.R + 7) / 8;
   const int64_t lo = (int64_t)blockIdx.x * D.CH8, hi = min(n8, lo + D.CH8);
   const uint4* f4 = reinterpret_cast<const uint4*>(D.fp);
   constexpr int UNR = 8;
-  for (int64_t i0 = lo + threadIdx.x; i0 < hi; i0 += UNR * BLOCK) {
+  constexpr int MQ = 2048;  // candidates per chunk (more: walked in place)
+  __shared__ int32_t s_q[MQ];
+  __shared__ int32_t s_qn;
+  for (int64_t c0 = lo; c0 < hi; c0 += UNR * BLOCK) {  // block-uniform
+    if (threadIdx.x == 0) s_qn = 0;
+    const int64_t i0 = c0 + threadIdx.x;
     uint4 v[UNR];
 #pragma unroll
     for (int u = 0; u < UNR; u++) {
       const int64_t i = i0 + u * BLOCK;
       v[u] = i < hi ? f4[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     }
+    int32_t nh = 0;
 #pragma unroll
     for (int u = 0; u < UNR; u++) {
       const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
 #pragma unroll
-      for (int q = 0; q < 8; q++) {
-        const uint32_t f = (w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu;
-        if (f == fW) {
-          const int32_t g = (int32_t)(8 * (i0 + u * BLOCK) + q);
-          mark_hit(D, g, W, tag, &s_n, lovf);
+      for (int q = 0; q < 8; q++) nh += ((w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu) == fW;
+    }
+    int32_t wt;
+    const int32_t ex = wave_excl_scan(nh, wt);
+    __syncthreads();  // s_qn reset visible
+    int32_t base = 0;
+    if (wave_lane() == 0 && wt) base = atomicAdd(&s_qn, wt);
+    int32_t j = __shfl(base, 0, 64) + ex;
+    if (nh) {
+#pragma unroll
+      for (int u = 0; u < UNR; u++) {
+        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          if (((w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu) == fW) {
+            const int32_t g = (int32_t)(8 * (i0 + u * BLOCK) + q);
+            if (j < MQ)
+              s_q[j] = g;
+            else
+              mark_hit(D, g, W, tag, &s_n, lovf);
+            j++;
+          }
         }
       }
     }
+    __syncthreads();
+    const int32_t nq = min(s_qn, MQ);
+    for (int32_t i = threadIdx.x; i < nq; i += BLOCK) mark_hit(D, s_q[i], W, tag, &s_n, lovf);
+    __syncthreads();  // the queue is reused by the next chunk
   }
-  __syncthreads();
   if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = min(s_n, (int32_t)D.LC);
 }
 
