@@ -39,19 +39,35 @@ CONFIGS = {
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 APPLY_BYTES_PER_MERGE = 156  # algorithmic bytes of one merged occurrence in k_apply
-PMC_SUMMARY = os.path.join(REPO, "profiles", "pmc_latest.json")
+MARK_HIT_BYTES = 24  # k_mark per merged occurrence: pk/tprev/tlen of the hit, pk of p, pk/tlen of b
+PMC_WINDOWS = os.path.join(REPO, "profiles", "pmc_windows.json")
+REF_TIMING = os.path.join(REPO, "profiles", "reference_cpu_timing.json")
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of k_<kernel> from the committed rocprofv3 PMC summary
-    of this bench command (FETCH_SIZE x2 + WRITE_SIZE, MI355X_MICROARCH.md), or None."""
+def pmc_traffic(kernel, window_key, part="kernels"):
+    """HBM bytes per launch of k_<kernel> measured by rocprofv3 FETCH_SIZE / WRITE_SIZE
+    passes of THIS bench window (tools/prof_window.sh: the dispatches between the two
+    k_window_mark launches), keyed by (config, warmup, steps, N); None when no pass
+    of this exact window is committed -- never another window's figure."""
     try:
-        with open(PMC_SUMMARY) as f:
-            d = json.load(f)
-        k = d["kernels"][f"k_{kernel}"]
-        return round(k["hbm_bytes_per_launch"], 1), os.path.relpath(d.get("source", PMC_SUMMARY), REPO)
+        with open(PMC_WINDOWS) as f:
+            d = json.load(f)[window_key]
+        return round(d[part][f"k_{kernel}"]["hbm_bytes_per_launch"], 1), d.get("source")
     except Exception:
         return None, None
+
+
+def host_cpu():
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"model": model, "nproc": os.cpu_count()}
 
 
 def parse():
@@ -126,8 +142,10 @@ def main():
     bin_ms = {k: eng.kernel_ms(k)[0] for k in ("bin_sample", "pair_count", "bin_claim", "bin_assign", "finalize")}
     bin_ms = {k: v for k, v in bin_ms.items() if v > 0}
     eng.run(args.warmup)
-    # ---- timed region: exactly K merges; HIP events only around the roofline kernel
-    eng.set_profiling(not args.no_profile, only=args.roofline_kernel, stride=args.event_stride)
+    # ---- timed region: exactly K merges; HIP events only around the roofline kernels
+    eng.set_profiling(not args.no_profile, only=f"{args.roofline_kernel},mark", stride=args.event_stride)
+    st0 = eng.state()
+    eng.marker(1)  # window bracket for rocprofv3 (outside the timer)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -137,11 +155,14 @@ def main():
     if world > 1:
         dist.barrier()
     T = time.perf_counter() - t0
+    eng.marker(2)
+    st1 = eng.state()
     if world > 1:
         tt = torch.tensor([T], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
     live_ms, live_n = eng.kernel_ms(args.roofline_kernel) if not args.no_profile else (0.0, 0)
+    mark_ms, mark_n = eng.kernel_ms("mark") if not args.no_profile else (0.0, 0)
     merges_log = list(eng.merges)
     R_local = int(shard["row_off"][-1])
     if rank != 0:
@@ -165,28 +186,41 @@ def main():
         assert rep.merges == merges_log, "replay diverged"
         rep.close()
 
-    # ---- roofline of the loop's dominant kernel, from the live events of the timed region
+    # ---- roofline of the loop's dominant kernels, from the live events of the timed region
+    wkey = f"config={args.config},warmup={args.warmup},steps={args.steps},n={world}"
+    window = merges_log[-done:] if done else []
+    n_merged = sum(m[2] for m in window)
     roofline = None
     if live_n:
         avg_s = live_ms / 1000.0 / live_n
-        window = merges_log[-done:] if done else []
-        n_merged = sum(m[2] for m in window)
-        if args.roofline_kernel == "apply":
-            # 156 B per merged occurrence (token records of p, a, b, c; two
-            # glue symbols; neighbour content hashes; two key-table probes; the rewritten
-            # token fields; five count read-modify-writes)
-            bytes_per_launch = APPLY_BYTES_PER_MERGE * n_merged / max(done, 1)
-            note = f"{APPLY_BYTES_PER_MERGE} B x merged occurrences (avg {n_merged / max(done, 1):.0f} per launch)"
-        else:  # mark, fingerprint-scan mode: the 2 B/slot scan
-            bytes_per_launch = 2.0 * R_local
-            note = "2 B x residue slots (fingerprint scan)"
+        # 156 B per merged occurrence (token records of p, a, b, c; two
+        # glue symbols; neighbour content hashes; two key-table probes; the rewritten
+        # token fields; five count read-modify-writes)
+        bytes_per_launch = APPLY_BYTES_PER_MERGE * n_merged / max(done, 1)
+        note = f"{APPLY_BYTES_PER_MERGE} B x merged occurrences (avg {n_merged / max(done, 1):.0f} per launch)"
         ach = bytes_per_launch / avg_s / 1e9
-        traffic, tsrc = pmc_traffic(args.roofline_kernel)
+        traffic, tsrc = pmc_traffic(args.roofline_kernel, wkey)
         roofline = {"kernel": f"k_{args.roofline_kernel}", "bound": "hbm", "achieved": round(ach, 2),
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "traffic_source": tsrc, "bytes_per_launch": round(bytes_per_launch, 1),
+                    "traffic_source": tsrc, "traffic_window": wkey, "bytes_per_launch": round(bytes_per_launch, 1),
                     "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": live_n,
                     "event_stride": args.event_stride, "algorithmic_bytes": note}
+    mark_roof = None
+    if mark_n:
+        avg_s = mark_ms / 1000.0 / mark_n
+        scan = not st0["post_valid"] and not st1["post_valid"]
+        if scan:  # every mark of the window scanned the 2 B/slot fingerprints; 24 B per hit confirmed
+            bpl = 2.0 * R_local + MARK_HIT_BYTES * n_merged / max(done, 1)
+            note = f"2 B x {R_local} residue slots (fingerprint scan) + {MARK_HIT_BYTES} B x merged occurrences"
+        else:  # posting mode: 8 B per posting entry read is not counted per launch here
+            bpl = None
+            note = "posting-index mode in the window: per-launch entry count not recorded"
+        traffic, tsrc = pmc_traffic("mark", wkey)
+        ach = bpl / avg_s / 1e9 if bpl else None
+        mark_roof = {"kernel": "k_mark", "bound": "hbm", "achieved": round(ach, 2) if ach else None,
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
+                     "traffic": traffic, "traffic_source": tsrc, "bytes_per_launch": round(bpl, 1) if bpl else None,
+                     "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": mark_n, "algorithmic_bytes": note}
     # the full content-keyed pair-count pass (BPE.bin) at iteration 0: SURVEY §8(d)
     # B_count = 20*T_live + 4*U_live with T = residues
     pair_count = None
@@ -200,7 +234,7 @@ def main():
             "count_kernel": {"kernel": "k_bin_count" if dense else "k_pairs_all",
                              "time_us": round(t_count * 1e6, 2), "achieved_GBs": round(bc / t_count / 1e9, 1),
                              "frac": round(bc / t_count / 1e9 / HBM_PEAK_GBS, 4),
-                             "traffic": pmc_traffic("bin_count" if dense else "pairs_all")[0]},
+                             "traffic": pmc_traffic("bin_count" if dense else "pairs_all", wkey, "pre_kernels")[0]},
             "pass": {"kernels": ("k_bin_sample+k_bin_rank+k_bin_flag+k_bin_precube | k_bin_count | k_bin_reduce | "
                                  "k_bin_ool_stage+k_bin_ool_claim+k_bin_ool_fix") if dense else "k_pairs_all+k_finalize",
                      "time_us": round(t_pass * 1e6, 2), "achieved_GBs": round(bc / t_pass / 1e9, 1),
@@ -211,6 +245,8 @@ def main():
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(corpus, B, args.warmup, args.steps, args.cpu_budget_s)
+        cpu["host"] = host_cpu()
+        cpu["reference"] = reference_estimate(window)
 
     value = done / T if T > 0 else 0.0
     out = {
@@ -233,6 +269,7 @@ def main():
                    if args.config in ("c3", "c5") else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
                    "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}"},
         "roofline": roofline,
+        "roofline_mark": mark_roof,
         "cpu_baseline": cpu,
         "pair_count_pass": pair_count,
         "kernels": kern,
@@ -244,6 +281,26 @@ def main():
         dist.barrier()
     if world > 1 or args.force_exchange:
         dist.destroy_process_group()
+
+
+def reference_estimate(window):
+    """The reference Python's own cost (foldingdiff/bpe.py BPE.step, timed in the build
+    container by tools/ref_timing.py on C3 subsets: ms per merged occurrence) applied
+    to this window's merged occurrences -- context, not a measurement on this host."""
+    try:
+        with open(REF_TIMING) as f:
+            rt = json.load(f)
+    except (OSError, ValueError):
+        return None
+    runs = rt["runs"]
+    ms_occ = max(r["ms_per_merged_occurrence"] for r in runs)
+    occ = sum(m[2] for m in window) / max(len(window), 1)
+    return {"value": round(1000.0 / (ms_occ * occ), 6) if occ else None, "unit": "merges/s",
+            "ms_per_merged_occurrence": ms_occ, "merged_occurrences_per_merge": round(occ, 1),
+            "cores": 1, "host": f"build container, {rt.get('cpus', '?')} vCPU (not the GPU box)",
+            "kind": "reference", "sample": f"{rt['generator']}: step() on the first "
+            + "/".join(str(r["chains"]) for r in runs) + " chains of the C3 corpus, "
+            + f"{rt.get('merges_timed', '?')} merges each; slowest per-occurrence cost used"}
 
 
 def cpu_baseline(corpus, B, warmup, steps, budget_s):

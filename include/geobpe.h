@@ -186,6 +186,10 @@ int64_t geobpe_debug_timeline(geobpe_ctx *ctx, int on, int64_t *h_out, int64_t c
 /* Restrict the timing to a comma-separated list of kernel names ("" = all). */
 int geobpe_set_profiling_filter(geobpe_ctx *ctx, const char *names);
 double geobpe_kernel_ms(geobpe_ctx *ctx, const char *name, int64_t *launches);
+/* Profiling: enqueue k_window_mark (one empty workgroup) on the engine stream.
+ * bench.py brackets its timed region with two of them (outside the timer) so a
+ * rocprofv3 trace / PMC pass can select exactly that window's dispatches. */
+int geobpe_marker(geobpe_ctx *ctx, int32_t tag);
 /* ---- PDB -> internal coordinates (the reference's
  * canonical_distances_and_dihedrals, foldingdiff/angles_and_coords.py:69-154) ----
  * geobpe_pdb_backbone: N, CA, C (x, y, z) of every amino-acid residue of the

@@ -75,7 +75,7 @@ __device__ inline int32_t bin_triple(int32_t la, int32_t gs, int32_t lb, int32_t
 // lanes active); lane 63, and a lane whose next group is past its range, loads it
 __device__ inline int32_t bin_next_tid(const Dev& D, int32_t tx, int64_t v, int64_t hi) {
   int32_t n = __builtin_amdgcn_update_dpp(-1, tx, 0x130, 0xF, 0xF, false);
-  if ((wave_lane() == 63 || v + 1 >= hi) && v < hi) n = (v + 1) * BIN_VEC < D.R ? D.tid[(v + 1) * BIN_VEC] : -1;
+  if ((wave_lane() == 63 || v + 1 >= hi) && v < hi) n = (v + 1) * BIN_VEC < D.R ? D.lab0[(v + 1) * BIN_VEC] : -1;
   return n;
 }
 
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_sample(Dev D, BinWork W) {
   int64_t lo, hi;
   bin_range(D, lo, hi);
   const int64_t he = bin_sample_end(lo, hi);
-  const int4* tv = (const int4*)D.tid;
+  const int4* tv = (const int4*)D.lab0;
   const int4* gv = (const int4*)D.gsym;
   for (int64_t v = lo + threadIdx.x; v < he; v += ABLOCK) {
     const int4 t = tv[v], s = gv[v];
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_flag(Dev D, BinWork W) {
   int64_t lo, hi;
   bin_range(D, lo, hi);
   const int64_t he = bin_sample_end(lo, hi);
-  const int4* tv = (const int4*)D.tid;
+  const int4* tv = (const int4*)D.lab0;
   const int4* gv = (const int4*)D.gsym;
   for (int64_t v = lo + threadIdx.x; v < he; v += ABLOCK) {
     const int4 t = tv[v], s = gv[v];
@@ -340,7 +340,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
   int64_t lo, hi;
   bin_range(D, lo, hi);
   const int64_t R = D.R;
-  const int4* tv = (const int4*)D.tid;
+  const int4* tv = (const int4*)D.lab0;
   const int4* gv = (const int4*)D.gsym;
   int4* pv = (int4*)D.pk;
   ushort4* fv = (ushort4*)D.fp;
@@ -407,7 +407,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
       const int32_t sy = D.gsym[g];
       int32_t k = -1;
       if (sy >= 0) {
-        const int32_t la = D.tid[g], lb = D.tid[g + 1];
+        const int32_t la = D.lab0[g], lb = D.lab0[g + 1];
         const int32_t cc = bin_cell(cl, cg, CL, CG, la, sy, lb);
         k = cc >= 0 ? s_map[cc] : -1;
         if (k >= 0)

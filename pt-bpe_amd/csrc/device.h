@@ -119,9 +119,13 @@ struct Dev {
   int32_t B, B2, B3, pad0;
   const int64_t* row_off;
   int32_t *rsym, *gsym;
-  // tokens (residue indexed)
-  int32_t *tid, *tlen, *tprev, *pk, *role;
-  u64 *th1, *th2;  // content hash of the token starting at a slot (= vh of its id; saves the vocab lookup)
+  // tokens (residue indexed).  tok[s] = {tid, tlen, tprev, role} of the token
+  // starting at slot s (tid -1: not a token start): one 16-B record, so the
+  // scattered reads of a merged occurrence touch one line per neighbour instead
+  // of one per field; content hashes come from the vocab (vh1/vh2[tid], L2-resident)
+  int4* tok;
+  int32_t* pk;    // key id of the pair (token at s, next token); -1: none
+  int32_t* lab0;  // initial residue labels (= tok[s].x before any merge): the bin pass streams these
   uint16_t* fp;  // 16-bit fingerprint of pk (0xFFFF = none): the mark scan reads these
   // vocab (token id indexed)
   u64 *vh1, *vh2;
@@ -304,6 +308,9 @@ __device__ inline void dbg_stamp(const Dev& D, int k) {
 
 __device__ inline uint32_t post_bkt(int32_t d) { return ((uint32_t)d * 2654435761u) >> (32 - NBKT_LOG2); }
 
+// token record fields (int4 tok[s] = {tid, tlen, tprev, role})
+__device__ inline int32_t* tok_f(const Dev& D, int64_t s, int f) { return reinterpret_cast<int32_t*>(D.tok + s) + f; }
+
 __device__ inline uint16_t key_fp(int32_t d) { return (uint16_t)((uint32_t)d % 65535u); }
 
 // a key whose rank-local delta left 0 joins the touched list: one reservation per
@@ -481,10 +488,31 @@ __device__ inline void agg_flush_hot(A& s, const Dev& D, HotApp& h, bool to_delt
       j++;
     }
   } else {
-    for (int i = threadIdx.x; i < A::N; i += blockDim.x) {
-      const int32_t k = s.key[i];
-      if (k < 0 || s.val[i] == 0) continue;
-      count_add_hot(D, h, k, s.val[i], th);
+    // every slot's add in flight before the first result is needed: the returning
+    // adds (positive deltas: the theta-crossing check) of a thread are issued back
+    // to back, not one round trip per slot
+    constexpr int U = A::N / 1024 > 0 ? A::N / 1024 : 1;
+    int32_t k[U], v[U], old[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const int i = threadIdx.x + u * (int)blockDim.x;
+      k[u] = i < A::N ? s.key[i] : -1;
+      v[u] = k[u] >= 0 ? s.val[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      old[u] = 0;
+      if (v[u] > 0 && th > 0)
+        old[u] = atomicAdd(&D.count[k[u]], v[u]);
+      else if (v[u] != 0)
+        atomicAdd(&D.count[k[u]], v[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++)
+      if (v[u] > 0 && th > 0 && old[u] < th && old[u] + v[u] >= th) hot_push(D, h, k[u]);
+    for (int i = threadIdx.x + U * (int)blockDim.x; i < A::N; i += blockDim.x) {  // blockDim < 1024
+      const int32_t kk = s.key[i];
+      if (kk >= 0 && s.val[i] != 0) count_add_hot(D, h, kk, s.val[i], th);
     }
   }
   hot_flush(D, h);

@@ -368,9 +368,8 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   int rc;
   const int64_t Rp = c->R + 8;  // int4 padding for the pk scan
   if ((rc = dalloc(c, &c->d_row_off, n_rows + 1)) || (rc = dalloc(c, &D.rsym, Rp, 0)) ||
-      (rc = dalloc(c, &D.gsym, Rp, 0)) || (rc = dalloc(c, &D.tid, Rp, 0xFF)) || (rc = dalloc(c, &D.tlen, Rp, 0)) ||
-      (rc = dalloc(c, &D.tprev, Rp, 0xFF)) || (rc = dalloc(c, &D.pk, Rp, 0xFF)) || (rc = dalloc(c, &D.role, Rp, 0)) ||
-      (rc = dalloc(c, &D.th1, Rp, 0)) || (rc = dalloc(c, &D.th2, Rp, 0)) ||
+      (rc = dalloc(c, &D.gsym, Rp, 0)) || (rc = dalloc(c, &D.tok, Rp, 0xFF)) || (rc = dalloc(c, &D.lab0, Rp, 0xFF)) ||
+      (rc = dalloc(c, &D.pk, Rp, 0xFF)) ||
       (rc = dalloc(c, &D.fp, Rp + 16, 0xFF)))
     return rc;
   D.row_off = c->d_row_off;
@@ -1049,6 +1048,14 @@ int64_t geobpe_verify_counts(geobpe_ctx* c) {
   hipLaunchKernelGGL(k_compare, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
   if (sync_state(c)) return -1;
   return c->h_state->nmismatch;
+}
+
+int geobpe_marker(geobpe_ctx* c, int32_t tag) {
+  if (!c) return GEOBPE_EARG;
+  HIPCHK(c, hipSetDevice(c->device));
+  hipLaunchKernelGGL(k_window_mark, dim3(1), dim3(64), 0, c->stream, tag, c->D.st);
+  HIPCHK(c, hipGetLastError());
+  return 0;
 }
 
 int64_t geobpe_debug_timeline(geobpe_ctx* c, int on, int64_t* h_out, int64_t cap) {

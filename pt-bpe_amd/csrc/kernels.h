@@ -5,6 +5,11 @@
 
 namespace gb {
 
+// profiling window bracket (geobpe_marker): does nothing
+__global__ void k_window_mark(int32_t tag, State* st) {
+  if (tag == INT32_MIN && threadIdx.x == 64) st->nskip = 0;  // never taken; keeps the kernel non-empty
+}
+
 // ====================================================================== prologue
 __constant__ int32_t c_type_col[GEOBPE_NTYPES] = {GEOBPE_COL_TAU, GEOBPE_COL_CAC1N, GEOBPE_COL_C1NCA,
                                                   GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_PHI};
@@ -123,13 +128,11 @@ __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_
     const int64_t a = D.row_off[r], b = D.row_off[r + 1];
     for (int64_t g = a + threadIdx.x; g < b; g += blockDim.x) {
       const int32_t sy = D.rsym[g];
-      D.tid[g] = label_of_sym[sy];
-      D.tlen[g] = 1;
-      D.th1[g] = D.th2[g] = (u64)(sy + 1);  // = vh of the residue token (geobpe_init_tokens)
-      D.tprev[g] = (g == a) ? -1 : (int32_t)(g - 1);
+      const int32_t lab = label_of_sym[sy];
+      D.tok[g] = make_int4(lab, 1, (g == a) ? -1 : (int32_t)(g - 1), 0);
+      D.lab0[g] = lab;
       D.pk[g] = -1;
       D.fp[g] = 0xFFFF;
-      D.role[g] = 0;
     }
   }
 }
@@ -229,16 +232,18 @@ __global__ __launch_bounds__(ABLOCK) void k_pairs_all(Dev D) {
   const int64_t SC = (D.R + gridDim.x - 1) / gridDim.x;
   const int64_t lo = (int64_t)blockIdx.x * SC, hi = min(D.R, lo + SC);
   for (int64_t g = lo + threadIdx.x; g < hi; g += blockDim.x) {
-    const int32_t L = D.tid[g];
+    const int4 tg = D.tok[g];
+    const int32_t L = tg.x;
     if (L < 0) continue;
-    const int32_t xlen = D.tlen[g];
+    const int32_t xlen = tg.y;
     const int32_t e = (int32_t)g + xlen - 1;
     if (D.rsym[e] >= D.B3) continue;  // last token of its chain
-    const int32_t Rr = D.tid[e + 1];
+    const int4 te = D.tok[e + 1];
+    const int32_t Rr = te.x;
     const int32_t gl = D.gsym[e];
-    const int32_t ylen = D.tlen[e + 1];
+    const int32_t ylen = te.y;
     u64 h1, h2;
-    combine(D, D.th1[g], D.th2[g], gl, D.th1[e + 1], D.th2[e + 1], ylen, h1, h2);
+    combine(D, D.vh1[L], D.vh2[L], gl, D.vh1[Rr], D.vh2[Rr], ylen, h1, h2);
     add_pair(D, &s_np, &s_ns, (int32_t)g, h1, h2, xlen + ylen, L, gl, Rr, 1);
   }
   close_regions(D, &s_np, &s_ns);
@@ -920,8 +925,8 @@ __device__ inline void emit_merge(const Dev& D, int32_t* s_n, int32_t t, int32_t
   e.p = p;
   e.b = b;
   e.c = c;
-  D.role[t] = (tag << 2) | 1;
-  D.role[b] = (tag << 2) | 2;
+  *tok_f(D, t, 3) = (tag << 2) | 1;
+  *tok_f(D, b, 3) = (tag << 2) | 2;
   const int32_t j = atomicAdd(s_n, 1);
   if (j < D.LC) {
     D.L[(int64_t)blockIdx.x * D.LC + j] = e;
@@ -935,25 +940,27 @@ __device__ inline void emit_merge(const Dev& D, int32_t* s_n, int32_t t, int32_t
 }
 
 __device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag, int32_t* s_n, int64_t* lovf) {
-  const int32_t pkg = D.pk[g], p = D.tprev[g], lg = D.tlen[g];
+  const int32_t pkg = D.pk[g];
+  const int4 tg = D.tok[g];
   if (pkg != W) return;
+  const int32_t p = tg.z, lg = tg.y;
   int32_t b = g + lg;
   const int32_t pkp = D.pk[p >= 0 ? p : g];
-  int32_t pkb = D.pk[b], lb = D.tlen[b];
+  int32_t pkb = D.pk[b], lb = D.tok[b].y;
   if (p >= 0 && pkp == W) return;  // not a run start: the run's head walks it
   int32_t t = g, pp = p;
   for (;;) {
     const int32_t c = pkb >= 0 ? b + lb : -1;
     emit_merge(D, s_n, t, pp, b, c, tag, lovf);
     if (pkb != W) break;
-    const int32_t pkc = D.pk[c], lc = D.tlen[c];
+    const int32_t pkc = D.pk[c], lc = D.tok[c].y;
     if (pkc != W) break;
     const int32_t d = c + lc;
     pp = b;
     t = c;
     b = d;
     pkb = D.pk[d];
-    lb = D.tlen[d];
+    lb = D.tok[d].y;
   }
 }
 
@@ -1275,12 +1282,18 @@ __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const
   // in ApplyCtx would become a flat load through the scratch stack.
   const int32_t ip = hasP ? e.p : e.a, ic = hasC ? e.c : e.a;
   const int32_t pkb = D.pk[e.b];
-  const int32_t rp = D.role[ip], pkp0 = D.pk[ip], L0 = D.tid[ip], ll0 = D.tlen[ip];
-  const u64 l1 = D.th1[ip], l2 = D.th2[ip];
+  const int4 tp = D.tok[ip], tcr = D.tok[ic];  // {tid, tlen, tprev, role} of p and c
+  const int32_t pkp0 = D.pk[ip];
   const int32_t glL = hasP ? D.gsym[e.a - 1] : 0;
-  const int32_t rc0 = D.role[ic], tc = D.tid[ic], rl0 = D.tlen[ic];
-  const u64 c1 = D.th1[ic], c2 = D.th2[ic];
   const int32_t glR = hasC ? D.gsym[e.a + A.wl - 1] : 0;
+  const int32_t rp = tp.w, L0 = tp.x, ll0 = tp.y;
+  const int32_t rc0 = tcr.w, tc = tcr.x, rl0 = tcr.y;
+  // the neighbours' content hashes by token id (vocab: small, L2-resident).  A
+  // right part p (or a left part c) is being rewritten by another thread: its
+  // id may read as -1 / the new id, and is not used then (pN / cL below)
+  const int32_t vp = max(L0, 0), vc = max(tc, 0);
+  const u64 l1 = D.vh1[vp], l2 = D.vh2[vp];
+  const u64 c1 = D.vh1[vc], c2 = D.vh2[vc];
   const int32_t pkp = hasP ? pkp0 : -1;
   const int32_t L = hasP ? L0 : 0;
   const int32_t ll = ll0;
@@ -1332,15 +1345,12 @@ __device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const
   if (pN) agg_add_hot(agg, D, hot, pkp, -1, A.to_delta, A.theta);
   if (dk >= 0) dbg_stamp(D, dk + 1);
   // step 2: bond_to_token / token_pos
-  D.tid[e.a] = A.nid;
-  D.tlen[e.a] = A.wl;
-  D.th1[e.a] = A.w1;
-  D.th2[e.a] = A.w2;
-  D.tid[e.b] = -1;
+  *reinterpret_cast<int2*>(D.tok + e.a) = make_int2(A.nid, A.wl);
+  *tok_f(D, e.b, 0) = -1;
   D.pk[e.b] = -1;
   D.fp[e.b] = 0xFFFF;
   if (hasC) {
-    D.tprev[e.c] = e.a;
+    *tok_f(D, e.c, 2) = e.a;
   } else {
     D.pk[e.a] = -1;
     D.fp[e.a] = 0xFFFF;
@@ -1824,7 +1834,7 @@ __global__ __launch_bounds__(BLOCK) void k_row_ntok(Dev D, int64_t* ntok) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.nrows; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = D.row_off[r], b = D.row_off[r + 1];
     int64_t n = 0;
-    for (int64_t g = a; g < b; g += D.tlen[g]) n++;
+    for (int64_t g = a; g < b; g += D.tok[g].y) n++;
     ntok[r] = n;
   }
 }
@@ -1833,10 +1843,12 @@ __global__ __launch_bounds__(BLOCK) void k_row_seg(Dev D, const int64_t* tok_off
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.nrows; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = D.row_off[r], b = D.row_off[r + 1];
     int64_t t = tok_off[r];
-    for (int64_t g = a; g < b; g += D.tlen[g]) {
+    for (int64_t g = a; g < b;) {
+      const int4 tg = D.tok[g];
       start[t] = (int32_t)(g - a);
-      id[t] = D.tid[g];
+      id[t] = tg.x;
       t++;
+      g += tg.y;
     }
   }
 }
@@ -1849,8 +1861,9 @@ __global__ __launch_bounds__(BLOCK) void k_row_encode(Dev D, const int64_t* id_o
     const int64_t a = D.row_off[r], b = D.row_off[r + 1];
     int64_t t = id_off[r];
     for (int64_t g = a; g < b;) {
-      const int64_t e = g + D.tlen[g] - 1;
-      ids[t++] = D.tid[g];
+      const int4 tg = D.tok[g];
+      const int64_t e = g + tg.y - 1;
+      ids[t++] = tg.x;
       if (e + 1 < b) {
         const int32_t gs = D.gsym[e];
         ids[t++] = K + B + gs / D.B2;

@@ -427,6 +427,19 @@ class GeoBPEEngine:
         self._chk(self.L.geobpe_set_profiling_filter(self._ctx, only.encode()))
         self._chk(self.L.geobpe_set_profiling(self._ctx, max(1, int(stride)) if on else 0))
 
+    def state(self) -> dict:
+        """Loop state (hot list, threshold, posting index) after a synchronisation."""
+        v = np.zeros(10, dtype=np.int64)
+        n = self.L.geobpe_debug_state(self._ctx, _p(v), 10)
+        if n < 0:
+            self._chk(int(n))
+        keys = ("hot_list", "theta", "ncand", "maxc", "nskip", "cl_valid", "iter", "K", "post_valid", "plog_total")
+        return {k: int(x) for k, x in zip(keys, v)}
+
+    def marker(self, tag: int = 0):
+        """Enqueue the empty k_window_mark kernel (brackets a profiled window)."""
+        self._chk(self.L.geobpe_marker(self._ctx, int(tag)))
+
     def kernel_ms(self, name: str):
         n = ctypes.c_int64(0)
         ms = self.L.geobpe_kernel_ms(self._ctx, name.encode(), ctypes.byref(n))
