@@ -502,20 +502,27 @@ __device__ inline void agg_flush_hot(A& s, const Dev& D, HotApp& h, bool to_delt
 #pragma unroll
     for (int u = 0; u < U; u++) {
       old[u] = 0;
+#ifdef GB_FLUSH_NORET  // (diagnostic A/B only: no theta-crossing check)
+      if (v[u] != 0) atomicAdd(&D.count[k[u]], v[u]);
+      continue;
+#endif
       if (v[u] > 0 && th > 0)
         old[u] = atomicAdd(&D.count[k[u]], v[u]);
       else if (v[u] != 0)
         atomicAdd(&D.count[k[u]], v[u]);
     }
+    dbg_stamp(D, 34);
 #pragma unroll
     for (int u = 0; u < U; u++)
       if (v[u] > 0 && th > 0 && old[u] < th && old[u] + v[u] >= th) hot_push(D, h, k[u]);
+    dbg_stamp(D, 35);
     for (int i = threadIdx.x + U * (int)blockDim.x; i < A::N; i += blockDim.x) {  // blockDim < 1024
       const int32_t kk = s.key[i];
       if (kk >= 0 && s.val[i] != 0) count_add_hot(D, h, kk, s.val[i], th);
     }
   }
   hot_flush(D, h);
+  dbg_stamp(D, 36);
 }
 
 

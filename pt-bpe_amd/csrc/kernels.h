@@ -1380,21 +1380,27 @@ __device__ inline int32_t key_done(const Dev& D, int32_t* s_ns, int32_t* s_chk, 
 // and CASes only if it is still empty; the L and R halves' first CASes are
 // issued back to back.
 __device__ inline void halves_resolve(const Dev& D, KeyCache& kc, int32_t* s_ns, int32_t* s_chk, Half& a, bool va,
-                                      Half& b, bool vb) {
+                                      Half& b, bool vb, int dk) {
   if (va) a.kcs = kc_find(kc, a.k, &a.res);
   if (vb) b.kcs = kc_find(kc, b.k, &b.res);
+  if (dk >= 0) dbg_stamp(D, dk);
   a.d = b.d = -1;
   const bool ra = va && a.res, rb = vb && b.res;
   u64 ca = ra ? a.cur : 1, cb = rb ? b.cur : 1;  // (1: no slot work for that half)
+#ifndef GB_NO_STAGGER
   if ((ra && ca == 0) || (rb && cb == 0)) {
     for (int i = 0; i < 1 + (int)(blockIdx.x & 15); i++) __builtin_amdgcn_s_sleep(2);
     if (ra && ca == 0) ca = ht_probe(D, a.s);
     if (rb && cb == 0) cb = ht_probe(D, b.s);
   }
+#endif
+  if (dk >= 0) dbg_stamp(D, dk + 1);
   u64 oa = ca, ob = cb;
   bool cla = false, clb = false;
   if (ra && ca == 0) oa = atomicCAS((unsigned long long*)&D.ht_key[a.s], 0ULL, (unsigned long long)a.k);
   if (rb && cb == 0) ob = atomicCAS((unsigned long long*)&D.ht_key[b.s], 0ULL, (unsigned long long)b.k);
+  if (dk >= 0 && (oa | ob) == 12345) dbg_stamp(D, 63);  // (keeps the CAS results live before the next stamp)
+  if (dk >= 0) dbg_stamp(D, dk + 2);
   if (ra) {
     int32_t slot;
     if (ca == 0 && oa == 0) {
@@ -1419,6 +1425,7 @@ __device__ inline void halves_resolve(const Dev& D, KeyCache& kc, int32_t* s_ns,
     }
     b.d = key_done(D, s_ns, s_chk, b, slot, clb);
   }
+  if (dk >= 0) dbg_stamp(D, dk + 3);
   if (va && a.res && a.kcs >= 0) {
     kc.h1[a.kcs] = a.h1;
     kc.id[a.kcs] = a.d >= 0 ? a.d : -2;
@@ -1571,7 +1578,7 @@ __global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta, int par) 
       apply_front(D, agg, hot, e, A, hl, vl, hr, vr, j0 < 2 * ABLOCK ? 40 + 10 * (int)(j0 / ABLOCK) : -1);
     }
     dbg_stamp(D, dbk++);
-    if (vl || vr) halves_resolve(D, kc, &s_ns, &s_chk, hl, vl, hr, vr);
+    if (vl || vr) halves_resolve(D, kc, &s_ns, &s_chk, hl, vl, hr, vr, j0 == 0 ? 30 : -1);
     dbg_stamp(D, dbk++);
     __syncthreads();
     dbg_stamp(D, dbk++);

@@ -40,7 +40,7 @@ for it in iters:
     names = {0: "start", 1: "setup", 60: "loop_end", 61: "flush_end", 62: "klist_end", 63: "end",
              20: "SEL.start", 21: "SEL.scanned", 22: "SEL.max", 23: "SEL.ties", 24: "SEL.staged", 25: "SEL.tourn",
              26: "SEL.end", 10: "MARK.start", 11: "MARK.state", 12: "MARK.bucket", 13: "MARK.hits"}
-    names.update({30: "r0.kcL", 31: "r0.globalL", 32: "r0.kcR", 33: "r0.globalR"})
+    names.update({30: "r0.res.kc", 31: "r0.res.reprobe", 32: "r0.res.cas", 33: "r0.res.done", 34: "flush.issued", 35: "flush.returned", 36: "flush.hot"})
     for r in range(2):
         for i, nm in enumerate(["front.loads", "front.agg", "finL.kc", "finL.store", "finL.agg", "finR.kc",
                                 "finR.store", "finR.agg"]):
