@@ -84,7 +84,7 @@ def parse():
                     help="N > 1: RCCL (default); gloo puts every rank on GPU 0 (a one-GPU rehearsal of the N > 1 path)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
-    ap.add_argument("--roofline-kernel", default="apply")
+    ap.add_argument("--roofline-kernel", default="commit")
     ap.add_argument("--event-stride", type=int, default=8,
                     help="time every k-th launch of the roofline kernel in the timed region")
     return ap.parse_args()
@@ -141,9 +141,10 @@ def main():
     U0 = eng.num_keys
     bin_ms = {k: eng.kernel_ms(k)[0] for k in ("bin_sample", "pair_count", "bin_claim", "bin_assign", "finalize")}
     bin_ms = {k: v for k, v in bin_ms.items() if v > 0}
+    pack_ms = eng.kernel_ms("bin_pack")[0]  # layout step for the merge loop (pk into the token records)
     eng.run(args.warmup)
     # ---- timed region: exactly K merges; HIP events only around the roofline kernels
-    eng.set_profiling(not args.no_profile, only=f"{args.roofline_kernel},mark", stride=args.event_stride)
+    eng.set_profiling(not args.no_profile, only=f"{args.roofline_kernel},find", stride=args.event_stride)
     st0 = eng.state()
     eng.marker(1)  # window bracket for rocprofv3 (outside the timer)
     if world > 1:
@@ -162,7 +163,7 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
     live_ms, live_n = eng.kernel_ms(args.roofline_kernel) if not args.no_profile else (0.0, 0)
-    mark_ms, mark_n = eng.kernel_ms("mark") if not args.no_profile else (0.0, 0)
+    mark_ms, mark_n = eng.kernel_ms("find") if not args.no_profile else (0.0, 0)
     merges_log = list(eng.merges)
     R_local = int(shard["row_off"][-1])
     if rank != 0:
@@ -180,7 +181,7 @@ def main():
         rep.run(args.warmup)
         rep.set_profiling(True)
         rep.run(done)
-        for k in ("select", "mark", "apply"):
+        for k in ("select", "find", "commit", "place"):
             ms, nl = rep.kernel_ms(k)
             kern[k] = {"ms_total": round(ms, 4), "launches": nl, "avg_us": round(1000 * ms / max(nl, 1), 3)}
         assert rep.merges == merges_log, "replay diverged"
@@ -240,6 +241,7 @@ def main():
                      "time_us": round(t_pass * 1e6, 2), "achieved_GBs": round(bc / t_pass / 1e9, 1),
                      "frac": round(bc / t_pass / 1e9 / HBM_PEAK_GBS, 4),
                      "ms": {k: round(v, 4) for k, v in bin_ms.items()}},
+            "layout_pack_us": round(pack_ms * 1000, 2),
         }
 
     cpu = None

@@ -18,24 +18,35 @@ constexpr u64 KMIX = 0x9E3779B97F4A7C15ULL;
 constexpr double TWO_PI = 6.283185307179586;  // 2*np.pi
 constexpr int BLOCK = 256;
 constexpr int ABLOCK = 1024;  // region kernels (bin pairs, finalize, apply, import): 16 waves per CU
-constexpr int RPB = 8;         // mark regions per apply workgroup (NB = RPB * NBA)
 constexpr int CL_MIN_SHRINK = 4096;
 constexpr int PIPE_MAX_WORLD = 64;   // ranks of a pipelined exchange  // hot-list length above which a 4x drop of theta re-scans
 constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per region)
 constexpr int NBKT = 1 << NBKT_LOG2;
-constexpr int SKIP_HOT = 1, SKIP_POST = 2, SKIP_MEASURE = 4;  // what a rebuild iteration does
+constexpr int SKIP_HOT = 1, SKIP_MEASURE = 4;  // what a rebuild iteration does
 constexpr int DBG_SLOTS = 64;
 #ifndef PW_LDS_DEF
 #define PW_LDS_DEF 2048
 #endif
 constexpr int PW_LDS = PW_LDS_DEF;  // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
-constexpr int KL_CHUNK = 4096;  // klist entries an apply workgroup reserves at a time
-#ifndef POST_SPAN_DEF
-#define POST_SPAN_DEF 64
+constexpr int KL_CHUNK = 4096;  // klist entries a commit workgroup reserves at a time
+// merge find -> commit hand-off (merge.h): per (owner, find workgroup) fixed record
+// slots, overflow to one global list
+constexpr int NBA_MAX = 256;
+#ifndef GB_SK
+#define GB_SK 48
 #endif
-// the posting index is rebuilt only when the winner's count is small enough that
-// the log lasts >= POST_SPAN / 2 merges (2 new pairs per occurrence)
-constexpr int POST_SPAN = POST_SPAN_DEF;
+#ifndef GB_FKC
+#define GB_FKC 2048
+#endif
+#ifndef GB_CKC
+#define GB_CKC 2048
+#endif
+constexpr int SK = GB_SK;    // key records per (owner, find workgroup)
+constexpr int SD = GB_SK;    // decrement records per (owner, find workgroup)
+constexpr int FKC = GB_FKC;  // find: new-key dedupe slots (LDS) per round
+constexpr int CKC = GB_CKC;  // commit: key dedupe slots (LDS) per owner
+constexpr int FMQ = 4096;    // find: candidate queue (LDS) per chunk of posting entries
+constexpr int LOG_CH_MAX = 64;  // posting-log chunks one owner may add in one merge
 
 // ------------------------------------------------------------------ records
 // Kernel-to-kernel state.  No field is written by a kernel that other
@@ -67,10 +78,11 @@ struct State {
   int64_t cl_measured; // max count found by a measure iteration
   int64_t nskip;       // rebuild iterations so far (stats)
   int64_t nunchecked;  // found-key records beyond the check regions (not verified)
-  // posting index (k_mark): bucket-sorted (key, slot) per region + the log of
-  // pairs made since its last rebuild
+  // posting index: bucket-sorted (key, slot) per region + per-owner logs of the
+  // pairs made since its last rebuild (chunks of one pool)
   int32_t post_valid, plog_ovf;
-  int64_t plog_total, npost;
+  int64_t pool_used, npost;   // pool chunks handed out since the last rebuild; rebuilds so far
+  int64_t nko2[2];            // key records past the fixed slots, by launch parity
   int64_t slot_max;    // pipelined exchange: the largest slot count of the last import (every rank)
 };
 
@@ -80,6 +92,9 @@ constexpr int SEL_MERGE = 0, SEL_SKIP = 1, SEL_DONE = 2;
 struct Sel {
   int32_t decision;
   int32_t skip;       // SKIP_* bits of a rebuild iteration
+  int32_t rebuild;    // merge: k_find rebuilds the posting index first (rank-local; the iteration still merges)
+  int32_t wown;       // merge: the owner whose posting log holds the winner's new pairs
+  int32_t pad2[2];
   int32_t theta_new;  // hot-list rebuild threshold
   int32_t build;      // hot-list counter the rebuild fills
   int32_t W, nid, iter, tag;
@@ -88,8 +103,8 @@ struct Sel {
   u64 w1, w2;         // content hash of the new token
 };
 
-struct LEntry {  // one merge: left token a (+ its prev p), right token b (+ next c)
-  int32_t a, p, b, c;
+struct LEntry {  // one merge: left token a, right token b, next token c; ya = the new token's length word
+  int32_t a, ya, b, c;
 };
 struct NewPair {
   int32_t target;  // residue whose pk receives the key (-1: none)
@@ -113,20 +128,31 @@ struct LogRec {  // one merge of the run (the merge list, device side)
   int64_t nmerged;
 };
 
+// a new pair key of a merge, find -> its owner's commit workgroup: content hash,
+// representative and n occurrence slots whose pk receive the key (T[tstart ..
+// tstart + n), or one slot -(tstart + 1) when tstart < 0)
+struct KRec {
+  u64 pkey, h1, h2;
+  int32_t len, idL, g, idR, n, tstart;
+};
+static_assert(sizeof(KRec) == 48, "key record layout");
+
 struct Dev {
   // corpus
   int64_t R, nrows;
   int32_t B, B2, B3, pad0;
   const int64_t* row_off;
   int32_t *rsym, *gsym;
-  // tokens (residue indexed).  tok[s] = {tid, tlen, tprev, role} of the token
-  // starting at slot s (tid -1: not a token start): one 16-B record, so the
-  // scattered reads of a merged occurrence touch one line per neighbour instead
-  // of one per field; content hashes come from the vocab (vh1/vh2[tid], L2-resident)
+  uint16_t* gs16;  // gsym as 16 bits when B^3 + B < 65535 (the merge loop reads these), else null
+  // tokens (residue indexed).  tok[s] = {tid, tlen, tprev, pk} of the token
+  // starting at slot s (tid -1: not a token start; pk: key id of the pair (this
+  // token, the next one), -1: none): one 16-B record, so the scattered reads of a
+  // merged occurrence touch one line per neighbour instead of one per field;
+  // content hashes come from the vocab (vh1/vh2[tid], L2-resident)
   int4* tok;
-  int32_t* pk;    // key id of the pair (token at s, next token); -1: none
+  int32_t* pk;    // the bin pass's pair keys (streamed there; k_pack copies them into tok.w)
   int32_t* lab0;  // initial residue labels (= tok[s].x before any merge): the bin pass streams these
-  uint16_t* fp;  // 16-bit fingerprint of pk (0xFFFF = none): the mark scan reads these
+  uint16_t* fp;  // 16-bit fingerprint of pk (0xFFFF = none), written by the bin pass
   // vocab (token id indexed)
   u64 *vh1, *vh2;
   int32_t* vlen;
@@ -139,17 +165,16 @@ struct Dev {
   // key table
   u64* ht_key;
   int64_t HC;
-  int32_t ht_shift, pad1;
+  int32_t ht_shift, hc_log2;
   // dense keys
   u64 *kh1, *kh2;
   int32_t *klen, *krep, *count, *dcount, *touch, *touched, *scratch;
   int64_t KCAP;     // klist capacity (keys)
   // per-workgroup output regions (no global returning atomics on the hot path)
-  int32_t NB;       // mark workgroups (one merge region each)
-  int32_t NBA;      // apply / finalize / bin / import workgroups (one pair region each), NB = RPB*NBA
-  int64_t CH8;      // 8-slot fingerprint groups per mark workgroup
-  int64_t LC;       // merge entries per mark region
-  int64_t RC;       // new pairs / new keys per apply region
+  int32_t NB;       // grid of the streaming helper kernels
+  int32_t NBA;      // find / commit / finalize / bin / import workgroups (one region each)
+  int64_t LC;       // merge entries per find region
+  int64_t RC;       // new pairs / new keys per commit / bin / import region
   LEntry* L;
   int32_t* Lcnt;
   LEntry* Lovf;
@@ -166,9 +191,22 @@ struct Dev {
   int2* post;       // (key, slot) of every live pair at the last rebuild, bucket-sorted per region
   int32_t* poff;    // [NBA][NBKT+1] bucket offsets within a region
   int64_t PR;
-  int2* plog;       // per apply workgroup: (key, slot) of the pairs it made since the rebuild
-  int32_t* plogn;
-  int64_t PLC, LOGMAX;
+  // posting logs: owner j's (key, slot) entries since the rebuild live in pool
+  // chunks pch[j * MAXCH + c], c < pnch[j], the last one filled to pfill[j]
+  int2* pool;
+  int32_t *pch, *pnch, *pfill;
+  int64_t POOL_CH;
+  int32_t CHUNK, MAXCH;
+  // find -> commit records (merge.h)
+  KRec* KS;         // [owner][find wg][SK]
+  int32_t* cntK;    // [owner][find wg]
+  int2* DS;         // [owner][find wg][SD] (key id, count delta)
+  int32_t* cntD;
+  KRec* KO;         // overflow: key records past their fixed slots
+  int64_t KO_cap;
+  int2 *KSid, *KOid;  // k_commit -> k_place: (key id, posting-log position) per record
+  int32_t* T;       // [find wg][TC]: occurrence slots grouped by new key
+  int64_t TC;
   // optional phase timeline (geobpe_debug_timeline): DBG_SLOTS wall-clock stamps per workgroup
   int64_t* dbg;
   int64_t ovf_cap;
@@ -308,8 +346,28 @@ __device__ inline void dbg_stamp(const Dev& D, int k) {
 
 __device__ inline uint32_t post_bkt(int32_t d) { return ((uint32_t)d * 2654435761u) >> (32 - NBKT_LOG2); }
 
-// token record fields (int4 tok[s] = {tid, tlen, tprev, role})
+// token record fields (int4 tok[s] = {tid, tlen, tprev, pk})
 __device__ inline int32_t* tok_f(const Dev& D, int64_t s, int f) { return reinterpret_cast<int32_t*>(D.tok + s) + f; }
+__device__ inline int32_t tok_pk(const Dev& D, int64_t s) { return D.tok[s].w; }
+// tok.y = residues (low 16 bits) | junction symbol after the token (high 16 bits,
+// 0xFFFF = chain end; only when the 16-bit symbols exist, else 0)
+__device__ inline int32_t tok_len(int32_t y) { return y & 0xFFFF; }
+// the junction symbol after a token whose length word is y and last residue e
+__device__ inline int32_t next_glue(const Dev& D, int32_t y, int64_t e) {
+  if (D.gs16) {
+    const uint32_t v = (uint32_t)y >> 16;
+    return v == 0xFFFF ? -1 : (int32_t)v;
+  }
+  return D.gsym[e];
+}
+// junction symbol after residue i (16-bit copy when B^3 fits, else the int32 array)
+__device__ inline int32_t glue(const Dev& D, int64_t i) {
+  if (D.gs16) {
+    const uint16_t v = D.gs16[i];
+    return v == 0xFFFF ? -1 : (int32_t)v;
+  }
+  return D.gsym[i];
+}
 
 __device__ inline uint16_t key_fp(int32_t d) { return (uint16_t)((uint32_t)d % 65535u); }
 
@@ -560,6 +618,10 @@ __device__ inline int32_t ht_resolve(const Dev& D, u64 k, u64 s, u64 cur, bool* 
   set_error(D, GEOBPE_ECAPACITY, -2);
   return -1;
 }
+
+// the commit workgroup that owns a key-table slot / a key (by its first probe slot)
+__device__ inline int owner_of_slot(const Dev& D, u64 s) { return (int)((s * (u64)D.NBA) >> D.hc_log2); }
+__device__ inline int owner_of_key(const Dev& D, u64 pkey) { return owner_of_slot(D, ht_first_slot(D, pkey)); }
 
 __device__ inline int32_t ht_insert(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
   const u64 k = probe_key(h1, h2, len);

@@ -3,15 +3,16 @@
 //
 // Replaces the Python/dict hot path of foldingdiff/bpe.py (BPE.initialize /
 // bin / step / quantize).  Integer work only (no
-// MFMA).  One merge iteration is three stream-ordered launches with no host
+// MFMA).  One merge iteration is four stream-ordered launches with no host
 // synchronisation:
 //   k_select  one 1024-thread workgroup: hot-list argmax + reference key-string
 //             tie-break (wave-parallel comparisons on LDS copies of the tied keys),
 //             the decision record (Sel) and merge-log entry
-//   k_mark    the winner's occurrences (posting index or fingerprint scan) and
-//             greedy run walks
-//   k_apply   rewrite tokens, count deltas, new pair keys (claimed in place),
-//             posting log; rebuild iterations (hot list / posting index)
+//   k_find    the winner's occurrences (posting index), greedy run walks, the new
+//             neighbour keys grouped per owner workgroup (merge.h)
+//   k_commit  per owner: one key-table resolve and one count update per key,
+//             posting-log space; hot-list rebuild iterations
+//   k_place   per region: token rewrites, pk of the occurrences, posting-log entries
 // The bin pass is k_pairs_all + k_finalize.
 
 #include <algorithm>
@@ -66,11 +67,11 @@ struct geobpe_ctx {
   std::vector<std::vector<int32_t>> vocab;
   int32_t K0 = 0;
   int ncu = 256;
-  int nb = 2048;  // mark workgroups (= D.NB)
+  int nb = 2048;  // grid of the streaming helper kernels (= D.NB)
   int64_t gen = 0;            // merge-loop launch pairs so far (parity selects Sel / overflow buffers)
   bool mark_pending = false;  // step_select decided a merge whose mark/apply are due
   bool pipelined = false;     // between geobpe_pipeline_begin and _end (device-side parity)
-  int nba = 256;  // apply / finalize / assign / bin / import workgroups (= D.NBA)
+  int nba = 256;  // find / commit / finalize / bin / import workgroups (= D.NBA, <= NBA_MAX)
   // profiling
   bool prof = false;
   int prof_stride = 1;      // time every prof_stride-th launch of each kernel
@@ -225,6 +226,7 @@ int alloc_keys(geobpe_ctx* c) {
   int sh = 0;
   while ((1LL << sh) < hc) sh++;
   D.ht_shift = 64 - sh;
+  D.hc_log2 = sh;
   int rc;
   // key arrays are indexed by the key id = key-table slot
   if ((rc = dalloc(c, &D.ht_key, D.HC, 0)) || (rc = dalloc(c, &D.kh1, D.HC)) || (rc = dalloc(c, &D.kh2, D.HC)) ||
@@ -240,6 +242,12 @@ int alloc_keys(geobpe_ctx* c) {
   if ((rc = dalloc(c, &D.clist, D.KCAP))) return rc;
   c->keys_ready = true;
   return 0;
+}
+
+// after the bin pass: pair keys into the token records, 16-bit junction symbols
+void enqueue_pack(geobpe_ctx* c) {
+  Timed t(c, "bin_pack");
+  hipLaunchKernelGGL(k_pack, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
 }
 
 // the launches of one merge iteration (no host synchronisation)
@@ -260,14 +268,18 @@ void enqueue_select(geobpe_ctx* c) {
     hipLaunchKernelGGL(k_select, dim3(1), dim3(SBLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
 }
 void enqueue_mark(geobpe_ctx* c) {
-  Timed t(c, "mark");
-  hipLaunchKernelGGL(k_mark, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
+  Timed t(c, "find");
+  hipLaunchKernelGGL(k_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
 }
 void enqueue_apply(geobpe_ctx* c) {
   {
-    Timed t(c, "apply");
-    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0,
+    Timed t(c, "commit");
+    hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0,
                        (int)(c->gen & 1));
+  }
+  {
+    Timed t(c, "place");
+    hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
   }
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1), c->ev, c->ev_cap,
@@ -322,8 +334,8 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->ncu = prop.multiProcessorCount;
-  c->nba = std::min(c->ncu, BLOCK);
-  c->nb = RPB * c->nba;
+  c->nba = std::min(c->ncu, NBA_MAX);
+  c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
   return 0;
@@ -360,6 +372,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
     if (n < 1) return fail(c, GEOBPE_EARG, "row %lld is empty", (long long)r);
     c->Lmax = std::max(c->Lmax, n);
   }
+  if (c->Lmax >= 65535) return fail(c, GEOBPE_EARG, "chain of %lld residues (token lengths are 16-bit)", (long long)c->Lmax);
   c->R = c->row_off[n_rows];
   if (c->R >= INT32_MAX / 4) return fail(c, GEOBPE_EARG, "too many residues for int32 indexing");
   Dev& D = c->D;
@@ -374,28 +387,41 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
     return rc;
   D.row_off = c->d_row_off;
   HIPCHK(c, hipMemcpyAsync(c->d_row_off, h_row_off, (n_rows + 1) * 8, hipMemcpyHostToDevice, c->stream));
-  // per-workgroup regions: a mark workgroup owns CH8 8-slot fingerprint groups
-  // (<= 4 merges per group it owns: LC); an apply workgroup handles RPB mark
-  // regions (<= 2 new pairs / keys per merge: RC)
-  const int64_t n8 = (c->R + 7) / 8;
-  D.CH8 = std::max<int64_t>(1, (n8 + c->nb - 1) / c->nb);
-  D.LC = 4 * D.CH8 + 64;
-  D.RC = 2 * RPB * D.LC + 256;
+  // per-workgroup regions: find region r = residue slots [r*PR, (r+1)*PR) (its
+  // merges: <= PR/2 + slack, the rest to the overflow list; their new keys' slots
+  // T: 2 per merge); commit / bin / import regions: new pairs, claimed keys, found
+  // keys (RC)
+  D.PR = (c->R + c->nba - 1) / c->nba;
+  D.LC = D.PR / 2 + 4096;
+  D.TC = 2 * D.LC;
+  D.RC = 2 * D.LC + (int64_t)c->nba * SK + 256;
   D.Lovf_cap = c->R / 2 + 1024;
   D.ovf_cap = c->R + 1024;
-  if ((rc = dalloc(c, &D.L, (int64_t)c->nb * D.LC)) || (rc = dalloc(c, &D.Lcnt, c->nb, 0)) ||
+  if ((rc = dalloc(c, &D.L, (int64_t)c->nba * D.LC)) || (rc = dalloc(c, &D.Lcnt, c->nba, 0)) ||
       (rc = dalloc(c, &D.Lovf, D.Lovf_cap)) || (rc = dalloc(c, &D.np, (int64_t)c->nba * D.RC)) ||
       (rc = dalloc(c, &D.npcnt, c->nba, 0)) || (rc = dalloc(c, &D.npovf, D.ovf_cap)) ||
       (rc = dalloc(c, &D.ns, (int64_t)c->nba * D.RC)) ||
       (rc = dalloc(c, &D.chk, (int64_t)c->nba * D.RC)) || (rc = dalloc(c, &D.chkcnt, c->nba, 0)))
     return rc;
-  // posting index: one residue region per apply workgroup; the log holds the pairs
-  // made since the last rebuild (k_mark has it rebuilt when it passes LOGMAX)
-  D.PR = (c->R + c->nba - 1) / c->nba;
-  D.LOGMAX = std::max<int64_t>((int64_t)c->nba * 64, c->R / 32);
-  D.PLC = 4 * D.LOGMAX / c->nba + 64;
+  // posting index: one residue region per find workgroup; per-owner logs of the
+  // pairs made since the last rebuild, in CHUNK-entry chunks of one pool of
+  // R + slack entries (a merge makes <= R new pairs; k_select has the index
+  // rebuilt before a merge that might not fit)
+  {
+    int64_t ch = 64;
+    while (ch < 4096 && ch * c->nba * 2 < c->R) ch <<= 1;
+    D.CHUNK = (int32_t)ch;
+  }
+  D.POOL_CH = (c->R + D.CHUNK - 1) / D.CHUNK + 2 * (int64_t)c->nba + 1;
+  D.MAXCH = (int32_t)D.POOL_CH;
+  D.KO_cap = std::max<int64_t>(1 << 16, std::min<int64_t>(c->R, 1 << 20));
   if ((rc = dalloc(c, &D.post, (int64_t)c->nba * D.PR)) || (rc = dalloc(c, &D.poff, (int64_t)c->nba * (NBKT + 1), 0)) ||
-      (rc = dalloc(c, &D.plog, (int64_t)c->nba * D.PLC)) || (rc = dalloc(c, &D.plogn, c->nba, 0)))
+      (rc = dalloc(c, &D.pool, D.POOL_CH * D.CHUNK)) || (rc = dalloc(c, &D.pch, (int64_t)c->nba * D.MAXCH)) ||
+      (rc = dalloc(c, &D.pnch, c->nba, 0)) || (rc = dalloc(c, &D.pfill, c->nba, 0)) ||
+      (rc = dalloc(c, &D.KS, (int64_t)c->nba * c->nba * SK)) || (rc = dalloc(c, &D.cntK, (int64_t)c->nba * c->nba, 0)) ||
+      (rc = dalloc(c, &D.DS, (int64_t)c->nba * c->nba * SD)) || (rc = dalloc(c, &D.cntD, (int64_t)c->nba * c->nba, 0)) ||
+      (rc = dalloc(c, &D.KO, D.KO_cap)) || (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) ||
+      (rc = dalloc(c, &D.KSid, (int64_t)c->nba * c->nba * SK)) || (rc = dalloc(c, &D.KOid, D.KO_cap)))
     return rc;
   const int need[6] = {GEOBPE_COL_PHI, GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_TAU, GEOBPE_COL_CAC1N,
                        GEOBPE_COL_C1NCA};
@@ -468,6 +494,10 @@ int geobpe_quantize(geobpe_ctx* c, int32_t B, const double* h_edges, double init
   D.B = B;
   D.B2 = B * B;
   D.B3 = B * B * B;
+  if (!D.gs16 && (int64_t)B * B * B + B < 65535) {
+    int rc;
+    if ((rc = dalloc(c, &D.gs16, c->R + 8, 0xFF))) return rc;
+  }
   double* de;
   HIPCHK(c, hipMalloc(&de, sizeof(double) * GEOBPE_NTYPES * (B + 1)));
   HIPCHK(c, hipMemcpyAsync(de, h_edges, sizeof(double) * GEOBPE_NTYPES * (B + 1), hipMemcpyHostToDevice, c->stream));
@@ -646,6 +676,7 @@ int geobpe_bin(geobpe_ctx* c) {
         hipLaunchKernelGGL(k_bin_verify, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
       }
     }
+    enqueue_pack(c);
     HIPCHK(c, hipGetLastError());
     rc = sync_state(c);
     if (!rc) {
@@ -664,6 +695,7 @@ int geobpe_bin(geobpe_ctx* c) {
   }
   HIPCHK(c, hipGetLastError());
   enqueue_commit(c, c->distributed);
+  enqueue_pack(c);
   HIPCHK(c, hipGetLastError());
   return sync_state(c);
 }
@@ -852,12 +884,16 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     hipLaunchKernelGGL(k_select, dim3(1), dim3(SBLOCK), 0, c->stream, c->D, -1);
   }
   {
-    Timed t(c, "mark");
-    hipLaunchKernelGGL(k_mark, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, -1);
+    Timed t(c, "find");
+    hipLaunchKernelGGL(k_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
   }
   {
-    Timed t(c, "apply");
-    hipLaunchKernelGGL(k_apply, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
+    Timed t(c, "commit");
+    hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
+  }
+  {
+    Timed t(c, "place");
+    hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, -1);
   }
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
@@ -974,7 +1010,7 @@ int64_t geobpe_debug_state(geobpe_ctx* c, int64_t* h_out, int64_t cap) {
   if (int rc = sync_state(c)) return rc;
   const State& s = *c->h_state;
   const int64_t v[10] = {s.ncl2[s.cl_act], s.theta, s.ncand, s.maxc, s.nskip, s.cl_valid,
-                         s.iter, s.K, s.post_valid, s.plog_total};
+                         s.iter, s.K, s.post_valid, s.pool_used};
   for (int i = 0; i < 10; i++) h_out[i] = v[i];
   return 10;
 }

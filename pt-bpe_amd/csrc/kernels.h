@@ -123,6 +123,20 @@ __global__ __launch_bounds__(BLOCK) void k_first(Dev D, int64_t row_base, u64* f
   }
 }
 
+// after the bin pass: the pair keys join the token records (tok.w = pk), and the
+// 16-bit junction symbols the merge loop reads
+__global__ __launch_bounds__(BLOCK) void k_pack(Dev D) {
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
+    *tok_f(D, g, 3) = D.pk[g];
+    if (D.gs16) {  // (every token is one residue here)
+      const int32_t v = D.gsym[g];
+      const uint32_t g16 = v < 0 ? 0xFFFFu : (uint32_t)v;
+      D.gs16[g] = (uint16_t)g16;
+      *tok_f(D, g, 1) = (int32_t)(1u | (g16 << 16));
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_of_sym) {
   for (int64_t r = blockIdx.x; r < D.nrows; r += gridDim.x) {
     const int64_t a = D.row_off[r], b = D.row_off[r + 1];
@@ -235,13 +249,13 @@ __global__ __launch_bounds__(ABLOCK) void k_pairs_all(Dev D) {
     const int4 tg = D.tok[g];
     const int32_t L = tg.x;
     if (L < 0) continue;
-    const int32_t xlen = tg.y;
+    const int32_t xlen = tok_len(tg.y);
     const int32_t e = (int32_t)g + xlen - 1;
     if (D.rsym[e] >= D.B3) continue;  // last token of its chain
     const int4 te = D.tok[e + 1];
     const int32_t Rr = te.x;
     const int32_t gl = D.gsym[e];
-    const int32_t ylen = te.y;
+    const int32_t ylen = tok_len(te.y);
     u64 h1, h2;
     combine(D, D.vh1[L], D.vh2[L], gl, D.vh1[Rr], D.vh2[Rr], ylen, h1, h2);
     add_pair(D, &s_np, &s_ns, (int32_t)g, h1, h2, xlen + ylen, L, gl, Rr, 1);
@@ -328,61 +342,6 @@ __device__ void measure_max(const Dev& D) {
   }
   m = block_max(m, s_red);
   if (threadIdx.x == 0 && m > 0) atomicMax((unsigned long long*)&D.st->cl_measured, (unsigned long long)m);
-}
-
-// posting-index rebuild (a rebuild iteration, run by k_apply's grid): workgroup r
-// counting-sorts the live pairs of residue region r by key bucket (LDS
-// histogram -> scan -> scatter), writes its bucket offsets and empties its log.
-// No cross-workgroup step: k_mark looks a bucket up in every region.
-__device__ void rebuild_postings(const Dev& D, int32_t* hist) {
-  __shared__ int32_t s_red[ABLOCK / 64];
-  constexpr int PER = NBKT / ABLOCK;
-  const int64_t r = blockIdx.x;
-  const int64_t g0 = r * D.PR, g1 = min(D.R, g0 + D.PR);
-  constexpr int UNR = 16;  // pk loads in flight per thread (the passes are latency-bound otherwise)
-  for (int i = threadIdx.x; i < NBKT; i += ABLOCK) hist[i] = 0;
-  __syncthreads();
-  for (int64_t g = g0 + threadIdx.x; g < g1; g += UNR * ABLOCK) {
-    int32_t d[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; u++) d[u] = g + u * ABLOCK < g1 ? D.pk[g + u * ABLOCK] : -1;
-#pragma unroll
-    for (int u = 0; u < UNR; u++)
-      if (d[u] >= 0) atomicAdd(&hist[post_bkt(d[u])], 1);
-  }
-  __syncthreads();
-  int32_t sum = 0;
-  for (int k = 0; k < PER; k++) sum += hist[threadIdx.x * PER + k];
-  int32_t tot;
-  int32_t run = block_excl_scan(sum, &tot, s_red);
-  int32_t* off = D.poff + r * (NBKT + 1);
-  __syncthreads();
-  for (int k = 0; k < PER; k++) {
-    const int b = threadIdx.x * PER + k;
-    const int32_t c = hist[b];
-    hist[b] = run;
-    off[b] = run;
-    run += c;
-  }
-  if (threadIdx.x == 0) off[NBKT] = tot;
-  __syncthreads();
-  int2* out = D.post + r * D.PR;
-  for (int64_t g = g0 + threadIdx.x; g < g1; g += UNR * ABLOCK) {
-    int32_t d[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; u++) d[u] = g + u * ABLOCK < g1 ? D.pk[g + u * ABLOCK] : -1;
-#pragma unroll
-    for (int u = 0; u < UNR; u++)
-      if (d[u] >= 0) out[atomicAdd(&hist[post_bkt(d[u])], 1)] = make_int2(d[u], (int32_t)(g + u * ABLOCK));
-  }
-  if (threadIdx.x == 0) D.plogn[r] = 0;
-  if (r == 0 && threadIdx.x == 0) {
-    State* st = D.st;
-    st->post_valid = 1;
-    st->plog_ovf = 0;
-    st->plog_total = 0;
-    st->npost += 1;
-  }
 }
 
 __global__ __launch_bounds__(ABLOCK) void k_finalize(Dev D, int to_delta) {
@@ -704,6 +663,15 @@ __device__ inline int32_t wave_tournament(SelStage& S, int32_t nt, int32_t B) {
   return r;
 }
 
+// the posting index must be rebuilt before a merge of count m: never built, a log
+// append was lost, or the log pool cannot take the merge's new pairs (<= 2 per
+// occurrence, <= R in all; each owner may open one more chunk)
+__device__ inline bool post_stale(const Dev& D, int64_t m) {
+  const State* st = D.st;
+  const int64_t need = (min(2 * m, D.R) + D.CHUNK - 1) / D.CHUNK + D.NBA;
+  return st->post_valid == 0 || st->plog_ovf != 0 || st->pool_used + need > D.POOL_CH;
+}
+
 __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
@@ -782,17 +750,13 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     }
     return;
   }
-  // posting index stale (log full / overflowed / never built) and the merges are
-  // small enough that a rebuild lasts >= 64 iterations: rebuild it this iteration
-  const bool post = !hot && (st->post_valid == 0 || st->plog_ovf != 0 || st->plog_total > D.LOGMAX) &&
-                    (int64_t)gm * POST_SPAN <= D.LOGMAX;
-  if (hot || post) {
+  if (hot) {
     if (rec) {
       out->decision = SEL_SKIP;
-      out->skip = (hot ? SKIP_HOT : 0) | (post ? SKIP_POST : 0);
+      out->skip = SKIP_HOT;
       out->theta_new = max(1, gm / 2);
       out->build = act ^ 1;
-      if (hot) st->ncl2[act ^ 1] = 0;
+      st->ncl2[act ^ 1] = 0;
     }
     return;
   }
@@ -884,6 +848,8 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     D.log[iter] = lr;
     out->decision = SEL_MERGE;
     out->skip = 0;
+    out->rebuild = post_stale(D, gm) ? 1 : 0;
+    out->wown = owner_of_key(D, probe_key(w1, w2, wl));
     out->W = W;
     out->nid = K;
     out->iter = iter;
@@ -900,74 +866,6 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
   }
   dbg_stamp(D, 26);
 }
-
-// ====================================================================== merge-apply
-// EHASH check of the keys k_apply found (not claimed) in the previous merge
-// iteration: their content hashes must be the key's canonical ones
-__device__ inline void check_found(const Dev& D, int32_t r) {
-  const int32_t n = D.chkcnt[r];
-  const NewPair* reg = D.chk + (int64_t)r * D.RC;
-  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const NewPair e = reg[i];
-    const int32_t d = e.target;
-    if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) set_error(D, GEOBPE_EHASH, i);
-  }
-}
-
-// a candidate occurrence g of the winner W: confirm it, and if g starts a run
-// of W pairs walk the run greedily left to right (bpe.py:1888-1916) -- merge
-// (t, b), skip the pair (b, c), merge (c, d) if it is W too, ...  Independent
-// loads are issued together: two dependent rounds per hit, two per run step.
-__device__ inline void emit_merge(const Dev& D, int32_t* s_n, int32_t t, int32_t p, int32_t b, int32_t c,
-                                  int32_t tag, int64_t* lovf) {
-  LEntry e;
-  e.a = t;
-  e.p = p;
-  e.b = b;
-  e.c = c;
-  *tok_f(D, t, 3) = (tag << 2) | 1;
-  *tok_f(D, b, 3) = (tag << 2) | 2;
-  const int32_t j = atomicAdd(s_n, 1);
-  if (j < D.LC) {
-    D.L[(int64_t)blockIdx.x * D.LC + j] = e;
-  } else {
-    const int64_t k = atomicAdd((unsigned long long*)lovf, 1ULL);
-    if (k < D.Lovf_cap)
-      D.Lovf[k] = e;
-    else
-      set_error(D, GEOBPE_ECAPACITY, -10);
-  }
-}
-
-__device__ inline void mark_hit(const Dev& D, int32_t g, int32_t W, int32_t tag, int32_t* s_n, int64_t* lovf) {
-  const int32_t pkg = D.pk[g];
-  const int4 tg = D.tok[g];
-  if (pkg != W) return;
-  const int32_t p = tg.z, lg = tg.y;
-  int32_t b = g + lg;
-  const int32_t pkp = D.pk[p >= 0 ? p : g];
-  int32_t pkb = D.pk[b], lb = D.tok[b].y;
-  if (p >= 0 && pkp == W) return;  // not a run start: the run's head walks it
-  int32_t t = g, pp = p;
-  for (;;) {
-    const int32_t c = pkb >= 0 ? b + lb : -1;
-    emit_merge(D, s_n, t, pp, b, c, tag, lovf);
-    if (pkb != W) break;
-    const int32_t pkc = D.pk[c], lc = D.tok[c].y;
-    if (pkc != W) break;
-    const int32_t d = c + lc;
-    pp = b;
-    t = c;
-    b = d;
-    pkb = D.pk[d];
-    lb = D.tok[d].y;
-  }
-}
-
-// The winner's occurrences, starting a walk at every run start.  Posting
-// mode (index valid): O(bucket + log) reads.  Otherwise scan the 16-bit key
-// fingerprints (4 x 16 B per lane in flight; each workgroup owns CH8 8-slot
-// groups), confirm on pk.  Either way one merge region per workgroup.
 
 // merge replay (bin/induce.py): merge t is the trained
 // token K0 + t, not the argmax.  Its key is looked up by content hash (find
@@ -1010,15 +908,6 @@ __global__ __launch_bounds__(64) void k_select_replay(Dev D, int par, const Repl
   }
   const int32_t c = W >= 0 ? D.count[W] : 0;
   if (c <= 0) W = -1;
-  const bool post = c > 0 && (st->post_valid == 0 || st->plog_ovf != 0 || st->plog_total > D.LOGMAX) &&
-                    (int64_t)c * POST_SPAN <= D.LOGMAX;
-  if (post) {
-    out->decision = SEL_SKIP;
-    out->skip = SKIP_POST;
-    out->theta_new = max(1, st->theta);
-    out->build = st->cl_act;
-    return;
-  }
   D.vh1[K] = r.h1;
   D.vh2[K] = r.h2;
   D.vlen[K] = r.len;
@@ -1033,6 +922,8 @@ __global__ __launch_bounds__(64) void k_select_replay(Dev D, int par, const Repl
   D.log[iter] = lr;
   out->decision = SEL_MERGE;
   out->skip = 0;
+  out->rebuild = post_stale(D, c) ? 1 : 0;
+  out->wown = owner_of_key(D, k);
   out->W = W;
   out->nid = K;
   out->iter = iter;
@@ -1048,627 +939,15 @@ __global__ __launch_bounds__(64) void k_select_replay(Dev D, int par, const Repl
   out->widR = r.idR;
 }
 
-__global__ __launch_bounds__(BLOCK) void k_mark(Dev D, int par) {
-  __shared__ int32_t s_n;
-  if (par < 0) {  // pipelined exchange (k_select set dgen)
-    if (D.st->stall) return;
-    par = D.st->dgen & 1;
-  }
-  const bool posting = D.st->post_valid && !D.st->plog_ovf;
-  const Sel& sel = D.sel[par];
-  if (!posting && blockIdx.x < D.NBA) check_found(D, blockIdx.x);
-  if (sel.decision != SEL_MERGE) {
-    if (posting && blockIdx.x % RPB == RPB - 1) check_found(D, blockIdx.x / RPB);
-    return;
-  }
-  if (sel.W < 0) {  // merge replay of a content with no occurrence: empty regions
-    if (posting && blockIdx.x % RPB == RPB - 1) check_found(D, blockIdx.x / RPB);
-    if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = 0;
-    return;
-  }
-  const int32_t W = sel.W, tag = sel.tag;
-  const uint32_t fW = (uint32_t)sel.wfp;
-  int64_t* lovf = &D.st->L_ovf2[par];
-  if (threadIdx.x == 0) s_n = 0;
-  __syncthreads();
-  if (posting) {
-    // posting mode: the winner's bucket in region r (bucket-sorted at the last
-    // rebuild) + region r's log, split over RPB-1 workgroups of the region; the
-    // last one checks the hashes of the keys found in the previous merge
-    const int32_t r = blockIdx.x / RPB, q = blockIdx.x % RPB;
-    if (q == RPB - 1) {
-      check_found(D, r);
-      if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = 0;
-      return;
-    }
-    const int32_t* off = D.poff + (int64_t)r * (NBKT + 1);
-    const uint32_t b = post_bkt(W);
-    const int32_t lo = off[b], n1 = off[b + 1] - lo;
-    const int32_t ntot = n1 + D.plogn[r];
-    const int32_t per = (ntot + RPB - 2) / (RPB - 1);
-    const int32_t i1 = min(ntot, (q + 1) * per);
-    const int2* P = D.post + (int64_t)r * D.PR + lo;
-    const int2* Lg = D.plog + (int64_t)r * D.PLC - n1;
-    for (int32_t i = q * per + threadIdx.x; i < i1; i += BLOCK) {
-      const int2 e = i < n1 ? P[i] : Lg[i];
-      if (e.x == W) {
-        const int32_t g = e.y;
-        mark_hit(D, g, W, tag, &s_n, lovf);
-      }
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = min(s_n, (int32_t)D.LC);
-    return;
-  }
-  // Fingerprint scan in chunks of UNR x BLOCK 8-slot groups.  The hits of a chunk
-  // are compacted into an LDS queue (per-lane hit counts -> wave prefix sum -> one
-  // LDS reservation per wave), then confirmed and walked one candidate per thread:
-  // the dependent loads of every hit are in flight together.  (Walking each hit
-  // where the scan finds it serialises the wave over its lanes' hits: ~17 hits per
-  // wave and chunk in the heavy merges, 3 dependent round trips each.)
-  const int64_t n8 = (D.R + 7) / 8;
-  const int64_t lo = (int64_t)blockIdx.x * D.CH8, hi = min(n8, lo + D.CH8);
-  const uint4* f4 = reinterpret_cast<const uint4*>(D.fp);
-  constexpr int UNR = 8;
-  constexpr int MQ = 2048;  // candidates per chunk (more: walked in place)
-  __shared__ int32_t s_q[MQ];
-  __shared__ int32_t s_qn;
-  for (int64_t c0 = lo; c0 < hi; c0 += UNR * BLOCK) {  // block-uniform
-    if (threadIdx.x == 0) s_qn = 0;
-    const int64_t i0 = c0 + threadIdx.x;
-    uint4 v[UNR];
-#pragma unroll
-    for (int u = 0; u < UNR; u++) {
-      const int64_t i = i0 + u * BLOCK;
-      v[u] = i < hi ? f4[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    }
-    int32_t nh = 0;
-#pragma unroll
-    for (int u = 0; u < UNR; u++) {
-      const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-      for (int q = 0; q < 8; q++) nh += ((w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu) == fW;
-    }
-    int32_t wt;
-    const int32_t ex = wave_excl_scan(nh, wt);
-    __syncthreads();  // s_qn reset visible
-    int32_t base = 0;
-    if (wave_lane() == 0 && wt) base = atomicAdd(&s_qn, wt);
-    int32_t j = __shfl(base, 0, 64) + ex;
-    if (nh) {
-#pragma unroll
-      for (int u = 0; u < UNR; u++) {
-        const uint32_t w[4] = {v[u].x, v[u].y, v[u].z, v[u].w};
-#pragma unroll
-        for (int q = 0; q < 8; q++) {
-          if (((w[q >> 1] >> (16 * (q & 1))) & 0xFFFFu) == fW) {
-            const int32_t g = (int32_t)(8 * (i0 + u * BLOCK) + q);
-            if (j < MQ)
-              s_q[j] = g;
-            else
-              mark_hit(D, g, W, tag, &s_n, lovf);
-            j++;
-          }
-        }
-      }
-    }
-    __syncthreads();
-    const int32_t nq = min(s_qn, MQ);
-    for (int32_t i = threadIdx.x; i < nq; i += BLOCK) mark_hit(D, s_q[i], W, tag, &s_n, lovf);
-    __syncthreads();  // the queue is reused by the next chunk
-  }
-  if (threadIdx.x == 0) D.Lcnt[blockIdx.x] = min(s_n, (int32_t)D.LC);
-}
-
-// rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014).
-// Latency-bound: every independent load is issued before any store.  New pair
-// keys get their id (key-table slot) here, so pk and the counts are final when the
-// kernel ends -- no separate finalize launch in the merge loop.
-struct ApplyCtx {
-  int32_t W, nid, wl, tagL, tagR, theta;
-  u64 w1, w2;
-  const u64* spw;                   // hash powers in LDS: base 1 at [0, PW_LDS), base 2 at [PW_LDS, 2 PW_LDS)
-  int32_t spwn;                     // entries staged per base
-  bool to_delta;
-};
-// P^k of both bases: LDS when staged, else global
-__device__ inline void pw_pair(const Dev& D, const ApplyCtx& A, int64_t k, u64& p1, u64& p2) {
-  if (k < A.spwn) {
-    p1 = A.spw[k];
-    p2 = A.spw[PW_LDS + k];
-  } else {
-    p1 = D.pw1[k];
-    p2 = D.pw2[k];
-  }
-}
-
-struct WgLog {  // this workgroup's posting log cursor (LDS)
-  int32_t n0, n, ovf;
-};
-
-// a pair made in this merge joins the posting log (k_mark finds it there until
-// the next posting rebuild)
-__device__ inline void log_pair(const Dev& D, WgLog& lg, int32_t d, int32_t slot) {
-  const int32_t j = atomicAdd(&lg.n, 1);
-  if (j < D.PLC)
-    D.plog[(int64_t)blockIdx.x * D.PLC + j] = make_int2(d, slot);
-  else
-    lg.ovf = 1;
-}
-
-// record of a key found (not claimed) in this launch: k_mark of the next
-// iteration checks it against the key's canonical hashes (EHASH)
-__device__ inline void emit_check(const Dev& D, int32_t* s_np, int32_t d, int32_t len, u64 h1, u64 h2) {
-  NewPair e;
-  e.target = d;
-  e.slot = -1;
-  e.len = len;
-  e.delta = 0;
-  e.h1 = h1;
-  e.h2 = h2;
-  const int32_t j = atomicAdd(s_np, 1);
-  if (j < D.RC)
-    D.chk[(int64_t)blockIdx.x * D.RC + j] = e;
-  else
-    atomicAdd((unsigned long long*)&D.st->nunchecked, 1ULL);
-}
-
-__device__ inline int32_t key_id_now(const Dev& D, int32_t* s_ns, int32_t* s_chk, u64 k, u64 s, u64 cur, u64 h1, u64 h2,
-                                     int32_t len, int32_t idL, int32_t g, int32_t idR) {
-  bool claimed;
-  const int32_t slot = ht_resolve(D, k, s, cur, &claimed);
-  if (slot < 0) return -1;
-  if (claimed) {
-    claim_payload(D, slot, h1, h2, len, idL, g, idR);
-    note_claim(D, s_ns, slot);
-  } else {
-    emit_check(D, s_chk, slot, len, h1, h2);
-  }
-  return slot;
-}
-
-// per-workgroup key cache (LDS): the occurrences a workgroup handles often make
-// the same new pair key; one thread (the resolver) goes to the global table, the
-// others take its dense id from LDS after the round's barrier -- the global CAS /
-// polling traffic per key is one per workgroup, not one per occurrence
-constexpr int KC_SZ = 2048;
-struct KeyCache {
-  u64 key[KC_SZ];
-  u64 h1[KC_SZ];
-  int32_t id[KC_SZ];  // -2: the resolver failed (error already set)
-};
-__device__ inline void kc_init(KeyCache& kc) {
-  for (int i = threadIdx.x; i < KC_SZ; i += blockDim.x) kc.key[i] = 0;
-}
-// slot of k in the cache (*res: this thread inserted it), -1 if the cache is full there
-__device__ inline int32_t kc_find(KeyCache& kc, u64 k, bool* res) {
-  int32_t h = (int32_t)((k * 0x9E3779B97F4A7C15ULL) >> 53);  // log2(KC_SZ) bits
-#pragma unroll 1
-  for (int probe = 0; probe < 16; probe++, h = (h + 1) & (KC_SZ - 1)) {
-    const u64 c = kc.key[h];
-    if (c == k) {
-      *res = false;
-      return h;
-    }
-    if (c == 0) {
-      const u64 old = atomicCAS((unsigned long long*)&kc.key[h], 0ULL, (unsigned long long)k);
-      if (old == 0 || old == k) {
-        *res = old == 0;
-        return h;
-      }
-    }
-  }
-  *res = true;
-  return -1;
-}
-
-// one new neighbour pair of a merged occurrence, between its key computation
-// and its dense id
-struct Half {
-  u64 k, s, cur, h1, h2;
-  int32_t len, idL, g, idR, target, kcs, d;
-  bool res;
-};
-
-// rewrite one merged occurrence and issue its count deltas (bpe.py:1924-2014)
-// up to the keys of its new neighbour pairs (step 5 finishes in k_apply).
-// Latency-bound: every independent load is issued before any store.
-__device__ inline void apply_front(const Dev& D, AggBig& agg, HotApp& hot, const LEntry e, const ApplyCtx& A, Half& hl,
-                                   bool& vl, Half& hr, bool& vr, int dk) {
-  const bool hasP = e.p >= 0, hasC = e.c >= 0;
-  // one round: everything that depends only on the entry, the neighbours' content
-  // hashes included (the per-slot token-hash cache th1/th2 + tlen).  Loads from
-  // valid addresses, then selects by value: a conditional load with a fallback
-  // in ApplyCtx would become a flat load through the scratch stack.
-  const int32_t ip = hasP ? e.p : e.a, ic = hasC ? e.c : e.a;
-  const int32_t pkb = D.pk[e.b];
-  const int4 tp = D.tok[ip], tcr = D.tok[ic];  // {tid, tlen, tprev, role} of p and c
-  const int32_t pkp0 = D.pk[ip];
-  const int32_t glL = hasP ? D.gsym[e.a - 1] : 0;
-  const int32_t glR = hasC ? D.gsym[e.a + A.wl - 1] : 0;
-  const int32_t rp = tp.w, L0 = tp.x, ll0 = tp.y;
-  const int32_t rc0 = tcr.w, tc = tcr.x, rl0 = tcr.y;
-  // the neighbours' content hashes by token id (vocab: small, L2-resident).  A
-  // right part p (or a left part c) is being rewritten by another thread: its
-  // id may read as -1 / the new id, and is not used then (pN / cL below)
-  const int32_t vp = max(L0, 0), vc = max(tc, 0);
-  const u64 l1 = D.vh1[vp], l2 = D.vh2[vp];
-  const u64 c1 = D.vh1[vc], c2 = D.vh2[vc];
-  const int32_t pkp = hasP ? pkp0 : -1;
-  const int32_t L = hasP ? L0 : 0;
-  const int32_t ll = ll0;
-  const bool pN = hasP && rp != A.tagR;  // p is never a left part; R or untouched
-  const bool cL = hasC && rc0 == A.tagL;
-  const int32_t idr = cL ? A.nid : tc;
-  const bool rN = hasC && !cL;
-  const u64 r1 = rN ? c1 : A.w1, r2 = rN ? c2 : A.w2;
-  const int32_t rl = rN ? rl0 : A.wl;
-  u64 pr1a = 0, pr1b = 0, pr2a = 0, pr2b = 0;
-  if (hasC) {
-    const int64_t ny = 2 * (int64_t)rl - 1;
-    pw_pair(D, A, ny + 1, pr1a, pr2a);
-    pw_pair(D, A, ny, pr1b, pr2b);
-  }
-  // new pair keys and their first table probes (issued together)
-  vl = pN;
-  vr = hasC;
-  if (pN) {  // X ++ g ++ W: powers of W's length
-    u64 pa1, pa2, pb1, pb2;
-    const int64_t nw = 2 * (int64_t)A.wl - 1;
-    pw_pair(D, A, nw + 1, pa1, pa2);
-    pw_pair(D, A, nw, pb1, pb2);
-    combine_pw(l1, l2, glL, A.w1, A.w2, pa1, pb1, pa2, pb2, hl.h1, hl.h2);
-    hl.len = ll + A.wl;
-    hl.k = probe_key(hl.h1, hl.h2, hl.len);
-    hl.s = ht_first_slot(D, hl.k);
-    hl.cur = ht_probe(D, hl.s);
-    hl.idL = L;
-    hl.g = glL;
-    hl.idR = A.nid;
-    hl.target = e.p;
-  }
-  if (hasC) {
-    combine_pw(A.w1, A.w2, glR, r1, r2, pr1a, pr1b, pr2a, pr2b, hr.h1, hr.h2);
-    hr.len = A.wl + rl;
-    hr.k = probe_key(hr.h1, hr.h2, hr.len);
-    hr.s = ht_first_slot(D, hr.k);
-    hr.cur = ht_probe(D, hr.s);
-    hr.idL = A.nid;
-    hr.g = glR;
-    hr.idR = idr;
-    hr.target = e.a;
-  }
-  // count deltas: step 4 (right neighbour pair) and step 3 (left neighbour pair);
-  // step 1 (the merged pair, -1 on W) is counted once per workgroup by the caller
-  if (dk >= 0) dbg_stamp(D, dk);
-  if (pkb >= 0) agg_add_hot(agg, D, hot, pkb, -1, A.to_delta, A.theta);
-  if (pN) agg_add_hot(agg, D, hot, pkp, -1, A.to_delta, A.theta);
-  if (dk >= 0) dbg_stamp(D, dk + 1);
-  // step 2: bond_to_token / token_pos
-  *reinterpret_cast<int2*>(D.tok + e.a) = make_int2(A.nid, A.wl);
-  *tok_f(D, e.b, 0) = -1;
-  D.pk[e.b] = -1;
-  D.fp[e.b] = 0xFFFF;
-  if (hasC) {
-    *tok_f(D, e.c, 2) = e.a;
-  } else {
-    D.pk[e.a] = -1;
-    D.fp[e.a] = 0xFFFF;
-  }
-}
-
-// before the round's barrier: look the key up in the workgroup cache; the
-// resolver (or an uncached thread) gets the dense id from the global table
-// after a claimed/found slot: payload + klist note, or the EHASH check record
-__device__ inline int32_t key_done(const Dev& D, int32_t* s_ns, int32_t* s_chk, const Half& x, int32_t slot,
-                                   bool claimed) {
-  if (slot < 0) return -1;
-  if (claimed) {
-    claim_payload(D, slot, x.h1, x.h2, x.len, x.idL, x.g, x.idR);
-    note_claim(D, s_ns, slot);
-  } else {
-    emit_check(D, s_chk, slot, x.len, x.h1, x.h2);
-  }
-  return slot;
-}
-
-// Before the round's barrier: look both halves up in the workgroup cache; the
-// resolvers go to the global table.  A key first seen in this launch is probed
-// by up to one resolver per workgroup at about the same time: a CAS each would
-// queue ~256 same-address atomics (~70 ns apiece).  So a resolver that finds the
-// slot empty waits a workgroup-dependent moment and probes again (agent scope),
-// and CASes only if it is still empty; the L and R halves' first CASes are
-// issued back to back.
-__device__ inline void halves_resolve(const Dev& D, KeyCache& kc, int32_t* s_ns, int32_t* s_chk, Half& a, bool va,
-                                      Half& b, bool vb, int dk) {
-  if (va) a.kcs = kc_find(kc, a.k, &a.res);
-  if (vb) b.kcs = kc_find(kc, b.k, &b.res);
-  if (dk >= 0) dbg_stamp(D, dk);
-  a.d = b.d = -1;
-  const bool ra = va && a.res, rb = vb && b.res;
-  u64 ca = ra ? a.cur : 1, cb = rb ? b.cur : 1;  // (1: no slot work for that half)
-#ifndef GB_NO_STAGGER
-  if ((ra && ca == 0) || (rb && cb == 0)) {
-    for (int i = 0; i < 1 + (int)(blockIdx.x & 15); i++) __builtin_amdgcn_s_sleep(2);
-    if (ra && ca == 0) ca = ht_probe(D, a.s);
-    if (rb && cb == 0) cb = ht_probe(D, b.s);
-  }
-#endif
-  if (dk >= 0) dbg_stamp(D, dk + 1);
-  u64 oa = ca, ob = cb;
-  bool cla = false, clb = false;
-  if (ra && ca == 0) oa = atomicCAS((unsigned long long*)&D.ht_key[a.s], 0ULL, (unsigned long long)a.k);
-  if (rb && cb == 0) ob = atomicCAS((unsigned long long*)&D.ht_key[b.s], 0ULL, (unsigned long long)b.k);
-  if (dk >= 0 && (oa | ob) == 12345) dbg_stamp(D, 63);  // (keeps the CAS results live before the next stamp)
-  if (dk >= 0) dbg_stamp(D, dk + 2);
-  if (ra) {
-    int32_t slot;
-    if (ca == 0 && oa == 0) {
-      cla = true;
-      slot = (int32_t)a.s;
-    } else if (oa == a.k) {
-      slot = (int32_t)a.s;
-    } else {  // another key here: probe on
-      slot = ht_resolve(D, a.k, (a.s + 1) & ((u64)D.HC - 1), ht_probe(D, (a.s + 1) & ((u64)D.HC - 1)), &cla);
-    }
-    a.d = key_done(D, s_ns, s_chk, a, slot, cla);
-  }
-  if (rb) {
-    int32_t slot;
-    if (cb == 0 && ob == 0) {
-      clb = true;
-      slot = (int32_t)b.s;
-    } else if (ob == b.k) {
-      slot = (int32_t)b.s;
-    } else {
-      slot = ht_resolve(D, b.k, (b.s + 1) & ((u64)D.HC - 1), ht_probe(D, (b.s + 1) & ((u64)D.HC - 1)), &clb);
-    }
-    b.d = key_done(D, s_ns, s_chk, b, slot, clb);
-  }
-  if (dk >= 0) dbg_stamp(D, dk + 3);
-  if (va && a.res && a.kcs >= 0) {
-    kc.h1[a.kcs] = a.h1;
-    kc.id[a.kcs] = a.d >= 0 ? a.d : -2;
-  }
-  if (vb && b.res && b.kcs >= 0) {
-    kc.h1[b.kcs] = b.h1;
-    kc.id[b.kcs] = b.d >= 0 ? b.d : -2;
-  }
-}
-
-// after the barrier: followers read the id; then pk / counts / posting log
-__device__ inline void half_finish(const Dev& D, AggBig& agg, HotApp& hot, KeyCache& kc, WgLog& lg, Half& x,
-                                   const ApplyCtx& A, int dk) {
-  if (!x.res) {
-    x.d = kc.id[x.kcs];
-    if (x.d >= 0 && kc.h1[x.kcs] != x.h1) {  // same probe key, other content
-      set_error(D, GEOBPE_EHASH, -13);
-      x.d = -1;
-    }
-  }
-  if (x.d < 0) return;
-  if (dk >= 0) dbg_stamp(D, dk);
-  D.pk[x.target] = x.d;
-  D.fp[x.target] = key_fp(x.d);
-  log_pair(D, lg, x.d, x.target);
-  if (dk >= 0) dbg_stamp(D, dk + 1);
-  agg_add_hot(agg, D, hot, x.d, 1, A.to_delta, A.theta);
-  if (dk >= 0) dbg_stamp(D, dk + 2);
-}
-
-// BPE.step's merge-apply (bpe.py:1888-2014) for this workgroup's RPB mark
-// regions (+ its share of the overflow list), in block-uniform rounds: front
-// half, key resolution, barrier, finish.  Also the merge log's n_merged, and
-// the rebuild iterations (hot list / posting index) k_select requests.
-__global__ __launch_bounds__(ABLOCK) void k_apply(Dev D, int to_delta, int par) {
-  // the posting rebuild's histogram and the merge's partial counts never live in
-  // the same launch: one 64 KB LDS buffer
-  __shared__ union {
-    AggBig agg;
-    int32_t hist[NBKT];
-  } u;
-  static_assert(sizeof(AggBig) == sizeof(int32_t) * NBKT, "LDS union layout");
-  AggBig& agg = u.agg;
-  __shared__ HotApp hot;
-  __shared__ WgLog lg;
-  __shared__ KeyCache kc;
-  __shared__ int32_t s_chk, s_ns;
-  __shared__ int32_t s_off[RPB + 1];
-  __shared__ int32_t s_red[ABLOCK / 64];
-  __shared__ u64 s_pw[2 * PW_LDS];
-  __shared__ int64_t s_kl[2];
-  State* st = D.st;
-  if (par < 0) {  // pipelined exchange (k_select set dgen)
-    if (st->stall) return;
-    par = st->dgen & 1;
-  }
-  const Sel sel = D.sel[par];  // this launch pair's decision (k_mark)
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->L_ovf2[par ^ 1] = 0;  // the next mark's overflow counter (idle since the last pair)
-    if (sel.decision == SEL_DONE) {
-      st->done = 1;
-      st->maxc = 0;
-    } else if (sel.decision == SEL_SKIP) {
-      st->nskip += 1;
-    }
-  }
-  if (sel.decision == SEL_DONE) return;
-  if (sel.decision == SEL_SKIP) {
-    if (sel.skip & SKIP_MEASURE) measure_max(D);
-    if (sel.skip & SKIP_HOT) rebuild_hot_list(D, sel.theta_new, sel.build);
-    if (sel.skip & SKIP_POST) rebuild_postings(D, u.hist);
-    return;
-  }
-  dbg_stamp(D, 0);
-  agg_init(agg);
-  hot_init(hot);
-  kc_init(kc);
-  ApplyCtx A;
-  A.W = sel.W;
-  A.nid = sel.nid;
-  const int32_t tag = sel.tag;
-  A.tagR = (tag << 2) | 2;
-  A.tagL = (tag << 2) | 1;
-  A.theta = st->theta;
-  A.to_delta = to_delta != 0;
-  A.w1 = sel.w1;
-  A.w2 = sel.w2;
-  A.wl = sel.wl;
-  A.spw = s_pw;
-  A.spwn = (int32_t)min(D.pwn, (int64_t)PW_LDS);
-  for (int i = threadIdx.x; i < A.spwn; i += blockDim.x) {
-    s_pw[i] = D.pw1[i];
-    s_pw[PW_LDS + i] = D.pw2[i];
-  }
-  if (blockIdx.x == 0) {  // _tokens[n] = json.loads(key): content(L) ++ [g] ++ content(R)
-    const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
-    const int64_t vL = D.voff[L], vR = D.voff[Rr];
-    const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
-    const int64_t pos = D.voff[A.nid], ln = nL + 1 + nR;
-    if (pos + ln > D.VSC) {
-      if (threadIdx.x == 0) set_error(D, GEOBPE_ECAPACITY, -9);
-    } else {
-      for (int64_t i = threadIdx.x; i < ln; i += blockDim.x)
-        D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
-      if (threadIdx.x == 0) D.voff[A.nid + 1] = pos + ln;
-    }
-  }
-  if (threadIdx.x < 64) {  // this workgroup's RPB mark regions: offsets by a wave scan
-    const int32_t c = threadIdx.x < RPB ? D.Lcnt[blockIdx.x * RPB + threadIdx.x] : 0;
-    int32_t tot;
-    const int32_t ex = wave_excl_scan(c, tot);
-    if (threadIdx.x < RPB) s_off[threadIdx.x] = ex;
-    if (threadIdx.x == 0) {
-      s_off[RPB] = tot;
-      s_chk = 0;
-      s_ns = 0;
-      lg.n0 = lg.n = D.plogn[blockIdx.x];
-      lg.ovf = 0;
-      s_kl[0] = D.kchunk[2 * blockIdx.x];
-      s_kl[1] = D.kchunk[2 * blockIdx.x + 1];
-    }
-  }
-  // speculative load of the first PRE entries of each of the RPB mark regions, in
-  // the same round as the state (late merges have a few entries per region)
-  constexpr int PRE = ABLOCK / RPB;
-  const int pr = threadIdx.x / PRE, pi = threadIdx.x % PRE;
-  LEntry pre;
-  if (pi < D.LC) pre = D.L[(int64_t)(blockIdx.x * RPB + pr) * D.LC + pi];
-  int32_t nm = 0;
-  if (blockIdx.x == 0) {  // merges applied this iteration -> merge log
-    const int4* l4 = reinterpret_cast<const int4*>(D.Lcnt);  // NB % 4 == 0
-    for (int32_t i = threadIdx.x; i < D.NB / 4; i += blockDim.x) {
-      const int4 v = l4[i];
-      nm += v.x + v.y + v.z + v.w;
-    }
-  }
-  __syncthreads();
-  const int32_t E = s_off[RPB];
-  const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
-  const int64_t oper = (novf + gridDim.x - 1) / gridDim.x;
-  const int64_t o_lo = (int64_t)blockIdx.x * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
-  dbg_stamp(D, 1);
-  int dbk = 2;
-  // one block-uniform round: front half, key resolution, barrier, finish
-  auto round = [&](bool act, const LEntry& e, bool ovf, int64_t j0) {
-    Half hl, hr;
-    bool vl = false, vr = false;
-    if (act) {
-      if (ovf) agg_add_hot(agg, D, hot, A.W, -1, A.to_delta, A.theta);  // step 1 for an overflow entry
-      apply_front(D, agg, hot, e, A, hl, vl, hr, vr, j0 < 2 * ABLOCK ? 40 + 10 * (int)(j0 / ABLOCK) : -1);
-    }
-    dbg_stamp(D, dbk++);
-    if (vl || vr) halves_resolve(D, kc, &s_ns, &s_chk, hl, vl, hr, vr, j0 == 0 ? 30 : -1);
-    dbg_stamp(D, dbk++);
-    __syncthreads();
-    dbg_stamp(D, dbk++);
-    if (vl) half_finish(D, agg, hot, kc, lg, hl, A, j0 < 2 * ABLOCK ? 42 + 10 * (int)(j0 / ABLOCK) : -1);
-    if (vr) half_finish(D, agg, hot, kc, lg, hr, A, j0 < 2 * ABLOCK ? 45 + 10 * (int)(j0 / ABLOCK) : -1);
-    dbg_stamp(D, dbk++);
-  };
-  // round 0: the prefetched entries
-  const int32_t cnt_r = s_off[pr + 1] - s_off[pr];
-  round(pi < cnt_r && pi < D.LC, pre, false, 0);
-  // then the rest of each region (entries >= PRE) and this workgroup's overflow share
-  __shared__ int32_t s_off2[RPB + 1];
-  if (threadIdx.x == 0) {
-    int32_t acc = 0;
-    for (int r = 0; r < RPB; r++) {
-      s_off2[r] = acc;
-      acc += max(0, s_off[r + 1] - s_off[r] - PRE);
-    }
-    s_off2[RPB] = acc;
-  }
-  __syncthreads();
-  const int32_t E2 = s_off2[RPB];
-  const int64_t total = E2 + o_n;
-  for (int64_t j0 = 0; j0 < total; j0 += blockDim.x) {
-    const int64_t j = j0 + threadIdx.x;
-    LEntry e;
-    bool ovf = false;
-    if (j < E2) {
-      int r = 0;
-      while (j >= s_off2[r + 1]) r++;
-      e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + PRE + (j - s_off2[r])];
-    } else if (j < total) {
-      e = D.Lovf[o_lo + (j - E2)];
-      ovf = true;
-    }
-    round(j < total, e, ovf, j0 + ABLOCK);
-  }
-  dbg_stamp(D, 60);
-  agg_flush_hot(agg, D, hot, A.to_delta, A.theta);  // (syncs the workgroup first)
-  dbg_stamp(D, 61);
-  if (threadIdx.x == 0) {
-    if (E) global_add(D, A.W, -E, A.to_delta);  // step 1 for the region entries
-    D.chkcnt[blockIdx.x] = min(s_chk, (int32_t)D.RC);
-    const int32_t ln = min(lg.n, (int32_t)D.PLC);
-    D.plogn[blockIdx.x] = ln;
-    if (ln > lg.n0) atomicAdd((unsigned long long*)&st->plog_total, (unsigned long long)(ln - lg.n0));
-    if (lg.ovf) st->plog_ovf = 1;
-  }
-  // this workgroup's claims join klist from its chunk (a reservation only when
-  // the chunk runs out; the chunk state was read at kernel start)
-  __syncthreads();
-  {
-    const int32_t n = min(s_ns, (int32_t)D.RC);
-    if (threadIdx.x == 0 && n) {
-      if (s_kl[1] - s_kl[0] < n) {
-        const int64_t sz = max((int64_t)KL_CHUNK, (int64_t)n);
-        s_kl[0] = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
-        s_kl[1] = s_kl[0] + sz;
-      }
-      D.kchunk[2 * blockIdx.x] = s_kl[0] + n;
-      D.kchunk[2 * blockIdx.x + 1] = s_kl[1];
-      atomicAdd((unsigned long long*)&st->nkeys, (unsigned long long)n);
-    }
-    __syncthreads();
-    const int32_t* reg = D.ns + (int64_t)blockIdx.x * D.RC;
-    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) klist_put(D, s_kl[0] + i, reg[i]);
-  }
-  dbg_stamp(D, 62);
-  if (blockIdx.x == 0) {
-    int32_t tot;
-    block_excl_scan(nm, &tot, s_red);
-    if (threadIdx.x == 0) {
-      D.log[sel.iter].nmerged = (int64_t)tot + novf;
-      st->iter = sel.iter + 1;
-      st->K = sel.nid + 1;
-      st->maxc = sel.maxc;
-      st->ncand = sel.ncand;
-    }
-  }
-  dbg_stamp(D, 63);
-}
+#include "merge.h"
 
 // ====================================================================== multi-rank deltas
 // merge events for the checkpoint's merge tree (TokenHierarchy / BinaryTreeBuilder.
-// combine, data_structures.py:32-60, 217-226): after a merge iteration's k_apply,
+// combine, data_structures.py:32-60, 217-226): after a merge iteration's k_commit,
 // (merge index, left token start, right token start) of every merged occurrence
-// from the mark regions and the overflow list.  Record mode only (one launch per
+// from the find regions and the overflow list.  Record mode only (one launch per
 // iteration); the hot kernels are unchanged.
 __global__ __launch_bounds__(BLOCK) void k_events(Dev D, int par, int4* ev, int64_t cap, unsigned long long* ev_n) {
-  __shared__ int32_t s_off[RPB + 1];
   __shared__ int64_t s_base;
   if (par < 0) {  // pipelined exchange (k_select set dgen)
     if (D.st->stall) return;
@@ -1679,22 +958,14 @@ __global__ __launch_bounds__(BLOCK) void k_events(Dev D, int par, int4* ev, int6
   const int64_t novf = min(D.st->L_ovf2[par], D.Lovf_cap);
   const int64_t per = (novf + gridDim.x - 1) / gridDim.x;
   const int64_t o_lo = min(novf, (int64_t)blockIdx.x * per), o_hi = min(novf, o_lo + per);
+  const int32_t nreg = blockIdx.x < D.NBA ? D.Lcnt[blockIdx.x] : 0;  // find region blockIdx.x
   if (threadIdx.x == 0) {
-    int32_t acc = 0;
-    for (int r = 0; r < RPB; r++) {
-      s_off[r] = acc;
-      acc += D.Lcnt[blockIdx.x * RPB + r];
-    }
-    s_off[RPB] = acc;
-    const int64_t n = acc + (o_hi - o_lo);
+    const int64_t n = nreg + (o_hi - o_lo);
     s_base = n ? (int64_t)atomicAdd(ev_n, (unsigned long long)n) : 0;
   }
   __syncthreads();
-  const int32_t nreg = s_off[RPB];
   for (int32_t j = threadIdx.x; j < nreg; j += BLOCK) {
-    int r = 0;
-    while (j >= s_off[r + 1]) r++;
-    const LEntry e = D.L[(int64_t)(blockIdx.x * RPB + r) * D.LC + (j - s_off[r])];
+    const LEntry e = D.L[(int64_t)blockIdx.x * D.LC + j];
     if (s_base + j < cap) ev[s_base + j] = make_int4(sel.iter, e.a, e.b, 0);
   }
   for (int64_t k = o_lo + threadIdx.x; k < o_hi; k += BLOCK) {
@@ -1841,7 +1112,7 @@ __global__ __launch_bounds__(BLOCK) void k_row_ntok(Dev D, int64_t* ntok) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.nrows; r += (int64_t)gridDim.x * blockDim.x) {
     const int64_t a = D.row_off[r], b = D.row_off[r + 1];
     int64_t n = 0;
-    for (int64_t g = a; g < b; g += D.tok[g].y) n++;
+    for (int64_t g = a; g < b; g += tok_len(D.tok[g].y)) n++;
     ntok[r] = n;
   }
 }
@@ -1855,7 +1126,7 @@ __global__ __launch_bounds__(BLOCK) void k_row_seg(Dev D, const int64_t* tok_off
       start[t] = (int32_t)(g - a);
       id[t] = tg.x;
       t++;
-      g += tg.y;
+      g += tok_len(tg.y);
     }
   }
 }
@@ -1869,7 +1140,7 @@ __global__ __launch_bounds__(BLOCK) void k_row_encode(Dev D, const int64_t* id_o
     int64_t t = id_off[r];
     for (int64_t g = a; g < b;) {
       const int4 tg = D.tok[g];
-      const int64_t e = g + tg.y - 1;
+      const int64_t e = g + tok_len(tg.y) - 1;
       ids[t++] = tg.x;
       if (e + 1 < b) {
         const int32_t gs = D.gsym[e];
@@ -1887,7 +1158,7 @@ __global__ __launch_bounds__(BLOCK) void k_recount(Dev D) {
   __shared__ Agg agg;
   agg_init(agg);
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t d = D.pk[g];
+    const int32_t d = tok_pk(D, g);
     if (d >= 0 && !agg_stage(agg, d, 1)) atomicAdd(&D.scratch[d], 1);
   }
   __syncthreads();

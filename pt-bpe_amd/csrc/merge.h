@@ -1,0 +1,1017 @@
+// merge.h -- one merge of BPE.step (foldingdiff/bpe.py:1792-2166) after k_select has
+// chosen the winner W: k_find and k_commit.  Included once, by kernels.h.
+//
+// The cost of a merge is global-memory round trips and global atomics.  A design
+// where every workgroup resolves the new pair keys of its own occurrences sends
+// each hot key to the key table once per workgroup (256 same-address CASes) and
+// each count to memory once per (workgroup, key) -- in the heavy early merges that
+// was 30 of k_apply's 56 us (profiles/r2_base/apply_timeline.txt).  Here every key
+// has ONE owner workgroup, chosen from its content (the first key-table slot of its
+// probe key): find workgroups group their occurrences' new keys and count
+// decrements by owner, commit workgroups aggregate each owner's keys across all
+// finders, resolve every key once and update every count once.
+//
+//  k_find   (NBA x 1024; read-only on the token state): the winner's candidate
+//           slots from the posting index (region r's bucket of W + 1/NBA of the
+//           log of W's owner), run starts, greedy walks, neighbour roles, the new
+//           neighbour pairs' content hashes; per round an LDS dedupe of the new
+//           keys, their occurrence slots grouped per key (T), one record per
+//           (key, owner) and the LDS-aggregated count decrements per owner.
+//  k_commit (NBA x 1024): the token rewrites of find region j; owner j's records
+//           from every finder -> LDS dedupe -> one key-table resolve (claim or
+//           find) per key -> pk of every occurrence slot, the owner's posting log,
+//           one count update per key (+ hot-list crossing check).
+// A posting index that is stale is rebuilt by k_find in the same iteration
+// (rank-local, so ranks never disagree on what an iteration does).
+#pragma once
+// (included inside namespace gb)
+
+// chunked per-owner posting log: entry k of owner o
+__device__ inline int64_t log_addr(const Dev& D, int o, int64_t k) {
+  return (int64_t)D.pch[(int64_t)o * D.MAXCH + k / D.CHUNK] * D.CHUNK + k % D.CHUNK;
+}
+__device__ inline int64_t log_len(const Dev& D, int o) {
+  const int32_t nc = D.pnch[o];
+  return nc > 0 ? (int64_t)(nc - 1) * D.CHUNK + D.pfill[o] : 0;
+}
+
+// posting index of residue region r (one workgroup, hist: NBKT ints of LDS): counting
+// sort of the region's live pairs by key bucket.  Entries of key W (>= 0) are also
+// pushed to the candidate queue q (capacity FMQ; *qn counts all, the overflow is
+// found again by the bucket read that follows).
+__device__ void build_region_postings(const Dev& D, int32_t r, int32_t* hist, int32_t W, int32_t* q, int32_t* qn) {
+  __shared__ int32_t s_red[ABLOCK / 64];
+  constexpr int PER = NBKT / ABLOCK;
+  const int64_t g0 = (int64_t)r * D.PR, g1 = min(D.R, g0 + D.PR);
+  constexpr int UNR = 16;  // pk loads in flight per thread
+  for (int i = threadIdx.x; i < NBKT; i += ABLOCK) hist[i] = 0;
+  __syncthreads();
+  for (int64_t g = g0 + threadIdx.x; g < g1; g += UNR * ABLOCK) {
+    int32_t d[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) d[u] = g + u * ABLOCK < g1 ? tok_pk(D, g + u * ABLOCK) : -1;
+#pragma unroll
+    for (int u = 0; u < UNR; u++)
+      if (d[u] >= 0) atomicAdd(&hist[post_bkt(d[u])], 1);
+  }
+  __syncthreads();
+  int32_t sum = 0;
+  for (int k = 0; k < PER; k++) sum += hist[threadIdx.x * PER + k];
+  int32_t tot;
+  int32_t run = block_excl_scan(sum, &tot, s_red);
+  int32_t* off = D.poff + (int64_t)r * (NBKT + 1);
+  __syncthreads();
+  for (int k = 0; k < PER; k++) {
+    const int b = threadIdx.x * PER + k;
+    const int32_t c = hist[b];
+    hist[b] = run;
+    off[b] = run;
+    run += c;
+  }
+  if (threadIdx.x == 0) off[NBKT] = tot;
+  __syncthreads();
+  int2* out = D.post + (int64_t)r * D.PR;
+  for (int64_t g = g0 + threadIdx.x; g < g1; g += UNR * ABLOCK) {
+    int32_t d[UNR];
+#pragma unroll
+    for (int u = 0; u < UNR; u++) d[u] = g + u * ABLOCK < g1 ? tok_pk(D, g + u * ABLOCK) : -1;
+#pragma unroll
+    for (int u = 0; u < UNR; u++) {
+      if (d[u] < 0) continue;
+      const int32_t slot = (int32_t)(g + u * ABLOCK);
+      out[atomicAdd(&hist[post_bkt(d[u])], 1)] = make_int2(d[u], slot);
+      if (d[u] == W) {
+        const int32_t j = atomicAdd(qn, 1);
+        if (j < FMQ) q[j] = slot;
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// record of a key found (not claimed): the next k_find checks it against the key's
+// canonical hashes (EHASH)
+__device__ inline void emit_check(const Dev& D, int32_t* s_np, int32_t d, int32_t len, u64 h1, u64 h2) {
+  NewPair e;
+  e.target = d;
+  e.slot = -1;
+  e.len = len;
+  e.delta = 0;
+  e.h1 = h1;
+  e.h2 = h2;
+  const int32_t j = atomicAdd(s_np, 1);
+  if (j < D.RC)
+    D.chk[(int64_t)blockIdx.x * D.RC + j] = e;
+  else
+    atomicAdd((unsigned long long*)&D.st->nunchecked, 1ULL);
+}
+
+// EHASH check of the keys the previous commit / import found (not claimed): their
+// content hashes must be the key's canonical ones
+__device__ inline void check_found(const Dev& D, int32_t r) {
+  const int32_t n = D.chkcnt[r];
+  const NewPair* reg = D.chk + (int64_t)r * D.RC;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const NewPair e = reg[i];
+    const int32_t d = e.target;
+    if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) set_error(D, GEOBPE_EHASH, i);
+  }
+}
+
+// ---------------------------------------------------------------------- k_find
+struct FHalf {  // a new neighbour pair of a merged occurrence
+  u64 pkey, h1, h2;
+  int32_t len, idL, g, idR, target;
+};
+
+struct FindCtx {
+  int32_t W, nid, wl, r, par;
+  u64 w1, w2;
+  u64 pa1, pb1, pa2, pb2;  // P^(2 wl), P^(2 wl - 1) of both bases (the left key's right part is W)
+  bool to_delta;
+};
+
+// LDS of k_find (the posting rebuild's histogram shares the dedupe arrays)
+struct FindLds {
+  union {
+    int32_t hist[NBKT];
+    struct {
+      u64 kkey[FKC];
+      u64 kh1[FKC];
+      int32_t kcnt[FKC];
+      int32_t kst[FKC];
+      AggT<12> agg;  // count decrements of this workgroup
+    } m;
+  } u;
+  int32_t q[FMQ];
+  int32_t curK[NBA_MAX], curD[NBA_MAX];
+  int32_t red[ABLOCK / 64];
+  int32_t qn, n, tb, fits, ktot;
+};
+
+__device__ inline void emit_occ(const Dev& D, FindCtx& F, int32_t* s_n, int32_t a, int32_t ya, int32_t b, int32_t c) {
+  LEntry e;
+  e.a = a;
+  e.ya = ya;
+  e.b = b;
+  e.c = c;
+  // one LDS reservation per wave instruction (the active lanes are the callers)
+  const u64 m = __ballot(1);
+  const int lane = wave_lane();
+  const int leader = __ffsll((long long)m) - 1;
+  int32_t base = 0;
+  if (lane == leader) base = atomicAdd(s_n, __popcll(m));
+  base = __shfl(base, leader, 64);
+  const int32_t j = base + __popcll(m & ((1ULL << lane) - 1));
+  if (j < D.LC) {
+    D.L[(int64_t)F.r * D.LC + j] = e;
+  } else {
+    const int64_t k = atomicAdd((unsigned long long*)&D.st->L_ovf2[F.par], 1ULL);
+    if (k < D.Lovf_cap)
+      D.Lovf[k] = e;
+    else
+      set_error(D, GEOBPE_ECAPACITY, -10);
+  }
+}
+
+// a key record into its owner's slot of this finder (or the overflow list)
+__device__ inline void emit_krec(const Dev& D, const FindCtx& F, int32_t* curK, const FHalf& h, int32_t n,
+                                 int32_t tstart) {
+  KRec k;
+  k.pkey = h.pkey;
+  k.h1 = h.h1;
+  k.h2 = h.h2;
+  k.len = h.len;
+  k.idL = h.idL;
+  k.g = h.g;
+  k.idR = h.idR;
+  k.n = n;
+  k.tstart = tstart;
+  const int o = owner_of_key(D, h.pkey);
+  const int32_t j = atomicAdd(&curK[o], 1);
+  if (j < SK) {
+    D.KS[((int64_t)o * D.NBA + F.r) * SK + j] = k;
+  } else {
+    const int64_t x = atomicAdd((unsigned long long*)&D.st->nko2[F.par], 1ULL);
+    if (x < D.KO_cap)
+      D.KO[x] = k;
+    else
+      set_error(D, GEOBPE_ECAPACITY, -41);
+  }
+}
+__device__ inline void emit_single(const Dev& D, const FindCtx& F, int32_t* curK, const FHalf& h) {
+  emit_krec(D, F, curK, h, 1, -(h.target + 1));
+}
+
+__device__ inline void dec_add(const Dev& D, const FindCtx& F, AggT<12>& agg, int32_t d, int32_t v) {
+  if (!agg_stage(agg, d, v)) global_add(D, d, v, F.to_delta);
+}
+
+// the new key (X, glR, right) of occurrence t: right = X when c is a left part
+__device__ inline void right_half(const Dev& D, const FindCtx& F, int32_t t, int32_t glR, bool cL, int32_t idc,
+                                  int32_t lc, u64 c1, u64 c2, FHalf& h) {
+  const int32_t rl = cL ? F.wl : lc;
+  const u64 r1 = cL ? F.w1 : c1, r2 = cL ? F.w2 : c2;
+  const int64_t ny = 2 * (int64_t)rl - 1;
+  combine_pw(F.w1, F.w2, glR, r1, r2, D.pw1[ny + 1], D.pw1[ny], D.pw2[ny + 1], D.pw2[ny], h.h1, h.h2);
+  h.len = F.wl + rl;
+  h.pkey = probe_key(h.h1, h.h2, h.len);
+  h.idL = F.nid;
+  h.g = glR;
+  h.idR = cL ? F.nid : idc;
+  h.target = t;
+}
+
+// a candidate slot g of W: confirm it and, at a run start, walk the run greedily left
+// to right (bpe.py:1888-1916): merge (t, b), skip (b, c), merge (c, d) if it is W
+// too, ...  Neighbour roles without any write: c is a left part iff pk[c] == W; the
+// run start's left neighbour p is a right part iff the W-run ending at (pp, p) has
+// odd length.  The first occurrence's new keys are returned (grouped by the caller),
+// a run's later occurrences send theirs as single records.
+__device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf& hl, bool& vl, FHalf& hr,
+                          bool& vr) {
+  vl = vr = false;
+  const int32_t W = F.W;
+  const int4 tg = D.tok[g];  // {tid, tlen, tprev, pk}
+  if (tg.w != W) return;
+  dbg_stamp(D, 40);
+  const int32_t p = tg.z;
+  const int32_t b = g + tok_len(tg.y);
+  // round 2: everything that depends only on (g, p, b)
+  const int32_t ip = p >= 0 ? p : g;
+  const int4 tp = D.tok[ip];
+  const int4 tb = D.tok[b];
+  if (p >= 0 && tp.w == W) return;  // not a run start: its run's start walks it
+  dbg_stamp(D, 41);
+  const int32_t glL = p >= 0 ? next_glue(D, tp.y, g - 1) : 0;
+  const int32_t glR = next_glue(D, tb.y, g + F.wl - 1);
+  // round 3: c, the run start's left context
+  const int32_t pkb = tb.w;
+  const int32_t c = pkb >= 0 ? b + tok_len(tb.y) : -1;
+  const int32_t ic = c >= 0 ? c : g;
+  const int4 tc = D.tok[ic];
+  const int32_t pp = p >= 0 ? tp.z : -1;
+  const int4 tpp = D.tok[pp >= 0 ? pp : g];
+  const int32_t vp = p >= 0 ? max(tp.x, 0) : 0;
+  const u64 l1 = D.vh1[vp], l2 = D.vh2[vp];
+  const bool cL = c >= 0 && tc.w == W;
+  const int32_t vc = c >= 0 ? max(tc.x, 0) : 0;
+  const u64 c1 = D.vh1[vc], c2 = D.vh2[vc];
+  bool pRight = false;
+  if (p >= 0 && pp >= 0 && tpp.w == W) {  // the W-run ending at (pp, p): its length's parity
+    int32_t m = 1, y = tpp.z;
+    for (;;) {
+      if (y < 0) break;
+      const int4 ty = D.tok[y];
+      if (ty.w != W) break;
+      m++;
+      y = ty.z;
+    }
+    pRight = (m & 1) != 0;
+  }
+  const bool pN = p >= 0 && !pRight;
+  dbg_stamp(D, 42);
+  // the first occurrence (g, b)
+  emit_occ(D, F, &S.n, g, F.wl | (tb.y & (int32_t)0xFFFF0000), b, c);
+  if (pkb >= 0) dec_add(D, F, S.u.m.agg, pkb, -1);
+  if (pN) {
+    dec_add(D, F, S.u.m.agg, tp.w, -1);
+    combine_pw(l1, l2, glL, F.w1, F.w2, F.pa1, F.pb1, F.pa2, F.pb2, hl.h1, hl.h2);
+    hl.len = tok_len(tp.y) + F.wl;
+    hl.pkey = probe_key(hl.h1, hl.h2, hl.len);
+    hl.idL = tp.x;
+    hl.g = glL;
+    hl.idR = F.nid;
+    hl.target = p;
+    vl = true;
+  }
+  dbg_stamp(D, 43);
+  if (c >= 0) {
+    right_half(D, F, g, glR, cL, tc.x, tok_len(tc.y), c1, c2, hr);
+    vr = true;
+  }
+  dbg_stamp(D, 44);
+  // the rest of the run: (c, d) while (b, c) and (c, d) are both W
+  int32_t cur_b = b, cur_c = c, cur_pkb = pkb;
+  bool cur_cL = cL;
+  int32_t lcur_c = tok_len(tc.y);
+  while (cur_pkb == W && cur_cL) {
+    const int32_t t = cur_c;
+    const int32_t b2 = t + lcur_c;
+    const int4 tb2 = D.tok[b2];
+    const int32_t glR2 = next_glue(D, tb2.y, t + F.wl - 1);
+    const int32_t pkb2 = tb2.w;
+    const int32_t c2i = pkb2 >= 0 ? b2 + tok_len(tb2.y) : -1;
+    const int4 tc2 = D.tok[c2i >= 0 ? c2i : t];
+    const bool cL2 = c2i >= 0 && tc2.w == W;
+    const int32_t vc2 = c2i >= 0 ? max(tc2.x, 0) : 0;
+    const u64 d1 = D.vh1[vc2], d2 = D.vh2[vc2];
+    emit_occ(D, F, &S.n, t, F.wl | (tb2.y & (int32_t)0xFFFF0000), b2, c2i);
+    if (pkb2 >= 0) dec_add(D, F, S.u.m.agg, pkb2, -1);
+    if (c2i >= 0) {
+      FHalf h;
+      right_half(D, F, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
+      emit_single(D, F, S.curK, h);
+    }
+    cur_b = b2;
+    cur_c = c2i;
+    cur_pkb = pkb2;
+    cur_cL = cL2;
+    lcur_c = tok_len(tc2.y);
+  }
+}
+
+// LDS dedupe slot of a new key (*res: this thread inserted it); -1 when the probes
+// run out (the half then goes as a single record)
+__device__ inline int32_t fkc_find(FindLds& S, const Dev& D, u64 k, u64 h1, bool* res) {
+  int32_t h = (int32_t)((k * 0x9E3779B97F4A7C15ULL) >> (64 - 11)) & (FKC - 1);
+#pragma unroll 1
+  for (int probe = 0; probe < 16; probe++, h = (h + 1) & (FKC - 1)) {
+    u64 c = S.u.m.kkey[h];
+    if (c == 0) {
+      c = atomicCAS((unsigned long long*)&S.u.m.kkey[h], 0ULL, (unsigned long long)k);
+      if (c == 0) {
+        S.u.m.kh1[h] = h1;
+        *res = true;
+        return h;
+      }
+    }
+    if (c == k) {
+      *res = false;
+      return h;
+    }
+  }
+  *res = false;
+  return -1;
+}
+
+__global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
+  __shared__ FindLds S;
+  State* st = D.st;
+  if (par < 0) {  // pipelined exchange (k_select set dgen)
+    if (st->stall) return;
+    par = st->dgen & 1;
+  }
+  const int32_t r = blockIdx.x;
+  dbg_stamp(D, 10);
+  const Sel sel = D.sel[par];
+  check_found(D, r);
+  if (sel.decision != SEL_MERGE) return;
+  FindCtx F;
+  F.W = sel.W;
+  F.nid = sel.nid;
+  F.wl = sel.wl;
+  F.r = r;
+  F.par = par;
+  F.w1 = sel.w1;
+  F.w2 = sel.w2;
+  F.to_delta = to_delta != 0;
+  {
+    const int64_t nw = 2 * (int64_t)max(F.wl, 1) - 1;
+    F.pa1 = D.pw1[nw + 1];
+    F.pb1 = D.pw1[nw];
+    F.pa2 = D.pw2[nw + 1];
+    F.pb2 = D.pw2[nw];
+  }
+  if (threadIdx.x == 0) {
+    S.qn = 0;
+    S.n = 0;
+    S.tb = 0;
+  }
+  for (int i = threadIdx.x; i < NBA_MAX; i += ABLOCK) S.curK[i] = S.curD[i] = 0;
+  // candidates: region r's bucket of W (+ 1/NBA of the log of W's owner)
+  const int32_t W = F.W;
+  const int o = sel.wown;
+  int32_t lo = 0, n1 = 0;
+  int64_t ls0 = 0, ls1 = 0;
+  bool queued = false;  // the rebuild queued the bucket's W entries already
+  if (sel.rebuild) {
+    __syncthreads();
+    build_region_postings(D, r, S.u.hist, W, S.q, &S.qn);
+    if (threadIdx.x == 0) {
+      D.pnch[r] = 0;  // (no finder reads a log in a rebuilding iteration)
+      D.pfill[r] = 0;
+      if (r == 0) {
+        st->pool_used = 0;
+        st->post_valid = 1;
+        st->plog_ovf = 0;
+        st->npost += 1;
+      }
+    }
+    queued = S.qn <= FMQ;
+  }
+  if (W >= 0 && !queued) {
+    const int32_t* off = D.poff + (int64_t)r * (NBKT + 1);
+    const uint32_t bk = post_bkt(W);
+    lo = off[bk];
+    n1 = off[bk + 1] - lo;
+    if (!sel.rebuild) {
+      const int64_t nlog = log_len(D, o);
+      ls0 = nlog * r / D.NBA;
+      ls1 = nlog * (r + 1) / D.NBA;
+    }
+  }
+  // dedupe + aggregation state
+  for (int i = threadIdx.x; i < FKC; i += ABLOCK) {
+    S.u.m.kkey[i] = 0;
+    S.u.m.kcnt[i] = 0;
+  }
+  for (int i = threadIdx.x; i < AggT<12>::N; i += ABLOCK) {
+    S.u.m.agg.key[i] = -1;
+    S.u.m.agg.val[i] = 0;
+  }
+  __syncthreads();
+  dbg_stamp(D, 11);
+  const int64_t ntot = queued ? (int64_t)S.qn : n1 + (ls1 - ls0);
+  const int2* P = D.post + (int64_t)r * D.PR + lo;
+  for (int64_t c0 = 0; c0 < ntot; c0 += FMQ) {  // block-uniform
+    int32_t nq;
+    if (queued) {
+      nq = (int32_t)ntot;
+    } else {
+      __syncthreads();
+      if (threadIdx.x == 0) S.qn = 0;
+      __syncthreads();
+      const int64_t c1 = min(ntot, c0 + FMQ);
+      for (int64_t i = c0 + threadIdx.x; i < c1; i += ABLOCK) {
+        const int2 e = i < n1 ? P[i] : D.pool[log_addr(D, o, ls0 + (i - n1))];
+        if (e.x == W) S.q[atomicAdd(&S.qn, 1)] = e.y;
+      }
+      __syncthreads();
+      nq = S.qn;
+    }
+    if (c0 == 0) dbg_stamp(D, 14);
+    for (int32_t q0 = 0; q0 < nq; q0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
+      const int32_t qi = q0 + threadIdx.x;
+      FHalf hl, hr;
+      bool vl = false, vr = false;
+      if (qi < nq) find_walk(D, F, S, S.q[qi], hl, vl, hr, vr);
+      if (c0 == 0 && q0 == 0) dbg_stamp(D, 15);
+      // group the new keys of this round: LDS slot, rank within the slot
+      bool rl = false, rr = false;
+      int32_t sl = -1, sr = -1, kl = 0, kr = 0;
+      if (vl) {
+        sl = fkc_find(S, D, hl.pkey, hl.h1, &rl);
+        if (sl >= 0) kl = atomicAdd(&S.u.m.kcnt[sl], 1);
+      }
+      if (vr) {
+        sr = fkc_find(S, D, hr.pkey, hr.h1, &rr);
+        if (sr >= 0) kr = atomicAdd(&S.u.m.kcnt[sr], 1);
+      }
+      __syncthreads();
+      if (vl && sl >= 0 && S.u.m.kh1[sl] != hl.h1) {  // same probe key, other content
+        set_error(D, GEOBPE_EHASH, -13);
+        sl = -1;
+        vl = false;
+      }
+      if (vr && sr >= 0 && S.u.m.kh1[sr] != hr.h1) {
+        set_error(D, GEOBPE_EHASH, -13);
+        sr = -1;
+        vr = false;
+      }
+      {  // exclusive scan of the slot counts -> T offsets
+        constexpr int PER = FKC / ABLOCK > 0 ? FKC / ABLOCK : 1;
+        int32_t v[PER], sum = 0;
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+          const int i = threadIdx.x * PER + k;
+          v[k] = i < FKC ? S.u.m.kcnt[i] : 0;
+          sum += v[k];
+        }
+        int32_t tot;
+        int32_t run = block_excl_scan(sum, &tot, S.red);
+#pragma unroll
+        for (int k = 0; k < PER; k++) {
+          const int i = threadIdx.x * PER + k;
+          if (i < FKC) S.u.m.kst[i] = run;
+          run += v[k];
+        }
+        if (threadIdx.x == 0) {
+          S.ktot = tot;
+          S.fits = (int64_t)S.tb + tot <= D.TC ? 1 : 0;
+        }
+      }
+      __syncthreads();
+      if (c0 == 0 && q0 == 0) dbg_stamp(D, 16);
+      const bool fits = S.fits != 0;
+      const int64_t tbase = (int64_t)r * D.TC + S.tb;
+      if (vl) {
+        if (sl >= 0 && fits) {
+          D.T[tbase + S.u.m.kst[sl] + kl] = hl.target;
+          if (rl) emit_krec(D, F, S.curK, hl, S.u.m.kcnt[sl], (int32_t)(tbase + S.u.m.kst[sl]));
+        } else {
+          emit_single(D, F, S.curK, hl);
+        }
+      }
+      if (vr) {
+        if (sr >= 0 && fits) {
+          D.T[tbase + S.u.m.kst[sr] + kr] = hr.target;
+          if (rr) emit_krec(D, F, S.curK, hr, S.u.m.kcnt[sr], (int32_t)(tbase + S.u.m.kst[sr]));
+        } else {
+          emit_single(D, F, S.curK, hr);
+        }
+      }
+      __syncthreads();
+      if (rl && sl >= 0) {
+        S.u.m.kkey[sl] = 0;
+        S.u.m.kcnt[sl] = 0;
+      }
+      if (rr && sr >= 0) {
+        S.u.m.kkey[sr] = 0;
+        S.u.m.kcnt[sr] = 0;
+      }
+      if (threadIdx.x == 0 && fits) S.tb += S.ktot;
+      __syncthreads();
+    }
+  }
+  dbg_stamp(D, 12);
+  // step 1 (the merged pair, -1 on W per occurrence: S.n counts them) and the
+  // decrements -> owners
+  if (threadIdx.x == 0 && S.n && W >= 0) dec_add(D, F, S.u.m.agg, W, -S.n);
+  __syncthreads();
+  for (int i = threadIdx.x; i < AggT<12>::N; i += ABLOCK) {
+    const int32_t k = S.u.m.agg.key[i], v = S.u.m.agg.val[i];
+    if (k < 0 || v == 0) continue;
+    const int ow = owner_of_slot(D, (u64)k);
+    const int32_t j = atomicAdd(&S.curD[ow], 1);
+    if (j < SD)
+      D.DS[((int64_t)ow * D.NBA + r) * SD + j] = make_int2(k, v);
+    else
+      global_add(D, k, v, F.to_delta);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < D.NBA; i += ABLOCK) {
+    D.cntK[(int64_t)i * D.NBA + r] = min(S.curK[i], SK);
+    D.cntD[(int64_t)i * D.NBA + r] = min(S.curD[i], SD);
+  }
+  if (threadIdx.x == 0) D.Lcnt[r] = min(S.n, (int32_t)D.LC);
+  dbg_stamp(D, 13);
+}
+
+// ---------------------------------------------------------------------- k_commit
+struct CommitLds {
+  union {
+    AggT<12> agg;  // decrements of this owner's keys
+  } u;
+  u64 ckey[CKC];
+  u64 ch1[CKC];
+  int32_t cn[CKC];     // occurrences of the key (over every finder)
+  int32_t cid[CKC];    // key id (-2: resolve failed)
+  int32_t cfirst[CKC]; // a record of the key
+  u64 ch2[CKC];        // the key's content (for the claim)
+  int4 crep[CKC];      // {len, idL, g, idR}
+  int32_t preK[NBA_MAX + 1], preD[NBA_MAX + 1];
+  int32_t chunk[LOG_CH_MAX + 1];
+  int32_t red[ABLOCK / 64];
+  int64_t logpos, lognew;
+  int32_t nKO, ns, chk, logok, c0, fbn;
+};
+
+// segment of a flat index i over NBA prefix sums pre[0..NBA] (pre[w] <= i < pre[w + 1])
+__device__ inline int32_t seg_of(const int32_t* pre, int32_t n, int32_t i) {
+  int32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const int32_t mid = (lo + hi) >> 1;
+    if (pre[mid] <= i)
+      lo = mid;
+    else
+      hi = mid;
+  }
+  return lo;
+}
+
+// record i of owner j: the fixed slots of finder w, then the overflow list; *at =
+// its index in KS, or -(index in KO + 1)
+__device__ inline bool commit_rec(const Dev& D, const CommitLds& S, int32_t j, int32_t i, KRec& k, int64_t* at) {
+  const int32_t totK = S.preK[D.NBA];
+  if (i < totK) {
+    const int32_t w = seg_of(S.preK, D.NBA, i);
+    *at = ((int64_t)j * D.NBA + w) * SK + (i - S.preK[w]);
+    k = D.KS[*at];
+    return true;
+  }
+  *at = -(int64_t)(i - totK) - 1;
+  k = D.KO[i - totK];
+  return owner_of_key(D, k.pkey) == j;
+}
+
+__device__ inline int32_t ckc_slot(CommitLds& S, u64 k, bool insert, bool* res) {
+  int32_t h = (int32_t)((k * 0xD6E8FEB86659FD93ULL) >> (64 - 11)) & (CKC - 1);
+  *res = false;
+#pragma unroll 1
+  for (int probe = 0; probe < 32; probe++, h = (h + 1) & (CKC - 1)) {
+    u64 c = S.ckey[h];
+    if (c == 0) {
+      if (!insert) return -1;
+      c = atomicCAS((unsigned long long*)&S.ckey[h], 0ULL, (unsigned long long)k);
+      if (c == 0) {
+        *res = true;
+        return h;
+      }
+    }
+    if (c == k) return h;
+  }
+  return -1;
+}
+
+// key id of a record's content: find or claim in the key table (claim: payload +
+// this owner's claim list; find: EHASH check record).  The owner is the only
+// workgroup resolving this key in this launch, so the first probe is the CAS itself
+// (it returns what the slot holds: empty -> claimed, the key -> found).
+__device__ inline int32_t commit_resolve(const Dev& D, CommitLds& S, const KRec& k, bool* claimed_out = nullptr) {
+  bool claimed = false;
+  const u64 s0 = ht_first_slot(D, k.pkey);
+  const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s0], 0ULL, (unsigned long long)k.pkey);
+  int32_t d;
+  if (old == 0) {
+    claimed = true;
+    d = (int32_t)s0;
+  } else if (old == k.pkey) {
+    d = (int32_t)s0;
+  } else {
+    const u64 s1 = (s0 + 1) & ((u64)D.HC - 1);
+    d = ht_resolve(D, k.pkey, s1, ht_probe(D, s1), &claimed);
+  }
+  if (claimed_out) *claimed_out = claimed;
+  if (d < 0) return -1;
+  if (claimed) {
+    claim_payload(D, d, k.h1, k.h2, k.len, k.idL, k.g, k.idR);
+    note_claim(D, &S.ns, d);
+  } else {
+    emit_check(D, &S.chk, d, k.len, k.h1, k.h2);
+  }
+  return d;
+}
+
+__device__ inline void log_put(const Dev& D, const CommitLds& S, int64_t pos, int32_t d, int32_t slot) {
+  const int64_t c = pos / D.CHUNK - S.c0;
+  D.pool[(int64_t)S.chunk[c] * D.CHUNK + pos % D.CHUNK] = make_int2(d, slot);
+}
+
+__global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par) {
+  __shared__ CommitLds S;
+  __shared__ HotApp hot;
+  __shared__ int64_t s_kl[2];
+  State* st = D.st;
+  if (par < 0) {  // pipelined exchange (k_select set dgen)
+    if (st->stall) return;
+    par = st->dgen & 1;
+  }
+  const Sel sel = D.sel[par];
+  const int32_t j = blockIdx.x;
+  if (j == 0 && threadIdx.x == 0) {
+    st->L_ovf2[par ^ 1] = 0;  // the next find's overflow counters (idle since the last pair)
+    st->nko2[par ^ 1] = 0;
+    if (sel.decision == SEL_DONE) {
+      st->done = 1;
+      st->maxc = 0;
+    } else if (sel.decision == SEL_SKIP) {
+      st->nskip += 1;
+    }
+  }
+  if (sel.decision == SEL_DONE) return;
+  if (sel.decision == SEL_SKIP) {
+    if (sel.skip & SKIP_MEASURE) measure_max(D);
+    if (sel.skip & SKIP_HOT) rebuild_hot_list(D, sel.theta_new, sel.build);
+    return;
+  }
+  dbg_stamp(D, 0);
+  const bool tod = to_delta != 0;
+  const int32_t nid = sel.nid;
+  const int32_t th = st->theta;
+  if (j == 0) {  // _tokens[n] = json.loads(key): content(L) ++ [g] ++ content(R)
+    const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
+    const int64_t vL = D.voff[L], vR = D.voff[Rr];
+    const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
+    const int64_t pos = D.voff[nid], ln = nL + 1 + nR;
+    if (pos + ln > D.VSC) {
+      if (threadIdx.x == 0) set_error(D, GEOBPE_ECAPACITY, -9);
+    } else {
+      for (int64_t i = threadIdx.x; i < ln; i += blockDim.x)
+        D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
+      if (threadIdx.x == 0) D.voff[nid + 1] = pos + ln;
+    }
+  }
+  // ---- owner j's record counts (every finder), state
+  for (int i = threadIdx.x; i < CKC; i += ABLOCK) {
+    S.ckey[i] = 0;
+    S.cn[i] = 0;
+  }
+  for (int i = threadIdx.x; i < AggT<12>::N; i += ABLOCK) {
+    S.u.agg.key[i] = -1;
+    S.u.agg.val[i] = 0;
+  }
+  hot_init(hot);
+  {
+    const int32_t cK = threadIdx.x < D.NBA ? D.cntK[(int64_t)j * D.NBA + threadIdx.x] : 0;
+    const int32_t cD = threadIdx.x < D.NBA ? D.cntD[(int64_t)j * D.NBA + threadIdx.x] : 0;
+    int32_t totK, totD;
+    const int32_t eK = block_excl_scan(cK, &totK, S.red);
+    const int32_t eD = block_excl_scan(cD, &totD, S.red);
+    if (threadIdx.x < D.NBA) {
+      S.preK[threadIdx.x] = eK;
+      S.preD[threadIdx.x] = eD;
+    }
+    if (threadIdx.x == 0) {
+      S.preK[D.NBA] = totK;
+      S.preD[D.NBA] = totD;
+      S.nKO = (int32_t)min(st->nko2[par], D.KO_cap);
+      S.ns = 0;
+      S.chk = 0;
+      S.fbn = 0;
+      s_kl[0] = D.kchunk[2 * j];
+      s_kl[1] = D.kchunk[2 * j + 1];
+    }
+  }
+  __syncthreads();
+  dbg_stamp(D, 1);
+  // ---- round 1: this owner's key records -> LDS dedupe (occurrence totals per key)
+  const int32_t nrec = S.preK[D.NBA] + S.nKO;
+  for (int32_t i = threadIdx.x; i < nrec; i += ABLOCK) {
+    KRec k;
+    int64_t at;
+    if (!commit_rec(D, S, j, i, k, &at)) continue;
+    bool res;
+    const int32_t s = ckc_slot(S, k.pkey, true, &res);
+    if (s >= 0) {
+      if (res) {
+        S.ch1[s] = k.h1;
+        S.cfirst[s] = i;
+        S.ch2[s] = k.h2;
+        S.crep[s] = make_int4(k.len, k.idL, k.g, k.idR);
+      }
+      atomicAdd(&S.cn[s], k.n);
+    } else {  // dedupe table full: this record on its own (found again in round 2)
+      const int32_t d = commit_resolve(D, S, k);
+      if (d >= 0) {
+        atomicAdd(&S.fbn, k.n);
+        if (tod)
+          global_add(D, d, k.n, true);
+        else
+          count_add_hot(D, hot, d, k.n, th);
+      }
+    }
+  }
+  // decrement records -> LDS aggregation
+  const int32_t ndec = S.preD[D.NBA];
+  for (int32_t i = threadIdx.x; i < ndec; i += ABLOCK) {
+    const int32_t lo = seg_of(S.preD, D.NBA, i);
+    const int2 x = D.DS[((int64_t)j * D.NBA + lo) * SD + (i - S.preD[lo])];
+    if (!agg_stage(S.u.agg, x.x, x.y)) global_add(D, x.x, x.y, tod);
+  }
+  __syncthreads();
+  dbg_stamp(D, 2);
+  // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
+  int32_t nlog = 0;
+  const bool alone = S.fbn == 0;  // no key of this owner was resolved outside the table
+  for (int32_t s = threadIdx.x; s < CKC; s += ABLOCK) {
+    const u64 key = S.ckey[s];
+    if (key == 0) continue;
+    KRec k;
+    k.pkey = key;
+    k.h1 = S.ch1[s];
+    k.h2 = S.ch2[s];
+    const int4 rp = S.crep[s];
+    k.len = rp.x;
+    k.idL = rp.y;
+    k.g = rp.z;
+    k.idR = rp.w;
+    bool claimed;
+    const int32_t d = commit_resolve(D, S, k, &claimed);
+    S.cid[s] = d >= 0 ? d : -2;
+    if (d >= 0) {
+      const int32_t n = S.cn[s];
+      if (tod) {
+        global_add(D, d, n, true);
+      } else if (claimed && alone) {  // a new key only this thread adds to: its count is n
+        D.count[d] = n;
+        if (th > 0 && n >= th) hot_push(D, hot, d);
+      } else {
+        count_add_hot(D, hot, d, n, th);
+      }
+      nlog += n;
+    }
+  }
+  // posting-log space for this merge's new pairs of this owner (one reservation)
+  {
+    int32_t tot;
+    block_excl_scan(nlog, &tot, S.red);
+    if (threadIdx.x == 0) {
+      S.lognew = tot + S.fbn;  // (+ records whose key did not fit the dedupe table)
+      const int32_t nc = D.pnch[j];
+      const int64_t p0 = nc > 0 ? (int64_t)(nc - 1) * D.CHUNK + D.pfill[j] : 0;
+      S.logpos = p0;
+      S.logok = 0;
+      const int64_t cap = p0 + S.lognew;
+      const int32_t c0 = (int32_t)(p0 / D.CHUNK);
+      const int32_t c1 = (int32_t)((cap + D.CHUNK - 1) / D.CHUNK);  // chunks [c0, c1) cover the appends
+      S.c0 = c0;
+      if (!st->plog_ovf && c1 - c0 <= LOG_CH_MAX && c1 <= D.MAXCH) {
+        const int32_t need = max(0, c1 - nc);
+        const int64_t base = need ? (int64_t)atomicAdd((unsigned long long*)&st->pool_used, (unsigned long long)need) : 0;
+        if (base + need <= D.POOL_CH) {
+          for (int32_t c = c0; c < c1; c++) {
+            const int32_t id = c < nc ? D.pch[(int64_t)j * D.MAXCH + c] : (int32_t)(base + (c - nc));
+            S.chunk[c - c0] = id;
+            if (c >= nc) D.pch[(int64_t)j * D.MAXCH + c] = id;
+          }
+          S.logok = 1;
+        }
+      }
+      if (!S.logok) st->plog_ovf = 1;  // the next merge rebuilds the posting index first
+    }
+  }
+  __syncthreads();
+  dbg_stamp(D, 3);
+  // ---- round 2: every record's key id and posting-log position (k_place writes pk
+  // and the log entries of its occurrence slots)
+  for (int32_t i0 = 0; i0 < nrec; i0 += ABLOCK) {  // block-uniform
+    const int32_t i = i0 + threadIdx.x;
+    KRec k;
+    int64_t at = 0;
+    bool mine = i < nrec && commit_rec(D, S, j, i, k, &at);
+    int32_t d = -1;
+    if (mine) {
+      bool res;
+      const int32_t s = ckc_slot(S, k.pkey, false, &res);
+      if (s >= 0) {
+        d = S.cid[s];
+        if (S.ch1[s] != k.h1) {  // same probe key, other content
+          set_error(D, GEOBPE_EHASH, -13);
+          d = -1;
+        }
+      } else {  // (round 1 resolved it on its own: find it again)
+        bool claimed;
+        d = ht_resolve(D, k.pkey, ht_first_slot(D, k.pkey), ht_probe(D, ht_first_slot(D, k.pkey)), &claimed);
+      }
+    }
+    const int32_t n = mine && d >= 0 ? k.n : 0;
+    int32_t tot;
+    const int32_t ex = block_excl_scan(n, &tot, S.red);
+    if (mine) {
+      const int2 v = make_int2(d >= 0 ? d : -1, S.logok && d >= 0 ? (int32_t)(S.logpos + ex) : -1);
+      if (at >= 0)
+        D.KSid[at] = v;
+      else
+        D.KOid[-at - 1] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) S.logpos += tot;
+  }
+  dbg_stamp(D, 4);
+  // ---- decrements of this owner's keys: one atomic per key
+  for (int i = threadIdx.x; i < AggT<12>::N; i += ABLOCK) {
+    const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
+    if (k < 0 || v == 0) continue;
+    global_add(D, k, v, tod);
+  }
+  hot_flush(D, hot);  // (syncs the workgroup first)
+  if (threadIdx.x == 0) {
+    D.chkcnt[j] = min(S.chk, (int32_t)D.RC);
+    if (S.logok) {
+      const int64_t end = S.logpos;
+      const int32_t nc = (int32_t)((end + D.CHUNK - 1) / D.CHUNK);
+      if (end > 0) {
+        D.pnch[j] = nc;
+        D.pfill[j] = (int32_t)(end - (int64_t)(nc - 1) * D.CHUNK);
+      }
+    }
+  }
+  // this owner's claims join klist from its chunk (a reservation only when the chunk
+  // runs out; the chunk state was read at kernel start)
+  __syncthreads();
+  {
+    const int32_t n = min(S.ns, (int32_t)D.RC);
+    if (threadIdx.x == 0 && n) {
+      if (s_kl[1] - s_kl[0] < n) {
+        const int64_t sz = max((int64_t)KL_CHUNK, (int64_t)n);
+        s_kl[0] = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
+        s_kl[1] = s_kl[0] + sz;
+      }
+      D.kchunk[2 * j] = s_kl[0] + n;
+      D.kchunk[2 * j + 1] = s_kl[1];
+      atomicAdd((unsigned long long*)&st->nkeys, (unsigned long long)n);
+    }
+    __syncthreads();
+    const int32_t* reg = D.ns + (int64_t)j * D.RC;
+    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) klist_put(D, s_kl[0] + i, reg[i]);
+  }
+  dbg_stamp(D, 5);
+  dbg_stamp(D, 6);
+}
+
+// ---------------------------------------------------------------------- k_place
+// Region j's half of the merge after its keys are resolved: the token rewrites of
+// find region j (step 2, bond_to_token / token_pos: tok[a] = {X, |X|}, b stops
+// being a token start, c's previous token is a) and, for every key record finder j
+// sent (and its share of the overflow list), pk of the occurrence slots and their
+// posting-log entries -- balanced by region, whatever the key skew.
+struct PlaceLds {
+  int32_t pre[NBA_MAX + 1];
+  int32_t tpre[ABLOCK + 1];  // this round's records: prefix of their slot counts
+  int32_t rts[ABLOCK], rid[ABLOCK], rlp[ABLOCK], rown[ABLOCK];
+  int32_t red[ABLOCK / 64];
+};
+
+__global__ __launch_bounds__(ABLOCK) void k_place(Dev D, int par) {
+  __shared__ PlaceLds S;
+  State* st = D.st;
+  if (par < 0) {  // pipelined exchange (k_select set dgen)
+    if (st->stall) return;
+    par = st->dgen & 1;
+  }
+  const Sel sel = D.sel[par];
+  if (sel.decision != SEL_MERGE) return;
+  const int32_t j = blockIdx.x;
+  dbg_stamp(D, 30);
+  const int32_t nid = sel.nid;
+  const int32_t nA = D.Lcnt[j];
+  const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
+  const int64_t oper = (novf + gridDim.x - 1) / gridDim.x;
+  const int64_t o_lo = (int64_t)j * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
+  const int64_t nko = min(st->nko2[par], D.KO_cap);
+  const int64_t kper = (nko + gridDim.x - 1) / gridDim.x;
+  const int64_t k_lo = (int64_t)j * kper, k_n = max((int64_t)0, min(nko, k_lo + kper) - k_lo);
+  {
+    const int32_t c = threadIdx.x < D.NBA ? D.cntK[(int64_t)threadIdx.x * D.NBA + j] : 0;
+    int32_t tot;
+    const int32_t e = block_excl_scan(c, &tot, S.red);
+    if (threadIdx.x < D.NBA) S.pre[threadIdx.x] = e;
+    if (threadIdx.x == 0) S.pre[D.NBA] = tot;
+  }
+  for (int64_t i = threadIdx.x; i < nA + o_n; i += ABLOCK) {
+    const LEntry e = i < nA ? D.L[(int64_t)j * D.LC + i] : D.Lovf[o_lo + (i - nA)];
+    *reinterpret_cast<int2*>(D.tok + e.a) = make_int2(nid, e.ya);
+    D.tok[e.b] = make_int4(-1, 0, -1, -1);  // (no other occurrence writes b's record)
+    if (e.c >= 0)
+      *tok_f(D, e.c, 2) = e.a;
+    else
+      *tok_f(D, e.a, 3) = -1;
+  }
+  __syncthreads();
+  dbg_stamp(D, 31);
+  const int32_t nrec = S.pre[D.NBA] + (int32_t)k_n;
+  for (int32_t i0 = 0; i0 < nrec; i0 += ABLOCK) {  // block-uniform rounds of records
+    const int32_t i = i0 + threadIdx.x;
+    int32_t n = 0, ts = 0, id = -1, lp = -1, ow = 0;
+    if (i < nrec) {
+      const int32_t nk = S.pre[D.NBA];
+      int2 v;
+      if (i < nk) {
+        ow = seg_of(S.pre, D.NBA, i);
+        const int64_t at = ((int64_t)ow * D.NBA + j) * SK + (i - S.pre[ow]);
+        const int2 nt = *reinterpret_cast<const int2*>(&D.KS[at].n);
+        v = D.KSid[at];
+        n = nt.x;
+        ts = nt.y;
+      } else {
+        const int64_t x = k_lo + (i - nk);
+        const KRec k = D.KO[x];
+        v = D.KOid[x];
+        ow = owner_of_key(D, k.pkey);
+        n = k.n;
+        ts = k.tstart;
+      }
+      id = v.x;
+      lp = v.y;
+      if (id < 0) n = 0;
+    }
+    int32_t tot;
+    const int32_t ex = block_excl_scan(n, &tot, S.red);
+    S.tpre[threadIdx.x] = ex;
+    S.rts[threadIdx.x] = ts;
+    S.rid[threadIdx.x] = id;
+    S.rlp[threadIdx.x] = lp;
+    S.rown[threadIdx.x] = ow;
+    if (threadIdx.x == 0) S.tpre[ABLOCK] = tot;
+    __syncthreads();
+    for (int32_t q = threadIdx.x; q < tot; q += ABLOCK) {  // every occurrence slot of the round
+      const int32_t r = seg_of(S.tpre, ABLOCK, q);
+      const int32_t k = q - S.tpre[r];
+      const int32_t tsr = S.rts[r], d = S.rid[r];
+      const int32_t t = tsr >= 0 ? D.T[tsr + k] : -(tsr + 1);
+      *tok_f(D, t, 3) = d;
+      const int32_t l = S.rlp[r];
+      if (l >= 0) {
+        const int64_t pos = (int64_t)l + k;
+        D.pool[log_addr(D, S.rown[r], pos)] = make_int2(d, t);
+      }
+    }
+    __syncthreads();
+  }
+  dbg_stamp(D, 32);
+  if (j == 0) {  // merges applied this iteration -> merge log, state
+    int32_t nm = 0;
+    for (int32_t i = threadIdx.x; i < D.NBA; i += blockDim.x) nm += D.Lcnt[i];
+    int32_t tot;
+    block_excl_scan(nm, &tot, S.red);
+    if (threadIdx.x == 0) {
+      D.log[sel.iter].nmerged = (int64_t)tot + novf;
+      st->iter = sel.iter + 1;
+      st->K = sel.nid + 1;
+      st->maxc = sel.maxc;
+      st->ncand = sel.ncand;
+    }
+  }
+  dbg_stamp(D, 33);
+}

@@ -433,7 +433,7 @@ class GeoBPEEngine:
         n = self.L.geobpe_debug_state(self._ctx, _p(v), 10)
         if n < 0:
             self._chk(int(n))
-        keys = ("hot_list", "theta", "ncand", "maxc", "nskip", "cl_valid", "iter", "K", "post_valid", "plog_total")
+        keys = ("hot_list", "theta", "ncand", "maxc", "nskip", "cl_valid", "iter", "K", "post_valid", "pool_used")
         return {k: int(x) for k, x in zip(keys, v)}
 
     def marker(self, tag: int = 0):

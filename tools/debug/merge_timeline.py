@@ -1,0 +1,48 @@
+"""Phase timeline of k_find / k_commit (and k_select) for a few merges on the C3
+corpus (geobpe_debug_timeline): per-workgroup wall-clock stamps (100 MHz), relative
+to the first k_commit start."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "pt-bpe_amd"))
+import torch  # noqa: E402,F401
+from geobpe import _native, synth  # noqa: E402
+from geobpe.engine import GeoBPEEngine  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 100_000
+iters = [int(x) for x in (sys.argv[2] if len(sys.argv) > 2 else "1,6,20,200,800").split(",")]
+corpus = synth.make_corpus(synth.make_lengths(n, 40, 560, seed=0), seed=0)
+eng = GeoBPEEngine(corpus, 5).initialize()
+eng.bin()
+L = _native.lib()
+names = {0: "C.start", 1: "C.init", 2: "C.records", 3: "C.resolved", 4: "C.published", 5: "C.flush+klist", 6: "C.end",
+         10: "F.start", 11: "F.setup", 14: "F.r0.queued", 15: "F.r0.walked", 16: "F.r0.grouped", 12: "F.walked",
+         13: "F.end", 40: "F.w.T1", 41: "F.w.T2", 42: "F.w.T3", 43: "F.w.emitted", 44: "F.w.hashed", 30: "P.start", 31: "P.tokens", 32: "P.slots", 33: "P.end",
+         20: "S.start", 21: "S.scanned", 22: "S.max", 23: "S.ties", 24: "S.staged", 25: "S.tourn", 26: "S.end"}
+done = 0
+for it in iters:
+    eng.run(it - done - 1)
+    done = it - 1
+    m = L.geobpe_debug_timeline(eng._ctx, 1, None, 0)
+    eng.run(1)
+    done += 1
+    buf = np.zeros(m, dtype=np.int64)
+    L.geobpe_debug_timeline(eng._ctx, 0, buf.ctypes.data_as(ctypes.c_void_p), m)
+    t = buf.reshape(-1, 64)
+    t = t[(t > 0).any(axis=1)]
+    if len(t) == 0:
+        print(f"merge {it}: (no stamps)")
+        continue
+    base = t[:, 0][t[:, 0] > 0].min() if (t[:, 0] > 0).any() else t[t > 0].min()
+    rel = (t - base) / 100.0
+    rel[t == 0] = np.nan
+    last = eng.merges[-1]
+    print(f"merge {it}: count {last[1]} merged {last[2]}  workgroups {len(t)}")
+    cols = [k for k in range(64) if not np.all(np.isnan(rel[:, k]))]
+    for k in sorted(cols, key=lambda k: np.nanmedian(rel[:, k])):
+        col = rel[:, k]
+        print(f"  {names.get(k, str(k)):14s} min {np.nanmin(col):8.1f}  med {np.nanmedian(col):8.1f}  max {np.nanmax(col):8.1f}")
+eng.close()
