@@ -181,7 +181,7 @@ def main():
         rep.run(args.warmup)
         rep.set_profiling(True)
         rep.run(done)
-        for k in ("select", "find", "commit", "place"):
+        for k in ("select", "find", "commit"):
             ms, nl = rep.kernel_ms(k)
             kern[k] = {"ms_total": round(ms, 4), "launches": nl, "avg_us": round(1000 * ms / max(nl, 1), 3)}
         assert rep.merges == merges_log, "replay diverged"

@@ -83,6 +83,7 @@ struct State {
   int32_t post_valid, plog_ovf;
   int64_t pool_used, npost;   // pool chunks handed out since the last rebuild; rebuilds so far
   int64_t nko2[2];            // key records past the fixed slots, by launch parity
+  int32_t place_par, pad3;    // launch parity of the merge k_place writes out (-1: none)
   int64_t slot_max;    // pipelined exchange: the largest slot count of the last import (every rank)
 };
 

@@ -70,6 +70,7 @@ struct geobpe_ctx {
   int nb = 2048;  // grid of the streaming helper kernels (= D.NB)
   int64_t gen = 0;            // merge-loop launch pairs so far (parity selects Sel / overflow buffers)
   bool mark_pending = false;  // step_select decided a merge whose mark/apply are due
+  bool place_pending = false; // a k_commit ran whose k_place has not (it rides with the next k_select)
   bool pipelined = false;     // between geobpe_pipeline_begin and _end (device-side parity)
   int nba = 256;  // find / commit / finalize / bin / import workgroups (= D.NBA, <= NBA_MAX)
   // profiling
@@ -185,7 +186,16 @@ int check_device_error(geobpe_ctx* c) {
   }
 }
 
+// the last committed merge's k_place, when no k_select has carried it yet
+void flush_place(geobpe_ctx* c) {
+  if (!c->place_pending) return;
+  c->place_pending = false;
+  Timed t(c, "place");
+  hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D);
+}
+
 int sync_state(geobpe_ctx* c) {
+  flush_place(c);
   HIPCHK(c, hipMemcpyAsync(c->h_state, c->D.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return check_device_error(c);
@@ -260,12 +270,17 @@ void enqueue_commit(geobpe_ctx* c, bool to_delta) {
 // k_apply, on launch parity gen & 1 (the double-buffered Sel record and
 // merge-overflow counter)
 void enqueue_select(geobpe_ctx* c) {
-  Timed t(c, "select");
-  if (c->replay)
+  if (c->replay) {
+    flush_place(c);
+    Timed t(c, "select");
     hipLaunchKernelGGL(k_select_replay, dim3(1), dim3(64), 0, c->stream, c->D, (int)(c->gen & 1),
                        (const ReplayRec*)c->replay, c->replay_n);
-  else
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SBLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
+    return;
+  }
+  Timed t(c, "select");  // (+ the previous merge's k_place in workgroups 1..nba)
+  const int grid = c->place_pending ? 1 + c->nba : 1;
+  c->place_pending = false;
+  hipLaunchKernelGGL(k_select, dim3(grid), dim3(SBLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
 }
 void enqueue_mark(geobpe_ctx* c) {
   Timed t(c, "find");
@@ -277,10 +292,10 @@ void enqueue_apply(geobpe_ctx* c) {
     hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0,
                        (int)(c->gen & 1));
   }
-  {
-    Timed t(c, "place");
-    hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
-  }
+  c->place_pending = true;
+#ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
+  flush_place(c);
+#endif
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1), c->ev, c->ev_cap,
                        c->ev_n);
@@ -301,6 +316,7 @@ int read_sel(geobpe_ctx* c, Sel* out) {
 // the state and the decision of the last select in one wait: two async copies
 // into pinned memory, one stream synchronisation
 int sync_state_sel(geobpe_ctx* c, Sel* out) {
+  flush_place(c);
   HIPCHK(c, hipMemcpyAsync(c->h_state, c->D.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipMemcpyAsync(c->h_sel, c->D.sel + (c->gen & 1), sizeof(Sel), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -329,8 +345,10 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   HIPCHK(c, hipHostMalloc((void**)&c->h_state, sizeof(State), hipHostMallocDefault));
   HIPCHK(c, hipHostMalloc((void**)&c->h_sel, sizeof(Sel), hipHostMallocDefault));
   memset(c->h_state, 0, sizeof(State));
+  c->h_state->place_par = -1;
   int rc;
   if ((rc = dalloc(c, &c->D.st, 1, 0)) || (rc = dalloc(c, &c->D.sel, 2, 0))) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->D.st, c->h_state, sizeof(State), hipMemcpyHostToDevice, c->stream));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->ncu = prop.multiProcessorCount;
@@ -880,8 +898,10 @@ int geobpe_pipeline_begin(geobpe_ctx* c) {
 int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   if (!c || !c->pipelined || !d_buf) return GEOBPE_EARG;
   {
-    Timed t(c, "select");
-    hipLaunchKernelGGL(k_select, dim3(1), dim3(SBLOCK), 0, c->stream, c->D, -1);
+    Timed t(c, "select");  // (+ the previous merge's k_place)
+    const int grid = c->place_pending ? 1 + c->nba : 1;
+    c->place_pending = false;
+    hipLaunchKernelGGL(k_select, dim3(grid), dim3(SBLOCK), 0, c->stream, c->D, -1);
   }
   {
     Timed t(c, "find");
@@ -891,10 +911,10 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     Timed t(c, "commit");
     hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
   }
-  {
-    Timed t(c, "place");
-    hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, -1);
-  }
+  c->place_pending = true;
+#ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
+  flush_place(c);
+#endif
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
   {
@@ -991,6 +1011,7 @@ int64_t geobpe_num_keys(geobpe_ctx* c) {
 }
 
 static int row_token_offsets(geobpe_ctx* c, std::vector<int64_t>& off, int64_t** d_off) {
+  flush_place(c);
   int64_t* dn;
   HIPCHK(c, hipMalloc(&dn, (c->nrows + 1) * 8));
   hipLaunchKernelGGL(k_row_ntok, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, dn);

@@ -359,6 +359,8 @@ __global__ __launch_bounds__(ABLOCK) void k_finalize(Dev D, int to_delta) {
   agg_flush_hot(agg, D, hot, to_delta != 0, th);
 }
 
+#include "merge.h"
+
 // ====================================================================== argmax + tie-break
 // the reference key string json.dumps(geo, sort_keys=True) of a content, char by
 // char (same rendering as keyjson.h::render_key)
@@ -676,6 +678,12 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
   State* st = D.st;
+  if (blockIdx.x > 0) {  // the previous merge's k_place rides along (it needs only k_commit's output)
+    __shared__ PlaceLds P;
+    place_body(D, blockIdx.x - 1, P);
+    return;
+  }
+  if (par == INT32_MIN) return;  // place only
   if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
     if (st->stall) return;
     const int32_t g = st->dgen + 1;
@@ -938,8 +946,6 @@ __global__ __launch_bounds__(64) void k_select_replay(Dev D, int par, const Repl
   out->wg = r.g;
   out->widR = r.idR;
 }
-
-#include "merge.h"
 
 // ====================================================================== multi-rank deltas
 // merge events for the checkpoint's merge tree (TokenHierarchy / BinaryTreeBuilder.

@@ -292,7 +292,7 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
   }
   dbg_stamp(D, 44);
   // the rest of the run: (c, d) while (b, c) and (c, d) are both W
-  int32_t cur_b = b, cur_c = c, cur_pkb = pkb;
+  int32_t cur_c = c, cur_pkb = pkb;
   bool cur_cL = cL;
   int32_t lcur_c = tok_len(tc.y);
   while (cur_pkb == W && cur_cL) {
@@ -313,7 +313,6 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
       right_half(D, F, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
       emit_single(D, F, S.curK, h);
     }
-    cur_b = b2;
     cur_c = c2i;
     cur_pkb = pkb2;
     cur_cL = cL2;
@@ -662,6 +661,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   if (j == 0 && threadIdx.x == 0) {
     st->L_ovf2[par ^ 1] = 0;  // the next find's overflow counters (idle since the last pair)
     st->nko2[par ^ 1] = 0;
+    st->place_par = sel.decision == SEL_MERGE ? par : -1;  // k_place's merge (with the next select)
     if (sel.decision == SEL_DONE) {
       st->done = 1;
       st->maxc = 0;
@@ -897,6 +897,20 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     for (int32_t i = threadIdx.x; i < n; i += blockDim.x) klist_put(D, s_kl[0] + i, reg[i]);
   }
   dbg_stamp(D, 5);
+  if (j == 0) {  // merges made this iteration -> merge log, state (k_select reads iter / K)
+    int32_t nm = 0;
+    for (int32_t i = threadIdx.x; i < D.NBA; i += blockDim.x) nm += D.Lcnt[i];
+    int32_t tot;
+    block_excl_scan(nm, &tot, S.red);
+    if (threadIdx.x == 0) {
+      const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
+      D.log[sel.iter].nmerged = (int64_t)tot + novf;
+      st->iter = sel.iter + 1;
+      st->K = sel.nid + 1;
+      st->maxc = sel.maxc;
+      st->ncand = sel.ncand;
+    }
+  }
   dbg_stamp(D, 6);
 }
 
@@ -913,24 +927,23 @@ struct PlaceLds {
   int32_t red[ABLOCK / 64];
 };
 
-__global__ __launch_bounds__(ABLOCK) void k_place(Dev D, int par) {
-  __shared__ PlaceLds S;
+// place the merge committed with launch parity st->place_par (k_commit sets it; -1:
+// nothing to place).  Idempotent until the next k_find: a re-run writes the same
+// values (the pipelined exchange may run it again behind a stall).
+__device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   State* st = D.st;
-  if (par < 0) {  // pipelined exchange (k_select set dgen)
-    if (st->stall) return;
-    par = st->dgen & 1;
-  }
+  const int32_t par = st->place_par;
+  if (par < 0) return;
   const Sel sel = D.sel[par];
   if (sel.decision != SEL_MERGE) return;
-  const int32_t j = blockIdx.x;
   dbg_stamp(D, 30);
   const int32_t nid = sel.nid;
   const int32_t nA = D.Lcnt[j];
   const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
-  const int64_t oper = (novf + gridDim.x - 1) / gridDim.x;
+  const int64_t oper = (novf + D.NBA - 1) / D.NBA;
   const int64_t o_lo = (int64_t)j * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
   const int64_t nko = min(st->nko2[par], D.KO_cap);
-  const int64_t kper = (nko + gridDim.x - 1) / gridDim.x;
+  const int64_t kper = (nko + D.NBA - 1) / D.NBA;
   const int64_t k_lo = (int64_t)j * kper, k_n = max((int64_t)0, min(nko, k_lo + kper) - k_lo);
   {
     const int32_t c = threadIdx.x < D.NBA ? D.cntK[(int64_t)threadIdx.x * D.NBA + j] : 0;
@@ -1000,18 +1013,9 @@ __global__ __launch_bounds__(ABLOCK) void k_place(Dev D, int par) {
     __syncthreads();
   }
   dbg_stamp(D, 32);
-  if (j == 0) {  // merges applied this iteration -> merge log, state
-    int32_t nm = 0;
-    for (int32_t i = threadIdx.x; i < D.NBA; i += blockDim.x) nm += D.Lcnt[i];
-    int32_t tot;
-    block_excl_scan(nm, &tot, S.red);
-    if (threadIdx.x == 0) {
-      D.log[sel.iter].nmerged = (int64_t)tot + novf;
-      st->iter = sel.iter + 1;
-      st->K = sel.nid + 1;
-      st->maxc = sel.maxc;
-      st->ncand = sel.ncand;
-    }
-  }
-  dbg_stamp(D, 33);
+}
+
+__global__ __launch_bounds__(ABLOCK) void k_place(Dev D) {
+  __shared__ PlaceLds S;
+  place_body(D, blockIdx.x, S);
 }

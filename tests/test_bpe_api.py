@@ -291,3 +291,47 @@ def test_rank_gather_helpers():
     ]
     a, b, eoff = BPE._merge_rank_events(parts)
     assert a.tolist() == [3, 7, 12, 15] and b.tolist() == [4, 8, 13, 16] and eoff.tolist() == [0, 3, 4]
+
+
+def _utility_golden():
+    import json
+    import os
+    from conftest import GOLDEN
+    with open(os.path.join(GOLDEN, "codebook_utility.json")) as f:
+        return json.load(f)
+
+
+def _close(u, want):
+    for k, v in want.items():
+        assert abs(u[k] - v) <= 1e-5 * max(1.0, abs(v)), (k, u[k], v)
+
+
+def test_codebook_utility_matches_reference_vectors():
+    """get_codebook_utility against the reference function's own outputs
+    (plotting.py:78-95 run in the build container: tests/golden/make_utility_golden.py)
+    on the fixtures' encoded ids; float32 arithmetic, tolerance 1e-5 relative."""
+    from conftest import load_golden
+    from geobpe.bpe import get_codebook_utility
+    for name, g in _utility_golden().items():
+        ids = g["ids"] if "ids" in g else load_golden(name)[2]["ids"]
+        _close(get_codebook_utility(ids, g["vocab_size"]), g["utility"])
+
+
+@pytest.mark.gpu
+def test_codebook_utility_of_device_encoding():
+    """The stats of bin/encode.py (codebook utility of quantize(tokenize()) over every
+    chain) on the HIP path's own encoding equal the reference's numbers."""
+    from conftest import load_golden
+    from geobpe.bpe import get_codebook_utility
+    from geobpe.engine import GeoBPEEngine
+    for name, g in _utility_golden().items():
+        if "ids" in g:
+            continue
+        meta, corpus, _ = load_golden(name)
+        eng = GeoBPEEngine(corpus, meta["bins"]["1"], device=0, strategy=meta.get("bin_strategy")).initialize()
+        eng.bin()
+        eng.run(len(meta["merges"]))
+        ids, _ = eng.encode()
+        assert eng.vocab_size == g["vocab_size"]
+        _close(get_codebook_utility(ids, eng.vocab_size), g["utility"])
+        eng.close()
