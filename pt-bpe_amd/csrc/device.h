@@ -345,6 +345,11 @@ __device__ inline void dbg_stamp(const Dev& D, int k) {
   if (D.dbg && threadIdx.x == 0 && k < DBG_SLOTS) D.dbg[(int64_t)blockIdx.x * DBG_SLOTS + k] = (int64_t)wall_clock64();
 }
 
+// debug timeline: a value instead of a time stamp (thread 0)
+__device__ inline void dbg_val(const Dev& D, int k, int64_t v) {
+  if (D.dbg && threadIdx.x == 0 && k < DBG_SLOTS) D.dbg[(int64_t)blockIdx.x * DBG_SLOTS + k] = v;
+}
+
 __device__ inline uint32_t post_bkt(int32_t d) { return ((uint32_t)d * 2654435761u) >> (32 - NBKT_LOG2); }
 
 // token record fields (int4 tok[s] = {tid, tlen, tprev, pk})

@@ -436,11 +436,13 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   if ((rc = dalloc(c, &D.post, (int64_t)c->nba * D.PR)) || (rc = dalloc(c, &D.poff, (int64_t)c->nba * (NBKT + 1), 0)) ||
       (rc = dalloc(c, &D.pool, D.POOL_CH * D.CHUNK)) || (rc = dalloc(c, &D.pch, (int64_t)c->nba * D.MAXCH)) ||
       (rc = dalloc(c, &D.pnch, c->nba, 0)) || (rc = dalloc(c, &D.pfill, c->nba, 0)) ||
-      (rc = dalloc(c, &D.KS, (int64_t)c->nba * c->nba * SK)) || (rc = dalloc(c, &D.cntK, (int64_t)c->nba * c->nba, 0)) ||
+      (rc = dalloc(c, &D.KS, (int64_t)c->nba * c->nba * SK + D.KO_cap)) || (rc = dalloc(c, &D.cntK, (int64_t)c->nba * c->nba, 0)) ||
       (rc = dalloc(c, &D.DS, (int64_t)c->nba * c->nba * SD)) || (rc = dalloc(c, &D.cntD, (int64_t)c->nba * c->nba, 0)) ||
-      (rc = dalloc(c, &D.KO, D.KO_cap)) || (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) ||
-      (rc = dalloc(c, &D.KSid, (int64_t)c->nba * c->nba * SK)) || (rc = dalloc(c, &D.KOid, D.KO_cap)))
+      (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) ||
+      (rc = dalloc(c, &D.KSid, (int64_t)c->nba * c->nba * SK + D.KO_cap)))
     return rc;
+  D.KO = D.KS + (int64_t)c->nba * c->nba * SK;  // (one allocation: a record index into KS covers both)
+  D.KOid = D.KSid + (int64_t)c->nba * c->nba * SK;
   const int need[6] = {GEOBPE_COL_PHI, GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_TAU, GEOBPE_COL_CAC1N,
                        GEOBPE_COL_C1NCA};
   for (int q = 0; q < 6; q++) {

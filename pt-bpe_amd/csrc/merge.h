@@ -617,7 +617,7 @@ __device__ inline int32_t ckc_slot(CommitLds& S, u64 k, bool insert, bool* res) 
 // this owner's claim list; find: EHASH check record).  The owner is the only
 // workgroup resolving this key in this launch, so the first probe is the CAS itself
 // (it returns what the slot holds: empty -> claimed, the key -> found).
-__device__ inline int32_t commit_resolve(const Dev& D, CommitLds& S, const KRec& k, bool* claimed_out = nullptr) {
+__device__ __attribute__((always_inline)) inline int32_t commit_resolve(const Dev& D, CommitLds& S, const KRec& k, bool* claimed_out = nullptr) {
   bool claimed = false;
   const u64 s0 = ht_first_slot(D, k.pkey);
   const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s0], 0ULL, (unsigned long long)k.pkey);
@@ -647,18 +647,88 @@ __device__ inline void log_put(const Dev& D, const CommitLds& S, int64_t pos, in
   D.pool[(int64_t)S.chunk[c] * D.CHUNK + pos % D.CHUNK] = make_int2(d, slot);
 }
 
+// record i past the first PER of each finder's slot (prefix sums preE over finders),
+// then the overflow list: its index in KS (KO is KS's tail, from NBA * NBA * SK)
+__device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nba, int32_t j, int32_t PER, int32_t nE,
+                                   int32_t i) {
+  if (i < nE) {
+    const int32_t ww = seg_of(preE, nba, i);
+    return ((int64_t)j * nba + ww) * SK + PER + (i - preE[ww]);
+  }
+  return (int64_t)nba * nba * SK + (i - nE);
+}
+
+// a record whose key did not fit the dedupe table: resolved and counted on its own
+__device__ __attribute__((always_inline)) inline void commit_fallback(const Dev& D, CommitLds& S, HotApp& hot, const KRec& k, bool tod, int32_t th) {
+  const int32_t d = commit_resolve(D, S, k);
+  if (d >= 0) {
+    atomicAdd(&S.fbn, k.n);
+    if (tod)
+      global_add(D, d, k.n, true);
+    else
+      count_add_hot(D, hot, d, k.n, th);
+  }
+}
+
+// a record's key id and posting-log position (block-uniform: every thread calls it)
+__device__ __attribute__((always_inline)) inline void commit_publish(const Dev& D, CommitLds& S, bool mine, const KRec& k, int64_t at) {
+  int32_t d = -1;
+  if (mine) {
+    bool res;
+    const int32_t s = ckc_slot(S, k.pkey, false, &res);
+    if (s >= 0) {
+      d = S.cid[s];
+      if (S.ch1[s] != k.h1) {  // same probe key, other content
+        set_error(D, GEOBPE_EHASH, -13);
+        d = -1;
+      }
+    } else {  // (round 1 resolved it on its own: find it again)
+      bool claimed;
+      d = ht_resolve(D, k.pkey, ht_first_slot(D, k.pkey), ht_probe(D, ht_first_slot(D, k.pkey)), &claimed);
+    }
+  }
+  const int32_t n = mine && d >= 0 ? k.n : 0;
+  int32_t tot;
+  const int32_t ex = block_excl_scan(n, &tot, S.red);
+  if (mine) {
+    const int2 v = make_int2(d >= 0 ? d : -1, S.logok && d >= 0 ? (int32_t)(S.logpos + ex) : -1);
+    D.KSid[at] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) S.logpos += tot;
+}
+
 __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par) {
   __shared__ CommitLds S;
   __shared__ HotApp hot;
   __shared__ int64_t s_kl[2];
+  __shared__ int32_t s_preE[NBA_MAX + 1], s_preF[NBA_MAX + 1];
   State* st = D.st;
   if (par < 0) {  // pipelined exchange (k_select set dgen)
     if (st->stall) return;
     par = st->dgen & 1;
   }
-  const Sel sel = D.sel[par];
   const int32_t j = blockIdx.x;
-  if (j == 0 && threadIdx.x == 0) {
+  // ---- one round of loads for everything that depends only on j: the record
+  // counts of every finder and, speculatively, the first PER records of each
+  // finder's slot (a finder sends an owner ~1-2 records in the heavy merges), the
+  // same for the decrement records, the log cursor, the state
+  const int32_t nba = D.NBA;
+  const int32_t PER = ABLOCK / nba;  // >= 4 (NBA <= 256)
+  const int32_t t = threadIdx.x;
+  const int32_t w = t % nba, k0 = t / nba;
+  const bool lane_ok = k0 < PER;
+  const int64_t seg = (int64_t)j * nba + w;
+  const int32_t cK = D.cntK[seg], cD = D.cntD[seg];
+  const KRec r0 = D.KS[seg * SK + min(k0, SK - 1)];
+  const int2 d0 = D.DS[seg * SD + min(k0, SD - 1)];
+  const Sel sel = D.sel[par];
+  const int32_t th = st->theta;
+  const int32_t pn = D.pnch[j], pf = D.pfill[j];
+  const int64_t nko_raw = st->nko2[par];
+  int32_t lc = 0;
+  if (j == 0 && t < nba) lc = D.Lcnt[t];
+  if (j == 0 && t == 0) {
     st->L_ovf2[par ^ 1] = 0;  // the next find's overflow counters (idle since the last pair)
     st->nko2[par ^ 1] = 0;
     st->place_par = sel.decision == SEL_MERGE ? par : -1;  // k_place's merge (with the next select)
@@ -678,44 +748,42 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   dbg_stamp(D, 0);
   const bool tod = to_delta != 0;
   const int32_t nid = sel.nid;
-  const int32_t th = st->theta;
   if (j == 0) {  // _tokens[n] = json.loads(key): content(L) ++ [g] ++ content(R)
     const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
     const int64_t vL = D.voff[L], vR = D.voff[Rr];
     const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
     const int64_t pos = D.voff[nid], ln = nL + 1 + nR;
     if (pos + ln > D.VSC) {
-      if (threadIdx.x == 0) set_error(D, GEOBPE_ECAPACITY, -9);
+      if (t == 0) set_error(D, GEOBPE_ECAPACITY, -9);
     } else {
-      for (int64_t i = threadIdx.x; i < ln; i += blockDim.x)
+      for (int64_t i = t; i < ln; i += blockDim.x)
         D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
-      if (threadIdx.x == 0) D.voff[nid + 1] = pos + ln;
+      if (t == 0) D.voff[nid + 1] = pos + ln;
     }
   }
-  // ---- owner j's record counts (every finder), state
-  for (int i = threadIdx.x; i < CKC; i += ABLOCK) {
+  for (int i = t; i < CKC; i += ABLOCK) {
     S.ckey[i] = 0;
     S.cn[i] = 0;
   }
-  for (int i = threadIdx.x; i < AggT<12>::N; i += ABLOCK) {
+  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
     S.u.agg.key[i] = -1;
     S.u.agg.val[i] = 0;
   }
   hot_init(hot);
-  {
-    const int32_t cK = threadIdx.x < D.NBA ? D.cntK[(int64_t)j * D.NBA + threadIdx.x] : 0;
-    const int32_t cD = threadIdx.x < D.NBA ? D.cntD[(int64_t)j * D.NBA + threadIdx.x] : 0;
-    int32_t totK, totD;
-    const int32_t eK = block_excl_scan(cK, &totK, S.red);
-    const int32_t eD = block_excl_scan(cD, &totD, S.red);
-    if (threadIdx.x < D.NBA) {
-      S.preK[threadIdx.x] = eK;
-      S.preD[threadIdx.x] = eD;
+  {  // records past the first PER of a finder's slot: prefix sums
+    const int32_t eK = t < nba ? max(0, min(cK, SK) - PER) : 0;
+    const int32_t eD = t < nba ? max(0, min(cD, SD) - PER) : 0;
+    int32_t totE, totF;
+    const int32_t xE = block_excl_scan(eK, &totE, S.red);
+    const int32_t xF = block_excl_scan(eD, &totF, S.red);
+    if (t < nba) {
+      s_preE[t] = xE;
+      s_preF[t] = xF;
     }
-    if (threadIdx.x == 0) {
-      S.preK[D.NBA] = totK;
-      S.preD[D.NBA] = totD;
-      S.nKO = (int32_t)min(st->nko2[par], D.KO_cap);
+    if (t == 0) {
+      s_preE[nba] = totE;
+      s_preF[nba] = totF;
+      S.nKO = (int32_t)min(nko_raw, D.KO_cap);
       S.ns = 0;
       S.chk = 0;
       S.fbn = 0;
@@ -725,38 +793,34 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   }
   __syncthreads();
   dbg_stamp(D, 1);
-  // ---- round 1: this owner's key records -> LDS dedupe (occurrence totals per key)
-  const int32_t nrec = S.preK[D.NBA] + S.nKO;
-  for (int32_t i = threadIdx.x; i < nrec; i += ABLOCK) {
-    KRec k;
-    int64_t at;
-    if (!commit_rec(D, S, j, i, k, &at)) continue;
-    bool res;
-    const int32_t s = ckc_slot(S, k.pkey, true, &res);
-    if (s >= 0) {
-      if (res) {
-        S.ch1[s] = k.h1;
-        S.cfirst[s] = i;
-        S.ch2[s] = k.h2;
-        S.crep[s] = make_int4(k.len, k.idL, k.g, k.idR);
-      }
-      atomicAdd(&S.cn[s], k.n);
-    } else {  // dedupe table full: this record on its own (found again in round 2)
-      const int32_t d = commit_resolve(D, S, k);
-      if (d >= 0) {
-        atomicAdd(&S.fbn, k.n);
-        if (tod)
-          global_add(D, d, k.n, true);
-        else
-          count_add_hot(D, hot, d, k.n, th);
-      }
-    }
+  // ---- round 1: key records -> LDS dedupe (occurrence totals per key); decrements -> LDS
+#define COMMIT_INSERT(k)                                          \
+  do {                                                            \
+    bool res_;                                                    \
+    const int32_t s_ = ckc_slot(S, (k).pkey, true, &res_);        \
+    if (s_ >= 0) {                                                \
+      if (res_) {                                                 \
+        S.ch1[s_] = (k).h1;                                       \
+        S.ch2[s_] = (k).h2;                                       \
+        S.crep[s_] = make_int4((k).len, (k).idL, (k).g, (k).idR); \
+      }                                                           \
+      atomicAdd(&S.cn[s_], (k).n);                                \
+    } else {                                                      \
+      commit_fallback(D, S, hot, (k), tod, th);                   \
+    }                                                             \
+  } while (0)
+  const bool mine0 = lane_ok && k0 < min(cK, SK);
+  if (mine0) COMMIT_INSERT(r0);
+  if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) global_add(D, d0.x, d0.y, tod);
+  const int32_t nE = s_preE[nba], nF = s_preF[nba], nKO = S.nKO;
+  for (int32_t i = t; i < nE + nKO; i += ABLOCK) {  // extras, then the overflow list
+    const int64_t at = extra_at(D, s_preE, nba, j, PER, nE, i);
+    const KRec k = D.KS[at];
+    if (i < nE || owner_of_key(D, k.pkey) == j) COMMIT_INSERT(k);
   }
-  // decrement records -> LDS aggregation
-  const int32_t ndec = S.preD[D.NBA];
-  for (int32_t i = threadIdx.x; i < ndec; i += ABLOCK) {
-    const int32_t lo = seg_of(S.preD, D.NBA, i);
-    const int2 x = D.DS[((int64_t)j * D.NBA + lo) * SD + (i - S.preD[lo])];
+  for (int32_t i = t; i < nF; i += ABLOCK) {
+    const int32_t ww = seg_of(s_preF, nba, i);
+    const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
     if (!agg_stage(S.u.agg, x.x, x.y)) global_add(D, x.x, x.y, tod);
   }
   __syncthreads();
@@ -764,7 +828,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
   int32_t nlog = 0;
   const bool alone = S.fbn == 0;  // no key of this owner was resolved outside the table
-  for (int32_t s = threadIdx.x; s < CKC; s += ABLOCK) {
+  for (int32_t s = t; s < CKC; s += ABLOCK) {
     const u64 key = S.ckey[s];
     if (key == 0) continue;
     KRec k;
@@ -796,25 +860,17 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   {
     int32_t tot;
     block_excl_scan(nlog, &tot, S.red);
-    if (threadIdx.x == 0) {
-      S.lognew = tot + S.fbn;  // (+ records whose key did not fit the dedupe table)
-      const int32_t nc = D.pnch[j];
-      const int64_t p0 = nc > 0 ? (int64_t)(nc - 1) * D.CHUNK + D.pfill[j] : 0;
+    if (t == 0) {
+      const int64_t add = (int64_t)tot + S.fbn;  // (+ records whose key did not fit the dedupe table)
+      const int64_t p0 = pn > 0 ? (int64_t)(pn - 1) * D.CHUNK + pf : 0;
       S.logpos = p0;
       S.logok = 0;
-      const int64_t cap = p0 + S.lognew;
-      const int32_t c0 = (int32_t)(p0 / D.CHUNK);
-      const int32_t c1 = (int32_t)((cap + D.CHUNK - 1) / D.CHUNK);  // chunks [c0, c1) cover the appends
-      S.c0 = c0;
-      if (!st->plog_ovf && c1 - c0 <= LOG_CH_MAX && c1 <= D.MAXCH) {
-        const int32_t need = max(0, c1 - nc);
+      const int32_t c1 = (int32_t)((p0 + add + D.CHUNK - 1) / D.CHUNK);  // chunks [0, c1) hold the log
+      if (!st->plog_ovf && c1 - (int32_t)(p0 / D.CHUNK) <= LOG_CH_MAX && c1 <= D.MAXCH) {
+        const int32_t need = max(0, c1 - pn);
         const int64_t base = need ? (int64_t)atomicAdd((unsigned long long*)&st->pool_used, (unsigned long long)need) : 0;
         if (base + need <= D.POOL_CH) {
-          for (int32_t c = c0; c < c1; c++) {
-            const int32_t id = c < nc ? D.pch[(int64_t)j * D.MAXCH + c] : (int32_t)(base + (c - nc));
-            S.chunk[c - c0] = id;
-            if (c >= nc) D.pch[(int64_t)j * D.MAXCH + c] = id;
-          }
+          for (int32_t c = pn; c < c1; c++) D.pch[(int64_t)j * D.MAXCH + c] = (int32_t)(base + (c - pn));
           S.logok = 1;
         }
       }
@@ -824,49 +880,25 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   __syncthreads();
   dbg_stamp(D, 3);
   // ---- round 2: every record's key id and posting-log position (k_place writes pk
-  // and the log entries of its occurrence slots)
-  for (int32_t i0 = 0; i0 < nrec; i0 += ABLOCK) {  // block-uniform
-    const int32_t i = i0 + threadIdx.x;
-    KRec k;
-    int64_t at = 0;
-    bool mine = i < nrec && commit_rec(D, S, j, i, k, &at);
-    int32_t d = -1;
-    if (mine) {
-      bool res;
-      const int32_t s = ckc_slot(S, k.pkey, false, &res);
-      if (s >= 0) {
-        d = S.cid[s];
-        if (S.ch1[s] != k.h1) {  // same probe key, other content
-          set_error(D, GEOBPE_EHASH, -13);
-          d = -1;
-        }
-      } else {  // (round 1 resolved it on its own: find it again)
-        bool claimed;
-        d = ht_resolve(D, k.pkey, ht_first_slot(D, k.pkey), ht_probe(D, ht_first_slot(D, k.pkey)), &claimed);
-      }
-    }
-    const int32_t n = mine && d >= 0 ? k.n : 0;
-    int32_t tot;
-    const int32_t ex = block_excl_scan(n, &tot, S.red);
-    if (mine) {
-      const int2 v = make_int2(d >= 0 ? d : -1, S.logok && d >= 0 ? (int32_t)(S.logpos + ex) : -1);
-      if (at >= 0)
-        D.KSid[at] = v;
-      else
-        D.KOid[-at - 1] = v;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) S.logpos += tot;
+  // and the log entries of its occurrence slots); the first PER records per finder
+  // are still in registers
+  commit_publish(D, S, mine0, r0, seg * SK + k0);
+  for (int32_t i0 = 0; i0 < nE + nKO; i0 += ABLOCK) {  // block-uniform
+    const int32_t i = i0 + t;
+    const int64_t at = i < nE + nKO ? extra_at(D, s_preE, nba, j, PER, nE, i) : 0;
+    const KRec k = D.KS[at];
+    const bool mine = i < nE + nKO && (i < nE || owner_of_key(D, k.pkey) == j);
+    commit_publish(D, S, mine, k, at);
   }
   dbg_stamp(D, 4);
   // ---- decrements of this owner's keys: one atomic per key
-  for (int i = threadIdx.x; i < AggT<12>::N; i += ABLOCK) {
+  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
     const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
     if (k < 0 || v == 0) continue;
     global_add(D, k, v, tod);
   }
   hot_flush(D, hot);  // (syncs the workgroup first)
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     D.chkcnt[j] = min(S.chk, (int32_t)D.RC);
     if (S.logok) {
       const int64_t end = S.logpos;
@@ -882,7 +914,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   __syncthreads();
   {
     const int32_t n = min(S.ns, (int32_t)D.RC);
-    if (threadIdx.x == 0 && n) {
+    if (t == 0 && n) {
       if (s_kl[1] - s_kl[0] < n) {
         const int64_t sz = max((int64_t)KL_CHUNK, (int64_t)n);
         s_kl[0] = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
@@ -894,15 +926,13 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     }
     __syncthreads();
     const int32_t* reg = D.ns + (int64_t)j * D.RC;
-    for (int32_t i = threadIdx.x; i < n; i += blockDim.x) klist_put(D, s_kl[0] + i, reg[i]);
+    for (int32_t i = t; i < n; i += blockDim.x) klist_put(D, s_kl[0] + i, reg[i]);
   }
   dbg_stamp(D, 5);
   if (j == 0) {  // merges made this iteration -> merge log, state (k_select reads iter / K)
-    int32_t nm = 0;
-    for (int32_t i = threadIdx.x; i < D.NBA; i += blockDim.x) nm += D.Lcnt[i];
     int32_t tot;
-    block_excl_scan(nm, &tot, S.red);
-    if (threadIdx.x == 0) {
+    block_excl_scan(lc, &tot, S.red);
+    if (t == 0) {
       const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
       D.log[sel.iter].nmerged = (int64_t)tot + novf;
       st->iter = sel.iter + 1;

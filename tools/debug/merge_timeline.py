@@ -36,6 +36,12 @@ for it in iters:
     if len(t) == 0:
         print(f"merge {it}: (no stamps)")
         continue
+    vals = {7: "C.records(n)", 8: "C.decrements(n)"}
+    for k, nm in vals.items():  # values, not times
+        v = t[:, k][t[:, k] > 0]
+        if len(v):
+            print(f"  {nm:14s} min {v.min():8d}  med {int(np.median(v)):8d}  max {v.max():8d}  sum {v.sum()}")
+        t[:, k] = 0
     base = t[:, 0][t[:, 0] > 0].min() if (t[:, 0] > 0).any() else t[t > 0].min()
     rel = (t - base) / 100.0
     rel[t == 0] = np.nan
