@@ -38,8 +38,13 @@ CONFIGS = {
     "c5": (100_000, 40, 560, 5, 5000),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
-APPLY_BYTES_PER_MERGE = 156  # algorithmic bytes of one merged occurrence in k_apply
-MARK_HIT_BYTES = 24  # k_mark per merged occurrence: pk/tprev/tlen of the hit, pk of p, pk/tlen of b
+# algorithmic bytes
+FIND_BYTES_PER_OCC = 128   # k_find per merged occurrence: posting entry 8, token records of p, g, b, c 64,
+                           # vocab hashes of p and c 32, merge entry 16, two occurrence slots (T) 8
+PLACE_BYTES_PER_OCC = 76   # k_place: merge entry 16, T 8, token rewrites 28, two pk 8, two log entries 16
+COMMIT_KREC_BYTES = 56     # k_commit per key record: 48 read + (id, log position) 8 written
+COMMIT_DREC_BYTES = 8      # per decrement record
+COMMIT_KEY_BYTES = 44      # per key: table slot 8 (CAS), count 4, payload (h1, h2, len, representative) 32
 PMC_WINDOWS = os.path.join(REPO, "profiles", "pmc_windows.json")
 REF_TIMING = os.path.join(REPO, "profiles", "reference_cpu_timing.json")
 
@@ -84,7 +89,7 @@ def parse():
                     help="N > 1: RCCL (default); gloo puts every rank on GPU 0 (a one-GPU rehearsal of the N > 1 path)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
-    ap.add_argument("--roofline-kernel", default="commit")
+    ap.add_argument("--roofline-kernel", default="auto", help="auto: the slower of k_find / k_commit")
     ap.add_argument("--event-stride", type=int, default=8,
                     help="time every k-th launch of the roofline kernel in the timed region")
     return ap.parse_args()
@@ -144,7 +149,7 @@ def main():
     pack_ms = eng.kernel_ms("bin_pack")[0]  # layout step for the merge loop (pk into the token records)
     eng.run(args.warmup)
     # ---- timed region: exactly K merges; HIP events only around the roofline kernels
-    eng.set_profiling(not args.no_profile, only=f"{args.roofline_kernel},find", stride=args.event_stride)
+    eng.set_profiling(not args.no_profile, only="find,commit", stride=args.event_stride)
     st0 = eng.state()
     eng.marker(1)  # window bracket for rocprofv3 (outside the timer)
     if world > 1:
@@ -162,8 +167,7 @@ def main():
         tt = torch.tensor([T], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
-    live_ms, live_n = eng.kernel_ms(args.roofline_kernel) if not args.no_profile else (0.0, 0)
-    mark_ms, mark_n = eng.kernel_ms("find") if not args.no_profile else (0.0, 0)
+    ktimes = {k: (eng.kernel_ms(k) if not args.no_profile else (0.0, 0)) for k in ("find", "commit")}
     merges_log = list(eng.merges)
     R_local = int(shard["row_off"][-1])
     if rank != 0:
@@ -174,54 +178,59 @@ def main():
 
     # ---- per-kernel table: a replay of the same merges with every kernel timed
     kern = {}
+    commit_work = None
     if not args.no_profile and world == 1 and not args.no_replay:
         rep = GeoBPEEngine(shard, B, device=local, max_vocab=1 << 20)
         rep.initialize()
         rep.bin()
         rep.run(args.warmup)
-        rep.set_profiling(True)
+        rep.set_profiling(True)  # (every launch timed; k_commit's work counters on)
+        rs0 = rep.state()
         rep.run(done)
+        rs1 = rep.state()
         for k in ("select", "find", "commit"):
             ms, nl = rep.kernel_ms(k)
-            kern[k] = {"ms_total": round(ms, 4), "launches": nl, "avg_us": round(1000 * ms / max(nl, 1), 3)}
+            kern["select+place" if k == "select" else k] = {"ms_total": round(ms, 4), "launches": nl,
+                                                           "avg_us": round(1000 * ms / max(nl, 1), 3)}
+        commit_work = {k: rs1[k] - rs0[k] for k in ("commit_key_records", "commit_decrement_records", "commit_keys")}
         assert rep.merges == merges_log, "replay diverged"
         rep.close()
 
-    # ---- roofline of the loop's dominant kernels, from the live events of the timed region
+    # ---- roofline of the loop's kernels, from the live events of the timed region
     wkey = f"config={args.config},warmup={args.warmup},steps={args.steps},n={world}"
     window = merges_log[-done:] if done else []
     n_merged = sum(m[2] for m in window)
-    roofline = None
-    if live_n:
-        avg_s = live_ms / 1000.0 / live_n
-        # 156 B per merged occurrence (token records of p, a, b, c; two
-        # glue symbols; neighbour content hashes; two key-table probes; the rewritten
-        # token fields; five count read-modify-writes)
-        bytes_per_launch = APPLY_BYTES_PER_MERGE * n_merged / max(done, 1)
-        note = f"{APPLY_BYTES_PER_MERGE} B x merged occurrences (avg {n_merged / max(done, 1):.0f} per launch)"
-        ach = bytes_per_launch / avg_s / 1e9
-        traffic, tsrc = pmc_traffic(args.roofline_kernel, wkey)
-        roofline = {"kernel": f"k_{args.roofline_kernel}", "bound": "hbm", "achieved": round(ach, 2),
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": traffic,
-                    "traffic_source": tsrc, "traffic_window": wkey, "bytes_per_launch": round(bytes_per_launch, 1),
-                    "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": live_n,
-                    "event_stride": args.event_stride, "algorithmic_bytes": note}
-    mark_roof = None
-    if mark_n:
-        avg_s = mark_ms / 1000.0 / mark_n
-        scan = not st0["post_valid"] and not st1["post_valid"]
-        if scan:  # every mark of the window scanned the 2 B/slot fingerprints; 24 B per hit confirmed
-            bpl = 2.0 * R_local + MARK_HIT_BYTES * n_merged / max(done, 1)
-            note = f"2 B x {R_local} residue slots (fingerprint scan) + {MARK_HIT_BYTES} B x merged occurrences"
-        else:  # posting mode: 8 B per posting entry read is not counted per launch here
-            bpl = None
-            note = "posting-index mode in the window: per-launch entry count not recorded"
-        traffic, tsrc = pmc_traffic("mark", wkey)
-        ach = bpl / avg_s / 1e9 if bpl else None
-        mark_roof = {"kernel": "k_mark", "bound": "hbm", "achieved": round(ach, 2) if ach else None,
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
-                     "traffic": traffic, "traffic_source": tsrc, "bytes_per_launch": round(bpl, 1) if bpl else None,
-                     "avg_launch_us": round(avg_s * 1e6, 3), "launches_timed": mark_n, "algorithmic_bytes": note}
+    per = lambda x: x / max(done, 1)  # noqa: E731
+    work = {"find": (FIND_BYTES_PER_OCC * per(n_merged),
+                     f"{FIND_BYTES_PER_OCC} B x merged occurrences (avg {per(n_merged):.0f} per launch)"),
+            "commit": (None, "k_commit work counters come from the profiled replay (--no-replay: unknown)")}
+    if commit_work:
+        cw = {k: per(v) for k, v in commit_work.items()}
+        work["commit"] = (COMMIT_KREC_BYTES * cw["commit_key_records"] + COMMIT_DREC_BYTES * cw["commit_decrement_records"]
+                          + COMMIT_KEY_BYTES * cw["commit_keys"],
+                          f"{COMMIT_KREC_BYTES} B x key records + {COMMIT_DREC_BYTES} B x decrement records + "
+                          f"{COMMIT_KEY_BYTES} B x keys (avg {cw['commit_key_records']:.0f} / "
+                          f"{cw['commit_decrement_records']:.0f} / {cw['commit_keys']:.0f} per launch, counted in the "
+                          f"profiled replay of the same merges)")
+    roofs = {}
+    for k, (ms, nl) in ktimes.items():
+        if not nl:
+            continue
+        avg_s = ms / 1000.0 / nl
+        bpl, note = work[k]
+        ach = bpl / avg_s / 1e9 if bpl is not None else None
+        traffic, tsrc = pmc_traffic(k, wkey)
+        roofs[k] = {"kernel": f"k_{k}", "bound": "hbm", "achieved": round(ach, 2) if ach else None,
+                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
+                    "traffic": traffic, "traffic_source": tsrc, "traffic_window": wkey,
+                    "bytes_per_launch": round(bpl, 1) if bpl is not None else None, "avg_launch_us": round(avg_s * 1e6, 3),
+                    "launches_timed": nl, "event_stride": args.event_stride, "algorithmic_bytes": note}
+    if args.roofline_kernel == "auto":
+        dom = max(roofs, key=lambda k: roofs[k]["avg_launch_us"]) if roofs else None
+    else:
+        dom = args.roofline_kernel if args.roofline_kernel in roofs else None
+    roofline = roofs.get(dom) if dom else None
+    roofline_other = {k: v for k, v in roofs.items() if k != dom}
     # the full content-keyed pair-count pass (BPE.bin) at iteration 0: SURVEY §8(d)
     # B_count = 20*T_live + 4*U_live with T = residues
     pair_count = None
@@ -271,7 +280,7 @@ def main():
                    if args.config in ("c3", "c5") else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
                    "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}"},
         "roofline": roofline,
-        "roofline_mark": mark_roof,
+        "roofline_other": roofline_other,
         "cpu_baseline": cpu,
         "pair_count_pass": pair_count,
         "kernels": kern,

@@ -139,6 +139,9 @@ int geobpe_pipeline_resolve(geobpe_ctx *ctx, const void *d_in, int64_t n_records
 int geobpe_pipeline_end(geobpe_ctx *ctx);
 /* Residues of the whole (all-rank) corpus: sizes the replicated key table. */
 int geobpe_set_global_residues(geobpe_ctx *ctx, int64_t n);
+/* This context's rank in the exchange (pipelined import: its own slot's records carry
+   their local key ids, so they are not probed again). */
+int geobpe_set_rank(geobpe_ctx *ctx, int32_t rank);
 
 /* ---- introspection / exports ---- */
 /* Key string (json.dumps(geo, sort_keys=True)) of vocab id v's content. */

@@ -84,6 +84,7 @@ struct State {
   int64_t pool_used, npost;   // pool chunks handed out since the last rebuild; rebuilds so far
   int64_t nko2[2];            // key records past the fixed slots, by launch parity
   int32_t place_par, pad3;    // launch parity of the merge k_place writes out (-1: none)
+  int64_t stat_krec, stat_drec, stat_keys;  // k_commit work (profiling only): key records, decrement records, keys
   int64_t slot_max;    // pipelined exchange: the largest slot count of the last import (every rank)
 };
 
@@ -210,6 +211,12 @@ struct Dev {
   int64_t TC;
   // optional phase timeline (geobpe_debug_timeline): DBG_SLOTS wall-clock stamps per workgroup
   int64_t* dbg;
+  int32_t stats, pad4;  // k_commit accumulates stat_* (profiling)
+  // pipelined exchange: k_commit writes this rank's delta records straight into the
+  // slot buffer (xrec[0 .. xcap), st->ntouched counts them; no touched list, no
+  // rank-local delta array, no export pass); null: the touched-list path
+  DeltaRec* xrec;
+  int64_t xcap;
   int64_t ovf_cap;
   // argmax
   int32_t* clist;  // hot list (capacity KCAP)
@@ -403,7 +410,54 @@ __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_de
     atomicAdd(&D.count[d], v);
     return;
   }
+  if (D.xrec) {  // pipelined exchange: a record of its own (the LDS-staged paths reserve per workgroup)
+    const unsigned long long j = atomicAdd((unsigned long long*)&D.st->ntouched, 1ULL);
+    if ((int64_t)j < D.xcap) {
+      DeltaRec r;
+      r.h1 = D.kh1[d];
+      r.h2 = D.kh2[d];
+      r.len = D.klen[d];
+      r.idL = D.krep[3 * (int64_t)d];
+      r.g = D.krep[3 * (int64_t)d + 1];
+      r.idR = D.krep[3 * (int64_t)d + 2];
+      r.delta = v;
+      r.pad = d + 1;
+      D.xrec[j] = r;
+    }
+    return;
+  }
   if (atomicAdd(&D.dcount[d], v) == 0) touched_append(D, d);
+}
+
+// rank-local deltas of one workgroup whose keys join the touched list: buffered in
+// LDS, one reservation on the global list per workgroup (a wave-level reservation
+// from every workgroup queues thousands of atomics on one counter)
+constexpr int TB_N = 2048;
+struct TouchBuf {
+  int32_t n;
+  int32_t buf[TB_N];
+};
+__device__ inline void touch_add(const Dev& D, TouchBuf& tb, int32_t d, int32_t v) {
+  if (atomicAdd(&D.dcount[d], v) != 0) return;
+  const int32_t j = atomicAdd(&tb.n, 1);
+  if (j < TB_N)
+    tb.buf[j] = d;
+  else
+    touched_append(D, d);
+}
+__device__ inline void touch_flush(const Dev& D, TouchBuf& tb) {
+  __shared__ unsigned long long s_base;
+  __syncthreads();
+  const int32_t n = min(tb.n, TB_N);
+  if (threadIdx.x == 0 && n > 0) s_base = atomicAdd((unsigned long long*)&D.st->ntouched, (unsigned long long)n);
+  __syncthreads();
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const int64_t j = (int64_t)s_base + i;
+    if (j < D.KCAP)
+      D.touched[j] = tb.buf[i];
+    else
+      set_error(D, GEOBPE_ECAPACITY, -31);
+  }
 }
 
 // LDS-staged per-workgroup partial counts, flushed with one global atomic per

@@ -63,6 +63,7 @@ struct geobpe_ctx {
   unsigned long long* ev_n = nullptr;
   int32_t bin_cube[2] = {0, 0};  // cube shape (CL, CG) of the last dense bin
   int64_t global_residues = 0;
+  int32_t rank = 0;  // this context's slot in the pipelined exchange
   // host vocab mirror (content per token id), synced lazily from the device log
   std::vector<std::vector<int32_t>> vocab;
   int32_t K0 = 0;
@@ -613,6 +614,12 @@ int geobpe_set_global_residues(geobpe_ctx* c, int64_t n) {
   return 0;
 }
 
+int geobpe_set_rank(geobpe_ctx* c, int32_t rank) {
+  if (!c || rank < 0 || rank >= PIPE_MAX_WORLD) return GEOBPE_EARG;
+  c->rank = rank;
+  return 0;
+}
+
 int geobpe_set_bin_dense(geobpe_ctx* c, int on) {
   if (!c) return GEOBPE_EARG;
   if (c->keys_ready) return fail(c, GEOBPE_EARG, "set_bin_dense must precede bin()");
@@ -905,13 +912,16 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     c->place_pending = false;
     hipLaunchKernelGGL(k_select, dim3(grid), dim3(SBLOCK), 0, c->stream, c->D, -1);
   }
+  Dev D = c->D;  // find and commit write this rank's delta records into the slot buffer
+  D.xrec = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
+  D.xcap = cap_total;
   {
     Timed t(c, "find");
-    hipLaunchKernelGGL(k_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
+    hipLaunchKernelGGL(k_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D, 1, -1);
   }
   {
     Timed t(c, "commit");
-    hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 1, -1);
+    hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D, 1, -1);
   }
   c->place_pending = true;
 #ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
@@ -921,8 +931,7 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
   {
     Timed t(c, "export");
-    DeltaRec* out = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
-    hipLaunchKernelGGL(k_export_dev, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, out, cap_total, 1, (int64_t*)d_buf);
+    hipLaunchKernelGGL(k_export_head, dim3(1), dim3(64), 0, c->stream, c->D, (int64_t*)d_buf, cap_total);
   }
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -933,7 +942,7 @@ int geobpe_pipeline_import(geobpe_ctx* c, const void* d_slots, int32_t world, in
   {
     Timed t(c, "import");
     hipLaunchKernelGGL(k_import_fixed, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, (const uint8_t*)d_slots, world,
-                       cap_fixed);
+                       cap_fixed, c->rank < world ? c->rank : -1);
   }
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -1032,10 +1041,11 @@ int64_t geobpe_debug_state(geobpe_ctx* c, int64_t* h_out, int64_t cap) {
   if (!c || !h_out || cap < 10) return GEOBPE_EARG;
   if (int rc = sync_state(c)) return rc;
   const State& s = *c->h_state;
-  const int64_t v[10] = {s.ncl2[s.cl_act], s.theta, s.ncand, s.maxc, s.nskip, s.cl_valid,
-                         s.iter, s.K, s.post_valid, s.pool_used};
-  for (int i = 0; i < 10; i++) h_out[i] = v[i];
-  return 10;
+  const int64_t v[13] = {s.ncl2[s.cl_act], s.theta, s.ncand, s.maxc, s.nskip, s.cl_valid,
+                         s.iter, s.K, s.post_valid, s.pool_used, s.stat_krec, s.stat_drec, s.stat_keys};
+  const int64_t n = std::min<int64_t>(cap, 13);
+  for (int64_t i = 0; i < n; i++) h_out[i] = v[i];
+  return n;
 }
 
 int64_t geobpe_num_tokens(geobpe_ctx* c) {
@@ -1216,6 +1226,7 @@ int geobpe_set_profiling(geobpe_ctx* c, int on) {
   collect_events(c);
   c->prof = on > 0;
   c->prof_stride = on > 1 ? on : 1;
+  c->D.stats = c->prof && c->prof_stride == 1 ? 1 : 0;  // (work counters only under full profiling)
   c->prof_seen.clear();
   c->ktime.clear();
   return 0;

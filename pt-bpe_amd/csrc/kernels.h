@@ -1022,6 +1022,16 @@ __global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int6
     out[j] = r;
   }
 }
+// pipelined exchange: the slot header of the records k_commit wrote (no-op while
+// stalled: the stalled merge's records stay for the full re-exchange)
+__global__ void k_export_head(Dev D, int64_t* d_count, int64_t cap) {
+  State* st = D.st;
+  if (st->stall) return;
+  const int64_t n = st->ntouched;
+  d_count[0] = n;
+  if (n > cap) set_error(D, GEOBPE_ECAPACITY, -30);
+}
+
 __global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap) {
   State* st = D.st;
   const int64_t n = st->ntouched;
@@ -1054,7 +1064,7 @@ __global__ __launch_bounds__(ABLOCK) void k_import(Dev D, const DeltaRec* in, in
 // no LDS aggregation to gain), with the hot-list crossing check; a found key's
 // content joins this workgroup's check region (verified by the next k_mark, as
 // k_apply's finds are).  Also opens the next delta epoch (the export consumed it).
-__global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* in, int world, int64_t capf) {
+__global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* in, int world, int64_t capf, int myrank) {
   __shared__ int32_t s_ns, s_chk, s_bad;
   __shared__ int64_t s_cnt[PIPE_MAX_WORLD + 1];
   __shared__ HotApp hot;
@@ -1097,6 +1107,10 @@ __global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* i
     const DeltaRec* recs = reinterpret_cast<const DeltaRec*>(in + r * slot + sizeof(DeltaRec));
     const DeltaRec rr = recs[j - s_cnt[r]];
     if (rr.delta == 0) continue;
+    if (r == myrank && rr.pad > 0) {  // this rank's own record: its key id, resolved by k_commit
+      count_add_hot(D, hot, rr.pad - 1, rr.delta, th);
+      continue;
+    }
     bool claimed;
     const int32_t d = ht_insert(D, rr.h1, rr.h2, rr.len, &claimed);
     if (d < 0) continue;

@@ -548,6 +548,8 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
 }
 
 // ---------------------------------------------------------------------- k_commit
+struct CommitLds;
+__device__ void commit_export(const Dev& D, CommitLds& S);
 struct CommitLds {
   union {
     AggT<12> agg;  // decrements of this owner's keys
@@ -698,11 +700,59 @@ __device__ __attribute__((always_inline)) inline void commit_publish(const Dev& 
   if (threadIdx.x == 0) S.logpos += tot;
 }
 
+// pipelined exchange: this owner's delta records -- every resolved key with its
+// occurrence total, every decremented key with its (negative) total -- straight
+// into the rank's slot buffer, one reservation per workgroup.  The import adds every
+// rank's records (this rank's included) to the replicated counts.
+__device__ void commit_export(const Dev& D, CommitLds& S) {
+  __shared__ unsigned long long s_xb;
+  const int t = threadIdx.x;
+  int32_t c = 0;
+  for (int32_t s = t; s < CKC; s += ABLOCK) c += S.ckey[s] != 0 && S.cid[s] >= 0;
+  for (int i = t; i < AggT<12>::N; i += ABLOCK) c += S.u.agg.key[i] >= 0 && S.u.agg.val[i] != 0;
+  int32_t tot;
+  const int32_t ex = block_excl_scan(c, &tot, S.red);
+  if (t == 0) s_xb = tot ? atomicAdd((unsigned long long*)&D.st->ntouched, (unsigned long long)tot) : 0ULL;
+  __syncthreads();
+  int64_t j = (int64_t)s_xb + ex;
+  for (int32_t s = t; s < CKC; s += ABLOCK) {
+    if (S.ckey[s] == 0 || S.cid[s] < 0) continue;
+    const int4 rp = S.crep[s];
+    DeltaRec r;
+    r.h1 = S.ch1[s];
+    r.h2 = S.ch2[s];
+    r.len = rp.x;
+    r.idL = rp.y;
+    r.g = rp.z;
+    r.idR = rp.w;
+    r.delta = S.cn[s];
+    r.pad = S.cid[s] + 1;  // (the import of this rank's own slot uses it instead of probing)
+    if (j < D.xcap) D.xrec[j] = r;
+    j++;
+  }
+  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+    const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
+    if (k < 0 || v == 0) continue;
+    DeltaRec r;
+    r.h1 = D.kh1[k];
+    r.h2 = D.kh2[k];
+    r.len = D.klen[k];
+    r.idL = D.krep[3 * (int64_t)k];
+    r.g = D.krep[3 * (int64_t)k + 1];
+    r.idR = D.krep[3 * (int64_t)k + 2];
+    r.delta = v;
+    r.pad = k + 1;
+    if (j < D.xcap) D.xrec[j] = r;
+    j++;
+  }
+}
+
 __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par) {
   __shared__ CommitLds S;
   __shared__ HotApp hot;
   __shared__ int64_t s_kl[2];
   __shared__ int32_t s_preE[NBA_MAX + 1], s_preF[NBA_MAX + 1];
+  __shared__ TouchBuf tb;
   State* st = D.st;
   if (par < 0) {  // pipelined exchange (k_select set dgen)
     if (st->stall) return;
@@ -770,6 +820,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     S.u.agg.val[i] = 0;
   }
   hot_init(hot);
+  if (t == 0) tb.n = 0;
   {  // records past the first PER of a finder's slot: prefix sums
     const int32_t eK = t < nba ? max(0, min(cK, SK) - PER) : 0;
     const int32_t eD = t < nba ? max(0, min(cD, SD) - PER) : 0;
@@ -826,7 +877,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   __syncthreads();
   dbg_stamp(D, 2);
   // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
-  int32_t nlog = 0;
+  int32_t nlog = 0, nkeys = 0;
   const bool alone = S.fbn == 0;  // no key of this owner was resolved outside the table
   for (int32_t s = t; s < CKC; s += ABLOCK) {
     const u64 key = S.ckey[s];
@@ -846,7 +897,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     if (d >= 0) {
       const int32_t n = S.cn[s];
       if (tod) {
-        global_add(D, d, n, true);
+        if (!D.xrec) touch_add(D, tb, d, n);  // (direct records: written below)
       } else if (claimed && alone) {  // a new key only this thread adds to: its count is n
         D.count[d] = n;
         if (th > 0 && n >= th) hot_push(D, hot, d);
@@ -854,6 +905,18 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
         count_add_hot(D, hot, d, n, th);
       }
       nlog += n;
+      nkeys++;
+    }
+  }
+  if (D.stats) {  // (profiling: the work of this launch, for the bench's algorithmic bytes)
+    int32_t tk, tr, td;
+    block_excl_scan(nkeys, &tk, S.red);
+    block_excl_scan(mine0 ? 1 : 0, &tr, S.red);
+    block_excl_scan(lane_ok && k0 < min(cD, SD) ? 1 : 0, &td, S.red);
+    if (t == 0) {
+      atomicAdd((unsigned long long*)&st->stat_keys, (unsigned long long)tk);
+      atomicAdd((unsigned long long*)&st->stat_krec, (unsigned long long)(tr + nE + nKO));
+      atomicAdd((unsigned long long*)&st->stat_drec, (unsigned long long)(td + nF));
     }
   }
   // posting-log space for this merge's new pairs of this owner (one reservation)
@@ -895,8 +958,13 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   for (int i = t; i < AggT<12>::N; i += ABLOCK) {
     const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
     if (k < 0 || v == 0) continue;
-    global_add(D, k, v, tod);
+    if (!tod)
+      atomicAdd(&D.count[k], v);
+    else if (!D.xrec)
+      touch_add(D, tb, k, v);
   }
+  if (tod && !D.xrec) touch_flush(D, tb);  // (block-uniform)
+  if (tod && D.xrec) commit_export(D, S);  // (block-uniform)
   hot_flush(D, hot);  // (syncs the workgroup first)
   if (t == 0) {
     D.chkcnt[j] = min(S.chk, (int32_t)D.RC);

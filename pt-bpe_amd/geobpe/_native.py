@@ -68,6 +68,7 @@ def lib():
         "geobpe_delta_import": (ctypes.c_int, [P, P, I64]),
         "geobpe_set_distributed": (ctypes.c_int, [P, ctypes.c_int]),
         "geobpe_set_global_residues": (ctypes.c_int, [P, I64]),
+        "geobpe_set_rank": (ctypes.c_int, [P, ctypes.c_int32]),
         "geobpe_token_json": (I64, [P, I32, ctypes.c_char_p, I64]),
         "geobpe_token_content": (I64, [P, I32, P, I64]),
         "geobpe_vocab_count": (I64, [P]),
@@ -113,7 +114,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_quantize", "geobpe_symbol_first", "geobpe_init_tokens", "geobpe_bin", "geobpe_set_bin_dense", "geobpe_step",
     "geobpe_run", "geobpe_merge_log", "geobpe_key_json", "geobpe_debug_key_less", "geobpe_debug_counts", "geobpe_debug_state", "geobpe_debug_key",
     "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
-    "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_token_json", "geobpe_token_content",
+    "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_set_rank", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
     "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_marker", "geobpe_synchronize",
     "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",

@@ -152,8 +152,10 @@ class TorchGroup:
         ok = False
         try:
             engine._chk(L.geobpe_pipeline_poll(ctx, out))
-            it0, done, ahead = int(out[1]), 0, 1
-            capf = int(fixed) if fixed else self.PIPE_CAP_MIN
+            # the poll window and the slot size carry over from the last call (a run of
+            # merges is often split into several calls: warm-up, timed window)
+            it0, done, ahead = int(out[1]), 0, getattr(self, "_ahead", 1)
+            capf = int(fixed) if fixed else getattr(self, "_capf", self.PIPE_CAP_MIN)
             with T.cuda.stream(engine.torch_stream):
                 while done < n_merges:
                     slot = (1 + capf) * REC
@@ -179,6 +181,7 @@ class TorchGroup:
                     if not fixed:
                         capf = min(self.PIPE_CAP_MAX, max(self.PIPE_CAP_MIN, 1 << (2 * max(smax, 1) - 1).bit_length()))
                     done = it - it0
+                    self._ahead, self._capf = ahead, capf
                     if fin:
                         break
             ok = True

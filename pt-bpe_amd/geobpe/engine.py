@@ -226,6 +226,7 @@ class GeoBPEEngine:
         if self.distributed:
             self._chk(self.L.geobpe_set_distributed(self._ctx, 1))
             self._chk(self.L.geobpe_set_global_residues(self._ctx, self.group.total_residues))
+            self._chk(self.L.geobpe_set_rank(self._ctx, int(getattr(self.group, "rank", 0))))
         self._chk(self.L.geobpe_set_bin_dense(self._ctx, 1 if self.bin_dense else 0))
         self._chk(self.L.geobpe_bin(self._ctx))
         if self.distributed:
@@ -429,11 +430,12 @@ class GeoBPEEngine:
 
     def state(self) -> dict:
         """Loop state (hot list, threshold, posting index) after a synchronisation."""
-        v = np.zeros(10, dtype=np.int64)
-        n = self.L.geobpe_debug_state(self._ctx, _p(v), 10)
+        v = np.zeros(13, dtype=np.int64)
+        n = self.L.geobpe_debug_state(self._ctx, _p(v), 13)
         if n < 0:
             self._chk(int(n))
-        keys = ("hot_list", "theta", "ncand", "maxc", "nskip", "cl_valid", "iter", "K", "post_valid", "pool_used")
+        keys = ("hot_list", "theta", "ncand", "maxc", "nskip", "cl_valid", "iter", "K", "post_valid", "pool_used",
+                "commit_key_records", "commit_decrement_records", "commit_keys")
         return {k: int(x) for k, x in zip(keys, v)}
 
     def marker(self, tag: int = 0):
