@@ -45,7 +45,11 @@ FIXTURES = {
     # config 1 shape: the bundled PDB subset (tests/golden/pdb, from the reference's
     # data/vqvae_pretrain/train) featurised by pdb_angles.py, 5 bins, 50 merges
     "c1_pdb12_b5": ("pdb", None, None, 5, 50, 0, 0.0),
+    # config 1 at its stated size: every PDB of the reference's data/vqvae_pretrain/train
+    # (72 files, read here at generation time; only the featurised angles travel)
+    "c1_pdb72_b5": ("pdb72", None, None, 5, 50, 0, 0.0),
 }
+PDB72 = "/root/reference/data/vqvae_pretrain/train"
 
 
 def _stub_optional_deps():
@@ -82,9 +86,9 @@ def run_one(name: str) -> None:
 
     n_seqs, lo, hi, bins, merges, seed, rep = FIXTURES[name][:7]
     strategy = FIXTURES[name][7] if len(FIXTURES[name]) > 7 else "histogram"
-    if n_seqs == "pdb":
+    if n_seqs in ("pdb", "pdb72"):
         import pdb_angles
-        corpus, _ = pdb_angles.pdb_dir_corpus(os.path.join(HERE, "pdb"))
+        corpus, _ = pdb_angles.pdb_dir_corpus(os.path.join(HERE, "pdb") if n_seqs == "pdb" else PDB72)
         n_seqs = len(corpus["row_off"]) - 1
     else:
         lengths = synth.make_lengths(n_seqs, lo, hi, seed=seed)
