@@ -123,8 +123,9 @@ int geobpe_set_distributed(geobpe_ctx *ctx, int on);
 /* Pipelined multi-rank loop (no host wait per merge).  The
    reference has no distributed step (BPE.step, bpe.py:1792-2166, is serial); this
    replaces a host-synchronised step_select / step_apply / delta exchange per merge.
-   Per iteration: geobpe_pipeline_iter enqueues select / mark / apply and the export
-   into d_buf = [header record: int64 count][records ... cap_total]; the caller
+   Per iteration: geobpe_pipeline_iter enqueues select (+ the previous merge's place) /
+   find / commit, which write this rank's delta records straight into
+   d_buf = [header record: int64 count][records ... cap_total], and the header; the caller
    all-gathers the first (1 + cap_fixed) records of every rank's d_buf; then
    geobpe_pipeline_import consumes the gathered slots.  A rank whose count exceeds
    cap_fixed stalls every pipelined kernel; geobpe_pipeline_poll reports
@@ -177,12 +178,15 @@ int64_t geobpe_encode(geobpe_ctx *ctx, int32_t *h_ids, int64_t *h_row_id_off);
  * keys (0 = consistent), or -1 on error. */
 int64_t geobpe_verify_counts(geobpe_ctx *ctx);
 /* Per-kernel time (ms summed over launches, HIP events on the context stream)
- * while profiling is enabled.  names: "pair_count", "finalize" (bin), "select",
- * "mark", "apply" (merge loop), "recount".  on = 0: off; on = 1: every
+ * while profiling is enabled.  names: "pair_count", "finalize", "bin_pack" (bin),
+ * "select" (+ the previous merge's place), "find", "commit", "place" (a place
+ * launched on its own), "recount".  The merge loop's k_commit also counts its work
+ * (key / decrement records, keys: geobpe_debug_state) when on = 1.  on = 0: off; on = 1: every
  * launch; on = k > 1: every k-th launch of each kernel (sampling keeps the event
  * packets from stretching the stream they measure). */
 int geobpe_set_profiling(geobpe_ctx *ctx, int on);
-/* Debug: per-workgroup phase timestamps (wall clock, 100 MHz) of k_apply.
+/* Debug: per-workgroup phase timestamps (wall clock, 100 MHz) of k_select / k_find /
+ * k_commit / k_place (tools/debug/merge_timeline.py).
  * on = 1 enables and clears (returns the slot count); on = 0 copies up to cap
  * stamps to h_out and disables. */
 int64_t geobpe_debug_timeline(geobpe_ctx *ctx, int on, int64_t *h_out, int64_t cap);
