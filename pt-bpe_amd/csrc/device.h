@@ -84,7 +84,8 @@ struct State {
   int64_t pool_used, npost;   // pool chunks handed out since the last rebuild; rebuilds so far
   int64_t nko2[2];            // key records past the fixed slots, by launch parity
   int32_t place_par, pad3;    // launch parity of the merge k_place writes out (-1: none)
-  int64_t stat_krec, stat_drec, stat_keys;  // k_commit work (profiling only): key records, decrement records, keys
+  int64_t stat_krec, stat_drec, stat_keys;
+  int64_t nxovf;  // entries of Dev.xovf (pipelined exchange)  // k_commit work (profiling only): key records, decrement records, keys
   int64_t slot_max;    // pipelined exchange: the largest slot count of the last import (every rank)
 };
 
@@ -217,6 +218,7 @@ struct Dev {
   // rank-local delta array, no export pass); null: the touched-list path
   DeltaRec* xrec;
   int64_t xcap;
+  int2* xovf;  // (key, delta) of the rare unstaged adds of a pipelined iteration
   int64_t ovf_cap;
   // argmax
   int32_t* clist;  // hot list (capacity KCAP)
@@ -410,20 +412,13 @@ __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_de
     atomicAdd(&D.count[d], v);
     return;
   }
-  if (D.xrec) {  // pipelined exchange: a record of its own (the LDS-staged paths reserve per workgroup)
-    const unsigned long long j = atomicAdd((unsigned long long*)&D.st->ntouched, 1ULL);
-    if ((int64_t)j < D.xcap) {
-      DeltaRec r;
-      r.h1 = D.kh1[d];
-      r.h2 = D.kh2[d];
-      r.len = D.klen[d];
-      r.idL = D.krep[3 * (int64_t)d];
-      r.g = D.krep[3 * (int64_t)d + 1];
-      r.idR = D.krep[3 * (int64_t)d + 2];
-      r.delta = v;
-      r.pad = d + 1;
-      D.xrec[j] = r;
-    }
+  if (D.xrec) {  // pipelined exchange, rare path: (key, delta) to a side list that k_export_head
+                 // turns into records (a record built here costs k_find its register budget)
+    const unsigned long long j = atomicAdd((unsigned long long*)&D.st->nxovf, 1ULL);
+    if ((int64_t)j < D.KCAP)
+      D.xovf[j] = make_int2(d, v);
+    else
+      set_error(D, GEOBPE_ECAPACITY, -32);
     return;
   }
   if (atomicAdd(&D.dcount[d], v) == 0) touched_append(D, d);

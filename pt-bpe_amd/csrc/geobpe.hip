@@ -246,7 +246,7 @@ int alloc_keys(geobpe_ctx* c) {
       (rc = dalloc(c, &D.klist, D.KCAP, 0xFF)) || (rc = dalloc(c, &D.kchunk, 2 * (int64_t)c->nba, 0)))
     return rc;
   if (c->distributed) {
-    if ((rc = dalloc(c, &D.dcount, D.HC, 0)) ||
+    if ((rc = dalloc(c, &D.xovf, D.KCAP)) || (rc = dalloc(c, &D.dcount, D.HC, 0)) ||
         (rc = dalloc(c, &D.touched, D.KCAP)))
       return rc;
   }
@@ -931,7 +931,8 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
   {
     Timed t(c, "export");
-    hipLaunchKernelGGL(k_export_head, dim3(1), dim3(64), 0, c->stream, c->D, (int64_t*)d_buf, cap_total);
+    hipLaunchKernelGGL(k_export_head, dim3(16), dim3(BLOCK), 0, c->stream, c->D, reinterpret_cast<DeltaRec*>(d_buf) + 1,
+                       (int64_t*)d_buf, cap_total);
   }
   HIPCHK(c, hipGetLastError());
   return 0;

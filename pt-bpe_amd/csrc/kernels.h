@@ -1024,12 +1024,30 @@ __global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int6
 }
 // pipelined exchange: the slot header of the records k_commit wrote (no-op while
 // stalled: the stalled merge's records stay for the full re-exchange)
-__global__ void k_export_head(Dev D, int64_t* d_count, int64_t cap) {
+__global__ __launch_bounds__(BLOCK) void k_export_head(Dev D, DeltaRec* out, int64_t* d_count, int64_t cap) {
   State* st = D.st;
   if (st->stall) return;
-  const int64_t n = st->ntouched;
-  d_count[0] = n;
-  if (n > cap) set_error(D, GEOBPE_ECAPACITY, -30);
+  const int64_t n0 = st->ntouched, nx = min(st->nxovf, D.KCAP);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nx; i += (int64_t)gridDim.x * blockDim.x) {
+    const int2 e = D.xovf[i];  // the side list's (key, delta) as records
+    const int32_t d = e.x;
+    DeltaRec r;
+    r.h1 = D.kh1[d];
+    r.h2 = D.kh2[d];
+    r.len = D.klen[d];
+    r.idL = D.krep[3 * (int64_t)d];
+    r.g = D.krep[3 * (int64_t)d + 1];
+    r.idR = D.krep[3 * (int64_t)d + 2];
+    r.delta = e.y;
+    r.pad = d + 1;
+    if (n0 + i < cap) out[n0 + i] = r;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    const int64_t n = n0 + nx;
+    d_count[0] = n;
+    if (n > cap) set_error(D, GEOBPE_ECAPACITY, -30);
+    st->nxovf = 0;
+  }
 }
 
 __global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap) {

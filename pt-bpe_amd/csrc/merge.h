@@ -208,8 +208,8 @@ __device__ inline void dec_add(const Dev& D, const FindCtx& F, AggT<12>& agg, in
 }
 
 // the new key (X, glR, right) of occurrence t: right = X when c is a left part
-__device__ inline void right_half(const Dev& D, const FindCtx& F, int32_t t, int32_t glR, bool cL, int32_t idc,
-                                  int32_t lc, u64 c1, u64 c2, FHalf& h) {
+__device__ inline void right_half(const Dev& D, const FindCtx& F, const FindLds& S, int32_t t, int32_t glR, bool cL,
+                                  int32_t idc, int32_t lc, u64 c1, u64 c2, FHalf& h) {
   const int32_t rl = cL ? F.wl : lc;
   const u64 r1 = cL ? F.w1 : c1, r2 = cL ? F.w2 : c2;
   const int64_t ny = 2 * (int64_t)rl - 1;
@@ -287,7 +287,7 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
   }
   dbg_stamp(D, 43);
   if (c >= 0) {
-    right_half(D, F, g, glR, cL, tc.x, tok_len(tc.y), c1, c2, hr);
+    right_half(D, F, S, g, glR, cL, tc.x, tok_len(tc.y), c1, c2, hr);
     vr = true;
   }
   dbg_stamp(D, 44);
@@ -310,7 +310,7 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
     if (pkb2 >= 0) dec_add(D, F, S.u.m.agg, pkb2, -1);
     if (c2i >= 0) {
       FHalf h;
-      right_half(D, F, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
+      right_half(D, F, S, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
       emit_single(D, F, S.curK, h);
     }
     cur_c = c2i;
