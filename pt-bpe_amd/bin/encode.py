@@ -78,6 +78,10 @@ def parse_args(argv=None):
     p.add_argument("--bins", type=str2dict, default="1-10")
     p.add_argument("--p-min-size", type=int_or_inf, default=float("inf"))
     p.add_argument("--max-iter", type=int, default=10000)
+    p.add_argument("--num-p", type=str2dict, default="1-3",
+                   help="k-medoids partitions per token size (RMSD mode, --p-min-size < inf)")
+    p.add_argument("--max-num-strucs", type=int, default=500)
+    p.add_argument("--rmsd-super-res", type=str2bool, default=False)
     p.add_argument("--glue-opt", type=str2bool, default=False)
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--save-every", type=int, default=10)
@@ -194,6 +198,7 @@ def main(argv=None) -> int:
     bpe = BPE(shard, bins=args.bins, bin_strategy=args.bin_strategy, save_dir=args.save_dir,
               res_init=args.res_init, std_bonds=not args.free_bonds,
               rmsd_partition_min_size=args.p_min_size, glue_opt=args.glue_opt, seed=args.seed,
+              num_partitions=args.num_p, max_num_strucs=args.max_num_strucs, rmsd_super_res=args.rmsd_super_res,
               device=device, record_tree=args.ckpt_format == "pkl", group=group,
               global_corpus=corpus if group is not None else None)
     t0 = time.time()

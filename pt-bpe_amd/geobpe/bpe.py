@@ -170,6 +170,19 @@ def _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_siz
 
 
 class BPE:
+    def __new__(cls, *args, **kwargs):
+        """A finite rmsd_partition_min_size (the reference's default is 4) selects the
+        RMSD-partitioned mode, geobpe.rmsd_bpe.RmsdBPE."""
+        if cls is BPE:
+            import inspect
+            ba = inspect.signature(BPE.__init__).bind(None, *args, **kwargs)
+            ba.apply_defaults()
+            p = ba.arguments["rmsd_partition_min_size"]
+            if p != float("inf") and p < 10 ** 9:
+                from .rmsd_bpe import RmsdBPE
+                return RmsdBPE(*args, **kwargs)
+        return super().__new__(cls)
+
     def __init__(self, structures, bins, bin_strategy="histogram", save_dir="./plots/bpe",
                  compute_sec_structs=False, plot_iou_with_sec_structs=False, res_init=False, std_bonds=True,
                  rmsd_partition_min_size=4, rmsd_super_res=False, rmsd_only=False, num_partitions=3,

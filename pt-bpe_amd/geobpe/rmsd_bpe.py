@@ -1,0 +1,658 @@
+"""GeoBPE in the reference's RMSD-partitioned mode.
+
+With a finite ``rmsd_partition_min_size`` (p) the reference's ``BPE`` turns every token of at
+least p bonds into a family of k-medoids partitions under Kabsch RMSD:
+
+  reference (foldingdiff/bpe.py)                 here
+  _init_res_tokens, res_geo branch  :231-379     RmsdBPE._init_residues / _partition_residues
+  compute_geo_key (pt1 / pt2 rules) :1192-1299   RmsdBPE._pair_key
+  bin                               :1431-1474   RmsdBPE.bin
+  rmsd_partition                    :1739-1789   RmsdBPE._partition
+  step (RMSD branches, recurring    :1792-2166   RmsdBPE.step / _merge
+    keys, the repeat at :2164-2166)
+  _compute_assignment(_inner)       :645-657     RmsdBPE._assign (one device batch)
+  Tokenizer.compute_coords /        tokenizer.py:347-363, :204-230
+    key_coords                                   RmsdBPE._span_coords / _struc_coords
+
+Where the time goes in the reference -- NeRF coordinates and Kabsch RMSD of every
+occurrence against every medoid (process pools), and the O(M^2) k-medoids matrix -- runs on
+the GPU here as batches: one ``geobpe_nerf`` launch for all occurrences of a key, one
+``geobpe_rmsd`` launch for the matrix and one for occurrences x medoids (csrc/rmsd.h).
+
+The bookkeeping around them is host code, because the keys stop being content hashes in
+this mode: a partitioned token's interior enters the key as raw floats (the medoid's
+geometry) and the junction as bin indices (bpe.py:1247-1296), so the key of a span depends on
+where it is split and on which medoid each side was assigned.  The device engine of the
+scoped mode (split-invariant 2x61-bit content hashes) does not apply; this class keeps the
+reference's dictionaries instead, with the same add/remove sequence per key, so
+``list(_geo_dict[key])`` -- the order k-medoids sees the occurrences in -- is the reference's.
+
+Reachable configurations (tests/golden/rmsd_mode_probe.json, rm_p4.json): p <= 3 partitions
+the residues at initialize() and every merge; p >= 4 never creates ``_sphere_dict``, so the
+first merge of >= p bonds raises AttributeError there, as it does here.  Not built: glue
+optimisation (LBFGS, ``glue_opt=True``), ``rmsd_only``, free bonds in this mode.
+"""
+from __future__ import annotations
+
+import json
+import time
+from collections import defaultdict
+
+import numpy as np
+
+from . import rmsd as _rmsd
+from .synth import COLUMNS
+
+BOND_TYPES = ["N:CA", "CA:C", "0C:1N"]
+BOND_ANGLES = ["tau", "CA:C:1N", "C:1N:1CA"]
+DIHEDRALS = ["psi", "omega", "phi"]
+STD_LENGTH = {"N:CA": 1.46, "CA:C": 1.54, "0C:1N": 1.34}       # nerf.py:17-19
+GLUE = ["omega", "C:1N:1CA", "phi"]                            # bpe.py:383
+TWO_PI = 2 * np.pi
+# the residue-level partition keys of _sphere_dict (bpe.py:333-338)
+RES_SPHERE_KEY = {3: '{"N:CA": [0], "CA:C": [0], "0C:1N": [0], "tau": [0], "CA:C:1N": [0], "psi": [0]}',
+                  2: '{"CA:C": [0], "0C:1N": [0], "CA:C:1N": [0]}'}
+
+
+def _get_ind(v, values):
+    from .bpe import get_ind
+    return get_ind(v, values)
+
+
+class _Chain:
+    """One chain's internal coordinates (current and original) and segmentation: the state
+    of the reference's Tokenizer that this mode reads and writes (tokenizer.py:131-202,
+    253-286).  Bond j -> init N:CA / CA:C for j < 2, else column BOND_TYPES[j%3] row
+    (j-2)//3; angle a -> init tau for a = 0, else BOND_ANGLES[a%3] row (a-1)//3; dihedral d ->
+    DIHEDRALS[d%3] row (d+1)//3.  The init values are shared by both copies (the
+    reference's ``orig`` flag only switches the DataFrame)."""
+
+    __slots__ = ("cur", "orig", "init", "n", "token_pos", "btt", "fname")
+
+    def __init__(self, cols: dict, init, fname=None):
+        self.cur = {c: np.array(cols[c], dtype=np.float64) for c in COLUMNS}
+        self.orig = {c: np.array(cols[c], dtype=np.float64) for c in COLUMNS}
+        self.init = list(init)
+        self.n = len(self.cur["phi"])
+        self.token_pos = []
+        self.btt = {}
+        self.fname = fname
+
+    def _bond(self, j, src):
+        return self.init[j] if j < 2 else float(src[BOND_TYPES[j % 3]][(j - 2) // 3])
+
+    def _angle(self, a, src):
+        return self.init[2] if a == 0 else float(src[BOND_ANGLES[a % 3]][(a - 1) // 3])
+
+    def _dihedral(self, d, src):
+        return float(src[DIHEDRALS[d % 3]][(d + 1) // 3])
+
+    def geo(self, idx, l, orig=False):
+        """token_geo(idx, l, orig) (tokenizer.py:169-202)."""
+        if idx + l - 1 > 3 * self.n - 1:
+            raise ValueError(f"idx+l cannot exceed {3 * self.n - 1}")
+        src = self.orig if orig else self.cur
+        out = {}
+        for j in range(idx, idx + l):
+            out.setdefault(BOND_TYPES[j % 3], []).append(self._bond(j, src))
+        for j in range(idx, idx + l - 1):
+            out.setdefault(BOND_ANGLES[j % 3], []).append(self._angle(j, src))
+        for j in range(idx, idx + l - 2):
+            out.setdefault(DIHEDRALS[j % 3], []).append(self._dihedral(j, src))
+        return out
+
+    def set_geo(self, idx, l, vals):
+        """set_token_geo(idx, l, vals) (tokenizer.py:253-286): values consumed in order."""
+        it = {k: iter(v) for k, v in vals.items()}
+        for j in range(idx, idx + l):
+            v = next(it[BOND_TYPES[j % 3]])
+            if j < 2:
+                self.init[j] = v
+            else:
+                self.cur[BOND_TYPES[j % 3]][(j - 2) // 3] = v
+        for j in range(idx, idx + l - 1):
+            v = next(it[BOND_ANGLES[j % 3]])
+            if j == 0:
+                self.init[2] = v
+            else:
+                self.cur[BOND_ANGLES[j % 3]][(j - 1) // 3] = v
+        for j in range(idx, idx + l - 2):
+            self.cur[DIHEDRALS[j % 3]][(j + 1) // 3] = next(it[DIHEDRALS[j % 3]])
+        for k, rest in it.items():
+            if next(rest, None) is not None:
+                raise AssertionError(f"set_token_geo: values of {k} left over")
+
+    def tokens(self):
+        return list(self.btt.values())
+
+    def glue(self, b):
+        """The three glue values after a token ending before bond b (tokenizer.py:384-391)."""
+        return (self._dihedral(b - 2, self.cur), self._dihedral(b - 1, self.cur), self._angle(b - 1, self.cur))
+
+
+class RmsdTokenizer:
+    """Tokenizer view of one chain in the RMSD mode: ``bond_to_token`` with tuple ids
+    ``(n, p)``, ``token_pos``, ``tokens``, ``tokenize()`` (tokenizer.py:379-392)."""
+
+    def __init__(self, chain: _Chain):
+        self._c = chain
+        self.n = chain.n
+        self.fname = chain.fname
+
+    @property
+    def bond_to_token(self):
+        return dict(self._c.btt)
+
+    @property
+    def token_pos(self):
+        return list(self._c.token_pos)
+
+    @property
+    def tokens(self):
+        return self._c.tokens()
+
+    def token_geo(self, idx, l, orig=False):
+        return self._c.geo(idx, l, orig)
+
+    def tokenize(self):
+        out = []
+        last = 3 * self.n - 1
+        for start, tid, length in self._c.btt.values():
+            out.append(("MOTIF", tid))
+            b = start + length
+            if b < last:
+                om, ph, cn = self._c.glue(b)
+                out.append(("DIHEDRAL", DIHEDRALS[(b - 2) % 3], om))
+                out.append(("DIHEDRAL", DIHEDRALS[(b - 1) % 3], ph))
+                out.append(("BOND_ANGLE", BOND_ANGLES[(b - 1) % 3], cn))
+        return out
+
+
+class RmsdBPE:
+    """foldingdiff.bpe.BPE with a finite rmsd_partition_min_size (see the module docstring).
+    Constructed by ``geobpe.bpe.BPE(...)`` when the arguments ask for this mode."""
+
+    def __init__(self, structures, bins, bin_strategy="histogram", save_dir="./plots/bpe",
+                 compute_sec_structs=False, plot_iou_with_sec_structs=False, res_init=False, std_bonds=True,
+                 rmsd_partition_min_size=4, rmsd_super_res=False, rmsd_only=False, num_partitions=3,
+                 max_num_strucs=500, glue_opt=False, glue_opt_prior=0.0, glue_opt_every=10,
+                 glue_opt_method="all", seed=None, device: int = 0, group=None, **_unused):
+        from .bpe import ThresholdDict, structures_to_corpus
+        if group is not None:
+            raise NotImplementedError("the RMSD mode runs on one GPU (no row sharding)")
+        if not isinstance(bins, dict) or list(bins) != [1]:
+            raise NotImplementedError("the RMSD mode runs with one grid, bins={1: B}")
+        if not res_init:
+            raise NotImplementedError("the RMSD mode needs res_init=True (bond-level init is not built)")
+        if not std_bonds:
+            raise NotImplementedError("free bonds in the RMSD mode are not built")
+        if glue_opt:
+            raise NotImplementedError("glue optimisation (LBFGS over NeRF, bpe.py:423-578) is not built")
+        if rmsd_only or compute_sec_structs:
+            raise NotImplementedError("rmsd_only / secondary-structure priorities are not built")
+        if isinstance(structures, dict) and "row_off" in structures:
+            corpus = structures
+            fnames = list(structures["fnames"]) if structures.get("fnames") is not None else None
+        else:
+            structures = list(structures)
+            corpus = structures_to_corpus(structures)
+            fnames = [s.get("fname") if isinstance(s, dict) else None for s in structures]
+        self._corpus = corpus
+        self._fnames = fnames
+        self.bins = bins
+        self.B = int(bins[1])
+        self.bin_strategy = bin_strategy
+        self.save_dir = save_dir
+        self.compute_sec_structs = compute_sec_structs
+        self.plot_iou_with_sec_structs = plot_iou_with_sec_structs
+        self.res_init = res_init
+        self.std_bonds = std_bonds
+        self.rmsd_partition_min_size = rmsd_partition_min_size
+        self.rmsd_super_res = bool(rmsd_super_res)
+        self.rmsd_only = rmsd_only
+        self.num_partitions = ThresholdDict(num_partitions) if isinstance(num_partitions, dict) else num_partitions
+        self.max_num_strucs = max_num_strucs
+        self.glue_opt = glue_opt
+        self.glue_opt_prior = glue_opt_prior
+        self.glue_opt_every = glue_opt_every
+        self.glue_opt_method = glue_opt_method
+        self.seed = seed
+        self.rng = np.random.default_rng(seed)
+        self.device = int(device)
+        self.n = len(corpus["row_off"]) - 1
+        self._step = 0
+        self._times = []
+        self._ious = []
+        self._tokens = {}
+        self._chains = []
+        self._merge_log = []  # [key, count] of every merge popped, recurring repeats included
+        self.assign_calls = 0  # device assignment batches (tests check the GPU path ran)
+
+    # ------------------------------------------------------------ geometry on the device
+    def _span_coords(self, spans, orig):
+        """Tokenizer.compute_coords(index, length, orig) for [(chain, index, length)], one
+        device NeRF batch: the span rounded out to whole residues, then its atoms."""
+        geos, cuts = [], []
+        for ci, index, length in spans:
+            c = self._chains[ci]
+            length = min(length, 3 * c.n - 1 - index)
+            start = 3 * (index // 3)
+            end = 3 * (((index + length - 1) + 1) // 3) + 1
+            geos.append(c.geo(start, end - start + 1, orig))
+            cuts.append((index - start, end - (index + length - 1)))
+        if not geos:
+            return []
+        xyz = _rmsd.geo_coords(geos, device=self.device)
+        return [x[a:len(x) - b] for x, (a, b) in zip(xyz, cuts)]
+
+    def _struc_coords(self, strucs):
+        """Tokenizer.key_coords(struc) (tokenizer.py:204-230) for medoid geometries that
+        start at a residue's N:CA bond: NeRF of the struc, padded to whole residues (the
+        padding only places atoms after the kept ones), first num_bonds + 1 atoms."""
+        geos, keep = [], []
+        for s in strucs:
+            nb = sum(len(s.get(k, [])) for k in BOND_TYPES)
+            if len(s.get("N:CA", [])) < len(s.get("CA:C", [])) or len(s.get("N:CA", [])) == 0:
+                raise NotImplementedError("medoid geometry that does not start at an N:CA bond")
+            r = nb // 3 + 1  # whole residues that place atom nb
+            g = {k: list(s.get(k, [])) for k in BOND_TYPES + BOND_ANGLES + DIHEDRALS}
+            g["N:CA"] += [1.46] * (r - len(g["N:CA"]))
+            g["CA:C"] += [1.54] * (r - len(g["CA:C"]))
+            g["tau"] += [1.94] * (r - len(g["tau"]))
+            for k, v in (("0C:1N", 1.34), ("CA:C:1N", 2.03), ("C:1N:1CA", 2.12), ("psi", 0.0), ("omega", np.pi),
+                         ("phi", -1.0)):
+                g[k] += [v] * (r - 1 - len(g[k]))
+            geos.append(g)
+            keep.append(nb + 1)
+        xyz = _rmsd.geo_coords(geos, device=self.device)
+        return [x[:k] for x, k in zip(xyz, keep)]
+
+    def _assign(self, coords, medoid_coords):
+        """_compute_assignment_inner for every occurrence (bpe.py:654-657): argmin over the
+        medoids of compute_rmsd(occurrence, medoid) -- one device launch."""
+        self.assign_calls += 1
+        if not coords:
+            return []
+        return [int(a) for a in _rmsd.assign(coords, medoid_coords, device=self.device)]
+
+    # ------------------------------------------------------------ initialize (bpe.py:91-103)
+    def initialize(self, path=None):
+        from .bpe import BOND_LENGTHS, ThresholdDict
+        thr = ThresholdDict()
+        thr[1] = self._grid_thresholds()
+        for i, bt in enumerate(BOND_TYPES):
+            thr[bt] = [(BOND_LENGTHS[i], BOND_LENGTHS[i])]
+        self._thresholds = thr
+        ro = self._corpus["row_off"]
+        init = _rmsd.init_geometry()
+        self._chains = []
+        for r in range(self.n):
+            cols = {c: np.asarray(self._corpus[c][ro[r]:ro[r + 1]], dtype=np.float64) for c in COLUMNS}
+            self._chains.append(_Chain(cols, init, self._fnames[r] if self._fnames else None))
+        self._init_residues()
+        return self
+
+    def _grid_thresholds(self):
+        """Grid-1 thresholds of the six angle types (bpe.py:820-876): the device min / max /
+        count pass of the scoped mode's engine, then np.histogram edges on the host."""
+        from .engine import GeoBPEEngine
+        e = GeoBPEEngine(self._corpus, self.B, device=self.device, strategy=self.bin_strategy)
+        try:
+            e.initialize()
+            return {k: list(v) for k, v in e.thresholds.items()}
+        finally:
+            e.close()
+
+    def _centre(self, k, ind, size):
+        lookup = self._thresholds if k in BOND_TYPES else self._thresholds[size]
+        return sum(lookup[k][ind]) / 2
+
+    def _init_residues(self):
+        p = self.rmsd_partition_min_size
+        for c in self._chains:  # std bonds for every bond (bpe.py:714-737)
+            for j in range(3 * c.n - 1):
+                bt = BOND_TYPES[j % 3]
+                c.set_geo(j, 1, {bt: [sum(self._thresholds[bt][0]) / 2]})
+        label_dict, res_geo, labels = {}, {}, []
+        for ci, c in enumerate(self._chains):
+            lab = []
+            for i in range(c.n):
+                start, length = 3 * i, (3 if i < c.n - 1 else 2)
+                if length < p:  # binned residue (bpe.py:237-249)
+                    geo = c.geo(start, length)
+                    cen = {}
+                    for k, vals in geo.items():
+                        q = []
+                        for v in vals:
+                            if k in BOND_TYPES:
+                                q.append(_get_ind(v, self._thresholds[k]))
+                            else:
+                                q.append(_get_ind((v + TWO_PI) % TWO_PI, self._thresholds[length][k]))
+                        cen[k] = [self._centre(k, x, length) for x in q]
+                    s = json.dumps(cen, sort_keys=True)
+                    n = label_dict.setdefault(s, len(label_dict))
+                    c.set_geo(start, length, cen)
+                    lab.append(n)
+                else:
+                    res_geo.setdefault(length, []).append((ci, start, length))
+                    lab.append(None)
+            labels.append(lab)
+        for ci, c in enumerate(self._chains):
+            c.btt = {3 * i: (3 * i, labels[ci][i], 3 if i < c.n - 1 else 2) for i in range(c.n)}
+            c.token_pos = [3 * (j // 3) for j in range(3 * c.n - 1)]
+        if res_geo:
+            self._sphere_dict = {}
+            self._tokens = {}
+            for n, size in enumerate(res_geo):
+                self._partition_residues(n, size, res_geo[size])
+        for c in self._chains:  # glue angles -> grid-1 bin centres, NaN kept (bpe.py:381-391)
+            for k in GLUE:
+                col = c.cur[k]
+                for r in range(c.n):
+                    v = col[r]
+                    if v == v:
+                        col[r] = self._centre(k, _get_ind((v + TWO_PI) % TWO_PI, self._thresholds[1][k]), 1)
+        if not res_geo:
+            self._tokens = {n: json.loads(s) for s, n in label_dict.items()}
+
+    def _partition_residues(self, n, size, occ):
+        """The res_geo partition of one residue size (bpe.py:266-379)."""
+        if size not in RES_SPHERE_KEY:
+            raise NotImplementedError(f"residue size {size}")
+        N = len(occ)
+        active = (self.rng.choice(N, self.max_num_strucs, replace=False) if N > self.max_num_strucs
+                  else np.arange(N))
+        sup = self.rmsd_super_res
+        coords = self._span_coords(occ, sup)
+        act = [coords[i] for i in active]
+        medoids = _rmsd.k_medoids(act, self.num_partitions[size], rng=self.rng, device=self.device)
+        assign = self._assign(coords, [act[m] for m in medoids])
+        key = RES_SPHERE_KEY[size]
+        self._sphere_dict[key] = []
+        for p, m in enumerate(medoids):
+            ci, start, length = occ[int(active[m])]
+            struc = self._chains[ci].geo(start, length, sup)
+            self._sphere_dict[key].append(struc)
+            self._tokens[(n, p)] = struc
+        for (ci, start, length), p in zip(occ, assign):
+            c = self._chains[ci]
+            c.set_geo(start, length, self._tokens[(n, p)])
+            c.btt[start] = (start, (n, p), length)
+
+    # ------------------------------------------------------------ keys (bpe.py:1192-1299)
+    def _pair_key(self, ci, idx1, l1, l2):
+        c = self._chains[ci]
+        idx2 = idx1 + l1
+        t1, t2 = c.btt[c.token_pos[idx1]], c.btt[c.token_pos[idx2]]
+        if t1[0] == t2[0]:
+            raise RuntimeError("pair of one token")  # the reference stops in breakpoint() here
+        pt1, pt2 = isinstance(t1[1], tuple), isinstance(t2[1], tuple)
+        L = l1 + l2
+        geo = c.geo(idx1, L)
+        ph = idx1 % 3
+        for k, vals in geo.items():
+            if k in BOND_TYPES:
+                base, kind = (BOND_TYPES.index(k) + 3 - ph) % 3, 0
+            elif k in BOND_ANGLES:
+                base, kind = (BOND_ANGLES.index(k) + 3 - ph) % 3, 1
+            else:
+                base, kind = (DIHEDRALS.index(k) + 3 - ph) % 3, 2
+            out = []
+            for m, v in enumerate(vals):
+                i = base + 3 * m
+                if pt1 and pt2:
+                    q = kind == 1 and i == l1 - 1 or kind == 2 and (i == l1 - 2 or i == l1 - 1)
+                elif pt1:
+                    q = i >= (l1, l1 - 1, l1 - 2)[kind]
+                elif pt2:
+                    q = i < l1
+                else:
+                    q = True
+                if not q:
+                    out.append(v)
+                elif kind == 0:
+                    out.append(_get_ind(v, self._thresholds[k]))
+                else:
+                    out.append(_get_ind((v + TWO_PI) % TWO_PI, self._thresholds[L][k]))
+            geo[k] = out
+        return json.dumps(geo, sort_keys=True)
+
+    # ------------------------------------------------------------ bin (bpe.py:1431-1474)
+    def bin(self):
+        from sortedcontainers import SortedList
+        self._geo_dict = defaultdict(set)
+        for ci, c in enumerate(self._chains):
+            toks = c.tokens()
+            for (i1, _, l1), (i2, _, l2) in zip(toks, toks[1:]):
+                self._geo_dict[self._pair_key(ci, i1, l1, l2)].add((ci, i2))
+        self._priority = SortedList()
+        self._key_to_priority = {}
+        for key, occ in self._geo_dict.items():
+            pr = (True, -len(occ), key)
+            self._priority.add(pr)
+            self._key_to_priority[key] = pr
+        self._sphere_keys = {}
+
+    @property
+    def _priority_dict(self):
+        """The reference's SortedDict of priorities, as its sorted key view."""
+        return list(self._priority)
+
+    # ------------------------------------------------------------ step (bpe.py:1792-2166)
+    def step(self):
+        while True:
+            self._merge()
+            if not len(self._priority):
+                raise IndexError("peekitem on an empty priority dict (bpe.py:2164)")
+            if self._priority[0][0]:
+                return
+
+    def _partition(self, key, length):
+        """rmsd_partition (bpe.py:1739-1789): k-medoids over (a sample of) the occurrences,
+        every occurrence assigned to its nearest medoid, the medoids' geometry recorded."""
+        occ = list(self._geo_dict[key])
+        N = len(occ)
+        active = (self.rng.choice(N, self.max_num_strucs, replace=False) if N > self.max_num_strucs
+                  else np.arange(N))
+        spans = [(ci, self._chains[ci].token_pos[index - 1], length) for ci, index in occ]
+        sup = self.rmsd_super_res
+        coords = self._span_coords(spans, sup)
+        act = [coords[i] for i in active]
+        medoids = _rmsd.k_medoids(act, self.num_partitions[length], rng=self.rng, device=self.device)
+        assign = self._assign(coords, [act[m] for m in medoids])
+        strucs = []
+        for m in medoids:
+            ci, i1, _ = spans[int(active[m])]
+            strucs.append(self._chains[ci].geo(i1, length, sup))
+        self._sphere_dict[key] = strucs
+        return occ, assign
+
+    def _merge(self):
+        t0 = time.time()
+        if not len(self._priority):
+            raise IndexError("peekitem on an empty priority dict")
+        flag, negc, key = self._priority[0]
+        recurring = not flag
+        self._merge_log.append([key, -negc])
+        key_dict = json.loads(key)
+        length = sum(len(key_dict.get(k, [])) for k in BOND_TYPES)
+        rmsd = length >= self.rmsd_partition_min_size
+        if rmsd:
+            if not hasattr(self, "_sphere_dict"):
+                # p >= 4: the reference never creates _sphere_dict (bpe.py:264, 1780)
+                raise AttributeError("'BPE' object has no attribute '_sphere_dict'")
+            if recurring:
+                occ = list(self._geo_dict[key])
+                spans = [(ci, self._chains[ci].token_pos[index - 1], length) for ci, index in occ]
+                assign = self._assign(self._span_coords(spans, self.rmsd_super_res),
+                                      self._struc_coords(self._sphere_dict[key]))
+            else:
+                occ, assign = self._partition(key, length)
+        n = len(self._tokens)
+        if not rmsd:
+            binned = {k: [self._centre(k, v, length) if isinstance(v, int) else v for v in vals]
+                      for k, vals in key_dict.items()}
+            self._tokens[n] = key_dict
+        elif recurring:
+            n = sorted({k[0] for k in self._tokens})[list(self._sphere_dict).index(key)]
+        else:
+            for p, struc in enumerate(self._sphere_dict[key]):
+                self._tokens[(n, p)] = struc
+        if not rmsd:
+            occ = list(self._geo_dict[key])
+        diff = {}
+
+        def note(k, d):
+            diff[k] = diff.get(k, 0) + d
+
+        gd = self._geo_dict
+        last_ci = last_i1 = None
+        for idx in sorted(range(len(occ)), key=occ.__getitem__):
+            ci, i2 = occ[idx]
+            c = self._chains[ci]
+            tp = c.token_pos
+            i1 = tp[i2 - 1]
+            l1 = i2 - i1
+            l2 = length - l1
+            overlaps = last_ci == ci and last_i1 + length > i1
+            if overlaps != ((ci, i2) not in gd[key]):
+                raise RuntimeError("occurrence bookkeeping out of step (the reference stops in breakpoint())")
+            if overlaps:
+                continue
+            if not (l1 > 0 and l2 > 0):
+                raise AssertionError("bad split")
+            if self._pair_key(ci, i1, l1, l2) != key:
+                continue  # bpe.py:1918-1920 (breakpoint(); continue)
+            gd[key].remove((ci, i2))
+            note(key, -1)
+            left = right = None
+            if i1:
+                i0 = tp[i1 - 1]
+                l0 = i1 - i0
+                left = self._pair_key(ci, i0, l0, l1)
+            if i2 + l2 < len(tp):
+                i3 = i2 + l2
+                l3 = 0
+                while i3 + l3 < len(tp) and tp[i3 + l3] == i3:
+                    l3 += 1
+                right = self._pair_key(ci, i2, l2, l3)
+            if left:
+                gd[left].remove((ci, i1))
+                note(left, -1)
+            if right:
+                gd[right].remove((ci, i3))
+                note(right, -1)
+            for j in range(i2, i2 + l2):
+                tp[j] = i1
+            c.btt.pop(i2)
+            c.btt[i1] = (i1, (n, assign[idx]) if rmsd else n, length)
+            if rmsd:
+                c.set_geo(i1, length, self._sphere_dict[key][assign[idx]])
+            if left:
+                k = self._pair_key(ci, i0, l0, length)
+                gd[k].add((ci, i1))
+                note(k, +1)
+            if right:
+                k = self._pair_key(ci, i1, length, l3)
+                gd[k].add((ci, i3))
+                note(k, +1)
+            if not rmsd:
+                c.set_geo(i1, length, binned)
+            last_ci, last_i1 = ci, i1
+        if not recurring:
+            self._step += 1
+        for k, d in diff.items():  # step 7 (bpe.py:2077-2138)
+            pr = self._key_to_priority.pop(k, None)
+            count = 0
+            if pr is not None:
+                self._priority.remove(pr)
+                count = -pr[1]
+            count += d
+            if count != len(gd[k]):
+                raise AssertionError(f"count of {k[:60]} out of step")
+            if count:
+                pr = (k not in getattr(self, "_sphere_dict", {}), -count, k)
+                self._key_to_priority[k] = pr
+                self._priority.add(pr)
+            else:
+                gd.pop(k)
+        self._times.append(time.time() - t0)
+
+    def run(self, n_steps: int) -> int:
+        """n step() calls (bin/encode.py's loop, bpe.py:398); stops early when no pair is
+        left.  Returns the calls completed."""
+        done = 0
+        for _ in range(n_steps):
+            if not len(self._priority):
+                break
+            try:
+                self.step()
+            except IndexError:  # the last merge emptied the priority dict (bpe.py:2164)
+                done += 1
+                break
+            done += 1
+        return done
+
+    @property
+    def merges(self):
+        """[(key string, count)] of every merge, recurring repeats included."""
+        return [tuple(m) for m in self._merge_log]
+
+    # ------------------------------------------------------------ views / encode
+    @property
+    def tokenizers(self):
+        return [RmsdTokenizer(c) for c in self._chains]
+
+    @property
+    def vocab_size(self):
+        return len(self._tokens) + self.cum_bin_count()
+
+    def cum_bin_count(self, key=None):
+        from .bpe import BPE
+        return BPE.cum_bin_count(self, key)
+
+    def quantize(self, tokenized):
+        """bpe.py:928-956 (MOTIF ids by position in _tokens: a token id that is not in
+        _tokens -- p = 3 leaves the binned last residues out -- raises ValueError there too)."""
+        from .bpe import BPE
+        if isinstance(tokenized, RmsdTokenizer):
+            return BPE._quantize_tuples(self, tokenized.tokenize())
+        if len(tokenized) and isinstance(tokenized[0], RmsdTokenizer):
+            return [BPE._quantize_tuples(self, t.tokenize()) for t in tokenized]
+        return BPE._quantize_tuples(self, tokenized)
+
+    def dequantize(self, quantized):
+        from .bpe import BPE
+        return BPE.dequantize(self, quantized)
+
+    def recover(self, tokenized):
+        from .bpe import BPE
+        return BPE.recover(self, tokenized)
+
+    def encode_all(self):
+        """quantize(tokenize()) of every chain as (ids, row offsets)."""
+        q = [self.quantize(t) for t in self.tokenizers]
+        off = np.zeros(len(q) + 1, dtype=np.int64)
+        np.cumsum([len(x) for x in q], out=off[1:])
+        return np.array([i for x in q for i in x], dtype=np.int64), off
+
+    def capacity(self, tokenizer=False):
+        from .bpe import BPE
+        return BPE.capacity(self, tokenizer)
+
+    def save_checkpoint(self, path: str) -> None:
+        raise NotImplementedError("bpe_iter=*.pkl checkpoints of the RMSD mode (tuple token ids, "
+                                  "_sphere_dict) are not built; use --ckpt-format json")
+
+    def geometry(self):
+        """Every chain's current 9 columns, concatenated (the reference's DataFrames)."""
+        return {c: np.concatenate([ch.cur[c] for ch in self._chains]) for c in COLUMNS}
+
+    def visualize(self, key, output_path):
+        return None
+
+    def plot_times(self, output_path):
+        return None
+
+    def close(self):
+        return None

@@ -1,0 +1,164 @@
+"""Golden fixtures for the RMSD-partitioned mode, made by running the
+REFERENCE in this container (never on the GPU box; only the outputs travel).
+
+The reference's `BPE` is run with a finite `rmsd_partition_min_size` (p), `res_init=True`,
+`std_bonds=True`, `glue_opt=False` on small synthetic corpora.  Its RMSD paths need worker
+pools (the `max_workers == 0` branches call `_compute_assignment` with four arguments,
+`bpe.py:305,1767`, a TypeError), so this runs with SLURM_CPUS_PER_TASK=2.
+
+Per fixture `<name>`:
+  <name>.npz   the corpus, and the reference's per-chain geometry after initialize() and at
+               the end (9 columns, float64) plus each chain's init triple
+               (_init_n_ca, _init_ca_c, _init_bond_angle);
+  <name>.json  the settings, the (flag, -count, key) popped at every step() entry (the
+               reference's step() recurses for recurring keys, bpe.py:2164-2166), _step and
+               len(_tokens) after each top-level call, _tokens, _sphere_dict keys, the
+               segmentation [(start bond, id, #bonds)] per chain, quantize() of every chain
+               (or the exception it raises), and what initialize/bin/step raised, if anything.
+
+Usage: python tests/golden/make_rmsd_mode_golden.py [name ...]
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import traceback
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "pt-bpe_amd"))
+sys.path.insert(0, HERE)
+
+NUM_P = {2: 2, 3: 3, 5: 2, 8: 1}
+# name: (n_chains, len_lo, len_hi, seed, B, p_min_size, super_res, max_num_strucs, step calls)
+FIXTURES = {
+    "rm_p0": (10, 20, 40, 21, 5, 0, False, 60, 25),
+    "rm_p0_super": (10, 20, 40, 21, 5, 0, True, 60, 25),
+    "rm_p3_super": (8, 15, 35, 22, 4, 3, True, 50, 20),
+    "rm_p2_super_b3": (12, 10, 30, 23, 3, 2, True, 400, 30),
+    "rm_p4": (6, 20, 30, 24, 5, 4, False, 60, 3),
+    "rm_p0_b2_long": (16, 12, 30, 25, 2, 0, False, 80, 120),
+    "rm_p0_super_b2_long": (16, 12, 30, 25, 2, 0, True, 80, 120),
+    "rm_p0_b1_exhaust": (20, 10, 30, 26, 1, 0, False, 80, 250),
+    # one partition per size and one bin: every residue alike, so equal geometry is built by
+    # different merge orders and keys recur after their merge (bpe.py:1823-1847, 1862-1866)
+    "rm_p0_b1_one_partition": (30, 6, 40, 27, 1, 0, False, 80, 400, {2: 1, 3: 1}),
+}
+COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
+
+
+def _id(v):
+    return [int(x) for x in v] if isinstance(v, tuple) else int(v)
+
+
+def run_one(name):
+    import numpy as np
+    from geobpe import synth
+    from make_golden import _stub_optional_deps
+
+    nch, lo, hi, seed, B, p, sup, maxs, calls = FIXTURES[name][:9]
+    num_p = FIXTURES[name][9] if len(FIXTURES[name]) > 9 else NUM_P
+    corpus = synth.make_corpus(synth.make_lengths(nch, lo, hi, seed=seed), seed=seed)
+    _stub_optional_deps()
+    sys.path.insert(0, "/root/reference")
+    import foldingdiff.bpe as RB
+    from foldingdiff.tokenizer import Tokenizer
+
+    RB.BPE.visualize = lambda self, key, path: None
+    Tokenizer.visualize_bonds = lambda self, *a, **k: None
+    popped = []
+    inner_step = RB.BPE.step
+
+    def recording_step(self):
+        top = self._priority_dict.peekitem(0)[0]
+        popped.append([bool(top[0]), int(top[1]), top[2]])
+        return inner_step(self)
+
+    RB.BPE.step = recording_step
+    structs = []
+    for i, row in enumerate(synth.corpus_rows(corpus)):
+        s = Tokenizer.init_structure(len(row["phi"]))
+        for c in COLS:
+            s["angles"][c] = row[c].astype(np.float64)
+        s["fname"] = f"synthetic_{i}"
+        structs.append(s)
+
+    def geometry(bpe, tag, arrays):
+        for c in COLS:
+            arrays[f"{tag}_{c}"] = np.concatenate(
+                [np.array([float(x) for x in t.angles_and_dists[c]]) for t in bpe.tokenizers])
+        arrays[f"{tag}_init"] = np.array([[float(t._init_n_ca), float(t._init_ca_c), float(t._init_bond_angle)]
+                                          for t in bpe.tokenizers])
+
+    def segmentation(bpe):
+        return [[[int(s), _id(v[1]), int(v[2])] for s, v in t.bond_to_token.items()] for t in bpe.tokenizers]
+
+    meta = {"name": name, "n_chains": nch, "len_lo": lo, "len_hi": hi, "seed": seed, "bins": {"1": B},
+            "rmsd_partition_min_size": p, "rmsd_super_res": sup, "max_num_strucs": maxs,
+            "num_partitions": {str(k): v for k, v in num_p.items()}, "rng_seed": 0, "calls": [],
+            "raised": None, "generator": "tests/golden/make_rmsd_mode_golden.py (reference: /root/reference "
+                                         "foldingdiff/bpe.py, run in the build container)"}
+    arrays = dict(corpus)
+    bpe = RB.BPE(structs, bins={1: B}, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_golden_"),
+                 rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(num_p),
+                 max_num_strucs=maxs, res_init=True, std_bonds=True, seed=0)
+    try:
+        bpe.initialize()
+        geometry(bpe, "init", arrays)
+        meta["init_tokens"] = [[_id(k), v] for k, v in bpe._tokens.items()]
+        meta["init_segmentation"] = segmentation(bpe)
+        meta["init_sphere_keys"] = list(getattr(bpe, "_sphere_dict", {}) or {})
+        bpe.bin()
+        meta["bin_keys"] = len(bpe._priority_dict)
+        meta["bin_top"] = [[bool(a), int(b), c] for (a, b, c) in list(bpe._priority_dict.keys())[:20]]
+        for _ in range(calls):
+            if len(bpe._priority_dict) == 0:
+                break
+            n0 = len(popped)
+            bpe.step()
+            meta["calls"].append({"popped": popped[n0:], "step": bpe._step, "n_tokens": len(bpe._tokens)})
+    except BaseException as e:  # noqa: BLE001 - the fixture records what the reference raises
+        meta["raised"] = {"type": type(e).__name__, "msg": str(e)[:300], "popped_so_far": popped[-1:],
+                          "where": traceback.format_exc().splitlines()[-4:]}
+    if "init_tokens" in meta:
+        geometry(bpe, "final", arrays)
+        meta["tokens"] = [[_id(k), v] for k, v in bpe._tokens.items()]
+        meta["sphere_keys"] = list(getattr(bpe, "_sphere_dict", {}) or {})
+        meta["segmentation"] = segmentation(bpe)
+        meta["step"] = bpe._step
+        q = []
+        for t in bpe.tokenizers:
+            try:
+                q.append([int(x) for x in bpe.quantize(t)])
+            except Exception as e:  # noqa: BLE001
+                q.append({"raised": type(e).__name__})
+        meta["quantize"] = q
+        meta["vocab_size"] = bpe.vocab_size
+        if getattr(bpe, "_priority_dict", None):
+            meta["final_top"] = [[bool(a), int(b), c] for (a, b, c) in list(bpe._priority_dict.keys())[:20]]
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+    with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+        json.dump(meta, f)
+    merges = sum(len(c["popped"]) for c in meta["calls"])
+    print(f"{name}: calls={len(meta['calls'])} merges={merges} step={meta.get('step')} "
+          f"raised={meta['raised'] and meta['raised']['type']}", flush=True)
+
+
+def main(argv):
+    if len(argv) >= 2 and argv[0] == "--one":
+        run_one(argv[1])
+        return
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg", SLURM_CPUS_PER_TASK="2",
+               PYTHONBREAKPOINT="0")
+    for name in argv or list(FIXTURES):
+        r = subprocess.run([sys.executable, "-W", "ignore", __file__, "--one", name], env=env,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        out = [ln for ln in r.stdout.splitlines() if ln.startswith(name + ":")]
+        print(out[-1] if out and r.returncode == 0 else f"{name}: rc={r.returncode} {r.stderr[-800:]}", flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

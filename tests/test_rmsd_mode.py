@@ -1,0 +1,143 @@
+"""RMSD-partitioned mode against the reference's own outputs.
+
+Fixtures: tests/golden/rm_*.json|npz, made by tests/golden/make_rmsd_mode_golden.py running
+foldingdiff.bpe.BPE with a finite rmsd_partition_min_size (p = 0, 2, 3 with and without
+rmsd_super_res, and p = 4, which the reference cannot step).  Compared exactly: the
+residue partition (token ids, medoid geometries, every chain's geometry after
+initialize()), the bin() priorities, every merge popped (including the recurring-key
+repeats inside one step() call), _tokens, _sphere_dict keys, segmentation, every chain's final
+geometry, quantize() (or the exception the reference raised) and vocab_size.
+
+The GPU tests run the product path (device NeRF / RMSD batches, device thresholds).  The
+CPU test runs the same host bookkeeping with the oracle's numpy NeRF / Kabsch standing in
+for the device batches (oracle/rmsd.py, oracle/prologue.py: test infrastructure).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
+NAMES = sorted(f[:-5] for f in os.listdir(GOLDEN) if f.startswith("rm_") and f.endswith(".json"))
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        meta = json.load(f)
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        arrs = {k: z[k] for k in z.files}
+    corpus = {k: arrs[k] for k in COLS + ["row_off"]}
+    return meta, corpus, arrs
+
+
+def _tid(v):
+    return tuple(v) if isinstance(v, list) else v
+
+
+def _geometry_equal(bpe, arrs, tag):
+    g = bpe.geometry()
+    for c in COLS:
+        a, b = g[c], arrs[f"{tag}_{c}"]
+        assert a.shape == b.shape and np.array_equal(a, b, equal_nan=True), f"{tag} geometry {c}"
+    init = np.array([ch.init for ch in bpe._chains])
+    assert np.array_equal(init, arrs[f"{tag}_init"]), f"{tag} init triples"
+
+
+def _segmentation(bpe):
+    return [[[s, list(v[1]) if isinstance(v[1], tuple) else v[1], v[2]] for s, v in t.bond_to_token.items()]
+            for t in bpe.tokenizers]
+
+
+def run_and_compare(name, device=True):
+    from geobpe.bpe import BPE
+    from geobpe.rmsd_bpe import RmsdBPE
+
+    meta, corpus, arrs = _load(name)
+    bpe = BPE(corpus, bins={1: meta["bins"]["1"]}, rmsd_partition_min_size=meta["rmsd_partition_min_size"],
+              rmsd_super_res=meta["rmsd_super_res"], num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=True, seed=meta["rng_seed"])
+    assert isinstance(bpe, RmsdBPE)
+    popped = []
+    inner = bpe._merge
+
+    def recording():
+        popped.append(list(bpe._priority[0]))
+        return inner()
+
+    bpe._merge = recording
+    bpe.initialize()
+    assert [[list(k) if isinstance(k, tuple) else k, v] for k, v in bpe._tokens.items()] == meta["init_tokens"]
+    assert list(getattr(bpe, "_sphere_dict", {})) == meta["init_sphere_keys"]
+    assert _segmentation(bpe) == meta["init_segmentation"]
+    _geometry_equal(bpe, arrs, "init")
+    bpe.bin()
+    assert len(bpe._priority) == meta["bin_keys"]
+    assert [list(p) for p in bpe._priority[:20]] == meta["bin_top"]
+    raised = None
+    for call in meta["calls"]:
+        n0 = len(popped)
+        bpe.step()
+        assert popped[n0:] == call["popped"], f"merge {len(popped)}"
+        assert (bpe._step, len(bpe._tokens)) == (call["step"], call["n_tokens"])
+    if meta["raised"]:
+        with pytest.raises(Exception) as ei:
+            bpe.step()
+        raised = type(ei.value).__name__
+        assert raised == meta["raised"]["type"]
+        assert popped[-1:] == meta["raised"]["popped_so_far"]
+    assert [[list(k) if isinstance(k, tuple) else k, v] for k, v in bpe._tokens.items()] == meta["tokens"]
+    assert list(getattr(bpe, "_sphere_dict", {})) == meta["sphere_keys"]
+    assert _segmentation(bpe) == meta["segmentation"]
+    _geometry_equal(bpe, arrs, "final")
+    q = []
+    for t in bpe.tokenizers:
+        try:
+            q.append(bpe.quantize(t))
+        except ValueError as e:
+            q.append({"raised": type(e).__name__})
+    assert q == meta["quantize"]
+    assert bpe.vocab_size == meta["vocab_size"]
+    if "final_top" in meta:
+        assert [list(p) for p in bpe._priority[:20]] == meta["final_top"]
+    return bpe
+
+
+@pytest.fixture
+def host_geometry(monkeypatch):
+    """The oracle's numpy NeRF / Kabsch / thresholds in place of the device batches."""
+    import oracle.prologue as prologue
+    import oracle.rmsd as orm
+    from geobpe import rmsd, rmsd_bpe
+
+    monkeypatch.setattr(rmsd, "geo_coords", lambda geos, device=0: [orm.nerf(g) for g in geos])
+    monkeypatch.setattr(rmsd, "rmsd_matrix", lambda S, device=0: orm.rmsd_matrix(S))
+    monkeypatch.setattr(rmsd, "rmsd_cross", lambda A, B, device=0: np.array([[orm.rmsd(a, b) for b in B] for a in A]))
+    monkeypatch.setattr(rmsd_bpe.RmsdBPE, "_grid_thresholds",
+                        lambda self: prologue.thresholds(self._corpus, self.B))
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_rmsd_mode_host_logic_matches_reference(name, host_geometry):
+    run_and_compare(name)
+
+
+def test_rmsd_mode_dispatch_and_scope():
+    from geobpe.bpe import BPE
+    from geobpe.rmsd_bpe import RmsdBPE
+    _, corpus, _ = _load(NAMES[0])
+    assert isinstance(BPE(corpus, bins={1: 5}, res_init=True), RmsdBPE)  # the reference's default p = 4
+    with pytest.raises(NotImplementedError):
+        BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=3, glue_opt=True)
+    assert not isinstance(BPE.__new__(BPE, corpus, bins={1: 5}, res_init=True,
+                                      rmsd_partition_min_size=float("inf")), RmsdBPE)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_rmsd_mode_device_matches_reference(name):
+    bpe = run_and_compare(name)
+    if name != "rm_p4":
+        assert bpe.assign_calls > 0  # the device RMSD batches ran
