@@ -1,0 +1,115 @@
+"""Time the RMSD-partitioned mode: this build vs the reference.
+
+  python tools/rmsd_mode_timing.py geobpe    [N LO HI STEPS P SUPER]   (GPU box: RmsdBPE, device batches)
+  python tools/rmsd_mode_timing.py reference [N LO HI STEPS P SUPER]   (build container only: foldingdiff)
+
+Both run the same synthetic corpus (geobpe.synth, seed 31), bins={1: 5},
+num_partitions={2: 2, 3: 5, 5: 2, 8: 1}, max_num_strucs=500, res_init, std_bonds, seed 0,
+and print one JSON line: initialize / bin seconds, seconds per step() call, merges, and
+(geobpe) the share of step time spent in the device batches.  The reference uses worker
+pools (SLURM_CPUS_PER_TASK = 8, this container's CPUs); its step() also renders no plots
+(visualize patched out, as in the fixtures).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "pt-bpe_amd"))
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+NUM_P = {2: 2, 3: 5, 5: 2, 8: 1}
+
+
+def corpus_of(n, lo, hi):
+    from geobpe import synth
+    return synth.make_corpus(synth.make_lengths(n, lo, hi, seed=31), seed=31)
+
+
+def run_geobpe(n, lo, hi, steps, p, sup):
+    import torch  # noqa: F401  (HIP runtime shared with torch)
+    from geobpe import rmsd
+    from geobpe.bpe import BPE
+    corpus = corpus_of(n, lo, hi)
+    dev_t = [0.0]
+    for name in ("geo_coords", "rmsd_matrix", "rmsd_cross"):
+        f = getattr(rmsd, name)
+
+        def timed(*a, _f=f, **k):
+            t0 = time.perf_counter()
+            r = _f(*a, **k)
+            dev_t[0] += time.perf_counter() - t0
+            return r
+        setattr(rmsd, name, timed)
+    bpe = BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=p, rmsd_super_res=sup,
+              num_partitions=dict(NUM_P), max_num_strucs=500, seed=0)
+    t0 = time.perf_counter()
+    bpe.initialize()
+    t1 = time.perf_counter()
+    bpe.bin()
+    t2 = time.perf_counter()
+    d0 = dev_t[0]
+    done = bpe.run(steps)
+    t3 = time.perf_counter()
+    return {"impl": "geobpe (RmsdBPE, device NeRF/RMSD batches)", "chains": n, "residues": int(corpus["row_off"][-1]),
+            "p_min_size": p, "super_res": sup, "initialize_s": t1 - t0, "bin_s": t2 - t1, "steps": done,
+            "merges": len(bpe.merges), "s_per_step": (t3 - t2) / max(done, 1),
+            "device_share_of_steps": (dev_t[0] - d0) / max(t3 - t2, 1e-9)}
+
+
+def run_reference(n, lo, hi, steps, p, sup):
+    import numpy as np
+    from make_golden import _stub_optional_deps
+    corpus = corpus_of(n, lo, hi)
+    _stub_optional_deps()
+    sys.path.insert(0, "/root/reference")
+    import foldingdiff.bpe as RB
+    from foldingdiff.tokenizer import Tokenizer
+    from geobpe import synth
+    RB.BPE.visualize = lambda self, key, path: None
+    Tokenizer.visualize_bonds = lambda self, *a, **k: None
+    structs = []
+    for i, row in enumerate(synth.corpus_rows(corpus)):
+        s = Tokenizer.init_structure(len(row["phi"]))
+        for c in synth.COLUMNS:
+            s["angles"][c] = row[c].astype(np.float64)
+        s["fname"] = f"synthetic_{i}"
+        structs.append(s)
+    bpe = RB.BPE(structs, bins={1: 5}, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_time_"), res_init=True,
+                 rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(NUM_P), max_num_strucs=500,
+                 std_bonds=True, seed=0)
+    t0 = time.perf_counter()
+    bpe.initialize()
+    t1 = time.perf_counter()
+    bpe.bin()
+    t2 = time.perf_counter()
+    for _ in range(steps):
+        bpe.step()
+    t3 = time.perf_counter()
+    return {"impl": "reference foldingdiff.bpe.BPE (8 worker processes, this container)", "chains": n,
+            "residues": int(corpus["row_off"][-1]), "p_min_size": p, "super_res": sup, "initialize_s": t1 - t0,
+            "bin_s": t2 - t1, "steps": steps, "s_per_step": (t3 - t2) / max(steps, 1)}
+
+
+def main():
+    which = sys.argv[1]
+    n, lo, hi, steps, p = (int(x) for x in (sys.argv[2:7] if len(sys.argv) >= 7 else (200, 40, 120, 20, 0)))
+    sup = (sys.argv[7] if len(sys.argv) > 7 else "1") == "1"
+    if which == "reference" and os.environ.get("SLURM_CPUS_PER_TASK") is None:
+        env = dict(os.environ, SLURM_CPUS_PER_TASK="8", PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg",
+                   PYTHONBREAKPOINT="0")
+        r = subprocess.run([sys.executable, "-W", "ignore", __file__] + sys.argv[1:], env=env,
+                           stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True)
+        print([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        return
+    out = (run_reference if which == "reference" else run_geobpe)(n, lo, hi, steps, p, sup)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
