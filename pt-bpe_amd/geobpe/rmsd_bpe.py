@@ -34,6 +34,7 @@ optimisation (LBFGS, ``glue_opt=True``), ``rmsd_only``, free bonds in this mode.
 """
 from __future__ import annotations
 
+import bisect
 import json
 import time
 from collections import defaultdict
@@ -54,9 +55,23 @@ RES_SPHERE_KEY = {3: '{"N:CA": [0], "CA:C": [0], "0C:1N": [0], "tau": [0], "CA:C
                   2: '{"CA:C": [0], "0C:1N": [0], "CA:C:1N": [0]}'}
 
 
+_LEFT = {}
+
+
 def _get_ind(v, values):
-    from .bpe import get_ind
-    return get_ind(v, values)
+    """BPE.get_ind (bpe.py:1164-1189), with the left edges of each threshold list cached."""
+    left = _LEFT.get(id(values))
+    if left is None or left[0] is not values:
+        left = _LEFT[id(values)] = (values, [a for a, _ in values])
+    ind = bisect.bisect_right(left[1], v) - 1
+    if ind < 0:
+        raise ValueError(f"value {v} is below the first bin range")
+    a, b = values[ind]
+    if ind == len(values) - 1 and v == b:
+        return ind
+    if a <= v < b:
+        return ind
+    raise ValueError(f"value {v} does not fall into any bin")
 
 
 class _Chain:
@@ -70,8 +85,10 @@ class _Chain:
     __slots__ = ("cur", "orig", "init", "n", "token_pos", "btt", "fname")
 
     def __init__(self, cols: dict, init, fname=None):
-        self.cur = {c: np.array(cols[c], dtype=np.float64) for c in COLUMNS}
-        self.orig = {c: np.array(cols[c], dtype=np.float64) for c in COLUMNS}
+        # Python lists: the host bookkeeping reads and writes single values (the
+        # reference's object DataFrame cells); numpy scalar indexing is ~5x slower here
+        self.cur = {c: [float(v) for v in cols[c]] for c in COLUMNS}
+        self.orig = {c: [float(v) for v in cols[c]] for c in COLUMNS}
         self.init = list(init)
         self.n = len(self.cur["phi"])
         self.token_pos = []
@@ -79,26 +96,32 @@ class _Chain:
         self.fname = fname
 
     def _bond(self, j, src):
-        return self.init[j] if j < 2 else float(src[BOND_TYPES[j % 3]][(j - 2) // 3])
+        return self.init[j] if j < 2 else src[BOND_TYPES[j % 3]][(j - 2) // 3]
 
     def _angle(self, a, src):
-        return self.init[2] if a == 0 else float(src[BOND_ANGLES[a % 3]][(a - 1) // 3])
+        return self.init[2] if a == 0 else src[BOND_ANGLES[a % 3]][(a - 1) // 3]
 
     def _dihedral(self, d, src):
-        return float(src[DIHEDRALS[d % 3]][(d + 1) // 3])
+        return src[DIHEDRALS[d % 3]][(d + 1) // 3]
 
     def geo(self, idx, l, orig=False):
-        """token_geo(idx, l, orig) (tokenizer.py:169-202)."""
+        """token_geo(idx, l, orig) (tokenizer.py:169-202).  Same-type items of a span sit
+        in consecutive rows of their column, so each type is one slice (bonds 0, 1 and
+        angle 0 are the chain's init values, in front of their column's rows)."""
         if idx + l - 1 > 3 * self.n - 1:
             raise ValueError(f"idx+l cannot exceed {3 * self.n - 1}")
         src = self.orig if orig else self.cur
+        init = self.init
         out = {}
-        for j in range(idx, idx + l):
-            out.setdefault(BOND_TYPES[j % 3], []).append(self._bond(j, src))
-        for j in range(idx, idx + l - 1):
-            out.setdefault(BOND_ANGLES[j % 3], []).append(self._angle(j, src))
-        for j in range(idx, idx + l - 2):
-            out.setdefault(DIHEDRALS[j % 3], []).append(self._dihedral(j, src))
+        for j in range(idx, idx + min(l, 3)):  # bonds: row (j - 2) // 3; j < 2 -> init
+            k, cnt = BOND_TYPES[j % 3], len(range(j, idx + l, 3))
+            out[k] = [init[j]] + src[k][:cnt - 1] if j < 2 else src[k][(j - 2) // 3:(j - 2) // 3 + cnt]
+        for a in range(idx, idx + min(l - 1, 3)):  # angles: row (a - 1) // 3; a = 0 -> init
+            k, cnt = BOND_ANGLES[a % 3], len(range(a, idx + l - 1, 3))
+            out[k] = [init[2]] + src[k][:cnt - 1] if a == 0 else src[k][(a - 1) // 3:(a - 1) // 3 + cnt]
+        for d in range(idx, idx + min(l - 2, 3)):  # dihedrals: row (d + 1) // 3
+            k, cnt = DIHEDRALS[d % 3], len(range(d, idx + l - 2, 3))
+            out[k] = src[k][(d + 1) // 3:(d + 1) // 3 + cnt]
         return out
 
     def set_geo(self, idx, l, vals):
@@ -283,6 +306,7 @@ class RmsdBPE:
         for i, bt in enumerate(BOND_TYPES):
             thr[bt] = [(BOND_LENGTHS[i], BOND_LENGTHS[i])]
         self._thresholds = thr
+        self._thr_by_len = {}
         ro = self._corpus["row_off"]
         init = _rmsd.init_geometry()
         self._chains = []
@@ -390,30 +414,36 @@ class RmsdBPE:
         L = l1 + l2
         geo = c.geo(idx1, L)
         ph = idx1 % 3
+        thr_all = self._thresholds
+        thr_L = self._thr_by_len.get(L)
+        if thr_L is None:
+            thr_L = self._thr_by_len[L] = thr_all[L]
+        # which span items are quantized (bpe.py:1247-1285), as a range [lo, hi) of the
+        # item's index i within the span, per kind (bond, angle, dihedral)
+        if pt1 and pt2:
+            rng = ((0, 0), (l1 - 1, l1), (l1 - 2, l1))
+        elif pt1:
+            rng = ((l1, L), (l1 - 1, L), (l1 - 2, L))
+        elif pt2:
+            rng = ((0, l1), (0, l1), (0, l1))
+        else:
+            rng = ((0, L), (0, L), (0, L))
         for k, vals in geo.items():
             if k in BOND_TYPES:
-                base, kind = (BOND_TYPES.index(k) + 3 - ph) % 3, 0
+                base, kind, thr = (BOND_TYPES.index(k) + 3 - ph) % 3, 0, thr_all[k]
             elif k in BOND_ANGLES:
-                base, kind = (BOND_ANGLES.index(k) + 3 - ph) % 3, 1
+                base, kind, thr = (BOND_ANGLES.index(k) + 3 - ph) % 3, 1, thr_L[k]
             else:
-                base, kind = (DIHEDRALS.index(k) + 3 - ph) % 3, 2
-            out = []
-            for m, v in enumerate(vals):
-                i = base + 3 * m
-                if pt1 and pt2:
-                    q = kind == 1 and i == l1 - 1 or kind == 2 and (i == l1 - 2 or i == l1 - 1)
-                elif pt1:
-                    q = i >= (l1, l1 - 1, l1 - 2)[kind]
-                elif pt2:
-                    q = i < l1
-                else:
-                    q = True
-                if not q:
-                    out.append(v)
-                elif kind == 0:
-                    out.append(_get_ind(v, self._thresholds[k]))
-                else:
-                    out.append(_get_ind((v + TWO_PI) % TWO_PI, self._thresholds[L][k]))
+                base, kind, thr = (DIHEDRALS.index(k) + 3 - ph) % 3, 2, thr_L[k]
+            lo, hi = rng[kind]
+            m_lo = max(0, -((base - lo) // 3))      # first m with base + 3m >= lo
+            m_hi = min(len(vals), -((base - hi) // 3))
+            if m_lo >= m_hi:
+                continue
+            out = list(vals)
+            for m in range(m_lo, m_hi):
+                v = vals[m]
+                out[m] = _get_ind(v, thr) if kind == 0 else _get_ind((v + TWO_PI) % TWO_PI, thr)
             geo[k] = out
         return json.dumps(geo, sort_keys=True)
 
@@ -646,7 +676,7 @@ class RmsdBPE:
 
     def geometry(self):
         """Every chain's current 9 columns, concatenated (the reference's DataFrames)."""
-        return {c: np.concatenate([ch.cur[c] for ch in self._chains]) for c in COLUMNS}
+        return {c: np.concatenate([np.asarray(ch.cur[c], dtype=np.float64) for ch in self._chains]) for c in COLUMNS}
 
     def visualize(self, key, output_path):
         return None
