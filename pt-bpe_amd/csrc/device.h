@@ -38,6 +38,9 @@ constexpr int NBA_MAX = 256;
 #ifndef GB_FKC
 #define GB_FKC 2048
 #endif
+#ifndef COMMIT_SPEC
+#define COMMIT_SPEC 0  // k_commit: 1 = load every finder slot's first records before the scans
+#endif
 #ifndef GB_CKC
 #define GB_CKC 2048
 #endif

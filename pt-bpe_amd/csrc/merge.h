@@ -770,8 +770,12 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const bool lane_ok = k0 < PER;
   const int64_t seg = (int64_t)j * nba + w;
   const int32_t cK = D.cntK[seg], cD = D.cntD[seg];
+#if COMMIT_SPEC
+  // speculative: the first PER records of every finder's slot in the first round
+  // (~15 MB per launch, mostly empty slots; it held the prefix scans below ~4 us)
   const KRec r0 = D.KS[seg * SK + min(k0, SK - 1)];
   const int2 d0 = D.DS[seg * SD + min(k0, SD - 1)];
+#endif
   const Sel sel = D.sel[par];
   const int32_t th = st->theta;
   const int32_t pn = D.pnch[j], pf = D.pfill[j];
@@ -811,6 +815,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       if (t == 0) D.voff[nid + 1] = pos + ln;
     }
   }
+  dbg_stamp(D, 50);
   for (int i = t; i < CKC; i += ABLOCK) {
     S.ckey[i] = 0;
     S.cn[i] = 0;
@@ -821,6 +826,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   }
   hot_init(hot);
   if (t == 0) tb.n = 0;
+  dbg_stamp(D, 51);
   {  // records past the first PER of a finder's slot: prefix sums
     const int32_t eK = t < nba ? max(0, min(cK, SK) - PER) : 0;
     const int32_t eD = t < nba ? max(0, min(cD, SD) - PER) : 0;
@@ -844,6 +850,13 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   }
   __syncthreads();
   dbg_stamp(D, 1);
+#if !COMMIT_SPEC
+  // the first PER records of each finder's slot, only where they exist
+  KRec r0;
+  int2 d0 = make_int2(0, 0);
+  if (lane_ok && k0 < min(cK, SK)) r0 = D.KS[seg * SK + k0];
+  if (lane_ok && k0 < min(cD, SD)) d0 = D.DS[seg * SD + k0];
+#endif
   // ---- round 1: key records -> LDS dedupe (occurrence totals per key); decrements -> LDS
 #define COMMIT_INSERT(k)                                          \
   do {                                                            \
@@ -876,6 +889,11 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   }
   __syncthreads();
   dbg_stamp(D, 2);
+  if (D.dbg) {  // (debug timeline: this owner's work, block-uniform)
+    const int32_t nr = __syncthreads_count(mine0), nd = __syncthreads_count(lane_ok && k0 < min(cD, SD));
+    dbg_val(D, 7, nr + nE + nKO);
+    dbg_val(D, 8, nd + nF);
+  }
   // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
   int32_t nlog = 0, nkeys = 0;
   const bool alone = S.fbn == 0;  // no key of this owner was resolved outside the table
@@ -907,6 +925,11 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       nlog += n;
       nkeys++;
     }
+  }
+  if (D.dbg) {
+    int32_t tk;
+    block_excl_scan(nkeys, &tk, S.red);
+    dbg_val(D, 9, tk);
   }
   if (D.stats) {  // (profiling: the work of this launch, for the bench's algorithmic bytes)
     int32_t tk, tr, td;
