@@ -173,13 +173,10 @@ class GeoBPEEngine:
             n_rows_total = self.n_rows
             if self.distributed:
                 mm, cnt, n_rows_total = self.group.reduce_ranges(mm, cnt, self.n_rows)
-            w0 = (init_bond_angle() + TWO_PI) % TWO_PI
+            self._range_stats = (mm.copy(), cnt.copy(), n_rows_total)
             self.thresholds = {}
             for t, key in enumerate(ANGLE_TYPES):
-                mn, mx, c = float(mm[2 * t]), float(mm[2 * t + 1]), int(cnt[t])
-                if key == "tau" and n_rows_total > 0:  # bpe.py:845-846: + _bond_angle(0) per tokenizer
-                    mn, mx, c = (min(mn, w0), max(mx, w0), c + n_rows_total) if c > 0 else (w0, w0, n_rows_total)
-                e = histogram_edges(mn, mx, c, self.B, self.cover)
+                e = self._hist_edges(t, key, self.B)
                 edges[t] = e
                 self.thresholds[key] = [(float(s), float(f)) for s, f in zip(e[:-1], e[1:])]
         self._edges = edges
@@ -207,6 +204,28 @@ class GeoBPEEngine:
         self._chk(self.L.geobpe_init_tokens(self._ctx, _p(label_of_sym), self.K0))
         self._initialized = True
         return self
+
+    def _hist_edges(self, t: int, key: str, B: int) -> np.ndarray:
+        """np.histogram edges of angle type t with B bins from the device min / max /
+        count (bpe.py:836-866; tau also holds every chain's init angle, :845-846)."""
+        mm, cnt, n_rows_total = self._range_stats
+        w0 = (init_bond_angle() + TWO_PI) % TWO_PI
+        mn, mx, c = float(mm[2 * t]), float(mm[2 * t + 1]), int(cnt[t])
+        if key == "tau" and n_rows_total > 0:
+            mn, mx, c = (min(mn, w0), max(mx, w0), c + n_rows_total) if c > 0 else (w0, w0, n_rows_total)
+        return histogram_edges(mn, mx, c, B, self.cover)
+
+    def thresholds_for(self, B: int) -> dict:
+        """Thresholds of another grid size's bin count over the same values (a multi-grid
+        ``bins`` schedule: bpe.py:836-869 runs the same histogram per size)."""
+        out = {}
+        for t, key in enumerate(ANGLE_TYPES):
+            if self.strategy == "uniform":
+                e = equal_count_edges(self._cols[COLUMNS.index(key)], self.n_rows, key, int(B))
+            else:
+                e = self._hist_edges(t, key, int(B))
+            out[key] = [(float(s), float(f)) for s, f in zip(e[:-1], e[1:])]
+        return out
 
     def replay_load(self, rec: dict):
         """Merge replay: merge t becomes the trained token K0 + t (geobpe.induce

@@ -203,8 +203,8 @@ class RmsdBPE:
         from .bpe import ThresholdDict, structures_to_corpus
         if group is not None:
             raise NotImplementedError("the RMSD mode runs on one GPU (no row sharding)")
-        if not isinstance(bins, dict) or list(bins) != [1]:
-            raise NotImplementedError("the RMSD mode runs with one grid, bins={1: B}")
+        if not isinstance(bins, dict) or 1 not in bins:
+            raise KeyError("bins must be a dict with key 1 (quantize/capacity need bins[1], bpe.py:896,909,952)")
         if not res_init:
             raise NotImplementedError("the RMSD mode needs res_init=True (bond-level init is not built)")
         if not std_bonds:
@@ -302,7 +302,8 @@ class RmsdBPE:
     def initialize(self, path=None):
         from .bpe import BOND_LENGTHS, ThresholdDict
         thr = ThresholdDict()
-        thr[1] = self._grid_thresholds()
+        for size, grid in self._grid_thresholds().items():
+            thr[size] = grid
         for i, bt in enumerate(BOND_TYPES):
             thr[bt] = [(BOND_LENGTHS[i], BOND_LENGTHS[i])]
         self._thresholds = thr
@@ -317,13 +318,15 @@ class RmsdBPE:
         return self
 
     def _grid_thresholds(self):
-        """Grid-1 thresholds of the six angle types (bpe.py:820-876): the device min / max /
-        count pass of the scoped mode's engine, then np.histogram edges on the host."""
+        """{size: thresholds} of the six angle types for every grid of ``bins``
+        (bpe.py:820-876): the device min / max / count pass of the scoped mode's engine,
+        then np.histogram edges with each size's bin count on the host."""
         from .engine import GeoBPEEngine
         e = GeoBPEEngine(self._corpus, self.B, device=self.device, strategy=self.bin_strategy)
         try:
             e.initialize()
-            return {k: list(v) for k, v in e.thresholds.items()}
+            return {s: ({k: list(v) for k, v in e.thresholds.items()} if s == 1 else e.thresholds_for(b))
+                    for s, b in self.bins.items()}
         finally:
             e.close()
 

@@ -46,6 +46,11 @@ FIXTURES = {
     # one partition per size and one bin: every residue alike, so equal geometry is built by
     # different merge orders and keys recur after their merge (bpe.py:1823-1847, 1862-1866)
     "rm_p0_b1_one_partition": (30, 6, 40, 27, 1, 0, False, 80, 400, {2: 1, 3: 1}),
+    # multi-grid schedules (bins {size: B}): junctions of a key of L bonds are binned at
+    # grid(L); the RMSD mode sets the medoid geometry before the neighbour keys, so the
+    # keys stay consistent (unlike the scoped mode)
+    "rm_p0_multigrid": (12, 20, 40, 28, {1: 5, 6: 3, 9: 4, 15: 2}, 0, False, 60, 60),
+    "rm_p3_super_multigrid": (10, 15, 40, 29, {1: 4, 2: 6, 7: 6}, 3, True, 60, 40),
 }
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
@@ -96,13 +101,15 @@ def run_one(name):
     def segmentation(bpe):
         return [[[int(s), _id(v[1]), int(v[2])] for s, v in t.bond_to_token.items()] for t in bpe.tokenizers]
 
-    meta = {"name": name, "n_chains": nch, "len_lo": lo, "len_hi": hi, "seed": seed, "bins": {"1": B},
+    bins = dict(B) if isinstance(B, dict) else {1: B}
+    meta = {"name": name, "n_chains": nch, "len_lo": lo, "len_hi": hi, "seed": seed,
+            "bins": {str(k): v for k, v in bins.items()},
             "rmsd_partition_min_size": p, "rmsd_super_res": sup, "max_num_strucs": maxs,
             "num_partitions": {str(k): v for k, v in num_p.items()}, "rng_seed": 0, "calls": [],
             "raised": None, "generator": "tests/golden/make_rmsd_mode_golden.py (reference: /root/reference "
                                          "foldingdiff/bpe.py, run in the build container)"}
     arrays = dict(corpus)
-    bpe = RB.BPE(structs, bins={1: B}, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_golden_"),
+    bpe = RB.BPE(structs, bins=bins, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_golden_"),
                  rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(num_p),
                  max_num_strucs=maxs, res_init=True, std_bonds=True, seed=0)
     try:

@@ -26,6 +26,10 @@ CASES = {
     "p3": (3, {2: 2, 3: 3, 5: 2, 8: 1}, 40, False, 6),
     "p3_super": (3, {2: 2, 3: 3, 5: 2, 8: 1}, 40, True, 6),
     "p0": (0, {2: 2, 3: 3, 5: 2, 8: 1}, 40, False, 6),
+    # multi-grid schedules in the RMSD mode (the scoped mode's step() goes stale with them)
+    "p0_multigrid": (0, {2: 2, 3: 3, 5: 2, 8: 1}, 40, False, 12, {1: 5, 6: 3, 9: 4}),
+    "p0_super_multigrid": (0, {2: 2, 3: 3, 5: 2, 8: 1}, 40, True, 12, {1: 5, 6: 3, 9: 4}),
+    "p3_super_multigrid": (3, {2: 2, 3: 3, 5: 2, 8: 1}, 40, True, 12, {1: 4, 7: 6}),
 }
 
 
@@ -34,7 +38,8 @@ def run_case(name):
     from geobpe import synth
     from make_golden import _stub_optional_deps
 
-    p, nump, maxs, sup, merges = CASES[name]
+    p, nump, maxs, sup, merges = CASES[name][:5]
+    bins = CASES[name][5] if len(CASES[name]) > 5 else {1: 5}
     lengths = synth.make_lengths(8, 20, 40, seed=11)
     corpus = synth.make_corpus(lengths, seed=11)
     _stub_optional_deps()
@@ -54,7 +59,7 @@ def run_case(name):
     out = {"case": name, "p_min_size": p, "num_partitions": {str(k): v for k, v in nump.items()}, "max_num_strucs": maxs,
            "rmsd_super_res": sup, "events": []}
     try:
-        bpe = B.BPE(structs, bins={1: 5}, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_probe_"),
+        bpe = B.BPE(structs, bins=dict(bins), save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_probe_"),
                     rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=nump,
                     max_num_strucs=maxs, res_init=True, std_bonds=True, seed=0)
         bpe.initialize()
@@ -73,13 +78,13 @@ def run_case(name):
 
 
 def main():
-    if len(sys.argv) == 3 and sys.argv[1] == "--one":
+    if len(sys.argv) == 3 and sys.argv[1] == "--one":  # noqa: SIM102
         print("JSON" + json.dumps(run_case(sys.argv[2])))
         return
     env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg", SLURM_CPUS_PER_TASK="2",
                PYTHONBREAKPOINT="0")
     res = []
-    for name in CASES:
+    for name in (sys.argv[1:] or CASES):
         r = subprocess.run([sys.executable, "-W", "ignore", __file__, "--one", name], env=env,
                            stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True, timeout=900)
         line = [ln for ln in r.stdout.splitlines() if ln.startswith("JSON")]

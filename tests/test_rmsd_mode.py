@@ -56,7 +56,7 @@ def run_and_compare(name, device=True):
     from geobpe.rmsd_bpe import RmsdBPE
 
     meta, corpus, arrs = _load(name)
-    bpe = BPE(corpus, bins={1: meta["bins"]["1"]}, rmsd_partition_min_size=meta["rmsd_partition_min_size"],
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()}, rmsd_partition_min_size=meta["rmsd_partition_min_size"],
               rmsd_super_res=meta["rmsd_super_res"], num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
               max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=True, seed=meta["rng_seed"])
     assert isinstance(bpe, RmsdBPE)
@@ -116,7 +116,7 @@ def host_geometry(monkeypatch):
     monkeypatch.setattr(rmsd, "rmsd_matrix", lambda S, device=0: orm.rmsd_matrix(S))
     monkeypatch.setattr(rmsd, "rmsd_cross", lambda A, B, device=0: np.array([[orm.rmsd(a, b) for b in B] for a in A]))
     monkeypatch.setattr(rmsd_bpe.RmsdBPE, "_grid_thresholds",
-                        lambda self: prologue.thresholds(self._corpus, self.B))
+                        lambda self: {s: prologue.thresholds(self._corpus, b) for s, b in self.bins.items()})
 
 
 @pytest.mark.parametrize("name", NAMES)
