@@ -178,6 +178,10 @@ def main(argv=None) -> int:
     log.info(args)
 
     from geobpe.bpe import BPE
+    rmsd_mode = args.p_min_size != float("inf")
+    if rmsd_mode and args.ckpt_format == "pkl":
+        raise SystemExit("--p-min-size < inf (the RMSD-partitioned mode) writes --ckpt-format json checkpoints; "
+                         "its bpe_iter=*.pkl form is not built")
     corpus = load_corpus(args.data_dir, args.toy)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     group, rank, shard, device = None, 0, corpus, args.device
@@ -212,7 +216,12 @@ def main(argv=None) -> int:
 
     start, ck, keys = latest_checkpoint(args.save_dir)
     if ck is not None:  # resume: re-run the saved number of merges, then check them against the file
-        done = bpe.run(len(keys))
+        if rmsd_mode:  # a step() may merge more than once there (recurring keys, bpe.py:2164-2166)
+            while len(bpe.merges) < len(keys) and bpe.run(1):
+                pass
+            done = len(bpe.merges)
+        else:
+            done = bpe.run(len(keys))
         if [m[0] for m in bpe.merges] != keys or done != len(keys):
             raise SystemExit(f"replay of {ck} diverged from the saved merge list")
         log.info("resumed from %s at iter=%d", ck, start)

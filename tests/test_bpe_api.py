@@ -175,6 +175,26 @@ def test_cli_resume_reproduces_one_shot(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cli_rmsd_mode_resume_reproduces_one_shot(tmp_path):
+    """bin/encode.py in the RMSD-partitioned mode (--p-min-size 0, --num-p, json
+    checkpoints): a run resumed at iter 10 ends with the one-shot run's merges and stats."""
+    cli = _encode_cli()
+    common = ["--data-dir", "synthetic:40:20:60:9", "--bins", "1-5", "--save-every", "5", "--p-min-size", "0",
+              "--num-p", "2-2:3-3:5-2", "--max-num-strucs", "60", "--rmsd-super-res", "true",
+              "--ckpt-format", "json", "--log-dir", str(tmp_path / "logs")]
+    one, two = tmp_path / "one", tmp_path / "two"
+    assert cli.main(common + ["--save-dir", str(one), "--max-iter", "21"]) == 0
+    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "11"]) == 0
+    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "21"]) == 0  # resumes at 10
+    a = json.loads((one / "bpe_iter=20.json").read_text())["merges"]
+    b = json.loads((two / "bpe_iter=20.json").read_text())["merges"]
+    assert a == b and len(a) >= 20
+    assert json.loads((one / "stats=20.json").read_text()) == json.loads((two / "stats=20.json").read_text())
+    with pytest.raises(SystemExit):  # pickle checkpoints of this mode are not built
+        cli.main(common[:-4] + ["--log-dir", str(tmp_path / "logs"), "--save-dir", str(tmp_path / "x")])
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("name", ["g40x50_b5", "g25x1-12_b3_short"])
 def test_checkpoint_from_device_matches_reference_pickle(name):
     """BPE.save_checkpoint on the HIP path (device merge-event log for the merge
