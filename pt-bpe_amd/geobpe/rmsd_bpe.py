@@ -30,7 +30,8 @@ reference's dictionaries instead, with the same add/remove sequence per key, so
 Reachable configurations (tests/golden/rmsd_mode_probe.json, rm_p4.json): p <= 3 partitions
 the residues at initialize() and every merge; p >= 4 never creates ``_sphere_dict``, so the
 first merge of >= p bonds raises AttributeError there, as it does here.  Not built: glue
-optimisation (LBFGS, ``glue_opt=True``), ``rmsd_only``, free bonds in this mode.
+optimisation (LBFGS, ``glue_opt=True``) and ``rmsd_only``.  Free bond lengths
+(``std_bonds=False``) run where the reference runs them (p <= 2; p >= 3 raises its KeyError).
 """
 from __future__ import annotations
 
@@ -207,8 +208,8 @@ class RmsdBPE:
             raise KeyError("bins must be a dict with key 1 (quantize/capacity need bins[1], bpe.py:896,909,952)")
         if not res_init:
             raise NotImplementedError("the RMSD mode needs res_init=True (bond-level init is not built)")
-        if not std_bonds:
-            raise NotImplementedError("free bonds in the RMSD mode are not built")
+        if not std_bonds and bin_strategy == "uniform":
+            raise NotImplementedError("free bonds with uniform (equal-count) bins are not built")
         if glue_opt:
             raise NotImplementedError("glue optimisation (LBFGS over NeRF, bpe.py:423-578) is not built")
         if rmsd_only or compute_sec_structs:
@@ -304,8 +305,12 @@ class RmsdBPE:
         thr = ThresholdDict()
         for size, grid in self._grid_thresholds().items():
             thr[size] = grid
-        for i, bt in enumerate(BOND_TYPES):
-            thr[bt] = [(BOND_LENGTHS[i], BOND_LENGTHS[i])]
+        if self.std_bonds:  # bpe.py:874-876
+            for i, bt in enumerate(BOND_TYPES):
+                thr[bt] = [(BOND_LENGTHS[i], BOND_LENGTHS[i])]
+        else:  # free bonds: bond-length histograms per grid too (bpe.py:830-831)
+            for size, grid in self._bond_thresholds().items():
+                thr[size].update(grid)
         self._thresholds = thr
         self._thr_by_len = {}
         ro = self._corpus["row_off"]
@@ -330,22 +335,46 @@ class RmsdBPE:
         finally:
             e.close()
 
+    def _bond_thresholds(self):
+        """{size: {bond type: thresholds}} with free bonds: np.histogram edges of every
+        chain's bond lengths (zeros / NaN padding dropped, the chain's two init lengths
+        added; bpe.py:841-852, plotting.py:316-319 non-circular) per grid's bin count.  An
+        order statistic of the host copy of the input, like the uniform strategy's edges."""
+        ro = self._corpus["row_off"]
+        n_ca, ca_c, _ = _rmsd.init_geometry()
+        out = {s: {} for s in self.bins}
+        for bt in BOND_TYPES:
+            col = np.asarray(self._corpus[bt], dtype=np.float64)
+            vals = col[np.nan_to_num(col, nan=0.0) != 0.0]
+            if bt in ("N:CA", "CA:C"):
+                vals = np.concatenate([vals, np.full(len(ro) - 1, n_ca if bt == "N:CA" else ca_c)])
+            for s, b in self.bins.items():
+                e = np.histogram_bin_edges(vals, bins=int(b))
+                out[s][bt] = [(float(a), float(c)) for a, c in zip(e[:-1], e[1:])]
+        return out
+
     def _centre(self, k, ind, size):
-        lookup = self._thresholds if k in BOND_TYPES else self._thresholds[size]
+        lookup = self._thresholds if k in BOND_TYPES and self.std_bonds else self._thresholds[size]
         return sum(lookup[k][ind]) / 2
 
     def _init_residues(self):
         p = self.rmsd_partition_min_size
-        for c in self._chains:  # std bonds for every bond (bpe.py:714-737)
+        for c in self._chains:  # every bond -> its bin centre (bpe.py:714-737)
             for j in range(3 * c.n - 1):
                 bt = BOND_TYPES[j % 3]
-                c.set_geo(j, 1, {bt: [sum(self._thresholds[bt][0]) / 2]})
+                if self.std_bonds:
+                    v = sum(self._thresholds[bt][0]) / 2
+                else:  # grid 1's bin of the length (strict get_ind, bpe.py:731)
+                    v = self._centre(bt, _get_ind(c.geo(j, 1)[bt][0], self._thresholds[1][bt]), 1)
+                c.set_geo(j, 1, {bt: [v]})
         label_dict, res_geo, labels = {}, {}, []
         for ci, c in enumerate(self._chains):
             lab = []
             for i in range(c.n):
                 start, length = 3 * i, (3 if i < c.n - 1 else 2)
                 if length < p:  # binned residue (bpe.py:237-249)
+                    if not self.std_bonds:  # quant_geo reads _thresholds[bond] (bpe.py:1518-1524)
+                        raise KeyError("N:CA")
                     geo = c.geo(start, length)
                     cen = {}
                     for k, vals in geo.items():
@@ -433,7 +462,7 @@ class RmsdBPE:
             rng = ((0, L), (0, L), (0, L))
         for k, vals in geo.items():
             if k in BOND_TYPES:
-                base, kind, thr = (BOND_TYPES.index(k) + 3 - ph) % 3, 0, thr_all[k]
+                base, kind, thr = (BOND_TYPES.index(k) + 3 - ph) % 3, 0, (thr_all[k] if self.std_bonds else thr_L[k])
             elif k in BOND_ANGLES:
                 base, kind, thr = (BOND_ANGLES.index(k) + 3 - ph) % 3, 1, thr_L[k]
             else:

@@ -51,6 +51,11 @@ FIXTURES = {
     # keys stay consistent (unlike the scoped mode)
     "rm_p0_multigrid": (12, 20, 40, 28, {1: 5, 6: 3, 9: 4, 15: 2}, 0, False, 60, 60),
     "rm_p3_super_multigrid": (10, 15, 40, 29, {1: 4, 2: 6, 7: 6}, 3, True, 60, 40),
+    # free bond lengths (--free-bonds, as in the README runs): bonds binned per grid too;
+    # p = 3 raises KeyError in initialize() there
+    "rm_p0_super_freebonds": (10, 20, 40, 30, 5, 0, True, 60, 40, NUM_P, False),
+    "rm_p2_freebonds_multigrid": (12, 15, 35, 31, {1: 4, 6: 3}, 2, False, 60, 40, NUM_P, False),
+    "rm_p3_freebonds": (6, 15, 30, 32, 5, 3, False, 60, 5, NUM_P, False),
 }
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
@@ -66,6 +71,7 @@ def run_one(name):
 
     nch, lo, hi, seed, B, p, sup, maxs, calls = FIXTURES[name][:9]
     num_p = FIXTURES[name][9] if len(FIXTURES[name]) > 9 else NUM_P
+    std = FIXTURES[name][10] if len(FIXTURES[name]) > 10 else True
     corpus = synth.make_corpus(synth.make_lengths(nch, lo, hi, seed=seed), seed=seed)
     _stub_optional_deps()
     sys.path.insert(0, "/root/reference")
@@ -104,14 +110,14 @@ def run_one(name):
     bins = dict(B) if isinstance(B, dict) else {1: B}
     meta = {"name": name, "n_chains": nch, "len_lo": lo, "len_hi": hi, "seed": seed,
             "bins": {str(k): v for k, v in bins.items()},
-            "rmsd_partition_min_size": p, "rmsd_super_res": sup, "max_num_strucs": maxs,
+            "rmsd_partition_min_size": p, "rmsd_super_res": sup, "max_num_strucs": maxs, "std_bonds": std,
             "num_partitions": {str(k): v for k, v in num_p.items()}, "rng_seed": 0, "calls": [],
             "raised": None, "generator": "tests/golden/make_rmsd_mode_golden.py (reference: /root/reference "
                                          "foldingdiff/bpe.py, run in the build container)"}
     arrays = dict(corpus)
     bpe = RB.BPE(structs, bins=bins, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_golden_"),
                  rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(num_p),
-                 max_num_strucs=maxs, res_init=True, std_bonds=True, seed=0)
+                 max_num_strucs=maxs, res_init=True, std_bonds=std, seed=0)
     try:
         bpe.initialize()
         geometry(bpe, "init", arrays)

@@ -30,6 +30,9 @@ CASES = {
     "p0_multigrid": (0, {2: 2, 3: 3, 5: 2, 8: 1}, 40, False, 12, {1: 5, 6: 3, 9: 4}),
     "p0_super_multigrid": (0, {2: 2, 3: 3, 5: 2, 8: 1}, 40, True, 12, {1: 5, 6: 3, 9: 4}),
     "p3_super_multigrid": (3, {2: 2, 3: 3, 5: 2, 8: 1}, 40, True, 12, {1: 4, 7: 6}),
+    # free bond lengths (--free-bonds true, the README runs)
+    "p0_super_freebonds": (0, {2: 2, 3: 3, 5: 2, 8: 1}, 40, True, 12, {1: 5}, False),
+    "p3_freebonds": (3, {2: 2, 3: 3, 5: 2, 8: 1}, 40, False, 12, {1: 5}, False),
 }
 
 
@@ -40,6 +43,7 @@ def run_case(name):
 
     p, nump, maxs, sup, merges = CASES[name][:5]
     bins = CASES[name][5] if len(CASES[name]) > 5 else {1: 5}
+    std = CASES[name][6] if len(CASES[name]) > 6 else True
     lengths = synth.make_lengths(8, 20, 40, seed=11)
     corpus = synth.make_corpus(lengths, seed=11)
     _stub_optional_deps()
@@ -61,7 +65,7 @@ def run_case(name):
     try:
         bpe = B.BPE(structs, bins=dict(bins), save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_probe_"),
                     rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=nump,
-                    max_num_strucs=maxs, res_init=True, std_bonds=True, seed=0)
+                    max_num_strucs=maxs, res_init=True, std_bonds=std, seed=0)
         bpe.initialize()
         out["events"].append(["initialize", "ok", len(bpe._tokens), [str(k) for k in list(bpe._tokens)[:12]]])
         bpe.bin()

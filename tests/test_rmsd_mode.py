@@ -58,8 +58,14 @@ def run_and_compare(name, device=True):
     meta, corpus, arrs = _load(name)
     bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()}, rmsd_partition_min_size=meta["rmsd_partition_min_size"],
               rmsd_super_res=meta["rmsd_super_res"], num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
-              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=True, seed=meta["rng_seed"])
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta.get("std_bonds", True),
+              seed=meta["rng_seed"])
     assert isinstance(bpe, RmsdBPE)
+    if "init_tokens" not in meta:  # the reference raised in initialize()
+        with pytest.raises(Exception) as ei:
+            bpe.initialize()
+        assert type(ei.value).__name__ == meta["raised"]["type"]
+        return bpe
     popped = []
     inner = bpe._merge
 
@@ -139,5 +145,5 @@ def test_rmsd_mode_dispatch_and_scope():
 @pytest.mark.parametrize("name", NAMES)
 def test_rmsd_mode_device_matches_reference(name):
     bpe = run_and_compare(name)
-    if name != "rm_p4":
+    if name not in ("rm_p4", "rm_p3_freebonds"):
         assert bpe.assign_calls > 0  # the device RMSD batches ran
