@@ -38,6 +38,9 @@ constexpr int NBA_MAX = 256;
 #ifndef GB_FKC
 #define GB_FKC 2048
 #endif
+#ifndef FIND_NT
+#define FIND_NT 0  // k_find: non-temporal stores of its outputs (A/B)
+#endif
 #ifndef COMMIT_SPEC
 #define COMMIT_SPEC 0  // k_commit: 1 = load every finder slot's first records before the scans
 #endif

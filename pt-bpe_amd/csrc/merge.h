@@ -26,6 +26,34 @@
 #pragma once
 // (included inside namespace gb)
 
+// k_find's outputs (merge entries, key / decrement records, T slots) are read once, by
+// k_commit / k_place on other XCDs: FIND_NT=1 stores them non-temporal (A/B)
+template <typename V>
+__device__ inline void out_store(V* p, const V& v) {
+#if FIND_NT
+  static_assert(sizeof(V) % 16 == 0 || sizeof(V) == 8 || sizeof(V) == 4, "store width");
+  if constexpr (sizeof(V) % 16 == 0) {
+    const int4* src = reinterpret_cast<const int4*>(&v);
+    int4* dst = reinterpret_cast<int4*>(p);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(V) / 16); i++) {
+      __builtin_nontemporal_store(src[i].x, &dst[i].x);
+      __builtin_nontemporal_store(src[i].y, &dst[i].y);
+      __builtin_nontemporal_store(src[i].z, &dst[i].z);
+      __builtin_nontemporal_store(src[i].w, &dst[i].w);
+    }
+  } else if constexpr (sizeof(V) == 8) {
+    const int2 x = *reinterpret_cast<const int2*>(&v);
+    __builtin_nontemporal_store(x.x, &reinterpret_cast<int2*>(p)->x);
+    __builtin_nontemporal_store(x.y, &reinterpret_cast<int2*>(p)->y);
+  } else {
+    __builtin_nontemporal_store(*reinterpret_cast<const int32_t*>(&v), reinterpret_cast<int32_t*>(p));
+  }
+#else
+  *p = v;
+#endif
+}
+
 // chunked per-owner posting log: entry k of owner o
 __device__ inline int64_t log_addr(const Dev& D, int o, int64_t k) {
   return (int64_t)D.pch[(int64_t)o * D.MAXCH + k / D.CHUNK] * D.CHUNK + k % D.CHUNK;
@@ -164,7 +192,7 @@ __device__ inline void emit_occ(const Dev& D, FindCtx& F, int32_t* s_n, int32_t 
   base = __shfl(base, leader, 64);
   const int32_t j = base + __popcll(m & ((1ULL << lane) - 1));
   if (j < D.LC) {
-    D.L[(int64_t)F.r * D.LC + j] = e;
+    out_store(&D.L[(int64_t)F.r * D.LC + j], e);
   } else {
     const int64_t k = atomicAdd((unsigned long long*)&D.st->L_ovf2[F.par], 1ULL);
     if (k < D.Lovf_cap)
@@ -190,7 +218,7 @@ __device__ inline void emit_krec(const Dev& D, const FindCtx& F, int32_t* curK, 
   const int o = owner_of_key(D, h.pkey);
   const int32_t j = atomicAdd(&curK[o], 1);
   if (j < SK) {
-    D.KS[((int64_t)o * D.NBA + F.r) * SK + j] = k;
+    out_store(&D.KS[((int64_t)o * D.NBA + F.r) * SK + j], k);
   } else {
     const int64_t x = atomicAdd((unsigned long long*)&D.st->nko2[F.par], 1ULL);
     if (x < D.KO_cap)
@@ -496,7 +524,7 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       const int64_t tbase = (int64_t)r * D.TC + S.tb;
       if (vl) {
         if (sl >= 0 && fits) {
-          D.T[tbase + S.u.m.kst[sl] + kl] = hl.target;
+          out_store(&D.T[tbase + S.u.m.kst[sl] + kl], hl.target);
           if (rl) emit_krec(D, F, S.curK, hl, S.u.m.kcnt[sl], (int32_t)(tbase + S.u.m.kst[sl]));
         } else {
           emit_single(D, F, S.curK, hl);
@@ -504,7 +532,7 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       }
       if (vr) {
         if (sr >= 0 && fits) {
-          D.T[tbase + S.u.m.kst[sr] + kr] = hr.target;
+          out_store(&D.T[tbase + S.u.m.kst[sr] + kr], hr.target);
           if (rr) emit_krec(D, F, S.curK, hr, S.u.m.kcnt[sr], (int32_t)(tbase + S.u.m.kst[sr]));
         } else {
           emit_single(D, F, S.curK, hr);
@@ -534,7 +562,7 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
     const int ow = owner_of_slot(D, (u64)k);
     const int32_t j = atomicAdd(&S.curD[ow], 1);
     if (j < SD)
-      D.DS[((int64_t)ow * D.NBA + r) * SD + j] = make_int2(k, v);
+      out_store(&D.DS[((int64_t)ow * D.NBA + r) * SD + j], make_int2(k, v));
     else
       global_add(D, k, v, F.to_delta);
   }
