@@ -56,6 +56,10 @@ FIXTURES = {
     "rm_p0_super_freebonds": (10, 20, 40, 30, 5, 0, True, 60, 40, NUM_P, False),
     "rm_p2_freebonds_multigrid": (12, 15, 35, 31, {1: 4, 6: 3}, 2, False, 60, 40, NUM_P, False),
     "rm_p3_freebonds": (6, 15, 30, 32, 5, 3, False, 60, 5, NUM_P, False),
+    # config 1's corpus (every PDB of the reference's data/vqvae_pretrain/train, featurised by
+    # pdb_angles.py) in the README's first run minus glue optimisation: --bins 1-50, p = 0,
+    # --num-p 2-2:3-5:5-1:6-2:8-1, max_num_strucs 500, free bonds, rmsd_super_res
+    "rm_pdb72_readme": ("pdb72", None, None, 0, 50, 0, True, 500, 20, {2: 2, 3: 5, 5: 1, 6: 2, 8: 1}, False),
 }
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
@@ -72,7 +76,12 @@ def run_one(name):
     nch, lo, hi, seed, B, p, sup, maxs, calls = FIXTURES[name][:9]
     num_p = FIXTURES[name][9] if len(FIXTURES[name]) > 9 else NUM_P
     std = FIXTURES[name][10] if len(FIXTURES[name]) > 10 else True
-    corpus = synth.make_corpus(synth.make_lengths(nch, lo, hi, seed=seed), seed=seed)
+    if nch == "pdb72":
+        import pdb_angles
+        corpus, _ = pdb_angles.pdb_dir_corpus("/root/reference/data/vqvae_pretrain/train")
+        nch = len(corpus["row_off"]) - 1
+    else:
+        corpus = synth.make_corpus(synth.make_lengths(nch, lo, hi, seed=seed), seed=seed)
     _stub_optional_deps()
     sys.path.insert(0, "/root/reference")
     import foldingdiff.bpe as RB
