@@ -38,6 +38,9 @@ constexpr int NBA_MAX = 256;
 #ifndef GB_FKC
 #define GB_FKC 2048
 #endif
+#ifndef PLACE_PRE
+#define PLACE_PRE 1  // k_place: the first round's records loaded before the token rewrites
+#endif
 #ifndef FIND_NT
 #define FIND_NT 0  // k_find: non-temporal stores of its outputs (A/B)
 #endif

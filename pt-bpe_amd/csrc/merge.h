@@ -1076,6 +1076,31 @@ struct PlaceLds {
   int32_t red[ABLOCK / 64];
 };
 
+// record i of finder region j's records (the owners' slots, then its share k_lo.. of the
+// overflow list): occurrence count, T start, key id, posting-log position, owner
+__device__ inline void place_record(const Dev& D, const PlaceLds& S, int32_t j, int32_t i, int32_t nk, int64_t k_lo,
+                                    int32_t& n, int32_t& ts, int32_t& id, int32_t& lp, int32_t& ow) {
+  int2 v;
+  if (i < nk) {
+    ow = seg_of(S.pre, D.NBA, i);
+    const int64_t at = ((int64_t)ow * D.NBA + j) * SK + (i - S.pre[ow]);
+    const int2 nt = *reinterpret_cast<const int2*>(&D.KS[at].n);
+    v = D.KSid[at];
+    n = nt.x;
+    ts = nt.y;
+  } else {
+    const int64_t x = k_lo + (i - nk);
+    const KRec k = D.KO[x];
+    v = D.KOid[x];
+    ow = owner_of_key(D, k.pkey);
+    n = k.n;
+    ts = k.tstart;
+  }
+  id = v.x;
+  lp = v.y;
+  if (id < 0) n = 0;
+}
+
 // place the merge committed with launch parity st->place_par (k_commit sets it; -1:
 // nothing to place).  Idempotent until the next k_find: a re-run writes the same
 // values (the pipelined exchange may run it again behind a stall).
@@ -1101,6 +1126,16 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
     if (threadIdx.x < D.NBA) S.pre[threadIdx.x] = e;
     if (threadIdx.x == 0) S.pre[D.NBA] = tot;
   }
+  // this thread's record of the first round, loaded before the token rewrites so that its
+  // latency hides behind them (PLACE_PRE; the records depend only on k_commit)
+  int32_t p_n = 0, p_ts = 0, p_id = -1, p_lp = -1, p_ow = 0;
+#if PLACE_PRE
+  __syncthreads();  // S.pre
+  {
+    const int32_t i = threadIdx.x, nk = S.pre[D.NBA];
+    if (i < nk + (int32_t)k_n) place_record(D, S, j, i, nk, k_lo, p_n, p_ts, p_id, p_lp, p_ow);
+  }
+#endif
   for (int64_t i = threadIdx.x; i < nA + o_n; i += ABLOCK) {
     const LEntry e = i < nA ? D.L[(int64_t)j * D.LC + i] : D.Lovf[o_lo + (i - nA)];
     *reinterpret_cast<int2*>(D.tok + e.a) = make_int2(nid, e.ya);
@@ -1112,31 +1147,14 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   }
   __syncthreads();
   dbg_stamp(D, 31);
-  const int32_t nrec = S.pre[D.NBA] + (int32_t)k_n;
-  for (int32_t i0 = 0; i0 < nrec; i0 += ABLOCK) {  // block-uniform rounds of records
+  const int32_t nrec2 = S.pre[D.NBA] + (int32_t)k_n;
+  for (int32_t i0 = 0; i0 < nrec2; i0 += ABLOCK) {  // block-uniform rounds of records
     const int32_t i = i0 + threadIdx.x;
     int32_t n = 0, ts = 0, id = -1, lp = -1, ow = 0;
-    if (i < nrec) {
-      const int32_t nk = S.pre[D.NBA];
-      int2 v;
-      if (i < nk) {
-        ow = seg_of(S.pre, D.NBA, i);
-        const int64_t at = ((int64_t)ow * D.NBA + j) * SK + (i - S.pre[ow]);
-        const int2 nt = *reinterpret_cast<const int2*>(&D.KS[at].n);
-        v = D.KSid[at];
-        n = nt.x;
-        ts = nt.y;
-      } else {
-        const int64_t x = k_lo + (i - nk);
-        const KRec k = D.KO[x];
-        v = D.KOid[x];
-        ow = owner_of_key(D, k.pkey);
-        n = k.n;
-        ts = k.tstart;
-      }
-      id = v.x;
-      lp = v.y;
-      if (id < 0) n = 0;
+    if (PLACE_PRE && i0 == 0) {
+      n = p_n, ts = p_ts, id = p_id, lp = p_lp, ow = p_ow;
+    } else if (i < nrec2) {
+      place_record(D, S, j, i, S.pre[D.NBA], k_lo, n, ts, id, lp, ow);
     }
     int32_t tot;
     const int32_t ex = block_excl_scan(n, &tot, S.red);
