@@ -38,6 +38,12 @@ constexpr int NBA_MAX = 256;
 #ifndef GB_FKC
 #define GB_FKC 2048
 #endif
+#ifndef EARLY_LOADS
+#define EARLY_LOADS 0  // k_find: the EHASH-check records loaded first, compared last (A/B: spills, slower)
+#endif
+#ifndef EARLY_KCHUNK
+#define EARLY_KCHUNK 1  // k_commit: the owner's klist chunk loaded with the first round
+#endif
 #ifndef PLACE_PRE
 #define PLACE_PRE 1  // k_place: the first round's records loaded before the token rewrites
 #endif

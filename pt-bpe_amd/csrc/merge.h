@@ -146,6 +146,16 @@ __device__ inline void check_found(const Dev& D, int32_t r) {
   }
 }
 
+// check_found with this thread's first record already loaded (EARLY_LOADS)
+__device__ inline void check_found_tail(const Dev& D, int32_t r, int32_t n, const NewPair& e0) {
+  const NewPair* reg = D.chk + (int64_t)r * D.RC;
+  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
+    const NewPair e = i < (int32_t)blockDim.x ? e0 : reg[i];
+    const int32_t d = e.target;
+    if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) set_error(D, GEOBPE_EHASH, i);
+  }
+}
+
 // ---------------------------------------------------------------------- k_find
 struct FHalf {  // a new neighbour pair of a merged occurrence
   u64 pkey, h1, h2;
@@ -382,8 +392,21 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   const int32_t r = blockIdx.x;
   dbg_stamp(D, 10);
   const Sel sel = D.sel[par];
+#if EARLY_LOADS
+  // EHASH check of the keys the previous commit / import found: the first ABLOCK records
+  // are loaded now and compared after the merge work (their two dependent rounds used to
+  // precede the candidate loads)
+  const int32_t nchk = D.chkcnt[r];
+  NewPair chk0;
+  if ((int32_t)threadIdx.x < nchk) chk0 = D.chk[(int64_t)r * D.RC + threadIdx.x];
+  if (sel.decision != SEL_MERGE) {
+    check_found_tail(D, r, nchk, chk0);
+    return;
+  }
+#else
   check_found(D, r);
   if (sel.decision != SEL_MERGE) return;
+#endif
   FindCtx F;
   F.W = sel.W;
   F.nid = sel.nid;
@@ -572,6 +595,9 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
     D.cntD[(int64_t)i * D.NBA + r] = min(S.curD[i], SD);
   }
   if (threadIdx.x == 0) D.Lcnt[r] = min(S.n, (int32_t)D.LC);
+#if EARLY_LOADS
+  check_found_tail(D, r, nchk, chk0);
+#endif
   dbg_stamp(D, 13);
 }
 
@@ -808,6 +834,9 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const int32_t th = st->theta;
   const int32_t pn = D.pnch[j], pf = D.pfill[j];
   const int64_t nko_raw = st->nko2[par];
+#if EARLY_KCHUNK
+  const int64_t kl0 = D.kchunk[2 * j], kl1 = D.kchunk[2 * j + 1];  // (this owner's klist chunk)
+#endif
   int32_t lc = 0;
   if (j == 0 && t < nba) lc = D.Lcnt[t];
   if (j == 0 && t == 0) {
@@ -872,8 +901,13 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       S.ns = 0;
       S.chk = 0;
       S.fbn = 0;
+#if EARLY_KCHUNK
+      s_kl[0] = kl0;
+      s_kl[1] = kl1;
+#else
       s_kl[0] = D.kchunk[2 * j];
       s_kl[1] = D.kchunk[2 * j + 1];
+#endif
     }
   }
   __syncthreads();
