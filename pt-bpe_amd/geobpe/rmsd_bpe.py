@@ -258,7 +258,7 @@ class RmsdBPE:
         device NeRF batch: the span rounded out to whole residues, then its atoms."""
         geos, cuts = [], []
         for ci, index, length in spans:
-            c = self._chains[ci]
+            c = ci if isinstance(ci, _Chain) else self._chains[ci]
             length = min(length, 3 * c.n - 1 - index)
             start = 3 * (index // 3)
             end = 3 * (((index + length - 1) + 1) // 3) + 1
@@ -437,7 +437,7 @@ class RmsdBPE:
 
     # ------------------------------------------------------------ keys (bpe.py:1192-1299)
     def _pair_key(self, ci, idx1, l1, l2):
-        c = self._chains[ci]
+        c = ci if isinstance(ci, _Chain) else self._chains[ci]
         idx2 = idx1 + l1
         t1, t2 = c.btt[c.token_pos[idx1]], c.btt[c.token_pos[idx2]]
         if t1[0] == t2[0]:
@@ -659,6 +659,126 @@ class RmsdBPE:
     def merges(self):
         """[(key string, count)] of every merge, recurring repeats included."""
         return [tuple(m) for m in self._merge_log]
+
+    # ------------------------------------------------------------ induce (bpe.py:1053-1140)
+    def tokenize(self, structure):
+        """BPE.tokenize: a new chain segmented with the trained vocabulary.  Its bonds go
+        to their bins (out-of-range lengths clamp, ``strict=False``); every residue is
+        assigned to its nearest residue medoid (device NeRF + RMSD); the glue angles go to
+        grid-1 centres; then every merge key, in training order, is applied to the chain
+        alone (``step_helper``, bpe.py:1316-1425: nearest medoid per occurrence, greedy left
+        to right, the medoid's geometry written back).  Returns (tokenizer, metrics) with
+        metrics["L"] = the token count before and after each key; the reference's backbone
+        RMSD / lDDT against the PDB need esm's ProteinChain and are not computed.
+
+        ``structure``: {"angles": 9 columns, "fname": ...} (the reference's structure
+        dict) or a mapping of the 9 columns."""
+        if not self.res_init:
+            raise NotImplementedError
+        ang = structure["angles"] if isinstance(structure, dict) and "angles" in structure else structure
+        fname = structure.get("fname") if isinstance(structure, dict) else None
+        c = _Chain({k: np.asarray(ang[k], dtype=np.float64) for k in COLUMNS}, _rmsd.init_geometry(), fname)
+        for j in range(3 * c.n - 1):  # _set_bond_length_worker(t, strict=False) (bpe.py:715-737)
+            bt = BOND_TYPES[j % 3]
+            if self.std_bonds:
+                v = sum(self._thresholds[bt][0]) / 2
+            else:
+                thr = self._thresholds[1][bt]
+                x = c.geo(j, 1)[bt][0]
+                ind = 0 if x < thr[0][0] else (len(thr) - 1 if x > thr[-1][1] else _get_ind(x, thr))
+                v = sum(thr[ind]) / 2
+            c.set_geo(j, 1, {bt: [v]})
+        res_geo = {}
+        for i in range(c.n):
+            res_geo.setdefault(3 if i < c.n - 1 else 2, []).append(3 * i)
+        c.token_pos = [3 * (j // 3) for j in range(3 * c.n - 1)]
+        c.btt = {3 * i: (3 * i, None, 3 if i < c.n - 1 else 2) for i in range(c.n)}
+        for n, size in enumerate(res_geo):  # nearest residue medoid (bpe.py:1072-1099)
+            geo = c.geo(0, 5) if size == 3 else c.geo(0, 2)
+            strucs = []
+            p = 0
+            while (n, p) in self._tokens:
+                key = self._tokens[(n, p)]
+                for k in key:
+                    geo[k][:len(key[k])] = key[k]
+                strucs.append({k: list(v) for k, v in geo.items()})
+                p += 1
+            med = [x[:size + 1] for x in _rmsd.geo_coords(strucs, device=self.device)]
+            starts = res_geo[size]
+            assign = self._assign(self._span_coords([(c, s0, size) for s0 in starts], False), med)
+            for s0, p in zip(starts, assign):
+                c.set_geo(s0, size, self._tokens[(n, p)])
+                c.btt[s0] = (s0, (n, p), size)
+        for k in GLUE:  # grid-1 glue centres, NaN kept (bpe.py:1101-1108)
+            col = c.cur[k]
+            for r in range(c.n):
+                v = col[r]
+                if v == v:
+                    col[r] = self._centre(k, _get_ind((v + TWO_PI) % TWO_PI, self._thresholds[1][k]), 1)
+        geo_dict = defaultdict(set)  # bin_helper (bpe.py:1301-1314)
+        toks = c.tokens()
+        for (i1, _, l1), (i2, _, l2) in zip(toks, toks[1:]):
+            geo_dict[self._pair_key(c, i1, l1, l2)].add(i2)
+        uniq = sorted({k[0] for k in self._tokens})
+        keys = list(self._sphere_dict)
+        if len(uniq) != len(keys):
+            raise AssertionError("_tokens and _sphere_dict out of step")
+        metrics = {"L": [len(c.btt)]}
+        for n, key in zip(uniq[2:], keys[2:]):
+            if key in geo_dict:
+                self._step_helper(geo_dict, c, key, n)
+            metrics["L"].append(len(c.btt))
+        return RmsdTokenizer(c), metrics
+
+    def _step_helper(self, geo_dict, c, key, n):
+        """step() on one chain for a trained key (bpe.py:1316-1404)."""
+        key_dict = json.loads(key)
+        length = sum(len(key_dict.get(k, [])) for k in BOND_TYPES)
+        vals = list(geo_dict[key])
+        tp = c.token_pos
+        spans = [(c, tp[index - 1], length) for index in vals]
+        assign = self._assign(self._span_coords(spans, self.rmsd_super_res), self._struc_coords(self._sphere_dict[key]))
+        last_i1 = None
+        for idx in sorted(range(len(vals)), key=vals.__getitem__):
+            i2 = vals[idx]
+            i1 = tp[i2 - 1]
+            l1 = i2 - i1
+            l2 = length - l1
+            overlaps = last_i1 is not None and last_i1 + length > i1
+            if overlaps != (i2 not in geo_dict[key]):
+                raise RuntimeError("occurrence bookkeeping out of step (the reference stops in breakpoint())")
+            if overlaps:
+                continue
+            if not (l1 > 0 and l2 > 0):
+                raise AssertionError("bad split")
+            if self._pair_key(c, i1, l1, l2) != key:
+                continue  # bpe.py:1350-1352
+            geo_dict[key].remove(i2)
+            left = right = None
+            if i1:
+                i0 = tp[i1 - 1]
+                l0 = i1 - i0
+                left = self._pair_key(c, i0, l0, l1)
+            if i2 + l2 < len(tp):
+                i3 = i2 + l2
+                l3 = 0
+                while i3 + l3 < len(tp) and tp[i3 + l3] == i3:
+                    l3 += 1
+                right = self._pair_key(c, i2, l2, l3)
+            if left:
+                geo_dict[left].remove(i1)
+            if right:
+                geo_dict[right].remove(i3)
+            for j in range(i2, i2 + l2):
+                tp[j] = i1
+            c.btt.pop(i2)
+            c.btt[i1] = (i1, (n, assign[idx]), length)
+            c.set_geo(i1, length, self._sphere_dict[key][assign[idx]])
+            if left:
+                geo_dict[self._pair_key(c, i0, l0, length)].add(i1)
+            if right:
+                geo_dict[self._pair_key(c, i1, length, l3)].add(i3)
+            last_i1 = i1
 
     # ------------------------------------------------------------ views / encode
     @property

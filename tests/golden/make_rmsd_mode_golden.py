@@ -61,6 +61,19 @@ FIXTURES = {
     # --num-p 2-2:3-5:5-1:6-2:8-1, max_num_strucs 500, free bonds, rmsd_super_res
     "rm_pdb72_readme": ("pdb72", None, None, 0, 50, 0, True, 500, 20, {2: 2, 3: 5, 5: 1, 6: 2, 8: 1}, False),
 }
+# BPE.tokenize (bpe.py:1053-1140, the RMSD mode's induce) after the training calls, on: the
+# first three training chains, the first 60 % of chains 3 and 4 (values inside the trained
+# bins), and new synthetic chains (chains, len_lo, len_hi, seed) -- those usually hold a value
+# outside the trained range, and the reference's get_ind raises ValueError (recorded).  It
+# needs the residue partitions of both sizes (p <= 2: it skips the first two _sphere_dict
+# keys, :1116-1119)
+INDUCE = {
+    "rm_p0": (5, 15, 45, 99),
+    "rm_p0_super": (5, 15, 45, 98),
+    "rm_p2_super_b3": (6, 10, 30, 97),
+    "rm_p0_super_freebonds": (5, 15, 45, 96),
+    "rm_pdb72_readme": (4, 40, 120, 95),
+}
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
 
@@ -145,6 +158,8 @@ def run_one(name):
     except BaseException as e:  # noqa: BLE001 - the fixture records what the reference raises
         meta["raised"] = {"type": type(e).__name__, "msg": str(e)[:300], "popped_so_far": popped[-1:],
                           "where": traceback.format_exc().splitlines()[-4:]}
+    if name in INDUCE and not meta["raised"]:
+        run_induce(name, bpe, Tokenizer, RB, meta, arrays, corpus)
     if "init_tokens" in meta:
         geometry(bpe, "final", arrays)
         meta["tokens"] = [[_id(k), v] for k, v in bpe._tokens.items()]
@@ -167,6 +182,72 @@ def run_one(name):
     merges = sum(len(c["popped"]) for c in meta["calls"])
     print(f"{name}: calls={len(meta['calls'])} merges={merges} step={meta.get('step')} "
           f"raised={meta['raised'] and meta['raised']['type']}", flush=True)
+
+
+class _Chain:  # esm's ProteinChain stand-in: the metrics it feeds (bb RMSD, lDDT) are not recorded
+    @classmethod
+    def from_pdb(cls, *a, **k):
+        return cls()
+
+    @classmethod
+    def from_backbone_atom_coordinates(cls, *a, **k):
+        return cls()
+
+    def rmsd(self, *a, **k):
+        return 0.0
+
+    def lddt_ca(self, *a, **k):
+        import numpy as np
+        return np.zeros(1)
+
+
+def induce_corpus(train, name):
+    """The chains run_induce tokenizes (see INDUCE), as one corpus."""
+    import numpy as np
+    from geobpe import synth
+    n_new, lo, hi, seed = INDUCE[name]
+    ro = train["row_off"]
+    rows = []
+    for r in range(5):
+        a, b = int(ro[r]), int(ro[r + 1])
+        if r >= 3:
+            b = a + max(2, int(0.6 * (b - a)))
+        rows.append({c: np.array(train[c][a:b], dtype=np.float64) for c in COLS})
+        if r >= 3:  # the reference's padding at the new end (angles_and_coords.py:101-149)
+            for c in ["psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]:
+                rows[-1][c][-1] = np.nan
+            for c in ["0C:1N", "N:CA", "CA:C"]:
+                rows[-1][c][-1] = 0.0
+    new = synth.make_corpus(synth.make_lengths(n_new, lo, hi, seed=seed), seed=seed)
+    rows += list(synth.corpus_rows(new))
+    out = {c: np.concatenate([x[c] for x in rows]) for c in COLS}
+    out["row_off"] = np.concatenate([[0], np.cumsum([len(x["phi"]) for x in rows])]).astype(np.int64)
+    return out, rows
+
+
+def run_induce(name, bpe, Tokenizer, RB, meta, arrays, train):
+    import numpy as np
+    corpus, rows = induce_corpus(train, name)
+    for c in COLS + ["row_off"]:
+        arrays[f"new_{c}"] = corpus[c]
+    RB.ProteinChain = _Chain
+    out = []
+    for i, row in enumerate(rows):
+        s = Tokenizer.init_structure(len(row["phi"]))
+        for c in COLS:
+            s["angles"][c] = row[c]
+        s["fname"] = f"new_{i}"
+        try:
+            t, metrics = bpe.tokenize(Tokenizer(s))
+        except Exception as e:  # noqa: BLE001 - recorded: the reference's behaviour on this chain
+            out.append({"raised": type(e).__name__, "msg": str(e)[:200]})
+            continue
+        out.append({"segmentation": [[int(a), _id(v[1]), int(v[2])] for a, v in t.bond_to_token.items()],
+                    "L": [int(x) for x in metrics["L"]]})
+        for c in COLS:
+            arrays[f"new{i}_{c}"] = np.array([float(x) for x in t.angles_and_dists[c]])
+        arrays[f"new{i}_init"] = np.array([float(t._init_n_ca), float(t._init_ca_c), float(t._init_bond_angle)])
+    meta["induce"] = out
 
 
 def main(argv):

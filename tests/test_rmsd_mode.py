@@ -108,6 +108,21 @@ def run_and_compare(name, device=True):
     assert bpe.vocab_size == meta["vocab_size"]
     if "final_top" in meta:
         assert [list(p) for p in bpe._priority[:20]] == meta["final_top"]
+    for i, want in enumerate(meta.get("induce", [])):  # BPE.tokenize of held-out / training chains
+        ro = arrs["new_row_off"]
+        struct = {"angles": {c: arrs[f"new_{c}"][ro[i]:ro[i + 1]] for c in COLS}, "fname": f"new_{i}"}
+        if "raised" in want:
+            with pytest.raises(Exception) as ei:
+                bpe.tokenize(struct)
+            assert type(ei.value).__name__ == want["raised"]
+            continue
+        t, metrics = bpe.tokenize(struct)
+        got = [[s0, list(v[1]) if isinstance(v[1], tuple) else v[1], v[2]] for s0, v in t.bond_to_token.items()]
+        assert got == want["segmentation"], f"induce {i}"
+        assert metrics["L"] == want["L"], f"induce {i}"
+        for c in COLS:
+            assert np.array_equal(np.asarray(t._c.cur[c]), arrs[f"new{i}_{c}"], equal_nan=True), f"induce {i} {c}"
+        assert np.array_equal(np.array(t._c.init), arrs[f"new{i}_init"])
     return bpe
 
 
