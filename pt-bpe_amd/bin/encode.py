@@ -138,7 +138,18 @@ def _saved_keys(path: str):
     from geobpe import refpickle
     if not refpickle.is_complete(path):  # encode.py:183-200 skips incomplete pickles
         return None
-    return refpickle.merge_keys(refpickle.load(path))
+    obj = refpickle.load(path)
+    if getattr(obj, "_sphere_dict", None) is not None:  # RMSD mode: one _sphere_dict key per step()
+        return rmsd_merge_keys(obj)
+    return refpickle.merge_keys(obj)
+
+
+def rmsd_merge_keys(bpe) -> list:
+    """The RMSD mode's merge keys in merge order: _sphere_dict without the residue
+    partitions' keys (bpe.py:333-339, 1780)."""
+    from geobpe.rmsd_bpe import RES_SPHERE_KEY
+    res = set(RES_SPHERE_KEY.values())
+    return [k for k in getattr(bpe, "_sphere_dict", {}) if k not in res]
 
 
 def latest_checkpoint(save_dir: str):
@@ -179,9 +190,6 @@ def main(argv=None) -> int:
 
     from geobpe.bpe import BPE
     rmsd_mode = args.p_min_size != float("inf")
-    if rmsd_mode and args.ckpt_format == "pkl":
-        raise SystemExit("--p-min-size < inf (the RMSD-partitioned mode) writes --ckpt-format json checkpoints; "
-                         "its bpe_iter=*.pkl form is not built")
     corpus = load_corpus(args.data_dir, args.toy)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     group, rank, shard, device = None, 0, corpus, args.device
@@ -217,12 +225,14 @@ def main(argv=None) -> int:
     start, ck, keys = latest_checkpoint(args.save_dir)
     if ck is not None:  # resume: re-run the saved number of merges, then check them against the file
         if rmsd_mode:  # a step() may merge more than once there (recurring keys, bpe.py:2164-2166)
-            while len(bpe.merges) < len(keys) and bpe.run(1):
+            got = (lambda: rmsd_merge_keys(bpe)) if ck.endswith(".pkl") else (lambda: [m[0] for m in bpe.merges])
+            while len(got()) < len(keys) and bpe.run(1):
                 pass
-            done = len(bpe.merges)
+            merged = got()
         else:
-            done = bpe.run(len(keys))
-        if [m[0] for m in bpe.merges] != keys or done != len(keys):
+            bpe.run(len(keys))
+            merged = [m[0] for m in bpe.merges]
+        if merged != keys:
             raise SystemExit(f"replay of {ck} diverged from the saved merge list")
         log.info("resumed from %s at iter=%d", ck, start)
 

@@ -83,7 +83,7 @@ class _Chain:
     DIHEDRALS[d%3] row (d+1)//3.  The init values are shared by both copies (the
     reference's ``orig`` flag only switches the DataFrame)."""
 
-    __slots__ = ("cur", "orig", "init", "n", "token_pos", "btt", "fname")
+    __slots__ = ("cur", "orig", "init", "n", "token_pos", "btt", "fname", "tokens0", "events")
 
     def __init__(self, cols: dict, init, fname=None):
         # Python lists: the host bookkeeping reads and writes single values (the
@@ -95,6 +95,8 @@ class _Chain:
         self.token_pos = []
         self.btt = {}
         self.fname = fname
+        self.tokens0 = []  # Tokenizer.tokens: the initial tokens (step() never updates them, bpe.py:1955-1965)
+        self.events = []   # merge tree: (left start, right start, parent value) per merge (data_structures.py:32-60)
 
     def _bond(self, j, src):
         return self.init[j] if j < 2 else src[BOND_TYPES[j % 3]][(j - 2) // 3]
@@ -401,6 +403,8 @@ class RmsdBPE:
             self._tokens = {}
             for n, size in enumerate(res_geo):
                 self._partition_residues(n, size, res_geo[size])
+        for c in self._chains:
+            c.tokens0 = list(c.btt.values())
         for c in self._chains:  # glue angles -> grid-1 bin centres, NaN kept (bpe.py:381-391)
             for k in GLUE:
                 col = c.cur[k]
@@ -487,6 +491,7 @@ class RmsdBPE:
             toks = c.tokens()
             for (i1, _, l1), (i2, _, l2) in zip(toks, toks[1:]):
                 self._geo_dict[self._pair_key(ci, i1, l1, l2)].add((ci, i2))
+        self._geo_step = {k: 0 for k in self._geo_dict}
         self._priority = SortedList()
         self._key_to_priority = {}
         for key, occ in self._geo_dict.items():
@@ -608,6 +613,7 @@ class RmsdBPE:
                 tp[j] = i1
             c.btt.pop(i2)
             c.btt[i1] = (i1, (n, assign[idx]) if rmsd else n, length)
+            c.events.append((i1, i2, c.btt[i1]))
             if rmsd:
                 c.set_geo(i1, length, self._sphere_dict[key][assign[idx]])
             if left:
@@ -822,9 +828,120 @@ class RmsdBPE:
         from .bpe import BPE
         return BPE.capacity(self, tokenizer)
 
+    # ------------------------------------------------------------ checkpoints
+    def checkpoint_object(self):
+        """The reference's BPE object graph of this run (what bin/encode.py pickles,
+        bpe.py:33-88 + the RMSD mode's _sphere_dict): tokenizers with their current and
+        original frames, init triple, initial tokens, token_pos and bond_to_token holding the
+        merge tree; _tokens, _sphere_dict, _geo_dict, _priority_dict, _key_to_priority,
+        _geo_step, the per-grid thresholds / bin counts / centres / weights, and the rng in
+        its current state -- so the reference resumes this run (tests/test_rmsd_mode.py)."""
+        import pandas as pd
+        import torch
+        from sortedcontainers import SortedDict
+
+        from . import refpickle as R
+        C = R._real_or_local()
+        toks = []
+        for c in self._chains:
+            tok = R._new(C["Tokenizer"], {})
+            nodes = {v[0]: R._new(C["Node"], {"value": v, "left": None, "right": None}) for v in c.tokens0}
+            leaves = {v[0]: R._new(C["Node"], {"value": v, "left": None, "right": None}) for v in c.tokens0}
+            for a, b, v in c.events:  # BinaryTreeBuilder.combine
+                left, right = nodes.pop(a), nodes.pop(b)
+                nodes[v[0]] = R._new(C["Node"], {"value": v, "left": left, "right": right})
+            tree = R._new(C["BinaryTreeBuilder"], {"nodes": nodes, "leaves": leaves})
+            hier = R._new_dict(C["TokenHierarchy"], list(c.btt.items()), {"parent": tok, "tree": tree})
+            n = c.n
+            cur = {k: list(c.cur[k]) for k in COLUMNS}
+            cur_dt = {k: (np.float64 if k in GLUE else object) for k in COLUMNS}  # bpe.py:388 re-assigns the glue columns
+            idxes = sum([[i, i, i] for i in range(1, n + 1)], [])
+            tok.__dict__.update({
+                "_angles_and_dists": R._frame(pd, cur, cur_dt),
+                "_angles_and_dists_orig": R._frame(pd, {k: list(c.orig[k]) for k in COLUMNS}, {k: object for k in COLUMNS}),
+                "_coords": None, "beta_coords": None, "_idxes": idxes,
+                "_res_idx_map": dict(zip(idxes[0::3], range(0, len(idxes), 3))), "_full_coords": None,
+                "compute_sec_structs": False, "_sec": None, "_side_chains": None, "aa": None, "fname": c.fname,
+                "n": n, "bond_labels": sum([[0, 1, 2] for _ in range(n - 1)] + [[0, 1]], []),
+                "atom_labels": np.tile([0, 1, 2], n), "edges": [[j, j + 1, 0] for j in range(1, 3 * n)],
+                "_bond_to_token": hier, "_init_n_ca": c.init[0], "_init_ca_c": c.init[1],
+                "_init_bond_angle": c.init[2], "token_pos": list(c.token_pos), "tokens": list(c.tokens0),
+            })
+            toks.append(tok)
+
+        sizes = sorted(k for k in self.bins)
+        thr = R._new_dict(C["ThresholdDict"], [(k, v) for k, v in self._thresholds.items()], {"_int_keys": sizes})
+        counts = self._bin_count_values()
+        mk = lambda items: R._new_dict(C["ThresholdDict"], items, {"_int_keys": sizes})  # noqa: E731
+        bin_counts = mk([(s0, counts[s0]) for s0 in sizes])
+        centers = mk([(s0, {k: torch.tensor(v, dtype=torch.float32).mean(axis=-1)
+                            for k, v in self._grid_only(s0).items()}) for s0 in sizes])
+        weights = mk([(s0, {k: torch.tensor(v, dtype=torch.float32) / sum(v) for k, v in counts[s0].items()})
+                      for s0 in sizes])
+        nump = self.num_partitions
+        if isinstance(nump, dict):
+            nump = R._new_dict(C["ThresholdDict"], list(dict.items(nump)),
+                               {"_int_keys": sorted(k for k in nump if isinstance(k, int))})
+        attrs = {
+            "tokenizers": toks, "compute_sec_structs": self.compute_sec_structs,
+            "plot_iou_with_sec_structs": self.plot_iou_with_sec_structs,
+            "rmsd_partition_min_size": self.rmsd_partition_min_size, "rmsd_super_res": self.rmsd_super_res,
+            "rmsd_only": self.rmsd_only, "glue_opt": self.glue_opt, "glue_opt_every": self.glue_opt_every,
+            "glue_opt_prior": self.glue_opt_prior, "glue_opt_method": self.glue_opt_method, "num_partitions": nump,
+            "max_num_strucs": self.max_num_strucs, "res_init": self.res_init, "std_bonds": self.std_bonds,
+            "bins": dict(self.bins), "bin_strategy": self.bin_strategy, "n": self.n, "seed": self.seed,
+            "rng": self.rng, "save_dir": self.save_dir, "_step": self._step, "_times": list(self._times),
+            "_ious": [], "_thresholds": thr, "_bin_counts": bin_counts, "_bin_centers": centers,
+            "_bin_weights": weights, "_tokens": dict(self._tokens),
+        }
+        if hasattr(self, "_sphere_dict"):
+            attrs["_sphere_dict"] = self._sphere_dict
+        if hasattr(self, "_geo_dict"):
+            attrs.update({"_geo_dict": self._geo_dict, "_priority_dict": SortedDict({p: None for p in self._priority}),
+                          "_key_to_priority": self._key_to_priority, "_geo_step": self._geo_step,
+                          "_sphere_keys": {}})
+        return R._new(C["BPE"], attrs)
+
+    def _grid_only(self, size):
+        return {k: v for k, v in self._thresholds[size].items()}
+
+    def _bin_count_values(self):
+        """_bin_counts per grid (bpe.py:841-867): np.histogram counts of the values the
+        thresholds came from (angles wrapped to [0, 2pi), tau with every chain's init angle;
+        bond lengths too with free bonds)."""
+        ro = self._corpus["row_off"]
+        n_ca, ca_c, tau0 = _rmsd.init_geometry()
+        keys = BOND_ANGLES + DIHEDRALS + ([] if self.std_bonds else BOND_TYPES)
+        vals = {}
+        for k in keys:
+            col = np.asarray(self._corpus[k], dtype=np.float64)
+            v = col[np.nan_to_num(col, nan=0.0) != 0.0]
+            extra = {"tau": tau0, "N:CA": n_ca, "CA:C": ca_c}.get(k)
+            if extra is not None:
+                v = np.concatenate([v, np.full(len(ro) - 1, extra)])
+            vals[k] = v if k in BOND_TYPES else (v + TWO_PI) % TWO_PI
+        out = {}
+        for s0, b in self.bins.items():
+            out[s0] = {}
+            for k in keys:
+                if self.bin_strategy.startswith("histogram"):
+                    rng_ = (0, TWO_PI) if "cover" in self.bin_strategy and k not in BOND_TYPES else None
+                    cnt = np.histogram(vals[k], bins=int(b), range=rng_)[0]
+                else:
+                    edges = [a for a, _ in self._thresholds[s0][k]] + [self._thresholds[s0][k][-1][1]]
+                    cnt = np.histogram(vals[k], bins=np.array(edges))[0]
+                out[s0][k] = [np.int64(x) for x in cnt]
+        return out
+
     def save_checkpoint(self, path: str) -> None:
-        raise NotImplementedError("bpe_iter=*.pkl checkpoints of the RMSD mode (tuple token ids, "
-                                  "_sphere_dict) are not built; use --ckpt-format json")
+        """``bpe_iter=t.pkl`` in the reference's format (bin/encode.py:427), written atomically."""
+        import os
+
+        from . import refpickle as R
+        tmp = path + ".tmp"
+        with open(tmp, "wb") as f:
+            R.dump(self.checkpoint_object(), f)
+        os.replace(tmp, path)
 
     def geometry(self):
         """Every chain's current 9 columns, concatenated (the reference's DataFrames)."""

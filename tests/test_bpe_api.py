@@ -176,22 +176,30 @@ def test_cli_resume_reproduces_one_shot(tmp_path):
 
 @pytest.mark.gpu
 def test_cli_rmsd_mode_resume_reproduces_one_shot(tmp_path):
-    """bin/encode.py in the RMSD-partitioned mode (--p-min-size 0, --num-p, json
-    checkpoints): a run resumed at iter 10 ends with the one-shot run's merges and stats."""
+    """bin/encode.py in the RMSD-partitioned mode (--p-min-size 0, --num-p): a run resumed
+    at iter 10 ends with the one-shot run's merges and stats, with json checkpoints and with
+    bpe_iter=*.pkl (the reference's pickle of this mode: segmentation and geometry too)."""
+    from geobpe import refpickle
     cli = _encode_cli()
-    common = ["--data-dir", "synthetic:40:20:60:9", "--bins", "1-5", "--save-every", "5", "--p-min-size", "0",
-              "--num-p", "2-2:3-3:5-2", "--max-num-strucs", "60", "--rmsd-super-res", "true",
-              "--ckpt-format", "json", "--log-dir", str(tmp_path / "logs")]
-    one, two = tmp_path / "one", tmp_path / "two"
-    assert cli.main(common + ["--save-dir", str(one), "--max-iter", "21"]) == 0
-    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "11"]) == 0
-    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "21"]) == 0  # resumes at 10
-    a = json.loads((one / "bpe_iter=20.json").read_text())["merges"]
-    b = json.loads((two / "bpe_iter=20.json").read_text())["merges"]
-    assert a == b and len(a) >= 20
-    assert json.loads((one / "stats=20.json").read_text()) == json.loads((two / "stats=20.json").read_text())
-    with pytest.raises(SystemExit):  # pickle checkpoints of this mode are not built
-        cli.main(common[:-4] + ["--log-dir", str(tmp_path / "logs"), "--save-dir", str(tmp_path / "x")])
+    for fmt in ("json", "pkl"):
+        common = ["--data-dir", "synthetic:40:20:60:9", "--bins", "1-5", "--save-every", "5", "--p-min-size", "0",
+                  "--num-p", "2-2:3-3:5-2", "--max-num-strucs", "60", "--rmsd-super-res", "true",
+                  "--ckpt-format", fmt, "--log-dir", str(tmp_path / "logs")]
+        one, two = tmp_path / f"one_{fmt}", tmp_path / f"two_{fmt}"
+        assert cli.main(common + ["--save-dir", str(one), "--max-iter", "21"]) == 0
+        assert cli.main(common + ["--save-dir", str(two), "--max-iter", "11"]) == 0
+        assert cli.main(common + ["--save-dir", str(two), "--max-iter", "21"]) == 0  # resumes at 10
+        if fmt == "json":
+            a = json.loads((one / "bpe_iter=20.json").read_text())["merges"]
+            b = json.loads((two / "bpe_iter=20.json").read_text())["merges"]
+            assert a == b and len(a) >= 20
+        else:
+            a, b = refpickle.load(str(one / "bpe_iter=20.pkl")), refpickle.load(str(two / "bpe_iter=20.pkl"))
+            assert list(a._sphere_dict) == list(b._sphere_dict) and a._step == b._step >= 20
+            for ta, tb in zip(a.tokenizers, b.tokenizers):
+                assert dict(ta._bond_to_token) == dict(tb._bond_to_token)
+                assert ta._angles_and_dists.equals(tb._angles_and_dists)
+        assert json.loads((one / "stats=20.json").read_text()) == json.loads((two / "stats=20.json").read_text())
 
 
 @pytest.mark.gpu

@@ -162,3 +162,101 @@ def test_rmsd_mode_device_matches_reference(name):
     bpe = run_and_compare(name)
     if name not in ("rm_p4", "rm_p3_freebonds"):
         assert bpe.assign_calls > 0  # the device RMSD batches ran
+
+
+REF_RESUME = r'''
+import sys, json, pickle, tempfile
+import numpy as np
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import make_golden as MG
+MG._stub_optional_deps()
+sys.path.insert(0, "/root/reference")
+import foldingdiff.bpe as B
+from foldingdiff.tokenizer import Tokenizer
+from geobpe import synth
+B.BPE.visualize = lambda self, key, path: None
+Tokenizer.visualize_bonds = lambda self, *a, **k: None
+popped = []
+inner = B.BPE.step
+def rec(self):
+    top = self._priority_dict.peekitem(0)[0]
+    popped.append([bool(top[0]), int(top[1]), top[2]])
+    return inner(self)
+B.BPE.step = rec
+def tid(v):
+    return [int(x) for x in v] if isinstance(v, tuple) else int(v)
+def resume(bpe, n):
+    calls = []
+    for _ in range(n):
+        n0 = len(popped)
+        bpe.step()
+        calls.append({"popped": popped[n0:], "step": bpe._step, "n_tokens": len(bpe._tokens)})
+    return {"calls": calls,
+            "segmentation": [[[int(s), tid(v[1]), int(v[2])] for s, v in t.bond_to_token.items()] for t in bpe.tokenizers],
+            "quantize": [[int(x) for x in bpe.quantize(t)] for t in bpe.tokenizers], "vocab_size": bpe.vocab_size}
+name, k, rest = sys.argv[4], int(sys.argv[5]), int(sys.argv[6])
+m = json.load(open(f"{sys.argv[2]}/{name}.json"))
+z = np.load(f"{sys.argv[2]}/{name}.npz")
+corpus = {c: z[c] for c in synth.COLUMNS + ["row_off"]}
+structs = []
+for i, row in enumerate(synth.corpus_rows(corpus)):
+    s = Tokenizer.init_structure(len(row["phi"]))
+    for c in synth.COLUMNS:
+        s["angles"][c] = row[c].astype(np.float64)
+    s["fname"] = f"synthetic_{i}"
+    structs.append(s)
+ref = B.BPE(structs, bins={int(a): b for a, b in m["bins"].items()}, save_dir=tempfile.mkdtemp(),
+            rmsd_partition_min_size=m["rmsd_partition_min_size"], rmsd_super_res=m["rmsd_super_res"],
+            num_partitions={int(a): b for a, b in m["num_partitions"].items()}, max_num_strucs=m["max_num_strucs"],
+            res_init=True, std_bonds=m.get("std_bonds", True), seed=0)
+ref.initialize()
+ref.bin()
+for _ in range(k):
+    ref.step()
+own = resume(pickle.loads(pickle.dumps(ref)), rest)   # the reference resuming its own checkpoint
+ours = resume(pickle.load(open(sys.argv[3], "rb")), rest)
+print("JSON" + json.dumps({"own": own, "ours": ours}))
+'''
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/foldingdiff"), reason="reference not present (GPU box)")
+@pytest.mark.parametrize("name", ["rm_p0", "rm_p0_multigrid", "rm_p0_super"])
+def test_reference_resumes_rmsd_mode_checkpoint(name, host_geometry, tmp_path):
+    """bpe_iter=*.pkl of the RMSD mode: the reference unpickles this build's checkpoint
+    taken after 10 step() calls and keeps training.  Its merges, segmentation, quantize ids
+    and vocab size equal those of the reference resuming its OWN checkpoint of the same
+    point.  (A pickle round trip rebuilds every _geo_dict set, and the order a rebuilt set
+    iterates in is what k-medoids sees, bpe.py:1744: with rmsd_super_res or multi-grid
+    keys the resumed run can leave the uninterrupted one -- the reference's own resume
+    does too.  Where every occurrence of a key is congruent, rm_p0, it also equals the
+    uninterrupted run.)"""
+    import subprocess
+    import sys
+    from conftest import REPO
+    from geobpe.bpe import BPE
+    meta, corpus, _ = _load(name)
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()},
+              rmsd_partition_min_size=meta["rmsd_partition_min_size"], rmsd_super_res=meta["rmsd_super_res"],
+              num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta.get("std_bonds", True),
+              seed=meta["rng_seed"])
+    bpe.initialize()
+    bpe.bin()
+    k = 10
+    for _ in range(k):
+        bpe.step()
+    p = str(tmp_path / f"bpe_iter={k}.pkl")
+    bpe.save_checkpoint(p)
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg", SLURM_CPUS_PER_TASK="2",
+               PYTHONBREAKPOINT="0")
+    rest = len(meta["calls"]) - k
+    r = subprocess.run([sys.executable, "-W", "ignore", "-c", REF_RESUME, os.path.join(REPO, "pt-bpe_amd"),
+                        os.path.join(REPO, "tests", "golden"), p, name, str(k), str(rest)], env=env,
+                       capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("JSON")][-1][4:])
+    assert out["ours"] == out["own"]
+    assert out["ours"]["calls"] == meta["calls"][k:]
+    if name == "rm_p0":
+        assert out["ours"]["segmentation"] == meta["segmentation"]
+        assert out["ours"]["quantize"] == meta["quantize"]
