@@ -15,6 +15,11 @@ side of the reference's ``bin/induce.py`` (flags :34-51, main :141-239).
     ``n`` turned into a list, induce.py:230-239).
 Chains with a residue geometry outside the trained vocabulary, or values outside
 the trained histogram range, raise ValueError (get_ind, bpe.py:1164-1189).
+
+A checkpoint of the RMSD-partitioned mode (it holds ``_sphere_dict``) is induced the
+reference's way instead: ``BPE.tokenize`` of every chain (bpe.py:1053-1140, here
+geobpe.rmsd_bpe.RmsdBPE.tokenize on device NeRF / RMSD batches), then the same
+utility.json and output pickle (induce.py:216-239).
 """
 from __future__ import annotations
 
@@ -82,6 +87,8 @@ def main(argv=None) -> int:
             g.write(f.read())
 
     bpe = refpickle.load(args.src_pkl)
+    if getattr(bpe, "_sphere_dict", None) is not None:
+        return induce_rmsd(args, bpe, save_dir)
     B = int(bpe.bins[1])
     thr = {k: [tuple(p) for p in v] for k, v in bpe._thresholds[1].items()}
     corpus = load_corpus(args.data_dir, args.toy)
@@ -114,6 +121,48 @@ def main(argv=None) -> int:
         refpickle.dump(bpe, f)
     os.replace(tmp, out_path)
     print(json.dumps({"out": os.path.abspath(out_path), "chains": nrows, "tokens": int(len(ids)),
+                      "seconds": round(time.time() - t0, 3)} | utility))
+    return 0
+
+
+def induce_rmsd(args, obj, save_dir: str) -> int:
+    """RMSD mode: the trained state from the checkpoint, BPE.tokenize per chain, the
+    utility of quantize(t.tokenize()) over all chains, the output pickle."""
+    from geobpe import refpickle
+    from geobpe.bpe import get_codebook_utility
+    from geobpe.rmsd_bpe import RmsdBPE
+    from geobpe.synth import COLUMNS
+    from encode import load_corpus
+
+    corpus = load_corpus(args.data_dir, args.toy)
+    bpe = RmsdBPE.from_checkpoint(obj, device=args.device)
+    t0 = time.time()
+    ro = corpus["row_off"]
+    fnames = corpus.get("fnames")
+    toks, ids, ntok = [], [], 0
+    for i in range(len(ro) - 1):
+        struct = {"angles": {c: corpus[c][ro[i]:ro[i + 1]] for c in COLUMNS},
+                  "fname": fnames[i] if fnames is not None else f"{args.data_dir}#{i}"}
+        t, _ = bpe.tokenize(struct)
+        ids.append(bpe.quantize(t))
+        ntok += len(t.bond_to_token)
+        toks.append(RmsdBPE.tokenizer_record(t))
+    utility = get_codebook_utility(np.array([x for q in ids for x in q], dtype=np.int64), bpe.vocab_size)
+    with open(os.path.join(save_dir, "utility.json"), "w") as f:
+        json.dump(utility, f)
+    if args.append:
+        if not isinstance(obj.n, list):
+            obj.n = [obj.n]
+        obj.n.append(len(toks))
+        obj.tokenizers.extend(toks)
+    else:
+        obj.tokenizers = toks
+    out_path = os.path.join(save_dir, os.path.basename(args.src_pkl))
+    tmp = out_path + ".tmp"
+    with open(tmp, "wb") as f:
+        refpickle.dump(obj, f)
+    os.replace(tmp, out_path)
+    print(json.dumps({"out": os.path.abspath(out_path), "chains": len(toks), "tokens": ntok,
                       "seconds": round(time.time() - t0, 3)} | utility))
     return 0
 

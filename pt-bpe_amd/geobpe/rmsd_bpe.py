@@ -715,6 +715,7 @@ class RmsdBPE:
             for s0, p in zip(starts, assign):
                 c.set_geo(s0, size, self._tokens[(n, p)])
                 c.btt[s0] = (s0, (n, p), size)
+        c.tokens0 = list(c.btt.values())
         for k in GLUE:  # grid-1 glue centres, NaN kept (bpe.py:1101-1108)
             col = c.cur[k]
             for r in range(c.n):
@@ -779,6 +780,7 @@ class RmsdBPE:
                 tp[j] = i1
             c.btt.pop(i2)
             c.btt[i1] = (i1, (n, assign[idx]), length)
+            c.events.append((i1, i2, c.btt[i1]))
             c.set_geo(i1, length, self._sphere_dict[key][assign[idx]])
             if left:
                 geo_dict[self._pair_key(c, i0, l0, length)].add(i1)
@@ -842,33 +844,49 @@ class RmsdBPE:
 
         from . import refpickle as R
         C = R._real_or_local()
-        toks = []
-        for c in self._chains:
-            tok = R._new(C["Tokenizer"], {})
-            nodes = {v[0]: R._new(C["Node"], {"value": v, "left": None, "right": None}) for v in c.tokens0}
-            leaves = {v[0]: R._new(C["Node"], {"value": v, "left": None, "right": None}) for v in c.tokens0}
-            for a, b, v in c.events:  # BinaryTreeBuilder.combine
-                left, right = nodes.pop(a), nodes.pop(b)
-                nodes[v[0]] = R._new(C["Node"], {"value": v, "left": left, "right": right})
-            tree = R._new(C["BinaryTreeBuilder"], {"nodes": nodes, "leaves": leaves})
-            hier = R._new_dict(C["TokenHierarchy"], list(c.btt.items()), {"parent": tok, "tree": tree})
-            n = c.n
-            cur = {k: list(c.cur[k]) for k in COLUMNS}
-            cur_dt = {k: (np.float64 if k in GLUE else object) for k in COLUMNS}  # bpe.py:388 re-assigns the glue columns
-            idxes = sum([[i, i, i] for i in range(1, n + 1)], [])
-            tok.__dict__.update({
-                "_angles_and_dists": R._frame(pd, cur, cur_dt),
-                "_angles_and_dists_orig": R._frame(pd, {k: list(c.orig[k]) for k in COLUMNS}, {k: object for k in COLUMNS}),
-                "_coords": None, "beta_coords": None, "_idxes": idxes,
-                "_res_idx_map": dict(zip(idxes[0::3], range(0, len(idxes), 3))), "_full_coords": None,
-                "compute_sec_structs": False, "_sec": None, "_side_chains": None, "aa": None, "fname": c.fname,
-                "n": n, "bond_labels": sum([[0, 1, 2] for _ in range(n - 1)] + [[0, 1]], []),
-                "atom_labels": np.tile([0, 1, 2], n), "edges": [[j, j + 1, 0] for j in range(1, 3 * n)],
-                "_bond_to_token": hier, "_init_n_ca": c.init[0], "_init_ca_c": c.init[1],
-                "_init_bond_angle": c.init[2], "token_pos": list(c.token_pos), "tokens": list(c.tokens0),
-            })
-            toks.append(tok)
+        toks = [self.tokenizer_record(c, C) for c in self._chains]
+        return self._bpe_record(toks, C)
 
+    @staticmethod
+    def tokenizer_record(c, C=None):
+        """The reference Tokenizer object of one chain (tokenizer.py:24-61 attributes, the
+        frames, bond_to_token with the merge tree)."""
+        import pandas as pd
+
+        from . import refpickle as R
+        if isinstance(c, RmsdTokenizer):
+            c = c._c
+        C = C or R._real_or_local()
+        tok = R._new(C["Tokenizer"], {})
+        nodes = {v[0]: R._new(C["Node"], {"value": v, "left": None, "right": None}) for v in c.tokens0}
+        leaves = {v[0]: R._new(C["Node"], {"value": v, "left": None, "right": None}) for v in c.tokens0}
+        for a, b, v in c.events:  # BinaryTreeBuilder.combine
+            left, right = nodes.pop(a), nodes.pop(b)
+            nodes[v[0]] = R._new(C["Node"], {"value": v, "left": left, "right": right})
+        tree = R._new(C["BinaryTreeBuilder"], {"nodes": nodes, "leaves": leaves})
+        hier = R._new_dict(C["TokenHierarchy"], list(c.btt.items()), {"parent": tok, "tree": tree})
+        n = c.n
+        cur = {k: list(c.cur[k]) for k in COLUMNS}
+        cur_dt = {k: (np.float64 if k in GLUE else object) for k in COLUMNS}  # bpe.py:388 re-assigns the glue columns
+        idxes = sum([[i, i, i] for i in range(1, n + 1)], [])
+        tok.__dict__.update({
+            "_angles_and_dists": R._frame(pd, cur, cur_dt),
+            "_angles_and_dists_orig": R._frame(pd, {k: list(c.orig[k]) for k in COLUMNS}, {k: object for k in COLUMNS}),
+            "_coords": None, "beta_coords": None, "_idxes": idxes,
+            "_res_idx_map": dict(zip(idxes[0::3], range(0, len(idxes), 3))), "_full_coords": None,
+            "compute_sec_structs": False, "_sec": None, "_side_chains": None, "aa": None, "fname": c.fname,
+            "n": n, "bond_labels": sum([[0, 1, 2] for _ in range(n - 1)] + [[0, 1]], []),
+            "atom_labels": np.tile([0, 1, 2], n), "edges": [[j, j + 1, 0] for j in range(1, 3 * n)],
+            "_bond_to_token": hier, "_init_n_ca": c.init[0], "_init_ca_c": c.init[1],
+            "_init_bond_angle": c.init[2], "token_pos": list(c.token_pos), "tokens": list(c.tokens0),
+        })
+        return tok
+
+    def _bpe_record(self, toks, C):
+        import torch
+        from sortedcontainers import SortedDict
+
+        from . import refpickle as R
         sizes = sorted(k for k in self.bins)
         thr = R._new_dict(C["ThresholdDict"], [(k, v) for k, v in self._thresholds.items()], {"_int_keys": sizes})
         counts = self._bin_count_values()
@@ -901,6 +919,36 @@ class RmsdBPE:
                           "_key_to_priority": self._key_to_priority, "_geo_step": self._geo_step,
                           "_sphere_keys": {}})
         return R._new(C["BPE"], attrs)
+
+    @classmethod
+    def from_checkpoint(cls, obj, device: int = 0):
+        """The trained state tokenize() needs, from a checkpoint of this mode (this build's or
+        the reference's, read by geobpe.refpickle.load): settings, _thresholds, _tokens,
+        _sphere_dict.  bin/induce.py's RMSD-mode path."""
+        from .bpe import ThresholdDict
+        self = cls.__new__(cls)
+        self.bins = dict(obj.bins)
+        self.B = int(self.bins[1])
+        for k in ("bin_strategy", "res_init", "std_bonds", "rmsd_partition_min_size", "rmsd_super_res",
+                  "rmsd_only", "glue_opt", "glue_opt_method", "glue_opt_every", "glue_opt_prior",
+                  "max_num_strucs", "seed", "save_dir", "compute_sec_structs", "plot_iou_with_sec_structs"):
+            setattr(self, k, getattr(obj, k, None))
+        self.rmsd_super_res = bool(self.rmsd_super_res)
+        self.std_bonds = True if self.std_bonds is None else bool(self.std_bonds)
+        if self.glue_opt or self.rmsd_only:
+            raise NotImplementedError("checkpoints trained with glue_opt / rmsd_only")
+        thr = ThresholdDict()
+        for k, v in dict.items(obj._thresholds):
+            thr[k] = v
+        self._thresholds = thr
+        self._thr_by_len = {}
+        self._tokens = dict(obj._tokens)
+        self._sphere_dict = dict(obj._sphere_dict)
+        self.num_partitions = getattr(obj, "num_partitions", 3)
+        self.device = int(device)
+        self.assign_calls = 0
+        self._chains, self._times, self._merge_log, self._step = [], [], [], int(getattr(obj, "_step", 0))
+        return self
 
     def _grid_only(self, size):
         return {k: v for k, v in self._thresholds[size].items()}

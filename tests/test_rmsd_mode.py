@@ -260,3 +260,46 @@ def test_reference_resumes_rmsd_mode_checkpoint(name, host_geometry, tmp_path):
     if name == "rm_p0":
         assert out["ours"]["segmentation"] == meta["segmentation"]
         assert out["ours"]["quantize"] == meta["quantize"]
+
+
+@pytest.mark.parametrize("name", ["rm_p0_super", "rm_p2_super_b3"])
+def test_induce_cli_rmsd_mode(name, host_geometry, tmp_path):
+    """bin/induce.py on a checkpoint of the RMSD mode: the trained run (this build) is
+    saved as bpe_iter=*.pkl, the CLI tokenizes the fixture's held-out chains (those the
+    reference tokenized without error), and the output pickle's tokenizers carry the
+    reference's segmentation of each."""
+    import importlib.util
+    from conftest import REPO
+    from geobpe import refpickle, synth
+    from geobpe.bpe import BPE
+    meta, corpus, arrs = _load(name)
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()},
+              rmsd_partition_min_size=meta["rmsd_partition_min_size"], rmsd_super_res=meta["rmsd_super_res"],
+              num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta.get("std_bonds", True),
+              seed=meta["rng_seed"])
+    bpe.initialize()
+    bpe.bin()
+    for _ in meta["calls"]:
+        bpe.step()
+    src = tmp_path / "train" / f"bpe_iter={len(meta['calls'])}.pkl"
+    src.parent.mkdir()
+    bpe.save_checkpoint(str(src))
+    ok = [i for i, w in enumerate(meta["induce"]) if "raised" not in w]
+    ro = arrs["new_row_off"]
+    rows = [{c: arrs[f"new_{c}"][ro[i]:ro[i + 1]] for c in COLS} for i in ok]
+    new = {c: np.concatenate([r[c] for r in rows]) for c in COLS}
+    new["row_off"] = np.concatenate([[0], np.cumsum([len(r["phi"]) for r in rows])]).astype(np.int64)
+    synth.save_corpus(str(tmp_path / "new.npz"), new)
+    spec = importlib.util.spec_from_file_location("geobpe_induce_cli", os.path.join(REPO, "pt-bpe_amd", "bin", "induce.py"))
+    cli = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(cli)
+    out = tmp_path / "out"
+    assert cli.main(["--src-pkl", str(src), "--data-dir", str(tmp_path / "new.npz"), "--save-dir", str(out),
+                     "--log-dir", str(tmp_path / "logs")]) == 0
+    obj = refpickle.load(str(out / src.name))
+    assert len(obj.tokenizers) == len(ok)
+    for t, i in zip(obj.tokenizers, ok):
+        got = [[s0, list(v[1]) if isinstance(v[1], tuple) else v[1], v[2]] for s0, v in t._bond_to_token.items()]
+        assert got == meta["induce"][i]["segmentation"]
+    assert (out / "utility.json").exists()
