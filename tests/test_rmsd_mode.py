@@ -264,6 +264,16 @@ def test_reference_resumes_rmsd_mode_checkpoint(name, host_geometry, tmp_path):
 
 @pytest.mark.parametrize("name", ["rm_p0_super", "rm_p2_super_b3"])
 def test_induce_cli_rmsd_mode(name, host_geometry, tmp_path):
+    _induce_cli(name, tmp_path)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["rm_p0_super", "rm_p2_super_b3", "rm_pdb72_readme"])
+def test_induce_cli_rmsd_mode_device(name, tmp_path):
+    _induce_cli(name, tmp_path)
+
+
+def _induce_cli(name, tmp_path):
     """bin/induce.py on a checkpoint of the RMSD mode: the trained run (this build) is
     saved as bpe_iter=*.pkl, the CLI tokenizes the fixture's held-out chains (those the
     reference tokenized without error), and the output pickle's tokenizers carry the
