@@ -52,6 +52,10 @@ STD_LENGTH = {"N:CA": 1.46, "CA:C": 1.54, "0C:1N": 1.34}       # nerf.py:17-19
 GLUE = ["omega", "C:1N:1CA", "phi"]                            # bpe.py:383
 TWO_PI = 2 * np.pi
 # the residue-level partition keys of _sphere_dict (bpe.py:333-338)
+# item type -> (position of its first item in a residue, kind: 0 bond, 1 angle, 2 dihedral)
+_ITEM = {k: (i, 0) for i, k in enumerate(BOND_TYPES)} | {k: (i, 1) for i, k in enumerate(BOND_ANGLES)} | \
+    {k: (i, 2) for i, k in enumerate(DIHEDRALS)}
+_ENC = json.JSONEncoder(sort_keys=True)  # json.dumps(geo, sort_keys=True) (bpe.py:1147-1149)
 RES_SPHERE_KEY = {3: '{"N:CA": [0], "CA:C": [0], "0C:1N": [0], "tau": [0], "CA:C:1N": [0], "psi": [0]}',
                   2: '{"CA:C": [0], "0C:1N": [0], "CA:C:1N": [0]}'}
 
@@ -362,12 +366,15 @@ class RmsdBPE:
     def _init_residues(self):
         p = self.rmsd_partition_min_size
         for c in self._chains:  # every bond -> its bin centre (bpe.py:714-737)
-            for j in range(3 * c.n - 1):
+            if self.std_bonds:  # bonds 0, 1 (the init lengths) and rows 0..n-2 of the three columns
+                std = {bt: sum(self._thresholds[bt][0]) / 2 for bt in BOND_TYPES}
+                c.init[0], c.init[1] = std["N:CA"], std["CA:C"]
+                for bt in BOND_TYPES:
+                    c.cur[bt][:max(c.n - 1, 0)] = [std[bt]] * max(c.n - 1, 0)
+                continue
+            for j in range(3 * c.n - 1):  # free bonds: grid 1's bin of the length (strict get_ind, bpe.py:731)
                 bt = BOND_TYPES[j % 3]
-                if self.std_bonds:
-                    v = sum(self._thresholds[bt][0]) / 2
-                else:  # grid 1's bin of the length (strict get_ind, bpe.py:731)
-                    v = self._centre(bt, _get_ind(c.geo(j, 1)[bt][0], self._thresholds[1][bt]), 1)
+                v = self._centre(bt, _get_ind(c.geo(j, 1)[bt][0], self._thresholds[1][bt]), 1)
                 c.set_geo(j, 1, {bt: [v]})
         label_dict, res_geo, labels = {}, {}, []
         for ci, c in enumerate(self._chains):
@@ -465,32 +472,37 @@ class RmsdBPE:
         else:
             rng = ((0, L), (0, L), (0, L))
         for k, vals in geo.items():
-            if k in BOND_TYPES:
-                base, kind, thr = (BOND_TYPES.index(k) + 3 - ph) % 3, 0, (thr_all[k] if self.std_bonds else thr_L[k])
-            elif k in BOND_ANGLES:
-                base, kind, thr = (BOND_ANGLES.index(k) + 3 - ph) % 3, 1, thr_L[k]
-            else:
-                base, kind, thr = (DIHEDRALS.index(k) + 3 - ph) % 3, 2, thr_L[k]
+            t0, kind = _ITEM[k]
             lo, hi = rng[kind]
+            if lo >= hi:
+                continue
+            base = (t0 + 3 - ph) % 3
             m_lo = max(0, -((base - lo) // 3))      # first m with base + 3m >= lo
             m_hi = min(len(vals), -((base - hi) // 3))
             if m_lo >= m_hi:
                 continue
+            thr = (thr_all[k] if self.std_bonds else thr_L[k]) if kind == 0 else thr_L[k]
             out = list(vals)
             for m in range(m_lo, m_hi):
                 v = vals[m]
                 out[m] = _get_ind(v, thr) if kind == 0 else _get_ind((v + TWO_PI) % TWO_PI, thr)
             geo[k] = out
-        return json.dumps(geo, sort_keys=True)
+        return _ENC.encode(geo)
 
     # ------------------------------------------------------------ bin (bpe.py:1431-1474)
     def bin(self):
         from sortedcontainers import SortedList
         self._geo_dict = defaultdict(set)
+        # the key of every live pair by (chain, start of its second token): a pair's key
+        # changes only when a merge replaces the pair, so step() reads the old neighbour keys
+        # from here instead of re-deriving them from the geometry (bpe.py:1917, 1933, 1941)
+        self._pk = {}
         for ci, c in enumerate(self._chains):
             toks = c.tokens()
             for (i1, _, l1), (i2, _, l2) in zip(toks, toks[1:]):
-                self._geo_dict[self._pair_key(ci, i1, l1, l2)].add((ci, i2))
+                k = self._pair_key(ci, i1, l1, l2)
+                self._geo_dict[k].add((ci, i2))
+                self._pk[(ci, i2)] = k
         self._geo_step = {k: 0 for k in self._geo_dict}
         self._priority = SortedList()
         self._key_to_priority = {}
@@ -588,21 +600,23 @@ class RmsdBPE:
                 continue
             if not (l1 > 0 and l2 > 0):
                 raise AssertionError("bad split")
-            if self._pair_key(ci, i1, l1, l2) != key:
+            pk = self._pk
+            if pk.get((ci, i2)) != key:
                 continue  # bpe.py:1918-1920 (breakpoint(); continue)
             gd[key].remove((ci, i2))
+            del pk[(ci, i2)]
             note(key, -1)
             left = right = None
             if i1:
                 i0 = tp[i1 - 1]
                 l0 = i1 - i0
-                left = self._pair_key(ci, i0, l0, l1)
+                left = pk[(ci, i1)]
             if i2 + l2 < len(tp):
                 i3 = i2 + l2
                 l3 = 0
                 while i3 + l3 < len(tp) and tp[i3 + l3] == i3:
                     l3 += 1
-                right = self._pair_key(ci, i2, l2, l3)
+                right = pk[(ci, i3)]
             if left:
                 gd[left].remove((ci, i1))
                 note(left, -1)
@@ -619,10 +633,12 @@ class RmsdBPE:
             if left:
                 k = self._pair_key(ci, i0, l0, length)
                 gd[k].add((ci, i1))
+                pk[(ci, i1)] = k
                 note(k, +1)
             if right:
                 k = self._pair_key(ci, i1, length, l3)
                 gd[k].add((ci, i3))
+                pk[(ci, i3)] = k
                 note(k, +1)
             if not rmsd:
                 c.set_geo(i1, length, binned)
