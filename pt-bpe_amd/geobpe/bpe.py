@@ -149,6 +149,8 @@ def _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_siz
         # re-snaps the merged span to grid(|token|) (bpe.py:2010-2013): with several grids the
         # stored keys go stale and step() reaches breakpoint() at bpe.py:1917-1920
         # (tests/golden/multigrid_reference.json)
+        # (BPE(...) hands such schedules to the host mirror, geobpe.rmsd_bpe; this is the
+        # device engine's own guard)
         raise NotImplementedError("multi-grid bin schedules (--bins 1-a:s-b): the reference's step() is inconsistent "
                                   "for them (stale neighbour keys -> breakpoint at bpe.py:1919); see DESIGN.md §7")
     if bin_strategy not in ("histogram", "histogram-cover", "uniform"):
@@ -178,7 +180,10 @@ class BPE:
             ba = inspect.signature(BPE.__init__).bind(None, *args, **kwargs)
             ba.apply_defaults()
             p = ba.arguments["rmsd_partition_min_size"]
-            if p != float("inf") and p < 10 ** 9:
+            bins = ba.arguments["bins"]
+            if (p != float("inf") and p < 10 ** 9) or (isinstance(bins, dict) and len(bins) > 1 and 1 in bins):
+                # the host mirror: RMSD partitioning, or a multi-grid schedule without it (the
+                # reference's stale-key semantics); the device engine runs bins={1: B}
                 from .rmsd_bpe import RmsdBPE
                 return RmsdBPE(*args, **kwargs)
         return super().__new__(cls)

@@ -585,6 +585,10 @@ class RmsdBPE:
             diff[k] = diff.get(k, 0) + d
 
         gd = self._geo_dict
+        # without RMSD partitioning, a multi-grid schedule re-snaps a merged span after its
+        # neighbour keys were computed (bpe.py:2010-2013), so stored keys can go stale: then
+        # every key is derived afresh from the geometry, as the reference does
+        stale_ok = not rmsd and len(self.bins) > 1
         last_ci = last_i1 = None
         for idx in sorted(range(len(occ)), key=occ.__getitem__):
             ci, i2 = occ[idx]
@@ -594,15 +598,17 @@ class RmsdBPE:
             l1 = i2 - i1
             l2 = length - l1
             overlaps = last_ci == ci and last_i1 + length > i1
-            if overlaps != ((ci, i2) not in gd[key]):
-                raise RuntimeError("occurrence bookkeeping out of step (the reference stops in breakpoint())")
+            # (overlaps != not present: the reference calls breakpoint() and, with breakpoints
+            # off, carries on, bpe.py:1909-1912; only stale multi-grid keys get here)
             if overlaps:
                 continue
             if not (l1 > 0 and l2 > 0):
                 raise AssertionError("bad split")
             pk = self._pk
-            if pk.get((ci, i2)) != key:
-                continue  # bpe.py:1918-1920 (breakpoint(); continue)
+            if pk.get((ci, i2)) != key or (stale_ok and self._pair_key(ci, i1, l1, l2) != key):
+                # bpe.py:1917-1920 (breakpoint(); continue): the stored key is the pair's key
+                # unless a multi-grid re-snap made it stale (no RMSD partitioning)
+                continue
             gd[key].remove((ci, i2))
             del pk[(ci, i2)]
             note(key, -1)
@@ -610,13 +616,13 @@ class RmsdBPE:
             if i1:
                 i0 = tp[i1 - 1]
                 l0 = i1 - i0
-                left = pk[(ci, i1)]
+                left = self._pair_key(ci, i0, l0, l1) if stale_ok else pk[(ci, i1)]
             if i2 + l2 < len(tp):
                 i3 = i2 + l2
                 l3 = 0
                 while i3 + l3 < len(tp) and tp[i3 + l3] == i3:
                     l3 += 1
-                right = pk[(ci, i3)]
+                right = self._pair_key(ci, i2, l2, l3) if stale_ok else pk[(ci, i3)]
             if left:
                 gd[left].remove((ci, i1))
                 note(left, -1)

@@ -56,6 +56,12 @@ FIXTURES = {
     "rm_p0_super_freebonds": (10, 20, 40, 30, 5, 0, True, 60, 40, NUM_P, False),
     "rm_p2_freebonds_multigrid": (12, 15, 35, 31, {1: 4, 6: 3}, 2, False, 60, 40, NUM_P, False),
     "rm_p3_freebonds": (6, 15, 30, 32, 5, 3, False, 60, 5, NUM_P, False),
+    # no RMSD partitioning (p = inf) with a multi-grid schedule: the reference's step()
+    # re-snaps after computing the neighbour keys, its stored keys go stale and, with
+    # breakpoints off, it skips those occurrences (bpe.py:1909-1920) -- its own semantics,
+    # recorded here
+    "rm_pinf_multigrid": (20, 30, 80, 33, {1: 5, 2: 6, 3: 8, 5: 4, 6: 7, 9: 5, 12: 3, 15: 1}, float("inf"),
+                          False, 60, 30),
     # config 1's corpus (every PDB of the reference's data/vqvae_pretrain/train, featurised by
     # pdb_angles.py) in the README's first run minus glue optimisation: --bins 1-50, p = 0,
     # --num-p 2-2:3-5:5-1:6-2:8-1, max_num_strucs 500, free bonds, rmsd_super_res

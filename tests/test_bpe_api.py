@@ -22,7 +22,7 @@ def _bpe(meta, corpus):
     (dict(glue_opt=True), NotImplementedError),
     (dict(std_bonds=False), KeyError),  # as the reference's initialize() (free-bonds probe)
     (dict(bin_strategy="quantile"), NotImplementedError),
-    (dict(bins={1: 5, 10: 3}), NotImplementedError),
+
     (dict(bins={2: 5}), KeyError),
 ])
 def test_out_of_scope_configurations_are_rejected(kw, exc):
