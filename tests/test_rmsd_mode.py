@@ -160,7 +160,8 @@ def test_rmsd_mode_dispatch_and_scope():
 @pytest.mark.parametrize("name", NAMES)
 def test_rmsd_mode_device_matches_reference(name):
     bpe = run_and_compare(name)
-    if name not in ("rm_p4", "rm_p3_freebonds"):
+    meta = _load(name)[0]
+    if meta["rmsd_partition_min_size"] <= 3 and "init_tokens" in meta:
         assert bpe.assign_calls > 0  # the device RMSD batches ran
 
 
