@@ -123,6 +123,29 @@ class Tokenizer:
             pos.extend([s] * nb)
         return pos
 
+    def compute_coords(self, index=0, length=float("inf"), orig=False):
+        """Tokenizer.compute_coords (tokenizer.py:347-363): NeRF (on the device) of the
+        chain's geometry -- every value the run reads at its bin centre and the standard
+        bond lengths (the frame a scoped run leaves, geobpe.refpickle.chain_frames), or the
+        input values with orig=True (the init lengths / angle are the run's in both)."""
+        import pandas as pd
+
+        from . import refpickle, rmsd
+        b = self._bpe
+        corpus = b._global_corpus if b._global_corpus is not None else b._corpus
+        ro = corpus["row_off"]
+        cols = {c: np.asarray(corpus[c][ro[self.row]:ro[self.row + 1]], dtype=np.float64) for c in COLUMNS}
+        thr1 = {k: [tuple(p) for p in v] for k, v in b._thresholds[1].items()}
+        q, o = refpickle.chain_frames(pd, cols, thr1)
+        frame = o if orig else q
+        tau = thr1["tau"]
+        from .engine import init_bond_angle
+        init = (BOND_LENGTHS[0], BOND_LENGTHS[1],
+                sum(tau[get_ind((init_bond_angle() + 2 * np.pi) % (2 * np.pi), tau)]) / 2)
+        ln = min(length, 3 * self.n - 1 - index)
+        return rmsd.compute_coords({c: frame[c].tolist() for c in COLUMNS}, [(index, int(ln))], init=init,
+                                   device=b._engine.device)[0]
+
     def tokenize(self):
         """tokenizer.py:379-392: MOTIF ids and the glue values (bin centres) after
         every token but the last."""
@@ -452,6 +475,18 @@ class BPE:
             else:
                 repl[tok[1]].append(tok[2])
         return dict(repl)
+
+    @staticmethod
+    def init_structure(n):
+        """bpe.py:1005-1027."""
+        from .rmsd_bpe import init_structure
+        return init_structure(n)
+
+    def recover_structure(self, repl, tokenized):
+        """bpe.py:1029-1051 (bin/train.py:715-716): a tokenizer (chain view with
+        bond_to_token, token_geo, tokenize, compute_coords) built from recovered geometry."""
+        from .rmsd_bpe import recover_structure
+        return recover_structure(self._tokens, repl, tokenized, self._engine.device)
 
     def capacity(self, tokenizer=False):
         """bpe.py:885-902."""

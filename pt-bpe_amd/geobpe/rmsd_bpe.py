@@ -160,14 +160,73 @@ class _Chain:
         return (self._dihedral(b - 2, self.cur), self._dihedral(b - 1, self.cur), self._angle(b - 1, self.cur))
 
 
+def chain_coords(c: "_Chain", index=0, length=float("inf"), orig=False, device: int = 0):
+    cols = c.orig if orig else c.cur
+    ln = min(length, 3 * c.n - 1 - index)
+    return _rmsd.compute_coords(cols, [(index, int(ln))], init=tuple(c.init), device=device)[0]
+
+
+def init_structure(n: int) -> dict:
+    """Tokenizer.init_structure / BPE.init_structure (tokenizer.py:395-417, bpe.py:1005-1027)."""
+    import pandas as pd
+    angles = {c: [0.0] * n if c in BOND_TYPES else [np.nan] * n for c in COLUMNS}
+    idxes = sum([[i, i, i] for i in range(1, n + 1)], [])
+    return {"angles": pd.DataFrame(angles), "coords": None, "c_beta": None, "full_idxes": idxes,
+            "full_coords": None, "side_chain": None, "aa": None, "fname": None}
+
+
+def recover_structure(tokens: dict, repl: dict, tokenized, device: int = 0) -> "RmsdTokenizer":
+    """BPE.recover_structure (bpe.py:1029-1051): a chain whose rows come from the recovered
+    geometry (the init bond / angle of residue 0 dropped, the last row left at the
+    init_structure defaults), the raw init triple of a new Tokenizer, and one token per
+    MOTIF of ``tokenized`` with its id's bond count."""
+    n = len(repl["N:CA"])
+    cols = {c: [0.0] * n if c in BOND_TYPES else [np.nan] * n for c in COLUMNS}
+
+    def put(c, lo, hi, vals):
+        vals = list(vals)
+        rows = list(range(n))[lo:hi]
+        if len(vals) != len(rows):
+            raise ValueError(f"recover_structure: {c} has {len(vals)} values for {len(rows)} rows")
+        for r, v in zip(rows, vals):
+            cols[c][r] = float(v)
+
+    put("N:CA", None, -1, repl["N:CA"][1:])
+    put("CA:C", None, -1, repl["CA:C"][1:])
+    put("0C:1N", None, -1, repl["0C:1N"])
+    put("phi", 1, None, repl["phi"])
+    put("psi", None, -1, repl["psi"])
+    put("omega", None, -1, repl["omega"])
+    put("tau", None, -1, repl["tau"][1:])
+    put("CA:C:1N", None, -1, repl["CA:C:1N"])
+    put("C:1N:1CA", None, -1, repl["C:1N:1CA"])
+    c = _Chain(cols, _rmsd.init_geometry())
+    cur = 0
+    for tok in tokenized:
+        if tok[0] == "MOTIF":
+            nb = sum(len(tokens[tok[1]].get(k, [])) for k in BOND_TYPES)
+            c.btt[cur] = (cur, tok[1], nb)
+            c.token_pos.extend([cur] * nb)
+            cur += nb
+    c.tokens0 = list(c.btt.values())
+    return RmsdTokenizer(c, device)
+
+
 class RmsdTokenizer:
     """Tokenizer view of one chain in the RMSD mode: ``bond_to_token`` with tuple ids
     ``(n, p)``, ``token_pos``, ``tokens``, ``tokenize()`` (tokenizer.py:379-392)."""
 
-    def __init__(self, chain: _Chain):
+    def __init__(self, chain: _Chain, device: int = 0):
         self._c = chain
         self.n = chain.n
         self.fname = chain.fname
+        self._device = device
+
+    def compute_coords(self, index=0, length=float("inf"), orig=False):
+        """Tokenizer.compute_coords (tokenizer.py:347-363): backbone atoms of bonds
+        index..index+length by NeRF of the chain's current (or original) geometry, on the
+        device; the init lengths / angle are the chain's current ones in both cases."""
+        return chain_coords(self._c, index, length, orig, self._device)
 
     @property
     def bond_to_token(self):
@@ -757,7 +816,7 @@ class RmsdBPE:
             if key in geo_dict:
                 self._step_helper(geo_dict, c, key, n)
             metrics["L"].append(len(c.btt))
-        return RmsdTokenizer(c), metrics
+        return RmsdTokenizer(c, self.device), metrics
 
     def _step_helper(self, geo_dict, c, key, n):
         """step() on one chain for a trained key (bpe.py:1316-1404)."""
@@ -813,7 +872,13 @@ class RmsdBPE:
     # ------------------------------------------------------------ views / encode
     @property
     def tokenizers(self):
-        return [RmsdTokenizer(c) for c in self._chains]
+        return [RmsdTokenizer(c, self.device) for c in self._chains]
+
+    init_structure = staticmethod(init_structure)
+
+    def recover_structure(self, repl, tokenized):
+        """bpe.py:1029-1051 (bin/train.py:715-716)."""
+        return recover_structure(self._tokens, repl, tokenized, self.device)
 
     @property
     def vocab_size(self):
