@@ -48,7 +48,6 @@ from .synth import COLUMNS
 BOND_TYPES = ["N:CA", "CA:C", "0C:1N"]
 BOND_ANGLES = ["tau", "CA:C:1N", "C:1N:1CA"]
 DIHEDRALS = ["psi", "omega", "phi"]
-STD_LENGTH = {"N:CA": 1.46, "CA:C": 1.54, "0C:1N": 1.34}       # nerf.py:17-19
 GLUE = ["omega", "C:1N:1CA", "phi"]                            # bpe.py:383
 TWO_PI = 2 * np.pi
 # the residue-level partition keys of _sphere_dict (bpe.py:333-338)
@@ -101,9 +100,6 @@ class _Chain:
         self.fname = fname
         self.tokens0 = []  # Tokenizer.tokens: the initial tokens (step() never updates them, bpe.py:1955-1965)
         self.events = []   # merge tree: (left start, right start, parent value) per merge (data_structures.py:32-60)
-
-    def _bond(self, j, src):
-        return self.init[j] if j < 2 else src[BOND_TYPES[j % 3]][(j - 2) // 3]
 
     def _angle(self, a, src):
         return self.init[2] if a == 0 else src[BOND_ANGLES[a % 3]][(a - 1) // 3]

@@ -33,10 +33,6 @@ def _load(name):
     return meta, corpus, arrs
 
 
-def _tid(v):
-    return tuple(v) if isinstance(v, list) else v
-
-
 def _geometry_equal(bpe, arrs, tag):
     g = bpe.geometry()
     for c in COLS:
