@@ -354,6 +354,10 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
     c->ncu = prop.multiProcessorCount;
   c->nba = std::min(c->ncu, NBA_MAX);
+  if (const char* e = getenv("GEOBPE_NBA")) {  // (A/B: merge workgroups other than one per CU)
+    const int v = atoi(e);
+    if (v >= 8 && v <= NBA_MAX) c->nba = v;
+  }
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
