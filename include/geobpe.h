@@ -245,6 +245,23 @@ int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const dou
    (the last six: the junction to the next residue of the span); h_xyz: N, CA, C of
    every residue (9 float64 per residue). */
 int geobpe_nerf(int device, int64_t n_spans, const int64_t *h_res_off, const double *h_geo, double *h_xyz);
+/* Glue optimisation of the RMSD mode: L-BFGS (torch.optim.LBFGS, max_iter 20,
+   strong-Wolfe line search) over every glue triple (omega_k, C:1N:1CA_k, phi_k) of each
+   chain, minimising the exit-frame loss of the chain's NeRF against cached frames plus the
+   optional von Mises prior.  Replaces BPE.glue_opt_all / _opt_glue_worker / opt_glue /
+   optimize_glues_entry_torch / fk_segment_torch (bpe.py:106-135, 423-578, 739-807), one
+   chain per thread.  h_res_off[n_chains + 1]: residue offsets; h_geo: 9 float64 per
+   residue (geobpe_nerf's layout, float32-representable values); per glue (r - 1 per
+   chain, in order): h_x0 3 float32 (raw start values), h_tgt 12 float32 (target frame R
+   row-major, then t); h_grid[n_chains]: prior table per chain; h_prior: n_grid x 3 types
+   (omega, C:1N:1CA, phi) x {centres[kmax], weights[kmax]}; h_kcnt: n_grid x 3 bin
+   counts; lam: glue_opt_prior; w_rot / w_trans: wR / wt.  Out: h_xout 3 float32 per glue
+   (the wrapped optimum, before snapping), h_stats 2 per chain (iterations, evaluations),
+   h_loss 2 per chain (first and last loss). */
+int geobpe_glue_opt(int device, int64_t n_chains, const int64_t *h_res_off, const double *h_geo, const float *h_x0,
+                    const float *h_tgt, const int32_t *h_grid, int32_t n_grid, int32_t kmax, const float *h_prior,
+                    const int32_t *h_kcnt, float lam, double w_rot, double w_trans, float *h_xout, int32_t *h_stats,
+                    double *h_loss);
 int geobpe_set_record_events(geobpe_ctx *ctx, int on);
 int64_t geobpe_events(geobpe_ctx *ctx, int32_t *h_merge, int32_t *h_a, int32_t *h_b);
 

@@ -31,6 +31,7 @@
 #include "kernels.h"
 #include "featurize.h"
 #include "rmsd.h"
+#include "glue.h"
 
 using namespace gb;
 
@@ -1401,6 +1402,94 @@ int geobpe_nerf(int device, int64_t n_spans, const int64_t* h_res_off, const dou
   hipFree(d_off);
   hipFree(d_geo);
   hipFree(d_out);
+  hipStreamDestroy(s);
+  return rc;
+}
+
+int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, const double* h_geo, const float* h_x0,
+                    const float* h_tgt, const int32_t* h_grid, int32_t n_grid, int32_t kmax, const float* h_prior,
+                    const int32_t* h_kcnt, float lam, double w_rot, double w_trans, float* h_xout, int32_t* h_stats,
+                    double* h_loss) {
+  if (n_chains < 0 || !h_res_off) return GEOBPE_EARG;
+  if (n_chains == 0) return 0;
+  const int64_t R = h_res_off[n_chains];
+  int64_t rmax = 0;
+  for (int64_t i = 0; i < n_chains; i++) {
+    const int64_t r = h_res_off[i + 1] - h_res_off[i];
+    if (r < 0) return GEOBPE_EARG;
+    rmax = std::max(rmax, r);
+  }
+  const int64_t G = R - n_chains;  // glues: r - 1 per chain
+  if (R == 0 || G <= 0) return 0;
+  if (!h_geo || !h_x0 || !h_tgt || !h_grid || !h_prior || !h_kcnt || !h_xout || !h_stats || !h_loss) return GEOBPE_EARG;
+  if (n_grid <= 0 || kmax <= 0) return GEOBPE_EARG;
+  for (int64_t i = 0; i < n_chains; i++)
+    if (h_grid[i] < 0 || h_grid[i] >= n_grid) return GEOBPE_EARG;
+  for (int64_t i = 0; i < 3 * (int64_t)n_grid; i++)
+    if (h_kcnt[i] <= 0 || h_kcnt[i] > kmax) return GEOBPE_EARG;
+  if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
+  hipStream_t s;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GEOBPE_EHIP;
+  const int64_t pmax = 3 * (rmax - 1), S = n_chains;
+  GlueProb P{};
+  P.S = S;
+  P.kmax = kmax;
+  P.lam = lam;
+  P.wR = w_rot;
+  P.wt = w_trans;
+  P.pmax = pmax;
+  int64_t *d_off = nullptr;
+  double *d_geo = nullptr, *d_loss = nullptr;
+  float *d_x0 = nullptr, *d_tgt = nullptr, *d_prior = nullptr, *d_xout = nullptr;
+  int32_t *d_grid = nullptr, *d_kcnt = nullptr, *d_stats = nullptr;
+  int rc = 0;
+  const int64_t nx = 9 * rmax * S;
+  if (hipMalloc(&d_off, (S + 1) * 8) != hipSuccess || hipMalloc(&d_geo, R * 9 * 8) != hipSuccess ||
+      hipMalloc(&d_x0, G * 3 * 4) != hipSuccess || hipMalloc(&d_tgt, G * 12 * 4) != hipSuccess ||
+      hipMalloc(&d_grid, S * 4) != hipSuccess || hipMalloc(&d_prior, (int64_t)n_grid * 6 * kmax * 4) != hipSuccess ||
+      hipMalloc(&d_kcnt, (int64_t)n_grid * 3 * 4) != hipSuccess || hipMalloc(&d_xout, G * 3 * 4) != hipSuccess ||
+      hipMalloc(&d_stats, S * 2 * 4) != hipSuccess || hipMalloc(&d_loss, S * 2 * 8) != hipSuccess ||
+      hipMalloc(&P.X, nx * 8) != hipSuccess || hipMalloc(&P.AX, nx * 8) != hipSuccess ||
+      hipMalloc(&P.V, (int64_t)GLUE_NVEC * pmax * S * 4) != hipSuccess ||
+      hipMalloc(&P.H, (int64_t)2 * GLUE_HIST * pmax * S * 4) != hipSuccess) {
+    rc = GEOBPE_EHIP;
+  } else {
+    hipMemcpyAsync(d_off, h_res_off, (S + 1) * 8, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_geo, h_geo, R * 9 * 8, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_x0, h_x0, G * 3 * 4, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_tgt, h_tgt, G * 12 * 4, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_grid, h_grid, S * 4, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_prior, h_prior, (int64_t)n_grid * 6 * kmax * 4, hipMemcpyHostToDevice, s);
+    hipMemcpyAsync(d_kcnt, h_kcnt, (int64_t)n_grid * 3 * 4, hipMemcpyHostToDevice, s);
+    P.roff = d_off;
+    P.geo = d_geo;
+    P.tgt = d_tgt;
+    P.grid = d_grid;
+    P.prior = d_prior;
+    P.kcnt = d_kcnt;
+    hipLaunchKernelGGL(k_glue_opt, dim3((unsigned)((S + 63) / 64)), dim3(64), 0, s, P, (const float*)d_x0, d_xout,
+                       d_stats, d_loss);
+    if (hipGetLastError() != hipSuccess) rc = GEOBPE_EHIP;
+    if (!rc && (hipMemcpyAsync(h_xout, d_xout, G * 3 * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(h_stats, d_stats, S * 2 * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+                hipMemcpyAsync(h_loss, d_loss, S * 2 * 8, hipMemcpyDeviceToHost, s) != hipSuccess))
+      rc = GEOBPE_EHIP;
+    if (hipStreamSynchronize(s) != hipSuccess) rc = GEOBPE_EHIP;
+  }
+  hipFree(d_off);
+  hipFree(d_geo);
+  hipFree(d_x0);
+  hipFree(d_tgt);
+  hipFree(d_grid);
+  hipFree(d_prior);
+  hipFree(d_kcnt);
+  hipFree(d_xout);
+  hipFree(d_stats);
+  hipFree(d_loss);
+  hipFree(P.X);
+  hipFree(P.AX);
+  hipFree(P.V);
+  hipFree(P.H);
   hipStreamDestroy(s);
   return rc;
 }

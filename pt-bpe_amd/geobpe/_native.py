@@ -98,6 +98,8 @@ def lib():
         "geobpe_featurize": (ctypes.c_int, [ctypes.c_int, I64, P, P, P]),
         "geobpe_events": (I64, [P, P, P, P]),
         "geobpe_nerf": (ctypes.c_int, [ctypes.c_int, I64, P, P, P]),
+        "geobpe_glue_opt": (ctypes.c_int, [ctypes.c_int, I64, P, P, P, P, P, ctypes.c_int32, ctypes.c_int32, P, P,
+                                           ctypes.c_float, ctypes.c_double, ctypes.c_double, P, P, P]),
         "geobpe_rmsd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P, P,
                                        ctypes.c_int, P]),
     }
@@ -120,7 +122,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",
     "geobpe_delta_export_async", "geobpe_delta_import_async", "geobpe_pipeline_begin", "geobpe_pipeline_iter",
     "geobpe_pipeline_import", "geobpe_pipeline_poll", "geobpe_pipeline_resolve", "geobpe_pipeline_end", "geobpe_pdb_backbone", "geobpe_pdb_error",
-    "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf",
+    "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf", "geobpe_glue_opt",
 ]
 
 

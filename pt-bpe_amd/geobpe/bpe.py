@@ -189,7 +189,9 @@ def _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_siz
     if rmsd_partition_min_size != float("inf") and rmsd_partition_min_size < 10 ** 9:
         raise NotImplementedError("RMSD partitioning (p_min_size < inf) is float geometry, SURVEY §8(f) row 4")
     if glue_opt:
-        raise NotImplementedError("glue optimisation (LBFGS) is float geometry, SURVEY §8(f) row 4")
+        raise NotImplementedError("glue optimisation without RMSD partitioning: the reference re-optimises "
+                                  "glues only after RMSD-key merges (bpe.py:2027); run it with a finite "
+                                  "rmsd_partition_min_size (geobpe.rmsd_bpe.RmsdBPE)")
     if compute_sec_structs:
         raise NotImplementedError("secondary-structure priorities are not in this build")
 

@@ -29,8 +29,10 @@ reference's dictionaries instead, with the same add/remove sequence per key, so
 
 Reachable configurations (tests/golden/rmsd_mode_probe.json, rm_p4.json): p <= 3 partitions
 the residues at initialize() and every merge; p >= 4 never creates ``_sphere_dict``, so the
-first merge of >= p bonds raises AttributeError there, as it does here.  Not built: glue
-optimisation (LBFGS, ``glue_opt=True``) and ``rmsd_only``.  Free bond lengths
+first merge of >= p bonds raises AttributeError there, as it does here.  Glue optimisation
+(``glue_opt=True``, ``glue_opt_method="all"``, bpe.py:106-135, 192-229, 2027-2071) runs as one
+device L-BFGS launch over the chains (geobpe/glue.py, csrc/glue.h).  Not built: the "each"
+glue method and ``rmsd_only``.  Free bond lengths
 (``std_bonds=False``) run where the reference runs them (p <= 2; p >= 3 raises its KeyError).
 """
 from __future__ import annotations
@@ -271,8 +273,9 @@ class RmsdBPE:
             raise NotImplementedError("the RMSD mode needs res_init=True (bond-level init is not built)")
         if not std_bonds and bin_strategy == "uniform":
             raise NotImplementedError("free bonds with uniform (equal-count) bins are not built")
-        if glue_opt:
-            raise NotImplementedError("glue optimisation (LBFGS over NeRF, bpe.py:423-578) is not built")
+        if glue_opt and glue_opt_method != "all":
+            raise NotImplementedError("glue_opt_method='each' (per-occurrence glue opt, bpe.py:365-369, "
+                                      "1978-1982) is not built; 'all' is (geobpe/glue.py)")
         if rmsd_only or compute_sec_structs:
             raise NotImplementedError("rmsd_only / secondary-structure priorities are not built")
         if isinstance(structures, dict) and "row_off" in structures:
@@ -431,6 +434,9 @@ class RmsdBPE:
                 bt = BOND_TYPES[j % 3]
                 v = self._centre(bt, _get_ind(c.geo(j, 1)[bt][0], self._thresholds[1][bt]), 1)
                 c.set_geo(j, 1, {bt: [v]})
+        if self.glue_opt:  # exit frames of the bond-standardized chains (bpe.py:192-229)
+            from .glue import exit_frames
+            self._exit_frames = exit_frames(self._chains, device=self.device)
         label_dict, res_geo, labels = {}, {}, []
         for ci, c in enumerate(self._chains):
             lab = []
@@ -467,7 +473,9 @@ class RmsdBPE:
                 self._partition_residues(n, size, res_geo[size])
         for c in self._chains:
             c.tokens0 = list(c.btt.values())
-        for c in self._chains:  # glue angles -> grid-1 bin centres, NaN kept (bpe.py:381-391)
+        for c in (self._chains if not (res_geo and self.glue_opt) else []):
+            # glue angles -> grid-1 bin centres, NaN kept (bpe.py:381-391); with glue_opt and
+            # partitioned residues they stay raw until glue_opt_all snaps them
             for k in GLUE:
                 col = c.cur[k]
                 for r in range(c.n):
@@ -476,6 +484,56 @@ class RmsdBPE:
                         col[r] = self._centre(k, _get_ind((v + TWO_PI) % TWO_PI, self._thresholds[1][k]), 1)
         if not res_geo:
             self._tokens = {n: json.loads(s) for s, n in label_dict.items()}
+
+    # ------------------------------------------------------------ glue optimisation
+    def glue_opt_all(self):
+        """BPE.glue_opt_all (bpe.py:106-135): every chain's glues optimised against its
+        cached exit frames (bin/encode.py:331-332 calls it after initialize())."""
+        self._glue_opt(range(self.n))
+
+    def _glue_opt(self, cis):
+        """_opt_glue_worker + opt_glue (bpe.py:739-807) for the chains cis, as one device
+        launch: glue k = (omega_k, C:1N:1CA_k, phi_{k+1}) of every initial token but the last,
+        started from the current values, aimed at exit frame (start + length) // 3 - 1 of the
+        cached chain; the optimum snapped to grid(3n - 4)'s bins and written back.  Returns
+        the chains' indices."""
+        from . import glue as G
+        cis = list(cis)
+        if not cis:
+            return cis
+        sizes = sorted(self.bins)
+        if not hasattr(self, "_glue_prior"):
+            counts = self._bin_count_values()
+            self._glue_prior = G.prior_tables([self._thresholds[s0] for s0 in sizes], [counts[s0] for s0 in sizes])
+        geos, x0s, tgts, grids = [], [], [], []
+        for ci in cis:
+            c = self._chains[ci]
+            g = G.pack_chain(c.cur, c.init)
+            toks = c.tokens0[:-1]
+            geos.append(g)
+            x0s.append(np.stack([[c.cur["omega"][(i + ln) // 3 - 1], c.cur["C:1N:1CA"][(i + ln) // 3 - 1],
+                                  c.cur["phi"][(i + ln) // 3]] for i, _, ln in toks]).astype(np.float32)
+                       if toks else np.zeros((0, 3), np.float32))
+            R, t = self._exit_frames[ci]
+            rows = [(i + ln) // 3 - 1 for i, _, ln in toks]  # R_occs[res_no - 2], bpe.py:751-755
+            tgts.append((R[rows], t[rows]))
+            L = 3 * c.n - 4
+            grids.append(max([k for k in sizes if k <= L], default=sizes[0]))
+        if any(len(x) != len(g) - 1 for x, g in zip(x0s, geos)):
+            raise NotImplementedError("glue opt over initial tokens other than one per residue")
+        lam = float(self.glue_opt_prior) if self.glue_opt_prior and self.glue_opt_prior > 0.0 else 0.0
+        outs, stats, _ = G.optimize_chains(geos, x0s, tgts, [sizes.index(k) for k in grids], self._glue_prior, lam,
+                                           device=self.device)
+        self.glue_calls = getattr(self, "glue_calls", 0) + 1
+        for ci, opt, gk in zip(cis, outs, grids):
+            c = self._chains[ci]
+            thr = self._thresholds[gk]
+            for k, (i, _, ln) in enumerate(c.tokens0[:-1]):
+                row = (i + ln) // 3 - 1
+                c.cur["omega"][row] = G.snap_bin(thr["omega"], opt[k, 0])
+                c.cur["C:1N:1CA"][row] = G.snap_bin(thr["C:1N:1CA"], opt[k, 1])
+                c.cur["phi"][row + 1] = G.snap_bin(thr["phi"], opt[k, 2])
+        return cis
 
     def _partition_residues(self, n, size, occ):
         """The res_geo partition of one residue size (bpe.py:266-379)."""
@@ -704,6 +762,28 @@ class RmsdBPE:
             if not rmsd:
                 c.set_geo(i1, length, binned)
             last_ci, last_i1 = ci, i1
+        # glue re-optimisation of every chain the merge touched (bpe.py:2027-2071): all glues
+        # of each chain, then every adjacent token pair whose key changed moves between sets
+        if (rmsd and self.glue_opt and not self.rmsd_only and self.glue_opt_method == "all"
+                and self._step % self.glue_opt_every == 0):
+            uniq = set(ci for ci, _ in occ)
+            pk = self._pk
+            for ci in self._glue_opt(list(uniq)):
+                btt = self._chains[ci].btt
+                last = 3 * self._chains[ci].n - 1
+                for i1, (_, _, l1) in list(btt.items()):
+                    if i1 + l1 == last:
+                        continue
+                    i2 = i1 + l1
+                    l2 = btt[i2][2]
+                    old = pk[(ci, i2)]
+                    new = self._pair_key(ci, i1, l1, l2)
+                    if new != old:
+                        gd[old].remove((ci, i2))
+                        note(old, -1)
+                        gd[new].add((ci, i2))
+                        pk[(ci, i2)] = new
+                        note(new, +1)
         if not recurring:
             self._step += 1
         for k, d in diff.items():  # step 7 (bpe.py:2077-2138)

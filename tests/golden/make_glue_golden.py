@@ -1,0 +1,194 @@
+"""Golden fixtures for glue optimisation (`bpe.py:106-135, 423-578,
+739-807`), made by running the REFERENCE in this container (never on the GPU box).
+
+The reference's `BPE` is run in the RMSD mode with `glue_opt=True` on small synthetic corpora,
+the way `bin/encode.py:323-332` drives it: `initialize()`, then `glue_opt_all()` for
+`glue_opt_method="all"`, then `bin()` and `step()` calls.  Worker pools are required
+(`glue_opt_all`'s `max_workers == 0` branch calls `_opt_glue_worker` with two arguments,
+`bpe.py:113`, a TypeError), so this runs with SLURM_CPUS_PER_TASK=2.
+
+Per fixture `<name>`:
+  <name>.npz   the corpus; the per-chain geometry (9 columns, float64) after initialize()
+               ("init"), after glue_opt_all() ("glued") and at the end ("final");
+  <name>.json  the settings, the (flag, -count, key) popped per step() call, segmentation,
+               _tokens, and whatever initialize / glue_opt_all / bin / step raised.
+
+Usage: python tests/golden/make_glue_golden.py [name ...]
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import traceback
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, "pt-bpe_amd"))
+sys.path.insert(0, HERE)
+
+NUM_P = {2: 2, 3: 3, 5: 2, 8: 1}
+# name: (n_chains, len_lo, len_hi, seed, B, p, super_res, method, prior, every, step calls)
+FIXTURES = {
+    "gl_all_p0": (6, 12, 30, 41, 5, 0, False, "all", 0.0, 10, 12),
+    "gl_all_p0_prior": (6, 12, 30, 42, 5, 0, True, "all", 1.0, 1, 6),
+    "gl_each_p0": (5, 10, 20, 43, 5, 0, False, "each", 0.0, 10, 6),
+}
+COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
+
+
+def _id(v):
+    return [int(x) for x in v] if isinstance(v, tuple) else int(v)
+
+
+def run_one(name):
+    import numpy as np
+    from geobpe import synth
+    from make_golden import _stub_optional_deps
+
+    nch, lo, hi, seed, B, p, sup, method, prior, every, calls = FIXTURES[name]
+    corpus = synth.make_corpus(synth.make_lengths(nch, lo, hi, seed=seed), seed=seed)
+    _stub_optional_deps()
+    sys.path.insert(0, "/root/reference")
+    import foldingdiff.bpe as RB
+    from foldingdiff.tokenizer import Tokenizer
+
+    RB.BPE.visualize = lambda self, key, path: None
+    Tokenizer.visualize_bonds = lambda self, *a, **k: None
+    popped = []
+    inner_step = RB.BPE.step
+
+    def recording_step(self):
+        top = self._priority_dict.peekitem(0)[0]
+        popped.append([bool(top[0]), int(top[1]), top[2]])
+        return inner_step(self)
+
+    RB.BPE.step = recording_step
+    structs = []
+    for i, row in enumerate(synth.corpus_rows(corpus)):
+        s = Tokenizer.init_structure(len(row["phi"]))
+        for c in COLS:
+            s["angles"][c] = row[c].astype(np.float64)
+        s["fname"] = f"synthetic_{i}"
+        structs.append(s)
+
+    def geometry(bpe, tag, arrays):
+        for c in COLS:
+            arrays[f"{tag}_{c}"] = np.concatenate(
+                [np.array([float(x) for x in t.angles_and_dists[c]]) for t in bpe.tokenizers])
+        arrays[f"{tag}_init"] = np.array([[float(t._init_n_ca), float(t._init_ca_c), float(t._init_bond_angle)]
+                                          for t in bpe.tokenizers])
+
+    def segmentation(bpe):
+        return [[[int(s), _id(v[1]), int(v[2])] for s, v in t.bond_to_token.items()] for t in bpe.tokenizers]
+
+    meta = {"name": name, "n_chains": nch, "len_lo": lo, "len_hi": hi, "seed": seed, "bins": {"1": B},
+            "rmsd_partition_min_size": p, "rmsd_super_res": sup, "glue_opt_method": method,
+            "glue_opt_prior": prior, "glue_opt_every": every, "num_partitions": {str(k): v for k, v in NUM_P.items()},
+            "max_num_strucs": 60, "std_bonds": True, "rng_seed": 0, "calls": [], "raised": None,
+            "generator": "tests/golden/make_glue_golden.py (reference: /root/reference foldingdiff/bpe.py, "
+                         "run in the build container)"}
+    arrays = dict(corpus)
+    bpe = RB.BPE(structs, bins={1: B}, save_dir=tempfile.mkdtemp(prefix="geobpe_glue_golden_"),
+                 rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(NUM_P), max_num_strucs=60,
+                 res_init=True, std_bonds=True, glue_opt=True, glue_opt_prior=prior, glue_opt_every=every,
+                 glue_opt_method=method, seed=0)
+    stage = "initialize"
+    try:
+        bpe.initialize()
+        geometry(bpe, "init", arrays)
+        meta["init_segmentation"] = segmentation(bpe)
+        stage = "glue_opt_all"
+        if method == "all":
+            lbfgs_record(RB, bpe, meta, arrays)
+            bpe.glue_opt_all()
+        geometry(bpe, "glued", arrays)
+        stage = "bin"
+        bpe.bin()
+        stage = "step"
+        for _ in range(calls):
+            if len(bpe._priority_dict) == 0:
+                break
+            n0 = len(popped)
+            bpe.step()
+            meta["calls"].append({"popped": popped[n0:], "step": bpe._step, "n_tokens": len(bpe._tokens)})
+    except BaseException as e:  # noqa: BLE001 - the fixture records what the reference raises
+        meta["raised"] = {"stage": stage, "type": type(e).__name__, "msg": str(e)[:300],
+                          "popped_so_far": popped[-1:], "where": traceback.format_exc().splitlines()[-6:]}
+    geometry(bpe, "final", arrays)
+    meta["tokens"] = [[_id(k), v] for k, v in bpe._tokens.items()]
+    meta["segmentation"] = segmentation(bpe)
+    meta["step"] = bpe._step
+    np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **arrays)
+    with open(os.path.join(HERE, f"{name}.json"), "w") as f:
+        json.dump(meta, f)
+    merges = sum(len(c["popped"]) for c in meta["calls"])
+    print(f"{name}: calls={len(meta['calls'])} merges={merges} step={meta.get('step')} "
+          f"raised={meta['raised'] and (meta['raised']['stage'], meta['raised']['type'])}", flush=True)
+
+
+def lbfgs_record(RB, bpe, meta, arrays):
+    """The optimiser's own view of glue_opt_all (bpe.py:106-135) for every chain, in this
+    process: _opt_glue_worker on a copy of each tokenizer, with LBFGS.step wrapped to record
+    the wrapped optimum before snapping (what the device kernel returns), the iteration and
+    evaluation counts and the loss of the first and last evaluation."""
+    import pickle
+    import numpy as np
+    import torch
+    rec = []
+
+    class RecLBFGS(torch.optim.LBFGS):
+        def step(self, closure):
+            losses = []
+
+            def wrapped():
+                v = closure()
+                losses.append(float(v))
+                return v
+            out = super().step(wrapped)
+            raw = self.param_groups[0]["params"][0].detach().clone()
+            wr = torch.remainder(torch.atan2(torch.sin(raw), torch.cos(raw)) + (2.0 * np.pi), 2.0 * np.pi)
+            st = self.state[self._params[0]]
+            rec.append({"opt": wr.numpy().astype(np.float64), "n_iter": int(st["n_iter"]),
+                        "func_evals": int(st["func_evals"]), "loss0": losses[0], "loss": losses[-1]})
+            return out
+
+    saved = RB.LBFGS
+    RB.LBFGS = RecLBFGS
+    try:
+        RB.BPE._init_opt_glue_worker(bpe._bin_centers, bpe._bin_weights, bpe._thresholds, bpe.glue_opt_prior)
+        for t in bpe.tokenizers:
+            frames = np.load(t.cached_all_frames)
+            arrays.setdefault("frames_R", []).append(np.asarray(frames["R_occs"], dtype=np.float64))
+            arrays.setdefault("frames_t", []).append(np.asarray(frames["t_occs"], dtype=np.float64))
+            RB.BPE._opt_glue_worker(pickle.loads(pickle.dumps(t)))
+    finally:
+        RB.LBFGS = saved
+    arrays["frames_R"] = np.concatenate(arrays["frames_R"])
+    arrays["frames_t"] = np.concatenate(arrays["frames_t"])
+    arrays["lbfgs_opt"] = np.concatenate([r["opt"] for r in rec])
+    # grid 1's prior tables (bins {1: B}: every chain length looks up grid 1)
+    arrays["prior_centers"] = np.stack([bpe._bin_centers[1][k].numpy() for k in ["omega", "C:1N:1CA", "phi"]])
+    arrays["prior_weights"] = np.stack([bpe._bin_weights[1][k].numpy() for k in ["omega", "C:1N:1CA", "phi"]])
+    arrays["thresholds"] = np.stack([np.asarray(bpe._thresholds[1][k], dtype=np.float64)
+                                     for k in ["omega", "C:1N:1CA", "phi"]])
+    meta["lbfgs"] = [{k: v for k, v in r.items() if k != "opt"} for r in rec]
+
+
+def main(argv):
+    if len(argv) >= 2 and argv[0] == "--one":
+        run_one(argv[1])
+        return
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg", SLURM_CPUS_PER_TASK="2",
+               PYTHONBREAKPOINT="0")
+    for name in argv or list(FIXTURES):
+        r = subprocess.run([sys.executable, "-W", "ignore", __file__, "--one", name], env=env,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        out = [ln for ln in r.stdout.splitlines() if ln.startswith(name + ":")]
+        print(out[-1] if out and r.returncode == 0 else f"{name}: rc={r.returncode} {r.stderr[-800:]}", flush=True)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])

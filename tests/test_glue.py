@@ -1,0 +1,197 @@
+"""Glue optimisation of the RMSD mode (bpe.py:106-135, 192-229, 423-578,
+739-807, 2027-2071) against the reference's own outputs.
+
+Fixtures: tests/golden/gl_*.json|npz, made by tests/golden/make_glue_golden.py running
+foldingdiff.bpe.BPE(glue_opt=True, glue_opt_method="all") as bin/encode.py drives it
+(initialize, glue_opt_all, bin, step).  They hold the reference optimiser's own optimum for
+every chain (LBFGS.step wrapped, before snapping), the cached exit frames, the geometry after
+initialize / glue_opt_all / the steps, and every merge popped.
+
+- oracle/glue.py (torch restatement) reproduces the reference's optimum bit for bit (CPU);
+- the device kernel (csrc/glue.h, one chain per thread, through the C-ABI) lands within
+  GLUE_TOL rad of it and snaps every glue to the reference's bin (GPU);
+- RmsdBPE(glue_opt=True) reproduces the geometry after glue_opt_all and the whole merge
+  sequence with its glue re-optimisations (GPU; and on the CPU with the oracle standing in
+  for the device launch).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
+NAMES = ["gl_all_p0", "gl_all_p0_prior"]
+GLUE_TOL = 2e-3  # rad: device optimum vs the reference's (float32 L-BFGS, 20 iterations)
+
+
+def _load(name):
+    with open(os.path.join(GOLDEN, name + ".json")) as f:
+        meta = json.load(f)
+    with np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False) as z:
+        arrs = {k: z[k] for k in z.files}
+    return meta, arrs
+
+
+def _problems(meta, arrs):
+    """Per chain: packed geometry after initialize(), start glues, target frames."""
+    from geobpe.glue import pack_chain
+    ro = arrs["row_off"]
+    geos, x0s, tgts = [], [], []
+    fo = 0
+    for ci in range(len(ro) - 1):
+        a, b = int(ro[ci]), int(ro[ci + 1])
+        n = b - a
+        g = pack_chain({c: arrs[f"init_{c}"][a:b] for c in COLS}, arrs["init_init"][ci])
+        geos.append(g)
+        x0s.append(g[:n - 1][:, [7, 5, 8]].astype(np.float32))
+        tgts.append((arrs["frames_R"][fo:fo + n - 1], arrs["frames_t"][fo:fo + n - 1]))
+        fo += n - 1
+    return geos, x0s, tgts
+
+
+def _prior(meta, arrs):
+    c, w = arrs["prior_centers"], arrs["prior_weights"]
+    return [(c[t], w[t]) for t in range(3)], float(meta["glue_opt_prior"])
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_oracle_matches_reference_optimum(name):
+    from oracle import glue as og
+    meta, arrs = _load(name)
+    prior, lam = _prior(meta, arrs)
+    go = 0
+    for ci, (g, x0, (R, t)) in enumerate(zip(*_problems(meta, arrs))):
+        opt, it, ev, l0, l1 = og.optimize(g, x0, R, t, prior, lam)
+        want = arrs["lbfgs_opt"][go:go + len(x0)]
+        go += len(x0)
+        assert np.array_equal(opt, want.astype(np.float32)), f"chain {ci}"
+        rec = meta["lbfgs"][ci]
+        assert (it, ev, l0, l1) == (rec["n_iter"], rec["func_evals"], rec["loss0"], rec["loss"])
+
+
+def _snap_all(opt, thr):
+    from geobpe.glue import snap_bin
+    return np.array([[snap_bin(thr[t], v) for t, v in enumerate(row)] for row in opt])
+
+
+def _glued(arrs, ci, n):
+    a = int(arrs["row_off"][ci])
+    om = arrs["glued_omega"][a:a + n - 1]
+    cn = arrs["glued_C:1N:1CA"][a:a + n - 1]
+    ph = arrs["glued_phi"][a + 1:a + n]
+    return np.stack([om, cn, ph], axis=1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_device_glue_opt_matches_reference(name):
+    from geobpe import glue as G
+    meta, arrs = _load(name)
+    geos, x0s, tgts = _problems(meta, arrs)
+    (pc, pw), lam = zip(*_prior(meta, arrs)), float(meta["glue_opt_prior"])
+    table = np.zeros((1, 3, 2, pc[0].shape[0]), np.float32)
+    for t in range(3):
+        table[0, t, 0], table[0, t, 1] = pc[t], pw[t]
+    counts = np.full((1, 3), pc[0].shape[0], np.int32)
+    outs, stats, loss = G.optimize_chains(geos, x0s, tgts, [0] * len(geos), (table, counts), lam)
+    thr = [[tuple(e) for e in arrs["thresholds"][t]] for t in range(3)]
+    go = 0
+    for ci, (opt, x0) in enumerate(zip(outs, x0s)):
+        want = arrs["lbfgs_opt"][go:go + len(x0)]
+        go += len(x0)
+        d = np.abs(opt.astype(np.float64) - want)
+        d = np.minimum(d, 2 * np.pi - d)
+        assert d.max() < GLUE_TOL, f"chain {ci}: max |device - reference| = {d.max()}"
+        assert np.array_equal(_snap_all(opt, thr), _glued(arrs, ci, len(x0) + 1)), f"chain {ci} snapped"
+        rec = meta["lbfgs"][ci]
+        assert abs(loss[ci, 0] - rec["loss0"]) < 1e-6 * rec["loss0"]
+        assert abs(loss[ci, 1] - rec["loss"]) < 1e-3 * rec["loss"]
+
+
+def run_and_compare(name):
+    from geobpe.bpe import BPE
+    from geobpe.rmsd_bpe import RmsdBPE
+    meta, arrs = _load(name)
+    corpus = {k: arrs[k] for k in COLS + ["row_off"]}
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()},
+              rmsd_partition_min_size=meta["rmsd_partition_min_size"], rmsd_super_res=meta["rmsd_super_res"],
+              num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta["std_bonds"],
+              glue_opt=True, glue_opt_prior=meta["glue_opt_prior"], glue_opt_every=meta["glue_opt_every"],
+              glue_opt_method=meta["glue_opt_method"], seed=meta["rng_seed"])
+    assert isinstance(bpe, RmsdBPE)
+    popped = []
+    inner = bpe._merge
+
+    def recording():
+        popped.append(list(bpe._priority[0]))
+        return inner()
+
+    bpe._merge = recording
+    bpe.initialize()
+    _geometry_equal(bpe, arrs, "init")
+    bpe.glue_opt_all()
+    _geometry_equal(bpe, arrs, "glued")
+    bpe.bin()
+    for call in meta["calls"]:
+        n0 = len(popped)
+        bpe.step()
+        assert popped[n0:] == call["popped"], f"merge {len(popped)}"
+        assert (bpe._step, len(bpe._tokens)) == (call["step"], call["n_tokens"])
+    assert [[list(s) for s in x] for x in _segmentation(bpe)] == meta["segmentation"]
+    _geometry_equal(bpe, arrs, "final")
+    return bpe
+
+
+def _segmentation(bpe):
+    return [[[s, list(v[1]) if isinstance(v[1], tuple) else v[1], v[2]] for s, v in t.bond_to_token.items()]
+            for t in bpe.tokenizers]
+
+
+def _geometry_equal(bpe, arrs, tag):
+    g = bpe.geometry()
+    for c in COLS:
+        a, b = g[c], arrs[f"{tag}_{c}"]
+        assert a.shape == b.shape and np.array_equal(a, b, equal_nan=True), f"{tag} geometry {c}"
+    assert np.array_equal(np.array([ch.init for ch in bpe._chains]), arrs[f"{tag}_init"]), f"{tag} init"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", NAMES)
+def test_rmsd_mode_glue_opt_device_matches_reference(name):
+    bpe = run_and_compare(name)
+    assert bpe.glue_calls >= 2  # glue_opt_all and at least one re-optimisation in step()
+
+
+@pytest.fixture
+def host_glue(monkeypatch):
+    """The oracle's numpy NeRF / Kabsch / thresholds and the torch optimiser restatement in
+    place of the device batches."""
+    import oracle.glue as og
+    import oracle.prologue as prologue
+    import oracle.rmsd as orm
+    from geobpe import glue, rmsd, rmsd_bpe
+
+    monkeypatch.setattr(rmsd, "geo_coords", lambda geos, device=0: [orm.nerf(g) for g in geos])
+    monkeypatch.setattr(rmsd, "rmsd_matrix", lambda S, device=0: orm.rmsd_matrix(S))
+    monkeypatch.setattr(rmsd, "rmsd_cross", lambda A, B, device=0: np.array([[orm.rmsd(a, b) for b in B] for a in A]))
+    monkeypatch.setattr(rmsd_bpe.RmsdBPE, "_grid_thresholds",
+                        lambda self: {s: prologue.thresholds(self._corpus, b) for s, b in self.bins.items()})
+
+    def opt_chains(geos, x0s, targets, grids, prior, lam, device=0, w_rot=1.0, w_trans=0.1):
+        table, counts = prior
+        outs = []
+        for g, x0, (R, t), gi in zip(geos, x0s, targets, grids):
+            pr = [(table[gi, k, 0, :counts[gi, k]], table[gi, k, 1, :counts[gi, k]]) for k in range(3)]
+            outs.append(og.optimize(g, x0, R, t, pr, lam)[0])
+        return outs, None, None
+
+    monkeypatch.setattr(glue, "optimize_chains", opt_chains)
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_rmsd_mode_glue_opt_host_logic_matches_reference(name, host_glue):
+    run_and_compare(name)
