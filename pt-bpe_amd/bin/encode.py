@@ -18,9 +18,12 @@ Differences (all outside SURVEY.md §8's hot path):
   * ``--run-chunk M`` (ours): merges issued per device call between host
     syncs; the reference steps one at a time.  Outputs do not depend on it.
 
-Out-of-scope flag values (res-init false, free bonds, p-min-size < inf,
-glue-opt, uniform bins, multi-grid --bins) raise NotImplementedError from
-geobpe.bpe.BPE before any work starts.
+Out-of-scope flag values (res-init false, --glue-opt-method each, glue-opt
+without --p-min-size, uniform bins with free bonds) raise NotImplementedError
+from geobpe.bpe.BPE before any work starts.  With --p-min-size < inf the run is
+the RMSD-partitioned mode (geobpe.rmsd_bpe.RmsdBPE); --glue-opt true with
+--glue-opt-method all runs glue_opt_all after initialize (encode.py:331-332) and
+the per-step re-optimisation, on the device.
 """
 from __future__ import annotations
 
@@ -83,6 +86,10 @@ def parse_args(argv=None):
     p.add_argument("--max-num-strucs", type=int, default=500)
     p.add_argument("--rmsd-super-res", type=str2bool, default=False)
     p.add_argument("--glue-opt", type=str2bool, default=False)
+    p.add_argument("--glue-opt-prior", type=float, default=0.0)
+    p.add_argument("--glue-opt-every", type=int, default=10)
+    p.add_argument("--glue-opt-method", choices=["each", "all"], default="each",
+                   help="RMSD mode: 'all' runs (device L-BFGS); 'each' is not built")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--save-every", type=int, default=10)
     p.add_argument("--run-chunk", type=int, default=0, help="merges per device call (0: = save-every)")
@@ -209,12 +216,15 @@ def main(argv=None) -> int:
         group = TorchGroup(int(shard["row_off"][-1]), device=device)
     bpe = BPE(shard, bins=args.bins, bin_strategy=args.bin_strategy, save_dir=args.save_dir,
               res_init=args.res_init, std_bonds=not args.free_bonds,
-              rmsd_partition_min_size=args.p_min_size, glue_opt=args.glue_opt, seed=args.seed,
+              rmsd_partition_min_size=args.p_min_size, glue_opt=args.glue_opt, glue_opt_prior=args.glue_opt_prior,
+              glue_opt_every=args.glue_opt_every, glue_opt_method=args.glue_opt_method, seed=args.seed,
               num_partitions=args.num_p, max_num_strucs=args.max_num_strucs, rmsd_super_res=args.rmsd_super_res,
               device=device, record_tree=args.ckpt_format == "pkl", group=group,
               global_corpus=corpus if group is not None else None)
     t0 = time.time()
     bpe.initialize()
+    if args.glue_opt and args.glue_opt_method == "all":  # encode.py:331-332
+        bpe.glue_opt_all()
     st = stats(bpe)  # (every rank takes part in the gather; rank 0 writes)
     if rank == 0:
         with open(os.path.join(args.save_dir, "initial_stats=-1.json"), "w") as f:

@@ -31,8 +31,9 @@ Reachable configurations (tests/golden/rmsd_mode_probe.json, rm_p4.json): p <= 3
 the residues at initialize() and every merge; p >= 4 never creates ``_sphere_dict``, so the
 first merge of >= p bonds raises AttributeError there, as it does here.  Glue optimisation
 (``glue_opt=True``, ``glue_opt_method="all"``, bpe.py:106-135, 192-229, 2027-2071) runs as one
-device L-BFGS launch over the chains (geobpe/glue.py, csrc/glue.h).  Not built: the "each"
-glue method and ``rmsd_only``.  Free bond lengths
+device L-BFGS launch over the chains (geobpe/glue.py, csrc/glue.h).  The "each" method
+stops where the reference's does (an AssertionError in initialize(), bpe.py:761).  Not
+built: ``rmsd_only``.  Free bond lengths
 (``std_bonds=False``) run where the reference runs them (p <= 2; p >= 3 raises its KeyError).
 """
 from __future__ import annotations
@@ -273,9 +274,8 @@ class RmsdBPE:
             raise NotImplementedError("the RMSD mode needs res_init=True (bond-level init is not built)")
         if not std_bonds and bin_strategy == "uniform":
             raise NotImplementedError("free bonds with uniform (equal-count) bins are not built")
-        if glue_opt and glue_opt_method != "all":
-            raise NotImplementedError("glue_opt_method='each' (per-occurrence glue opt, bpe.py:365-369, "
-                                      "1978-1982) is not built; 'all' is (geobpe/glue.py)")
+        if glue_opt and glue_opt_method not in ("all", "each"):
+            raise ValueError(f"glue_opt_method must be 'all' or 'each', not {glue_opt_method!r}")
         if rmsd_only or compute_sec_structs:
             raise NotImplementedError("rmsd_only / secondary-structure priorities are not built")
         if isinstance(structures, dict) and "row_off" in structures:
@@ -434,7 +434,7 @@ class RmsdBPE:
                 bt = BOND_TYPES[j % 3]
                 v = self._centre(bt, _get_ind(c.geo(j, 1)[bt][0], self._thresholds[1][bt]), 1)
                 c.set_geo(j, 1, {bt: [v]})
-        if self.glue_opt:  # exit frames of the bond-standardized chains (bpe.py:192-229)
+        if self.glue_opt and self.glue_opt_method == "all":  # exit frames, bond-standardized (bpe.py:192-229)
             from .glue import exit_frames
             self._exit_frames = exit_frames(self._chains, device=self.device)
         label_dict, res_geo, labels = {}, {}, []
@@ -466,6 +466,12 @@ class RmsdBPE:
         for ci, c in enumerate(self._chains):
             c.btt = {3 * i: (3 * i, labels[ci][i], 3 if i < c.n - 1 else 2) for i in range(c.n)}
             c.token_pos = [3 * (j // 3) for j in range(3 * c.n - 1)]
+        if res_geo and self.glue_opt and self.glue_opt_method == "each" and \
+                any(start > 0 for occ in res_geo.values() for _, start, _ in occ):
+            # the reference's "each" method calls opt_glue without bin centres in the main
+            # process (bpe.py:365-369) and stops at its assert (bpe.py:761); with p >= 4 no
+            # residue is partitioned and the first RMSD merge raises AttributeError instead
+            raise AssertionError("opt_glue: bin_centers is None and BIN_CENTERS is not set (bpe.py:761)")
         if res_geo:
             self._sphere_dict = {}
             self._tokens = {}

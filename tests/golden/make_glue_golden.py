@@ -40,7 +40,7 @@ COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:
 
 
 def _id(v):
-    return [int(x) for x in v] if isinstance(v, tuple) else int(v)
+    return [int(x) for x in v] if isinstance(v, tuple) else (None if v is None else int(v))
 
 
 def run_one(name):

@@ -195,3 +195,17 @@ def host_glue(monkeypatch):
 @pytest.mark.parametrize("name", NAMES)
 def test_rmsd_mode_glue_opt_host_logic_matches_reference(name, host_glue):
     run_and_compare(name)
+
+
+def test_each_method_raises_like_reference(host_glue):
+    """glue_opt_method="each" (bin/encode.py's default): the reference stops in initialize()
+    at opt_glue's assert (bpe.py:761; gl_each_p0 records it)."""
+    from geobpe.bpe import BPE
+    meta, arrs = _load("gl_each_p0")
+    assert meta["raised"]["stage"] == "initialize" and meta["raised"]["type"] == "AssertionError"
+    corpus = {k: arrs[k] for k in COLS + ["row_off"]}
+    bpe = BPE(corpus, bins={1: 5}, rmsd_partition_min_size=0, num_partitions={int(k): v for k, v in
+              meta["num_partitions"].items()}, max_num_strucs=60, res_init=True, glue_opt=True,
+              glue_opt_method="each", seed=0)
+    with pytest.raises(AssertionError):
+        bpe.initialize()

@@ -147,7 +147,7 @@ def test_rmsd_mode_dispatch_and_scope():
     _, corpus, _ = _load(NAMES[0])
     assert isinstance(BPE(corpus, bins={1: 5}, res_init=True), RmsdBPE)  # the reference's default p = 4
     with pytest.raises(NotImplementedError):
-        BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=3, glue_opt=True, glue_opt_method="each")
+        BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=3, rmsd_only=True)
     assert not isinstance(BPE.__new__(BPE, corpus, bins={1: 5}, res_init=True,
                                       rmsd_partition_min_size=float("inf")), RmsdBPE)
 
