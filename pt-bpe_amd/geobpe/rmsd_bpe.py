@@ -497,30 +497,37 @@ class RmsdBPE:
         cached exit frames (bin/encode.py:331-332 calls it after initialize())."""
         self._glue_opt(range(self.n))
 
-    def _glue_opt(self, cis):
-        """_opt_glue_worker + opt_glue (bpe.py:739-807) for the chains cis, as one device
-        launch: glue k = (omega_k, C:1N:1CA_k, phi_{k+1}) of every initial token but the last,
-        started from the current values, aimed at exit frame (start + length) // 3 - 1 of the
-        cached chain; the optimum snapped to grid(3n - 4)'s bins and written back.  Returns
-        the chains' indices."""
-        from . import glue as G
-        cis = list(cis)
-        if not cis:
-            return cis
-        sizes = sorted(self.bins)
+    def _glue_prior_tables(self):
+        """_bin_centers / _bin_weights of every grid (bpe.py:834-872) as device tables."""
         if not hasattr(self, "_glue_prior"):
+            from . import glue as G
+            sizes = sorted(self.bins)
             counts = self._bin_count_values()
             self._glue_prior = G.prior_tables([self._thresholds[s0] for s0 in sizes], [counts[s0] for s0 in sizes])
+        return self._glue_prior
+
+    def _glue_opt(self, cis, chains=None, frames=None):
+        """_opt_glue_worker + opt_glue (bpe.py:739-807) for the chains cis (or the given
+        chain objects and their cached frames), as one device launch: glue k = (omega_k,
+        C:1N:1CA_k, phi_{k+1}) of every initial token but the last, started from the current
+        values, aimed at exit frame (start + length) // 3 - 1 of the cached chain; the optimum
+        snapped to grid(3n - 4)'s bins and written back.  Returns cis."""
+        from . import glue as G
+        cis = list(cis)
+        if chains is None:
+            chains = [self._chains[ci] for ci in cis]
+            frames = [self._exit_frames[ci] for ci in cis]
+        if not chains:
+            return cis
+        sizes = sorted(self.bins)
         geos, x0s, tgts, grids = [], [], [], []
-        for ci in cis:
-            c = self._chains[ci]
+        for c, (R, t) in zip(chains, frames):
             g = G.pack_chain(c.cur, c.init)
             toks = c.tokens0[:-1]
             geos.append(g)
             x0s.append(np.stack([[c.cur["omega"][(i + ln) // 3 - 1], c.cur["C:1N:1CA"][(i + ln) // 3 - 1],
                                   c.cur["phi"][(i + ln) // 3]] for i, _, ln in toks]).astype(np.float32)
                        if toks else np.zeros((0, 3), np.float32))
-            R, t = self._exit_frames[ci]
             rows = [(i + ln) // 3 - 1 for i, _, ln in toks]  # R_occs[res_no - 2], bpe.py:751-755
             tgts.append((R[rows], t[rows]))
             L = 3 * c.n - 4
@@ -528,11 +535,10 @@ class RmsdBPE:
         if any(len(x) != len(g) - 1 for x, g in zip(x0s, geos)):
             raise NotImplementedError("glue opt over initial tokens other than one per residue")
         lam = float(self.glue_opt_prior) if self.glue_opt_prior and self.glue_opt_prior > 0.0 else 0.0
-        outs, stats, _ = G.optimize_chains(geos, x0s, tgts, [sizes.index(k) for k in grids], self._glue_prior, lam,
-                                           device=self.device)
+        outs, _, _ = G.optimize_chains(geos, x0s, tgts, [sizes.index(k) for k in grids], self._glue_prior_tables(),
+                                       lam, device=self.device)
         self.glue_calls = getattr(self, "glue_calls", 0) + 1
-        for ci, opt, gk in zip(cis, outs, grids):
-            c = self._chains[ci]
+        for c, opt, gk in zip(chains, outs, grids):
             thr = self._thresholds[gk]
             for k, (i, _, ln) in enumerate(c.tokens0[:-1]):
                 row = (i + ln) // 3 - 1
@@ -857,6 +863,13 @@ class RmsdBPE:
                 ind = 0 if x < thr[0][0] else (len(thr) - 1 if x > thr[-1][1] else _get_ind(x, thr))
                 v = sum(thr[ind]) / 2
             c.set_geo(j, 1, {bt: [v]})
+        if self.glue_opt and self.glue_opt_method == "each" and c.n > 1:
+            # opt_glue without bin centres in this process (bpe.py:1090-1093, 761)
+            raise AssertionError("opt_glue: bin_centers is None and BIN_CENTERS is not set (bpe.py:761)")
+        frames = None
+        if self.glue_opt:  # t.cached_all_frames (bpe.py:1062-1063)
+            from .glue import exit_frames
+            frames = exit_frames([c], device=self.device)
         res_geo = {}
         for i in range(c.n):
             res_geo.setdefault(3 if i < c.n - 1 else 2, []).append(3 * i)
@@ -879,7 +892,9 @@ class RmsdBPE:
                 c.set_geo(s0, size, self._tokens[(n, p)])
                 c.btt[s0] = (s0, (n, p), size)
         c.tokens0 = list(c.btt.values())
-        for k in GLUE:  # grid-1 glue centres, NaN kept (bpe.py:1101-1108)
+        if self.glue_opt:  # glue_opt "all" (bpe.py:1109-1112)
+            self._glue_opt([0], [c], frames)
+        for k in (GLUE if not self.glue_opt else []):  # grid-1 glue centres, NaN kept (bpe.py:1101-1108)
             col = c.cur[k]
             for r in range(c.n):
                 v = col[r]
@@ -894,14 +909,17 @@ class RmsdBPE:
         if len(uniq) != len(keys):
             raise AssertionError("_tokens and _sphere_dict out of step")
         metrics = {"L": [len(c.btt)]}
+        count = 0
         for n, key in zip(uniq[2:], keys[2:]):
             if key in geo_dict:
-                self._step_helper(geo_dict, c, key, n)
+                self._step_helper(geo_dict, c, key, n, opt=count % self.glue_opt_every == 0, frames=frames)
+                count += 1
             metrics["L"].append(len(c.btt))
         return RmsdTokenizer(c, self.device), metrics
 
-    def _step_helper(self, geo_dict, c, key, n):
-        """step() on one chain for a trained key (bpe.py:1316-1404)."""
+    def _step_helper(self, geo_dict, c, key, n, opt=False, frames=None):
+        """step() on one chain for a trained key (bpe.py:1316-1425), with the glue
+        re-optimisation of glue_opt "all" when opt (bpe.py:1405-1424)."""
         key_dict = json.loads(key)
         length = sum(len(key_dict.get(k, [])) for k in BOND_TYPES)
         vals = list(geo_dict[key])
@@ -950,6 +968,15 @@ class RmsdBPE:
             if right:
                 geo_dict[self._pair_key(c, i1, length, l3)].add(i3)
             last_i1 = i1
+        if self.glue_opt and self.glue_opt_method == "all" and opt and not self.rmsd_only:
+            toks = c.tokens()
+            old = [self._pair_key(c, i1, l1, l2) for (i1, _, l1), (_, _, l2) in zip(toks, toks[1:])]
+            self._glue_opt([0], [c], frames)
+            for ((i1, _, l1), (i2, _, l2)), ok in zip(zip(toks, toks[1:]), old):
+                nk = self._pair_key(c, i1, l1, l2)
+                if nk != ok:
+                    geo_dict[ok].remove(i2)
+                    geo_dict[nk].add(i2)
 
     # ------------------------------------------------------------ views / encode
     @property
@@ -1104,8 +1131,23 @@ class RmsdBPE:
             setattr(self, k, getattr(obj, k, None))
         self.rmsd_super_res = bool(self.rmsd_super_res)
         self.std_bonds = True if self.std_bonds is None else bool(self.std_bonds)
-        if self.glue_opt or self.rmsd_only:
-            raise NotImplementedError("checkpoints trained with glue_opt / rmsd_only")
+        if self.rmsd_only:
+            raise NotImplementedError("checkpoints trained with rmsd_only")
+        if self.glue_opt:  # the prior tables from the checkpoint's _bin_centers / _bin_weights
+            from .glue import GLUE
+
+            def arr(v):
+                return np.asarray(v.numpy() if hasattr(v, "numpy") else v, dtype=np.float32)
+            sizes = sorted(self.bins)
+            kmax = max(len(arr(dict.__getitem__(obj._bin_centers, s0)[k])) for s0 in sizes for k in GLUE)
+            table = np.zeros((len(sizes), 3, 2, kmax), dtype=np.float32)
+            counts = np.zeros((len(sizes), 3), dtype=np.int32)
+            for gi, s0 in enumerate(sizes):
+                for t, k in enumerate(GLUE):
+                    c = arr(dict.__getitem__(obj._bin_centers, s0)[k])
+                    w = arr(dict.__getitem__(obj._bin_weights, s0)[k])
+                    table[gi, t, 0, :len(c)], table[gi, t, 1, :len(w)], counts[gi, t] = c, w, len(c)
+            self._glue_prior = (table, counts)
         thr = ThresholdDict()
         for k, v in dict.items(obj._thresholds):
             thr[k] = v

@@ -36,6 +36,9 @@ FIXTURES = {
     "gl_all_p0_prior": (6, 12, 30, 42, 5, 0, True, "all", 1.0, 1, 6),
     "gl_each_p0": (5, 10, 20, 43, 5, 0, False, "each", 0.0, 10, 6),
 }
+# BPE.tokenize (the RMSD mode's induce, bpe.py:1053-1140, with glue_opt "all") of these
+# training chains after the steps
+INDUCE = {"gl_all_p0": [0, 3], "gl_all_p0_prior": [1, 4]}
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
 
@@ -117,6 +120,28 @@ def run_one(name):
     except BaseException as e:  # noqa: BLE001 - the fixture records what the reference raises
         meta["raised"] = {"stage": stage, "type": type(e).__name__, "msg": str(e)[:300],
                           "popped_so_far": popped[-1:], "where": traceback.format_exc().splitlines()[-6:]}
+    if not meta["raised"] and name in INDUCE:
+        from make_rmsd_mode_golden import _Chain
+        RB.ProteinChain = _Chain
+        out = []
+        ro = corpus["row_off"]
+        for i in INDUCE[name]:  # training chains, tokenized afresh
+            row = {c: np.asarray(corpus[c][ro[i]:ro[i + 1]], dtype=np.float64) for c in COLS}
+            s = Tokenizer.init_structure(len(row["phi"]))
+            for c in COLS:
+                s["angles"][c] = row[c]
+            s["fname"] = f"induce_{i}"
+            try:
+                t, metrics = bpe.tokenize(Tokenizer(s))
+            except Exception as e:  # noqa: BLE001 - recorded
+                out.append({"chain": i, "raised": type(e).__name__, "msg": str(e)[:200]})
+                continue
+            out.append({"chain": i, "segmentation": [[int(a), _id(v[1]), int(v[2])] for a, v in t.bond_to_token.items()],
+                        "L": [int(x) for x in metrics["L"]]})
+            for c in COLS:
+                arrays[f"induce{i}_{c}"] = np.array([float(x) for x in t.angles_and_dists[c]])
+            arrays[f"induce{i}_init"] = np.array([float(t._init_n_ca), float(t._init_ca_c), float(t._init_bond_angle)])
+        meta["induce"] = out
     geometry(bpe, "final", arrays)
     meta["tokens"] = [[_id(k), v] for k, v in bpe._tokens.items()]
     meta["segmentation"] = segmentation(bpe)
