@@ -48,6 +48,24 @@ struct GlueProb {
   int64_t pmax;
 };
 
+// float32 elementary functions rounded from float64: the reference's float32 torch ops on
+// the CPU (glibc / SLEEF, ~correctly rounded) are matched more closely than by the ~1-2 ulp
+// single-precision device library, and the trajectory of 20 L-BFGS iterations amplifies
+// every ulp
+#ifdef GLUE_DEVICE_TRIG  // A/B build switch: the single-precision device library
+__device__ inline float f_sin(float a) { return sinf(a); }
+__device__ inline float f_cos(float a) { return cosf(a); }
+__device__ inline float f_atan2(float y, float x) { return atan2f(y, x); }
+__device__ inline float f_exp(float a) { return expf(a); }
+__device__ inline float f_log(float a) { return logf(a); }
+#else
+__device__ inline float f_sin(float a) { return (float)sin((double)a); }
+__device__ inline float f_cos(float a) { return (float)cos((double)a); }
+__device__ inline float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
+__device__ inline float f_exp(float a) { return (float)exp((double)a); }
+__device__ inline float f_log(float a) { return (float)log((double)a); }
+#endif
+
 struct IV {  // a strided float vector of one chain
   float* p;
   int64_t S;
@@ -57,15 +75,23 @@ struct IV {  // a strided float vector of one chain
 __device__ inline float glue_wrap(float a) {
   // torch.remainder(torch.atan2(sin a, cos a) + 2 pi, 2 pi) on float32 (bpe.py:490-493)
   const float two_pi = 6.28318530717958647692f;
-  float w = atan2f(sinf(a), cosf(a)) + two_pi;
+  float w = f_atan2(f_sin(a), f_cos(a)) + two_pi;
   float r = fmodf(w, two_pi);
   if (r < 0.f) r += two_pi;
   return r;
 }
 
+// autograd of glue_wrap: remainder passes the gradient; atan2(y = sin a, x = cos a) gives
+// g x / (y^2 + x^2) to y and -g y / (y^2 + x^2) to x; then sin' = cos, cos' = -sin
+__device__ inline float glue_wrap_back(float a, float g) {
+  const float y = f_sin(a), x = f_cos(a);
+  const float den = y * y + x * x;
+  return (g * x / den) * x + (g * -y / den) * (-y);
+}
+
 // the placement offsets (float32, place_dihedral's d before .type(m.dtype), nerf.py:200-207)
 __device__ inline void glue_d(float A, float L, float T, float& d0, float& d1, float& d2) {
-  const float cA = cosf(A), sA = sinf(A), cT = cosf(T), sT = sinf(T);
+  const float cA = f_cos(A), sA = f_sin(A), cT = f_cos(T), sT = f_sin(T);
   d0 = -L * cA;
   d1 = L * cT * sA;
   d2 = L * sT * sA;
@@ -103,9 +129,10 @@ __device__ inline void glue_place_back(V3 a, V3 b, V3 c, float A, float L, float
   glue_d(A, L, T, f0, f1, f2);
   // d (float64 after the cast) -> the float32 gradient of d, then float32 chain rule
   const float g0 = (float)v_dot(G, bc), g1 = (float)v_dot(G, nbc), g2 = (float)v_dot(G, n);
-  const float cA = cosf(A), sA = sinf(A), cT = cosf(T), sT = sinf(T);
-  gA = g0 * (L * sA) + g1 * (L * cT) * cA + g2 * (L * sT) * cA;
-  gT = g1 * (-(L * sT)) * sA + g2 * (L * cT) * sA;
+  // autograd's float32 chain through d0 = (-L) cos A, d1 = (L cos T) sin A, d2 = (L sin T) sin A
+  const float cA = f_cos(A), sA = f_sin(A), cT = f_cos(T), sT = f_sin(T);
+  gA = ((g0 * (-L)) * (-sA) + (g1 * (L * cT)) * cA) + (g2 * (L * sT)) * cA;
+  gT = ((g1 * sA) * L) * (-sT) + ((g2 * sA) * L) * cT;
   gc = v_addv(gc, G);
   V3 g_bc = v_scale(G, (double)f0);
   const V3 g_nbc = v_scale(G, (double)f1);
@@ -213,14 +240,14 @@ __device__ double glue_eval(const GlueProb& P, int64_t s, int64_t r, const doubl
       const float* cen = pr + (2 * t) * P.kmax;
       const float* wt = cen + P.kmax;
       float mx = -INFINITY;
-      for (int j = 0; j < kc[t]; j++) mx = fmaxf(mx, kappa * cosf(a - cen[j]) + logf(wt[j] + 1e-12f));
+      for (int j = 0; j < kc[t]; j++) mx = fmaxf(mx, kappa * f_cos(a - cen[j]) + f_log(wt[j] + 1e-12f));
       float se = 0.f, sg = 0.f;
       for (int j = 0; j < kc[t]; j++) {
-        const float e = expf(kappa * cosf(a - cen[j]) + logf(wt[j] + 1e-12f) - mx);
+        const float e = f_exp(kappa * f_cos(a - cen[j]) + f_log(wt[j] + 1e-12f) - mx);
         se += e;
-        sg += e * kappa * sinf(a - cen[j]);
+        sg += e * kappa * f_sin(a - cen[j]);
       }
-      term += -(mx + logf(se));
+      term += -(mx + f_log(se));
       gp[t] = P.lam * (sg / se);
     }
     prior += term;
@@ -254,6 +281,7 @@ __device__ double glue_eval(const GlueProb& P, int64_t s, int64_t r, const doubl
     stx(AX, S, j - 2, gbv);
     stx(AX, S, j - 1, gc);
   }
+  for (int64_t i = 0; i < 3 * (r - 1); i++) grad[i] = glue_wrap_back(x[i], grad[i]);
   return loss;
 }
 

@@ -35,6 +35,11 @@ FIXTURES = {
     "gl_all_p0": (6, 12, 30, 41, 5, 0, False, "all", 0.0, 10, 12),
     "gl_all_p0_prior": (6, 12, 30, 42, 5, 0, True, "all", 1.0, 1, 6),
     "gl_each_p0": (5, 10, 20, 43, 5, 0, False, "each", 0.0, 10, 6),
+    # config 1's corpus (the reference's bundled PDBs, featurised by pdb_angles.py) in the
+    # README's first run: --bins 1-50, p = 0, --num-p 2-2:3-5:5-1:6-2:8-1, 500 structures,
+    # free bonds, rmsd_super_res, glue opt "all" with prior 0 every 10 steps; 20 merges
+    "gl_pdb72_readme": ("pdb72", None, None, 0, 50, 0, True, "all", 0.0, 10, 20,
+                        {"num_p": {2: 2, 3: 5, 5: 1, 6: 2, 8: 1}, "std_bonds": False, "max_num_strucs": 500}),
 }
 # BPE.tokenize (the RMSD mode's induce, bpe.py:1053-1140, with glue_opt "all") of these
 # training chains after the steps
@@ -51,8 +56,15 @@ def run_one(name):
     from geobpe import synth
     from make_golden import _stub_optional_deps
 
-    nch, lo, hi, seed, B, p, sup, method, prior, every, calls = FIXTURES[name]
-    corpus = synth.make_corpus(synth.make_lengths(nch, lo, hi, seed=seed), seed=seed)
+    nch, lo, hi, seed, B, p, sup, method, prior, every, calls = FIXTURES[name][:11]
+    extra = FIXTURES[name][11] if len(FIXTURES[name]) > 11 else {}
+    num_p, std, maxs = extra.get("num_p", NUM_P), extra.get("std_bonds", True), extra.get("max_num_strucs", 60)
+    if nch == "pdb72":
+        import pdb_angles
+        corpus, _ = pdb_angles.pdb_dir_corpus("/root/reference/data/vqvae_pretrain/train")
+        nch = len(corpus["row_off"]) - 1
+    else:
+        corpus = synth.make_corpus(synth.make_lengths(nch, lo, hi, seed=seed), seed=seed)
     _stub_optional_deps()
     sys.path.insert(0, "/root/reference")
     import foldingdiff.bpe as RB
@@ -89,14 +101,14 @@ def run_one(name):
 
     meta = {"name": name, "n_chains": nch, "len_lo": lo, "len_hi": hi, "seed": seed, "bins": {"1": B},
             "rmsd_partition_min_size": p, "rmsd_super_res": sup, "glue_opt_method": method,
-            "glue_opt_prior": prior, "glue_opt_every": every, "num_partitions": {str(k): v for k, v in NUM_P.items()},
-            "max_num_strucs": 60, "std_bonds": True, "rng_seed": 0, "calls": [], "raised": None,
+            "glue_opt_prior": prior, "glue_opt_every": every, "num_partitions": {str(k): v for k, v in num_p.items()},
+            "max_num_strucs": maxs, "std_bonds": std, "rng_seed": 0, "calls": [], "raised": None,
             "generator": "tests/golden/make_glue_golden.py (reference: /root/reference foldingdiff/bpe.py, "
                          "run in the build container)"}
     arrays = dict(corpus)
     bpe = RB.BPE(structs, bins={1: B}, save_dir=tempfile.mkdtemp(prefix="geobpe_glue_golden_"),
-                 rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(NUM_P), max_num_strucs=60,
-                 res_init=True, std_bonds=True, glue_opt=True, glue_opt_prior=prior, glue_opt_every=every,
+                 rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(num_p), max_num_strucs=maxs,
+                 res_init=True, std_bonds=std, glue_opt=True, glue_opt_prior=prior, glue_opt_every=every,
                  glue_opt_method=method, seed=0)
     stage = "initialize"
     try:
@@ -104,7 +116,7 @@ def run_one(name):
         geometry(bpe, "init", arrays)
         meta["init_segmentation"] = segmentation(bpe)
         stage = "glue_opt_all"
-        if method == "all":
+        if method == "all" and not extra:  # (the optimiser's own view: the small corpora only)
             lbfgs_record(RB, bpe, meta, arrays)
             bpe.glue_opt_all()
         geometry(bpe, "glued", arrays)
@@ -206,7 +218,7 @@ def main(argv):
     if len(argv) >= 2 and argv[0] == "--one":
         run_one(argv[1])
         return
-    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg", SLURM_CPUS_PER_TASK="2",
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg", SLURM_CPUS_PER_TASK="6",
                PYTHONBREAKPOINT="0")
     for name in argv or list(FIXTURES):
         r = subprocess.run([sys.executable, "-W", "ignore", __file__, "--one", name], env=env,
