@@ -118,6 +118,7 @@ def run_one(name):
         stage = "glue_opt_all"
         if method == "all" and not extra:  # (the optimiser's own view: the small corpora only)
             lbfgs_record(RB, bpe, meta, arrays)
+        if method == "all":
             bpe.glue_opt_all()
         geometry(bpe, "glued", arrays)
         stage = "bin"
