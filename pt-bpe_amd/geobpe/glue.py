@@ -142,3 +142,15 @@ def snap_bin(arr, x):
         return arr[-1][1]
     i = bisect.bisect_right([np.float32(b) for _, b in arr], x)
     return sum(arr[i]) / 2
+
+
+def snap_many(arr, xs) -> np.ndarray:
+    """snap_bin over an array of optima (same float32 comparisons, numpy searchsorted with
+    side="right" = bisect_right)."""
+    xs = np.asarray(xs, dtype=np.float32)
+    right = np.array([np.float32(b) for _, b in arr], dtype=np.float32)
+    centre = np.array([sum(e) / 2 for e in arr], dtype=np.float64)
+    i = np.minimum(np.searchsorted(right, xs, side="right"), len(arr) - 1)
+    out = centre[i]
+    out = np.where(xs < np.float32(arr[0][0]), arr[0][0], out)
+    return np.where(xs >= np.float32(arr[-1][1]), arr[-1][1], out)

@@ -540,11 +540,12 @@ class RmsdBPE:
         self.glue_calls = getattr(self, "glue_calls", 0) + 1
         for c, opt, gk in zip(chains, outs, grids):
             thr = self._thresholds[gk]
+            om, cn, ph = (G.snap_many(thr[k], opt[:, t]).tolist() for t, k in enumerate(G.GLUE))
             for k, (i, _, ln) in enumerate(c.tokens0[:-1]):
                 row = (i + ln) // 3 - 1
-                c.cur["omega"][row] = G.snap_bin(thr["omega"], opt[k, 0])
-                c.cur["C:1N:1CA"][row] = G.snap_bin(thr["C:1N:1CA"], opt[k, 1])
-                c.cur["phi"][row + 1] = G.snap_bin(thr["phi"], opt[k, 2])
+                c.cur["omega"][row] = om[k]
+                c.cur["C:1N:1CA"][row] = cn[k]
+                c.cur["phi"][row + 1] = ph[k]
         return cis
 
     def _partition_residues(self, n, size, occ):

@@ -11,6 +11,6 @@ tail -12 $OUT/glue_gpu.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python tools/glue_timing.py geobpe 64 60 300 > $OUT/glue_timing_64.json 2> $OUT/glue_timing_64.err || exit $?
 cat $OUT/glue_timing_64.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/glue_prof -o glue -- python3 tools/glue_timing.py geobpe 2000 60 300 > $OUT/glue_timing_2000.json 2> $OUT/glue_timing_2000.err || exit $?
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/glue_prof -o glue -- python3 tools/glue_timing.py geobpe 2000 60 300 > $OUT/glue_timing_2000.json 2> $OUT/glue_timing_2000.err || exit $?
 cat $OUT/glue_timing_2000.json
 bash tools/r2_end.sh $1
