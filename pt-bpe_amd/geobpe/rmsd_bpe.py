@@ -1041,13 +1041,16 @@ class RmsdBPE:
 
         from . import refpickle as R
         C = R._real_or_local()
-        toks = [self.tokenizer_record(c, C) for c in self._chains]
+        glue = self.glue_opt and self.glue_opt_method == "all"
+        toks = [self.tokenizer_record(c, C, self._exit_frames[i] if glue else None, bool(self.glue_opt))
+                for i, c in enumerate(self._chains)]
         return self._bpe_record(toks, C)
 
     @staticmethod
-    def tokenizer_record(c, C=None):
+    def tokenizer_record(c, C=None, frames=None, glue_opt=False):
         """The reference Tokenizer object of one chain (tokenizer.py:24-61 attributes, the
-        frames, bond_to_token with the merge tree)."""
+        frames, bond_to_token with the merge tree; with glue opt the cached exit frames,
+        ``cached_all_frames`` = (R_occs, t_occs), bpe.py:742-748, 1063)."""
         import pandas as pd
 
         from . import refpickle as R
@@ -1064,7 +1067,8 @@ class RmsdBPE:
         hier = R._new_dict(C["TokenHierarchy"], list(c.btt.items()), {"parent": tok, "tree": tree})
         n = c.n
         cur = {k: list(c.cur[k]) for k in COLUMNS}
-        cur_dt = {k: (np.float64 if k in GLUE else object) for k in COLUMNS}  # bpe.py:388 re-assigns the glue columns
+        # bpe.py:388 re-assigns the glue columns (float64), except with glue opt (bpe.py:381)
+        cur_dt = {k: (np.float64 if k in GLUE and not glue_opt else object) for k in COLUMNS}
         idxes = sum([[i, i, i] for i in range(1, n + 1)], [])
         tok.__dict__.update({
             "_angles_and_dists": R._frame(pd, cur, cur_dt),
@@ -1077,6 +1081,8 @@ class RmsdBPE:
             "_bond_to_token": hier, "_init_n_ca": c.init[0], "_init_ca_c": c.init[1],
             "_init_bond_angle": c.init[2], "token_pos": list(c.token_pos), "tokens": list(c.tokens0),
         })
+        if frames is not None:
+            tok.__dict__["cached_all_frames"] = (list(frames[0]), list(frames[1]))
         return tok
 
     def _bpe_record(self, toks, C):

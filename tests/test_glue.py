@@ -269,3 +269,63 @@ def test_each_method_raises_like_reference(host_glue):
               glue_opt_method="each", seed=0)
     with pytest.raises(AssertionError):
         bpe.initialize()
+
+
+REF_RESUME_GLUE = r'''
+import sys, json, pickle
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[2])
+import make_golden as MG
+MG._stub_optional_deps()
+sys.path.insert(0, "/root/reference")
+import foldingdiff.bpe as B
+from foldingdiff.tokenizer import Tokenizer
+B.BPE.visualize = lambda self, key, path: None
+Tokenizer.visualize_bonds = lambda self, *a, **k: None
+popped = []
+inner = B.BPE.step
+def rec(self):
+    top = self._priority_dict.peekitem(0)[0]
+    popped.append([bool(top[0]), int(top[1]), top[2]])
+    return inner(self)
+B.BPE.step = rec
+bpe = pickle.load(open(sys.argv[3], "rb"))
+calls = []
+for _ in range(int(sys.argv[4])):
+    n0 = len(popped)
+    bpe.step()
+    calls.append({"popped": popped[n0:], "step": bpe._step, "n_tokens": len(bpe._tokens)})
+print("JSON" + json.dumps(calls))
+'''
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/foldingdiff"), reason="reference not present (GPU box)")
+def test_reference_resumes_glue_opt_checkpoint(host_glue, tmp_path):
+    """bpe_iter=*.pkl with glue_opt: the reference unpickles this build's checkpoint taken
+    after 5 step() calls (cached exit frames included) and keeps training through the glue
+    re-optimisation at step 10; its merges equal its own uninterrupted run (gl_all_p0)."""
+    import subprocess
+    import sys
+    from conftest import REPO
+    from geobpe.bpe import BPE
+    meta, arrs = _load("gl_all_p0")
+    corpus = {k: arrs[k] for k in COLS + ["row_off"]}
+    bpe = BPE(corpus, bins={1: 5}, rmsd_partition_min_size=0, num_partitions={int(k): v for k, v in
+              meta["num_partitions"].items()}, max_num_strucs=meta["max_num_strucs"], res_init=True,
+              glue_opt=True, glue_opt_every=meta["glue_opt_every"], seed=0)
+    bpe.initialize()
+    bpe.glue_opt_all()
+    bpe.bin()
+    k = 5
+    for _ in range(k):
+        bpe.step()
+    p = str(tmp_path / f"bpe_iter={k}.pkl")
+    bpe.save_checkpoint(p)
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1", MPLBACKEND="Agg", SLURM_CPUS_PER_TASK="2",
+               PYTHONBREAKPOINT="0")
+    rest = len(meta["calls"]) - k
+    r = subprocess.run([sys.executable, "-W", "ignore", "-c", REF_RESUME_GLUE, os.path.join(REPO, "pt-bpe_amd"),
+                        os.path.join(REPO, "tests", "golden"), p, str(rest)], env=env,
+                       capture_output=True, text=True, timeout=1200)
+    assert r.returncode == 0, r.stderr[-3000:]
+    calls = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("JSON")][-1][4:])
+    assert calls == meta["calls"][k:]
