@@ -329,3 +329,25 @@ def test_reference_resumes_glue_opt_checkpoint(host_glue, tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     calls = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("JSON")][-1][4:])
     assert calls == meta["calls"][k:]
+
+
+def test_induce_from_glue_opt_checkpoint(host_glue, tmp_path):
+    """bin/induce.py's RMSD-mode route on a checkpoint trained with glue opt: the trained
+    state comes back from the pickle (RmsdBPE.from_checkpoint, prior tables from
+    _bin_centers / _bin_weights) and tokenize() segments and glues the chains as the
+    reference's trained object does (gl_all_p0 "induce")."""
+    from geobpe import refpickle
+    from geobpe.rmsd_bpe import RmsdBPE
+    meta, arrs = _load("gl_all_p0")
+    bpe = run_and_compare("gl_all_p0")
+    p = str(tmp_path / "bpe_iter=12.pkl")
+    bpe.save_checkpoint(p)
+    back = RmsdBPE.from_checkpoint(refpickle.load(p))
+    ro = arrs["row_off"]
+    for want in meta["induce"]:
+        i = want["chain"]
+        t, metrics = back.tokenize({"angles": {c: arrs[c][ro[i]:ro[i + 1]] for c in COLS}, "fname": f"induce_{i}"})
+        got = [[s0, list(v[1]) if isinstance(v[1], tuple) else v[1], v[2]] for s0, v in t.bond_to_token.items()]
+        assert got == want["segmentation"] and metrics["L"] == want["L"], f"induce {i}"
+        for c in COLS:
+            assert np.array_equal(np.asarray(t._c.cur[c]), arrs[f"induce{i}_{c}"], equal_nan=True), f"induce {i} {c}"
