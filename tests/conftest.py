@@ -16,9 +16,10 @@ def pytest_configure(config):
 
 
 def golden_names():
-    # rm_* (tests/test_rmsd_mode.py) and recover_ref (tests/test_recover.py) have layouts of their own
+    # rm_* (tests/test_rmsd_mode.py), gl_* (tests/test_glue.py) and recover_ref (tests/test_recover.py)
+    # have layouts of their own
     return sorted(f[:-5] for f in os.listdir(GOLDEN)
-                  if f.endswith(".json") and not f.startswith(("rm_", "recover_"))
+                  if f.endswith(".json") and not f.startswith(("rm_", "gl_", "recover_"))
                   and os.path.exists(os.path.join(GOLDEN, f[:-5] + ".npz")))
 
 
