@@ -138,7 +138,9 @@ def _glue_close(a, b, thr, what):
         return 0
     e = np.asarray(thr[what.split()[-1]], dtype=np.float64)
     width = float(np.max(e[:, 1] - e[:, 0]))
-    assert np.all(np.abs(a[bad] - b[bad]) <= 1.01 * width), f"{what}: a glue more than one bin away"
+    d = np.abs(a[bad] - b[bad])
+    d = np.minimum(d, 2 * np.pi - d)  # angles: the first and last bins are neighbours on the circle
+    assert np.all(d <= 1.01 * width), f"{what}: a glue more than one bin away"
     assert bad.sum() <= max(1, GLUE_FLIPS * len(a)), f"{what}: {int(bad.sum())} of {len(a)} glues in another bin"
     return int(bad.sum())
 
