@@ -165,12 +165,6 @@ __device__ inline void stx(double* X, int64_t S, int64_t atom, V3 v) {
   p[S] = v.y;
   p[2 * S] = v.z;
 }
-__device__ inline void addx(double* X, int64_t S, int64_t atom, V3 v) {
-  double* p = X + atom * 3 * S;
-  p[0] += v.x;
-  p[S] += v.y;
-  p[2 * S] += v.z;
-}
 
 // loss and gradient of one chain at the parameters x (glue k = (omega_k, theta_k, phi_k),
 // raw values; wrapped here as the closure does)
@@ -199,7 +193,7 @@ __device__ double glue_eval(const GlueProb& P, int64_t s, int64_t r, const doubl
     p2 = nCA;
     p1 = nC;
   }
-  for (int64_t a = 0; a < 3 * r; a++) stx(AX, S, a, V3{0, 0, 0});
+  for (int64_t a = 0; a < 3; a++) stx(AX, S, a, V3{0, 0, 0});  // atoms 3.. are written below
   // -- frames of residues 1..r-1 against the targets (bpe.py:539-548)
   double rot = 0.0, trans = 0.0;
   for (int64_t k = 0; k + 1 < r; k++) {
@@ -222,9 +216,9 @@ __device__ double glue_eval(const GlueProb& P, int64_t s, int64_t r, const doubl
     gx = v_addv(gx, v_cross(eu, gw));
     const V3 gu = v_cross(gw, ex);
     const V3 gvx = glue_normalize_back(vx, gx), gvu = glue_normalize_back(vu, gu);
-    addx(AX, S, 3 * i + 2, gvx);
-    addx(AX, S, 3 * i, gvu);
-    addx(AX, S, 3 * i + 1, v_addv(v_scale(v_addv(gvx, gvu), -1.0), v_scale(dt, 2.0 * P.wt)));
+    stx(AX, S, 3 * i + 2, gvx);  // each atom's frame term, written once
+    stx(AX, S, 3 * i, gvu);
+    stx(AX, S, 3 * i + 1, v_addv(v_scale(v_addv(gvx, gvu), -1.0), v_scale(dt, 2.0 * P.wt)));
   }
   double loss = P.wR * rot + P.wt * trans;
   // -- prior: mixture of von Mises per glue angle (bpe.py:527-534, 549-558), float32
@@ -256,30 +250,36 @@ __device__ double glue_eval(const GlueProb& P, int64_t s, int64_t r, const doubl
     grad[3 * k + 2] = gp[2];
   }
   if (P.lam != 0.f) loss += (double)(P.lam * prior);
-  // -- reverse sweep over the placements (atoms 3r-1 .. 3; atoms 0..2 hold no parameter)
+  // -- reverse sweep over the placements (atoms 3r-1 .. 3; atoms 0..2 hold no parameter).
+  // Atom m's adjoint takes its frame term plus the placements of atoms m+1..m+3, so walking
+  // down, the adjoints of j-1 and j-2 and the atoms j-1, j-2 ride in registers and each step
+  // loads only atom j-3 and its frame term (no store-to-load round trip through memory)
+  V3 R0 = ldx(AX, S, 3 * r - 1), R1 = ldx(AX, S, 3 * r - 2), R2 = ldx(AX, S, 3 * r - 3);
+  V3 C1 = ldx(X, S, 3 * r - 2), C2 = ldx(X, S, 3 * r - 3);
   for (int64_t j = 3 * r - 1; j >= 3; j--) {
     const int64_t i = j / 3, k = i - 1;
     const double* gk = g + 9 * k;
     const double* gn = gk + 9;
-    const V3 a = ldx(X, S, j - 3), b = ldx(X, S, j - 2), c = ldx(X, S, j - 1);
-    const V3 G = ldx(AX, S, j);
-    V3 ga = ldx(AX, S, j - 3), gbv = ldx(AX, S, j - 2), gc = ldx(AX, S, j - 1);
+    const V3 C3 = ldx(X, S, j - 3);
+    V3 R3 = ldx(AX, S, j - 3);
     float gA = 0.f, gT = 0.f;
     if (j % 3 == 0) {
-      glue_place_back(a, b, c, (float)gk[4], (float)gk[3], (float)gk[6], G, ga, gbv, gc, gA, gT);
+      glue_place_back(C3, C2, C1, (float)gk[4], (float)gk[3], (float)gk[6], R0, R3, R2, R1, gA, gT);
     } else if (j % 3 == 1) {
       const float om = glue_wrap(x[3 * k]), th = glue_wrap(x[3 * k + 1]);
-      glue_place_back(a, b, c, th, (float)gn[0], om, G, ga, gbv, gc, gA, gT);
+      glue_place_back(C3, C2, C1, th, (float)gn[0], om, R0, R3, R2, R1, gA, gT);
       grad[3 * k] += gT;
       grad[3 * k + 1] += gA;
     } else {
       const float ph = glue_wrap(x[3 * k + 2]);
-      glue_place_back(a, b, c, (float)gn[2], (float)gn[1], ph, G, ga, gbv, gc, gA, gT);
+      glue_place_back(C3, C2, C1, (float)gn[2], (float)gn[1], ph, R0, R3, R2, R1, gA, gT);
       grad[3 * k + 2] += gT;
     }
-    stx(AX, S, j - 3, ga);
-    stx(AX, S, j - 2, gbv);
-    stx(AX, S, j - 1, gc);
+    R0 = R1;
+    R1 = R2;
+    R2 = R3;
+    C1 = C2;
+    C2 = C3;
   }
   for (int64_t i = 0; i < 3 * (r - 1); i++) grad[i] = glue_wrap_back(x[i], grad[i]);
   return loss;
