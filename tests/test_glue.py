@@ -353,3 +353,39 @@ def test_induce_from_glue_opt_checkpoint(host_glue, tmp_path):
         assert got == want["segmentation"] and metrics["L"] == want["L"], f"induce {i}"
         for c in COLS:
             assert np.array_equal(np.asarray(t._c.cur[c]), arrs[f"induce{i}_{c}"], equal_nan=True), f"induce {i} {c}"
+
+
+def _cli_glue_resume(tmp_path):
+    """bin/encode.py with --glue-opt true --glue-opt-method all (RMSD mode): glue_opt_all after
+    initialize, re-optimisation every 5 steps; a run resumed at iter 10 from its
+    bpe_iter=10.pkl ends where the one-shot run does (merges, geometry, stats).  (Seed 1: with
+    seed 9 a glue optimum leaves the histogram range, snap_bin returns the first edge, the
+    key's (v + 2 pi) % 2 pi lands 1 ulp below it and get_ind raises ValueError, in the
+    reference too, bpe.py:515-517, 1164-1189.)"""
+    import json as _json
+    from test_bpe_api import _encode_cli
+    from geobpe import refpickle
+    cli = _encode_cli()
+    common = ["--data-dir", "synthetic:12:15:30:1", "--bins", "1-5", "--save-every", "5", "--p-min-size", "0",
+              "--num-p", "2-2:3-3:5-2", "--max-num-strucs", "60", "--glue-opt", "true", "--glue-opt-method", "all",
+              "--glue-opt-every", "5", "--log-dir", str(tmp_path / "logs")]
+    one, two = tmp_path / "one", tmp_path / "two"
+    assert cli.main(common + ["--save-dir", str(one), "--max-iter", "16"]) == 0
+    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "11"]) == 0
+    assert cli.main(common + ["--save-dir", str(two), "--max-iter", "16"]) == 0  # resumes at 10
+    a, b = refpickle.load(str(one / "bpe_iter=15.pkl")), refpickle.load(str(two / "bpe_iter=15.pkl"))
+    assert list(a._sphere_dict) == list(b._sphere_dict) and a._step == b._step >= 15
+    for ta, tb in zip(a.tokenizers, b.tokenizers):
+        assert dict(ta._bond_to_token) == dict(tb._bond_to_token)
+        assert ta._angles_and_dists.equals(tb._angles_and_dists)
+        assert hasattr(ta, "cached_all_frames")
+    assert _json.loads((one / "stats=15.json").read_text()) == _json.loads((two / "stats=15.json").read_text())
+
+
+def test_cli_glue_opt_resume_host(host_glue, tmp_path):
+    _cli_glue_resume(tmp_path)
+
+
+@pytest.mark.gpu
+def test_cli_glue_opt_resume_device(tmp_path):
+    _cli_glue_resume(tmp_path)
