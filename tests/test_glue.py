@@ -389,3 +389,31 @@ def test_cli_glue_opt_resume_host(host_glue, tmp_path):
 @pytest.mark.gpu
 def test_cli_glue_opt_resume_device(tmp_path):
     _cli_glue_resume(tmp_path)
+
+
+@pytest.mark.gpu
+def test_device_glue_opt_edge_lengths():
+    """Chains of 1, 2, 3 and 40 residues in one launch: a 1-residue chain has no glue (empty
+    output, no iterations); the others land near the oracle's optimum (tolerances above)."""
+    from geobpe import glue, rmsd, synth
+    from oracle import glue as og
+    from oracle import rmsd as orm
+    corpus = synth.make_corpus(synth.make_lengths(1, 40, 41, seed=4), seed=4)
+    cols = {c: corpus[c] for c in synth.COLUMNS}
+    geos, x0s, tgts = [], [], []
+    for n in (1, 2, 3, 40):
+        sub = {c: np.array(v[:n]) for c, v in cols.items()}
+        g = glue.pack_chain(sub, rmsd.init_geometry())
+        xyz = orm.nerf(rmsd.token_geo(sub, 0, 3 * n - 1)).reshape(n, 3, 3)[:max(n - 1, 0)]
+        R, t = glue.frame_from_triad(xyz[:, 0], xyz[:, 1], xyz[:, 2])
+        geos.append(g)
+        x0s.append((g[:n - 1][:, [7, 5, 8]] + 0.03).astype(np.float32))
+        tgts.append((R, t))
+    prior = (np.zeros((1, 3, 2, 1), np.float32), np.ones((1, 3), np.int32))
+    outs, stats, loss = glue.optimize_chains(geos, x0s, tgts, [0] * 4, prior, 0.0)
+    assert outs[0].shape == (0, 3) and tuple(stats[0]) == (0, 0)
+    for g, x0, (R, t), out, ls in zip(geos[1:], x0s[1:], tgts[1:], outs[1:], loss[1:]):
+        ref = og.optimize(g, x0, R, t)
+        d = np.abs(out.astype(np.float64) - ref[0])
+        assert np.median(np.minimum(d, 2 * np.pi - d)) < 1e-2
+        assert abs(ls[1] - ref[4]) <= GLUE_LOSS * abs(ref[4]) + 1e-9
