@@ -322,9 +322,11 @@ __global__ __launch_bounds__(64) void k_glue_opt(GlueProb P, const float* x0, fl
   if (s >= P.S) return;
   const int64_t a0 = P.roff[s], r = P.roff[s + 1] - a0;
   const int64_t np = 3 * (r - 1), g0 = a0 - s;  // glues of this chain and their first index
-  if (r < 2) {
+  if (r < 2) {  // no glue
     stats[2 * s] = 0;
     stats[2 * s + 1] = 0;
+    losses[2 * s] = 0.0;
+    losses[2 * s + 1] = 0.0;
     return;
   }
   const double* g = P.geo + 9 * a0;
