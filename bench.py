@@ -8,9 +8,12 @@ covers the config's 1000 merges.  The prologue (thresholds, quantisation,
 labels) and the initial histogram (BPE.bin) run before the timed region and are
 reported separately.  Inputs are resident in HBM when the timer starts.
 
-N > 1: launched by torch.distributed.run, one rank per GPU (RCCL); the corpus is
-row-sharded (same 100k chains in total: strong scaling), the ranks exchange count
-deltas once per iteration.
+N > 1: one rank per GPU (RCCL); the corpus is row-sharded (same 100k chains in
+total: strong scaling), the ranks exchange count deltas once per iteration.
+Launched by torch.distributed.run (WORLD_SIZE set: it must equal --gpus), or as
+plain ``python bench.py --gpus N``: the parent then starts torch.distributed.run
+with N ranks as a child process before anything touches the GPU and exits with
+its status.
 
 rank 0 prints ONE JSON line.
 """
@@ -19,6 +22,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -89,14 +94,41 @@ def parse():
                     help="N > 1: RCCL (default); gloo puts every rank on GPU 0 (a one-GPU rehearsal of the N > 1 path)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
-    ap.add_argument("--roofline-kernel", default="auto", help="auto: the slower of k_find / k_commit")
-    ap.add_argument("--event-stride", type=int, default=8,
-                    help="time every k-th launch of the roofline kernel in the timed region")
+    ap.add_argument("--roofline-kernel", default="auto", help="auto: the slowest merge-loop kernel")
+    ap.add_argument("--event-stride", type=int, default=1,
+                    help="time every k-th launch of the merge-loop kernels in the timed region (1: all)")
+    ap.add_argument("--emit-merges", action="store_true",
+                    help="add the merge list ([key string, count] of every merge so far) to the JSON line")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(args) -> int:
+    """``--gpus N`` (N > 1) without a launcher: start torch.distributed.run with N
+    ranks as a child process (this process never touches the GPU) and return its
+    exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
     args = parse()
+    if args.gpus < 1:
+        sys.exit("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
+    if "WORLD_SIZE" in os.environ and int(os.environ["WORLD_SIZE"]) != args.gpus:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
     if args.force_exchange:  # rehearsal of the exchange only: no tables that need per-merge counts
         args.no_profile = args.no_replay = args.no_cpu_baseline = True
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -148,8 +180,9 @@ def main():
     bin_ms = {k: v for k, v in bin_ms.items() if v > 0}
     pack_ms = eng.kernel_ms("bin_pack")[0]  # layout step for the merge loop (pk into the token records)
     eng.run(args.warmup)
-    # ---- timed region: exactly K merges; HIP events only around the roofline kernels
-    eng.set_profiling(not args.no_profile, only="find,commit", stride=args.event_stride)
+    # ---- timed region: exactly K merges; HIP events around the merge-loop launches
+    # (k_select carries the previous merge's k_place), on the engine's stream
+    eng.set_profiling(not args.no_profile, only="select,find,commit", stride=args.event_stride)
     st0 = eng.state()
     eng.marker(1)  # window bracket for rocprofv3 (outside the timer)
     if world > 1:
@@ -167,31 +200,41 @@ def main():
         tt = torch.tensor([T], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
-    ktimes = {k: (eng.kernel_ms(k) if not args.no_profile else (0.0, 0)) for k in ("find", "commit")}
+    ktimes = {k: (eng.kernel_ms(k) if not args.no_profile else (0.0, 0)) for k in ("select", "find", "commit")}
     merges_log = list(eng.merges)
     R_local = int(shard["row_off"][-1])
+    n_ranks = dist.get_world_size() if dist.is_initialized() else 1
+    rank_res = [R_local]
+    if world > 1:
+        rr = [None] * world
+        dist.all_gather_object(rr, R_local)
+        rank_res = [int(x) for x in rr]
+    merge_list = eng.merge_keys() if args.emit_merges else None
     if rank != 0:
         if world > 1:
             dist.barrier()
             dist.destroy_process_group()
         return
 
-    # ---- per-kernel table: a replay of the same merges with every kernel timed
+    # ---- per-kernel table: the live events of the timed region (every event_stride-th launch)
     kern = {}
+    for k, (ms, nl) in ktimes.items():
+        if nl:
+            kern["select+place" if k == "select" else k] = {"ms_total": round(ms, 4), "launches": nl,
+                                                           "avg_us": round(1000 * ms / nl, 3)}
+    # k_commit's work (key records, decrement records, keys) for its algorithmic bytes: counted
+    # by an instrumented replay of the same merges (its atomics slow k_commit, so no times
+    # are taken from it)
     commit_work = None
     if not args.no_profile and world == 1 and not args.no_replay:
         rep = GeoBPEEngine(shard, B, device=local, max_vocab=1 << 20)
         rep.initialize()
         rep.bin()
         rep.run(args.warmup)
-        rep.set_profiling(True)  # (every launch timed; k_commit's work counters on)
+        rep.set_profiling(True, only="commit")  # (stride 1: k_commit's work counters on)
         rs0 = rep.state()
         rep.run(done)
         rs1 = rep.state()
-        for k in ("select", "find", "commit"):
-            ms, nl = rep.kernel_ms(k)
-            kern["select+place" if k == "select" else k] = {"ms_total": round(ms, 4), "launches": nl,
-                                                           "avg_us": round(1000 * ms / max(nl, 1), 3)}
         commit_work = {k: rs1[k] - rs0[k] for k in ("commit_key_records", "commit_decrement_records", "commit_keys")}
         assert rep.merges == merges_log, "replay diverged"
         rep.close()
@@ -200,18 +243,23 @@ def main():
     wkey = f"config={args.config},warmup={args.warmup},steps={args.steps},n={world}"
     window = merges_log[-done:] if done else []
     n_merged = sum(m[2] for m in window)
+    # the select launch of merge t places merge t - 1
+    placed = sum(m[2] for m in merges_log[-done - 1:-1]) if done and len(merges_log) > done else n_merged
     per = lambda x: x / max(done, 1)  # noqa: E731
     work = {"find": (FIND_BYTES_PER_OCC * per(n_merged),
                      f"{FIND_BYTES_PER_OCC} B x merged occurrences (avg {per(n_merged):.0f} per launch)"),
-            "commit": (None, "k_commit work counters come from the profiled replay (--no-replay: unknown)")}
+            "select": (PLACE_BYTES_PER_OCC * per(placed),
+                       f"k_place's {PLACE_BYTES_PER_OCC} B x merged occurrences of the previous merge (avg "
+                       f"{per(placed):.0f} per launch); the one-workgroup k_select beside it is not counted"),
+            "commit": (None, "k_commit work counters come from the instrumented replay (--no-replay: unknown)")}
     if commit_work:
         cw = {k: per(v) for k, v in commit_work.items()}
         work["commit"] = (COMMIT_KREC_BYTES * cw["commit_key_records"] + COMMIT_DREC_BYTES * cw["commit_decrement_records"]
                           + COMMIT_KEY_BYTES * cw["commit_keys"],
                           f"{COMMIT_KREC_BYTES} B x key records + {COMMIT_DREC_BYTES} B x decrement records + "
                           f"{COMMIT_KEY_BYTES} B x keys (avg {cw['commit_key_records']:.0f} / "
-                          f"{cw['commit_decrement_records']:.0f} / {cw['commit_keys']:.0f} per launch, counted in the "
-                          f"profiled replay of the same merges)")
+                          f"{cw['commit_decrement_records']:.0f} / {cw['commit_keys']:.0f} per launch, counted by an "
+                          f"instrumented replay of the same merges)")
     roofs = {}
     for k, (ms, nl) in ktimes.items():
         if not nl:
@@ -219,8 +267,8 @@ def main():
         avg_s = ms / 1000.0 / nl
         bpl, note = work[k]
         ach = bpl / avg_s / 1e9 if bpl is not None else None
-        traffic, tsrc = pmc_traffic(k, wkey)
-        roofs[k] = {"kernel": f"k_{k}", "bound": "hbm", "achieved": round(ach, 2) if ach else None,
+        traffic, tsrc = pmc_traffic(k, wkey)  # (k_select's dispatches carry k_place)
+        roofs[k] = {"kernel": "k_select+k_place" if k == "select" else f"k_{k}", "bound": "hbm", "achieved": round(ach, 2) if ach else None,
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
                     "traffic": traffic, "traffic_source": tsrc, "traffic_window": wkey,
                     "bytes_per_launch": round(bpl, 1) if bpl is not None else None, "avg_launch_us": round(avg_s * 1e6, 3),
@@ -264,7 +312,7 @@ def main():
         "metric": "BPE merge iters/sec on PDB-pretrain-scale corpus",
         "value": round(value, 2),
         "unit": "merges/s",
-        "n_gpus": world,
+        "n_gpus": n_ranks,
         "steps": done,
         "warmup": args.warmup,
         "ms_per_step": round(1000 * T / max(done, 1), 4),
@@ -278,7 +326,8 @@ def main():
                                 + f": {n} synthetic chains, len U{{{lo}..{hi}}}, {R_total} residues, "
                                 f"bins {{1: {B}}}, merges {args.warmup + 1}..{args.warmup + done}")
                    if args.config in ("c3", "c5") else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
-                   "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}"},
+                   "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}",
+                   "rank_residues": rank_res, "backend": (args.dist_backend if world > 1 else None)},
         "roofline": roofline,
         "roofline_other": roofline_other,
         "cpu_baseline": cpu,
@@ -287,6 +336,8 @@ def main():
         "prologue_s": {"generate": round(t_gen, 3), "initialize": round(t_init, 3), "bin": round(t_bin, 3)},
         "final": {"vocab": eng.vocab_count, "keys": eng.num_keys},
     }
+    if merge_list is not None:
+        out["merge_list"] = merge_list
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

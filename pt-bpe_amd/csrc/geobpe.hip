@@ -1416,7 +1416,7 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
   int64_t rmax = 0;
   for (int64_t i = 0; i < n_chains; i++) {
     const int64_t r = h_res_off[i + 1] - h_res_off[i];
-    if (r < 0) return GEOBPE_EARG;
+    if (r < 1) return GEOBPE_EARG;  // (the glue offsets g0 = a0 - s assume >= 1 residue per chain)
     rmax = std::max(rmax, r);
   }
   const int64_t G = R - n_chains;  // glues: r - 1 per chain

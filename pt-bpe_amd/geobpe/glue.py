@@ -76,6 +76,8 @@ def optimize_chains(geos, x0s, targets, grids, prior, lam: float, device: int = 
     L = _native.lib()
     n = len(geos)
     rs = [len(g) for g in geos]
+    if any(r < 1 for r in rs):
+        raise ValueError("glue opt: a chain with no residues")
     off = np.zeros(n + 1, dtype=np.int64)
     np.cumsum(rs, out=off[1:])
     geo = np.ascontiguousarray(np.concatenate(geos) if n else np.zeros((0, 9)), dtype=np.float64)

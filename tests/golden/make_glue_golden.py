@@ -40,6 +40,12 @@ FIXTURES = {
     # free bonds, rmsd_super_res, glue opt "all" with prior 0 every 10 steps; 20 merges
     "gl_pdb72_readme": ("pdb72", None, None, 0, 50, 0, True, "all", 0.0, 10, 20,
                         {"num_p": {2: 2, 3: 5, 5: 1, 6: 2, 8: 1}, "std_bonds": False, "max_num_strucs": 500}),
+    # the same corpus in the README's pareto run (README.md:48; BASELINE configs[4]'s schedule string
+    # is its --num-p): --bins 1-500, p = 0, --num-p 2-100:3-500:5-20:6-100:8-5:9-20:11-1:12-5:14-1,
+    # 500 structures, free bonds, rmsd_super_res, glue opt "all" with prior 1.0 EVERY step; 4 merges
+    "gl_pdb72_pareto": ("pdb72", None, None, 0, 500, 0, True, "all", 1.0, 1, 4,
+                        {"num_p": {2: 100, 3: 500, 5: 20, 6: 100, 8: 5, 9: 20, 11: 1, 12: 5, 14: 1},
+                         "std_bonds": False, "max_num_strucs": 500}),
 }
 # BPE.tokenize (the RMSD mode's induce, bpe.py:1053-1140, with glue_opt "all") of these
 # training chains after the steps
