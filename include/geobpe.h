@@ -98,6 +98,11 @@ int geobpe_step(geobpe_ctx *ctx, int32_t *new_id, int32_t *count, int64_t *n_mer
  * (the winner, tie-break and new token are resolved on the device), then wait;
  * *n_done = merges actually made (fewer if the pairs ran out). */
 int geobpe_run(geobpe_ctx *ctx, int64_t n_iters, int64_t *n_done);
+/* Late-merge path (same results): once a merge's count is <= max_count, geobpe_run /
+ * geobpe_step run the merges in one workgroup over per-key posting lists (k_tail, many
+ * merges per launch) instead of the full-grid kernels; 0 = never (default 4096;
+ * environment GEOBPE_TAIL overrides at create).  Single rank, no merge replay. */
+int geobpe_set_tail(geobpe_ctx *ctx, int64_t max_count);
 /* The merge list so far: 3 int64 per merge (new id, count, merges applied);
  * returns the number of merges (copies at most cap). */
 int64_t geobpe_merge_log(geobpe_ctx *ctx, int64_t *h_out, int64_t cap);

@@ -102,6 +102,12 @@ struct State {
   int64_t stat_krec, stat_drec, stat_keys;
   int64_t nxovf;  // entries of Dev.xovf (pipelined exchange)  // k_commit work (profiling only): key records, decrement records, keys
   int64_t slot_max;    // pipelined exchange: the largest slot count of the last import (every rank)
+  // late-merge path (tail.h): per-key posting lists in one pool
+  int64_t kpool_used;  // pool entries handed out since the last list build
+  int32_t kp_valid;    // 1: the lists hold every live pair (0: rebuild before the next tail launch)
+  int32_t tail_exit;   // why the last k_tail stopped: 0 merges done / error, 1 + Sel decision otherwise
+  int32_t tail_par;    // launch parity after the last k_tail
+  int32_t pad5;
 };
 
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
@@ -235,6 +241,19 @@ struct Dev {
   int64_t xcap;
   int2* xovf;  // (key, delta) of the rare unstaged adds of a pipelined iteration
   int64_t ovf_cap;
+  // late-merge path (tail.h): key d's posting list is kpool[kp_off[d] .. + kp_n[d]) (capacity
+  // kp_cap[d]; entries whose token no longer carries the key are skipped); per-merge scratch
+  int32_t *kp_off, *kp_n, *kp_cap, *kpool;
+  int64_t KPOOL;
+  int4* TM;       // merged occurrences {a, ya, b, c}
+  int2* TH;       // new pairs {slot, key}
+  int4* TS;       // posting entries past a list's capacity {key, position, slot}
+  int32_t* TR;    // keys whose list is regrown
+  NewPair* TK;    // keys found (not claimed): EHASH check
+  int64_t TMcap, THcap;
+  int4* ev;       // merge-event log (record mode; see geobpe_set_record_events), or null
+  int64_t ev_cap;
+  unsigned long long* ev_n;
   // argmax
   int32_t* clist;  // hot list (capacity KCAP)
   LogRec* log;

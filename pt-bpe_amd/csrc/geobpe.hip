@@ -75,6 +75,10 @@ struct geobpe_ctx {
   bool place_pending = false; // a k_commit ran whose k_place has not (it rides with the next k_select)
   bool pipelined = false;     // between geobpe_pipeline_begin and _end (device-side parity)
   int nba = 256;  // find / commit / finalize / bin / import workgroups (= D.NBA, <= NBA_MAX)
+  // late-merge path (tail.h): merges whose count is <= tail_thresh run in k_tail
+  int64_t tail_thresh = 4096;  // 0: never
+  bool tail_on = false;        // switched (one way: the full-grid kernels' posting index goes stale)
+  bool tail_ready = false;     // its arrays are allocated
   // profiling
   bool prof = false;
   int prof_stride = 1;      // time every prof_stride-th launch of each kernel
@@ -326,6 +330,74 @@ int sync_state_sel(geobpe_ctx* c, Sel* out) {
   return check_device_error(c);
 }
 
+// ---------------------------------------------------------------- late-merge path (tail.h)
+bool tail_enabled(const geobpe_ctx* c) { return c->tail_thresh > 0 && !c->distributed && !c->replay; }
+
+int tail_alloc(geobpe_ctx* c) {
+  if (c->tail_ready) return 0;
+  Dev& D = c->D;
+  D.KPOOL = std::min<int64_t>(6 * c->R + 65536, INT32_MAX - 1);
+  D.TMcap = c->R / 2 + 1024;
+  D.THcap = c->R + 2048;
+  int rc;
+  if ((rc = dalloc(c, &D.kp_off, D.HC)) || (rc = dalloc(c, &D.kp_n, D.HC)) || (rc = dalloc(c, &D.kp_cap, D.HC)) ||
+      (rc = dalloc(c, &D.kpool, D.KPOOL)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, D.THcap)) ||
+      (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)))
+    return rc;
+  c->tail_ready = true;
+  return 0;
+}
+
+// per-key posting lists of the live pairs (a counting sort by key), after any pending place
+void tail_build(geobpe_ctx* c) {
+  flush_place(c);
+  Timed t(c, "tail_build");
+  hipLaunchKernelGGL(k_kp_reset, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  hipLaunchKernelGGL(k_kp_count, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  hipLaunchKernelGGL(k_kp_alloc, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  hipLaunchKernelGGL(k_kp_fill, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+}
+
+// up to n merges in k_tail (one workgroup, one launch for many merges); a hot-list rebuild
+// or the end is run by k_commit on the parity the tail stopped at; stale lists are rebuilt
+int tail_run(geobpe_ctx* c, int64_t n) {
+  int rc;
+  if ((rc = tail_alloc(c)) || (rc = sync_state(c))) return rc;
+  const int32_t it0 = c->h_state->iter;
+  while (!c->h_state->done) {
+    const int64_t left = n - (c->h_state->iter - it0);
+    if (left <= 0) break;
+    if (!c->h_state->kp_valid) tail_build(c);
+    const int32_t before = c->h_state->iter;
+    {
+      Timed t(c, "tail");
+      hipLaunchKernelGGL(k_tail, dim3(1), dim3(SBLOCK), 0, c->stream, c->D, (int)(c->gen & 1), left);
+    }
+    HIPCHK(c, hipGetLastError());
+    if ((rc = sync_state(c))) return rc;
+    c->gen += c->h_state->iter - before;  // (one launch parity per merge)
+    if (c->h_state->tail_exit > 0) {  // an iteration that is no merge: rebuild / measure / done
+      Timed t(c, "commit");
+      hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 0, (int)(c->gen & 1));
+      c->gen++;
+      HIPCHK(c, hipGetLastError());
+      if ((rc = sync_state(c))) return rc;
+    }
+  }
+  return 0;
+}
+
+// the next batch of full-grid iterations before the switch is checked: long while the
+// merges are far above the threshold (the check costs a synchronisation)
+int64_t tail_batch(const geobpe_ctx* c, int64_t want) {
+  if (!tail_enabled(c)) return want;
+  const int64_t m = c->h_state->maxc;
+  return std::min<int64_t>(want, m == 0 ? 16 : (m > 8 * c->tail_thresh ? 64 : 8));
+}
+void tail_check_switch(geobpe_ctx* c) {
+  if (tail_enabled(c) && c->h_state->maxc > 0 && c->h_state->maxc <= c->tail_thresh) c->tail_on = true;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------- C ABI
@@ -359,6 +431,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
     const int v = atoi(e);
     if (v >= 8 && v <= NBA_MAX) c->nba = v;
   }
+  if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = full-grid kernels only)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
@@ -625,6 +698,13 @@ int geobpe_set_rank(geobpe_ctx* c, int32_t rank) {
   return 0;
 }
 
+int geobpe_set_tail(geobpe_ctx* c, int64_t max_count) {
+  if (!c || max_count < 0) return GEOBPE_EARG;
+  c->tail_thresh = max_count;
+  if (!max_count && c->tail_on) return fail(c, GEOBPE_EARG, "the late-merge path is already in use");
+  return 0;
+}
+
 int geobpe_set_bin_dense(geobpe_ctx* c, int on) {
   if (!c) return GEOBPE_EARG;
   if (c->keys_ready) return fail(c, GEOBPE_EARG, "set_bin_dense must precede bin()");
@@ -781,13 +861,19 @@ int geobpe_step(geobpe_ctx* c, int32_t* new_id, int32_t* count, int64_t* n_merge
   if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
   if (c->distributed) return fail(c, GEOBPE_EARG, "geobpe_step in distributed mode: use step_select/apply + deltas");
   HIPCHK(c, hipSetDevice(c->device));
-  const int32_t it0 = c->h_state->iter;
   int rc;
-  for (;;) {  // a rebuild iteration merges nothing: go again
-    enqueue_iteration(c);
-    HIPCHK(c, hipGetLastError());
-    if ((rc = sync_state(c))) return rc;
-    if (c->h_state->iter != it0 || c->h_state->done) break;
+  if ((rc = sync_state(c))) return rc;
+  const int32_t it0 = c->h_state->iter;
+  if (c->tail_on && tail_enabled(c)) {
+    if ((rc = tail_run(c, 1))) return rc;
+  } else {
+    for (;;) {  // a rebuild iteration merges nothing: go again
+      enqueue_iteration(c);
+      HIPCHK(c, hipGetLastError());
+      if ((rc = sync_state(c))) return rc;
+      if (c->h_state->iter != it0 || c->h_state->done) break;
+    }
+    tail_check_switch(c);
   }
   if (c->h_state->iter == it0) {
     *new_id = -1;
@@ -810,12 +896,19 @@ int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) {
   HIPCHK(c, hipSetDevice(c->device));
   const int32_t it0 = c->h_state->iter;
   int rc;
-  // hot-list rebuild iterations merge nothing: top up until n merges or done
+  // hot-list rebuild iterations merge nothing: top up until n merges or done; the small
+  // merges go to the one-workgroup path
   for (int64_t want = n_iters; want > 0;) {
-    for (int64_t i = 0; i < want; i++) enqueue_iteration(c);
+    if (c->tail_on && tail_enabled(c)) {
+      if ((rc = tail_run(c, want))) return rc;
+      break;
+    }
+    const int64_t batch = tail_batch(c, want);
+    for (int64_t i = 0; i < batch; i++) enqueue_iteration(c);
     HIPCHK(c, hipGetLastError());
     if ((rc = sync_state(c))) return rc;
     if (c->h_state->done) break;
+    tail_check_switch(c);
     want = n_iters - (c->h_state->iter - it0);
   }
   if (n_done) *n_done = c->h_state->iter - it0;
@@ -1506,6 +1599,9 @@ int geobpe_set_record_events(geobpe_ctx* c, int on) {
     c->ev = nullptr;
     c->ev_n = nullptr;
     c->ev_cap = 0;
+    c->D.ev = nullptr;
+    c->D.ev_n = nullptr;
+    c->D.ev_cap = 0;
     return 0;
   }
   if (c->ev) return 0;
@@ -1514,6 +1610,9 @@ int geobpe_set_record_events(geobpe_ctx* c, int on) {
   HIPCHK(c, hipMalloc(&c->ev, (size_t)c->ev_cap * sizeof(int4)));
   HIPCHK(c, hipMalloc(&c->ev_n, sizeof(unsigned long long)));
   HIPCHK(c, hipMemsetAsync(c->ev_n, 0, sizeof(unsigned long long), c->stream));
+  c->D.ev = c->ev;  // (k_tail writes its merges' events itself)
+  c->D.ev_cap = c->ev_cap;
+  c->D.ev_n = c->ev_n;
   return 0;
 }
 

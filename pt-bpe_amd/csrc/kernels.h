@@ -674,54 +674,62 @@ __device__ inline bool post_stale(const Dev& D, int64_t m) {
   return st->post_valid == 0 || st->plog_ovf != 0 || st->pool_used + need > D.POOL_CH;
 }
 
-__global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
-  __shared__ int32_t s_red[SBLOCK / 64];
-  __shared__ SelStage S;
+// plain loads in a kernel that reads state written by earlier launches; loads that
+// bypass this CU's L1 (agent scope) where the same launch changes the data with
+// atomics (the persistent late-merge kernel, tail.h)
+template <bool COH, class T>
+__device__ inline T ldc(const T* p) {
+  if constexpr (COH)
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    return *p;
+}
+
+// the argmax + tie-break of one iteration (every thread of the workgroup calls it): the
+// decision goes to Sel[par] and, when lsel is given, to LDS (thread 0 writes both)
+template <bool COH>
+__device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, Sel* lsel) {
   State* st = D.st;
-  if (blockIdx.x > 0) {  // the previous merge's k_place rides along (it needs only k_commit's output)
-    __shared__ PlaceLds P;
-    place_body(D, blockIdx.x - 1, P);
-    return;
-  }
-  if (par == INT32_MIN) return;  // place only
-  if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
-    if (st->stall) return;
-    const int32_t g = st->dgen + 1;
-    par = g & 1;
-    __syncthreads();  // every thread has read dgen
-    if (threadIdx.x == 0) st->dgen = g;
-  }
   Sel* out = D.sel + par;
   const bool rec = threadIdx.x == 0;
+  Sel o{};
+  auto publish = [&]() {
+    *out = o;
+    if (lsel) *lsel = o;
+  };
   dbg_stamp(D, 20);  // (debug timeline slots 20-26: k_select phases)
-  const int32_t act = st->cl_act;
+  const int32_t act = ldc<COH>(&st->cl_act);
   // the first SEL_UNR * SBLOCK list entries are loaded with the state (clist
   // capacity KCAP >= SEL_UNR * SBLOCK; entries past n are masked below)
   int32_t d0[SEL_UNR];
 #pragma unroll
   for (int q = 0; q < SEL_UNR; q++) d0[q] = D.clist[threadIdx.x + q * SBLOCK];
-  const int64_t n = st->ncl2[act];
-  const int32_t th = st->theta, iter = st->iter, K = st->K;
-  const bool valid = st->cl_valid != 0;
-  if (st->done) {
-    if (rec) out->decision = SEL_DONE;
+  const int64_t n = ldc<COH>(&st->ncl2[act]);
+  const int32_t th = ldc<COH>(&st->theta), iter = ldc<COH>(&st->iter), K = ldc<COH>(&st->K);
+  const bool valid = ldc<COH>(&st->cl_valid) != 0;
+  if (ldc<COH>(&st->done)) {
+    if (rec) {
+      o.decision = SEL_DONE;
+      publish();
+    }
     return;
   }
   if (!valid) {  // no usable list: measure the maximum, then rebuild at half of it
     if (!rec) return;
     const Sel& prev = D.sel[par ^ 1];
     const bool measured = prev.decision == SEL_SKIP && (prev.skip & SKIP_MEASURE);
-    const int64_t ms = measured ? st->cl_measured : 0;
+    const int64_t ms = measured ? ldc<COH>(&st->cl_measured) : 0;
     if (measured && ms == 0) {
-      out->decision = SEL_DONE;
-      out->maxc = 0;
+      o.decision = SEL_DONE;
+      o.maxc = 0;
     } else {
-      out->decision = SEL_SKIP;
-      out->skip = measured ? SKIP_HOT : SKIP_MEASURE;
-      out->theta_new = (int32_t)max((int64_t)1, ms / 2);
-      out->build = act ^ 1;
+      o.decision = SEL_SKIP;
+      o.skip = measured ? SKIP_HOT : SKIP_MEASURE;
+      o.theta_new = (int32_t)max((int64_t)1, ms / 2);
+      o.build = act ^ 1;
       st->ncl2[act ^ 1] = 0;  // (no mark workgroup reads the idle counter)
     }
+    publish();
     return;
   }
   // ---- pass over the list: SEL_UNR entries per thread in flight; keep this thread's maximum
@@ -734,7 +742,7 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
       d[q] = i < n ? (i0 < SBLOCK ? d0[q] : D.clist[i]) : -1;
     }
 #pragma unroll
-    for (int q = 0; q < SEL_UNR; q++) c[q] = d[q] >= 0 ? D.count[d[q]] : 0;
+    for (int q = 0; q < SEL_UNR; q++) c[q] = d[q] >= 0 ? ldc<COH>(&D.count[d[q]]) : 0;
 #pragma unroll
     for (int q = 0; q < SEL_UNR; q++) {
       if (c[q] > m) {
@@ -753,25 +761,28 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
   const bool hot = gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th);
   if (hot && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
     if (rec) {
-      out->decision = SEL_DONE;
-      out->maxc = 0;
+      o.decision = SEL_DONE;
+      o.maxc = 0;
+      publish();
     }
     return;
   }
   if (hot) {
     if (rec) {
-      out->decision = SEL_SKIP;
-      out->skip = SKIP_HOT;
-      out->theta_new = max(1, gm / 2);
-      out->build = act ^ 1;
+      o.decision = SEL_SKIP;
+      o.skip = SKIP_HOT;
+      o.theta_new = max(1, gm / 2);
+      o.build = act ^ 1;
       st->ncl2[act ^ 1] = 0;
+      publish();
     }
     return;
   }
   if (K >= D.KC) {
     if (rec) {
       set_error(D, GEOBPE_ECAPACITY, -9);
-      out->decision = SEL_DONE;
+      o.decision = SEL_DONE;
+      publish();
     }
     return;
   }
@@ -784,7 +795,7 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     } else {
       for (int64_t i = threadIdx.x; i < n; i += SBLOCK) {
         const int32_t d = D.clist[i];
-        if (D.count[d] == gm) {
+        if (ldc<COH>(&D.count[d]) == gm) {
           const int32_t j = atomicAdd(&S.nt, 1);
           if (j < SEL_TMAX) S.key[j] = d;
         }
@@ -806,8 +817,8 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
       len = S.seq[t].nA + S.seq[t].nC;
     }
     int32_t tot;
-    const int32_t o = block_excl_scan(len, &tot, s_red);
-    if (t < nt) S.off[t] = o;
+    const int32_t o2 = block_excl_scan(len, &tot, s_red);
+    if (t < nt) S.off[t] = o2;
     __syncthreads();
     if (tot <= SEL_SYMS) {  // copy into LDS, one candidate per wave, 64 symbols a step
       for (int32_t c = t >> 6; c < nt; c += SBLOCK / 64) {
@@ -834,7 +845,7 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     if (t < 256)
       for (int64_t i = t; i < n; i += 256) {
         const int32_t d = D.clist[i];
-        if (D.count[d] == gm && (best < 0 || (d != best && key_less(D, d, best, jb)))) best = d;
+        if (ldc<COH>(&D.count[d]) == gm && (best < 0 || (d != best && key_less(D, d, best, jb)))) best = d;
       }
     W = block_min_key(D, best, S.idx, jb);
   }
@@ -854,25 +865,46 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     lr.idR = Rr;
     lr.nmerged = 0;
     D.log[iter] = lr;
-    out->decision = SEL_MERGE;
-    out->skip = 0;
-    out->rebuild = post_stale(D, gm) ? 1 : 0;
-    out->wown = owner_of_key(D, probe_key(w1, w2, wl));
-    out->W = W;
-    out->nid = K;
-    out->iter = iter;
-    out->tag = iter + 1;
-    out->maxc = gm;
-    out->ncand = nt;
-    out->w1 = w1;
-    out->w2 = w2;
-    out->wl = wl;
-    out->wfp = key_fp(W);
-    out->widL = L;
-    out->wg = g;
-    out->widR = Rr;
+    o.decision = SEL_MERGE;
+    o.skip = 0;
+    o.rebuild = post_stale(D, gm) ? 1 : 0;
+    o.wown = owner_of_key(D, probe_key(w1, w2, wl));
+    o.W = W;
+    o.nid = K;
+    o.iter = iter;
+    o.tag = iter + 1;
+    o.maxc = gm;
+    o.ncand = nt;
+    o.w1 = w1;
+    o.w2 = w2;
+    o.wl = wl;
+    o.wfp = key_fp(W);
+    o.widL = L;
+    o.wg = g;
+    o.widR = Rr;
+    publish();
   }
   dbg_stamp(D, 26);
+}
+
+__global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
+  __shared__ int32_t s_red[SBLOCK / 64];
+  __shared__ SelStage S;
+  State* st = D.st;
+  if (blockIdx.x > 0) {  // the previous merge's k_place rides along (it needs only k_commit's output)
+    __shared__ PlaceLds P;
+    place_body(D, blockIdx.x - 1, P);
+    return;
+  }
+  if (par == INT32_MIN) return;  // place only
+  if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
+    if (st->stall) return;
+    const int32_t g = st->dgen + 1;
+    par = g & 1;
+    __syncthreads();  // every thread has read dgen
+    if (threadIdx.x == 0) st->dgen = g;
+  }
+  select_core<false>(D, par, S, s_red, nullptr);
 }
 
 // merge replay (bin/induce.py): merge t is the trained
@@ -1234,5 +1266,7 @@ __global__ __launch_bounds__(256) void k_debug_key_less(Dev D, const int32_t* pa
     out[i] = j != w ? 2 : (j ? 1 : 0);
   }
 }
+
+#include "tail.h"
 
 }  // namespace gb

@@ -82,9 +82,11 @@ def _stream_handle(device: int):
 class GeoBPEEngine:
     def __init__(self, corpus: dict, bins: int, device: int = 0, max_vocab: int = 1 << 20,
                  group=None, stream=None, use_torch_stream: bool = True, cover: bool = False,
-                 bin_dense: bool = True, strategy: Optional[str] = None):
+                 bin_dense: bool = True, strategy: Optional[str] = None, tail: Optional[int] = None):
         """``corpus``: ``{column: float64[R]}`` + ``row_off`` (geobpe.synth layout) for
-        THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs."""
+        THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs.
+        ``tail``: merges of at most this count run in the one-workgroup late-merge
+        kernel (include/geobpe.h geobpe_set_tail; None = the library default, 0 = never)."""
         self.L = _native.lib()
         self.B = int(bins)
         self.device = int(device)
@@ -115,6 +117,8 @@ class GeoBPEEngine:
         if rc:
             msg = self.L.geobpe_last_error(self._ctx) if self._ctx else b"create failed"
             raise _native.GeoBPEError(f"geobpe_create: {msg.decode() if msg else rc}")
+        if tail is not None:
+            self._chk(self.L.geobpe_set_tail(self._ctx, int(tail)))
         self.K0 = 0
         self.merges = []  # [(new_id, count, n_merged)]
         self.thresholds = None
