@@ -95,8 +95,9 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
     ap.add_argument("--roofline-kernel", default="auto", help="auto: the slowest merge-loop kernel")
-    ap.add_argument("--event-stride", type=int, default=1,
-                    help="time every k-th launch of the merge-loop kernels in the timed region (1: all)")
+    ap.add_argument("--event-stride", type=int, default=8,
+                    help="time every k-th launch of the merge-loop kernels in the timed region (event records "
+                         "are host work: at stride 1 the host, not the GPU, sets the pace)")
     ap.add_argument("--emit-merges", action="store_true",
                     help="add the merge list ([key string, count] of every merge so far) to the JSON line")
     return ap.parse_args()
@@ -216,28 +217,36 @@ def main():
             dist.destroy_process_group()
         return
 
-    # ---- per-kernel table: the live events of the timed region (every event_stride-th launch)
-    kern = {}
-    for k, (ms, nl) in ktimes.items():
-        if nl:
-            kern["select+place" if k == "select" else k] = {"ms_total": round(ms, 4), "launches": nl,
-                                                           "avg_us": round(1000 * ms / nl, 3)}
-    # k_commit's work (key records, decrement records, keys) for its algorithmic bytes: counted
-    # by an instrumented replay of the same merges (its atomics slow k_commit, so no times
-    # are taken from it)
-    commit_work = None
+    # ---- per-kernel table: a replay of the same merges with EVERY launch timed (the timed
+    # region samples every event_stride-th launch only); a second replay counts k_commit's
+    # work (key records, decrement records, keys) for its algorithmic bytes -- its counters'
+    # atomics slow k_commit, so no times are taken from that one
+    kern, replay_avg, commit_work = {}, {}, None
     if not args.no_profile and world == 1 and not args.no_replay:
-        rep = GeoBPEEngine(shard, B, device=local, max_vocab=1 << 20)
-        rep.initialize()
-        rep.bin()
-        rep.run(args.warmup)
-        rep.set_profiling(True, only="commit")  # (stride 1: k_commit's work counters on)
-        rs0 = rep.state()
-        rep.run(done)
-        rs1 = rep.state()
-        commit_work = {k: rs1[k] - rs0[k] for k in ("commit_key_records", "commit_decrement_records", "commit_keys")}
-        assert rep.merges == merges_log, "replay diverged"
-        rep.close()
+        for instrumented in (False, True):
+            rep = GeoBPEEngine(shard, B, device=local, max_vocab=1 << 20)
+            rep.initialize()
+            rep.bin()
+            rep.run(args.warmup)
+            names = "commit" if instrumented else "select,find,commit,tail,tail_build"
+            rep.set_profiling(True, only=names)  # (every launch)
+            rep.set_work_counters(instrumented)
+            rep.set_hold(3000 + 60 * min(done, 64))  # (the launches queue behind a spin: no host gaps)
+            rs0 = rep.state()
+            rep.run(done)
+            rs1 = rep.state()
+            if instrumented:
+                commit_work = {k: rs1[k] - rs0[k] for k in ("commit_key_records", "commit_decrement_records",
+                                                            "commit_keys")}
+            else:
+                for k in ("select", "find", "commit", "tail", "tail_build"):
+                    ms, nl = rep.kernel_ms(k)
+                    if nl:
+                        kern["select+place" if k == "select" else k] = {
+                            "ms_total": round(ms, 4), "launches": nl, "avg_us": round(1000 * ms / nl, 3)}
+                        replay_avg[k] = 1000 * ms / nl
+            assert rep.merges == merges_log, "replay diverged"
+            rep.close()
 
     # ---- roofline of the loop's kernels, from the live events of the timed region
     wkey = f"config={args.config},warmup={args.warmup},steps={args.steps},n={world}"
@@ -272,9 +281,10 @@ def main():
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
                     "traffic": traffic, "traffic_source": tsrc, "traffic_window": wkey,
                     "bytes_per_launch": round(bpl, 1) if bpl is not None else None, "avg_launch_us": round(avg_s * 1e6, 3),
-                    "launches_timed": nl, "event_stride": args.event_stride, "algorithmic_bytes": note}
-    if args.roofline_kernel == "auto":
-        dom = max(roofs, key=lambda k: roofs[k]["avg_launch_us"]) if roofs else None
+                    "launches_timed": nl, "event_stride": args.event_stride, "algorithmic_bytes": note,
+                    "replay_avg_launch_us": round(replay_avg[k], 3) if k in replay_avg else None}
+    if args.roofline_kernel == "auto":  # the slowest by every launch of the replay, else by the samples
+        dom = max(roofs, key=lambda k: replay_avg.get(k, roofs[k]["avg_launch_us"])) if roofs else None
     else:
         dom = args.roofline_kernel if args.roofline_kernel in roofs else None
     roofline = roofs.get(dom) if dom else None

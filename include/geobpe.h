@@ -100,7 +100,7 @@ int geobpe_step(geobpe_ctx *ctx, int32_t *new_id, int32_t *count, int64_t *n_mer
 int geobpe_run(geobpe_ctx *ctx, int64_t n_iters, int64_t *n_done);
 /* Late-merge path (same results): once a merge's count is <= max_count, geobpe_run /
  * geobpe_step run the merges in one workgroup over per-key posting lists (k_tail, many
- * merges per launch) instead of the full-grid kernels; 0 = never (default 4096;
+ * merges per launch) instead of the full-grid kernels; 0 = never (default 256;
  * environment GEOBPE_TAIL overrides at create).  Single rank, no merge replay. */
 int geobpe_set_tail(geobpe_ctx *ctx, int64_t max_count);
 /* The merge list so far: 3 int64 per merge (new id, count, merges applied);
@@ -190,6 +190,14 @@ int64_t geobpe_verify_counts(geobpe_ctx *ctx);
  * launch; on = k > 1: every k-th launch of each kernel (sampling keeps the event
  * packets from stretching the stream they measure). */
 int geobpe_set_profiling(geobpe_ctx *ctx, int on);
+/* k_commit's work counters (key records, decrement records, keys: geobpe_debug_state
+ * slots 10-12) on or off; geobpe_set_profiling with stride 1 turns them on (they slow
+ * k_commit: a timing run turns them off after it). */
+int geobpe_set_work_counters(geobpe_ctx *ctx, int on);
+/* Timing aid: geobpe_run enqueues a kernel that spins for `us` microseconds before each
+ * batch of iterations, so per-launch events measure kernels queued behind it rather than
+ * the host's enqueue pace (0 = off, the default). */
+int geobpe_set_hold(geobpe_ctx *ctx, int64_t us);
 /* Debug: per-workgroup phase timestamps (wall clock, 100 MHz) of k_select / k_find /
  * k_commit / k_place (tools/debug/merge_timeline.py).
  * on = 1 enables and clears (returns the slot count); on = 0 copies up to cap

@@ -76,9 +76,10 @@ struct geobpe_ctx {
   bool pipelined = false;     // between geobpe_pipeline_begin and _end (device-side parity)
   int nba = 256;  // find / commit / finalize / bin / import workgroups (= D.NBA, <= NBA_MAX)
   // late-merge path (tail.h): merges whose count is <= tail_thresh run in k_tail
-  int64_t tail_thresh = 4096;  // 0: never
+  int64_t tail_thresh = 256;   // 0: never
   bool tail_on = false;        // switched (one way: the full-grid kernels' posting index goes stale)
   bool tail_ready = false;     // its arrays are allocated
+  int64_t hold_us = 0;         // geobpe_set_hold: a k_hold launch before each batch of iterations
   // profiling
   bool prof = false;
   int prof_stride = 1;      // time every prof_stride-th launch of each kernel
@@ -904,6 +905,7 @@ int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) {
       break;
     }
     const int64_t batch = tail_batch(c, want);
+    if (c->hold_us > 0) hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, c->stream, (int64_t)(100 * c->hold_us));
     for (int64_t i = 0; i < batch; i++) enqueue_iteration(c);
     HIPCHK(c, hipGetLastError());
     if ((rc = sync_state(c))) return rc;
@@ -1328,6 +1330,18 @@ int geobpe_set_profiling(geobpe_ctx* c, int on) {
   c->D.stats = c->prof && c->prof_stride == 1 ? 1 : 0;  // (work counters only under full profiling)
   c->prof_seen.clear();
   c->ktime.clear();
+  return 0;
+}
+
+int geobpe_set_hold(geobpe_ctx* c, int64_t us) {
+  if (!c || us < 0 || us > 1000000) return GEOBPE_EARG;
+  c->hold_us = us;
+  return 0;
+}
+
+int geobpe_set_work_counters(geobpe_ctx* c, int on) {
+  if (!c) return GEOBPE_EARG;
+  c->D.stats = on ? 1 : 0;
   return 0;
 }
 

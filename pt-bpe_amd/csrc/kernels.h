@@ -10,6 +10,14 @@ __global__ void k_window_mark(int32_t tag, State* st) {
   if (tag == INT32_MIN && threadIdx.x == 64) st->nskip = 0;  // never taken; keeps the kernel non-empty
 }
 
+// timing aid (geobpe_set_hold): one thread spins for `ticks` of the 100 MHz wall clock, so
+// the host can queue the launches behind it and event-timed kernels start from a backlog
+// instead of waiting on the host's enqueue
+__global__ void k_hold(int64_t ticks) {
+  const int64_t t0 = (int64_t)wall_clock64();
+  while ((int64_t)wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+
 // ====================================================================== prologue
 __constant__ int32_t c_type_col[GEOBPE_NTYPES] = {GEOBPE_COL_TAU, GEOBPE_COL_CAC1N, GEOBPE_COL_C1NCA,
                                                   GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_PHI};

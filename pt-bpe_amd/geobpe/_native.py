@@ -80,6 +80,8 @@ def lib():
         "geobpe_verify_counts": (I64, [P]),
         "geobpe_debug_timeline": (I64, [P, ctypes.c_int, P, I64]),
         "geobpe_set_profiling": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_set_work_counters": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_set_hold": (ctypes.c_int, [P, I64]),
         "geobpe_kernel_ms": (D, [P, ctypes.c_char_p, pI64]),
         "geobpe_set_profiling_filter": (ctypes.c_int, [P, ctypes.c_char_p]),
         "geobpe_marker": (ctypes.c_int, [P, ctypes.c_int32]),
@@ -119,7 +121,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_set_rank", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",
-    "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_marker", "geobpe_synchronize",
+    "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_work_counters", "geobpe_set_hold", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_marker", "geobpe_synchronize",
     "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",
     "geobpe_delta_export_async", "geobpe_delta_import_async", "geobpe_pipeline_begin", "geobpe_pipeline_iter",
     "geobpe_pipeline_import", "geobpe_pipeline_poll", "geobpe_pipeline_resolve", "geobpe_pipeline_end", "geobpe_pdb_backbone", "geobpe_pdb_error",

@@ -451,6 +451,14 @@ class GeoBPEEngine:
         self._chk(self.L.geobpe_set_profiling_filter(self._ctx, only.encode()))
         self._chk(self.L.geobpe_set_profiling(self._ctx, max(1, int(stride)) if on else 0))
 
+    def set_hold(self, us: int = 0):
+        """A spin kernel of ``us`` microseconds before each batch of run() (event timing)."""
+        self._chk(self.L.geobpe_set_hold(self._ctx, int(us)))
+
+    def set_work_counters(self, on: bool = True):
+        """k_commit's work counters (state() keys commit_*) on or off."""
+        self._chk(self.L.geobpe_set_work_counters(self._ctx, 1 if on else 0))
+
     def state(self) -> dict:
         """Loop state (hot list, threshold, posting index) after a synchronisation."""
         v = np.zeros(13, dtype=np.int64)
