@@ -108,11 +108,12 @@ struct State {
   int32_t tail_exit;   // why the last k_tail stopped: 0 merges done / error, 1 + Sel decision otherwise
   int32_t tail_par;    // launch parity after the last k_tail
   int32_t pad5;
+  int64_t mid_nm[2], mid_nh[2];  // mid.h: merged occurrences / new pairs of k_mid_find, by launch parity
 };
 
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
 // and the host read it).  Every mark workgroup computes the same decision.
-constexpr int SEL_MERGE = 0, SEL_SKIP = 1, SEL_DONE = 2;
+constexpr int SEL_MERGE = 0, SEL_SKIP = 1, SEL_DONE = 2, SEL_STALL = 3;  // STALL: mid.h, lists being rebuilt
 struct Sel {
   int32_t decision;
   int32_t skip;       // SKIP_* bits of a rebuild iteration

@@ -80,6 +80,10 @@ struct geobpe_ctx {
   bool tail_on = false;        // switched (one way: the full-grid kernels' posting index goes stale)
   bool tail_ready = false;     // its arrays are allocated
   int64_t hold_us = 0;         // geobpe_set_hold: a k_hold launch before each batch of iterations
+  // middle regime (mid.h): merges whose count is <= mid_thresh run as k_mid_sel + k_mid_find
+  int64_t mid_thresh = 16384;  // 0: never
+  bool mid_on = false;         // switched (one way)
+  bool place_mid = false;      // the pending place is k_mid_sel's (else k_place's)
   // profiling
   bool prof = false;
   int prof_stride = 1;      // time every prof_stride-th launch of each kernel
@@ -193,12 +197,15 @@ int check_device_error(geobpe_ctx* c) {
   }
 }
 
-// the last committed merge's k_place, when no k_select has carried it yet
+// the last committed merge's k_place (or mid.h place), when no select launch has carried it yet
 void flush_place(geobpe_ctx* c) {
   if (!c->place_pending) return;
   c->place_pending = false;
   Timed t(c, "place");
-  hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D);
+  if (c->place_mid)
+    hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, c->D, INT32_MIN);
+  else
+    hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D);
 }
 
 int sync_state(geobpe_ctx* c) {
@@ -284,6 +291,7 @@ void enqueue_select(geobpe_ctx* c) {
                        (const ReplayRec*)c->replay, c->replay_n);
     return;
   }
+  if (c->place_pending && c->place_mid) flush_place(c);
   Timed t(c, "select");  // (+ the previous merge's k_place in workgroups 1..nba)
   const int grid = c->place_pending ? 1 + c->nba : 1;
   c->place_pending = false;
@@ -300,6 +308,7 @@ void enqueue_apply(geobpe_ctx* c) {
                        (int)(c->gen & 1));
   }
   c->place_pending = true;
+  c->place_mid = false;
 #ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
   flush_place(c);
 #endif
@@ -312,6 +321,25 @@ void enqueue_iteration(geobpe_ctx* c) {
   enqueue_select(c);
   enqueue_mark(c);
   enqueue_apply(c);
+}
+
+// one merge iteration of the middle regime (mid.h): select (+ the previous place) -> find
+void enqueue_iteration_mid(geobpe_ctx* c) {
+  const int par = (int)(c->gen & 1);
+  {
+    Timed t(c, "select");  // (+ the previous merge's place in workgroups 1..nba)
+    const bool carry = c->place_pending && c->place_mid;
+    if (c->place_pending && !c->place_mid) flush_place(c);
+    c->place_pending = false;
+    hipLaunchKernelGGL(k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->stream, c->D, par);
+  }
+  {
+    Timed t(c, "find");
+    hipLaunchKernelGGL(k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, par);
+  }
+  c->place_pending = true;
+  c->place_mid = true;
+  c->gen++;
 }
 
 // the Sel record of the last mark launch (after a sync)
@@ -388,15 +416,31 @@ int tail_run(geobpe_ctx* c, int64_t n) {
   return 0;
 }
 
-// the next batch of full-grid iterations before the switch is checked: long while the
-// merges are far above the threshold (the check costs a synchronisation)
+bool mid_enabled(const geobpe_ctx* c) { return c->mid_thresh > 0 && !c->distributed && !c->replay; }
+
+// the next batch of iterations before the regime switches are checked: long while the
+// merges are far above the next threshold (the check costs a synchronisation)
 int64_t tail_batch(const geobpe_ctx* c, int64_t want) {
-  if (!tail_enabled(c)) return want;
+  const bool mid = mid_enabled(c) && !c->mid_on, tail = tail_enabled(c);
+  if (!mid && !tail) return want;
+  const int64_t th = mid ? c->mid_thresh : c->tail_thresh;
   const int64_t m = c->h_state->maxc;
-  return std::min<int64_t>(want, m == 0 ? 16 : (m > 8 * c->tail_thresh ? 64 : 8));
+  return std::min<int64_t>(want, m == 0 ? 16 : (m > 8 * th ? 64 : 8));
 }
 void tail_check_switch(geobpe_ctx* c) {
-  if (tail_enabled(c) && c->h_state->maxc > 0 && c->h_state->maxc <= c->tail_thresh) c->tail_on = true;
+  const int64_t m = c->h_state->maxc;
+  if (m <= 0) return;
+  if (mid_enabled(c) && m <= c->mid_thresh) c->mid_on = true;
+  if (tail_enabled(c) && m <= c->tail_thresh) c->tail_on = true;
+}
+
+// per-key lists usable by the middle regime: built at the switch, rebuilt when a place
+// lost entries (the stalled iterations merged nothing) or the pool is 3/4 used
+int mid_prepare(geobpe_ctx* c) {
+  int rc;
+  if ((rc = tail_alloc(c))) return rc;
+  if (!c->h_state->kp_valid || c->h_state->kpool_used > c->D.KPOOL / 4 * 3) tail_build(c);
+  return 0;
 }
 
 }  // namespace
@@ -432,7 +476,8 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
     const int v = atoi(e);
     if (v >= 8 && v <= NBA_MAX) c->nba = v;
   }
-  if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = full-grid kernels only)
+  if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
+  if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
@@ -706,6 +751,13 @@ int geobpe_set_tail(geobpe_ctx* c, int64_t max_count) {
   return 0;
 }
 
+int geobpe_set_mid(geobpe_ctx* c, int64_t max_count) {
+  if (!c || max_count < 0) return GEOBPE_EARG;
+  c->mid_thresh = max_count;
+  if (!max_count && c->mid_on) return fail(c, GEOBPE_EARG, "the middle-regime path is already in use");
+  return 0;
+}
+
 int geobpe_set_bin_dense(geobpe_ctx* c, int on) {
   if (!c) return GEOBPE_EARG;
   if (c->keys_ready) return fail(c, GEOBPE_EARG, "set_bin_dense must precede bin()");
@@ -868,8 +920,14 @@ int geobpe_step(geobpe_ctx* c, int32_t* new_id, int32_t* count, int64_t* n_merge
   if (c->tail_on && tail_enabled(c)) {
     if ((rc = tail_run(c, 1))) return rc;
   } else {
-    for (;;) {  // a rebuild iteration merges nothing: go again
-      enqueue_iteration(c);
+    for (;;) {  // a rebuild (or stalled) iteration merges nothing: go again
+      const bool mid = c->mid_on && mid_enabled(c);
+      if (mid) {
+        if ((rc = mid_prepare(c))) return rc;
+        enqueue_iteration_mid(c);
+      } else {
+        enqueue_iteration(c);
+      }
       HIPCHK(c, hipGetLastError());
       if ((rc = sync_state(c))) return rc;
       if (c->h_state->iter != it0 || c->h_state->done) break;
@@ -904,9 +962,16 @@ int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) {
       if ((rc = tail_run(c, want))) return rc;
       break;
     }
+    const bool mid = c->mid_on && mid_enabled(c);
+    if (mid && (rc = mid_prepare(c))) return rc;
     const int64_t batch = tail_batch(c, want);
     if (c->hold_us > 0) hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, c->stream, (int64_t)(100 * c->hold_us));
-    for (int64_t i = 0; i < batch; i++) enqueue_iteration(c);
+    for (int64_t i = 0; i < batch; i++) {
+      if (mid)
+        enqueue_iteration_mid(c);
+      else
+        enqueue_iteration(c);
+    }
     HIPCHK(c, hipGetLastError());
     if ((rc = sync_state(c))) return rc;
     if (c->h_state->done) break;

@@ -1276,5 +1276,6 @@ __global__ __launch_bounds__(256) void k_debug_key_less(Dev D, const int32_t* pa
 }
 
 #include "tail.h"
+#include "mid.h"
 
 }  // namespace gb

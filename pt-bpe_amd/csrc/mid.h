@@ -1,0 +1,534 @@
+// mid.h -- the middle regime of BPE.step (foldingdiff/bpe.py:1792-2166): merges of up to
+// a few ten thousand occurrences, on the per-key posting lists of tail.h.  Included once,
+// by kernels.h, after tail.h.
+//
+// Two launches per merge:
+//   k_mid_sel   workgroup 0: select_core (argmax + reference tie-break); workgroups 1..G:
+//               the previous merge's place -- token rewrites, pk of the new pairs, and the
+//               new pairs' posting entries, each place workgroup owning the keys of one
+//               hash bucket (it groups its keys' new pairs in LDS and appends them, growing
+//               a list where needed: no other workgroup touches those lists, so no
+//               cross-workgroup allocation protocol)
+//   k_mid_find  G workgroups: the winner's list split over them, the greedy run walks of
+//               k_find, the new pairs' keys deduplicated per round in LDS and resolved once
+//               per (workgroup, key): find-or-claim, +n on the count (hot-list crossing);
+//               -1 on the destroyed pairs (LDS-aggregated); merged occurrences and new pairs
+//               to two global lists for the place
+// Compared with the full-grid find/commit/place (merge.h) there is no owner hand-off
+// (key records, decrement records, posting logs): the per-key lists make the candidates
+// exact and a late merge's keys are few per workgroup.
+#pragma once
+// (included inside namespace gb)
+
+constexpr int MKC = 1024;  // k_mid_find: new-key dedupe slots per round (LDS)
+constexpr int MPK = 2048;  // k_mid_sel place: key grouping slots per round (LDS)
+
+struct MidFindLds {
+  u64 key[MKC], h1[MKC], h2[MKC];
+  int4 rep[MKC];  // {len, idL, g, idR}
+  int32_t cnt[MKC], did[MKC];
+  int32_t occ[MKC];  // occupied slots, in insertion order
+  AggT<12> agg;      // count decrements
+  HotApp hot;
+  int32_t red[ABLOCK / 64];
+  int32_t nocc, nm, chk, ns;
+};
+
+// ---------------------------------------------------------------------- find
+struct MidCtx {
+  int32_t W, nid, wl, th, par, iter;
+  u64 w1, w2;
+  u64 pa1, pb1, pa2, pb2;
+};
+
+__device__ inline void mid_occ(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t a, int32_t ya, int32_t b,
+                               int32_t c) {
+  const int64_t j = wave_reserve64((unsigned long long*)&D.st->mid_nm[F.par]);
+  if (j < D.TMcap)
+    D.TM[j] = make_int4(a, ya, b, c);
+  else
+    set_error(D, GEOBPE_ECAPACITY, -70);
+  atomicAdd(&S.nm, 1);
+  if (D.ev) {  // merge events (record mode): (merge, left start, right start)
+    const int64_t k = wave_reserve64(D.ev_n);
+    if (k < D.ev_cap) D.ev[k] = make_int4(F.iter, a, b, 0);
+  }
+}
+
+__device__ inline void mid_pair(const Dev& D, const MidCtx& F, int32_t target, int32_t d) {
+  const int64_t j = wave_reserve64((unsigned long long*)&D.st->mid_nh[F.par]);
+  if (j < D.THcap)
+    D.TH[j] = make_int2(target, d);
+  else
+    set_error(D, GEOBPE_ECAPACITY, -71);
+}
+
+// a new pair resolved on its own (a run's later occurrence, or the round's table is full)
+__device__ void mid_single(const Dev& D, MidFindLds& S, const MidCtx& F, u64 h1, u64 h2, int32_t len, int32_t idL,
+                           int32_t g, int32_t idR, int32_t target) {
+  bool claimed;
+  const int32_t d = ht_insert(D, h1, h2, len, &claimed);
+  if (d < 0) return;
+  if (claimed) {
+    claim_payload(D, d, h1, h2, len, idL, g, idR);
+    klist_put(D, wave_reserve64((unsigned long long*)&D.st->U), d);
+    atomicAdd((unsigned long long*)&D.st->nkeys, 1ULL);
+  } else {
+    emit_check(D, &S.chk, d, len, h1, h2);
+  }
+  count_add_hot(D, S.hot, d, 1, F.th);
+  mid_pair(D, F, target, d);
+}
+
+struct MidHalf {
+  u64 pkey, h1, h2;
+  int32_t len, idL, g, idR, target;
+};
+
+__device__ inline void mid_right(const Dev& D, const MidCtx& F, int32_t t, int32_t glR, bool cL, int32_t idc,
+                                 int32_t lc, u64 c1, u64 c2, MidHalf& h) {
+  const int32_t rl = cL ? F.wl : lc;
+  const u64 r1 = cL ? F.w1 : c1, r2 = cL ? F.w2 : c2;
+  const int64_t ny = 2 * (int64_t)rl - 1;
+  combine_pw(F.w1, F.w2, glR, r1, r2, D.pw1[ny + 1], D.pw1[ny], D.pw2[ny + 1], D.pw2[ny], h.h1, h.h2);
+  h.len = F.wl + rl;
+  h.pkey = probe_key(h.h1, h.h2, h.len);
+  h.idL = F.nid;
+  h.g = glR;
+  h.idR = cL ? F.nid : idc;
+  h.target = t;
+}
+
+// the walk of merge.h find_walk: the first occurrence's new pairs are returned (grouped
+// by the caller), a run's later occurrences resolve theirs on their own
+__device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g, MidHalf& hl, bool& vl, MidHalf& hr,
+                         bool& vr) {
+  vl = vr = false;
+  const int32_t W = F.W;
+  const int4 tg = D.tok[g];
+  if (tg.w != W) return;  // (a stale list entry)
+  const int32_t p = tg.z;
+  const int32_t b = g + tok_len(tg.y);
+  const int4 tp = D.tok[p >= 0 ? p : g];
+  const int4 tb = D.tok[b];
+  if (p >= 0 && tp.w == W) return;  // not a run start
+  const int32_t glL = p >= 0 ? next_glue(D, tp.y, g - 1) : 0;
+  const int32_t glR = next_glue(D, tb.y, g + F.wl - 1);
+  const int32_t pkb = tb.w;
+  const int32_t c = pkb >= 0 ? b + tok_len(tb.y) : -1;
+  const int4 tc = D.tok[c >= 0 ? c : g];
+  const int32_t pp = p >= 0 ? tp.z : -1;
+  const int4 tpp = D.tok[pp >= 0 ? pp : g];
+  const int32_t vp = p >= 0 ? max(tp.x, 0) : 0;
+  const u64 l1 = D.vh1[vp], l2 = D.vh2[vp];
+  const bool cL = c >= 0 && tc.w == W;
+  const int32_t vc = c >= 0 ? max(tc.x, 0) : 0;
+  const u64 c1 = D.vh1[vc], c2 = D.vh2[vc];
+  bool pRight = false;
+  if (p >= 0 && pp >= 0 && tpp.w == W) {  // the W-run ending at (pp, p): its length's parity
+    int32_t m = 1, y = tpp.z;
+    for (;;) {
+      if (y < 0) break;
+      const int4 ty = D.tok[y];
+      if (ty.w != W) break;
+      m++;
+      y = ty.z;
+    }
+    pRight = (m & 1) != 0;
+  }
+  const bool pN = p >= 0 && !pRight;
+  mid_occ(D, S, F, g, F.wl | (tb.y & (int32_t)0xFFFF0000), b, c);
+  if (pkb >= 0 && !agg_stage(S.agg, pkb, -1)) atomicAdd(&D.count[pkb], -1);
+  if (pN) {
+    if (!agg_stage(S.agg, tp.w, -1)) atomicAdd(&D.count[tp.w], -1);
+    combine_pw(l1, l2, glL, F.w1, F.w2, F.pa1, F.pb1, F.pa2, F.pb2, hl.h1, hl.h2);
+    hl.len = tok_len(tp.y) + F.wl;
+    hl.pkey = probe_key(hl.h1, hl.h2, hl.len);
+    hl.idL = tp.x;
+    hl.g = glL;
+    hl.idR = F.nid;
+    hl.target = p;
+    vl = true;
+  }
+  if (c >= 0) {
+    mid_right(D, F, g, glR, cL, tc.x, tok_len(tc.y), c1, c2, hr);
+    vr = true;
+  }
+  int32_t cur_c = c, cur_pkb = pkb;
+  bool cur_cL = cL;
+  int32_t lcur_c = tok_len(tc.y);
+  while (cur_pkb == W && cur_cL) {  // the rest of the run
+    const int32_t t = cur_c;
+    const int32_t b2 = t + lcur_c;
+    const int4 tb2 = D.tok[b2];
+    const int32_t glR2 = next_glue(D, tb2.y, t + F.wl - 1);
+    const int32_t pkb2 = tb2.w;
+    const int32_t c2i = pkb2 >= 0 ? b2 + tok_len(tb2.y) : -1;
+    const int4 tc2 = D.tok[c2i >= 0 ? c2i : t];
+    const bool cL2 = c2i >= 0 && tc2.w == W;
+    const int32_t vc2 = c2i >= 0 ? max(tc2.x, 0) : 0;
+    const u64 d1 = D.vh1[vc2], d2 = D.vh2[vc2];
+    mid_occ(D, S, F, t, F.wl | (tb2.y & (int32_t)0xFFFF0000), b2, c2i);
+    if (pkb2 >= 0 && !agg_stage(S.agg, pkb2, -1)) atomicAdd(&D.count[pkb2], -1);
+    if (c2i >= 0) {
+      MidHalf h;
+      mid_right(D, F, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
+      mid_single(D, S, F, h.h1, h.h2, h.len, h.idL, h.g, h.idR, h.target);
+    }
+    cur_c = c2i;
+    cur_pkb = pkb2;
+    cur_cL = cL2;
+    lcur_c = tok_len(tc2.y);
+  }
+}
+
+// round table slot of a new key; -1 when the probes run out (*ins: this thread inserted it)
+__device__ inline int32_t mkc_slot(MidFindLds& S, const MidHalf& h, bool* ins) {
+  int32_t s = (int32_t)((h.pkey * 0x9E3779B97F4A7C15ULL) >> (64 - 10)) & (MKC - 1);
+  *ins = false;
+#pragma unroll 1
+  for (int probe = 0; probe < 16; probe++, s = (s + 1) & (MKC - 1)) {
+    u64 c = S.key[s];
+    if (c == 0) {
+      c = atomicCAS((unsigned long long*)&S.key[s], 0ULL, (unsigned long long)h.pkey);
+      if (c == 0) {
+        *ins = true;
+        return s;
+      }
+    }
+    if (c == h.pkey) return s;
+  }
+  return -1;
+}
+
+__global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
+  __shared__ MidFindLds S;
+  State* st = D.st;
+  const int32_t w = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  Sel sel = D.sel[par];
+  // lists that lost entries (a place ran out of table or pool space in the launch that
+  // selected this merge): no merge until the host rebuilds them -- the select wrote only
+  // what the next select overwrites (Sel, the log entry, the new token's hashes)
+  if (!st->kp_valid) sel.decision = SEL_STALL;
+  check_found(D, w);  // keys the previous merge found in this region (EHASH)
+  if (w == 0 && t == 0) {
+    st->mid_nm[par ^ 1] = 0;  // the next merge's lists (the place of the last one has run)
+    st->mid_nh[par ^ 1] = 0;
+    st->place_par = sel.decision == SEL_MERGE ? par : -1;
+    if (sel.decision == SEL_DONE) {
+      st->done = 1;
+      st->maxc = 0;
+    } else if (sel.decision == SEL_SKIP) {
+      st->nskip += 1;
+    }
+  }
+  if (sel.decision == SEL_DONE || sel.decision == SEL_STALL) return;
+  if (sel.decision == SEL_SKIP) {
+    if (t == 0) D.chkcnt[w] = 0;
+    if (sel.skip & SKIP_MEASURE) measure_max(D);
+    if (sel.skip & SKIP_HOT) rebuild_hot_list(D, sel.theta_new, sel.build);
+    return;
+  }
+  MidCtx F;
+  F.W = sel.W;
+  F.nid = sel.nid;
+  F.wl = sel.wl;
+  F.w1 = sel.w1;
+  F.w2 = sel.w2;
+  F.th = st->theta;
+  F.par = par;
+  F.iter = sel.iter;
+  {
+    const int64_t nw = 2 * (int64_t)max(F.wl, 1) - 1;
+    F.pa1 = D.pw1[nw + 1];
+    F.pb1 = D.pw1[nw];
+    F.pa2 = D.pw2[nw + 1];
+    F.pb2 = D.pw2[nw];
+  }
+  if (w == 0) {  // _tokens[n] = json.loads(key); merge log; state the next select reads
+    const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
+    const int64_t vL = D.voff[L], vR = D.voff[Rr];
+    const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
+    const int64_t pos = D.voff[F.nid], ln = nL + 1 + nR;
+    if (pos + ln > D.VSC) {
+      if (t == 0) set_error(D, GEOBPE_ECAPACITY, -9);
+    } else {
+      for (int64_t i = t; i < ln; i += ABLOCK)
+        D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
+      if (t == 0) D.voff[F.nid + 1] = pos + ln;
+    }
+    if (t == 0) {
+      st->iter = sel.iter + 1;
+      st->K = sel.nid + 1;
+      st->maxc = sel.maxc;
+      st->ncand = sel.ncand;
+    }
+  }
+  for (int i = t; i < MKC; i += ABLOCK) {
+    S.key[i] = 0;
+    S.cnt[i] = 0;
+  }
+  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+    S.agg.key[i] = -1;
+    S.agg.val[i] = 0;
+  }
+  if (t == 0) {
+    S.nocc = S.nm = S.chk = 0;
+    S.hot.n = 0;
+  }
+  __syncthreads();
+  const int32_t nW = D.kp_n[F.W];
+  const int64_t offW = D.kp_off[F.W];
+  const int32_t lo = (int32_t)((int64_t)nW * w / G), hi = (int32_t)((int64_t)nW * (w + 1) / G);
+  for (int32_t c0 = lo; c0 < hi; c0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
+    const int32_t i = c0 + t;
+    MidHalf hl, hr;
+    bool vl = false, vr = false;
+    if (i < hi) mid_walk(D, S, F, D.kpool[offW + i], hl, vl, hr, vr);
+    // ---- this round's new keys: LDS dedupe, then one resolve + count update per key
+    bool il = false, ir = false;
+    int32_t sl = -1, sr = -1;
+    if (vl) {
+      sl = mkc_slot(S, hl, &il);
+      if (sl >= 0) atomicAdd(&S.cnt[sl], 1);
+    }
+    if (vr) {
+      sr = mkc_slot(S, hr, &ir);
+      if (sr >= 0) atomicAdd(&S.cnt[sr], 1);
+    }
+    if (il) {
+      S.h1[sl] = hl.h1;
+      S.h2[sl] = hl.h2;
+      S.rep[sl] = make_int4(hl.len, hl.idL, hl.g, hl.idR);
+      S.occ[atomicAdd(&S.nocc, 1)] = sl;
+    }
+    if (ir) {
+      S.h1[sr] = hr.h1;
+      S.h2[sr] = hr.h2;
+      S.rep[sr] = make_int4(hr.len, hr.idL, hr.g, hr.idR);
+      S.occ[atomicAdd(&S.nocc, 1)] = sr;
+    }
+    if (vl && sl < 0) mid_single(D, S, F, hl.h1, hl.h2, hl.len, hl.idL, hl.g, hl.idR, hl.target);
+    if (vr && sr < 0) mid_single(D, S, F, hr.h1, hr.h2, hr.len, hr.idL, hr.g, hr.idR, hr.target);
+    __syncthreads();
+    const int32_t nocc = S.nocc;
+    for (int32_t q = t; q < nocc; q += ABLOCK) {
+      const int32_t s = S.occ[q];
+      const int4 rp = S.rep[s];
+      bool claimed;
+      const u64 h1 = S.h1[s], h2 = S.h2[s];
+      const int32_t d = ht_insert(D, h1, h2, rp.x, &claimed);
+      S.did[s] = d;
+      if (d < 0) continue;
+      if (claimed) {
+        claim_payload(D, d, h1, h2, rp.x, rp.y, rp.z, rp.w);
+        klist_put(D, wave_reserve64((unsigned long long*)&st->U), d);
+        atomicAdd((unsigned long long*)&st->nkeys, 1ULL);
+      } else {
+        emit_check(D, &S.chk, d, rp.x, h1, h2);
+      }
+      count_add_hot(D, S.hot, d, S.cnt[s], F.th);
+    }
+    __syncthreads();
+    if (vl && sl >= 0) {
+      if (S.h1[sl] != hl.h1) set_error(D, GEOBPE_EHASH, -13);  // same probe key, other content
+      if (S.did[sl] >= 0) mid_pair(D, F, hl.target, S.did[sl]);
+    }
+    if (vr && sr >= 0) {
+      if (S.h1[sr] != hr.h1) set_error(D, GEOBPE_EHASH, -13);
+      if (S.did[sr] >= 0) mid_pair(D, F, hr.target, S.did[sr]);
+    }
+    __syncthreads();
+    for (int32_t q = t; q < nocc; q += ABLOCK) {  // clear the round's slots
+      const int32_t s = S.occ[q];
+      S.key[s] = 0;
+      S.cnt[s] = 0;
+    }
+    if (t == 0) S.nocc = 0;
+    __syncthreads();
+  }
+  // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
+  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+    const int32_t k = S.agg.key[i], v = S.agg.val[i];
+    if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
+  }
+  if (t == 0 && S.nm) {
+    atomicAdd(&D.count[F.W], -S.nm);
+    atomicAdd((unsigned long long*)&D.log[sel.iter].nmerged, (unsigned long long)S.nm);
+  }
+  hot_flush(D, S.hot);  // (syncs the workgroup first)
+  if (t == 0) D.chkcnt[w] = min(S.chk, (int32_t)D.RC);
+}
+
+// ---------------------------------------------------------------------- place
+struct MidPlaceLds {
+  int32_t key[MPK], cnt[MPK], base[MPK], cur[MPK];
+  int32_t occ[MPK];
+  int32_t big_old[TAIL_BIG], big_new[TAIL_BIG], big_pre[TAIL_BIG + 1];
+  int32_t red[ABLOCK / 64];
+  int32_t nocc, nbig, full;
+};
+
+__device__ inline uint32_t mid_bucket(int32_t d, int32_t G) {
+  return (uint32_t)(((u64)((uint32_t)d * 2654435761u) * (u64)G) >> 32);
+}
+
+// the key's slot in the place table (insert: claim an empty one); -1: not there / full
+__device__ inline int32_t mpk_slot(MidPlaceLds& S, int32_t d, bool insert, bool* ins) {
+  int32_t s = (int32_t)(((uint32_t)d * 0x85EBCA6Bu) >> (32 - 11)) & (MPK - 1);
+  *ins = false;
+#pragma unroll 1
+  for (int probe = 0; probe < 64; probe++, s = (s + 1) & (MPK - 1)) {
+    int32_t c = S.key[s];
+    if (c == -1) {
+      if (!insert) return -1;
+      c = atomicCAS(&S.key[s], -1, d);
+      if (c == -1) {
+        *ins = true;
+        return s;
+      }
+    }
+    if (c == d) return s;
+  }
+  return -1;
+}
+
+constexpr int MP_UNR = 8;  // new-pair list entries in flight per thread
+
+// place workgroup b of G: token rewrites and pk of its share of the merged occurrences and
+// new pairs, then the posting entries of the new pairs whose key is in bucket b -- one pass
+// counts them per key, the lists grow where needed, a second pass writes the entries
+__device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& S) {
+  State* st = D.st;
+  const int32_t par = st->place_par;
+  if (par < 0) return;
+  const Sel sel = D.sel[par];
+  if (sel.decision != SEL_MERGE) return;
+  const int32_t t = threadIdx.x;
+  const int64_t nm = min(st->mid_nm[par], D.TMcap), nh = min(st->mid_nh[par], D.THcap);
+  for (int i = t; i < MPK; i += ABLOCK) {
+    S.key[i] = -1;
+    S.cnt[i] = 0;
+    S.cur[i] = 0;
+  }
+  if (t == 0) S.nocc = S.nbig = S.full = 0;
+  for (int64_t i = nm * b / G + t; i < nm * (b + 1) / G; i += ABLOCK) {
+    const int4 e = D.TM[i];
+    *reinterpret_cast<int2*>(D.tok + e.x) = make_int2(sel.nid, e.y);
+    D.tok[e.z] = make_int4(-1, 0, -1, -1);
+    if (e.w >= 0)
+      *tok_f(D, e.w, 2) = e.x;
+    else
+      *tok_f(D, e.x, 3) = -1;
+  }
+  for (int64_t i = nh * b / G + t; i < nh * (b + 1) / G; i += ABLOCK) {
+    const int2 h = D.TH[i];
+    *tok_f(D, h.x, 3) = h.y;
+  }
+  __syncthreads();
+  // ---- pass 1: new entries per key of bucket b
+  for (int64_t i0 = t; i0 < nh; i0 += MP_UNR * ABLOCK) {
+    int32_t d[MP_UNR];
+#pragma unroll
+    for (int u = 0; u < MP_UNR; u++) d[u] = i0 + u * ABLOCK < nh ? D.TH[i0 + u * ABLOCK].y : -1;
+#pragma unroll
+    for (int u = 0; u < MP_UNR; u++) {
+      if (d[u] < 0 || mid_bucket(d[u], G) != (uint32_t)b) continue;
+      bool ins;
+      const int32_t s = mpk_slot(S, d[u], true, &ins);
+      if (s < 0) {
+        S.full = 1;  // (more keys than the table: the lists are rebuilt)
+        continue;
+      }
+      atomicAdd(&S.cnt[s], 1);
+      if (ins) S.occ[atomicAdd(&S.nocc, 1)] = s;
+    }
+  }
+  __syncthreads();
+  // ---- room for every key's new entries (a full list grows to 2x)
+  const int32_t nocc = S.nocc;
+  for (int32_t q = t; q < nocc; q += ABLOCK) {
+    const int32_t sl = S.occ[q];
+    const int32_t d = S.key[sl], add = S.cnt[sl];
+    const int32_t n = D.kp_n[d], cap = D.kp_cap[d];
+    S.base[sl] = n;
+    if (n + add > cap) {
+      const int32_t ncap = max(2 * (n + add), 16);
+      const int64_t at = (int64_t)atomicAdd((unsigned long long*)&st->kpool_used, (unsigned long long)ncap);
+      if (at + ncap > D.KPOOL) {
+        S.full = 1;
+        continue;
+      }
+      const int32_t old = D.kp_off[d];
+      if (n <= TAIL_SMALL) {
+        for (int32_t k = 0; k < n; k++) D.kpool[at + k] = D.kpool[(int64_t)old + k];
+      } else {
+        const int32_t x = atomicAdd(&S.nbig, 1);
+        if (x < TAIL_BIG) {
+          S.big_old[x] = old;
+          S.big_new[x] = (int32_t)at;
+          S.big_pre[x] = n;
+        } else {
+          S.full = 1;
+        }
+      }
+      D.kp_off[d] = (int32_t)at;
+      D.kp_cap[d] = ncap;
+    }
+    D.kp_n[d] = n + add;
+  }
+  __syncthreads();
+  const int32_t nb = min(S.nbig, TAIL_BIG);
+  if (nb > 0) {  // the big lists' old entries, by the whole workgroup
+    int32_t tc;
+    const int32_t cx = block_excl_scan(t < nb ? S.big_pre[t] : 0, &tc, S.red);
+    __syncthreads();
+    if (t < nb) S.big_pre[t] = cx;
+    if (t == 0) S.big_pre[nb] = tc;
+    __syncthreads();
+    for (int32_t q = t; q < tc; q += ABLOCK) {
+      const int32_t r = seg_of(S.big_pre, nb, q);
+      const int32_t k = q - S.big_pre[r];
+      D.kpool[(int64_t)S.big_new[r] + k] = D.kpool[(int64_t)S.big_old[r] + k];
+    }
+  }
+  // ---- pass 2: the entries
+  for (int64_t i0 = t; i0 < nh; i0 += MP_UNR * ABLOCK) {
+    int2 h[MP_UNR];
+#pragma unroll
+    for (int u = 0; u < MP_UNR; u++) h[u] = i0 + u * ABLOCK < nh ? D.TH[i0 + u * ABLOCK] : make_int2(-1, -1);
+#pragma unroll
+    for (int u = 0; u < MP_UNR; u++) {
+      if (h[u].y < 0 || mid_bucket(h[u].y, G) != (uint32_t)b) continue;
+      bool ins;
+      const int32_t s = mpk_slot(S, h[u].y, false, &ins);
+      if (s < 0) continue;
+      const int32_t r = atomicAdd(&S.cur[s], 1);
+      D.kpool[(int64_t)D.kp_off[h[u].y] + S.base[s] + r] = h[u].x;
+    }
+  }
+  __syncthreads();
+  if (S.full && t == 0) st->kp_valid = 0;
+}
+
+// workgroup 0: select (par >= 0; INT32_MIN: place only); workgroups 1..G: the place of the
+// merge st->place_par
+__global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par) {
+  if (blockIdx.x > 0) {
+    __shared__ MidPlaceLds P;
+    mid_place_body(D, blockIdx.x - 1, gridDim.x - 1, P);
+    return;
+  }
+  if (par == INT32_MIN) return;
+  __shared__ int32_t s_red[SBLOCK / 64];
+  __shared__ SelStage S;
+  if (!D.st->kp_valid) {  // the lists lost entries: no merge until the host rebuilds them
+    if (threadIdx.x == 0) {
+      Sel o{};
+      o.decision = SEL_STALL;
+      D.sel[par] = o;
+    }
+    return;
+  }
+  select_core<false>(D, par, S, s_red, nullptr);
+}

@@ -82,11 +82,14 @@ def _stream_handle(device: int):
 class GeoBPEEngine:
     def __init__(self, corpus: dict, bins: int, device: int = 0, max_vocab: int = 1 << 20,
                  group=None, stream=None, use_torch_stream: bool = True, cover: bool = False,
-                 bin_dense: bool = True, strategy: Optional[str] = None, tail: Optional[int] = None):
+                 bin_dense: bool = True, strategy: Optional[str] = None, tail: Optional[int] = None,
+                 mid: Optional[int] = None):
         """``corpus``: ``{column: float64[R]}`` + ``row_off`` (geobpe.synth layout) for
         THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs.
         ``tail``: merges of at most this count run in the one-workgroup late-merge
-        kernel (include/geobpe.h geobpe_set_tail; None = the library default, 0 = never)."""
+        kernel (include/geobpe.h geobpe_set_tail; None = the library default, 0 = never);
+        ``mid``: merges of at most this count run in the two-launch middle-regime kernels
+        (geobpe_set_mid)."""
         self.L = _native.lib()
         self.B = int(bins)
         self.device = int(device)
@@ -119,6 +122,8 @@ class GeoBPEEngine:
             raise _native.GeoBPEError(f"geobpe_create: {msg.decode() if msg else rc}")
         if tail is not None:
             self._chk(self.L.geobpe_set_tail(self._ctx, int(tail)))
+        if mid is not None:
+            self._chk(self.L.geobpe_set_mid(self._ctx, int(mid)))
         self.K0 = 0
         self.merges = []  # [(new_id, count, n_merged)]
         self.thresholds = None

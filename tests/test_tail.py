@@ -1,7 +1,8 @@
-"""The late-merge path (csrc/tail.h, k_tail): the same merges as the full-grid kernels
-and the CPU oracle, bit-exact (merge list with key strings and counts, encoded ids,
-incremental counts = a full recount), whether the switch happens at the first merge,
-mid-run or never.  Reference semantics: foldingdiff/bpe.py:1792-2166 (step)."""
+"""The middle-regime and late-merge paths (csrc/mid.h k_mid_sel + k_mid_find, csrc/tail.h
+k_tail): the same merges as the full-grid kernels and the CPU oracle, bit-exact (merge list
+with key strings and counts, encoded ids, incremental counts = a full recount), whether
+the switches happen at the first merge, mid-run or never.  Reference semantics:
+foldingdiff/bpe.py:1792-2166 (step)."""
 import numpy as np
 import pytest
 
@@ -24,18 +25,23 @@ def _oracle(oracle_lib, corpus, B, n):
     return o
 
 
-@pytest.mark.parametrize("tail", [0, 200, ALL_TAIL])
+# (mid, tail) thresholds: full-grid only, mid only, full-grid -> mid, mid -> tail,
+# full-grid -> mid -> tail, tail only
+REGIMES = [(0, 0), (ALL_TAIL, 0), (500, 0), (ALL_TAIL, 150), (600, 100), (0, ALL_TAIL)]
+
+
+@pytest.mark.parametrize("mid, tail", REGIMES)
 @pytest.mark.parametrize("cfg", [
     dict(n=2000, lo=40, hi=300, B=5, merges=400, seed=21, rep=0.0),
     dict(n=500, lo=40, hi=200, B=2, merges=400, seed=22, rep=0.05),  # long tokens, long runs
     dict(n=300, lo=1, hi=40, B=3, merges=300, seed=24, rep=0.2),     # 1-residue chains, repeats
     dict(n=800, lo=30, hi=250, B=12, merges=250, seed=23, rep=0.0),  # two-digit bins
 ])
-def test_tail_matches_oracle(cfg, tail, oracle_lib):
+def test_regimes_match_oracle(cfg, mid, tail, oracle_lib):
     from geobpe.engine import GeoBPEEngine
     corpus = _corpus(cfg["n"], cfg["lo"], cfg["hi"], cfg["seed"], cfg["rep"])
     o = _oracle(oracle_lib, corpus, cfg["B"], cfg["merges"])
-    eng = GeoBPEEngine(corpus, cfg["B"], device=0, tail=tail).initialize()
+    eng = GeoBPEEngine(corpus, cfg["B"], device=0, tail=tail, mid=mid).initialize()
     eng.bin()
     done = eng.run(10) + eng.run(cfg["merges"] - 10)
     assert done == len(o.merges)
@@ -47,13 +53,14 @@ def test_tail_matches_oracle(cfg, tail, oracle_lib):
     eng.close()
 
 
-def test_tail_step_by_step_and_exhaustion(oracle_lib):
-    """step() in the late-merge path, then run() to exhaustion (hot-list rebuilds and the
-    end handed to k_commit)."""
+@pytest.mark.parametrize("mid, tail", [(0, ALL_TAIL), (ALL_TAIL, 0)])
+def test_step_by_step_and_exhaustion(mid, tail, oracle_lib):
+    """step() in the late-merge / middle-regime path, then run() to exhaustion (hot-list
+    rebuilds and the end handled by k_commit / k_mid_find)."""
     from geobpe.engine import GeoBPEEngine
     corpus = _corpus(200, 5, 60, 31, 0.3)
     o = _oracle(oracle_lib, corpus, 3, 10 ** 6)
-    eng = GeoBPEEngine(corpus, 3, device=0, tail=ALL_TAIL).initialize()
+    eng = GeoBPEEngine(corpus, 3, device=0, tail=tail, mid=mid).initialize()
     eng.bin()
     for _ in range(40):
         assert eng.step() is not None
@@ -67,20 +74,21 @@ def test_tail_step_by_step_and_exhaustion(oracle_lib):
     eng.close()
 
 
-def test_tail_merge_events_match_full_grid():
-    """The merge-event log (the checkpoint's merge tree) of the late-merge path equals the
-    full-grid kernels'."""
+def test_merge_events_match_full_grid():
+    """The merge-event log (the checkpoint's merge tree) of the middle-regime and late-merge
+    paths equals the full-grid kernels'."""
     from geobpe.engine import GeoBPEEngine
     corpus = _corpus(400, 20, 120, 33, 0.1)
     out = []
-    for tail in (0, ALL_TAIL):
-        eng = GeoBPEEngine(corpus, 5, device=0, tail=tail).initialize()
+    for mid, tail in ((0, 0), (0, ALL_TAIL), (ALL_TAIL, 0)):
+        eng = GeoBPEEngine(corpus, 5, device=0, tail=tail, mid=mid).initialize()
         eng.record_events(True)
         eng.bin()
         eng.run(150)
         a, b, off = eng.events()
         out.append((eng.merge_keys(), a, b, off))
         eng.close()
-    assert out[0][0] == out[1][0]
-    for x, y in zip(out[0][1:], out[1][1:]):
-        assert np.array_equal(x, y)
+    for o in out[1:]:
+        assert out[0][0] == o[0]
+        for x, y in zip(out[0][1:], o[1:]):
+            assert np.array_equal(x, y)
