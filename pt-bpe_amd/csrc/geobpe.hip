@@ -369,7 +369,8 @@ int tail_alloc(geobpe_ctx* c) {
   D.TMcap = c->R / 2 + 1024;
   D.THcap = c->R + 2048;
   int rc;
-  if ((rc = dalloc(c, &D.kp_off, D.HC)) || (rc = dalloc(c, &D.kp_n, D.HC)) || (rc = dalloc(c, &D.kp_cap, D.HC)) ||
+  // (zero: a key claimed after the list build starts with an empty list of capacity 0)
+  if ((rc = dalloc(c, &D.kp_off, D.HC, 0)) || (rc = dalloc(c, &D.kp_n, D.HC, 0)) || (rc = dalloc(c, &D.kp_cap, D.HC, 0)) ||
       (rc = dalloc(c, &D.kpool, D.KPOOL)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, D.THcap)) ||
       (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)))
     return rc;
