@@ -205,6 +205,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
   __shared__ MidFindLds S;
   State* st = D.st;
   const int32_t w = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  dbg_stamp(D, 10);
   Sel sel = D.sel[par];
   // lists that lost entries (a place ran out of table or pool space in the launch that
   // selected this merge): no merge until the host rebuilds them -- the select wrote only
@@ -277,6 +278,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
     S.hot.n = 0;
   }
   __syncthreads();
+  dbg_stamp(D, 11);
   const int32_t nW = D.kp_n[F.W];
   const int64_t offW = D.kp_off[F.W];
   const int32_t lo = (int32_t)((int64_t)nW * w / G), hi = (int32_t)((int64_t)nW * (w + 1) / G);
@@ -285,6 +287,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
     MidHalf hl, hr;
     bool vl = false, vr = false;
     if (i < hi) mid_walk(D, S, F, D.kpool[offW + i], hl, vl, hr, vr);
+    if (c0 == lo) dbg_stamp(D, 15);
     // ---- this round's new keys: LDS dedupe, then one resolve + count update per key
     bool il = false, ir = false;
     int32_t sl = -1, sr = -1;
@@ -311,6 +314,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
     if (vl && sl < 0) mid_single(D, S, F, hl.h1, hl.h2, hl.len, hl.idL, hl.g, hl.idR, hl.target);
     if (vr && sr < 0) mid_single(D, S, F, hr.h1, hr.h2, hr.len, hr.idL, hr.g, hr.idR, hr.target);
     __syncthreads();
+    if (c0 == lo) dbg_stamp(D, 16);
     const int32_t nocc = S.nocc;
     for (int32_t q = t; q < nocc; q += ABLOCK) {
       const int32_t s = S.occ[q];
@@ -330,6 +334,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
       count_add_hot(D, S.hot, d, S.cnt[s], F.th);
     }
     __syncthreads();
+    if (c0 == lo) dbg_stamp(D, 17);
     if (vl && sl >= 0) {
       if (S.h1[sl] != hl.h1) set_error(D, GEOBPE_EHASH, -13);  // same probe key, other content
       if (S.did[sl] >= 0) mid_pair(D, F, hl.target, S.did[sl]);
@@ -347,6 +352,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
     if (t == 0) S.nocc = 0;
     __syncthreads();
   }
+  dbg_stamp(D, 12);
   // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
   for (int i = t; i < AggT<12>::N; i += ABLOCK) {
     const int32_t k = S.agg.key[i], v = S.agg.val[i];
@@ -358,6 +364,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
   }
   hot_flush(D, S.hot);  // (syncs the workgroup first)
   if (t == 0) D.chkcnt[w] = min(S.chk, (int32_t)D.RC);
+  dbg_stamp(D, 13);
 }
 
 // ---------------------------------------------------------------------- place
@@ -405,6 +412,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& 
   const Sel sel = D.sel[par];
   if (sel.decision != SEL_MERGE) return;
   const int32_t t = threadIdx.x;
+  dbg_stamp(D, 30);
   const int64_t nm = min(st->mid_nm[par], D.TMcap), nh = min(st->mid_nh[par], D.THcap);
   for (int i = t; i < MPK; i += ABLOCK) {
     S.key[i] = -1;
@@ -426,6 +434,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& 
     *tok_f(D, h.x, 3) = h.y;
   }
   __syncthreads();
+  dbg_stamp(D, 31);
   // ---- pass 1: new entries per key of bucket b
   for (int64_t i0 = t; i0 < nh; i0 += MP_UNR * ABLOCK) {
     int32_t d[MP_UNR];
@@ -445,6 +454,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& 
     }
   }
   __syncthreads();
+  dbg_stamp(D, 32);
   // ---- room for every key's new entries (a full list grows to 2x)
   const int32_t nocc = S.nocc;
   for (int32_t q = t; q < nocc; q += ABLOCK) {
@@ -478,6 +488,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& 
     D.kp_n[d] = n + add;
   }
   __syncthreads();
+  dbg_stamp(D, 33);
   const int32_t nb = min(S.nbig, TAIL_BIG);
   if (nb > 0) {  // the big lists' old entries, by the whole workgroup
     int32_t tc;
@@ -508,6 +519,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& 
     }
   }
   __syncthreads();
+  dbg_stamp(D, 35);
   if (S.full && t == 0) st->kp_valid = 0;
 }
 
