@@ -109,6 +109,8 @@ struct State {
   int32_t tail_par;    // launch parity after the last k_tail
   int32_t pad5;
   int64_t mid_nm[2], mid_nh[2];  // mid.h: merged occurrences / new pairs of k_mid_find, by launch parity
+  int32_t place_par_prev;        // mid.h: parity of the merge whose new pairs the next find appends (-1: none)
+  int32_t pad6;
 };
 
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
@@ -119,7 +121,7 @@ struct Sel {
   int32_t skip;       // SKIP_* bits of a rebuild iteration
   int32_t rebuild;    // merge: k_find rebuilds the posting index first (rank-local; the iteration still merges)
   int32_t wown;       // merge: the owner whose posting log holds the winner's new pairs
-  int32_t pad2[2];
+  int32_t kpn, kpoff; // merge: the winner's per-key posting list (tail.h / mid.h), when built
   int32_t theta_new;  // hot-list rebuild threshold
   int32_t build;      // hot-list counter the rebuild fills
   int32_t W, nid, iter, tag;
@@ -247,7 +249,7 @@ struct Dev {
   int32_t *kp_off, *kp_n, *kp_cap, *kpool;
   int64_t KPOOL;
   int4* TM;       // merged occurrences {a, ya, b, c}
-  int2* TH;       // new pairs {slot, key}
+  int2* TH;       // new pairs {slot, key} (mid.h: two buffers of THcap, by launch parity)
   int4* TS;       // posting entries past a list's capacity {key, position, slot}
   int32_t* TR;    // keys whose list is regrown
   NewPair* TK;    // keys found (not claimed): EHASH check

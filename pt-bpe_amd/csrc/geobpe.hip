@@ -202,10 +202,13 @@ void flush_place(geobpe_ctx* c) {
   if (!c->place_pending) return;
   c->place_pending = false;
   Timed t(c, "place");
-  if (c->place_mid)
+  if (c->place_mid) {  // token rewrites, then the posting entries, then nothing is pending
     hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, c->D, INT32_MIN);
-  else
+    hipLaunchKernelGGL(k_mid_find, dim3(MID_APP), dim3(ABLOCK), 0, c->stream, c->D, (int)(c->gen & 1), 0, 0);
+    hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, c->D);
+  } else {
     hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D);
+  }
 }
 
 int sync_state(geobpe_ctx* c) {
@@ -334,8 +337,9 @@ void enqueue_iteration_mid(geobpe_ctx* c) {
     hipLaunchKernelGGL(k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->stream, c->D, par);
   }
   {
-    Timed t(c, "find");
-    hipLaunchKernelGGL(k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, par);
+    Timed t(c, "find");  // (+ the previous merge's posting entries in MID_APP more workgroups)
+    const int G = c->nba - MID_APP;
+    hipLaunchKernelGGL(k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, par, G, 1);
   }
   c->place_pending = true;
   c->place_mid = true;
@@ -371,7 +375,7 @@ int tail_alloc(geobpe_ctx* c) {
   int rc;
   // (zero: a key claimed after the list build starts with an empty list of capacity 0)
   if ((rc = dalloc(c, &D.kp_off, D.HC, 0)) || (rc = dalloc(c, &D.kp_n, D.HC, 0)) || (rc = dalloc(c, &D.kp_cap, D.HC, 0)) ||
-      (rc = dalloc(c, &D.kpool, D.KPOOL)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, D.THcap)) ||
+      (rc = dalloc(c, &D.kpool, D.KPOOL)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, 2 * D.THcap)) ||
       (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)))
     return rc;
   c->tail_ready = true;
@@ -386,6 +390,7 @@ void tail_build(geobpe_ctx* c) {
   hipLaunchKernelGGL(k_kp_count, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
   hipLaunchKernelGGL(k_kp_alloc, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
   hipLaunchKernelGGL(k_kp_fill, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, c->D);  // (nothing pending)
 }
 
 // up to n merges in k_tail (one workgroup, one launch for many merges); a hot-list rebuild

@@ -293,13 +293,13 @@ __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, cons
 // counter `build` (zeroed by k_mark) and clist = every key with count >= th.
 // Two coalesced passes over this workgroup's share of klist; one global
 // reservation per workgroup.
-__device__ void rebuild_hot_list(const Dev& D, int32_t th, int32_t build) {
+__device__ void rebuild_hot_list(const Dev& D, int32_t th, int32_t build, int32_t blk, int32_t nblk) {
   __shared__ int32_t s_red[ABLOCK / 64];
   __shared__ int64_t s_base;
   State* st = D.st;
   const int64_t U = min(st->U, D.KCAP);
-  const int64_t per = (U + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
+  const int64_t per = (U + nblk - 1) / nblk;
+  const int64_t lo = (int64_t)blk * per, hi = min(U, lo + per);
   constexpr int UNR = 16;  // loads in flight per thread
   int32_t n = 0;
   for (int64_t i = lo + threadIdx.x; i < hi; i += UNR * ABLOCK) {
@@ -323,21 +323,24 @@ __device__ void rebuild_hot_list(const Dev& D, int32_t th, int32_t build) {
     for (int u = 0; u < UNR; u++)
       if (d[u] >= 0 && D.count[d[u]] >= th) D.clist[j++] = d[u];  // j < U <= KCAP
   }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (blk == 0 && threadIdx.x == 0) {
     st->cl_act = build;
     st->theta = th;
     st->cl_valid = 1;
     st->cl_measured = 0;
   }
 }
+__device__ inline void rebuild_hot_list(const Dev& D, int32_t th, int32_t build) {
+  rebuild_hot_list(D, th, build, blockIdx.x, gridDim.x);
+}
 
 // a measure iteration: the global maximum count (the hot list must be rebuilt
 // from scratch and its threshold needs it)
-__device__ void measure_max(const Dev& D) {
+__device__ void measure_max(const Dev& D, int32_t blk, int32_t nblk) {
   __shared__ int32_t s_red[ABLOCK / 64];
   const int64_t U = min(D.st->U, D.KCAP);
-  const int64_t per = (U + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
+  const int64_t per = (U + nblk - 1) / nblk;
+  const int64_t lo = (int64_t)blk * per, hi = min(U, lo + per);
   constexpr int UNR = 16;
   int32_t m = 0;
   for (int64_t i = lo + threadIdx.x; i < hi; i += UNR * ABLOCK) {
@@ -351,6 +354,7 @@ __device__ void measure_max(const Dev& D) {
   m = block_max(m, s_red);
   if (threadIdx.x == 0 && m > 0) atomicMax((unsigned long long*)&D.st->cl_measured, (unsigned long long)m);
 }
+__device__ inline void measure_max(const Dev& D) { measure_max(D, blockIdx.x, gridDim.x); }
 
 __global__ __launch_bounds__(ABLOCK) void k_finalize(Dev D, int to_delta) {
   __shared__ AggBig agg;
@@ -887,6 +891,10 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
     o.w2 = w2;
     o.wl = wl;
     o.wfp = key_fp(W);
+    if (D.kp_n) {  // the winner's posting list (per-key lists: tail.h / mid.h)
+      o.kpn = ldc<COH>(&D.kp_n[W]);
+      o.kpoff = D.kp_off[W];
+    }
     o.widL = L;
     o.wg = g;
     o.widR = Rr;

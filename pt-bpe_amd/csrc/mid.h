@@ -1,37 +1,53 @@
 // mid.h -- the middle regime of BPE.step (foldingdiff/bpe.py:1792-2166): merges of up to
-// a few ten thousand occurrences, on the per-key posting lists of tail.h.  Included once,
-// by kernels.h, after tail.h.
+// a few thousand occurrences, on the per-key posting lists of tail.h.  Included once, by
+// kernels.h, after tail.h.
 //
-// Two launches per merge:
-//   k_mid_sel   workgroup 0: select_core (argmax + reference tie-break); workgroups 1..G:
-//               the previous merge's place -- token rewrites, pk of the new pairs, and the
-//               new pairs' posting entries, each place workgroup owning the keys of one
-//               hash bucket (it groups its keys' new pairs in LDS and appends them, growing
-//               a list where needed: no other workgroup touches those lists, so no
-//               cross-workgroup allocation protocol)
-//   k_mid_find  G workgroups: the winner's list split over them, the greedy run walks of
-//               k_find, the new pairs' keys deduplicated per round in LDS and resolved once
-//               per (workgroup, key): find-or-claim, +n on the count (hot-list crossing);
-//               -1 on the destroyed pairs (LDS-aggregated); merged occurrences and new pairs
-//               to two global lists for the place
-// Compared with the full-grid find/commit/place (merge.h) there is no owner hand-off
-// (key records, decrement records, posting logs): the per-key lists make the candidates
-// exact and a late merge's keys are few per workgroup.
+// Two launches per merge t:
+//   k_mid_sel   workgroup 0: select_core (argmax + reference tie-break), which also hands
+//               the winner's list bounds to the find; workgroups 1..P: merge t-1's token
+//               rewrites and pk of its new pairs, and the EHASH check of the keys its find
+//               found (the select is the longer of the two)
+//   k_mid_find  workgroups 0..G-1: find + commit of merge t -- the winner's candidates are
+//               its posting list plus merge t-1's new pairs of its key, split over the
+//               workgroups; the greedy run walks of k_find; the new pairs' keys deduplicated
+//               per round in LDS and resolved once per (workgroup, key): find-or-claim,
+//               +n on the count (hot-list crossing); -1 on the destroyed pairs
+//               (LDS-aggregated); merged occurrences and new pairs to global lists.
+//               Workgroups G..G+A-1: merge t-1's posting entries, each owning the keys of
+//               one hash bucket (no cross-workgroup allocation: a full list grows 2x by its
+//               owner).  The winner's own key is skipped: its pairs are being merged now
+//               (all of them: its count drops to 0), which is why the find reads them from
+//               the new-pair list instead.
+// So the list appends run beside the find, off the path from one merge to the next.
+// Compared with the full-grid find/commit/place (merge.h) there is no owner hand-off (key
+// records, decrement records, posting logs): the per-key lists make the candidates exact
+// and a late merge's keys are few per workgroup.
 #pragma once
 // (included inside namespace gb)
 
-constexpr int MKC = 1024;  // k_mid_find: new-key dedupe slots per round (LDS)
-constexpr int MPK = 2048;  // k_mid_sel place: key grouping slots per round (LDS)
+constexpr int MKC = 1024;   // k_mid_find: new-key dedupe slots per round (LDS)
+constexpr int MPK = 2048;   // appends: key grouping slots (LDS)
+constexpr int MID_APP = 32; // appending workgroups of k_mid_find (hash buckets of the keys)
+
+__device__ inline int2* mid_th(const Dev& D, int par) { return D.TH + (int64_t)par * D.THcap; }
 
 struct MidFindLds {
   u64 key[MKC], h1[MKC], h2[MKC];
   int4 rep[MKC];  // {len, idL, g, idR}
   int32_t cnt[MKC], did[MKC];
   int32_t occ[MKC];  // occupied slots, in insertion order
-  AggT<12> agg;      // count decrements
+  AggT<11> agg;      // count decrements
   HotApp hot;
   int32_t red[ABLOCK / 64];
-  int32_t nocc, nm, chk, ns;
+  int32_t nocc, nm, chk;
+};
+
+struct MidAppLds {
+  int32_t key[MPK], cnt[MPK], base[MPK], cur[MPK];
+  int32_t occ[MPK];
+  int32_t big_old[TAIL_BIG], big_new[TAIL_BIG], big_pre[TAIL_BIG + 1];
+  int32_t red[ABLOCK / 64];
+  int32_t nocc, nbig, full;
 };
 
 // ---------------------------------------------------------------------- find
@@ -58,16 +74,28 @@ __device__ inline void mid_occ(const Dev& D, MidFindLds& S, const MidCtx& F, int
 __device__ inline void mid_pair(const Dev& D, const MidCtx& F, int32_t target, int32_t d) {
   const int64_t j = wave_reserve64((unsigned long long*)&D.st->mid_nh[F.par]);
   if (j < D.THcap)
-    D.TH[j] = make_int2(target, d);
+    mid_th(D, F.par)[j] = make_int2(target, d);
   else
     set_error(D, GEOBPE_ECAPACITY, -71);
+}
+
+// find-or-claim with the CAS as the first probe (an empty first slot is claimed, the key
+// itself is found, anything else probes on)
+__device__ inline int32_t mid_resolve(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
+  const u64 k = probe_key(h1, h2, len);
+  const u64 s0 = ht_first_slot(D, k);
+  const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s0], 0ULL, (unsigned long long)k);
+  *claimed = old == 0;
+  if (old == 0 || old == k) return (int32_t)s0;
+  const u64 s1 = (s0 + 1) & ((u64)D.HC - 1);
+  return ht_resolve(D, k, s1, ht_probe(D, s1), claimed);
 }
 
 // a new pair resolved on its own (a run's later occurrence, or the round's table is full)
 __device__ void mid_single(const Dev& D, MidFindLds& S, const MidCtx& F, u64 h1, u64 h2, int32_t len, int32_t idL,
                            int32_t g, int32_t idR, int32_t target) {
   bool claimed;
-  const int32_t d = ht_insert(D, h1, h2, len, &claimed);
+  const int32_t d = mid_resolve(D, h1, h2, len, &claimed);
   if (d < 0) return;
   if (claimed) {
     claim_payload(D, d, h1, h2, len, idL, g, idR);
@@ -201,20 +229,12 @@ __device__ inline int32_t mkc_slot(MidFindLds& S, const MidHalf& h, bool* ins) {
   return -1;
 }
 
-__global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
-  __shared__ MidFindLds S;
+// find workgroup w of G (merge parity par, decision sel)
+__device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, int32_t G, MidFindLds& S) {
   State* st = D.st;
-  const int32_t w = blockIdx.x, G = gridDim.x, t = threadIdx.x;
+  const int32_t t = threadIdx.x;
   dbg_stamp(D, 10);
-  Sel sel = D.sel[par];
-  // lists that lost entries (a place ran out of table or pool space in the launch that
-  // selected this merge): no merge until the host rebuilds them -- the select wrote only
-  // what the next select overwrites (Sel, the log entry, the new token's hashes)
-  if (!st->kp_valid) sel.decision = SEL_STALL;
-  check_found(D, w);  // keys the previous merge found in this region (EHASH)
   if (w == 0 && t == 0) {
-    st->mid_nm[par ^ 1] = 0;  // the next merge's lists (the place of the last one has run)
-    st->mid_nh[par ^ 1] = 0;
     st->place_par = sel.decision == SEL_MERGE ? par : -1;
     if (sel.decision == SEL_DONE) {
       st->done = 1;
@@ -226,8 +246,8 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
   if (sel.decision == SEL_DONE || sel.decision == SEL_STALL) return;
   if (sel.decision == SEL_SKIP) {
     if (t == 0) D.chkcnt[w] = 0;
-    if (sel.skip & SKIP_MEASURE) measure_max(D);
-    if (sel.skip & SKIP_HOT) rebuild_hot_list(D, sel.theta_new, sel.build);
+    if (sel.skip & SKIP_MEASURE) measure_max(D, w, G);
+    if (sel.skip & SKIP_HOT) rebuild_hot_list(D, sel.theta_new, sel.build, w, G);
     return;
   }
   MidCtx F;
@@ -246,7 +266,13 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
     F.pa2 = D.pw2[nw + 1];
     F.pb2 = D.pw2[nw];
   }
-  if (w == 0) {  // _tokens[n] = json.loads(key); merge log; state the next select reads
+  // candidates: the winner's list, then the previous merge's new pairs (those of key W)
+  const int32_t nW = sel.kpn;
+  const int64_t offW = sel.kpoff;
+  const int2* thp = mid_th(D, par ^ 1);
+  const int64_t nP = st->place_par_prev == (par ^ 1) ? min(st->mid_nh[par ^ 1], D.THcap) : 0;
+  const int64_t ntot = nW + nP;
+  if (w == 0) {  // _tokens[n] = json.loads(key); state the next select reads
     const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
     const int64_t vL = D.voff[L], vR = D.voff[Rr];
     const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
@@ -269,7 +295,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
     S.key[i] = 0;
     S.cnt[i] = 0;
   }
-  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+  for (int i = t; i < AggT<11>::N; i += ABLOCK) {
     S.agg.key[i] = -1;
     S.agg.val[i] = 0;
   }
@@ -279,14 +305,21 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
   }
   __syncthreads();
   dbg_stamp(D, 11);
-  const int32_t nW = D.kp_n[F.W];
-  const int64_t offW = D.kp_off[F.W];
-  const int32_t lo = (int32_t)((int64_t)nW * w / G), hi = (int32_t)((int64_t)nW * (w + 1) / G);
-  for (int32_t c0 = lo; c0 < hi; c0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
-    const int32_t i = c0 + t;
+  const int64_t lo = ntot * w / G, hi = ntot * (w + 1) / G;
+  for (int64_t c0 = lo; c0 < hi; c0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
+    const int64_t i = c0 + t;
     MidHalf hl, hr;
     bool vl = false, vr = false;
-    if (i < hi) mid_walk(D, S, F, D.kpool[offW + i], hl, vl, hr, vr);
+    if (i < hi) {
+      int32_t g = -1;
+      if (i < nW) {
+        g = D.kpool[offW + i];
+      } else {
+        const int2 e = thp[i - nW];
+        if (e.y == F.W) g = e.x;
+      }
+      if (g >= 0) mid_walk(D, S, F, g, hl, vl, hr, vr);
+    }
     if (c0 == lo) dbg_stamp(D, 15);
     // ---- this round's new keys: LDS dedupe, then one resolve + count update per key
     bool il = false, ir = false;
@@ -321,7 +354,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
       const int4 rp = S.rep[s];
       bool claimed;
       const u64 h1 = S.h1[s], h2 = S.h2[s];
-      const int32_t d = ht_insert(D, h1, h2, rp.x, &claimed);
+      const int32_t d = mid_resolve(D, h1, h2, rp.x, &claimed);
       S.did[s] = d;
       if (d < 0) continue;
       if (claimed) {
@@ -354,7 +387,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
   }
   dbg_stamp(D, 12);
   // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
-  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+  for (int i = t; i < AggT<11>::N; i += ABLOCK) {
     const int32_t k = S.agg.key[i], v = S.agg.val[i];
     if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
   }
@@ -367,21 +400,13 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par) {
   dbg_stamp(D, 13);
 }
 
-// ---------------------------------------------------------------------- place
-struct MidPlaceLds {
-  int32_t key[MPK], cnt[MPK], base[MPK], cur[MPK];
-  int32_t occ[MPK];
-  int32_t big_old[TAIL_BIG], big_new[TAIL_BIG], big_pre[TAIL_BIG + 1];
-  int32_t red[ABLOCK / 64];
-  int32_t nocc, nbig, full;
-};
-
-__device__ inline uint32_t mid_bucket(int32_t d, int32_t G) {
-  return (uint32_t)(((u64)((uint32_t)d * 2654435761u) * (u64)G) >> 32);
+// ---------------------------------------------------------------------- appends
+__device__ inline uint32_t mid_bucket(int32_t d, int32_t A) {
+  return (uint32_t)(((u64)((uint32_t)d * 2654435761u) * (u64)A) >> 32);
 }
 
-// the key's slot in the place table (insert: claim an empty one); -1: not there / full
-__device__ inline int32_t mpk_slot(MidPlaceLds& S, int32_t d, bool insert, bool* ins) {
+// the key's slot in the append table (insert: claim an empty one); -1: not there / full
+__device__ inline int32_t mpk_slot(MidAppLds& S, int32_t d, bool insert, bool* ins) {
   int32_t s = (int32_t)(((uint32_t)d * 0x85EBCA6Bu) >> (32 - 11)) & (MPK - 1);
   *ins = false;
 #pragma unroll 1
@@ -402,47 +427,29 @@ __device__ inline int32_t mpk_slot(MidPlaceLds& S, int32_t d, bool insert, bool*
 
 constexpr int MP_UNR = 8;  // new-pair list entries in flight per thread
 
-// place workgroup b of G: token rewrites and pk of its share of the merged occurrences and
-// new pairs, then the posting entries of the new pairs whose key is in bucket b -- one pass
-// counts them per key, the lists grow where needed, a second pass writes the entries
-__device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& S) {
+// appending workgroup b of A: the posting entries of the new pairs in th[0..nh) whose key is
+// in bucket b, except key `skip` -- one pass counts them per key, the lists grow where
+// needed, a second pass writes the entries
+__device__ void mid_append_body(const Dev& D, const int2* th, int64_t nh, int32_t skip, int32_t b, int32_t A,
+                                MidAppLds& S) {
   State* st = D.st;
-  const int32_t par = st->place_par;
-  if (par < 0) return;
-  const Sel sel = D.sel[par];
-  if (sel.decision != SEL_MERGE) return;
   const int32_t t = threadIdx.x;
   dbg_stamp(D, 30);
-  const int64_t nm = min(st->mid_nm[par], D.TMcap), nh = min(st->mid_nh[par], D.THcap);
   for (int i = t; i < MPK; i += ABLOCK) {
     S.key[i] = -1;
     S.cnt[i] = 0;
     S.cur[i] = 0;
   }
   if (t == 0) S.nocc = S.nbig = S.full = 0;
-  for (int64_t i = nm * b / G + t; i < nm * (b + 1) / G; i += ABLOCK) {
-    const int4 e = D.TM[i];
-    *reinterpret_cast<int2*>(D.tok + e.x) = make_int2(sel.nid, e.y);
-    D.tok[e.z] = make_int4(-1, 0, -1, -1);
-    if (e.w >= 0)
-      *tok_f(D, e.w, 2) = e.x;
-    else
-      *tok_f(D, e.x, 3) = -1;
-  }
-  for (int64_t i = nh * b / G + t; i < nh * (b + 1) / G; i += ABLOCK) {
-    const int2 h = D.TH[i];
-    *tok_f(D, h.x, 3) = h.y;
-  }
   __syncthreads();
-  dbg_stamp(D, 31);
   // ---- pass 1: new entries per key of bucket b
   for (int64_t i0 = t; i0 < nh; i0 += MP_UNR * ABLOCK) {
     int32_t d[MP_UNR];
 #pragma unroll
-    for (int u = 0; u < MP_UNR; u++) d[u] = i0 + u * ABLOCK < nh ? D.TH[i0 + u * ABLOCK].y : -1;
+    for (int u = 0; u < MP_UNR; u++) d[u] = i0 + u * ABLOCK < nh ? th[i0 + u * ABLOCK].y : -1;
 #pragma unroll
     for (int u = 0; u < MP_UNR; u++) {
-      if (d[u] < 0 || mid_bucket(d[u], G) != (uint32_t)b) continue;
+      if (d[u] < 0 || d[u] == skip || mid_bucket(d[u], A) != (uint32_t)b) continue;
       bool ins;
       const int32_t s = mpk_slot(S, d[u], true, &ins);
       if (s < 0) {
@@ -507,10 +514,10 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& 
   for (int64_t i0 = t; i0 < nh; i0 += MP_UNR * ABLOCK) {
     int2 h[MP_UNR];
 #pragma unroll
-    for (int u = 0; u < MP_UNR; u++) h[u] = i0 + u * ABLOCK < nh ? D.TH[i0 + u * ABLOCK] : make_int2(-1, -1);
+    for (int u = 0; u < MP_UNR; u++) h[u] = i0 + u * ABLOCK < nh ? th[i0 + u * ABLOCK] : make_int2(-1, -1);
 #pragma unroll
     for (int u = 0; u < MP_UNR; u++) {
-      if (h[u].y < 0 || mid_bucket(h[u].y, G) != (uint32_t)b) continue;
+      if (h[u].y < 0 || h[u].y == skip || mid_bucket(h[u].y, A) != (uint32_t)b) continue;
       bool ins;
       const int32_t s = mpk_slot(S, h[u].y, false, &ins);
       if (s < 0) continue;
@@ -523,18 +530,83 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t G, MidPlaceLds& 
   if (S.full && t == 0) st->kp_valid = 0;
 }
 
-// workgroup 0: select (par >= 0; INT32_MIN: place only); workgroups 1..G: the place of the
-// merge st->place_par
-__global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par) {
-  if (blockIdx.x > 0) {
-    __shared__ MidPlaceLds P;
-    mid_place_body(D, blockIdx.x - 1, gridDim.x - 1, P);
+// workgroups 0..G-1: the find of merge `par` (find = 0: none, a flush); workgroups G..:
+// the posting entries of the previous merge (st->place_par_prev), skipping this merge's winner
+__global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int find) {
+  __shared__ union {
+    MidFindLds f;
+    MidAppLds a;
+  } U;
+  State* st = D.st;
+  Sel sel = D.sel[par];
+  // lists that lost entries (an append ran out of table or pool space): no merge until the
+  // host rebuilds them -- the select wrote only what the next select overwrites (Sel, the
+  // log entry, the new token's hashes)
+  const bool valid = st->kp_valid != 0;
+  if (!find || !valid) sel.decision = SEL_STALL;
+  if ((int)blockIdx.x < G) {
+    mid_find_body(D, sel, par, blockIdx.x, G, U.f);
     return;
   }
-  if (par == INT32_MIN) return;
+  if (st->place_par_prev != (par ^ 1) || !valid) return;
+  const int64_t nh = min(st->mid_nh[par ^ 1], D.THcap);
+  const int32_t skip = sel.decision == SEL_MERGE ? sel.W : -1;
+  mid_append_body(D, mid_th(D, par ^ 1), nh, skip, blockIdx.x - G, gridDim.x - G, U.a);
+}
+
+// ---------------------------------------------------------------------- select + place
+// token rewrites and pk of merge st->place_par, share b of P; the EHASH check of the keys
+// find workgroup b found
+__device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
+  State* st = D.st;
+  const int32_t t = threadIdx.x;
+  dbg_stamp(D, 36);
+  if (b < D.NBA) {  // (then consumed: the next find writes region b afresh)
+    check_found(D, b);
+    __syncthreads();
+    if (t == 0) D.chkcnt[b] = 0;
+  }
+  const int32_t par = st->place_par;
+  if (par < 0) return;
+  const Sel sel = D.sel[par];
+  if (sel.decision != SEL_MERGE) return;
+  const int64_t nm = min(st->mid_nm[par], D.TMcap), nh = min(st->mid_nh[par], D.THcap);
+  const int2* th = mid_th(D, par);
+  for (int64_t i = nm * b / P + t; i < nm * (b + 1) / P; i += ABLOCK) {
+    const int4 e = D.TM[i];
+    *reinterpret_cast<int2*>(D.tok + e.x) = make_int2(sel.nid, e.y);
+    D.tok[e.z] = make_int4(-1, 0, -1, -1);
+    if (e.w >= 0)
+      *tok_f(D, e.w, 2) = e.x;
+    else
+      *tok_f(D, e.x, 3) = -1;
+  }
+  for (int64_t i = nh * b / P + t; i < nh * (b + 1) / P; i += ABLOCK) {
+    const int2 h = th[i];
+    *tok_f(D, h.x, 3) = h.y;
+  }
+  dbg_stamp(D, 37);
+}
+
+// workgroup 0: select (par >= 0; INT32_MIN: place only); workgroups 1..P: the token
+// rewrites of merge st->place_par.  Workgroup 0 records which merge's new pairs the next
+// find's appends take (place_par_prev) and resets its parity's list cursors (nothing else
+// in this launch reads them).
+__global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par) {
+  if (blockIdx.x > 0) {
+    mid_place_body(D, blockIdx.x - 1, gridDim.x - 1);
+    return;
+  }
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
-  if (!D.st->kp_valid) {  // the lists lost entries: no merge until the host rebuilds them
+  State* st = D.st;
+  if (threadIdx.x == 0) st->place_par_prev = st->place_par;
+  if (par == INT32_MIN) return;
+  if (threadIdx.x == 0) {
+    st->mid_nm[par] = 0;
+    st->mid_nh[par] = 0;
+  }
+  if (!st->kp_valid) {  // the lists lost entries: no merge until the host rebuilds them
     if (threadIdx.x == 0) {
       Sel o{};
       o.decision = SEL_STALL;
@@ -543,4 +615,14 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par) {
     return;
   }
   select_core<false>(D, par, S, s_red, nullptr);
+}
+
+// after a flush (k_mid_sel place-only + k_mid_find appends-only): nothing is pending
+__global__ void k_mid_flushed(Dev D) {
+  if (threadIdx.x == 0) {
+    D.st->place_par = -1;
+    D.st->place_par_prev = -1;
+    D.st->mid_nh[0] = D.st->mid_nh[1] = 0;
+    D.st->mid_nm[0] = D.st->mid_nm[1] = 0;
+  }
 }

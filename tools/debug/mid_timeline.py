@@ -20,7 +20,7 @@ eng = GeoBPEEngine(corpus, 5, mid=mid, tail=0).initialize()
 eng.bin()
 L = _native.lib()
 names = {10: "F.start", 11: "F.setup", 15: "F.walked", 16: "F.deduped", 17: "F.resolved", 12: "F.rounds", 13: "F.end",
-         30: "P.start", 31: "P.tokens", 32: "P.counted", 33: "P.grown", 35: "P.end",
+         30: "A.start", 32: "A.counted", 33: "A.grown", 35: "A.end", 36: "P.start", 37: "P.end",
          20: "S.start", 21: "S.scanned", 22: "S.max", 23: "S.ties", 24: "S.staged", 25: "S.tourn", 26: "S.end"}
 done = 0
 for it in iters:
