@@ -100,7 +100,7 @@ int geobpe_step(geobpe_ctx *ctx, int32_t *new_id, int32_t *count, int64_t *n_mer
 int geobpe_run(geobpe_ctx *ctx, int64_t n_iters, int64_t *n_done);
 /* Late-merge path (same results): once a merge's count is <= max_count, geobpe_run /
  * geobpe_step run the merges in one workgroup over per-key posting lists (k_tail, many
- * merges per launch) instead of the full-grid kernels; 0 = never (default 256;
+ * merges per launch) instead of the full-grid kernels; 0 = never (the default: the middle regime is faster;
  * environment GEOBPE_TAIL overrides at create).  Single rank, no merge replay. */
 int geobpe_set_tail(geobpe_ctx *ctx, int64_t max_count);
 /* Middle regime (same results): once a merge's count is <= max_count, merges run as two

@@ -76,7 +76,7 @@ struct geobpe_ctx {
   bool pipelined = false;     // between geobpe_pipeline_begin and _end (device-side parity)
   int nba = 256;  // find / commit / finalize / bin / import workgroups (= D.NBA, <= NBA_MAX)
   // late-merge path (tail.h): merges whose count is <= tail_thresh run in k_tail
-  int64_t tail_thresh = 256;   // 0: never
+  int64_t tail_thresh = 0;     // 0: never (the mid path is faster at every count measured on C3)
   bool tail_on = false;        // switched (one way: the full-grid kernels' posting index goes stale)
   bool tail_ready = false;     // its arrays are allocated
   int64_t hold_us = 0;         // geobpe_set_hold: a k_hold launch before each batch of iterations
