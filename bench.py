@@ -47,6 +47,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 FIND_BYTES_PER_OCC = 128   # k_find per merged occurrence: posting entry 8, token records of p, g, b, c 64,
                            # vocab hashes of p and c 32, merge entry 16, two occurrence slots (T) 8
 PLACE_BYTES_PER_OCC = 76   # k_place: merge entry 16, T 8, token rewrites 28, two pk 8, two log entries 16
+MIDFIND_BYTES_PER_OCC = 132  # k_mid_find: list entry 4, token records of g, p, b, c 64, vocab hashes of p and c
+                             # 32, merge entry 16, two new-pair entries 16
+MIDSEL_BYTES_PER_OCC = 76    # k_mid_sel's token rewrites: merge entry 16, records of a, b, c 28, two new-pair
+                             # entries 16, two pk 8, (+ the appends beside the next find: two entries 8)
 COMMIT_KREC_BYTES = 56     # k_commit per key record: 48 read + (id, log position) 8 written
 COMMIT_DREC_BYTES = 8      # per decrement record
 COMMIT_KEY_BYTES = 44      # per key: table slot 8 (CAS), count 4, payload (h1, h2, len, representative) 32
@@ -183,7 +187,7 @@ def main():
     eng.run(args.warmup)
     # ---- timed region: exactly K merges; HIP events around the merge-loop launches
     # (k_select carries the previous merge's k_place), on the engine's stream
-    eng.set_profiling(not args.no_profile, only="select,find,commit", stride=args.event_stride)
+    eng.set_profiling(not args.no_profile, only="select,find,commit,mid_sel,mid_find", stride=args.event_stride)
     st0 = eng.state()
     eng.marker(1)  # window bracket for rocprofv3 (outside the timer)
     if world > 1:
@@ -201,7 +205,8 @@ def main():
         tt = torch.tensor([T], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         T = float(tt.item())
-    ktimes = {k: (eng.kernel_ms(k) if not args.no_profile else (0.0, 0)) for k in ("select", "find", "commit")}
+    KNAMES = ("select", "find", "commit", "mid_sel", "mid_find")
+    ktimes = {k: (eng.kernel_ms(k) if not args.no_profile else (0.0, 0)) for k in KNAMES}
     merges_log = list(eng.merges)
     R_local = int(shard["row_off"][-1])
     n_ranks = dist.get_world_size() if dist.is_initialized() else 1
@@ -228,7 +233,7 @@ def main():
             rep.initialize()
             rep.bin()
             rep.run(args.warmup)
-            names = "commit" if instrumented else "select,find,commit,tail,tail_build"
+            names = "commit" if instrumented else "select,find,commit,mid_sel,mid_find,tail,tail_build"
             rep.set_profiling(True, only=names)  # (every launch)
             rep.set_work_counters(instrumented)
             rep.set_hold(3000 + 60 * min(done, 64))  # (the launches queue behind a spin: no host gaps)
@@ -239,7 +244,7 @@ def main():
                 commit_work = {k: rs1[k] - rs0[k] for k in ("commit_key_records", "commit_decrement_records",
                                                             "commit_keys")}
             else:
-                for k in ("select", "find", "commit", "tail", "tail_build"):
+                for k in KNAMES + ("tail", "tail_build"):
                     ms, nl = rep.kernel_ms(k)
                     if nl:
                         kern["select+place" if k == "select" else k] = {
@@ -251,16 +256,32 @@ def main():
     # ---- roofline of the loop's kernels, from the live events of the timed region
     wkey = f"config={args.config},warmup={args.warmup},steps={args.steps},n={world}"
     window = merges_log[-done:] if done else []
-    n_merged = sum(m[2] for m in window)
+    # the window's merges: the full-grid kernels ran the first n_full, the middle regime
+    # (mid.h) the rest (the switch is one way); launch counts from the replay when it ran
+    def _launches(k):
+        kk = "select+place" if k == "select" else k
+        return kern[kk]["launches"] if kk in kern else ktimes[k][1] * args.event_stride
+    has_mid = bool(ktimes["mid_find"][1] or "mid_find" in kern)
+    n_full = min(len(window), _launches("find")) if has_mid else len(window)
+    w_full, w_mid = window[:n_full], window[n_full:]
+    n_merged = sum(m[2] for m in w_full)
+    mid_occ = sum(m[2] for m in w_mid)
     # the select launch of merge t places merge t - 1
-    placed = sum(m[2] for m in merges_log[-done - 1:-1]) if done and len(merges_log) > done else n_merged
-    per = lambda x: x / max(done, 1)  # noqa: E731
+    prev = merges_log[-done - 1:-1] if done and len(merges_log) > done else window
+    placed = sum(m[2] for m in prev[:n_full])
+    per = lambda x: x / max(len(w_full), 1)  # noqa: E731
+    per_mid = lambda x: x / max(len(w_mid), 1)  # noqa: E731
     work = {"find": (FIND_BYTES_PER_OCC * per(n_merged),
                      f"{FIND_BYTES_PER_OCC} B x merged occurrences (avg {per(n_merged):.0f} per launch)"),
             "select": (PLACE_BYTES_PER_OCC * per(placed),
                        f"k_place's {PLACE_BYTES_PER_OCC} B x merged occurrences of the previous merge (avg "
                        f"{per(placed):.0f} per launch); the one-workgroup k_select beside it is not counted"),
-            "commit": (None, "k_commit work counters come from the instrumented replay (--no-replay: unknown)")}
+            "commit": (None, "k_commit work counters come from the instrumented replay (--no-replay: unknown)"),
+            "mid_find": (MIDFIND_BYTES_PER_OCC * per_mid(mid_occ),
+                         f"{MIDFIND_BYTES_PER_OCC} B x merged occurrences (avg {per_mid(mid_occ):.0f} per launch)"),
+            "mid_sel": (MIDSEL_BYTES_PER_OCC * per_mid(mid_occ),
+                        f"{MIDSEL_BYTES_PER_OCC} B x merged occurrences of the previous merge (avg "
+                        f"{per_mid(mid_occ):.0f} per launch); the one-workgroup select beside it is not counted")}
     if commit_work:
         cw = {k: per(v) for k, v in commit_work.items()}
         work["commit"] = (COMMIT_KREC_BYTES * cw["commit_key_records"] + COMMIT_DREC_BYTES * cw["commit_decrement_records"]
@@ -277,7 +298,7 @@ def main():
         bpl, note = work[k]
         ach = bpl / avg_s / 1e9 if bpl is not None else None
         traffic, tsrc = pmc_traffic(k, wkey)  # (k_select's dispatches carry k_place)
-        roofs[k] = {"kernel": "k_select+k_place" if k == "select" else f"k_{k}", "bound": "hbm", "achieved": round(ach, 2) if ach else None,
+        roofs[k] = {"kernel": {"select": "k_select+k_place", "mid_sel": "k_mid_sel"}.get(k, f"k_{k}"), "bound": "hbm", "achieved": round(ach, 2) if ach else None,
                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
                     "traffic": traffic, "traffic_source": tsrc, "traffic_window": wkey,
                     "bytes_per_launch": round(bpl, 1) if bpl is not None else None, "avg_launch_us": round(avg_s * 1e6, 3),

@@ -330,14 +330,14 @@ void enqueue_iteration(geobpe_ctx* c) {
 void enqueue_iteration_mid(geobpe_ctx* c) {
   const int par = (int)(c->gen & 1);
   {
-    Timed t(c, "select");  // (+ the previous merge's place in workgroups 1..nba)
+    Timed t(c, "mid_sel");  // (+ the previous merge's token rewrites in workgroups 1..nba)
     const bool carry = c->place_pending && c->place_mid;
     if (c->place_pending && !c->place_mid) flush_place(c);
     c->place_pending = false;
     hipLaunchKernelGGL(k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->stream, c->D, par);
   }
   {
-    Timed t(c, "find");  // (+ the previous merge's posting entries in MID_APP more workgroups)
+    Timed t(c, "mid_find");  // (+ the previous merge's posting entries in MID_APP more workgroups)
     const int G = c->nba - MID_APP;
     hipLaunchKernelGGL(k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, par, G, 1);
   }
