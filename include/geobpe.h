@@ -284,6 +284,27 @@ int64_t geobpe_events(geobpe_ctx *ctx, int32_t *h_merge, int32_t *h_a, int32_t *
 
 int geobpe_synchronize(geobpe_ctx *ctx);
 
+/* ---- the engine's own multi-rank exchange (replaces the host-driven collectives of
+ * geobpe/dist.py TorchGroup.run_pipelined; the reference has no multi-GPU path) ----
+ * An RCCL communicator owned by the engine: rank 0 makes the 128-byte id, the caller
+ * broadcasts it, every rank attaches.  rccl_path: the RCCL library the process already
+ * uses (PyTorch's), NULL = "librccl.so.1". */
+int geobpe_comm_unique_id(const char *rccl_path, void *out128);
+int geobpe_comm_init_rccl(geobpe_ctx *ctx, const char *rccl_path, const void *unique_id, int32_t nranks,
+                          int32_t rank);
+const char *geobpe_comm_error(void);
+/* Or a host collective: fn gathers `bytes` host bytes from every rank, rank-major, into
+ * recv (nranks * bytes); called synchronously by geobpe_run_exchange (tests over gloo). */
+typedef int (*geobpe_allgather_fn)(void *user, const void *send, void *recv, int64_t bytes);
+int geobpe_comm_set_callback(geobpe_ctx *ctx, geobpe_allgather_fn fn, void *user, int32_t nranks, int32_t rank);
+/* Fixed slot size in records (0 = sized from the last import; tests force stalls with it). */
+int geobpe_comm_set_slot(geobpe_ctx *ctx, int64_t records);
+/* n_merges merges of the row-sharded N > 1 loop with no host wait per merge: per iteration
+ * the merge kernels and the slot export, one all-gather of the fixed slots on the engine's
+ * stream, the import; polls every few iterations; a merge whose records overflowed a slot
+ * is re-exchanged in full.  *n_done = merges made. */
+int geobpe_run_exchange(geobpe_ctx *ctx, int64_t n_merges, int64_t *n_done);
+
 #ifdef __cplusplus
 }
 #endif

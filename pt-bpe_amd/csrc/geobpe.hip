@@ -15,6 +15,9 @@
 //   k_place   per region: token rewrites, pk of the occurrences, posting-log entries
 // The bin pass is k_pairs_all + k_finalize.
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>  // types only: the functions are resolved at run time (the process's RCCL)
+
 #include <algorithm>
 #include <climits>
 #include <cmath>
@@ -34,6 +37,17 @@
 #include "glue.h"
 
 using namespace gb;
+
+// RCCL entry points, resolved with dlsym from the RCCL library the process already uses
+// (PyTorch's: one RCCL instance per process)
+struct RcclApi {
+  void* h = nullptr;
+  ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+  ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+  ncclResult_t (*AllGather)(const void*, void*, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+  ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+  const char* (*GetErrorString)(ncclResult_t) = nullptr;
+};
 
 struct geobpe_ctx {
   int device = 0;
@@ -84,6 +98,18 @@ struct geobpe_ctx {
   int64_t mid_thresh = 16384;  // 0: never
   bool mid_on = false;         // switched (one way)
   bool place_mid = false;      // the pending place is k_mid_sel's (else k_place's)
+  // the multi-rank exchange owned by the engine (geobpe_comm_*, geobpe_run_exchange)
+  int x_kind = 0;  // 0: none, 1: RCCL communicator, 2: host callback
+  RcclApi rccl;
+  ncclComm_t comm = nullptr;
+  geobpe_allgather_fn x_fn = nullptr;
+  void* x_user = nullptr;
+  int32_t x_world = 1, x_rank = 0;
+  uint8_t *x_pbuf = nullptr, *x_gath = nullptr, *x_tmp = nullptr, *x_flat = nullptr;
+  int64_t x_pcap = 0, x_tmp_bytes = 0, x_flat_bytes = 0;
+  uint8_t *x_hsend = nullptr, *x_hrecv = nullptr;  // (host callback: pinned staging)
+  int64_t x_hbytes = 0;
+  int64_t x_ahead = 1, x_capf = 1024, x_fixed = 0;  // poll window and slot size carry over between runs
   // profiling
   bool prof = false;
   int prof_stride = 1;      // time every prof_stride-th launch of each kernel
@@ -502,6 +528,11 @@ void geobpe_destroy(geobpe_ctx* c) {
     if (c->d_cols[i]) hipFree(c->d_cols[i]);
   if (c->h_state) hipHostFree(c->h_state);
   if (c->h_sel) hipHostFree(c->h_sel);
+  if (c->comm && c->rccl.CommDestroy) c->rccl.CommDestroy(c->comm);
+  for (uint8_t* p : {c->x_pbuf, c->x_gath, c->x_tmp, c->x_flat})
+    if (p) hipFree(p);
+  if (c->x_hsend) hipHostFree(c->x_hsend);
+  if (c->x_hrecv) hipHostFree(c->x_hrecv);
   for (auto e : c->evall) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->stream);
   delete c;
@@ -1726,6 +1757,211 @@ int geobpe_synchronize(geobpe_ctx* c) {
   if (!c) return GEOBPE_EARG;
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return sync_state(c);
+}
+
+// ---------------------------------------------------------------- the engine's own exchange
+static thread_local std::string g_comm_err;
+
+const char* geobpe_comm_error(void) { return g_comm_err.c_str(); }
+
+static int rccl_load(const char* path, RcclApi& a, std::string& err) {
+  if (a.h) return 0;
+  void* h = dlopen(path && *path ? path : "librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    err = std::string("dlopen RCCL: ") + dlerror();
+    return GEOBPE_EARG;
+  }
+  a.GetUniqueId = (decltype(a.GetUniqueId))dlsym(h, "ncclGetUniqueId");
+  a.CommInitRank = (decltype(a.CommInitRank))dlsym(h, "ncclCommInitRank");
+  a.AllGather = (decltype(a.AllGather))dlsym(h, "ncclAllGather");
+  a.CommDestroy = (decltype(a.CommDestroy))dlsym(h, "ncclCommDestroy");
+  a.GetErrorString = (decltype(a.GetErrorString))dlsym(h, "ncclGetErrorString");
+  if (!a.GetUniqueId || !a.CommInitRank || !a.AllGather || !a.CommDestroy) {
+    err = "RCCL library lacks ncclGetUniqueId / ncclCommInitRank / ncclAllGather / ncclCommDestroy";
+    return GEOBPE_EARG;
+  }
+  a.h = h;
+  return 0;
+}
+
+int geobpe_comm_unique_id(const char* rccl_path, void* out128) {
+  if (!out128) return GEOBPE_EARG;
+  static RcclApi api;
+  g_comm_err.clear();
+  int rc;
+  if ((rc = rccl_load(rccl_path, api, g_comm_err))) return rc;
+  ncclUniqueId id;
+  const ncclResult_t r = api.GetUniqueId(&id);
+  if (r != ncclSuccess) {
+    g_comm_err = std::string("ncclGetUniqueId: ") + (api.GetErrorString ? api.GetErrorString(r) : "?");
+    return GEOBPE_EHIP;
+  }
+  memcpy(out128, &id, sizeof id);
+  return 0;
+}
+
+int geobpe_comm_init_rccl(geobpe_ctx* c, const char* rccl_path, const void* unique_id, int32_t nranks, int32_t rank) {
+  if (!c || !unique_id || nranks < 1 || rank < 0 || rank >= nranks || nranks > PIPE_MAX_WORLD) return GEOBPE_EARG;
+  if (c->x_kind) return fail(c, GEOBPE_EARG, "exchange already set up");
+  std::string err;
+  if (rccl_load(rccl_path, c->rccl, err)) return fail(c, GEOBPE_EARG, "%s", err.c_str());
+  HIPCHK(c, hipSetDevice(c->device));
+  ncclUniqueId id;
+  memcpy(&id, unique_id, sizeof id);
+  const ncclResult_t r = c->rccl.CommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess)
+    return fail(c, GEOBPE_EHIP, "ncclCommInitRank: %s", c->rccl.GetErrorString ? c->rccl.GetErrorString(r) : "?");
+  c->x_kind = 1;
+  c->x_world = nranks;
+  c->x_rank = rank;
+  return 0;
+}
+
+int geobpe_comm_set_callback(geobpe_ctx* c, geobpe_allgather_fn fn, void* user, int32_t nranks, int32_t rank) {
+  if (!c || !fn || nranks < 1 || rank < 0 || rank >= nranks || nranks > PIPE_MAX_WORLD) return GEOBPE_EARG;
+  if (c->x_kind) return fail(c, GEOBPE_EARG, "exchange already set up");
+  c->x_kind = 2;
+  c->x_fn = fn;
+  c->x_user = user;
+  c->x_world = nranks;
+  c->x_rank = rank;
+  return 0;
+}
+
+int geobpe_comm_set_slot(geobpe_ctx* c, int64_t records) {
+  if (!c || records < 0) return GEOBPE_EARG;
+  c->x_fixed = records;  // 0: sized from the last import (2x the largest, a power of two, 1024..65536)
+  return 0;
+}
+
+namespace {
+
+int grow_dev(geobpe_ctx* c, uint8_t** p, int64_t* have, int64_t bytes) {
+  if (*have >= bytes) return 0;
+  if (*p) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(*p);
+    *p = nullptr;
+  }
+  HIPCHK(c, hipMalloc((void**)p, (size_t)std::max<int64_t>(bytes, 64)));
+  *have = bytes;
+  return 0;
+}
+
+// every rank's `bytes` from d_send, rank-major into d_recv (world * bytes), stream-ordered
+// for RCCL; through pinned host staging and the caller's collective for the callback
+int x_allgather(geobpe_ctx* c, const void* d_send, void* d_recv, int64_t bytes) {
+  if (bytes <= 0) return 0;
+  if (c->x_kind == 1) {
+    const ncclResult_t r = c->rccl.AllGather(d_send, d_recv, (size_t)bytes, ncclUint8, c->comm, c->stream);
+    if (r != ncclSuccess)
+      return fail(c, GEOBPE_EHIP, "ncclAllGather: %s", c->rccl.GetErrorString ? c->rccl.GetErrorString(r) : "?");
+    return 0;
+  }
+  const int64_t need = bytes * c->x_world;
+  if (c->x_hbytes < need) {
+    if (c->x_hsend) hipHostFree(c->x_hsend);
+    if (c->x_hrecv) hipHostFree(c->x_hrecv);
+    HIPCHK(c, hipHostMalloc((void**)&c->x_hsend, (size_t)need, hipHostMallocDefault));
+    HIPCHK(c, hipHostMalloc((void**)&c->x_hrecv, (size_t)need, hipHostMallocDefault));
+    c->x_hbytes = need;
+  }
+  HIPCHK(c, hipMemcpyAsync(c->x_hsend, d_send, (size_t)bytes, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  if (c->x_fn(c->x_user, c->x_hsend, c->x_hrecv, bytes) != 0) return fail(c, GEOBPE_EHIP, "exchange callback failed");
+  HIPCHK(c, hipMemcpyAsync(d_recv, c->x_hrecv, (size_t)need, hipMemcpyHostToDevice, c->stream));
+  return 0;
+}
+
+// the stalled merge: every rank's full record list (counts from the slot headers, then
+// records sized by the largest), compacted rank by rank, imported on every rank
+int x_resolve(geobpe_ctx* c) {
+  const int64_t REC = (int64_t)sizeof(DeltaRec), W = c->x_world;
+  int rc;
+  if ((rc = grow_dev(c, &c->x_tmp, &c->x_tmp_bytes, 8 * W))) return rc;
+  if ((rc = x_allgather(c, c->x_pbuf, c->x_tmp, 8))) return rc;
+  std::vector<int64_t> cnt(W);
+  HIPCHK(c, hipMemcpyAsync(cnt.data(), c->x_tmp, 8 * W, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  const int64_t m = *std::max_element(cnt.begin(), cnt.end());
+  if (m > c->x_pcap) return fail(c, GEOBPE_ECAPACITY, "delta export needs %lld records (cap %lld)", (long long)m,
+                                 (long long)c->x_pcap);
+  int64_t total = 0;
+  for (int64_t r : cnt) total += r;
+  if ((rc = grow_dev(c, &c->x_tmp, &c->x_tmp_bytes, std::max<int64_t>(8 * W, W * m * REC))) ||
+      (rc = grow_dev(c, &c->x_flat, &c->x_flat_bytes, std::max<int64_t>(total, 1) * REC)))
+    return rc;
+  if ((rc = x_allgather(c, c->x_pbuf + REC, c->x_tmp, m * REC))) return rc;
+  int64_t off = 0;
+  for (int64_t r = 0; r < W; r++) {
+    if (cnt[r])
+      HIPCHK(c, hipMemcpyAsync(c->x_flat + off * REC, c->x_tmp + r * m * REC, cnt[r] * REC, hipMemcpyDeviceToDevice,
+                               c->stream));
+    off += cnt[r];
+  }
+  return geobpe_pipeline_resolve(c, c->x_flat, total);
+}
+
+}  // namespace
+
+// the pipelined N > 1 loop with the engine's own exchange (TorchGroup.run_pipelined in C++):
+// per iteration select / find / commit and the slot export, ONE all-gather of the fixed
+// slots on the engine's stream, the import; a poll every few iterations (the window doubles
+// up to 64, back to 1 after a stall), a stalled merge re-exchanged in full.  Every rank sees
+// the same polls, so every rank issues the same collectives.
+int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
+  if (!c || n_merges < 0) return GEOBPE_EARG;
+  if (!c->distributed || !c->keys_ready) return fail(c, GEOBPE_EARG, "run_exchange needs a distributed, binned engine");
+  if (!c->x_kind) return fail(c, GEOBPE_EARG, "no exchange set up (geobpe_comm_init_rccl / geobpe_comm_set_callback)");
+  HIPCHK(c, hipSetDevice(c->device));
+  const int64_t REC = (int64_t)sizeof(DeltaRec), W = c->x_world;
+  constexpr int64_t CAP_MIN = 1024, CAP_MAX = 65536, AHEAD_MAX = 64;
+  int rc;
+  if (!c->x_pbuf) {
+    c->x_pcap = 3 * c->R + 65536;
+    const int64_t top = c->x_fixed ? c->x_fixed : CAP_MAX;
+    HIPCHK(c, hipMalloc((void**)&c->x_pbuf, (size_t)((1 + c->x_pcap) * REC)));
+    HIPCHK(c, hipMemsetAsync(c->x_pbuf, 0, (size_t)((1 + c->x_pcap) * REC), c->stream));
+    HIPCHK(c, hipMalloc((void**)&c->x_gath, (size_t)(W * (1 + top) * REC)));
+  }
+  if ((rc = geobpe_pipeline_begin(c))) return rc;
+  int64_t out[4];
+  int64_t done = 0;
+  rc = geobpe_pipeline_poll(c, out);
+  const int64_t it0 = out[1];
+  int64_t ahead = c->x_ahead, capf = c->x_fixed ? c->x_fixed : c->x_capf;
+  while (!rc && done < n_merges) {
+    const int64_t slot = (1 + capf) * REC;
+    const int64_t k = std::min(ahead, n_merges - done);  // an iteration merges at most once
+    for (int64_t i = 0; i < k && !rc; i++) {
+      if ((rc = geobpe_pipeline_iter(c, c->x_pbuf, c->x_pcap))) break;
+      if ((rc = x_allgather(c, c->x_pbuf, c->x_gath, slot))) break;
+      rc = geobpe_pipeline_import(c, c->x_gath, (int32_t)W, capf);
+    }
+    if (rc || (rc = geobpe_pipeline_poll(c, out))) break;
+    const bool stalled = out[0] != 0, fin = out[2] != 0;
+    const int64_t it = out[1], smax = out[3];
+    if (stalled) {
+      if ((rc = x_resolve(c))) break;
+      ahead = 1;
+    } else {
+      ahead = std::min<int64_t>(2 * ahead, AHEAD_MAX);
+    }
+    if (!c->x_fixed) {
+      int64_t p2 = 1;
+      while (p2 < 2 * std::max<int64_t>(smax, 1)) p2 <<= 1;
+      capf = std::min(CAP_MAX, std::max(CAP_MIN, p2));
+    }
+    done = it - it0;
+    c->x_ahead = ahead;
+    c->x_capf = capf;
+    if (fin) break;
+  }
+  const int rc_end = geobpe_pipeline_end(c);
+  if (rc) return rc;  // (an error in flight is the one to report)
+  if (rc_end) return rc_end;
+  if (n_done) *n_done = done;
+  return 0;
 }
 
 }  // extern "C"

@@ -15,6 +15,19 @@ LIB_PATH = os.environ.get("GEOBPE_LIB") or os.path.join(HERE, "libgeobpe.so")  #
 
 E_OK, E_ARG, E_VALUE, E_CAPACITY, E_HIP, E_HASH = range(6)
 DELTA_RECORD_BYTES = 40
+# geobpe_allgather_fn: (user, host send, host recv, bytes per rank) -> 0 on success
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64)
+
+
+def rccl_path():
+    """The RCCL library this process's PyTorch uses (the engine's communicator binds to the
+    same instance), or None for the system's librccl.so.1."""
+    try:
+        import torch
+        p = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+        return p if os.path.exists(p) else None
+    except ImportError:  # pragma: no cover
+        return None
 
 
 class GeoBPEError(RuntimeError):
@@ -97,6 +110,12 @@ def lib():
         "geobpe_pipeline_poll": (ctypes.c_int, [P, P]),
         "geobpe_pipeline_resolve": (ctypes.c_int, [P, P, I64]),
         "geobpe_pipeline_end": (ctypes.c_int, [P]),
+        "geobpe_comm_unique_id": (ctypes.c_int, [ctypes.c_char_p, P]),
+        "geobpe_comm_init_rccl": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int32, ctypes.c_int32]),
+        "geobpe_comm_error": (ctypes.c_char_p, []),
+        "geobpe_comm_set_callback": (ctypes.c_int, [P, P, P, ctypes.c_int32, ctypes.c_int32]),
+        "geobpe_comm_set_slot": (ctypes.c_int, [P, I64]),
+        "geobpe_run_exchange": (ctypes.c_int, [P, I64, pI64]),
         "geobpe_pdb_backbone": (I64, [ctypes.c_char_p, P, I64]),
         "geobpe_pdb_error": (ctypes.c_char_p, []),
         "geobpe_featurize": (ctypes.c_int, [ctypes.c_int, I64, P, P, P]),
@@ -125,7 +144,9 @@ EXPORTED_SYMBOLS = [
     "geobpe_verify_counts", "geobpe_debug_timeline", "geobpe_set_profiling", "geobpe_set_work_counters", "geobpe_set_hold", "geobpe_set_profiling_filter", "geobpe_kernel_ms", "geobpe_marker", "geobpe_synchronize",
     "geobpe_set_record_events", "geobpe_events", "geobpe_replay_load",
     "geobpe_delta_export_async", "geobpe_delta_import_async", "geobpe_pipeline_begin", "geobpe_pipeline_iter",
-    "geobpe_pipeline_import", "geobpe_pipeline_poll", "geobpe_pipeline_resolve", "geobpe_pipeline_end", "geobpe_pdb_backbone", "geobpe_pdb_error",
+    "geobpe_pipeline_import", "geobpe_pipeline_poll", "geobpe_pipeline_resolve", "geobpe_pipeline_end",
+    "geobpe_comm_unique_id", "geobpe_comm_init_rccl", "geobpe_comm_error", "geobpe_comm_set_callback",
+    "geobpe_comm_set_slot", "geobpe_run_exchange", "geobpe_pdb_backbone", "geobpe_pdb_error",
     "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf", "geobpe_glue_opt",
 ]
 

@@ -127,8 +127,57 @@ class TorchGroup:
     # ---------------------------------------------------------------- pipelined exchange
     PIPE_CAP_MIN, PIPE_CAP_MAX = 1024, 65536  # records per rank slot (40 B each)
     PIPE_AHEAD = 64      # iterations enqueued between polls (doubling from 1 after a stall)
+    engine_exchange = True  # the loop and its collectives in the engine (geobpe_run_exchange)
+
+    def _host_allgather(self, user, hsend, hrecv, nbytes):
+        """geobpe_allgather_fn over this group (gloo): host bytes of every rank, rank-major."""
+        try:
+            T = self.torch
+            src = np.ctypeslib.as_array((ctypes.c_uint8 * int(nbytes)).from_address(hsend)).copy()
+            out = T.empty(self.world_size * int(nbytes), dtype=T.uint8)
+            self.dist.all_gather_into_tensor(out, T.from_numpy(src), group=self.pg)
+            ctypes.memmove(hrecv, out.numpy().ctypes.data, self.world_size * int(nbytes))
+            return 0
+        except Exception:  # pragma: no cover - reported by the engine as a failed exchange
+            return 1
+
+    def attach(self, engine):
+        """The engine's own exchange: an RCCL communicator (backend nccl: rank 0's id
+        broadcast over this group) or this group's host collective (gloo)."""
+        if getattr(engine, "_x_attached", False):
+            return
+        L, T = engine.L, self.torch
+        if self.backend == "nccl":
+            path = _native.rccl_path()
+            pb = path.encode() if path else None
+            uid = np.zeros(128, dtype=np.uint8)
+            if self.rank == 0:
+                rc = L.geobpe_comm_unique_id(pb, uid.ctypes.data_as(ctypes.c_void_p))
+                if rc:
+                    raise _native.GeoBPEError(f"geobpe_comm_unique_id: {L.geobpe_comm_error().decode()}")
+            t = T.from_numpy(uid).to(self.comm_dev)
+            self.dist.broadcast(t, src=0, group=self.pg)
+            uid = t.cpu().numpy()
+            engine._chk(L.geobpe_comm_init_rccl(engine._ctx, pb, uid.ctypes.data_as(ctypes.c_void_p),
+                                                self.world_size, self.rank))
+        else:
+            self._cb = _native.ALLGATHER_FN(self._host_allgather)  # (kept alive with the group)
+            engine._chk(L.geobpe_comm_set_callback(engine._ctx, ctypes.cast(self._cb, ctypes.c_void_p), None,
+                                                   self.world_size, self.rank))
+        fixed = getattr(self, "pipe_cap", None)
+        if fixed:
+            engine._chk(L.geobpe_comm_set_slot(engine._ctx, int(fixed)))
+        engine._x_attached = True
 
     def run_pipelined(self, engine, n_merges: int) -> int:
+        if self.engine_exchange:
+            self.attach(engine)
+            n = ctypes.c_int64(0)
+            engine._chk(engine.L.geobpe_run_exchange(engine._ctx, int(n_merges), ctypes.byref(n)))
+            return int(n.value)
+        return self._run_pipelined_host(engine, n_merges)
+
+    def _run_pipelined_host(self, engine, n_merges: int) -> int:
         """``n_merges`` merges with no host wait per merge (include/geobpe.h,
         geobpe_pipeline_*): per iteration the engine enqueues select / mark / apply
         and its export into a fixed slot, one all-gather of the slots follows on the

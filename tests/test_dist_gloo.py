@@ -94,6 +94,8 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
         g = TorchGroup(int(shard["row_off"][-1]), device=0)
         if mode == "small-slots":  # most merges overflow the fixed slots: the stall / resolve path
             g.pipe_cap = 16
+        if mode == "host-loop":  # the Python-driven loop (geobpe.dist) instead of geobpe_run_exchange
+            g.engine_exchange = False
         e = GeoBPEEngine(shard, 5, device=0, group=g).initialize()
         e.pipelined = mode != "stepwise"
         e.bin()
@@ -114,12 +116,13 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise"),
-                                         (3, "mixed"), (4, "small-slots")])
+                                         (3, "mixed"), (4, "small-slots"), (2, "host-loop")])
 def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
     """The full N>1 path (TorchGroup exchange, one process per rank) with gloo on
-    one device: the pipelined exchange (fixed slots, stall + full re-exchange of an
-    overflowing merge), the same with tiny slots, and the host-synchronised
-    per-merge exchange; merge list and segmentation equal the oracle's."""
+    one device: the engine's pipelined loop (geobpe_run_exchange over the group's host
+    collective: fixed slots, stall + full re-exchange of an overflowing merge), the same
+    with tiny slots, the Python-driven loop, and the host-synchronised per-merge
+    exchange; merge list and segmentation equal the oracle's."""
     import multiprocessing as mp
     from geobpe import synth
     ctx = mp.get_context("spawn")
