@@ -290,12 +290,24 @@ def main():
                           f"{COMMIT_KEY_BYTES} B x keys (avg {cw['commit_key_records']:.0f} / "
                           f"{cw['commit_decrement_records']:.0f} / {cw['commit_keys']:.0f} per launch, counted by an "
                           f"instrumented replay of the same merges)")
+    # the sampled launches (every event_stride-th of each kernel in the timed region) pair
+    # with their own merges' bytes when the window had no rebuild iteration (one launch of
+    # each kernel per merge); the replay's every-launch average pairs with the window average
+    per_occ = {"find": FIND_BYTES_PER_OCC, "select": PLACE_BYTES_PER_OCC, "mid_find": MIDFIND_BYTES_PER_OCC,
+               "mid_sel": MIDSEL_BYTES_PER_OCC}
+    src_of = {"find": w_full, "select": prev[:n_full], "mid_find": w_mid, "mid_sel": prev[n_full:]}
+    no_skip = st1["nskip"] == st0["nskip"]
     roofs = {}
     for k, (ms, nl) in ktimes.items():
         if not nl:
             continue
         avg_s = ms / 1000.0 / nl
         bpl, note = work[k]
+        if no_skip and k in per_occ:
+            smp = src_of[k][::args.event_stride][:nl]
+            if len(smp) == nl:
+                bpl = per_occ[k] * sum(m[2] for m in smp) / nl
+                note += f"; the {nl} timed launches' own merges: avg {bpl / per_occ[k]:.0f} occurrences"
         ach = bpl / avg_s / 1e9 if bpl is not None else None
         traffic, tsrc = pmc_traffic(k, wkey)  # (k_select's dispatches carry k_place)
         roofs[k] = {"kernel": {"select": "k_select+k_place", "mid_sel": "k_mid_sel"}.get(k, f"k_{k}"), "bound": "hbm", "achieved": round(ach, 2) if ach else None,
@@ -303,7 +315,9 @@ def main():
                     "traffic": traffic, "traffic_source": tsrc, "traffic_window": wkey,
                     "bytes_per_launch": round(bpl, 1) if bpl is not None else None, "avg_launch_us": round(avg_s * 1e6, 3),
                     "launches_timed": nl, "event_stride": args.event_stride, "algorithmic_bytes": note,
-                    "replay_avg_launch_us": round(replay_avg[k], 3) if k in replay_avg else None}
+                    "replay_avg_launch_us": round(replay_avg[k], 3) if k in replay_avg else None,
+                    "replay_achieved": (round(work[k][0] / (replay_avg[k] * 1e-6) / 1e9, 2)
+                                        if k in replay_avg and work[k][0] is not None else None)}
     if args.roofline_kernel == "auto":  # the slowest by every launch of the replay, else by the samples
         dom = max(roofs, key=lambda k: replay_avg.get(k, roofs[k]["avg_launch_us"])) if roofs else None
     else:
