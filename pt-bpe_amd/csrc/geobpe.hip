@@ -448,7 +448,10 @@ int tail_run(geobpe_ctx* c, int64_t n) {
   return 0;
 }
 
-bool mid_enabled(const geobpe_ctx* c) { return c->mid_thresh > 0 && !c->distributed && !c->replay; }
+// (multi-rank: inside the pipelined exchange only -- its iterations write delta records)
+bool mid_enabled(const geobpe_ctx* c) {
+  return c->mid_thresh > 0 && !c->replay && (!c->distributed || c->pipelined);
+}
 
 // the next batch of iterations before the regime switches are checked: long while the
 // merges are far above the next threshold (the check costs a synchronisation)
@@ -472,6 +475,18 @@ int mid_prepare(geobpe_ctx* c) {
   int rc;
   if ((rc = tail_alloc(c))) return rc;
   if (!c->h_state->kp_valid || c->h_state->kpool_used > c->D.KPOOL / 4 * 3) tail_build(c);
+  return 0;
+}
+
+// back to the full-grid kernels (the host-stepped multi-rank path): everything pending is
+// placed, the full-grid posting index and the per-key lists are marked stale (each is
+// rebuilt when its path runs again)
+int mid_leave(geobpe_ctx* c) {
+  if (!c->mid_on) return 0;
+  flush_place(c);
+  HIPCHK(c, hipMemsetAsync(&c->D.st->post_valid, 0, 4, c->stream));
+  HIPCHK(c, hipMemsetAsync(&c->D.st->kp_valid, 0, 4, c->stream));
+  c->mid_on = false;
   return 0;
 }
 
@@ -908,6 +923,7 @@ int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {
   if (c->pipelined) return fail(c, GEOBPE_EARG, "step_select inside a pipelined exchange");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  if ((rc = mid_leave(c))) return rc;
   Sel sel;
   for (;;) {
     enqueue_select(c);
@@ -1108,15 +1124,37 @@ int geobpe_pipeline_begin(geobpe_ctx* c) {
 
 int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   if (!c || !c->pipelined || !d_buf) return GEOBPE_EARG;
+  Dev D = c->D;  // find and commit write this rank's delta records into the slot buffer
+  D.xrec = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
+  D.xcap = cap_total;
+  if (c->mid_on && mid_enabled(c)) {  // the middle regime (mid.h), device parity
+    if (c->place_pending && !c->place_mid) flush_place(c);
+    {
+      Timed t(c, "mid_sel");
+      c->place_pending = false;
+      hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, D, -1);
+    }
+    {
+      Timed t(c, "mid_find");
+      hipLaunchKernelGGL(k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D, -1, c->nba - MID_APP, 1);
+    }
+    c->place_pending = true;
+    c->place_mid = true;
+    {
+      Timed t(c, "export");
+      hipLaunchKernelGGL(k_export_head, dim3(16), dim3(BLOCK), 0, c->stream, c->D,
+                         reinterpret_cast<DeltaRec*>(d_buf) + 1, (int64_t*)d_buf, cap_total);
+    }
+    HIPCHK(c, hipGetLastError());
+    return 0;
+  }
+  if (c->place_pending && c->place_mid) flush_place(c);
   {
     Timed t(c, "select");  // (+ the previous merge's k_place)
     const int grid = c->place_pending ? 1 + c->nba : 1;
     c->place_pending = false;
     hipLaunchKernelGGL(k_select, dim3(grid), dim3(SBLOCK), 0, c->stream, c->D, -1);
   }
-  Dev D = c->D;  // find and commit write this rank's delta records into the slot buffer
-  D.xrec = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
-  D.xcap = cap_total;
   {
     Timed t(c, "find");
     hipLaunchKernelGGL(k_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D, 1, -1);
@@ -1931,6 +1969,14 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
   const int64_t it0 = out[1];
   int64_t ahead = c->x_ahead, capf = c->x_fixed ? c->x_fixed : c->x_capf;
   while (!rc && done < n_merges) {
+    // the middle regime once this rank's share of a merge is small (a poll is a quiescent
+    // point: the lists are built, or rebuilt after an iteration stalled on them)
+    if (!c->mid_on && mid_enabled(c) && c->h_state->iter > 0) {
+      LogRec lr;
+      HIPCHK(c, hipMemcpy(&lr, c->D.log + (c->h_state->iter - 1), sizeof lr, hipMemcpyDeviceToHost));
+      if (lr.nmerged <= c->mid_thresh) c->mid_on = true;
+    }
+    if (c->mid_on && (rc = mid_prepare(c))) break;
     const int64_t slot = (1 + capf) * REC;
     const int64_t k = std::min(ahead, n_merges - done);  // an iteration merges at most once
     for (int64_t i = 0; i < k && !rc; i++) {

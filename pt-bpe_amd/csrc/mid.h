@@ -79,6 +79,38 @@ __device__ inline void mid_pair(const Dev& D, const MidCtx& F, int32_t target, i
     set_error(D, GEOBPE_ECAPACITY, -71);
 }
 
+// multi-rank (D.xrec set, the pipelined exchange): count changes go out as delta records
+// (the import adds every rank's, this rank's included, with the hot-list check); the
+// record carries this rank's key id (pad = id + 1: no probe on import)
+__device__ inline void mid_emit(const Dev& D, u64 h1, u64 h2, int32_t len, int32_t idL, int32_t g, int32_t idR,
+                                int32_t delta, int32_t d) {
+  DeltaRec r;
+  r.h1 = h1;
+  r.h2 = h2;
+  r.len = len;
+  r.idL = idL;
+  r.g = g;
+  r.idR = idR;
+  r.delta = delta;
+  r.pad = d + 1;
+  const int64_t j = wave_reserve64((unsigned long long*)&D.st->ntouched);
+  if (j < D.xcap)
+    D.xrec[j] = r;
+  else
+    set_error(D, GEOBPE_ECAPACITY, -72);
+}
+__device__ inline void mid_emit_id(const Dev& D, int32_t d, int32_t delta) {
+  mid_emit(D, D.kh1[d], D.kh2[d], D.klen[d], D.krep[3 * (int64_t)d], D.krep[3 * (int64_t)d + 1],
+           D.krep[3 * (int64_t)d + 2], delta, d);
+}
+// -v on key d: a count atomic, or a record (multi-rank)
+__device__ inline void mid_dec(const Dev& D, int32_t d, int32_t v) {
+  if (D.xrec)
+    mid_emit_id(D, d, v);
+  else
+    atomicAdd(&D.count[d], v);
+}
+
 // find-or-claim with the CAS as the first probe (an empty first slot is claimed, the key
 // itself is found, anything else probes on)
 __device__ inline int32_t mid_resolve(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
@@ -104,7 +136,10 @@ __device__ void mid_single(const Dev& D, MidFindLds& S, const MidCtx& F, u64 h1,
   } else {
     emit_check(D, &S.chk, d, len, h1, h2);
   }
-  count_add_hot(D, S.hot, d, 1, F.th);
+  if (D.xrec)
+    mid_emit(D, h1, h2, len, idL, g, idR, 1, d);
+  else
+    count_add_hot(D, S.hot, d, 1, F.th);
   mid_pair(D, F, target, d);
 }
 
@@ -166,9 +201,9 @@ __device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g
   }
   const bool pN = p >= 0 && !pRight;
   mid_occ(D, S, F, g, F.wl | (tb.y & (int32_t)0xFFFF0000), b, c);
-  if (pkb >= 0 && !agg_stage(S.agg, pkb, -1)) atomicAdd(&D.count[pkb], -1);
+  if (pkb >= 0 && !agg_stage(S.agg, pkb, -1)) mid_dec(D, pkb, -1);
   if (pN) {
-    if (!agg_stage(S.agg, tp.w, -1)) atomicAdd(&D.count[tp.w], -1);
+    if (!agg_stage(S.agg, tp.w, -1)) mid_dec(D, tp.w, -1);
     combine_pw(l1, l2, glL, F.w1, F.w2, F.pa1, F.pb1, F.pa2, F.pb2, hl.h1, hl.h2);
     hl.len = tok_len(tp.y) + F.wl;
     hl.pkey = probe_key(hl.h1, hl.h2, hl.len);
@@ -197,7 +232,7 @@ __device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g
     const int32_t vc2 = c2i >= 0 ? max(tc2.x, 0) : 0;
     const u64 d1 = D.vh1[vc2], d2 = D.vh2[vc2];
     mid_occ(D, S, F, t, F.wl | (tb2.y & (int32_t)0xFFFF0000), b2, c2i);
-    if (pkb2 >= 0 && !agg_stage(S.agg, pkb2, -1)) atomicAdd(&D.count[pkb2], -1);
+    if (pkb2 >= 0 && !agg_stage(S.agg, pkb2, -1)) mid_dec(D, pkb2, -1);
     if (c2i >= 0) {
       MidHalf h;
       mid_right(D, F, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
@@ -269,8 +304,9 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
   // candidates: the winner's list, then the previous merge's new pairs (those of key W)
   const int32_t nW = sel.kpn;
   const int64_t offW = sel.kpoff;
-  const int2* thp = mid_th(D, par ^ 1);
-  const int64_t nP = st->place_par_prev == (par ^ 1) ? min(st->mid_nh[par ^ 1], D.THcap) : 0;
+  const int32_t pp = st->place_par_prev;  // the previous merge's parity (-1: its pairs are in the lists)
+  const int2* thp = mid_th(D, pp >= 0 ? pp : 0);
+  const int64_t nP = pp >= 0 ? min(st->mid_nh[pp], D.THcap) : 0;
   const int64_t ntot = nW + nP;
   if (w == 0) {  // _tokens[n] = json.loads(key); state the next select reads
     const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
@@ -364,7 +400,10 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
       } else {
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
-      count_add_hot(D, S.hot, d, S.cnt[s], F.th);
+      if (D.xrec)
+        mid_emit(D, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
+      else
+        count_add_hot(D, S.hot, d, S.cnt[s], F.th);
     }
     __syncthreads();
     if (c0 == lo) dbg_stamp(D, 17);
@@ -389,10 +428,10 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
   // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
   for (int i = t; i < AggT<11>::N; i += ABLOCK) {
     const int32_t k = S.agg.key[i], v = S.agg.val[i];
-    if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
+    if (k >= 0 && v != 0) mid_dec(D, k, v);
   }
   if (t == 0 && S.nm) {
-    atomicAdd(&D.count[F.W], -S.nm);
+    mid_dec(D, F.W, -S.nm);
     atomicAdd((unsigned long long*)&D.log[sel.iter].nmerged, (unsigned long long)S.nm);
   }
   hot_flush(D, S.hot);  // (syncs the workgroup first)
@@ -530,14 +569,19 @@ __device__ void mid_append_body(const Dev& D, const int2* th, int64_t nh, int32_
   if (S.full && t == 0) st->kp_valid = 0;
 }
 
-// workgroups 0..G-1: the find of merge `par` (find = 0: none, a flush); workgroups G..:
-// the posting entries of the previous merge (st->place_par_prev), skipping this merge's winner
+// workgroups 0..G-1: the find of merge `par` (find = 0: none, a flush; par < 0: the
+// pipelined exchange's device parity); workgroups G..: the posting entries of the previous
+// merge (st->place_par_prev), skipping this merge's winner
 __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int find) {
   __shared__ union {
     MidFindLds f;
     MidAppLds a;
   } U;
   State* st = D.st;
+  if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
+    if (st->stall) return;
+    par = st->dgen & 1;
+  }
   Sel sel = D.sel[par];
   // lists that lost entries (an append ran out of table or pool space): no merge until the
   // host rebuilds them -- the select wrote only what the next select overwrites (Sel, the
@@ -548,10 +592,11 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int 
     mid_find_body(D, sel, par, blockIdx.x, G, U.f);
     return;
   }
-  if (st->place_par_prev != (par ^ 1) || !valid) return;
-  const int64_t nh = min(st->mid_nh[par ^ 1], D.THcap);
+  const int32_t pp = st->place_par_prev;
+  if (pp < 0 || !valid) return;
+  const int64_t nh = min(st->mid_nh[pp], D.THcap);
   const int32_t skip = sel.decision == SEL_MERGE ? sel.W : -1;
-  mid_append_body(D, mid_th(D, par ^ 1), nh, skip, blockIdx.x - G, gridDim.x - G, U.a);
+  mid_append_body(D, mid_th(D, pp), nh, skip, blockIdx.x - G, gridDim.x - G, U.a);
 }
 
 // ---------------------------------------------------------------------- select + place
@@ -602,6 +647,13 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par) {
   State* st = D.st;
   if (threadIdx.x == 0) st->place_par_prev = st->place_par;
   if (par == INT32_MIN) return;
+  if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
+    if (st->stall) return;
+    const int32_t g = st->dgen + 1;
+    par = g & 1;
+    __syncthreads();  // every thread has read dgen
+    if (threadIdx.x == 0) st->dgen = g;
+  }
   if (threadIdx.x == 0) {
     st->mid_nm[par] = 0;
     st->mid_nh[par] = 0;
