@@ -28,6 +28,7 @@ extern "C" {
 #define GEOBPE_ECAPACITY 3 /* a device table is full */
 #define GEOBPE_EHIP 4      /* HIP runtime error */
 #define GEOBPE_EHASH 5     /* content-hash collision detected (never expected) */
+#define GEOBPE_ESTATE 6    /* inconsistent device token links (internal error; never expected) */
 
 /* angle column order of the input table (= Tokenizer.init_structure,
  * foldingdiff/tokenizer.py:393-405): */

@@ -218,6 +218,8 @@ int check_device_error(geobpe_ctx* c) {
       return fail(c, GEOBPE_ECAPACITY, "device table capacity exceeded (site %lld)", (long long)pos);
     case GEOBPE_EHASH:
       return fail(c, GEOBPE_EHASH, "content hash collision detected (item %lld)", (long long)pos);
+    case GEOBPE_ESTATE:
+      return fail(c, GEOBPE_ESTATE, "inconsistent token links at slot %lld (internal error)", (long long)pos);
     default:
       return fail(c, (int)code, "device error %lld at %lld", (long long)code, (long long)pos);
   }
@@ -486,6 +488,10 @@ int mid_leave(geobpe_ctx* c) {
   flush_place(c);
   HIPCHK(c, hipMemsetAsync(&c->D.st->post_valid, 0, 4, c->stream));
   HIPCHK(c, hipMemsetAsync(&c->D.st->kp_valid, 0, 4, c->stream));
+  // k_commit zeroes only the other parity's overflow counters: the last full-grid merge
+  // before the switch left its own, which the next find of that parity would extend
+  HIPCHK(c, hipMemsetAsync(c->D.st->L_ovf2, 0, sizeof c->D.st->L_ovf2, c->stream));
+  HIPCHK(c, hipMemsetAsync(c->D.st->nko2, 0, sizeof c->D.st->nko2, c->stream));
   c->mid_on = false;
   return 0;
 }

@@ -302,7 +302,10 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
       if (y < 0) break;
       const int4 ty = D.tok[y];
       if (ty.w != W) break;
-      m++;
+      if (++m > D.R) {  // (a link cycle: report it instead of spinning)
+        set_error(D, GEOBPE_ESTATE, y);
+        break;
+      }
       y = ty.z;
     }
     pRight = (m & 1) != 0;
@@ -333,7 +336,11 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
   int32_t cur_c = c, cur_pkb = pkb;
   bool cur_cL = cL;
   int32_t lcur_c = tok_len(tc.y);
-  while (cur_pkb == W && cur_cL) {
+  for (int64_t steps = 0; cur_pkb == W && cur_cL; steps++) {
+    if (steps > D.R || lcur_c <= 0) {  // (a walk that does not advance: report it instead of spinning)
+      set_error(D, GEOBPE_ESTATE, cur_c);
+      break;
+    }
     const int32_t t = cur_c;
     const int32_t b2 = t + lcur_c;
     const int4 tb2 = D.tok[b2];
