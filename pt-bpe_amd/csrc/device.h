@@ -242,6 +242,9 @@ struct Dev {
   // rank-local delta array, no export pass); null: the touched-list path
   DeltaRec* xrec;
   int64_t xcap;
+  // the record counter: null = st->ntouched; the middle regime (mid.h) counts straight
+  // into the slot header, which is then final when k_mid_find ends (no header pass)
+  int64_t* xcnt;
   int2* xovf;  // (key, delta) of the rare unstaged adds of a pipelined iteration
   int64_t ovf_cap;
   // late-merge path (tail.h): key d's posting list is kpool[kp_off[d] .. + kp_n[d]) (capacity
@@ -449,8 +452,8 @@ __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_de
     atomicAdd(&D.count[d], v);
     return;
   }
-  if (D.xrec) {  // pipelined exchange, rare path: (key, delta) to a side list that k_export_head
-                 // turns into records (a record built here costs k_find its register budget)
+  if (D.xrec) {  // pipelined exchange, k_find's rare path: (key, delta) to a side list that
+                 // k_commit turns into records (a record built here costs k_find its register budget)
     const unsigned long long j = atomicAdd((unsigned long long*)&D.st->nxovf, 1ULL);
     if ((int64_t)j < D.KCAP)
       D.xovf[j] = make_int2(d, v);
@@ -459,6 +462,32 @@ __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_de
     return;
   }
   if (atomicAdd(&D.dcount[d], v) == 0) touched_append(D, d);
+}
+
+// pipelined exchange, k_commit's rare unstaged adds: a delta record straight into the
+// rank's slot (one reservation per wave instruction on the record counter)
+__device__ inline void rec_add(const Dev& D, int32_t d, int32_t v) {
+  const u64 m = __ballot(1);
+  const int lane = wave_lane();
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader)
+    base = atomicAdd((unsigned long long*)(D.xcnt ? D.xcnt : &D.st->ntouched), (unsigned long long)__popcll(m));
+  base = __shfl(base, leader, 64);
+  const int64_t j = (int64_t)(base + __popcll(m & ((1ULL << lane) - 1)));
+  DeltaRec r;
+  r.h1 = D.kh1[d];
+  r.h2 = D.kh2[d];
+  r.len = D.klen[d];
+  r.idL = D.krep[3 * (int64_t)d];
+  r.g = D.krep[3 * (int64_t)d + 1];
+  r.idR = D.krep[3 * (int64_t)d + 2];
+  r.delta = v;
+  r.pad = d + 1;
+  if (j < D.xcap)
+    D.xrec[j] = r;
+  else
+    set_error(D, GEOBPE_ECAPACITY, -33);
 }
 
 // rank-local deltas of one workgroup whose keys join the touched list: buffered in

@@ -106,6 +106,7 @@ struct geobpe_ctx {
   void* x_user = nullptr;
   int32_t x_world = 1, x_rank = 0;
   uint8_t *x_pbuf = nullptr, *x_gath = nullptr, *x_tmp = nullptr, *x_flat = nullptr;
+  int64_t* x_head = nullptr;  // the slot header of the last pipelined iteration (its record count)
   int64_t x_pcap = 0, x_tmp_bytes = 0, x_flat_bytes = 0;
   uint8_t *x_hsend = nullptr, *x_hrecv = nullptr;  // (host callback: pinned staging)
   int64_t x_hbytes = 0;
@@ -1133,6 +1134,12 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   Dev D = c->D;  // find and commit write this rank's delta records into the slot buffer
   D.xrec = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
   D.xcap = cap_total;
+  int64_t* head = reinterpret_cast<int64_t*>(d_buf);
+  if (head != c->x_head) {  // a buffer new to this engine: its count starts at 0 (then the import resets it)
+    HIPCHK(c, hipMemsetAsync(head, 0, 8, c->stream));
+    c->x_head = head;
+  }
+  D.xcnt = head;  // the records are counted in the slot header: final when the iteration's last kernel ends
   if (c->mid_on && mid_enabled(c)) {  // the middle regime (mid.h), device parity
     if (c->place_pending && !c->place_mid) flush_place(c);
     {
@@ -1146,11 +1153,6 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     }
     c->place_pending = true;
     c->place_mid = true;
-    {
-      Timed t(c, "export");
-      hipLaunchKernelGGL(k_export_head, dim3(16), dim3(BLOCK), 0, c->stream, c->D,
-                         reinterpret_cast<DeltaRec*>(d_buf) + 1, (int64_t*)d_buf, cap_total);
-    }
     HIPCHK(c, hipGetLastError());
     return 0;
   }
@@ -1175,11 +1177,6 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
 #endif
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
-  {
-    Timed t(c, "export");
-    hipLaunchKernelGGL(k_export_head, dim3(16), dim3(BLOCK), 0, c->stream, c->D, reinterpret_cast<DeltaRec*>(d_buf) + 1,
-                       (int64_t*)d_buf, cap_total);
-  }
   HIPCHK(c, hipGetLastError());
   return 0;
 }
@@ -1189,7 +1186,7 @@ int geobpe_pipeline_import(geobpe_ctx* c, const void* d_slots, int32_t world, in
   {
     Timed t(c, "import");
     hipLaunchKernelGGL(k_import_fixed, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, (const uint8_t*)d_slots, world,
-                       cap_fixed, c->rank < world ? c->rank : -1);
+                       cap_fixed, c->rank < world ? c->rank : -1, c->x_head);
   }
   HIPCHK(c, hipGetLastError());
   return 0;
@@ -1213,6 +1210,7 @@ int geobpe_pipeline_resolve(geobpe_ctx* c, const void* d_in, int64_t n_records) 
   if (!c || !c->pipelined) return GEOBPE_EARG;
   int rc;
   if ((rc = delta_import(c, d_in, n_records))) return rc;
+  if (c->x_head) HIPCHK(c, hipMemsetAsync(c->x_head, 0, 8, c->stream));  // (the stalled merge's count, consumed)
   HIPCHK(c, hipMemsetAsync(&c->D.st->stall, 0, 4, c->stream));
   return sync_state(c);
 }

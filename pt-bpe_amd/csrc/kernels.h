@@ -1070,34 +1070,6 @@ __global__ __launch_bounds__(BLOCK) void k_export_dev(Dev D, DeltaRec* out, int6
     out[j] = r;
   }
 }
-// pipelined exchange: the slot header of the records k_commit wrote (no-op while
-// stalled: the stalled merge's records stay for the full re-exchange)
-__global__ __launch_bounds__(BLOCK) void k_export_head(Dev D, DeltaRec* out, int64_t* d_count, int64_t cap) {
-  State* st = D.st;
-  if (st->stall) return;
-  const int64_t n0 = st->ntouched, nx = min(st->nxovf, D.KCAP);
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nx; i += (int64_t)gridDim.x * blockDim.x) {
-    const int2 e = D.xovf[i];  // the side list's (key, delta) as records
-    const int32_t d = e.x;
-    DeltaRec r;
-    r.h1 = D.kh1[d];
-    r.h2 = D.kh2[d];
-    r.len = D.klen[d];
-    r.idL = D.krep[3 * (int64_t)d];
-    r.g = D.krep[3 * (int64_t)d + 1];
-    r.idR = D.krep[3 * (int64_t)d + 2];
-    r.delta = e.y;
-    r.pad = d + 1;
-    if (n0 + i < cap) out[n0 + i] = r;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    const int64_t n = n0 + nx;
-    d_count[0] = n;
-    if (n > cap) set_error(D, GEOBPE_ECAPACITY, -30);
-    st->nxovf = 0;
-  }
-}
-
 __global__ void k_export_fin(Dev D, int64_t* d_count, int64_t cap) {
   State* st = D.st;
   const int64_t n = st->ntouched;
@@ -1130,7 +1102,8 @@ __global__ __launch_bounds__(ABLOCK) void k_import(Dev D, const DeltaRec* in, in
 // no LDS aggregation to gain), with the hot-list crossing check; a found key's
 // content joins this workgroup's check region (verified by the next k_mark, as
 // k_apply's finds are).  Also opens the next delta epoch (the export consumed it).
-__global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* in, int world, int64_t capf, int myrank) {
+__global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* in, int world, int64_t capf, int myrank,
+                                                        int64_t* own_head) {
   __shared__ int32_t s_ns, s_chk, s_bad;
   __shared__ int64_t s_cnt[PIPE_MAX_WORLD + 1];
   __shared__ HotApp hot;
@@ -1154,15 +1127,17 @@ __global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* i
     if (blockIdx.x == 0) {
       st->slot_max = mx;  // sizes the host's next slots
       st->ntouched = 0;   // the export of this merge consumed the touched list
+      st->nxovf = 0;      // (k_commit turned k_find's side list into records)
       st->epoch += 1;
     }
   }
   hot_init(hot);
   __syncthreads();
-  if (s_bad) {
+  if (s_bad) {  // (this rank's slot header keeps the stalled merge's count for the full re-exchange)
     if (blockIdx.x == 0 && threadIdx.x == 0) st->stall = 1;
     return;
   }
+  if (own_head && blockIdx.x == 0 && threadIdx.x == 0) *own_head = 0;  // (the middle regime counts into it)
   const int32_t th = st->theta;
   const int64_t n = s_cnt[world];
   const int64_t E = (n + gridDim.x - 1) / gridDim.x;

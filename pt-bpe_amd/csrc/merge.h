@@ -721,12 +721,22 @@ __device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nb
   return (int64_t)nba * nba * SK + (i - nE);
 }
 
+// a count change k_commit could not stage: a record (pipelined), the global count or the delta
+__device__ inline void commit_add(const Dev& D, int32_t d, int32_t v, bool tod) {
+  if (tod && D.xrec)
+    rec_add(D, d, v);
+  else
+    global_add(D, d, v, tod);
+}
+
 // a record whose key did not fit the dedupe table: resolved and counted on its own
 __device__ __attribute__((always_inline)) inline void commit_fallback(const Dev& D, CommitLds& S, HotApp& hot, const KRec& k, bool tod, int32_t th) {
   const int32_t d = commit_resolve(D, S, k);
   if (d >= 0) {
     atomicAdd(&S.fbn, k.n);
-    if (tod)
+    if (tod && D.xrec)
+      rec_add(D, d, k.n);
+    else if (tod)
       global_add(D, d, k.n, true);
     else
       count_add_hot(D, hot, d, k.n, th);
@@ -762,18 +772,23 @@ __device__ __attribute__((always_inline)) inline void commit_publish(const Dev& 
 }
 
 // pipelined exchange: this owner's delta records -- every resolved key with its
-// occurrence total, every decremented key with its (negative) total -- straight
-// into the rank's slot buffer, one reservation per workgroup.  The import adds every
-// rank's records (this rank's included) to the replicated counts.
+// occurrence total, every decremented key with its (negative) total, and its share of
+// k_find's side list -- straight into the rank's slot, one reservation per workgroup on
+// the slot header's count (final when k_commit ends: no header pass).  The import adds
+// every rank's records (this rank's included) to the replicated counts.
 __device__ void commit_export(const Dev& D, CommitLds& S) {
   __shared__ unsigned long long s_xb;
   const int t = threadIdx.x;
+  const int64_t nx = min(D.st->nxovf, D.KCAP);  // (k_find's; k_commit adds none)
+  const int64_t x0 = nx * blockIdx.x / gridDim.x, x1 = nx * (blockIdx.x + 1) / gridDim.x;
   int32_t c = 0;
   for (int32_t s = t; s < CKC; s += ABLOCK) c += S.ckey[s] != 0 && S.cid[s] >= 0;
   for (int i = t; i < AggT<12>::N; i += ABLOCK) c += S.u.agg.key[i] >= 0 && S.u.agg.val[i] != 0;
+  for (int64_t i = x0 + t; i < x1; i += ABLOCK) c++;
   int32_t tot;
   const int32_t ex = block_excl_scan(c, &tot, S.red);
-  if (t == 0) s_xb = tot ? atomicAdd((unsigned long long*)&D.st->ntouched, (unsigned long long)tot) : 0ULL;
+  if (t == 0)
+    s_xb = tot ? atomicAdd((unsigned long long*)(D.xcnt ? D.xcnt : &D.st->ntouched), (unsigned long long)tot) : 0ULL;
   __syncthreads();
   int64_t j = (int64_t)s_xb + ex;
   for (int32_t s = t; s < CKC; s += ABLOCK) {
@@ -791,9 +806,7 @@ __device__ void commit_export(const Dev& D, CommitLds& S) {
     if (j < D.xcap) D.xrec[j] = r;
     j++;
   }
-  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
-    const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
-    if (k < 0 || v == 0) continue;
+  auto put_id = [&](int32_t k, int32_t v) {
     DeltaRec r;
     r.h1 = D.kh1[k];
     r.h2 = D.kh2[k];
@@ -805,7 +818,16 @@ __device__ void commit_export(const Dev& D, CommitLds& S) {
     r.pad = k + 1;
     if (j < D.xcap) D.xrec[j] = r;
     j++;
+  };
+  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+    const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
+    if (k >= 0 && v != 0) put_id(k, v);
   }
+  for (int64_t i = x0 + t; i < x1; i += ABLOCK) {
+    const int2 e = D.xovf[i];
+    put_id(e.x, e.y);
+  }
+  if (t == 0 && (int64_t)s_xb + tot > D.xcap) set_error(D, GEOBPE_ECAPACITY, -30);
 }
 
 __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par) {
@@ -944,7 +966,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   } while (0)
   const bool mine0 = lane_ok && k0 < min(cK, SK);
   if (mine0) COMMIT_INSERT(r0);
-  if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) global_add(D, d0.x, d0.y, tod);
+  if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
   const int32_t nE = s_preE[nba], nF = s_preF[nba], nKO = S.nKO;
   for (int32_t i = t; i < nE + nKO; i += ABLOCK) {  // extras, then the overflow list
     const int64_t at = extra_at(D, s_preE, nba, j, PER, nE, i);
@@ -954,7 +976,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   for (int32_t i = t; i < nF; i += ABLOCK) {
     const int32_t ww = seg_of(s_preF, nba, i);
     const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
-    if (!agg_stage(S.u.agg, x.x, x.y)) global_add(D, x.x, x.y, tod);
+    if (!agg_stage(S.u.agg, x.x, x.y)) commit_add(D, x.x, x.y, tod);
   }
   __syncthreads();
   dbg_stamp(D, 2);

@@ -40,6 +40,7 @@ struct MidFindLds {
   HotApp hot;
   int32_t red[ABLOCK / 64];
   int32_t nocc, nm, chk;
+  int64_t xbase;
 };
 
 struct MidAppLds {
@@ -81,9 +82,14 @@ __device__ inline void mid_pair(const Dev& D, const MidCtx& F, int32_t target, i
 
 // multi-rank (D.xrec set, the pipelined exchange): count changes go out as delta records
 // (the import adds every rank's, this rank's included, with the hot-list check); the
-// record carries this rank's key id (pad = id + 1: no probe on import)
-__device__ inline void mid_emit(const Dev& D, u64 h1, u64 h2, int32_t len, int32_t idL, int32_t g, int32_t idR,
-                                int32_t delta, int32_t d) {
+// record carries this rank's key id (pad = id + 1: no probe on import).  Records are
+// reserved per workgroup phase (mid_reserve) where the count is known, one wave at a time
+// only on the rare paths (a run's later occurrences, a full LDS table).
+__device__ inline unsigned long long* mid_xcnt(const Dev& D) {
+  return (unsigned long long*)(D.xcnt ? D.xcnt : &D.st->ntouched);
+}
+__device__ inline void mid_put(const Dev& D, int64_t j, u64 h1, u64 h2, int32_t len, int32_t idL, int32_t g,
+                               int32_t idR, int32_t delta, int32_t d) {
   DeltaRec r;
   r.h1 = h1;
   r.h2 = h2;
@@ -93,15 +99,35 @@ __device__ inline void mid_emit(const Dev& D, u64 h1, u64 h2, int32_t len, int32
   r.idR = idR;
   r.delta = delta;
   r.pad = d + 1;
-  const int64_t j = wave_reserve64((unsigned long long*)&D.st->ntouched);
   if (j < D.xcap)
     D.xrec[j] = r;
   else
     set_error(D, GEOBPE_ECAPACITY, -72);
 }
+__device__ inline void mid_put_id(const Dev& D, int64_t j, int32_t d, int32_t delta) {
+  mid_put(D, j, D.kh1[d], D.kh2[d], D.klen[d], D.krep[3 * (int64_t)d], D.krep[3 * (int64_t)d + 1],
+          D.krep[3 * (int64_t)d + 2], delta, d);
+}
+__device__ inline void mid_emit(const Dev& D, u64 h1, u64 h2, int32_t len, int32_t idL, int32_t g, int32_t idR,
+                                int32_t delta, int32_t d) {
+  const u64 m = __ballot(1);
+  const int lane = wave_lane();
+  const int leader = __ffsll((long long)m) - 1;
+  unsigned long long base = 0;
+  if (lane == leader) base = atomicAdd(mid_xcnt(D), (unsigned long long)__popcll(m));
+  base = __shfl(base, leader, 64);
+  mid_put(D, (int64_t)base + __popcll(m & ((1ULL << lane) - 1)), h1, h2, len, idL, g, idR, delta, d);
+}
 __device__ inline void mid_emit_id(const Dev& D, int32_t d, int32_t delta) {
   mid_emit(D, D.kh1[d], D.kh2[d], D.klen[d], D.krep[3 * (int64_t)d], D.krep[3 * (int64_t)d + 1],
            D.krep[3 * (int64_t)d + 2], delta, d);
+}
+// n records of this workgroup (block-uniform call; n from LDS): the base index, one atomic
+__device__ inline int64_t mid_reserve(const Dev& D, int64_t* s_base, int32_t n) {
+  __syncthreads();
+  if (threadIdx.x == 0) *s_base = n > 0 ? (int64_t)atomicAdd(mid_xcnt(D), (unsigned long long)n) : 0;
+  __syncthreads();
+  return *s_base;
 }
 // -v on key d: a count atomic, or a record (multi-rank)
 __device__ inline void mid_dec(const Dev& D, int32_t d, int32_t v) {
@@ -392,6 +418,7 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
     __syncthreads();
     if (c0 == lo) dbg_stamp(D, 16);
     const int32_t nocc = S.nocc;
+    const int64_t xb = D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
     for (int32_t q = t; q < nocc; q += ABLOCK) {
       const int32_t s = S.occ[q];
       const int4 rp = S.rep[s];
@@ -399,7 +426,10 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
       const u64 h1 = S.h1[s], h2 = S.h2[s];
       const int32_t d = mid_resolve(D, h1, h2, rp.x, &claimed);
       S.did[s] = d;
-      if (d < 0) continue;
+      if (d < 0) {
+        if (D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, 0, -1);  // (no-op record)
+        continue;
+      }
       if (claimed) {
         claim_payload(D, d, h1, h2, rp.x, rp.y, rp.z, rp.w);
         klist_put(D, wave_reserve64((unsigned long long*)&st->U), d);
@@ -408,7 +438,7 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
       if (D.xrec)
-        mid_emit(D, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
+        mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
       else
         count_add_hot(D, S.hot, d, S.cnt[s], F.th);
     }
@@ -433,14 +463,34 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
   }
   dbg_stamp(D, 12);
   // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
-  for (int i = t; i < AggT<11>::N; i += ABLOCK) {
-    const int32_t k = S.agg.key[i], v = S.agg.val[i];
-    if (k >= 0 && v != 0) mid_dec(D, k, v);
+  if (D.xrec) {  // as records: the nonzero slots, compacted behind one reservation
+    constexpr int PER = AggT<11>::N / ABLOCK;
+    static_assert(AggT<11>::N % ABLOCK == 0, "agg slots per thread");
+    int32_t n = 0;
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int i = t + u * ABLOCK;
+      n += S.agg.key[i] >= 0 && S.agg.val[i] != 0;
+    }
+    const int32_t own = t == 0 && S.nm ? 1 : 0;
+    int32_t tot;
+    const int32_t ex = block_excl_scan(n + own, &tot, S.red);
+    int64_t j = mid_reserve(D, &S.xbase, tot) + ex;
+    if (own) mid_put_id(D, j++, F.W, -S.nm);
+#pragma unroll
+    for (int u = 0; u < PER; u++) {
+      const int i = t + u * ABLOCK;
+      const int32_t k = S.agg.key[i], v = S.agg.val[i];
+      if (k >= 0 && v != 0) mid_put_id(D, j++, k, v);
+    }
+  } else {
+    for (int i = t; i < AggT<11>::N; i += ABLOCK) {
+      const int32_t k = S.agg.key[i], v = S.agg.val[i];
+      if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
+    }
+    if (t == 0 && S.nm) atomicAdd(&D.count[F.W], -S.nm);
   }
-  if (t == 0 && S.nm) {
-    mid_dec(D, F.W, -S.nm);
-    atomicAdd((unsigned long long*)&D.log[sel.iter].nmerged, (unsigned long long)S.nm);
-  }
+  if (t == 0 && S.nm) atomicAdd((unsigned long long*)&D.log[sel.iter].nmerged, (unsigned long long)S.nm);
   hot_flush(D, S.hot);  // (syncs the workgroup first)
   if (t == 0) D.chkcnt[w] = min(S.chk, (int32_t)D.RC);
   dbg_stamp(D, 13);
