@@ -101,7 +101,7 @@ struct State {
   int32_t place_par, pad3;    // launch parity of the merge k_place writes out (-1: none)
   int64_t stat_krec, stat_drec, stat_keys;
   int64_t nxovf;  // entries of Dev.xovf (pipelined exchange)  // k_commit work (profiling only): key records, decrement records, keys
-  int64_t slot_max;    // pipelined exchange: the largest slot count of the last import (every rank)
+  int64_t slot_max;    // pipelined exchange: the largest slot count of the imports since the last poll (every rank)
   // late-merge path (tail.h): per-key posting lists in one pool
   int64_t kpool_used;  // pool entries handed out since the last list build
   int32_t kp_valid;    // 1: the lists hold every live pair (0: rebuild before the next tail launch)

@@ -415,9 +415,13 @@ int tail_alloc(geobpe_ctx* c) {
 void tail_build(geobpe_ctx* c) {
   flush_place(c);
   Timed t(c, "tail_build");
-  hipLaunchKernelGGL(k_kp_reset, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
-  hipLaunchKernelGGL(k_kp_count, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
-  hipLaunchKernelGGL(k_kp_alloc, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  if (c->distributed) {  // (a rank's counts are global: count its own live pairs)
+    hipLaunchKernelGGL(k_kp_reset, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+    hipLaunchKernelGGL(k_kp_count, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  } else {
+    hipMemsetAsync(&c->D.st->kpool_used, 0, 8, c->stream);
+  }
+  hipLaunchKernelGGL(k_kp_alloc, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, c->distributed ? 0 : 1);
   hipLaunchKernelGGL(k_kp_fill, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
   hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, c->D);  // (nothing pending)
 }
@@ -1201,6 +1205,7 @@ int geobpe_pipeline_poll(geobpe_ctx* c, int64_t* h_out4) {
   h_out4[1] = c->h_state->iter;
   h_out4[2] = c->h_state->done;
   h_out4[3] = c->h_state->slot_max;
+  HIPCHK(c, hipMemsetAsync(&c->D.st->slot_max, 0, 8, c->stream));  // (the next window's largest)
   return 0;
 }
 
@@ -1975,14 +1980,22 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
   while (!rc && done < n_merges) {
     // the middle regime once this rank's share of a merge is small (a poll is a quiescent
     // point: the lists are built, or rebuilt after an iteration stalled on them)
+    int64_t win = ahead;
     if (!c->mid_on && mid_enabled(c) && c->h_state->iter > 0) {
       LogRec lr;
       HIPCHK(c, hipMemcpy(&lr, c->D.log + (c->h_state->iter - 1), sizeof lr, hipMemcpyDeviceToHost));
-      if (lr.nmerged <= c->mid_thresh) c->mid_on = true;
+      if (lr.nmerged <= c->mid_thresh) {
+        c->mid_on = true;
+        // the middle regime's records are per (workgroup, key), not per owner and key: a
+        // merge of the same size sends up to ~4x as many -- a slot that small would stall
+        if (!c->x_fixed) capf = std::min(CAP_MAX, 4 * capf);
+      } else if (lr.nmerged <= 2 * c->mid_thresh) {
+        win = std::min<int64_t>(win, 8);  // (close: poll sooner)
+      }
     }
     if (c->mid_on && (rc = mid_prepare(c))) break;
     const int64_t slot = (1 + capf) * REC;
-    const int64_t k = std::min(ahead, n_merges - done);  // an iteration merges at most once
+    const int64_t k = std::min(win, n_merges - done);  // an iteration merges at most once
     for (int64_t i = 0; i < k && !rc; i++) {
       if ((rc = geobpe_pipeline_iter(c, c->x_pbuf, c->x_pcap))) break;
       if ((rc = x_allgather(c, c->x_pbuf, c->x_gath, slot))) break;

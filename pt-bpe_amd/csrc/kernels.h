@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* i
     s_ns = 0;
     s_chk = min(D.chkcnt[blockIdx.x], (int32_t)D.RC);  // after k_apply's finds
     if (blockIdx.x == 0) {
-      st->slot_max = mx;  // sizes the host's next slots
+      st->slot_max = max(st->slot_max, mx);  // sizes the host's next slots (the poll resets it)
       st->ntouched = 0;   // the export of this merge consumed the touched list
       st->nxovf = 0;      // (k_commit turned k_find's side list into records)
       st->epoch += 1;

@@ -403,8 +403,10 @@ __global__ __launch_bounds__(BLOCK) void k_kp_count(Dev D) {
 }
 
 // list space: n + n/2 + 4 entries per key with live pairs (growth room), one pool
-// reservation per round of the block
-__global__ __launch_bounds__(BLOCK) void k_kp_alloc(Dev D) {
+// reservation per round of the block.  from_count: n is the key's count (one rank: the
+// count of a key IS its number of live pair slots, k_recount's invariant -- no counting
+// pass); else k_kp_count's n (a rank's counts are global)
+__global__ __launch_bounds__(BLOCK) void k_kp_alloc(Dev D, int from_count) {
   __shared__ int32_t s_red[BLOCK / 64];
   __shared__ int64_t s_base;
   const int64_t U = min(D.st->U, D.KCAP);
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(BLOCK) void k_kp_alloc(Dev D) {
   for (int64_t i0 = lo; i0 < hi; i0 += BLOCK) {  // block-uniform
     const int64_t i = i0 + threadIdx.x;
     const int32_t d = i < hi ? D.klist[i] : -1;
-    const int32_t n = d >= 0 ? D.kp_n[d] : 0;
+    const int32_t n = d >= 0 ? max(from_count ? D.count[d] : D.kp_n[d], 0) : 0;
     const int32_t cap = n > 0 ? n + (n >> 1) + 4 : 0;
     int32_t tot;
     const int32_t ex = block_excl_scan(cap, &tot, s_red);

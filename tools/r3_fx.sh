@@ -14,6 +14,7 @@ trap 'kill $HB' EXIT
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 600 --timeout-method thread -k "$K" > $OUT/pytest.txt 2>&1; rc=$?
 tail -3 $OUT/pytest.txt
 [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 bench.py > $OUT/bench_default.json 2> $OUT/bench_default.err && echo DEF_OK && \
 timeout -k 10 240 python3 bench.py --gpus 1 --steps 20 --warmup 5 --force-exchange > $OUT/bench_fx_window.json 2> $OUT/bench_fx_window.err && echo FXW_OK && \
 timeout -k 10 300 python3 bench.py --gpus 1 --force-exchange > $OUT/bench_fx_default.json 2> $OUT/bench_fx_default.err && echo FXD_OK && \
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/p -o run -- python3 bench.py --gpus 1 --force-exchange > $OUT/bench_prof.json 2> $OUT/bench_prof.err && echo PROF_OK
