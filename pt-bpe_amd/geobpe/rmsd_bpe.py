@@ -558,7 +558,12 @@ class RmsdBPE:
         sup = self.rmsd_super_res
         coords = self._span_coords(occ, sup)
         act = [coords[i] for i in active]
-        medoids = _rmsd.k_medoids(act, self.num_partitions[size], rng=self.rng, device=self.device)
+        k = self.num_partitions[size]
+        medoids = _rmsd.k_medoids(act, k, rng=self.rng, device=self.device)
+        if len(medoids) != k:
+            # the reference stores the medoids in a memmap of num_partitions[size] entries
+            # (bpe.py:299-300): fewer structures than partitions fail the write there
+            raise ValueError(f"could not broadcast input array from shape ({len(medoids)},) into shape ({k},)")
         assign = self._assign(coords, [act[m] for m in medoids])
         key = RES_SPHERE_KEY[size]
         self._sphere_dict[key] = []

@@ -221,8 +221,15 @@ def run_and_compare(name, device=False):
     return bpe
 
 
+# BASELINE configs[4]'s pareto setting (README.md:48: --bins 1-500, p = 0, the nine-size
+# --num-p schedule, 500 structures, free bonds, rmsd_super_res, glue opt "all" with prior 1
+# every step) on 120 synthetic chains; on config 1's 71 PDB chains the reference itself stops
+# in initialize() (num_partitions[2] = 100 medoids of 71 structures), see below
+PARETO = ["gl_syn120_pareto"]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("name", NAMES + ["gl_pdb72_readme"])
+@pytest.mark.parametrize("name", NAMES + ["gl_pdb72_readme"] + PARETO)
 def test_rmsd_mode_glue_opt_device_matches_reference(name):
     bpe = run_and_compare(name, device=True)
     assert bpe.glue_calls >= 2  # glue_opt_all and at least one re-optimisation in step()
@@ -257,6 +264,35 @@ def host_glue(monkeypatch):
 @pytest.mark.parametrize("name", NAMES)
 def test_rmsd_mode_glue_opt_host_logic_matches_reference(name, host_glue):
     run_and_compare(name)
+
+
+@pytest.mark.skipif(os.environ.get("GEOBPE_SLOW_TESTS") != "1", reason="~20 min on one CPU core (GEOBPE_SLOW_TESTS=1)")
+@pytest.mark.parametrize("name", PARETO)
+def test_rmsd_mode_pareto_host_logic_matches_reference(name, host_glue):
+    """The pareto fixture exactly, with the torch optimiser restatement on the CPU (600 chain
+    optimisations): passed in the build container (19.5 min); the device run of the same
+    fixture is in the GPU suite."""
+    run_and_compare(name)
+
+
+@pytest.mark.gpu
+def test_pareto_on_config1_raises_like_reference():
+    """The pareto schedule on config 1's PDB chains (gl_pdb72_pareto): the reference's
+    _init_res_tokens writes num_partitions[size] medoids into a memmap of that size and fails
+    with ValueError when a size has fewer structures (bpe.py:300).  (GPU: the sizes before
+    the failing one run their k-medoids first -- 10 min with the CPU stand-ins.)"""
+    from geobpe.bpe import BPE
+    meta, arrs = _load("gl_pdb72_pareto")
+    assert meta["raised"]["stage"] == "initialize" and meta["raised"]["type"] == "ValueError"
+    corpus = {k: arrs[k] for k in COLS + ["row_off"]}
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()},
+              rmsd_partition_min_size=meta["rmsd_partition_min_size"], rmsd_super_res=meta["rmsd_super_res"],
+              num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta["std_bonds"],
+              glue_opt=True, glue_opt_prior=meta["glue_opt_prior"], glue_opt_every=meta["glue_opt_every"],
+              glue_opt_method=meta["glue_opt_method"], seed=meta["rng_seed"])
+    with pytest.raises(ValueError):
+        bpe.initialize()
 
 
 def test_each_method_raises_like_reference(host_glue):
