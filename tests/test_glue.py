@@ -32,7 +32,13 @@ NAMES = ["gl_all_p0", "gl_all_p0_prior"]
 # of glues snap to the reference's bin; final loss within -1.9 % .. +1.4 % of the reference's.
 GLUE_TOL_MAX = 0.1   # rad, any glue
 GLUE_LOSS = 0.05     # relative, final loss of a chain
-GLUE_FLIPS = 0.05    # share of glues allowed to snap to a neighbouring bin
+# Snapped glues in another bin than the reference's, on a coarse grid (bins >= 0.05 rad):
+# observed 1.5 % (gl_all_p0, 2 of 135), <= 0.3 % (gl_pdb72_readme, 50 bins); bound 2x.  On a
+# fine grid a bin is narrower than the drift (500 bins: 0.0054 rad; gl_syn120_pareto: 8.5 % of
+# phi glues in another bin, max 0.038 rad), so the bound is in radians there: at most 2 % of
+# glues further than GLUE_FINE_RAD (~ the drift's p99) and none past GLUE_TOL_MAX.
+GLUE_FLIPS = 0.03
+GLUE_FINE_RAD = 0.02
 
 
 def _load(name):
@@ -132,7 +138,9 @@ GLUE_COLS = ["omega", "C:1N:1CA", "phi"]
 
 
 def _glue_close(a, b, thr, what):
-    """Glue columns on the device: equal, except a few values one bin away."""
+    """Glue columns on the device: equal, except a few values in another bin -- one bin away
+    on a coarse grid, within the optimiser's drift (GLUE_TOL_MAX rad) on a fine one (500
+    bins: 0.0054 rad each)."""
     bad = ~((a == b) | (np.isnan(a) & np.isnan(b)))
     if not bad.any():
         return 0
@@ -140,8 +148,16 @@ def _glue_close(a, b, thr, what):
     width = float(np.max(e[:, 1] - e[:, 0]))
     d = np.abs(a[bad] - b[bad])
     d = np.minimum(d, 2 * np.pi - d)  # angles: the first and last bins are neighbours on the circle
-    assert np.all(d <= 1.01 * width), f"{what}: a glue more than one bin away"
-    assert bad.sum() <= max(1, GLUE_FLIPS * len(a)), f"{what}: {int(bad.sum())} of {len(a)} glues in another bin"
+    n = int(np.sum(~np.isnan(b)))
+    print(f"{what}: {int(bad.sum())} of {n} glues in another bin ({bad.sum() / max(n, 1):.2%}), "
+          f"max {d.max():.3g} rad = {d.max() / width:.1f} bins")
+    if width >= 0.05:
+        assert np.all(d <= 1.01 * width), f"{what}: a glue more than one bin away"
+        assert bad.sum() <= max(1, GLUE_FLIPS * n), f"{what}: {int(bad.sum())} of {n} glues in another bin"
+    else:
+        assert np.all(d <= GLUE_TOL_MAX), f"{what}: a glue past the drift bound"
+        far = int(np.sum(d > GLUE_FINE_RAD))
+        assert far <= max(1, 0.02 * n), f"{what}: {far} of {n} glues further than {GLUE_FINE_RAD} rad"
     return int(bad.sum())
 
 
