@@ -265,7 +265,6 @@ __device__ inline void cb_push(const Dev& D, ClaimBuf& cb, int32_t slot) {
     cb.slot[j] = slot;
   } else {  // rare: listed right away
     klist_put(D, (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL), slot);
-    atomicAdd((unsigned long long*)&D.st->nkeys, 1ULL);
   }
 }
 __device__ inline void cb_flush(const Dev& D, ClaimBuf& cb) {
@@ -274,7 +273,6 @@ __device__ inline void cb_flush(const Dev& D, ClaimBuf& cb) {
   const int32_t n = min(cb.n, BIN_CLAIM_BUF);
   if (threadIdx.x == 0 && n) {
     s_base = (int64_t)atomicAdd((unsigned long long*)&D.st->U, (unsigned long long)n);
-    atomicAdd((unsigned long long*)&D.st->nkeys, (unsigned long long)n);
   }
   __syncthreads();
   for (int32_t j = threadIdx.x; j < n; j += blockDim.x) klist_put(D, s_base + j, cb.slot[j]);

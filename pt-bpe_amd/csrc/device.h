@@ -253,6 +253,7 @@ struct Dev {
   int64_t KPOOL;
   int4* TM;       // merged occurrences {a, ya, b, c}
   int2* TH;       // new pairs {slot, key} (mid.h: two buffers of THcap, by launch parity)
+  int4* mcnt;     // mid.h: per find workgroup {TM count, TH count, merged, -} by parity [2][NBA_MAX]
   int4* TS;       // posting entries past a list's capacity {key, position, slot}
   int32_t* TR;    // keys whose list is regrown
   NewPair* TK;    // keys found (not claimed): EHASH check
@@ -353,6 +354,12 @@ __device__ inline int32_t wave_excl_scan(int32_t v, int32_t& total) {
   }
   total = __shfl(x, 63, 64);
   return x - v;
+}
+
+__device__ inline int32_t wave_sum(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
 }
 
 __device__ inline int32_t wave_max(int32_t v) {

@@ -399,13 +399,14 @@ int tail_alloc(geobpe_ctx* c) {
   if (c->tail_ready) return 0;
   Dev& D = c->D;
   D.KPOOL = std::min<int64_t>(6 * c->R + 65536, INT32_MAX - 1);
-  D.TMcap = c->R / 2 + 1024;
-  D.THcap = c->R + 2048;
+  D.TMcap = c->R / 2 + 1024 + MSEG_TM;  // (mid.h: the find workgroups' segments, then the spill list)
+  D.THcap = c->R + 2048 + MSEG_TH;
   int rc;
   // (zero: a key claimed after the list build starts with an empty list of capacity 0)
   if ((rc = dalloc(c, &D.kp_off, D.HC, 0)) || (rc = dalloc(c, &D.kp_n, D.HC, 0)) || (rc = dalloc(c, &D.kp_cap, D.HC, 0)) ||
-      (rc = dalloc(c, &D.kpool, D.KPOOL)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, 2 * D.THcap)) ||
-      (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)))
+      (rc = dalloc(c, &D.kpool, D.KPOOL, 0xFF)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, 2 * D.THcap)) ||
+      (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)) ||
+      (rc = dalloc(c, &D.mcnt, 2 * NBA_MAX, 0)))
     return rc;
   c->tail_ready = true;
   return 0;
@@ -457,7 +458,7 @@ int tail_run(geobpe_ctx* c, int64_t n) {
 
 // (multi-rank: inside the pipelined exchange only -- its iterations write delta records)
 bool mid_enabled(const geobpe_ctx* c) {
-  return c->mid_thresh > 0 && !c->replay && (!c->distributed || c->pipelined);
+  return c->mid_thresh > 0 && !c->replay && (!c->distributed || c->pipelined) && c->nba > MID_APP;
 }
 
 // the next batch of iterations before the regime switches are checked: long while the
@@ -1267,6 +1268,9 @@ int64_t geobpe_vocab_count(geobpe_ctx* c) {
 
 int64_t geobpe_num_keys(geobpe_ctx* c) {
   if (!c || !c->keys_ready) return 0;
+  if (sync_state(c)) return -1;
+  hipMemsetAsync(&c->D.st->nkeys, 0, 8, c->stream);
+  hipLaunchKernelGGL(k_count_keys, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
   if (sync_state(c)) return -1;
   return c->h_state->nkeys;
 }

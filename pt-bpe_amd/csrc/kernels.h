@@ -209,7 +209,6 @@ __device__ inline void note_claim(const Dev& D, int32_t* s_ns, int32_t slot) {
     D.ns[(int64_t)blockIdx.x * D.RC + j] = slot;
   else {  // rare: listed right away
     klist_put(D, (int64_t)atomicAdd((unsigned long long*)&D.st->U, 1ULL), slot);
-    atomicAdd((unsigned long long*)&D.st->nkeys, 1ULL);
   }
 }
 
@@ -234,7 +233,6 @@ __device__ inline void close_claims(const Dev& D, int32_t* s_ns) {
   const int32_t n = min(*s_ns, (int32_t)D.RC);
   if (threadIdx.x == 0) {
     s_base = n ? (int64_t)atomicAdd((unsigned long long*)&D.st->U, (unsigned long long)n) : 0;
-    if (n) atomicAdd((unsigned long long*)&D.st->nkeys, (unsigned long long)n);
   }
   __syncthreads();
   const int32_t* reg = D.ns + (int64_t)blockIdx.x * D.RC;
@@ -769,6 +767,23 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
   if (rec) S.nt = 0;
   dbg_stamp(D, 21);
   const int32_t gm = block_max(m, s_red);
+  // the payload of a key at the maximum, loaded by its thread while the ties are collected:
+  // when one key holds the maximum (nt == 1, the common case) that thread publishes without
+  // another round trip
+  int32_t pL = 0, pg = 0, pR = 0, pwl = 0, pkn = 0, pko = 0;
+  u64 pw1 = 0, pw2 = 0;
+  if (mkey >= 0 && m == gm && mcnt == 1) {
+    pL = D.krep[3 * (int64_t)mkey];
+    pg = D.krep[3 * (int64_t)mkey + 1];
+    pR = D.krep[3 * (int64_t)mkey + 2];
+    pw1 = D.kh1[mkey];
+    pw2 = D.kh2[mkey];
+    pwl = D.klen[mkey];
+    if (D.kp_n) {
+      pkn = ldc<COH>(&D.kp_n[mkey]);
+      pko = D.kp_off[mkey];
+    }
+  }
   dbg_stamp(D, 22);
   const bool hot = gm < th || (n > CL_MIN_SHRINK && (int64_t)gm >= 4 * (int64_t)th);
   if (hot && th <= 1 && gm == 0) {  // every key with count >= 1 is listed: nothing left
@@ -861,10 +876,12 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
       }
     W = block_min_key(D, best, S.idx, jb);
   }
-  if (rec) {
-    const int32_t L = D.krep[3 * (int64_t)W], g = D.krep[3 * (int64_t)W + 1], Rr = D.krep[3 * (int64_t)W + 2];
-    const u64 w1 = D.kh1[W], w2 = D.kh2[W];
-    const int32_t wl = D.klen[W];
+  const bool solo = nt == 1;  // (then exactly one thread has m == gm with mcnt == 1: it listed W)
+  if (solo ? (m == gm && mcnt == 1) : rec) {
+    const int32_t L = solo ? pL : D.krep[3 * (int64_t)W], g = solo ? pg : D.krep[3 * (int64_t)W + 1],
+                  Rr = solo ? pR : D.krep[3 * (int64_t)W + 2];
+    const u64 w1 = solo ? pw1 : D.kh1[W], w2 = solo ? pw2 : D.kh2[W];
+    const int32_t wl = solo ? pwl : D.klen[W];
     D.vh1[K] = w1;
     D.vh2[K] = w2;
     D.vlen[K] = wl;
@@ -892,8 +909,8 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
     o.wl = wl;
     o.wfp = key_fp(W);
     if (D.kp_n) {  // the winner's posting list (per-key lists: tail.h / mid.h)
-      o.kpn = ldc<COH>(&D.kp_n[W]);
-      o.kpoff = D.kp_off[W];
+      o.kpn = solo ? pkn : ldc<COH>(&D.kp_n[W]);
+      o.kpoff = solo ? pko : D.kp_off[W];
     }
     o.widL = L;
     o.wg = g;
@@ -1225,6 +1242,17 @@ __global__ __launch_bounds__(BLOCK) void k_recount(Dev D) {
   __syncthreads();
   for (int i = threadIdx.x; i < Agg::N; i += blockDim.x)
     if (agg.key[i] >= 0) atomicAdd(&D.scratch[agg.key[i]], agg.val[i]);
+}
+
+// the number of keys (klist entries; chunk tails hold -1): counted when asked for, so
+// no claim anywhere touches a shared key counter
+__global__ __launch_bounds__(BLOCK) void k_count_keys(Dev D) {
+  const int64_t U = min(D.st->U, D.KCAP);
+  int32_t n = 0;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < U; i += (int64_t)gridDim.x * blockDim.x)
+    n += D.klist[i] >= 0;
+  n = wave_sum(n);
+  if (wave_lane() == 0 && n) atomicAdd((unsigned long long*)&D.st->nkeys, (unsigned long long)n);
 }
 
 __global__ __launch_bounds__(BLOCK) void k_compare(Dev D) {

@@ -1104,7 +1104,6 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       }
       D.kchunk[2 * j] = s_kl[0] + n;
       D.kchunk[2 * j + 1] = s_kl[1];
-      atomicAdd((unsigned long long*)&st->nkeys, (unsigned long long)n);
     }
     __syncthreads();
     const int32_t* reg = D.ns + (int64_t)j * D.RC;

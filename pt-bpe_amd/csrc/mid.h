@@ -30,6 +30,17 @@ constexpr int MPK = 2048;   // appends: key grouping slots (LDS)
 constexpr int MID_APP = 32; // appending workgroups of k_mid_find (hash buckets of the keys)
 
 __device__ inline int2* mid_th(const Dev& D, int par) { return D.TH + (int64_t)par * D.THcap; }
+__device__ inline int32_t mid_G(const Dev& D) { return D.NBA - MID_APP; }  // find workgroups
+
+constexpr int MTM = 1024;  // k_mid_find: merged occurrences buffered per workgroup (LDS)
+constexpr int MTH = 2048;  // new pairs buffered per workgroup
+constexpr int MKL = 1024;  // claimed keys buffered per workgroup
+// The merged occurrences (TM) and new pairs (TH, per parity) of find workgroup w live in a
+// fixed segment [w * MTM, + D.mcnt[par][w].x) / [w * MTH, + .y) -- written without any
+// shared counter -- and past the segments in a spill list (st->mid_nm / mid_nh count it)
+// for what did not fit the LDS buffer
+constexpr int64_t MSEG_TM = (int64_t)NBA_MAX * MTM;
+constexpr int64_t MSEG_TH = (int64_t)NBA_MAX * MTH;
 
 struct MidFindLds {
   u64 key[MKC], h1[MKC], h2[MKC];
@@ -38,17 +49,30 @@ struct MidFindLds {
   int32_t occ[MKC];  // occupied slots, in insertion order
   AggT<11> agg;      // count decrements
   HotApp hot;
+  // the workgroup's list appends (merged occurrences, new pairs, claimed keys), written out
+  // behind one reservation each when the find ends -- a reservation per wave instruction
+  // on the shared counters put a returning global atomic on the walk's and the resolve's
+  // paths (past the buffers: the per-wave path)
+  int4 tm[MTM];
+  int2 th[MTH];
+  int32_t kl[MKL];
   int32_t red[ABLOCK / 64];
-  int32_t nocc, nm, chk;
-  int64_t xbase;
+  int32_t nocc, nm, chk, ntm, nth, nkl;
+  int64_t xbase, bk;
 };
 
+constexpr int MAE = 6144;  // appends: this bucket's entries kept from pass 1 (LDS)
+static_assert(MPK <= 2048, "an append entry packs its key slot in 11 bits");
+
 struct MidAppLds {
-  int32_t key[MPK], cnt[MPK], base[MPK], cur[MPK];
+  int32_t key[MPK], cnt[MPK], base[MPK], cur[MPK], off[MPK];
   int32_t occ[MPK];
+  int2 ent[MAE];  // this bucket's new pairs {slot, key}, then {slot, key slot << 21 | rank (as uint32)}
   int32_t big_old[TAIL_BIG], big_new[TAIL_BIG], big_pre[TAIL_BIG + 1];
+  int32_t pre[NBA_MAX + 1];  // prefix of the find workgroups' TH segment counts
   int32_t red[ABLOCK / 64];
-  int32_t nocc, nbig, full;
+  int32_t nocc, nbig, full, nent;
+  int64_t pbase;
 };
 
 // ---------------------------------------------------------------------- find
@@ -58,13 +82,29 @@ struct MidCtx {
   u64 pa1, pb1, pa2, pb2;
 };
 
+// one LDS slot per active lane, one LDS atomic per wave instruction
+__device__ inline int32_t lds_reserve(int32_t* n) {
+  const u64 m = __ballot(1);
+  const int lane = wave_lane();
+  const int leader = __ffsll((long long)m) - 1;
+  int32_t base = 0;
+  if (lane == leader) base = atomicAdd(n, __popcll(m));
+  base = __shfl(base, leader, 64);
+  return base + __popcll(m & ((1ULL << lane) - 1));
+}
+
 __device__ inline void mid_occ(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t a, int32_t ya, int32_t b,
                                int32_t c) {
-  const int64_t j = wave_reserve64((unsigned long long*)&D.st->mid_nm[F.par]);
-  if (j < D.TMcap)
-    D.TM[j] = make_int4(a, ya, b, c);
-  else
-    set_error(D, GEOBPE_ECAPACITY, -70);
+  const int32_t k = lds_reserve(&S.ntm);
+  if (k < MTM) {
+    S.tm[k] = make_int4(a, ya, b, c);
+  } else {
+    const int64_t j = MSEG_TM + wave_reserve64((unsigned long long*)&D.st->mid_nm[F.par]);
+    if (j < D.TMcap)
+      D.TM[j] = make_int4(a, ya, b, c);
+    else
+      set_error(D, GEOBPE_ECAPACITY, -70);
+  }
   atomicAdd(&S.nm, 1);
   if (D.ev) {  // merge events (record mode): (merge, left start, right start)
     const int64_t k = wave_reserve64(D.ev_n);
@@ -72,12 +112,60 @@ __device__ inline void mid_occ(const Dev& D, MidFindLds& S, const MidCtx& F, int
   }
 }
 
-__device__ inline void mid_pair(const Dev& D, const MidCtx& F, int32_t target, int32_t d) {
-  const int64_t j = wave_reserve64((unsigned long long*)&D.st->mid_nh[F.par]);
+__device__ inline void mid_pair(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t target, int32_t d) {
+  const int32_t k = lds_reserve(&S.nth);
+  if (k < MTH) {
+    S.th[k] = make_int2(target, d);
+    return;
+  }
+  const int64_t j = MSEG_TH + wave_reserve64((unsigned long long*)&D.st->mid_nh[F.par]);
   if (j < D.THcap)
     mid_th(D, F.par)[j] = make_int2(target, d);
   else
     set_error(D, GEOBPE_ECAPACITY, -71);
+}
+
+// a key this workgroup claimed joins klist
+__device__ inline void mid_claimed(const Dev& D, MidFindLds& S, int32_t d) {
+  const int32_t k = lds_reserve(&S.nkl);
+  if (k < MKL) {
+    S.kl[k] = d;
+    return;
+  }
+  klist_put(D, wave_reserve64((unsigned long long*)&D.st->U), d);
+}
+
+// the buffered appends out (block-uniform): TM / TH into this workgroup's segments and the
+// counts beside them, the claimed keys from this workgroup's klist chunk (a reservation only
+// when the chunk runs out) -- no shared counter, so the find workgroups ending together do not
+// queue on one address
+__device__ inline void mid_flush_lists(const Dev& D, MidFindLds& S, int par, int32_t w) {
+  State* st = D.st;
+  const int32_t t = threadIdx.x;
+  __syncthreads();
+  const int32_t a = min(S.ntm, MTM), b = min(S.nth, MTH), c = min(S.nkl, MKL);
+  if (t == 0) {
+    D.mcnt[par * NBA_MAX + w] = make_int4(a, b, S.nm, 0);
+    if (c) {
+      int64_t k0 = D.kchunk[2 * w], k1 = D.kchunk[2 * w + 1];
+      if (k1 - k0 < c) {
+        const int64_t sz = max((int64_t)KL_CHUNK, (int64_t)c);
+        k0 = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
+        k1 = k0 + sz;
+      }
+      D.kchunk[2 * w] = k0 + c;
+      D.kchunk[2 * w + 1] = k1;
+      S.bk = k0;
+    }
+  }
+  int4* tm = D.TM + (int64_t)w * MTM;
+  for (int32_t i = t; i < a; i += ABLOCK) tm[i] = S.tm[i];
+  int2* th = mid_th(D, par) + (int64_t)w * MTH;
+  for (int32_t i = t; i < b; i += ABLOCK) th[i] = S.th[i];
+  if (c) {
+    __syncthreads();
+    for (int32_t i = t; i < c; i += ABLOCK) klist_put(D, S.bk + i, S.kl[i]);
+  }
 }
 
 // multi-rank (D.xrec set, the pipelined exchange): count changes go out as delta records
@@ -137,6 +225,14 @@ __device__ inline void mid_dec(const Dev& D, int32_t d, int32_t v) {
     atomicAdd(&D.count[d], v);
 }
 
+// -1 on key d for a destroyed pair, staged in LDS.  One rank: not on W itself -- every pair
+// of W is merged or destroyed by the merge, so the find sets count[W] = 0 once instead of
+// every workgroup decrementing it
+__device__ inline void mid_dec_agg(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t d) {
+  if (!D.xrec && d == F.W) return;
+  if (!agg_stage(S.agg, d, -1)) mid_dec(D, d, -1);
+}
+
 // find-or-claim with the CAS as the first probe (an empty first slot is claimed, the key
 // itself is found, anything else probes on)
 __device__ inline int32_t mid_resolve(const Dev& D, u64 h1, u64 h2, int32_t len, bool* claimed) {
@@ -157,8 +253,7 @@ __device__ void mid_single(const Dev& D, MidFindLds& S, const MidCtx& F, u64 h1,
   if (d < 0) return;
   if (claimed) {
     claim_payload(D, d, h1, h2, len, idL, g, idR);
-    klist_put(D, wave_reserve64((unsigned long long*)&D.st->U), d);
-    atomicAdd((unsigned long long*)&D.st->nkeys, 1ULL);
+    mid_claimed(D, S, d);
   } else {
     emit_check(D, &S.chk, d, len, h1, h2);
   }
@@ -166,7 +261,7 @@ __device__ void mid_single(const Dev& D, MidFindLds& S, const MidCtx& F, u64 h1,
     mid_emit(D, h1, h2, len, idL, g, idR, 1, d);
   else
     count_add_hot(D, S.hot, d, 1, F.th);
-  mid_pair(D, F, target, d);
+  mid_pair(D, S, F, target, d);
 }
 
 struct MidHalf {
@@ -230,9 +325,9 @@ __device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g
   }
   const bool pN = p >= 0 && !pRight;
   mid_occ(D, S, F, g, F.wl | (tb.y & (int32_t)0xFFFF0000), b, c);
-  if (pkb >= 0 && !agg_stage(S.agg, pkb, -1)) mid_dec(D, pkb, -1);
+  if (pkb >= 0) mid_dec_agg(D, S, F, pkb);
   if (pN) {
-    if (!agg_stage(S.agg, tp.w, -1)) mid_dec(D, tp.w, -1);
+    mid_dec_agg(D, S, F, tp.w);
     combine_pw(l1, l2, glL, F.w1, F.w2, F.pa1, F.pb1, F.pa2, F.pb2, hl.h1, hl.h2);
     hl.len = tok_len(tp.y) + F.wl;
     hl.pkey = probe_key(hl.h1, hl.h2, hl.len);
@@ -265,7 +360,7 @@ __device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g
     const int32_t vc2 = c2i >= 0 ? max(tc2.x, 0) : 0;
     const u64 d1 = D.vh1[vc2], d2 = D.vh2[vc2];
     mid_occ(D, S, F, t, F.wl | (tb2.y & (int32_t)0xFFFF0000), b2, c2i);
-    if (pkb2 >= 0 && !agg_stage(S.agg, pkb2, -1)) mid_dec(D, pkb2, -1);
+    if (pkb2 >= 0) mid_dec_agg(D, S, F, pkb2);
     if (c2i >= 0) {
       MidHalf h;
       mid_right(D, F, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
@@ -298,7 +393,8 @@ __device__ inline int32_t mkc_slot(MidFindLds& S, const MidHalf& h, bool* ins) {
 }
 
 // find workgroup w of G (merge parity par, decision sel)
-__device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, int32_t G, MidFindLds& S) {
+__device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w,
+                                                                    int32_t G, MidFindLds& S) {
   State* st = D.st;
   const int32_t t = threadIdx.x;
   dbg_stamp(D, 10);
@@ -334,13 +430,19 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
     F.pa2 = D.pw2[nw + 1];
     F.pb2 = D.pw2[nw];
   }
-  // candidates: the winner's list, then the previous merge's new pairs (those of key W)
+  // candidates: share w of the winner's list, then the previous merge's new pairs of key W
+  // (find workgroup w's segment of them, and share w of the spill list)
   const int32_t nW = sel.kpn;
-  const int64_t offW = sel.kpoff;
   const int32_t pp = st->place_par_prev;  // the previous merge's parity (-1: its pairs are in the lists)
   const int2* thp = mid_th(D, pp >= 0 ? pp : 0);
-  const int64_t nP = pp >= 0 ? min(st->mid_nh[pp], D.THcap) : 0;
-  const int64_t ntot = nW + nP;
+  const int64_t l0 = (int64_t)nW * w / G, nl = (int64_t)nW * (w + 1) / G - l0;
+  const int64_t offW = sel.kpoff + l0;
+  const int64_t nsg = pp >= 0 ? min(D.mcnt[pp * NBA_MAX + w].y, MTH) : 0;
+  const int64_t nsp = pp >= 0 ? min(st->mid_nh[pp], D.THcap - MSEG_TH) : 0;
+  const int64_t s0 = nsp * w / G, ns = nsp * (w + 1) / G - s0;
+  const int2* segp = thp + (int64_t)w * MTH;
+  const int2* spp = thp + MSEG_TH + s0;
+  const int64_t ncand = nl + nsg + ns;
   if (w == 0) {  // _tokens[n] = json.loads(key); state the next select reads
     const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
     const int64_t vL = D.voff[L], vR = D.voff[Rr];
@@ -370,26 +472,26 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
   }
   if (t == 0) {
     S.nocc = S.nm = S.chk = 0;
+    S.ntm = S.nth = S.nkl = 0;
     S.hot.n = 0;
   }
   __syncthreads();
   dbg_stamp(D, 11);
-  const int64_t lo = ntot * w / G, hi = ntot * (w + 1) / G;
-  for (int64_t c0 = lo; c0 < hi; c0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
+  for (int64_t c0 = 0; c0 < ncand; c0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
     const int64_t i = c0 + t;
     MidHalf hl, hr;
     bool vl = false, vr = false;
-    if (i < hi) {
+    if (i < ncand) {
       int32_t g = -1;
-      if (i < nW) {
+      if (i < nl) {
         g = D.kpool[offW + i];
       } else {
-        const int2 e = thp[i - nW];
+        const int2 e = i < nl + nsg ? segp[i - nl] : spp[i - nl - nsg];
         if (e.y == F.W) g = e.x;
       }
-      if (g >= 0) mid_walk(D, S, F, g, hl, vl, hr, vr);
+      if (g >= 0 && g < D.R) mid_walk(D, S, F, g, hl, vl, hr, vr);  // (a bad list entry: no out-of-range read)
     }
-    if (c0 == lo) dbg_stamp(D, 15);
+    if (c0 == 0) dbg_stamp(D, 15);
     // ---- this round's new keys: LDS dedupe, then one resolve + count update per key
     bool il = false, ir = false;
     int32_t sl = -1, sr = -1;
@@ -416,7 +518,7 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
     if (vl && sl < 0) mid_single(D, S, F, hl.h1, hl.h2, hl.len, hl.idL, hl.g, hl.idR, hl.target);
     if (vr && sr < 0) mid_single(D, S, F, hr.h1, hr.h2, hr.len, hr.idL, hr.g, hr.idR, hr.target);
     __syncthreads();
-    if (c0 == lo) dbg_stamp(D, 16);
+    if (c0 == 0) dbg_stamp(D, 16);
     const int32_t nocc = S.nocc;
     const int64_t xb = D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
     for (int32_t q = t; q < nocc; q += ABLOCK) {
@@ -432,8 +534,7 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
       }
       if (claimed) {
         claim_payload(D, d, h1, h2, rp.x, rp.y, rp.z, rp.w);
-        klist_put(D, wave_reserve64((unsigned long long*)&st->U), d);
-        atomicAdd((unsigned long long*)&st->nkeys, 1ULL);
+        mid_claimed(D, S, d);
       } else {
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
@@ -443,14 +544,14 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
         count_add_hot(D, S.hot, d, S.cnt[s], F.th);
     }
     __syncthreads();
-    if (c0 == lo) dbg_stamp(D, 17);
+    if (c0 == 0) dbg_stamp(D, 17);
     if (vl && sl >= 0) {
       if (S.h1[sl] != hl.h1) set_error(D, GEOBPE_EHASH, -13);  // same probe key, other content
-      if (S.did[sl] >= 0) mid_pair(D, F, hl.target, S.did[sl]);
+      if (S.did[sl] >= 0) mid_pair(D, S, F, hl.target, S.did[sl]);
     }
     if (vr && sr >= 0) {
       if (S.h1[sr] != hr.h1) set_error(D, GEOBPE_EHASH, -13);
-      if (S.did[sr] >= 0) mid_pair(D, F, hr.target, S.did[sr]);
+      if (S.did[sr] >= 0) mid_pair(D, S, F, hr.target, S.did[sr]);
     }
     __syncthreads();
     for (int32_t q = t; q < nocc; q += ABLOCK) {  // clear the round's slots
@@ -461,6 +562,7 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
     if (t == 0) S.nocc = 0;
     __syncthreads();
   }
+  mid_flush_lists(D, S, F.par, w);
   dbg_stamp(D, 12);
   // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
   if (D.xrec) {  // as records: the nonzero slots, compacted behind one reservation
@@ -488,9 +590,9 @@ __device__ void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w, 
       const int32_t k = S.agg.key[i], v = S.agg.val[i];
       if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
     }
-    if (t == 0 && S.nm) atomicAdd(&D.count[F.W], -S.nm);
+    if (w == 0 && t == 0) D.count[F.W] = 0;  // (mid_dec_agg: every pair of W is gone)
   }
-  if (t == 0 && S.nm) atomicAdd((unsigned long long*)&D.log[sel.iter].nmerged, (unsigned long long)S.nm);
+  // (the merge's merged total: the next place sums the workgroups' counts into the log)
   hot_flush(D, S.hot);  // (syncs the workgroup first)
   if (t == 0) D.chkcnt[w] = min(S.chk, (int32_t)D.RC);
   dbg_stamp(D, 13);
@@ -523,11 +625,77 @@ __device__ inline int32_t mpk_slot(MidAppLds& S, int32_t d, bool insert, bool* i
 
 constexpr int MP_UNR = 8;  // new-pair list entries in flight per thread
 
-// appending workgroup b of A: the posting entries of the new pairs in th[0..nh) whose key is
-// in bucket b, except key `skip` -- one pass counts them per key, the lists grow where
-// needed, a second pass writes the entries
-__device__ void mid_append_body(const Dev& D, const int2* th, int64_t nh, int32_t skip, int32_t b, int32_t A,
-                                MidAppLds& S) {
+// appending workgroup b of A: the posting entries of merge pp's new pairs (the find
+// workgroups' segments of TH(pp) and its spill list) whose key is in bucket b, except key
+// `skip` -- one pass counts them per key (and keeps each entry with its rank in LDS), the
+// lists grow where needed (one pool reservation per round), then the kept entries are
+// written (a second pass over the new pairs only when more than MAE were kept).  Threads
+// split the segments TPS to a segment; every thread strides the spill list.
+// one new pair of merge pp in an appender: PASS 0 keeps it in LDS when its key is this
+// appender's (compacted, one LDS reservation per wave instruction); PASS 1 / 2 are the
+// fallback when more than MAE are kept -- 1 counts it for its key, 2 writes it
+template <int PASS>
+__device__ __attribute__((always_inline)) inline void mid_app_one(const Dev& D, MidAppLds& S, int2 h, int32_t skip,
+                                                                  int32_t b, int32_t A) {
+  const int32_t d = h.y;
+  if (d < 0 || d == skip || mid_bucket(d, A) != (uint32_t)b) return;
+  bool ins;
+  if constexpr (PASS == 0) {
+    const int32_t e = lds_reserve(&S.nent);
+    if (e < MAE) S.ent[e] = h;
+  } else if constexpr (PASS == 1) {
+    const int32_t s = mpk_slot(S, d, true, &ins);
+    if (s < 0) {
+      S.full = 1;  // (more keys than the table: the lists are rebuilt)
+      return;
+    }
+    atomicAdd(&S.cnt[s], 1);
+    if (ins) S.occ[atomicAdd(&S.nocc, 1)] = s;
+  } else {
+    const int32_t s = mpk_slot(S, d, false, &ins);
+    if (s < 0 || S.off[s] < 0) return;
+    const int32_t r = atomicAdd(&S.cur[s], 1);
+    D.kpool[(int64_t)S.off[s] + S.base[s] + r] = h.x;
+  }
+}
+// every new pair of merge pp through mid_app_one: a wave takes whole segments of the find
+// workgroups (64 lanes on consecutive entries, MP_UNR segments in flight; S.pre holds the
+// segment counts), every thread strides the spill list
+template <int PASS>
+__device__ __attribute__((always_inline)) inline void mid_app_pass(const Dev& D, MidAppLds& S, int32_t pp,
+                                                                   int32_t skip, int32_t b, int32_t A) {
+  const int2* th = mid_th(D, pp);
+  const int32_t NS = mid_G(D), t = threadIdx.x, lane = t & 63;
+  constexpr int NWV = ABLOCK / 64;
+  for (int32_t s0 = t >> 6; s0 < NS; s0 += NWV * MP_UNR) {  // (wave-uniform)
+    int32_t n[MP_UNR], nmax = 0;
+#pragma unroll
+    for (int u = 0; u < MP_UNR; u++) {
+      const int32_t sg = s0 + u * NWV;
+      n[u] = sg < NS ? S.pre[sg] : 0;
+      nmax = max(nmax, n[u]);
+    }
+    for (int32_t c = lane; c < nmax; c += 64) {
+      int2 h[MP_UNR];
+#pragma unroll
+      for (int u = 0; u < MP_UNR; u++)
+        h[u] = c < n[u] ? th[(int64_t)(s0 + u * NWV) * MTH + c] : make_int2(-1, -1);
+#pragma unroll
+      for (int u = 0; u < MP_UNR; u++) mid_app_one<PASS>(D, S, h[u], skip, b, A);
+    }
+  }
+  const int64_t nsp = min(D.st->mid_nh[pp], D.THcap - MSEG_TH);
+  const int2* sp = th + MSEG_TH;
+  for (int64_t i0 = t; i0 < nsp; i0 += MP_UNR * ABLOCK) {
+    int2 h[MP_UNR];
+#pragma unroll
+    for (int u = 0; u < MP_UNR; u++) h[u] = i0 + u * ABLOCK < nsp ? sp[i0 + u * ABLOCK] : make_int2(-1, -1);
+#pragma unroll
+    for (int u = 0; u < MP_UNR; u++) mid_app_one<PASS>(D, S, h[u], skip, b, A);
+  }
+}
+
+__device__ __attribute__((always_inline)) inline void mid_append_body(const Dev& D, int32_t pp, int32_t skip, int32_t b, int32_t A, MidAppLds& S) {
   State* st = D.st;
   const int32_t t = threadIdx.x;
   dbg_stamp(D, 30);
@@ -536,61 +704,84 @@ __device__ void mid_append_body(const Dev& D, const int2* th, int64_t nh, int32_
     S.cnt[i] = 0;
     S.cur[i] = 0;
   }
-  if (t == 0) S.nocc = S.nbig = S.full = 0;
+  if (t == 0) S.nocc = S.nbig = S.full = S.nent = 0;
+  if (t < mid_G(D)) S.pre[t] = min(D.mcnt[pp * NBA_MAX + t].y, MTH);  // (the segment counts)
   __syncthreads();
-  // ---- pass 1: new entries per key of bucket b
-  for (int64_t i0 = t; i0 < nh; i0 += MP_UNR * ABLOCK) {
-    int32_t d[MP_UNR];
-#pragma unroll
-    for (int u = 0; u < MP_UNR; u++) d[u] = i0 + u * ABLOCK < nh ? th[i0 + u * ABLOCK].y : -1;
-#pragma unroll
-    for (int u = 0; u < MP_UNR; u++) {
-      if (d[u] < 0 || d[u] == skip || mid_bucket(d[u], A) != (uint32_t)b) continue;
+  // ---- pass 1: this bucket's new pairs compacted into LDS, then counted per key (dense)
+  mid_app_pass<0>(D, S, pp, skip, b, A);
+  __syncthreads();
+  const bool kept = S.nent <= MAE;
+  if (kept) {
+    const int32_t ne = S.nent;
+    for (int32_t e = t; e < ne; e += ABLOCK) {
+      const int2 h = S.ent[e];
       bool ins;
-      const int32_t s = mpk_slot(S, d[u], true, &ins);
+      const int32_t s = mpk_slot(S, h.y, true, &ins);
       if (s < 0) {
         S.full = 1;  // (more keys than the table: the lists are rebuilt)
+        S.ent[e].x = -1;  // (dropped: the slot field marks it -- the packed word uses all 32 bits)
         continue;
       }
-      atomicAdd(&S.cnt[s], 1);
+      const int32_t r = atomicAdd(&S.cnt[s], 1);
       if (ins) S.occ[atomicAdd(&S.nocc, 1)] = s;
+      if (r < (1 << 21)) {
+        S.ent[e].y = (int32_t)(((uint32_t)s << 21) | (uint32_t)r);
+      } else {
+        S.ent[e].x = -1;
+        S.full = 1;
+      }
     }
+  } else {
+    mid_app_pass<1>(D, S, pp, skip, b, A);
   }
   __syncthreads();
   dbg_stamp(D, 32);
-  // ---- room for every key's new entries (a full list grows to 2x)
+  // ---- room for every key's new entries (a full list grows to 2x): one reservation per round
   const int32_t nocc = S.nocc;
-  for (int32_t q = t; q < nocc; q += ABLOCK) {
-    const int32_t sl = S.occ[q];
-    const int32_t d = S.key[sl], add = S.cnt[sl];
-    const int32_t n = D.kp_n[d], cap = D.kp_cap[d];
-    S.base[sl] = n;
-    if (n + add > cap) {
-      const int32_t ncap = max(2 * (n + add), 16);
-      const int64_t at = (int64_t)atomicAdd((unsigned long long*)&st->kpool_used, (unsigned long long)ncap);
-      if (at + ncap > D.KPOOL) {
-        S.full = 1;
-        continue;
-      }
-      const int32_t old = D.kp_off[d];
-      if (n <= TAIL_SMALL) {
-        for (int32_t k = 0; k < n; k++) D.kpool[at + k] = D.kpool[(int64_t)old + k];
-      } else {
-        const int32_t x = atomicAdd(&S.nbig, 1);
-        if (x < TAIL_BIG) {
-          S.big_old[x] = old;
-          S.big_new[x] = (int32_t)at;
-          S.big_pre[x] = n;
-        } else {
-          S.full = 1;
-        }
-      }
-      D.kp_off[d] = (int32_t)at;
-      D.kp_cap[d] = ncap;
+  for (int32_t q0 = 0; q0 < nocc; q0 += ABLOCK) {  // block-uniform
+    const int32_t q = q0 + t;
+    int32_t sl = -1, d = -1, add = 0, n = 0, cap = 0, ncap = 0;
+    if (q < nocc) {
+      sl = S.occ[q];
+      d = S.key[sl];
+      add = S.cnt[sl];
+      n = D.kp_n[d];
+      cap = D.kp_cap[d];
+      if (n + add > cap) ncap = max(2 * (n + add), 16);
     }
-    D.kp_n[d] = n + add;
+    int32_t tot;
+    const int32_t ex = block_excl_scan(ncap, &tot, S.red);
+    if (t == 0) S.pbase = tot ? (int64_t)atomicAdd((unsigned long long*)&st->kpool_used, (unsigned long long)tot) : 0;
+    __syncthreads();
+    if (q < nocc) {
+      S.base[sl] = n;
+      int32_t off = D.kp_off[d];
+      if (ncap > 0 && S.pbase + ex + ncap > D.KPOOL) {  // no room: the lists are rebuilt, this
+        S.full = 1;                                       // key's entries are not written
+        off = -1;
+      } else if (ncap > 0) {
+        const int64_t at = S.pbase + ex;
+        if (n <= TAIL_SMALL) {
+          for (int32_t k = 0; k < n; k++) D.kpool[at + k] = D.kpool[(int64_t)off + k];
+        } else {
+          const int32_t x = atomicAdd(&S.nbig, 1);
+          if (x < TAIL_BIG) {
+            S.big_old[x] = off;
+            S.big_new[x] = (int32_t)at;
+            S.big_pre[x] = n;
+          } else {
+            S.full = 1;
+          }
+        }
+        off = (int32_t)at;
+        D.kp_off[d] = off;
+        D.kp_cap[d] = ncap;
+      }
+      S.off[sl] = off;
+      if (off >= 0) D.kp_n[d] = n + add;
+    }
+    __syncthreads();
   }
-  __syncthreads();
   dbg_stamp(D, 33);
   const int32_t nb = min(S.nbig, TAIL_BIG);
   if (nb > 0) {  // the big lists' old entries, by the whole workgroup
@@ -606,20 +797,17 @@ __device__ void mid_append_body(const Dev& D, const int2* th, int64_t nh, int32_
       D.kpool[(int64_t)S.big_new[r] + k] = D.kpool[(int64_t)S.big_old[r] + k];
     }
   }
-  // ---- pass 2: the entries
-  for (int64_t i0 = t; i0 < nh; i0 += MP_UNR * ABLOCK) {
-    int2 h[MP_UNR];
-#pragma unroll
-    for (int u = 0; u < MP_UNR; u++) h[u] = i0 + u * ABLOCK < nh ? th[i0 + u * ABLOCK] : make_int2(-1, -1);
-#pragma unroll
-    for (int u = 0; u < MP_UNR; u++) {
-      if (h[u].y < 0 || h[u].y == skip || mid_bucket(h[u].y, A) != (uint32_t)b) continue;
-      bool ins;
-      const int32_t s = mpk_slot(S, h[u].y, false, &ins);
-      if (s < 0) continue;
-      const int32_t r = atomicAdd(&S.cur[s], 1);
-      D.kpool[(int64_t)D.kp_off[h[u].y] + S.base[s] + r] = h[u].x;
+  // ---- the entries
+  if (kept) {
+    const int32_t ne = S.nent;
+    for (int32_t e = t; e < ne; e += ABLOCK) {
+      const int2 x = S.ent[e];
+      if (x.x < 0) continue;
+      const int32_t sl = (int32_t)((uint32_t)x.y >> 21), r = x.y & ((1 << 21) - 1);  // (11 + 21 bits: unsigned)
+      if (S.off[sl] >= 0) D.kpool[(int64_t)S.off[sl] + S.base[sl] + r] = x.x;
     }
+  } else {  // (more than the LDS kept: a second pass over the new pairs, ranks afresh)
+    mid_app_pass<2>(D, S, pp, skip, b, A);
   }
   __syncthreads();
   dbg_stamp(D, 35);
@@ -651,9 +839,8 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int 
   }
   const int32_t pp = st->place_par_prev;
   if (pp < 0 || !valid) return;
-  const int64_t nh = min(st->mid_nh[pp], D.THcap);
   const int32_t skip = sel.decision == SEL_MERGE ? sel.W : -1;
-  mid_append_body(D, mid_th(D, pp), nh, skip, blockIdx.x - G, gridDim.x - G, U.a);
+  mid_append_body(D, pp, skip, blockIdx.x - G, gridDim.x - G, U.a);
 }
 
 // ---------------------------------------------------------------------- select + place
@@ -672,10 +859,14 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
   if (par < 0) return;
   const Sel sel = D.sel[par];
   if (sel.decision != SEL_MERGE) return;
-  const int64_t nm = min(st->mid_nm[par], D.TMcap), nh = min(st->mid_nh[par], D.THcap);
-  const int2* th = mid_th(D, par);
-  for (int64_t i = nm * b / P + t; i < nm * (b + 1) / P; i += ABLOCK) {
-    const int4 e = D.TM[i];
+  // find workgroup b's segments (b < G), share b of the spill lists
+  const int32_t G = mid_G(D);
+  const int4 mc = b < G ? D.mcnt[par * NBA_MAX + b] : make_int4(0, 0, 0, 0);
+  const int64_t nms = min(st->mid_nm[par], D.TMcap - MSEG_TM), nhs = min(st->mid_nh[par], D.THcap - MSEG_TH);
+  const int4* tms = D.TM + (int64_t)b * MTM;
+  const int64_t m0 = nms * b / P, nm = min(mc.x, MTM) + (nms * (b + 1) / P - m0);
+  for (int64_t i = t; i < nm; i += ABLOCK) {
+    const int4 e = i < min(mc.x, MTM) ? tms[i] : D.TM[MSEG_TM + m0 + i - min(mc.x, MTM)];
     *reinterpret_cast<int2*>(D.tok + e.x) = make_int2(sel.nid, e.y);
     D.tok[e.z] = make_int4(-1, 0, -1, -1);
     if (e.w >= 0)
@@ -683,9 +874,20 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
     else
       *tok_f(D, e.x, 3) = -1;
   }
-  for (int64_t i = nh * b / P + t; i < nh * (b + 1) / P; i += ABLOCK) {
-    const int2 h = th[i];
+  const int2* th = mid_th(D, par);
+  const int2* ths = th + (int64_t)b * MTH;
+  const int64_t h0 = nhs * b / P, nh = min(mc.y, MTH) + (nhs * (b + 1) / P - h0);
+  for (int64_t i = t; i < nh; i += ABLOCK) {
+    const int2 h = i < min(mc.y, MTH) ? ths[i] : th[MSEG_TH + h0 + i - min(mc.y, MTH)];
     *tok_f(D, h.x, 3) = h.y;
+  }
+  if (b == 0) {  // the merge's merged occurrences: the find workgroups' counts, summed
+    int32_t v = 0;
+    for (int32_t i = t; i < G; i += ABLOCK) v += D.mcnt[par * NBA_MAX + i].z;
+    __shared__ int32_t s_red[ABLOCK / 64];
+    int32_t tot;
+    block_excl_scan(v, &tot, s_red);
+    if (t == 0) D.log[sel.iter].nmerged = tot;
   }
   dbg_stamp(D, 37);
 }

@@ -71,7 +71,6 @@ __device__ void tail_half(const Dev& D, TailLds& S, const TailCtx& F, u64 h1, u6
   if (claimed) {
     claim_payload(D, d, h1, h2, len, idL, g, idR);
     klist_put(D, wave_reserve64((unsigned long long*)&D.st->U), d);
-    atomicAdd((unsigned long long*)&D.st->nkeys, 1ULL);
   } else {
     const int32_t j = atomicAdd(&S.nC, 1);
     if (j < D.THcap) {
@@ -258,7 +257,10 @@ __global__ __launch_bounds__(SBLOCK) void k_tail(Dev D, int par, int64_t n_max) 
     const int64_t offW = D.kp_off[F.W];
     for (int32_t c0 = 0; c0 < nW; c0 += SBLOCK) {
       const int32_t i = c0 + t;
-      if (i < nW) tail_walk(D, S, F, D.kpool[offW + i]);
+      if (i < nW) {
+        const int32_t g = D.kpool[offW + i];
+        if (g >= 0 && g < D.R) tail_walk(D, S, F, g);  // (a bad list entry: no out-of-range read)
+      }
     }
     __syncthreads();
     // ---- place: token rewrites (step 2, bond_to_token / token_pos) and pk of the new
