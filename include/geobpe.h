@@ -268,7 +268,8 @@ int geobpe_nerf(int device, int64_t n_spans, const int64_t *h_res_off, const dou
    chain, minimising the exit-frame loss of the chain's NeRF against cached frames plus the
    optional von Mises prior.  Replaces BPE.glue_opt_all / _opt_glue_worker / opt_glue /
    optimize_glues_entry_torch / fk_segment_torch (bpe.py:106-135, 423-578, 739-807), one
-   chain per thread.  h_res_off[n_chains + 1]: residue offsets; h_geo: 9 float64 per
+   64-lane wave per chain (k_glue_wave: prefix-product NeRF, suffix-sum gradient; environment
+   GEOBPE_GLUE_THREAD=1 selects the one-thread-per-chain k_glue_opt).  h_res_off[n_chains + 1]: residue offsets; h_geo: 9 float64 per
    residue (geobpe_nerf's layout, float32-representable values); per glue (r - 1 per
    chain, in order): h_x0 3 float32 (raw start values), h_tgt 12 float32 (target frame R
    row-major, then t); h_grid[n_chains]: prior table per chain; h_prior: n_grid x 3 types

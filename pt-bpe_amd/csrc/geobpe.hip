@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <mutex>
 #include <string>
 #include <type_traits>
 #include <vector>
@@ -1666,6 +1667,16 @@ int geobpe_nerf(int device, int64_t n_spans, const int64_t* h_res_off, const dou
   return rc;
 }
 
+namespace {
+struct GlueArena {  // geobpe_glue_opt's stream and scratch of one device (kept for the process)
+  hipStream_t s = nullptr;
+  char* buf = nullptr;
+  size_t cap = 0;
+};
+std::mutex g_glue_mu;
+std::map<int, GlueArena> g_glue;
+}  // namespace
+
 int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, const double* h_geo, const float* h_x0,
                     const float* h_tgt, const int32_t* h_grid, int32_t n_grid, int32_t kmax, const float* h_prior,
                     const int32_t* h_kcnt, float lam, double w_rot, double w_trans, float* h_xout, int32_t* h_stats,
@@ -1688,8 +1699,16 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
   for (int64_t i = 0; i < 3 * (int64_t)n_grid; i++)
     if (h_kcnt[i] <= 0 || h_kcnt[i] > kmax) return GEOBPE_EARG;
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
-  hipStream_t s;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GEOBPE_EHIP;
+  // one stream and one scratch arena per device, kept across calls and grown on demand
+  // (induce with glue opt calls this once per chain and per re-optimisation: a stream and
+  // 14 allocations per call used to outweigh the kernel)
+  std::lock_guard<std::mutex> lock(g_glue_mu);
+  GlueArena& ar = g_glue[device];
+  if (!ar.s && hipStreamCreateWithFlags(&ar.s, hipStreamNonBlocking) != hipSuccess) {
+    ar.s = nullptr;
+    return GEOBPE_EHIP;
+  }
+  hipStream_t s = ar.s;
   const int64_t pmax = 3 * (rmax - 1), S = n_chains;
   GlueProb P{};
   P.S = S;
@@ -1703,15 +1722,54 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
   float *d_x0 = nullptr, *d_tgt = nullptr, *d_prior = nullptr, *d_xout = nullptr;
   int32_t *d_grid = nullptr, *d_kcnt = nullptr, *d_stats = nullptr;
   int rc = 0;
-  const int64_t nx = 9 * rmax * S;
-  if (hipMalloc(&d_off, (S + 1) * 8) != hipSuccess || hipMalloc(&d_geo, R * 9 * 8) != hipSuccess ||
-      hipMalloc(&d_x0, G * 3 * 4) != hipSuccess || hipMalloc(&d_tgt, G * 12 * 4) != hipSuccess ||
-      hipMalloc(&d_grid, S * 4) != hipSuccess || hipMalloc(&d_prior, (int64_t)n_grid * 6 * kmax * 4) != hipSuccess ||
-      hipMalloc(&d_kcnt, (int64_t)n_grid * 3 * 4) != hipSuccess || hipMalloc(&d_xout, G * 3 * 4) != hipSuccess ||
-      hipMalloc(&d_stats, S * 2 * 4) != hipSuccess || hipMalloc(&d_loss, S * 2 * 8) != hipSuccess ||
-      hipMalloc(&P.X, nx * 8) != hipSuccess || hipMalloc(&P.AX, nx * 8) != hipSuccess ||
-      hipMalloc(&P.V, (int64_t)GLUE_NVEC * pmax * S * 4) != hipSuccess ||
-      hipMalloc(&P.H, (int64_t)2 * GLUE_HIST * pmax * S * 4) != hipSuccess) {
+  // one wave per chain (k_glue_wave, scratch at each chain's residue / glue offset); the
+  // one-thread-per-chain k_glue_opt (scratch interleaved over the chains, n_chains x the
+  // longest chain) stays as an A/B switch: GEOBPE_GLUE_THREAD=1
+  const char* ge = getenv("GEOBPE_GLUE_THREAD");
+  const bool wave = !(ge && atoi(ge) == 1);
+  const int64_t NG = 3 * G;
+  const int64_t nx = wave ? 9 * R : 9 * rmax * S;
+  const int64_t nv = wave ? NG : pmax * S;
+  const size_t sizes[14] = {(size_t)(S + 1) * 8, (size_t)R * 9 * 8, (size_t)G * 3 * 4, (size_t)G * 12 * 4,
+                            (size_t)S * 4, (size_t)n_grid * 6 * kmax * 4, (size_t)n_grid * 3 * 4, (size_t)G * 3 * 4,
+                            (size_t)S * 2 * 4, (size_t)S * 2 * 8, (size_t)nx * 8, (size_t)nx * 8,
+                            (size_t)GLUE_NVEC * nv * 4, (size_t)2 * GLUE_HIST * nv * 4};
+  size_t total = 0;
+  for (size_t z : sizes) total += (z + 255) / 256 * 256;
+  bool ok = true;
+  if (ar.cap < total) {
+    if (ar.buf) hipFree(ar.buf);
+    ar.buf = nullptr;
+    ar.cap = 0;
+    const size_t want = total + total / 4;
+    if (hipMalloc(&ar.buf, want) == hipSuccess)
+      ar.cap = want;
+    else
+      ok = false;
+  }
+  if (ok) {
+    void* ptr[14];
+    char* q = ar.buf;
+    for (int i = 0; i < 14; i++) {
+      ptr[i] = q;
+      q += (sizes[i] + 255) / 256 * 256;
+    }
+    d_off = (int64_t*)ptr[0];
+    d_geo = (double*)ptr[1];
+    d_x0 = (float*)ptr[2];
+    d_tgt = (float*)ptr[3];
+    d_grid = (int32_t*)ptr[4];
+    d_prior = (float*)ptr[5];
+    d_kcnt = (int32_t*)ptr[6];
+    d_xout = (float*)ptr[7];
+    d_stats = (int32_t*)ptr[8];
+    d_loss = (double*)ptr[9];
+    P.X = (double*)ptr[10];
+    P.AX = (double*)ptr[11];
+    P.V = (float*)ptr[12];
+    P.H = (float*)ptr[13];
+  }
+  if (!ok) {
     rc = GEOBPE_EHIP;
   } else {
     hipMemcpyAsync(d_off, h_res_off, (S + 1) * 8, hipMemcpyHostToDevice, s);
@@ -1727,8 +1785,29 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
     P.grid = d_grid;
     P.prior = d_prior;
     P.kcnt = d_kcnt;
-    hipLaunchKernelGGL(k_glue_opt, dim3((unsigned)((S + 63) / 64)), dim3(64), 0, s, P, (const float*)d_x0, d_xout,
-                       d_stats, d_loss);
+    if (wave) {
+      GlueWaveProb W{};
+      W.roff = d_off;
+      W.geo = d_geo;
+      W.tgt = d_tgt;
+      W.grid = d_grid;
+      W.prior = d_prior;
+      W.kcnt = d_kcnt;
+      W.kmax = kmax;
+      W.lam = lam;
+      W.wR = w_rot;
+      W.wt = w_trans;
+      W.X = P.X;
+      W.AX = P.AX;
+      W.V = P.V;
+      W.H = P.H;
+      W.NG = NG;
+      hipLaunchKernelGGL(k_glue_wave, dim3((unsigned)S), dim3(GW), 0, s, W, S, (const float*)d_x0, d_xout, d_stats,
+                         d_loss);
+    } else {
+      hipLaunchKernelGGL(k_glue_opt, dim3((unsigned)((S + 63) / 64)), dim3(64), 0, s, P, (const float*)d_x0, d_xout,
+                         d_stats, d_loss);
+    }
     if (hipGetLastError() != hipSuccess) rc = GEOBPE_EHIP;
     if (!rc && (hipMemcpyAsync(h_xout, d_xout, G * 3 * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
                 hipMemcpyAsync(h_stats, d_stats, S * 2 * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
@@ -1736,21 +1815,6 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
       rc = GEOBPE_EHIP;
     if (hipStreamSynchronize(s) != hipSuccess) rc = GEOBPE_EHIP;
   }
-  hipFree(d_off);
-  hipFree(d_geo);
-  hipFree(d_x0);
-  hipFree(d_tgt);
-  hipFree(d_grid);
-  hipFree(d_prior);
-  hipFree(d_kcnt);
-  hipFree(d_xout);
-  hipFree(d_stats);
-  hipFree(d_loss);
-  hipFree(P.X);
-  hipFree(P.AX);
-  hipFree(P.V);
-  hipFree(P.H);
-  hipStreamDestroy(s);
   return rc;
 }
 

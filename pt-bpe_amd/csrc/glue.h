@@ -547,4 +547,512 @@ __global__ __launch_bounds__(64) void k_glue_opt(GlueProb P, const float* x0, fl
   losses[2 * s + 1] = loss;
 }
 
+// ====================================================================== one wave per chain
+// k_glue_wave: the same optimiser with the 64 lanes of a wave on one chain.
+//
+// NeRF as a prefix product.  The frame a placement is made in -- columns bc, nbc, n at the
+// last atom c -- turns into the next atom's frame by a rotation that depends on the
+// placement offset d alone: bc' = R d^, n' = R normalize(e_x x d^), nbc' = n' x bc'
+// (nerf.py:200-207 with ab' = |c - b| bc).  So frame i = frame 2 o A_3 o ... o A_i with
+// A_j = (M(d_j), d_j) and (M, o) o (M', o') = (M M', o + M o'): each lane composes a chunk
+// of consecutive placements, a wave scan (6 shuffle steps) composes the chunks, each lane
+// re-applies its chunk from its prefix.
+//
+// The gradient without a reverse sweep.  Changing the torsion of atom i rotates atoms
+// i, i+1, ... rigidly about the axis bc through c = x_{i-1}; changing its bond angle rotates
+// them about -w, w = normalize(bc x (x_i - c)) (the plane b, c, x_i keeps its normal, so the
+// next placements follow rigidly).  With the atoms' loss gradients g_m (the frame terms,
+// independent per residue):
+//   dL/dtorsion_i = bc . (S1_i - c x S0_i),  dL/dangle_i = -w . (S1_i - c x S0_i),
+//   S0_i = sum_{m >= i} g_m,  S1_i = sum_{m >= i} x_m x g_m
+// -- suffix sums: a chunk sum per lane, a wave suffix scan, a backward walk of the chunk.
+//
+// The L-BFGS vectors are strided over the lanes (element i on lane i % 64); dot products,
+// maxima and the loss are butterfly reductions (the same bits on every lane, so the
+// optimiser's control flow stays wave-uniform).  Per-chain scratch sits at the chain's own
+// residue / glue offset (memory grows with the residues, not n_chains x the longest chain).
+// Parity is statistical, as for k_glue_opt: the exact derivative in float64 instead of
+// autograd's float32 chain, other summation orders (tests/test_glue.py bounds).
+constexpr int GW = 64;
+
+struct Aff {  // rigid transform: rotation columns c0 c1 c2, offset o
+  V3 c0, c1, c2, o;
+};
+__device__ inline V3 aff_rot(const Aff& A, V3 v) {
+  return {A.c0.x * v.x + A.c1.x * v.y + A.c2.x * v.z, A.c0.y * v.x + A.c1.y * v.y + A.c2.y * v.z,
+          A.c0.z * v.x + A.c1.z * v.y + A.c2.z * v.z};
+}
+__device__ inline Aff aff_then(const Aff& A, const Aff& B) {  // A o B
+  return {aff_rot(A, B.c0), aff_rot(A, B.c1), aff_rot(A, B.c2), v_addv(A.o, aff_rot(A, B.o))};
+}
+__device__ inline Aff aff_id() { return {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}, {0, 0, 0}}; }
+__device__ inline Aff aff_local(V3 d) {  // the placement with offset d in the frame's coordinates
+  const V3 e1 = v_scale(d, 1.0 / v_norm(d));
+  V3 e3 = {0.0, -e1.z, e1.y};
+  e3 = v_scale(e3, 1.0 / v_norm(e3));
+  return {e1, v_cross(e3, e1), e3, d};
+}
+__device__ inline V3 v_shfl(V3 v, int src) { return {__shfl(v.x, src, GW), __shfl(v.y, src, GW), __shfl(v.z, src, GW)}; }
+__device__ inline V3 v_shfl_up(V3 v, int k) {
+  return {__shfl_up(v.x, k, GW), __shfl_up(v.y, k, GW), __shfl_up(v.z, k, GW)};
+}
+__device__ inline V3 v_shfl_down(V3 v, int k) {
+  return {__shfl_down(v.x, k, GW), __shfl_down(v.y, k, GW), __shfl_down(v.z, k, GW)};
+}
+__device__ inline Aff aff_shfl_up(const Aff& a, int k) {
+  return {v_shfl_up(a.c0, k), v_shfl_up(a.c1, k), v_shfl_up(a.c2, k), v_shfl_up(a.o, k)};
+}
+__device__ inline double w_sum(double v) {
+#pragma unroll
+  for (int k = GW / 2; k >= 1; k >>= 1) v += __shfl_xor(v, k, GW);
+  return v;
+}
+__device__ inline float w_sumf(float v) {
+#pragma unroll
+  for (int k = GW / 2; k >= 1; k >>= 1) v += __shfl_xor(v, k, GW);
+  return v;
+}
+__device__ inline float w_maxf(float v) {
+#pragma unroll
+  for (int k = GW / 2; k >= 1; k >>= 1) v = fmaxf(v, __shfl_xor(v, k, GW));
+  return v;
+}
+
+struct WV {  // one float vector of a chain (contiguous at the chain's glue offset)
+  float* p;
+  __device__ float& operator[](int64_t i) const { return p[i]; }
+};
+
+struct GlueWaveProb {
+  const int64_t* roff;  // residue offsets [S + 1]
+  const double* geo;    // 9 per residue (k_nerf layout)
+  const float* tgt;     // 12 per glue
+  const int32_t* grid;
+  const float* prior;
+  const int32_t* kcnt;
+  int32_t kmax;
+  float lam;
+  double wR, wt;
+  double* X;    // atoms: 9 per residue, at the residue offset
+  double* AX;   // their loss gradients (and the placement offsets during the forward pass)
+  float* V;     // GLUE_NVEC vectors of NG (= 3 x glues) floats, each chain at 3 g0
+  float* H;     // 2 GLUE_HIST vectors of NG
+  int64_t NG;
+};
+
+// the (angle, length, torsion) of placement j (atom j + 3) of a chain at parameters x
+__device__ inline void glue_wparams(const double* g, WV x, int64_t j, float& A, float& L, float& T) {
+  const int64_t k = j / 3;
+  const double* gk = g + 9 * k;
+  const double* gn = gk + 9;
+  const int m = (int)(j - 3 * k);
+  if (m == 0) {
+    A = (float)gk[4], L = (float)gk[3], T = (float)gk[6];
+  } else if (m == 1) {
+    A = glue_wrap(x[3 * k + 1]), L = (float)gn[0], T = glue_wrap(x[3 * k]);
+  } else {
+    A = (float)gn[2], L = (float)gn[1], T = glue_wrap(x[3 * k + 2]);
+  }
+}
+
+// loss and gradient of one chain (r >= 2 residues) at x, by the wave; grad written in full
+// (one out-of-line copy: the optimiser calls it from four places)
+__device__ __attribute__((noinline)) double glue_eval_wave(const GlueWaveProb& P, int64_t a0, int64_t r, const double* g, const float* tg,
+                                 const float* pr, const int32_t* kc, WV x, WV grad) {
+  const int lane = threadIdx.x;
+  double* X = P.X + 9 * a0;
+  double* AX = P.AX + 9 * a0;
+  const int64_t n = 3 * (r - 1);  // placements (atoms 3 .. 3r - 1)
+  const int64_t CH = (n + GW - 1) / GW;
+  const int64_t j0 = min(n, (int64_t)lane * CH), j1 = min(n, j0 + CH);
+  __syncthreads();  // (x was written lane-strided)
+  // -- forward: this lane's chunk of placements, composed; offsets kept in AX meanwhile
+  Aff T = aff_id();
+  for (int64_t j = j0; j < j1; j++) {
+    float A, L, Tq;
+    glue_wparams(g, x, j, A, L, Tq);
+    float f0, f1, f2;
+    glue_d(A, L, Tq, f0, f1, f2);
+    const V3 d = {(double)f0, (double)f1, (double)f2};
+    stx(AX, 1, j + 3, d);
+    T = aff_then(T, aff_local(d));
+  }
+#pragma unroll
+  for (int k = 1; k < GW; k <<= 1) {
+    const Aff u = aff_shfl_up(T, k);
+    if (lane >= k) T = aff_then(u, T);
+  }
+  Aff F = aff_shfl_up(T, 1);  // exclusive prefix
+  if (lane == 0) F = aff_id();
+  V3 p3, p2, p1;
+  backbone_start(g[1], g[0], g[2], p3, p2, p1);
+  if (lane == 0) {
+    stx(X, 1, 0, p3);
+    stx(X, 1, 1, p2);
+    stx(X, 1, 2, p1);
+  }
+  {
+    const V3 bc = v_scale(v_sub(p1, p2), 1.0 / v_norm(v_sub(p1, p2)));
+    const V3 m = v_cross(v_sub(p2, p3), bc);
+    const V3 nn = v_scale(m, 1.0 / v_norm(m));
+    const Aff F2 = {bc, v_cross(nn, bc), nn, p1};
+    F = aff_then(F2, F);
+  }
+  for (int64_t j = j0; j < j1; j++) {
+    F = aff_then(F, aff_local(ldx(AX, 1, j + 3)));
+    stx(X, 1, j + 3, F.o);
+  }
+  __syncthreads();
+  // -- frames of residues 1..r-1 against the targets (bpe.py:539-548), lane-strided
+  double rot = 0.0, trans = 0.0;
+  for (int64_t i = 1 + lane; i < r; i += GW) {
+    const V3 N = ldx(X, 1, 3 * i), CA = ldx(X, 1, 3 * i + 1), C = ldx(X, 1, 3 * i + 2);
+    const float* Tg = tg + 12 * (i - 1);
+    const V3 vx = v_sub(C, CA), vu = v_sub(N, CA);
+    const V3 ex = glue_normalize(vx), eu = glue_normalize(vu);
+    const V3 w = v_cross(ex, eu);
+    const V3 ez = glue_normalize(w);
+    const V3 ey = v_cross(ez, ex);
+    const V3 Rx = {Tg[0], Tg[3], Tg[6]}, Ry = {Tg[1], Tg[4], Tg[7]}, Rz = {Tg[2], Tg[5], Tg[8]},
+             Rt = {Tg[9], Tg[10], Tg[11]};
+    const V3 dx = v_sub(ex, Rx), dy = v_sub(ey, Ry), dz = v_sub(ez, Rz), dt = v_sub(CA, Rt);
+    rot += 0.5 * (v_dot(dx, dx) + v_dot(dy, dy) + v_dot(dz, dz));
+    trans += v_dot(dt, dt);
+    V3 gx = v_scale(dx, P.wR), gy = v_scale(dy, P.wR), gz = v_scale(dz, P.wR);
+    gz = v_addv(gz, v_cross(ex, gy));
+    gx = v_addv(gx, v_cross(gy, ez));
+    const V3 gw = glue_normalize_back(w, gz);
+    gx = v_addv(gx, v_cross(eu, gw));
+    const V3 gu = v_cross(gw, ex);
+    const V3 gvx = glue_normalize_back(vx, gx), gvu = glue_normalize_back(vu, gu);
+    stx(AX, 1, 3 * i + 2, gvx);
+    stx(AX, 1, 3 * i, gvu);
+    stx(AX, 1, 3 * i + 1, v_addv(v_scale(v_addv(gvx, gvu), -1.0), v_scale(dt, 2.0 * P.wt)));
+  }
+  // -- prior (bpe.py:527-534, 549-558), float32, glue-strided: the gradient starts from it
+  float prior = 0.f;
+  for (int64_t k = lane; k + 1 < r; k += GW) {
+    float term = 0.f;
+    for (int t = 0; t < 3; t++) {
+      float gp = 0.f;
+      if (P.lam != 0.f) {
+        const float a = glue_wrap(x[3 * k + t]);
+        const float kappa = t == 0 ? 50.f : 20.f;
+        const float* cen = pr + (2 * t) * P.kmax;
+        const float* wt = cen + P.kmax;
+        float mx = -INFINITY;
+        for (int jj = 0; jj < kc[t]; jj++) mx = fmaxf(mx, kappa * f_cos(a - cen[jj]) + f_log(wt[jj] + 1e-12f));
+        float se = 0.f, sg = 0.f;
+        for (int jj = 0; jj < kc[t]; jj++) {
+          const float e = f_exp(kappa * f_cos(a - cen[jj]) + f_log(wt[jj] + 1e-12f) - mx);
+          se += e;
+          sg += e * kappa * f_sin(a - cen[jj]);
+        }
+        term += -(mx + f_log(se));
+        gp = P.lam * (sg / se);
+      }
+      grad[3 * k + t] = gp;
+    }
+    prior += term;
+  }
+  __syncthreads();
+  // -- the parameters' gradients from suffix sums of g_m and x_m x g_m over the atoms
+  V3 S0 = {0, 0, 0}, S1 = {0, 0, 0};
+  for (int64_t j = j0; j < j1; j++) {
+    const V3 gm = ldx(AX, 1, j + 3), xm = ldx(X, 1, j + 3);
+    S0 = v_addv(S0, gm);
+    S1 = v_addv(S1, v_cross(xm, gm));
+  }
+#pragma unroll
+  for (int k = 1; k < GW; k <<= 1) {
+    const V3 u0 = v_shfl_down(S0, k), u1 = v_shfl_down(S1, k);
+    if (lane + k < GW) {
+      S0 = v_addv(S0, u0);
+      S1 = v_addv(S1, u1);
+    }
+  }
+  {  // exclusive: the lanes after this one
+    const V3 u0 = v_shfl_down(S0, 1), u1 = v_shfl_down(S1, 1);
+    S0 = lane + 1 < GW ? u0 : V3{0, 0, 0};
+    S1 = lane + 1 < GW ? u1 : V3{0, 0, 0};
+  }
+  if (j1 > j0) {
+    V3 xi = ldx(X, 1, j1 - 1 + 3), c = ldx(X, 1, j1 - 1 + 2), b = ldx(X, 1, j1 - 1 + 1);
+    for (int64_t j = j1 - 1; j >= j0; j--) {
+      const V3 gm = ldx(AX, 1, j + 3);
+      S0 = v_addv(S0, gm);
+      S1 = v_addv(S1, v_cross(xi, gm));
+      const int64_t k = j / 3;
+      const int m = (int)(j - 3 * k);
+      if (m != 0) {
+        const V3 u = v_sub(c, b);
+        const V3 bc = v_scale(u, 1.0 / v_norm(u));
+        const V3 v = v_sub(S1, v_cross(c, S0));
+        const float gT = (float)v_dot(bc, v);
+        if (m == 1) {  // CA_{k+1}: torsion omega_k, angle C:1N:1CA_k
+          const V3 wv = v_cross(bc, v_sub(xi, c));
+          const float gA = (float)(-v_dot(v_scale(wv, 1.0 / v_norm(wv)), v));
+          grad[3 * k] = glue_wrap_back(x[3 * k], grad[3 * k] + gT);
+          grad[3 * k + 1] = glue_wrap_back(x[3 * k + 1], grad[3 * k + 1] + gA);
+        } else {  // C_{k+1}: torsion phi_{k+1}
+          grad[3 * k + 2] = glue_wrap_back(x[3 * k + 2], grad[3 * k + 2] + gT);
+        }
+      }
+      if (j > j0) {  // one atom back
+        xi = c;
+        c = b;
+        b = ldx(X, 1, j);
+      }
+    }
+  }
+  double loss = P.wR * w_sum(rot) + P.wt * w_sum(trans);
+  const float pri = w_sumf(prior);
+  if (P.lam != 0.f) loss += (double)(P.lam * pri);
+  __syncthreads();
+  return loss;
+}
+
+__device__ inline float w_dot(WV a, WV b, int64_t n) {
+  float s = 0.f;
+  for (int64_t i = threadIdx.x; i < n; i += GW) s += a[i] * b[i];
+  return w_sumf(s);
+}
+__device__ inline void w_copy(WV dst, WV src, int64_t n) {
+  for (int64_t i = threadIdx.x; i < n; i += GW) dst[i] = src[i];
+}
+
+// one chain per 64-thread workgroup; the control flow of k_glue_opt (torch/optim/lbfgs.py),
+// every scalar wave-uniform
+__global__ __launch_bounds__(GW) void k_glue_wave(GlueWaveProb P, int64_t S, const float* x0, float* xout,
+                                                  int32_t* stats, double* losses) {
+  const int64_t s = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (s >= S) return;
+  const int64_t a0 = P.roff[s], r = P.roff[s + 1] - a0;
+  const int64_t np = 3 * (r - 1), g0 = a0 - s;
+  if (r < 2) {
+    if (lane == 0) {
+      stats[2 * s] = 0;
+      stats[2 * s + 1] = 0;
+      losses[2 * s] = 0.0;
+      losses[2 * s + 1] = 0.0;
+    }
+    return;
+  }
+  const double* g = P.geo + 9 * a0;
+  const float* tg = P.tgt + 12 * g0;
+  const int32_t gi = P.grid[s];
+  const float* pr = P.prior + (int64_t)gi * 6 * P.kmax;
+  const int32_t* kc = P.kcnt + 3 * gi;
+  auto vec = [&](int v) { return WV{P.V + (int64_t)v * P.NG + 3 * g0}; };
+  auto hs = [&](int h) { return WV{P.H + (int64_t)h * P.NG + 3 * g0}; };
+  auto hy = [&](int h) { return WV{P.H + (int64_t)(GLUE_HIST + h) * P.NG + 3 * g0}; };
+  WV x = vec(0), d = vec(1), fg = vec(2), pg = vec(3), xi = vec(4), q = vec(5);
+  int gb[3] = {6, 7, 8};
+  __shared__ float ro[GLUE_HIST], al[GLUE_HIST];  // (wave-uniform values: every lane writes the same)
+  int nold = 0;
+  for (int64_t i = lane; i < np; i += GW) x[i] = x0[3 * g0 + i];
+  auto eval_at = [&](float t, WV out) -> double {
+    for (int64_t i = lane; i < np; i += GW) q[i] = xi[i] + t * d[i];
+    return glue_eval_wave(P, a0, r, g, tg, pr, kc, q, out);
+  };
+  auto vmaxabs = [&](WV v) {
+    float m = 0.f;
+    for (int64_t i = lane; i < np; i += GW) m = fmaxf(m, fabsf(v[i]));
+    return w_maxf(m);
+  };
+  double loss = glue_eval_wave(P, a0, r, g, tg, pr, kc, x, fg);
+  const double loss0 = loss;
+  int evals = 1, n_iter = 0;
+  float amax = vmaxabs(fg);
+  const float tol_grad = 1e-7f, tol_change = 1e-9f;
+  const int max_iter = 20, max_eval = 25;
+  float t = 1.f, H_diag = 1.f;
+  double prev_loss = loss;
+  if (!(amax <= tol_grad)) {
+    while (n_iter < max_iter) {
+      n_iter++;
+      if (n_iter == 1) {
+        for (int64_t i = lane; i < np; i += GW) d[i] = -fg[i];
+        nold = 0;
+        H_diag = 1.f;
+      } else {
+        float ys = 0.f, yy = 0.f;
+        for (int64_t i = lane; i < np; i += GW) {
+          const float yv = fg[i] - pg[i], sv = d[i] * t;
+          ys += yv * sv;
+          yy += yv * yv;
+        }
+        ys = w_sumf(ys);
+        yy = w_sumf(yy);
+        if (ys > 1e-10f) {
+          if (nold == GLUE_HIST) {  // unreachable with max_iter = 20; kept for the FIFO rule
+            for (int h = 0; h + 1 < GLUE_HIST; h++) {
+              w_copy(hs(h), hs(h + 1), np);
+              w_copy(hy(h), hy(h + 1), np);
+              ro[h] = ro[h + 1];
+            }
+            nold--;
+          }
+          const WV hsv = hs(nold), hyv = hy(nold);
+          for (int64_t i = lane; i < np; i += GW) {
+            hyv[i] = fg[i] - pg[i];
+            hsv[i] = d[i] * t;
+          }
+          ro[nold] = 1.f / ys;
+          nold++;
+          H_diag = ys / yy;
+        }
+        for (int64_t i = lane; i < np; i += GW) q[i] = -fg[i];
+        for (int h = nold - 1; h >= 0; h--) {
+          al[h] = w_dot(hs(h), q, np) * ro[h];
+          const WV yv = hy(h);
+          for (int64_t i = lane; i < np; i += GW) q[i] += -al[h] * yv[i];
+        }
+        for (int64_t i = lane; i < np; i += GW) d[i] = q[i] * H_diag;
+        for (int h = 0; h < nold; h++) {
+          const float be = w_dot(hy(h), d, np) * ro[h];
+          const WV sv = hs(h);
+          for (int64_t i = lane; i < np; i += GW) d[i] += (al[h] - be) * sv[i];
+        }
+      }
+      w_copy(pg, fg, np);
+      prev_loss = loss;
+      if (n_iter == 1) {
+        float s1 = 0.f;
+        for (int64_t i = lane; i < np; i += GW) s1 += fabsf(fg[i]);
+        t = fminf(1.f, 1.f / w_sumf(s1));
+      } else {
+        t = 1.f;
+      }
+      const float gtd = w_dot(fg, d, np);
+      if (gtd > -tol_change) break;
+      // ---- _strong_wolfe
+      w_copy(xi, x, np);
+      const int max_ls = max_eval - evals;
+      const float c1 = 1e-4f, c2 = 0.9f;
+      const float d_norm = vmaxabs(d);
+      const double f = loss;
+      WV gnew = vec(gb[0]);
+      double f_new = eval_at(t, gnew);
+      int ls_evals = 1;
+      float gtd_new = w_dot(gnew, d, np);
+      float t_prev = 0.f, gtd_prev = gtd;
+      double f_prev = f;
+      int gprev_buf = -1;
+      bool done = false;
+      int ls_iter = 0;
+      float br[2];
+      double bf[2];
+      float bgtd[2];
+      int bgb[2];
+      int nbr = 0;
+      while (ls_iter < max_ls) {
+        if ((float)f_new > (float)(f + (double)(c1 * t * gtd)) || (ls_iter > 1 && f_new >= f_prev)) {
+          br[0] = t_prev; br[1] = t; bf[0] = f_prev; bf[1] = f_new; bgtd[0] = gtd_prev; bgtd[1] = gtd_new;
+          bgb[0] = gprev_buf; bgb[1] = gb[0];
+          nbr = 2;
+          break;
+        }
+        if (fabsf(gtd_new) <= -c2 * gtd) {
+          br[0] = t; bf[0] = f_new; bgb[0] = gb[0];
+          nbr = 1;
+          done = true;
+          break;
+        }
+        if (gtd_new >= 0.f) {
+          br[0] = t_prev; br[1] = t; bf[0] = f_prev; bf[1] = f_new; bgtd[0] = gtd_prev; bgtd[1] = gtd_new;
+          bgb[0] = gprev_buf; bgb[1] = gb[0];
+          nbr = 2;
+          break;
+        }
+        const float min_step = t + 0.01f * (t - t_prev), max_step = t * 10.f;
+        const float tmp = t;
+        t = glue_cubic(t_prev, f_prev, gtd_prev, t, f_new, gtd_new, true, min_step, max_step);
+        t_prev = tmp;
+        f_prev = f_new;
+        {
+          const int old_prev = gprev_buf;
+          gprev_buf = gb[0];
+          gb[0] = (old_prev < 0) ? gb[1] : old_prev;
+          if (gb[0] == gprev_buf) gb[0] = gb[2];
+        }
+        gtd_prev = gtd_new;
+        gnew = vec(gb[0]);
+        f_new = eval_at(t, gnew);
+        ls_evals++;
+        gtd_new = w_dot(gnew, d, np);
+        ls_iter++;
+      }
+      if (ls_iter == max_ls) {
+        br[0] = 0.f; br[1] = t; bf[0] = f; bf[1] = f_new; bgb[0] = -1; bgb[1] = gb[0];
+        bgtd[0] = gtd; bgtd[1] = gtd_new;
+        nbr = 2;
+      }
+      int low = 0, high = 1;
+      if (nbr == 2) {
+        low = bf[0] <= bf[1] ? 0 : 1;
+        high = 1 - low;
+      }
+      bool insuf = false;
+      while (!done && ls_iter < max_ls) {
+        if (fabsf(br[1] - br[0]) * d_norm < tol_change) break;
+        t = glue_cubic(br[0], bf[0], bgtd[0], br[1], bf[1], bgtd[1], false, 0.f, 0.f);
+        const float bmax = fmaxf(br[0], br[1]), bmin = fminf(br[0], br[1]);
+        const float eps = 0.1f * (bmax - bmin);
+        if (fminf(bmax - t, t - bmin) < eps) {
+          if (insuf || t >= bmax || t <= bmin) {
+            t = (fabsf(t - bmax) < fabsf(t - bmin)) ? bmax - eps : bmin + eps;
+            insuf = false;
+          } else {
+            insuf = true;
+          }
+        } else {
+          insuf = false;
+        }
+        int fb = 6;
+        while (fb == bgb[0] || fb == bgb[1]) fb++;
+        gnew = vec(fb);
+        f_new = eval_at(t, gnew);
+        ls_evals++;
+        gtd_new = w_dot(gnew, d, np);
+        ls_iter++;
+        if ((float)f_new > (float)(f + (double)(c1 * t * gtd)) || f_new >= bf[low]) {
+          br[high] = t; bf[high] = f_new; bgb[high] = fb; bgtd[high] = gtd_new;
+          low = bf[0] <= bf[1] ? 0 : 1;
+          high = 1 - low;
+        } else {
+          if (fabsf(gtd_new) <= -c2 * gtd) {
+            done = true;
+          } else if (gtd_new * (br[high] - br[low]) >= 0.f) {
+            br[high] = br[low]; bf[high] = bf[low]; bgb[high] = bgb[low]; bgtd[high] = bgtd[low];
+          }
+          br[low] = t; bf[low] = f_new; bgb[low] = fb; bgtd[low] = gtd_new;
+        }
+      }
+      t = br[low];
+      loss = bf[low];
+      if (bgb[low] >= 0) w_copy(fg, vec(bgb[low]), np);
+      for (int64_t i = lane; i < np; i += GW) x[i] = xi[i] + t * d[i];
+      amax = vmaxabs(fg);
+      const bool opt_cond = amax <= tol_grad;
+      evals += ls_evals;
+      if (n_iter == max_iter) break;
+      if (evals >= max_eval) break;
+      if (opt_cond) break;
+      float dmax = 0.f;
+      for (int64_t i = lane; i < np; i += GW) dmax = fmaxf(dmax, fabsf(d[i] * t));
+      if (w_maxf(dmax) <= tol_change) break;
+      if (fabs(loss - prev_loss) < (double)tol_change) break;
+    }
+  }
+  for (int64_t i = lane; i < np; i += GW) xout[3 * g0 + i] = glue_wrap(x[i]);
+  if (lane == 0) {
+    stats[2 * s] = n_iter;
+    stats[2 * s + 1] = evals;
+    losses[2 * s] = loss0;
+    losses[2 * s + 1] = loss;
+  }
+}
+
 }  // namespace gb

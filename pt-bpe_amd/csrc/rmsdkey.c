@@ -1,0 +1,234 @@
+/* rmsdkey.c -- the pair key of the RMSD-partitioned mode (geobpe/rmsd_bpe.py RmsdBPE._pair_key),
+ * the host hot spot of a step: the reference's compute_geo_key (foldingdiff/bpe.py:1192-1299)
+ * reads a span's geometry (Tokenizer.token_geo, tokenizer.py:169-202), bins the items the pt1 /
+ * pt2 rules select (bpe.py:1247-1285, get_ind :1164-1189) and renders
+ * json.dumps(geo, sort_keys=True) (bpe.py:1147-1149), floats as Python's repr.
+ *
+ * A CPython extension so that it reads the chain's column lists in place (the host class keeps
+ * them as Python lists; set_token_geo writes single cells).  Floats are formatted by
+ * PyOS_double_to_string(v, 'r', 0, Py_DTSF_ADD_DOT_0) -- the routine float.__repr__ uses -- and
+ * non-finite values as json does (NaN, Infinity, -Infinity).  A value outside the bins raises
+ * the reference's ValueError with its message.
+ *
+ * key(cols, init, idx, l, ph, rng, thr) -> str
+ *   cols  tuple of 9 column lists in ITEM order (below); init: list of 3 floats
+ *   idx, l: the span (first bond, bonds); ph = idx % 3
+ *   rng   ((lo, hi) per kind: bonds, angles, dihedrals) of the binned item indices
+ *   thr   tuple of 9 (lefts, rights) float lists per item type, or None (type never binned)
+ */
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <math.h>
+#include <string.h>
+
+/* item types in json.dumps(sort_keys=True) order: name, kind (0 bond, 1 angle, 2 dihedral),
+ * position of the type's first item within a residue (bpe.py's _ITEM) */
+static const char* NAMES[9] = {"0C:1N", "C:1N:1CA", "CA:C", "CA:C:1N", "N:CA", "omega", "phi", "psi", "tau"};
+static const int KIND[9] = {0, 1, 0, 1, 0, 2, 2, 2, 1};
+static const int T0[9] = {2, 2, 1, 1, 0, 1, 2, 0, 0};
+static const double TWO_PI = 6.283185307179586; /* 2 * np.pi */
+
+typedef struct {
+  char* p;
+  Py_ssize_t n, cap;
+} Buf;
+
+static int buf_put(Buf* b, const char* s, Py_ssize_t n) {
+  if (b->n + n > b->cap) {
+    Py_ssize_t c = b->cap ? b->cap : 512;
+    while (c < b->n + n) c *= 2;
+    char* q = (char*)PyMem_Realloc(b->p, c);
+    if (!q) {
+      PyErr_NoMemory();
+      return -1;
+    }
+    b->p = q;
+    b->cap = c;
+  }
+  memcpy(b->p + b->n, s, n);
+  b->n += n;
+  return 0;
+}
+static int buf_str(Buf* b, const char* s) { return buf_put(b, s, (Py_ssize_t)strlen(s)); }
+
+static int put_float(Buf* b, double v) {
+  if (isnan(v)) return buf_str(b, "NaN");
+  if (isinf(v)) return buf_str(b, v > 0 ? "Infinity" : "-Infinity");
+  char* s = PyOS_double_to_string(v, 'r', 0, Py_DTSF_ADD_DOT_0, NULL);
+  if (!s) return -1;
+  int rc = buf_str(b, s);
+  PyMem_Free(s);
+  return rc;
+}
+
+/* Python's float % for a positive divisor (float_rem) */
+static double py_mod(double x, double y) {
+  double m = fmod(x, y);
+  if (m) {
+    if ((y < 0) != (m < 0)) m += y;
+  } else {
+    m = copysign(0.0, y);
+  }
+  return m;
+}
+
+/* BPE.get_ind (bpe.py:1164-1189): bisect_right over the left edges; -1 with ValueError set */
+static long get_ind(double v, PyObject* lefts, PyObject* rights) {
+  Py_ssize_t n = PyList_GET_SIZE(lefts), lo = 0, hi = n;
+  while (lo < hi) { /* bisect_right */
+    Py_ssize_t mid = (lo + hi) / 2;
+    if (v < PyFloat_AS_DOUBLE(PyList_GET_ITEM(lefts, mid)))
+      hi = mid;
+    else
+      lo = mid + 1;
+  }
+  Py_ssize_t ind = lo - 1;
+  PyObject* fv;
+  if (ind < 0) {
+    fv = PyFloat_FromDouble(v);
+    if (fv) {
+      PyErr_Format(PyExc_ValueError, "value %R is below the first bin range", fv);
+      Py_DECREF(fv);
+    }
+    return -1;
+  }
+  double a = PyFloat_AS_DOUBLE(PyList_GET_ITEM(lefts, ind)), b = PyFloat_AS_DOUBLE(PyList_GET_ITEM(rights, ind));
+  if (ind == n - 1 && v == b) return (long)ind;
+  if (a <= v && v < b) return (long)ind;
+  fv = PyFloat_FromDouble(v);
+  if (fv) {
+    PyErr_Format(PyExc_ValueError, "value %R does not fall into any bin", fv);
+    Py_DECREF(fv);
+  }
+  return -1;
+}
+
+static Py_ssize_t cnt_range(Py_ssize_t a, Py_ssize_t stop) { return a < stop ? (stop - a + 2) / 3 : 0; }
+static Py_ssize_t floordiv3(Py_ssize_t x) { return x >= 0 ? x / 3 : -((-x + 2) / 3); }
+
+/* value m of item type t of the span: token_geo's slices (init values in front of a column's rows) */
+static int item_value(PyObject* cols, PyObject* init, int t, Py_ssize_t first, Py_ssize_t m, double* out) {
+  PyObject* col = PyTuple_GET_ITEM(cols, t);
+  Py_ssize_t row;
+  const int kind = KIND[t];
+  if (kind == 0) { /* bond j = first (< 2: init[j], then rows from 0) */
+    if (first < 2) {
+      if (m == 0) {
+        *out = PyFloat_AsDouble(PyList_GET_ITEM(init, first));
+        return 0;
+      }
+      row = m - 1;
+    } else {
+      row = (first - 2) / 3 + m;
+    }
+  } else if (kind == 1) { /* angle a = first (0: init[2]) */
+    if (first == 0) {
+      if (m == 0) {
+        *out = PyFloat_AsDouble(PyList_GET_ITEM(init, 2));
+        return 0;
+      }
+      row = m - 1;
+    } else {
+      row = (first - 1) / 3 + m;
+    }
+  } else {
+    row = (first + 1) / 3 + m;
+  }
+  if (row < 0 || row >= PyList_GET_SIZE(col)) {
+    PyErr_SetString(PyExc_IndexError, "rmsdkey: span outside the chain");
+    return -1;
+  }
+  *out = PyFloat_AsDouble(PyList_GET_ITEM(col, row));
+  return PyErr_Occurred() ? -1 : 0;
+}
+
+static PyObject* key(PyObject* self, PyObject* args) {
+  PyObject *cols, *init, *rng, *thr;
+  Py_ssize_t idx, l, ph;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!O!nnnO!O!", &PyTuple_Type, &cols, &PyList_Type, &init, &idx, &l, &ph, &PyTuple_Type,
+                        &rng, &PyTuple_Type, &thr))
+    return NULL;
+  if (PyTuple_GET_SIZE(cols) != 9 || PyTuple_GET_SIZE(thr) != 9 || PyTuple_GET_SIZE(rng) != 3 ||
+      PyList_GET_SIZE(init) < 3) {
+    PyErr_SetString(PyExc_ValueError, "rmsdkey.key: bad argument shapes");
+    return NULL;
+  }
+  for (int t = 0; t < 9; t++)
+    if (!PyList_Check(PyTuple_GET_ITEM(cols, t))) {
+      PyErr_SetString(PyExc_TypeError, "rmsdkey.key: columns must be lists");
+      return NULL;
+    }
+  Py_ssize_t lo[3], hi[3];
+  for (int k = 0; k < 3; k++) {
+    PyObject* p = PyTuple_GET_ITEM(rng, k);
+    if (!PyArg_ParseTuple(p, "nn", &lo[k], &hi[k])) return NULL;
+  }
+  Buf b = {NULL, 0, 0};
+  int first_key = 1;
+  char num[32];
+  if (buf_str(&b, "{") < 0) goto fail;
+  for (int t = 0; t < 9; t++) {
+    const int kind = KIND[t];
+    /* the type's first item in the span and its count (token_geo: bonds over l, angles over
+       l - 1, dihedrals over l - 2 items; type j % 3 of the first three) */
+    const Py_ssize_t nitems = kind == 0 ? l : (kind == 1 ? l - 1 : l - 2);
+    Py_ssize_t first = -1;
+    for (Py_ssize_t j = idx; j < idx + (nitems < 3 ? nitems : 3); j++) {
+      const int tt = kind == 0 ? (int)(j % 3) : (int)(j % 3);
+      /* type of item j: BOND_TYPES / BOND_ANGLES / DIHEDRALS [j % 3] */
+      static const int BT[3] = {4, 2, 0}, BA[3] = {8, 3, 1}, DH[3] = {7, 5, 6};
+      const int ty = kind == 0 ? BT[tt] : (kind == 1 ? BA[tt] : DH[tt]);
+      if (ty == t) {
+        first = j;
+        break;
+      }
+    }
+    if (first < 0) continue;
+    const Py_ssize_t cnt = cnt_range(first, idx + nitems);
+    /* binned items m in [m_lo, m_hi): base + 3m in [lo, hi), base = (t0 + 3 - ph) % 3 */
+    const Py_ssize_t base = (T0[t] + 3 - ph) % 3;
+    Py_ssize_t m_lo = 0, m_hi = 0;
+    if (lo[kind] < hi[kind]) {
+      m_lo = -floordiv3(base - lo[kind]);
+      if (m_lo < 0) m_lo = 0;
+      m_hi = -floordiv3(base - hi[kind]);
+      if (m_hi > cnt) m_hi = cnt;
+    }
+    PyObject* th = PyTuple_GET_ITEM(thr, t);
+    if (m_lo < m_hi && (th == Py_None || !PyTuple_Check(th) || PyTuple_GET_SIZE(th) != 2)) {
+      PyErr_SetString(PyExc_ValueError, "rmsdkey.key: no thresholds for a binned item type");
+      goto fail;
+    }
+    if (!first_key && buf_str(&b, ", ") < 0) goto fail;
+    first_key = 0;
+    if (buf_str(&b, "\"") < 0 || buf_str(&b, NAMES[t]) < 0 || buf_str(&b, "\": [") < 0) goto fail;
+    for (Py_ssize_t m = 0; m < cnt; m++) {
+      double v;
+      if (item_value(cols, init, t, first, m, &v) < 0) goto fail;
+      if (m && buf_str(&b, ", ") < 0) goto fail;
+      if (m >= m_lo && m < m_hi) {
+        const double q = kind == 0 ? v : py_mod(v + TWO_PI, TWO_PI);
+        const long ind = get_ind(q, PyTuple_GET_ITEM(th, 0), PyTuple_GET_ITEM(th, 1));
+        if (ind < 0) goto fail;
+        snprintf(num, sizeof num, "%ld", ind);
+        if (buf_str(&b, num) < 0) goto fail;
+      } else if (put_float(&b, v) < 0) {
+        goto fail;
+      }
+    }
+    if (buf_str(&b, "]") < 0) goto fail;
+  }
+  if (buf_str(&b, "}") < 0) goto fail;
+  PyObject* out = PyUnicode_FromStringAndSize(b.p, b.n);
+  PyMem_Free(b.p);
+  return out;
+fail:
+  PyMem_Free(b.p);
+  return NULL;
+}
+
+static PyMethodDef METHODS[] = {{"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
+                                {NULL, NULL, 0, NULL}};
+static struct PyModuleDef MOD = {PyModuleDef_HEAD_INIT, "_rmsdkey", NULL, -1, METHODS, NULL, NULL, NULL, NULL};
+PyMODINIT_FUNC PyInit__rmsdkey(void) { return PyModule_Create(&MOD); }

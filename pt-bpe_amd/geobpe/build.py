@@ -38,5 +38,26 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return OUT
 
 
+KEY_SRC = os.path.join(CSRC, "rmsdkey.c")
+KEY_OUT = os.path.join(HERE, "_rmsdkey.so")
+
+
+def build_keys(force: bool = False, verbose: bool = False) -> str:
+    """The RMSD mode's pair-key builder (csrc/rmsdkey.c), a CPython extension built with gcc."""
+    import sysconfig
+    if not force and os.path.exists(KEY_OUT) and os.path.getmtime(KEY_SRC) <= os.path.getmtime(KEY_OUT):
+        return KEY_OUT
+    cmd = [shutil.which("gcc") or "gcc", "-O2", "-shared", "-fPIC", "-Wall", f"-I{sysconfig.get_paths()['include']}",
+           KEY_SRC, "-o", KEY_OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"gcc failed:\n{r.stderr[-4000:]}")
+    os.replace(KEY_OUT + ".tmp", KEY_OUT)
+    return KEY_OUT
+
+
 if __name__ == "__main__":
     print(build(force=True, verbose=True))
+    print(build_keys(force=True, verbose=True))

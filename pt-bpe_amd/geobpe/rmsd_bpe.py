@@ -58,6 +58,23 @@ TWO_PI = 2 * np.pi
 _ITEM = {k: (i, 0) for i, k in enumerate(BOND_TYPES)} | {k: (i, 1) for i, k in enumerate(BOND_ANGLES)} | \
     {k: (i, 2) for i, k in enumerate(DIHEDRALS)}
 _ENC = json.JSONEncoder(sort_keys=True)  # json.dumps(geo, sort_keys=True) (bpe.py:1147-1149)
+_KEY_ORDER = sorted(_ITEM)  # json key order of the nine item types
+
+
+def _load_keyc():
+    """The C pair-key builder (csrc/rmsdkey.c, built in-tree by geobpe/build.py)."""
+    import importlib.util
+    import os
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_rmsdkey.so")
+    if not os.path.exists(path):
+        return None
+    spec = importlib.util.spec_from_file_location("_rmsdkey", path)
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+_KEYC = _load_keyc()
 RES_SPHERE_KEY = {3: '{"N:CA": [0], "CA:C": [0], "0C:1N": [0], "tau": [0], "CA:C:1N": [0], "psi": [0]}',
                   2: '{"CA:C": [0], "0C:1N": [0], "CA:C:1N": [0]}'}
 
@@ -260,6 +277,8 @@ class RmsdBPE:
     """foldingdiff.bpe.BPE with a finite rmsd_partition_min_size (see the module docstring).
     Constructed by ``geobpe.bpe.BPE(...)`` when the arguments ask for this mode."""
 
+    _py_keys = False  # True: the pair keys in Python (_pair_key_py) instead of csrc/rmsdkey.c
+
     def __init__(self, structures, bins, bin_strategy="histogram", save_dir="./plots/bpe",
                  compute_sec_structs=False, plot_iou_with_sec_structs=False, res_init=False, std_bonds=True,
                  rmsd_partition_min_size=4, rmsd_super_res=False, rmsd_only=False, num_partitions=3,
@@ -377,6 +396,7 @@ class RmsdBPE:
                 thr[size].update(grid)
         self._thresholds = thr
         self._thr_by_len = {}
+        self._key_edges = {}
         ro = self._corpus["row_off"]
         init = _rmsd.init_geometry()
         self._chains = []
@@ -586,12 +606,6 @@ class RmsdBPE:
             raise RuntimeError("pair of one token")  # the reference stops in breakpoint() here
         pt1, pt2 = isinstance(t1[1], tuple), isinstance(t2[1], tuple)
         L = l1 + l2
-        geo = c.geo(idx1, L)
-        ph = idx1 % 3
-        thr_all = self._thresholds
-        thr_L = self._thr_by_len.get(L)
-        if thr_L is None:
-            thr_L = self._thr_by_len[L] = thr_all[L]
         # which span items are quantized (bpe.py:1247-1285), as a range [lo, hi) of the
         # item's index i within the span, per kind (bond, angle, dihedral)
         if pt1 and pt2:
@@ -602,6 +616,42 @@ class RmsdBPE:
             rng = ((0, l1), (0, l1), (0, l1))
         else:
             rng = ((0, L), (0, L), (0, L))
+        if _KEYC is not None and not self._py_keys:
+            if idx1 + L - 1 > 3 * c.n - 1:
+                raise ValueError(f"idx+l cannot exceed {3 * c.n - 1}")
+            edges = self._key_edges.get(L)
+            if edges is None:
+                edges = self._key_edges[L] = self._edges_for(L)
+            cur = c.cur
+            return _KEYC.key(tuple(cur[k] for k in _KEY_ORDER), c.init, idx1, L, idx1 % 3, rng, edges)
+        return self._pair_key_py(c, idx1, L, rng)
+
+    def _edges_for(self, L):
+        """The (left edges, right edges) lists of every item type's thresholds at span length L,
+        in json key order (rmsdkey.c's layout); None for a type whose thresholds do not exist."""
+        thr_all = self._thresholds
+        thr_L = self._thr_by_len.get(L)
+        if thr_L is None:
+            thr_L = self._thr_by_len[L] = thr_all[L]
+        out = []
+        for k in _KEY_ORDER:
+            kind = _ITEM[k][1]
+            try:
+                thr = (thr_all[k] if self.std_bonds else thr_L[k]) if kind == 0 else thr_L[k]
+                out.append(([float(a) for a, _ in thr], [float(b) for _, b in thr]))
+            except (KeyError, TypeError):
+                out.append(None)  # (the C key raises only if such a type is binned: then the
+        return tuple(out)         #  Python restatement reproduces the reference's error)
+
+    def _pair_key_py(self, c, idx1, L, rng):
+        """_pair_key in Python: the restatement rmsdkey.c follows (and the path taken for
+        its errors, so the reference's exceptions surface unchanged)."""
+        geo = c.geo(idx1, L)
+        ph = idx1 % 3
+        thr_all = self._thresholds
+        thr_L = self._thr_by_len.get(L)
+        if thr_L is None:
+            thr_L = self._thr_by_len[L] = thr_all[L]
         for k, vals in geo.items():
             t0, kind = _ITEM[k]
             lo, hi = rng[kind]
@@ -1165,6 +1215,7 @@ class RmsdBPE:
             thr[k] = v
         self._thresholds = thr
         self._thr_by_len = {}
+        self._key_edges = {}
         self._tokens = dict(obj._tokens)
         self._sphere_dict = dict(obj._sphere_dict)
         self.num_partitions = getattr(obj, "num_partitions", 3)

@@ -310,3 +310,54 @@ def _induce_cli(name, tmp_path):
         got = [[s0, list(v[1]) if isinstance(v[1], tuple) else v[1], v[2]] for s0, v in t._bond_to_token.items()]
         assert got == meta["induce"][i]["segmentation"]
     assert (out / "utility.json").exists()
+
+
+@pytest.mark.parametrize("name", ["rm_p0_multigrid", "rm_p3_super_multigrid", "rm_p2_freebonds_multigrid"])
+def test_pair_key_c_matches_python(name, host_geometry):
+    """csrc/rmsdkey.c (the pair key the host bookkeeping derives twice per merged occurrence)
+    against its Python restatement RmsdBPE._pair_key_py, on every adjacent token pair of every
+    chain after initialize(), after 6 merges and after 12 (partitioned and plain tokens, pt1 /
+    pt2 mixes, several grids); then a value outside the bins raises the same ValueError."""
+    from geobpe import rmsd_bpe
+    from geobpe.bpe import BPE
+    assert rmsd_bpe._KEYC is not None, "pt-bpe_amd/geobpe/_rmsdkey.so is not built (geobpe/build.py)"
+    meta, corpus, arrs = _load(name)
+    if "init_tokens" not in meta:
+        pytest.skip("the reference raised in initialize()")
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()}, rmsd_partition_min_size=meta["rmsd_partition_min_size"],
+              rmsd_super_res=meta["rmsd_super_res"], num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta.get("std_bonds", True),
+              seed=meta["rng_seed"])
+    bpe.initialize()
+    bpe.bin()
+
+    def both(ci, i1, l1, l2):
+        def one(py):
+            bpe._py_keys = py
+            try:
+                return bpe._pair_key(ci, i1, l1, l2)
+            except ValueError as e:
+                return ("ValueError", str(e))
+            finally:
+                bpe._py_keys = False
+        return one(False), one(True)
+
+    n = 0
+    for steps in (0, 6, 6):
+        for _ in range(steps):
+            bpe.step()
+        for ci, c in enumerate(bpe._chains):
+            toks = c.tokens()
+            for (i1, _, l1), (_, _, l2) in zip(toks, toks[1:]):
+                kc, kp = both(ci, i1, l1, l2)
+                assert kc == kp, (ci, i1, l1, l2)
+                n += 1
+    assert n > 500
+    # a value outside every bin: the reference's ValueError, the same message both ways
+    c = bpe._chains[0]
+    toks = c.tokens()
+    (i1, _, l1), (_, _, l2) = toks[0], toks[1]
+    for k in ("psi", "tau", "CA:C:1N"):
+        c.cur[k] = [v + 40.0 for v in c.cur[k]]
+    kc, kp = both(0, i1, l1, l2)
+    assert kc == kp

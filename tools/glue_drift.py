@@ -3,6 +3,7 @@
 
   python tools/glue_drift.py oracle OUT.npz [N]   (CPU: problems + the oracle's optimum)
   python tools/glue_drift.py device OUT.npz       (GPU box: device optimum vs the saved one;
+                                                   tests/golden/glue_drift_oracle.npz holds N = 120;
                                                    GEOBPE_LIB selects an A/B build)
 
 Problems: N synthetic chains (geobpe.synth, seed 5, 20..40 residues), std bond lengths;
@@ -78,6 +79,12 @@ def main(argv):
         np.savez_compressed(path, n=n, opt=np.concatenate(opt), loss=np.array(loss))
         print(f"oracle: {n} chains saved to {path}")
         return
+    print(json.dumps(device_stats(path)))
+
+
+def device_stats(path):
+    """The device optimum against the oracle's saved one: drift quantiles (rad), the share of
+    glues snapping to the same bin, final-loss ratio quantiles."""
     from geobpe import glue
     z = np.load(path)
     geos, x0s, R, T, thr = problems(int(z["n"]))
@@ -94,7 +101,7 @@ def main(argv):
            "drift_rad": {q: float(np.quantile(d, p)) for q, p in (("p50", .5), ("p90", .9), ("p99", .99), ("max", 1.0))},
            "same_bin": float(same.mean()), "loss_ratio": {"min": float(lr.min()), "p50": float(np.median(lr)),
                                                            "max": float(lr.max())}}
-    print(json.dumps(out))
+    return out
 
 
 if __name__ == "__main__":
