@@ -67,6 +67,19 @@ def start(l_ca_c, l_n_ca, theta):
     return ca + rv / np.linalg.norm(rv) * l_n_ca, ca, C_INIT.copy()
 
 
+def nerf_packed(off, packed) -> list:
+    """nerf() of spans in geobpe_nerf's packed layout (9 per residue: N:CA, CA:C, tau, 0C:1N,
+    CA:C:1N, C:1N:1CA, psi, omega, phi; off[n + 1] residue offsets) -- the CPU stand-in for
+    geobpe.rmsd.nerf_packed."""
+    cols = ["N:CA", "CA:C", "tau", "0C:1N", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"]
+    out = []
+    for a, b in zip(off[:-1], off[1:]):
+        blk = np.asarray(packed[a:b])
+        r = b - a
+        out.append(nerf({k: list(blk[:r if c < 3 else r - 1, c]) for c, k in enumerate(cols)}))
+    return out
+
+
 def nerf(geo: dict) -> np.ndarray:
     """Tokenizer.geo_nerf(geo).cartesian_coords (3r - 1 bonds -> 3r atoms)."""
     r = len(geo["N:CA"])

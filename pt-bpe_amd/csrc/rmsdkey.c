@@ -228,7 +228,66 @@ fail:
   return NULL;
 }
 
+/* pack(spans, out) -- the whole-residue geometry of many spans in geobpe_nerf's layout
+ * (9 float64 per residue: N:CA, CA:C, tau, 0C:1N, CA:C:1N, C:1N:1CA, psi, omega, phi; the last
+ * residue of a span only its first three), the token_geo of Tokenizer.compute_coords
+ * (tokenizer.py:347-363) without the dicts.  spans: list of (cols, init, q, r) -- the chain's
+ * nine column lists in that order, its init triple, the first residue q and the residues r;
+ * out: a writable C-contiguous float64 buffer of sum(r) * 9.  Residue q + k reads row
+ * q + k - 1 of N:CA / CA:C / tau (residue 0: init) and row q + k of the junction columns
+ * (phi: row q + k + 1) -- bond j -> row (j - 2) // 3, angle a -> (a - 1) // 3, dihedral d ->
+ * (d + 1) // 3 (rmsd_bpe._Chain). */
+static PyObject* pack(PyObject* self, PyObject* args) {
+  PyObject* spans;
+  Py_buffer out;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!w*", &PyList_Type, &spans, &out)) return NULL;
+  double* o = (double*)out.buf;
+  const Py_ssize_t cap = out.len / (Py_ssize_t)sizeof(double);
+  Py_ssize_t at = 0;
+  for (Py_ssize_t i = 0; i < PyList_GET_SIZE(spans); i++) {
+    PyObject *cols, *init;
+    Py_ssize_t q, r;
+    if (!PyArg_ParseTuple(PyList_GET_ITEM(spans, i), "O!O!nn", &PyTuple_Type, &cols, &PyList_Type, &init, &q, &r))
+      goto fail;
+    if (PyTuple_GET_SIZE(cols) != 9 || PyList_GET_SIZE(init) < 3 || q < 0 || r < 1 || at + 9 * r > cap) {
+      PyErr_SetString(PyExc_ValueError, "rmsdkey.pack: bad span");
+      goto fail;
+    }
+    for (Py_ssize_t k = 0; k < r; k++, at += 9) {
+      const Py_ssize_t res = q + k;
+      for (int c = 0; c < 9; c++) {
+        double v = 0.0;
+        if (c < 3) {
+          if (res == 0) {
+            v = PyFloat_AsDouble(PyList_GET_ITEM(init, c));
+          } else {
+            PyObject* col = PyTuple_GET_ITEM(cols, c);
+            if (res - 1 >= PyList_GET_SIZE(col)) goto range;
+            v = PyFloat_AsDouble(PyList_GET_ITEM(col, res - 1));
+          }
+        } else if (k + 1 < r) {
+          PyObject* col = PyTuple_GET_ITEM(cols, c);
+          const Py_ssize_t row = c == 8 ? res + 1 : res;
+          if (row >= PyList_GET_SIZE(col)) goto range;
+          v = PyFloat_AsDouble(PyList_GET_ITEM(col, row));
+        }
+        if (v == -1.0 && PyErr_Occurred()) goto fail;
+        o[at + c] = v;
+      }
+    }
+  }
+  PyBuffer_Release(&out);
+  return PyLong_FromSsize_t(at / 9);
+range:
+  PyErr_SetString(PyExc_IndexError, "rmsdkey.pack: span outside the chain");
+fail:
+  PyBuffer_Release(&out);
+  return NULL;
+}
+
 static PyMethodDef METHODS[] = {{"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
+                                {"pack", pack, METH_VARARGS, "whole-residue span geometry, geobpe_nerf layout"},
                                 {NULL, NULL, 0, NULL}};
 static struct PyModuleDef MOD = {PyModuleDef_HEAD_INIT, "_rmsdkey", NULL, -1, METHODS, NULL, NULL, NULL, NULL};
 PyMODINIT_FUNC PyInit__rmsdkey(void) { return PyModule_Create(&MOD); }

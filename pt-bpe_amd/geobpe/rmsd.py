@@ -83,8 +83,9 @@ def k_medoids_from_matrix(D: np.ndarray, k, max_iterations: int = 10, tol: float
     medoid_indices = rng.choice(np.arange(N), size=k, replace=False)
     assignments = np.zeros(N, dtype=int)
     for iteration in range(max_iterations):
-        for i in range(N):
-            assignments[i] = np.argmin(D[i, medoid_indices])
+        # (the reference's per-row np.argmin, all rows at once: the same float32 values, the
+        # same first-minimum rule)
+        assignments[:] = np.argmin(D[:, medoid_indices], axis=1)
         total_shift = 0.0
         new_medoid_indices = []
         for j in range(k):
@@ -148,7 +149,6 @@ def token_geo(cols: dict, idx: int, l: int, init=None) -> dict:
 def geo_coords(geos, device: int = 0):
     """Tokenizer.geo_nerf(geo).cartesian_coords for a batch of whole-residue geometry
     dicts (3r - 1 bonds each), on the device (csrc/rmsd.h k_nerf): [(3r, 3)]."""
-    L = _native.lib()
     rs = []
     for g in geos:
         nb = sum(len(g.get(k, [])) for k in BOND_TYPES)
@@ -165,13 +165,21 @@ def geo_coords(geos, device: int = 0):
         if r > 1:
             for c, k in enumerate(["0C:1N", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"], start=3):
                 blk[:r - 1, c] = g[k]
+    return nerf_packed(off, packed, device)
+
+
+def nerf_packed(off: np.ndarray, packed: np.ndarray, device: int = 0):
+    """geobpe_nerf on spans already packed (9 float64 per residue, off[n + 1] residue
+    offsets): [(3r, 3)] atoms per span."""
+    L = _native.lib()
+    R = int(off[-1])
     xyz = np.empty((max(R, 1), 3, 3), dtype=np.float64)
     if R:
-        rc = L.geobpe_nerf(int(device), len(geos), off.ctypes.data_as(ctypes.c_void_p),
+        rc = L.geobpe_nerf(int(device), len(off) - 1, off.ctypes.data_as(ctypes.c_void_p),
                            packed.ctypes.data_as(ctypes.c_void_p), xyz.ctypes.data_as(ctypes.c_void_p))
         if rc:
             raise _native.GeoBPEError(f"geobpe_nerf failed (code {rc})")
-    return [xyz[a:a + r].reshape(3 * r, 3) for a, r in zip(off[:-1], rs)]
+    return [xyz[a:b].reshape(3 * (b - a), 3) for a, b in zip(off[:-1], off[1:])]
 
 
 def compute_coords(cols: dict, spans, init=None, device: int = 0):

@@ -59,6 +59,7 @@ _ITEM = {k: (i, 0) for i, k in enumerate(BOND_TYPES)} | {k: (i, 1) for i, k in e
     {k: (i, 2) for i, k in enumerate(DIHEDRALS)}
 _ENC = json.JSONEncoder(sort_keys=True)  # json.dumps(geo, sort_keys=True) (bpe.py:1147-1149)
 _KEY_ORDER = sorted(_ITEM)  # json key order of the nine item types
+_PACK_ORDER = ["N:CA", "CA:C", "tau", "0C:1N", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"]  # geobpe_nerf's
 
 
 def _load_keyc():
@@ -339,17 +340,28 @@ class RmsdBPE:
     def _span_coords(self, spans, orig):
         """Tokenizer.compute_coords(index, length, orig) for [(chain, index, length)], one
         device NeRF batch: the span rounded out to whole residues, then its atoms."""
-        geos, cuts = [], []
+        packs, geos, cuts = [], [], []
         for ci, index, length in spans:
             c = ci if isinstance(ci, _Chain) else self._chains[ci]
             length = min(length, 3 * c.n - 1 - index)
             start = 3 * (index // 3)
             end = 3 * (((index + length - 1) + 1) // 3) + 1
-            geos.append(c.geo(start, end - start + 1, orig))
+            if _KEYC is not None:  # (the span's residues straight into the NeRF layout, csrc/rmsdkey.c)
+                src = c.orig if orig else c.cur
+                packs.append((tuple(src[k] for k in _PACK_ORDER), c.init, start // 3, (end - start + 2) // 3))
+            else:
+                geos.append(c.geo(start, end - start + 1, orig))
             cuts.append((index - start, end - (index + length - 1)))
-        if not geos:
+        if not cuts:
             return []
-        xyz = _rmsd.geo_coords(geos, device=self.device)
+        if _KEYC is not None:
+            off = np.zeros(len(packs) + 1, dtype=np.int64)
+            np.cumsum([p[3] for p in packs], out=off[1:])
+            packed = np.zeros((int(off[-1]), 9), dtype=np.float64)
+            _KEYC.pack(packs, packed)
+            xyz = _rmsd.nerf_packed(off, packed, device=self.device)
+        else:
+            xyz = _rmsd.geo_coords(geos, device=self.device)
         return [x[a:len(x) - b] for x, (a, b) in zip(xyz, cuts)]
 
     def _struc_coords(self, strucs):
