@@ -112,11 +112,6 @@ struct geobpe_ctx {
   uint8_t *x_hsend = nullptr, *x_hrecv = nullptr;  // (host callback: pinned staging)
   int64_t x_hbytes = 0;
   int64_t x_ahead = 1, x_capf = 1024, x_fixed = 0;  // poll window and slot size carry over between runs
-  // a full-grid merge's k_place overlaps the collective and the import on a side stream (it
-  // needs only k_commit's output and writes no count); the next select waits for it
-  bool x_overlap = false;  // (GEOBPE_X_OVERLAP=1: on)
-  hipStream_t x_side = nullptr;
-  hipEvent_t x_ev_commit = nullptr, x_ev_place = nullptr;
   // profiling
   bool prof = false;
   int prof_stride = 1;      // time every prof_stride-th launch of each kernel
@@ -543,7 +538,6 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   }
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
-  if (const char* e = getenv("GEOBPE_X_OVERLAP")) c->x_overlap = atoi(e) != 0;  // (A/B: 0 = place in the select)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
@@ -565,10 +559,6 @@ void geobpe_destroy(geobpe_ctx* c) {
   if (c->comm && c->rccl.CommDestroy) c->rccl.CommDestroy(c->comm);
   for (uint8_t* p : {c->x_pbuf, c->x_gath, c->x_tmp, c->x_flat})
     if (p) hipFree(p);
-  if (c->x_side) hipStreamSynchronize(c->x_side);
-  if (c->x_ev_commit) hipEventDestroy(c->x_ev_commit);
-  if (c->x_ev_place) hipEventDestroy(c->x_ev_place);
-  if (c->x_side) hipStreamDestroy(c->x_side);
   if (c->x_hsend) hipHostFree(c->x_hsend);
   if (c->x_hrecv) hipHostFree(c->x_hrecv);
   for (auto e : c->evall) hipEventDestroy(e);
@@ -2049,12 +2039,6 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
     HIPCHK(c, hipMemsetAsync(c->x_pbuf, 0, (size_t)((1 + c->x_pcap) * REC), c->stream));
     HIPCHK(c, hipMalloc((void**)&c->x_gath, (size_t)(W * (1 + top) * REC)));
   }
-  const bool overlap = c->x_overlap && !c->ev;  // (merge events ride behind each commit: no overlap then)
-  if (overlap && !c->x_side) {
-    HIPCHK(c, hipStreamCreateWithFlags(&c->x_side, hipStreamNonBlocking));
-    HIPCHK(c, hipEventCreateWithFlags(&c->x_ev_commit, hipEventDisableTiming));
-    HIPCHK(c, hipEventCreateWithFlags(&c->x_ev_place, hipEventDisableTiming));
-  }
   if ((rc = geobpe_pipeline_begin(c))) return rc;
   int64_t out[4];
   int64_t done = 0;
@@ -2082,21 +2066,8 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
     const int64_t k = std::min(win, n_merges - done);  // an iteration merges at most once
     for (int64_t i = 0; i < k && !rc; i++) {
       if ((rc = geobpe_pipeline_iter(c, c->x_pbuf, c->x_pcap))) break;
-      // the full-grid place of this merge beside the collective and the import: it reads
-      // k_commit's key ids / log positions and writes tokens, pk and posting logs, which
-      // neither touches; the next select (which then launches without place workgroups)
-      // waits for it
-      const bool side = overlap && c->place_pending && !c->place_mid;
-      if (side) {
-        HIPCHK(c, hipEventRecord(c->x_ev_commit, c->stream));
-        HIPCHK(c, hipStreamWaitEvent(c->x_side, c->x_ev_commit, 0));
-        hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->x_side, c->D);
-        HIPCHK(c, hipEventRecord(c->x_ev_place, c->x_side));
-        c->place_pending = false;
-      }
       if ((rc = x_allgather(c, c->x_pbuf, c->x_gath, slot))) break;
       rc = geobpe_pipeline_import(c, c->x_gath, (int32_t)W, capf);
-      if (side) HIPCHK(c, hipStreamWaitEvent(c->stream, c->x_ev_place, 0));
     }
     if (rc || (rc = geobpe_pipeline_poll(c, out))) break;
     const bool stalled = out[0] != 0, fin = out[2] != 0;
