@@ -1,0 +1,64 @@
+// frepr.cpp -- Python's repr(float) for rmsdkey.c, from std::to_chars' shortest round-trip
+// digits (the same digits float.__repr__'s dtoa mode 0 picks; checked against repr on 3e5
+// values, tests/test_rmsd_mode.py): fixed notation for a decimal point in (-4, 16], else
+// d.ddde+XX with at least two exponent digits, ".0" after an integral fixed value.
+// ~10x faster than PyOS_double_to_string, which dominated a key's cost.
+#include <charconv>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+
+extern "C" int geobpe_py_repr(double v, char* out) {  // out: >= 32 bytes; returns the length
+  char buf[40];
+  auto r = std::to_chars(buf, buf + sizeof buf - 1, v, std::chars_format::scientific);
+  *r.ptr = 0;
+  const char* p = buf;
+  int o = 0;
+  if (*p == '-') {
+    out[o++] = '-';
+    p++;
+  }
+  char dig[32];
+  int n = 0;
+  while (*p && *p != 'e') {
+    if (*p != '.') dig[n++] = *p;
+    p++;
+  }
+  const int e = atoi(p + 1);
+  if (n == 1 && dig[0] == '0') {
+    memcpy(out + o, "0.0", 3);
+    return o + 3;
+  }
+  const int decpt = e + 1;
+  if (decpt > -4 && decpt <= 16) {
+    if (decpt <= 0) {
+      out[o++] = '0';
+      out[o++] = '.';
+      for (int i = 0; i < -decpt; i++) out[o++] = '0';
+      memcpy(out + o, dig, n);
+      o += n;
+    } else if (decpt >= n) {
+      memcpy(out + o, dig, n);
+      o += n;
+      for (int i = 0; i < decpt - n; i++) out[o++] = '0';
+      out[o++] = '.';
+      out[o++] = '0';
+    } else {
+      memcpy(out + o, dig, decpt);
+      o += decpt;
+      out[o++] = '.';
+      memcpy(out + o, dig + decpt, n - decpt);
+      o += n - decpt;
+    }
+  } else {
+    out[o++] = dig[0];
+    if (n > 1) {
+      out[o++] = '.';
+      memcpy(out + o, dig + 1, n - 1);
+      o += n - 1;
+    }
+    const int x = decpt - 1;
+    o += snprintf(out + o, 8, "e%c%02d", x < 0 ? '-' : '+', x < 0 ? -x : x);
+  }
+  return o;
+}

@@ -5,8 +5,8 @@
  * json.dumps(geo, sort_keys=True) (bpe.py:1147-1149), floats as Python's repr.
  *
  * A CPython extension so that it reads the chain's column lists in place (the host class keeps
- * them as Python lists; set_token_geo writes single cells).  Floats are formatted by
- * PyOS_double_to_string(v, 'r', 0, Py_DTSF_ADD_DOT_0) -- the routine float.__repr__ uses -- and
+ * them as Python lists; set_token_geo writes single cells).  Floats are formatted as
+ * float.__repr__ does (frepr.cpp: std::to_chars' shortest digits in Python's layout) and
  * non-finite values as json does (NaN, Infinity, -Infinity).  A value outside the bins raises
  * the reference's ValueError with its message.
  *
@@ -51,14 +51,32 @@ static int buf_put(Buf* b, const char* s, Py_ssize_t n) {
 }
 static int buf_str(Buf* b, const char* s) { return buf_put(b, s, (Py_ssize_t)strlen(s)); }
 
+int geobpe_py_repr(double v, char* out); /* frepr.cpp: repr(float) from std::to_chars */
+
 static int put_float(Buf* b, double v) {
   if (isnan(v)) return buf_str(b, "NaN");
   if (isinf(v)) return buf_str(b, v > 0 ? "Infinity" : "-Infinity");
-  char* s = PyOS_double_to_string(v, 'r', 0, Py_DTSF_ADD_DOT_0, NULL);
-  if (!s) return -1;
-  int rc = buf_str(b, s);
-  PyMem_Free(s);
-  return rc;
+  char s[40];
+  return buf_put(b, s, geobpe_py_repr(v, s));
+}
+
+/* repr(float) of each value (the test of frepr.cpp against Python's own repr) */
+static PyObject* reprs(PyObject* self, PyObject* args) {
+  PyObject* vals;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!", &PyList_Type, &vals)) return NULL;
+  PyObject* out = PyList_New(PyList_GET_SIZE(vals));
+  if (!out) return NULL;
+  for (Py_ssize_t i = 0; i < PyList_GET_SIZE(vals); i++) {
+    const double v = PyFloat_AsDouble(PyList_GET_ITEM(vals, i));
+    if (v == -1.0 && PyErr_Occurred()) {
+      Py_DECREF(out);
+      return NULL;
+    }
+    char s[40];
+    PyList_SET_ITEM(out, i, PyUnicode_FromStringAndSize(s, geobpe_py_repr(v, s)));
+  }
+  return out;
 }
 
 /* Python's float % for a positive divisor (float_rem) */
@@ -286,8 +304,95 @@ fail:
   return NULL;
 }
 
+/* setgeo(cols, init, idx, l, vals) -> bool -- Tokenizer.set_token_geo (tokenizer.py:253-286) as
+ * the host class does it (rmsd_bpe._Chain.set_geo): the span's bonds, angles and dihedrals take
+ * vals[type]'s items in order (the same objects), bond 0/1 and angle 0 going to init.  cols: the
+ * nine column lists in json key order (as key()).  Returns False, having written nothing, when
+ * a type is missing, too short or has items left over: the Python version then raises the
+ * reference's error. */
+static PyObject* setgeo(PyObject* self, PyObject* args) {
+  PyObject *cols, *init, *vals;
+  Py_ssize_t idx, l;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!O!nnO!", &PyTuple_Type, &cols, &PyList_Type, &init, &idx, &l, &PyDict_Type, &vals))
+    return NULL;
+  if (PyTuple_GET_SIZE(cols) != 9 || PyList_GET_SIZE(init) < 3 || idx < 0 || l < 1) {
+    PyErr_SetString(PyExc_ValueError, "rmsdkey.setgeo: bad arguments");
+    return NULL;
+  }
+  static const int BT[3] = {4, 2, 0}, BA[3] = {8, 3, 1}, DH[3] = {7, 5, 6};
+  PyObject* seq[9] = {NULL};
+  Py_ssize_t need[9] = {0}, pos[9] = {0};
+  for (Py_ssize_t j = idx; j < idx + l; j++) need[BT[j % 3]]++;
+  for (Py_ssize_t j = idx; j < idx + l - 1; j++) need[BA[j % 3]]++;
+  for (Py_ssize_t j = idx; j < idx + l - 2; j++) need[DH[j % 3]]++;
+  PyObject* ok = Py_True;
+  /* every type in vals must be used up exactly; every needed type present and long enough */
+  PyObject *k, *v;
+  Py_ssize_t it = 0;
+  while (PyDict_Next(vals, &it, &k, &v)) {
+    int t = -1;
+    for (int q = 0; q < 9; q++)
+      if (PyUnicode_Check(k) && PyUnicode_CompareWithASCIIString(k, NAMES[q]) == 0) t = q;
+    if (t < 0) {
+      ok = Py_False;
+      break;
+    }
+    PyObject* f = PySequence_Fast(v, "rmsdkey.setgeo: values must be sequences");
+    if (!f) goto fail;
+    seq[t] = f;
+    if (PySequence_Fast_GET_SIZE(f) != need[t]) ok = Py_False;
+  }
+  for (int t = 0; t < 9 && ok == Py_True; t++)
+    if (need[t] > 0 && !seq[t]) ok = Py_False;
+  if (ok == Py_True) {
+    /* bounds first (Python would raise IndexError midway): all rows inside their columns */
+    for (Py_ssize_t j = idx; j < idx + l && ok == Py_True; j++)
+      if (j >= 2 && (j - 2) / 3 >= PyList_GET_SIZE(PyTuple_GET_ITEM(cols, BT[j % 3]))) ok = Py_False;
+    for (Py_ssize_t j = idx; j < idx + l - 1 && ok == Py_True; j++)
+      if (j >= 1 && (j - 1) / 3 >= PyList_GET_SIZE(PyTuple_GET_ITEM(cols, BA[j % 3]))) ok = Py_False;
+    for (Py_ssize_t j = idx; j < idx + l - 2 && ok == Py_True; j++)
+      if ((j + 1) / 3 >= PyList_GET_SIZE(PyTuple_GET_ITEM(cols, DH[j % 3]))) ok = Py_False;
+  }
+  if (ok == Py_True) {
+#define SETGEO_PUT(LIST, ROW, T)                                     \
+  do {                                                              \
+    PyObject* x_ = PySequence_Fast_GET_ITEM(seq[T], pos[T]++);      \
+    Py_INCREF(x_);                                                  \
+    PyList_SetItem((LIST), (ROW), x_);                              \
+  } while (0)
+    for (Py_ssize_t j = idx; j < idx + l; j++) {
+      const int t = BT[j % 3];
+      if (j < 2)
+        SETGEO_PUT(init, j, t);
+      else
+        SETGEO_PUT(PyTuple_GET_ITEM(cols, t), (j - 2) / 3, t);
+    }
+    for (Py_ssize_t j = idx; j < idx + l - 1; j++) {
+      const int t = BA[j % 3];
+      if (j == 0)
+        SETGEO_PUT(init, 2, t);
+      else
+        SETGEO_PUT(PyTuple_GET_ITEM(cols, t), (j - 1) / 3, t);
+    }
+    for (Py_ssize_t j = idx; j < idx + l - 2; j++) {
+      const int t = DH[j % 3];
+      SETGEO_PUT(PyTuple_GET_ITEM(cols, t), (j + 1) / 3, t);
+    }
+#undef SETGEO_PUT
+  }
+  for (int t = 0; t < 9; t++) Py_XDECREF(seq[t]);
+  Py_INCREF(ok);
+  return ok;
+fail:
+  for (int t = 0; t < 9; t++) Py_XDECREF(seq[t]);
+  return NULL;
+}
+
 static PyMethodDef METHODS[] = {{"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
                                 {"pack", pack, METH_VARARGS, "whole-residue span geometry, geobpe_nerf layout"},
+                                {"reprs", reprs, METH_VARARGS, "repr(float) of each value (test)"},
+                                {"setgeo", setgeo, METH_VARARGS, "set_token_geo into the chain's column lists"},
                                 {NULL, NULL, 0, NULL}};
 static struct PyModuleDef MOD = {PyModuleDef_HEAD_INIT, "_rmsdkey", NULL, -1, METHODS, NULL, NULL, NULL, NULL};
 PyMODINIT_FUNC PyInit__rmsdkey(void) { return PyModule_Create(&MOD); }

@@ -39,22 +39,28 @@ def build(force: bool = False, verbose: bool = False) -> str:
 
 
 KEY_SRC = os.path.join(CSRC, "rmsdkey.c")
+KEY_CPP = os.path.join(CSRC, "frepr.cpp")
 KEY_OUT = os.path.join(HERE, "_rmsdkey.so")
 
 
 def build_keys(force: bool = False, verbose: bool = False) -> str:
     """The RMSD mode's pair-key builder (csrc/rmsdkey.c), a CPython extension built with gcc."""
     import sysconfig
-    if not force and os.path.exists(KEY_OUT) and os.path.getmtime(KEY_SRC) <= os.path.getmtime(KEY_OUT):
+    if not force and os.path.exists(KEY_OUT) and all(os.path.getmtime(f) <= os.path.getmtime(KEY_OUT)
+                                                     for f in (KEY_SRC, KEY_CPP)):
         return KEY_OUT
-    cmd = [shutil.which("gcc") or "gcc", "-O2", "-shared", "-fPIC", "-Wall", f"-I{sysconfig.get_paths()['include']}",
-           KEY_SRC, "-o", KEY_OUT + ".tmp"]
-    if verbose:
-        print(" ".join(cmd))
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise RuntimeError(f"gcc failed:\n{r.stderr[-4000:]}")
+    obj = KEY_OUT + ".frepr.o"
+    cmds = [[shutil.which("g++") or "g++", "-O2", "-fPIC", "-std=c++17", "-Wall", "-c", KEY_CPP, "-o", obj],
+            [shutil.which("gcc") or "gcc", "-O2", "-shared", "-fPIC", "-Wall", f"-I{sysconfig.get_paths()['include']}",
+             KEY_SRC, obj, "-lstdc++", "-o", KEY_OUT + ".tmp"]]
+    for cmd in cmds:
+        if verbose:
+            print(" ".join(cmd))
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"{cmd[0]} failed:\n{r.stderr[-4000:]}")
     os.replace(KEY_OUT + ".tmp", KEY_OUT)
+    os.remove(obj)
     return KEY_OUT
 
 

@@ -149,7 +149,12 @@ class _Chain:
         return out
 
     def set_geo(self, idx, l, vals):
-        """set_token_geo(idx, l, vals) (tokenizer.py:253-286): values consumed in order."""
+        """set_token_geo(idx, l, vals) (tokenizer.py:253-286): values consumed in order.  In C
+        (csrc/rmsdkey.c setgeo) when the values fit exactly; otherwise here, which raises the
+        reference's error at the same point."""
+        if _KEYC is not None and type(vals) is dict and \
+                _KEYC.setgeo(tuple(self.cur[k] for k in _KEY_ORDER), self.init, idx, l, vals):
+            return
         it = {k: iter(v) for k, v in vals.items()}
         for j in range(idx, idx + l):
             v = next(it[BOND_TYPES[j % 3]])

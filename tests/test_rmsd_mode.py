@@ -362,3 +362,65 @@ def test_pair_key_c_matches_python(name, host_geometry):
         c.cur[k] = [v + 40.0 for v in c.cur[k]]
     kc, kp = both(0, i1, l1, l2)
     assert kc == kp
+
+
+def test_key_float_repr_matches_python():
+    """csrc/frepr.cpp (std::to_chars' shortest digits laid out as float.__repr__ does) against
+    Python's repr on 200 000 doubles: random bit patterns (subnormals, huge exponents), scaled
+    uniforms across 40 decades, three-decimal values, and the edges of the fixed / exponent
+    layouts."""
+    from geobpe import rmsd_bpe
+    assert rmsd_bpe._KEYC is not None, "pt-bpe_amd/geobpe/_rmsdkey.so is not built (geobpe/build.py)"
+    rng = np.random.default_rng(17)
+    bits = rng.integers(0, 2 ** 63, size=80_000, dtype=np.int64).view(np.float64)
+    bits = bits[np.isfinite(bits)]
+    sc = rng.random(80_000) * 10.0 ** rng.integers(-20, 20, size=80_000)
+    dec = rng.integers(-100_000, 100_000, size=40_000) / 1000.0
+    edge = [0.0, -0.0, 1e-4, 9.999999999999999e-05, 1e-5, 1e16, 9999999999999998.0, 1234567890123456.0,
+            12345678901234567.0, 0.1, 2 / 3, 1.5e300, 5e-324, 2.2250738585072014e-308, 6.283185307179586]
+    vals = [float(v) for v in np.concatenate([bits, sc, dec, -sc])] + edge
+    got = rmsd_bpe._KEYC.reprs(vals)
+    bad = [(v, g) for v, g in zip(vals, got) if g != repr(v)]
+    assert not bad, bad[:5]
+
+
+def test_set_geo_c_matches_python():
+    """csrc/rmsdkey.c setgeo (Tokenizer.set_token_geo into the chain's column lists) against the
+    Python version on random spans of fixture chains, and the fallback on values that do not
+    fit (the Python version then raises as the reference does)."""
+    import copy
+    from geobpe import rmsd_bpe
+    assert rmsd_bpe._KEYC is not None, "pt-bpe_amd/geobpe/_rmsdkey.so is not built (geobpe/build.py)"
+
+    class PyDict(dict):  # (type(vals) is not dict: the Python path)
+        pass
+
+    meta, corpus, arrs = _load("rm_p0_multigrid")
+    ro = corpus["row_off"]
+    rng = np.random.default_rng(5)
+    n = 0
+    for r in range(min(12, len(ro) - 1)):
+        cols = {c: corpus[c][ro[r]:ro[r + 1]] for c in COLS}
+        base = rmsd_bpe._Chain(cols, (1.46, 1.52, 1.94))
+        for _ in range(40):
+            l = int(rng.integers(1, min(12, 3 * base.n - 1) + 1))
+            idx = int(rng.integers(0, 3 * base.n - l + 1))
+            vals = {k: [v + 0.25 for v in vs] for k, vs in base.geo(idx, l).items()}
+            a, b = copy.deepcopy(base), copy.deepcopy(base)
+            a.set_geo(idx, l, vals)
+            b.set_geo(idx, l, PyDict(vals))
+            assert a.cur == b.cur and a.init == b.init, (r, idx, l)
+            n += 1
+    assert n > 300
+    # values that do not fit: too many, too few, an unknown type -- the Python error either way
+    c = rmsd_bpe._Chain({k: corpus[k][ro[0]:ro[1]] for k in COLS}, (1.46, 1.52, 1.94))
+    good = c.geo(3, 5)
+    for bad in ({**good, "N:CA": good["N:CA"] + [1.0]}, {**good, "CA:C": good["CA:C"][:-1]}, {**good, "x": [1.0]}):
+        errs = []
+        for v in (bad, PyDict(bad)):
+            try:
+                copy.deepcopy(c).set_geo(3, 5, v)
+                errs.append(None)
+            except Exception as e:  # noqa: BLE001
+                errs.append((type(e), str(e)))
+        assert errs[0] == errs[1] and errs[0] is not None

@@ -54,8 +54,17 @@ def run_geobpe(n, lo, hi, steps, p, sup):
     bpe.bin()
     t2 = time.perf_counter()
     d0 = dev_t[0]
+    prof = None
+    if os.environ.get("GEOBPE_PROFILE"):  # (host profile of the steps, top functions to stderr)
+        import cProfile
+        prof = cProfile.Profile()
+        prof.enable()
     done = bpe.run(steps)
     t3 = time.perf_counter()
+    if prof is not None:
+        import pstats
+        prof.disable()
+        pstats.Stats(prof, stream=sys.stderr).sort_stats("tottime").print_stats(25)
     return {"impl": "geobpe (RmsdBPE, device NeRF/RMSD batches)", "chains": n, "residues": int(corpus["row_off"][-1]),
             "p_min_size": p, "super_res": sup, "initialize_s": t1 - t0, "bin_s": t2 - t1, "steps": done,
             "merges": len(bpe.merges), "s_per_step": (t3 - t2) / max(done, 1),
