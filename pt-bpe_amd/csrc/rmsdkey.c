@@ -160,6 +160,9 @@ static int item_value(PyObject* cols, PyObject* init, int t, Py_ssize_t first, P
   return PyErr_Occurred() ? -1 : 0;
 }
 
+static PyObject* build_key(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ssize_t l, Py_ssize_t ph,
+                           const Py_ssize_t* lo, const Py_ssize_t* hi, PyObject* thr);
+
 static PyObject* key(PyObject* self, PyObject* args) {
   PyObject *cols, *init, *rng, *thr;
   Py_ssize_t idx, l, ph;
@@ -182,6 +185,11 @@ static PyObject* key(PyObject* self, PyObject* args) {
     PyObject* p = PyTuple_GET_ITEM(rng, k);
     if (!PyArg_ParseTuple(p, "nn", &lo[k], &hi[k])) return NULL;
   }
+  return build_key(cols, init, idx, l, ph, lo, hi, thr);
+}
+
+static PyObject* build_key(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ssize_t l, Py_ssize_t ph,
+                           const Py_ssize_t* lo, const Py_ssize_t* hi, PyObject* thr) {
   Buf b = {NULL, 0, 0};
   int first_key = 1;
   char num[32];
@@ -310,15 +318,11 @@ fail:
  * nine column lists in json key order (as key()).  Returns False, having written nothing, when
  * a type is missing, too short or has items left over: the Python version then raises the
  * reference's error. */
-static PyObject* setgeo(PyObject* self, PyObject* args) {
-  PyObject *cols, *init, *vals;
-  Py_ssize_t idx, l;
-  (void)self;
-  if (!PyArg_ParseTuple(args, "O!O!nnO!", &PyTuple_Type, &cols, &PyList_Type, &init, &idx, &l, &PyDict_Type, &vals))
-    return NULL;
+/* 1: written; 0: does not fit (nothing written); -1: error set */
+static int setgeo_impl(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ssize_t l, PyObject* vals) {
   if (PyTuple_GET_SIZE(cols) != 9 || PyList_GET_SIZE(init) < 3 || idx < 0 || l < 1) {
     PyErr_SetString(PyExc_ValueError, "rmsdkey.setgeo: bad arguments");
-    return NULL;
+    return -1;
   }
   static const int BT[3] = {4, 2, 0}, BA[3] = {8, 3, 1}, DH[3] = {7, 5, 6};
   PyObject* seq[9] = {NULL};
@@ -382,17 +386,372 @@ static PyObject* setgeo(PyObject* self, PyObject* args) {
 #undef SETGEO_PUT
   }
   for (int t = 0; t < 9; t++) Py_XDECREF(seq[t]);
-  Py_INCREF(ok);
-  return ok;
+  return ok == Py_True ? 1 : 0;
 fail:
   for (int t = 0; t < 9; t++) Py_XDECREF(seq[t]);
-  return NULL;
+  return -1;
+}
+
+static PyObject* setgeo(PyObject* self, PyObject* args) {
+  PyObject *cols, *init, *vals;
+  Py_ssize_t idx, l;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!O!nnO!", &PyTuple_Type, &cols, &PyList_Type, &init, &idx, &l, &PyDict_Type, &vals))
+    return NULL;
+  const int rc = setgeo_impl(cols, init, idx, l, vals);
+  if (rc < 0) return NULL;
+  return PyBool_FromLong(rc);
+}
+
+/* ---------------------------------------------------------------- the merge loop
+ * merge(st, occs, assigns, key, length, n, rmsd, vals, diff) -- the occurrence loop of
+ * BPE.step (bpe.py:1860-2013) as RmsdBPE._merge runs it (without the multi-grid stale-key
+ * path), on the host class's own objects: the same Python sets, dicts and lists are changed
+ * in the same order, so every later list(set) (the order k-medoids sees) is CPython's.
+ *   st      (chains, gd, pk, edges, edges_fn, names): the _Chain list, _geo_dict
+ *           (defaultdict(set)), _pk, the per-length threshold edges and the callable that
+ *           makes a missing length's, the column names in json key order
+ *   occs    the occurrences (ci, i2) in sorted order; assigns: their medoids (rmsd) or None
+ *   vals    rmsd: the medoid geometries of the key; else the binned geometry
+ *   diff    note(): key -> count change                                                  */
+typedef struct {
+  PyObject *chains, *gd, *pk, *edges, *edges_fn, *names, *diff;
+} MSt;
+
+static int key_error(PyObject* k) {
+  PyObject* a = PyTuple_Pack(1, k);
+  if (a) {
+    PyErr_SetObject(PyExc_KeyError, a);
+    Py_DECREF(a);
+  }
+  return -1;
+}
+
+static int note(MSt* m, PyObject* k, long d) {
+  PyObject* old = PyDict_GetItemWithError(m->diff, k);
+  if (!old && PyErr_Occurred()) return -1;
+  long v = (old ? PyLong_AsLong(old) : 0) + d;
+  PyObject* nv = PyLong_FromLong(v);
+  if (!nv) return -1;
+  const int rc = PyDict_SetItem(m->diff, k, nv);
+  Py_DECREF(nv);
+  return rc;
+}
+
+static PyObject* pair2(Py_ssize_t ci, Py_ssize_t i) {
+  PyObject *a = PyLong_FromSsize_t(ci), *b = PyLong_FromSsize_t(i);
+  PyObject* t = (a && b) ? PyTuple_Pack(2, a, b) : NULL;
+  Py_XDECREF(a);
+  Py_XDECREF(b);
+  return t;
+}
+
+/* the chain's column lists in json key order (a new tuple) */
+static PyObject* chain_cols(MSt* m, PyObject* chain) {
+  PyObject* cur = PyObject_GetAttrString(chain, "cur");
+  if (!cur) return NULL;
+  PyObject* t = PyTuple_New(9);
+  for (int i = 0; t && i < 9; i++) {
+    PyObject* col = PyObject_GetItem(cur, PyTuple_GET_ITEM(m->names, i));
+    if (!col) {
+      Py_CLEAR(t);
+      break;
+    }
+    PyTuple_SET_ITEM(t, i, col);
+  }
+  Py_DECREF(cur);
+  return t;
+}
+
+static Py_ssize_t list_int(PyObject* lst, Py_ssize_t i) {
+  if (i < 0 || i >= PyList_GET_SIZE(lst)) {
+    PyErr_SetString(PyExc_IndexError, "list index out of range");
+    return -1;
+  }
+  return PyLong_AsSsize_t(PyList_GET_ITEM(lst, i));
+}
+
+/* RmsdBPE._pair_key(c, i1, la, lb) (bpe.py:1192-1299) */
+static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp, PyObject* btt, Py_ssize_t nres,
+                           Py_ssize_t i1, Py_ssize_t la, Py_ssize_t lb) {
+  const Py_ssize_t p1 = list_int(tp, i1), p2 = p1 < 0 ? -1 : list_int(tp, i1 + la);
+  if (p1 < 0 || p2 < 0) return NULL;
+  PyObject *k1 = PyLong_FromSsize_t(p1), *k2 = PyLong_FromSsize_t(p2);
+  PyObject* t1 = k1 ? PyDict_GetItemWithError(btt, k1) : NULL;
+  PyObject* t2 = (t1 && k2) ? PyDict_GetItemWithError(btt, k2) : NULL;
+  if (!t1 || !t2) {
+    if (!PyErr_Occurred()) key_error(!t1 ? k1 : k2);
+    Py_XDECREF(k1);
+    Py_XDECREF(k2);
+    return NULL;
+  }
+  Py_DECREF(k1);
+  Py_DECREF(k2);
+  const int same = PyObject_RichCompareBool(PyTuple_GET_ITEM(t1, 0), PyTuple_GET_ITEM(t2, 0), Py_EQ);
+  if (same < 0) return NULL;
+  if (same) {
+    PyErr_SetString(PyExc_RuntimeError, "pair of one token");
+    return NULL;
+  }
+  const int pt1 = PyTuple_Check(PyTuple_GET_ITEM(t1, 1)), pt2 = PyTuple_Check(PyTuple_GET_ITEM(t2, 1));
+  const Py_ssize_t L = la + lb;
+  Py_ssize_t lo[3], hi[3];
+  if (pt1 && pt2) {
+    lo[0] = 0, hi[0] = 0, lo[1] = la - 1, hi[1] = la, lo[2] = la - 2, hi[2] = la;
+  } else if (pt1) {
+    lo[0] = la, hi[0] = L, lo[1] = la - 1, hi[1] = L, lo[2] = la - 2, hi[2] = L;
+  } else if (pt2) {
+    lo[0] = 0, hi[0] = la, lo[1] = 0, hi[1] = la, lo[2] = 0, hi[2] = la;
+  } else {
+    lo[0] = 0, hi[0] = L, lo[1] = 0, hi[1] = L, lo[2] = 0, hi[2] = L;
+  }
+  if (i1 + L - 1 > 3 * nres - 1) {
+    PyErr_Format(PyExc_ValueError, "idx+l cannot exceed %zd", 3 * nres - 1);
+    return NULL;
+  }
+  PyObject* kL = PyLong_FromSsize_t(L);
+  if (!kL) return NULL;
+  PyObject* thr = PyDict_GetItemWithError(m->edges, kL);
+  if (thr) {
+    Py_INCREF(thr);
+  } else if (!PyErr_Occurred()) {
+    thr = PyObject_CallOneArg(m->edges_fn, kL);  /* (computes and caches it) */
+  }
+  Py_DECREF(kL);
+  if (!thr) return NULL;
+  if (!PyTuple_Check(thr) || PyTuple_GET_SIZE(thr) != 9) {
+    Py_DECREF(thr);
+    PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: edges must be a 9-tuple");
+    return NULL;
+  }
+  PyObject* k = build_key(cols, init, i1, L, i1 % 3, lo, hi, thr);
+  Py_DECREF(thr);
+  return k;
+}
+
+static int set_in(MSt* m, PyObject* k, PyObject* item, int add) {
+  PyObject* set = PyObject_GetItem(m->gd, k);  /* (defaultdict: a missing key gets a new set) */
+  if (!set) return -1;
+  int rc;
+  if (add) {
+    rc = PySet_Add(set, item);
+  } else {
+    rc = PySet_Discard(set, item);
+    if (rc == 0) rc = key_error(item);
+    else if (rc == 1) rc = 0;
+  }
+  Py_DECREF(set);
+  return rc;
+}
+
+static int apply_geo(PyObject* chain, PyObject* cols, PyObject* init, Py_ssize_t i1, Py_ssize_t len, PyObject* vals) {
+  int rc = PyDict_CheckExact(vals) ? setgeo_impl(cols, init, i1, len, vals) : 0;
+  if (rc != 0) return rc < 0 ? -1 : 0;
+  PyObject* r = PyObject_CallMethod(chain, "set_geo", "nnO", i1, len, vals);  /* (the Python path: its errors) */
+  if (!r) return -1;
+  Py_DECREF(r);
+  return 0;
+}
+
+static PyObject* merge(PyObject* self, PyObject* args) {
+  PyObject *st, *occs, *assigns, *key, *vals, *diff;
+  Py_ssize_t length, n;
+  int rmsd;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!O!OUnnpOO!", &PyTuple_Type, &st, &PyList_Type, &occs, &assigns, &key, &length, &n,
+                        &rmsd, &vals, &PyDict_Type, &diff))
+    return NULL;
+  MSt m;
+  if (!PyArg_ParseTuple(st, "O!OO!O!OO!", &PyList_Type, &m.chains, &m.gd, &PyDict_Type, &m.pk, &PyDict_Type, &m.edges,
+                        &m.edges_fn, &PyTuple_Type, &m.names))
+    return NULL;
+  m.diff = diff;
+  PyObject* nobj = PyLong_FromSsize_t(n);
+  PyObject* lenobj = PyLong_FromSsize_t(length);
+  PyObject *chain = NULL, *cols = NULL, *init = NULL, *tp = NULL, *btt = NULL, *events = NULL, *nres_o = NULL;
+  PyObject *t12 = NULL, *t01 = NULL, *t23 = NULL, *left = NULL, *right = NULL;
+  Py_ssize_t cur_ci = -1, nres = 0, last_ci = -1, last_i1 = 0;
+  int have_last = 0, err = 0;
+  if (!nobj || !lenobj) goto fail;
+  for (Py_ssize_t q = 0; q < PyList_GET_SIZE(occs); q++) {
+    PyObject* oc = PyList_GET_ITEM(occs, q);
+    Py_ssize_t ci, i2;
+    if (!PyArg_ParseTuple(oc, "nn", &ci, &i2)) goto fail;
+    if (ci != cur_ci) {  /* the chain's objects, kept while its occurrences run */
+      Py_CLEAR(cols);
+      Py_CLEAR(init);
+      Py_CLEAR(tp);
+      Py_CLEAR(btt);
+      Py_CLEAR(events);
+      Py_CLEAR(nres_o);
+      if (ci < 0 || ci >= PyList_GET_SIZE(m.chains)) {
+        PyErr_SetString(PyExc_IndexError, "chain index out of range");
+        goto fail;
+      }
+      chain = PyList_GET_ITEM(m.chains, ci);
+      cols = chain_cols(&m, chain);
+      init = PyObject_GetAttrString(chain, "init");
+      tp = PyObject_GetAttrString(chain, "token_pos");
+      btt = PyObject_GetAttrString(chain, "btt");
+      events = PyObject_GetAttrString(chain, "events");
+      nres_o = PyObject_GetAttrString(chain, "n");
+      if (!cols || !init || !tp || !btt || !events || !nres_o) goto fail;
+      if (!PyList_Check(tp) || !PyDict_Check(btt) || !PyList_Check(events) || !PyList_Check(init)) {
+        PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: unexpected chain state");
+        goto fail;
+      }
+      nres = PyLong_AsSsize_t(nres_o);
+      cur_ci = ci;
+    }
+    const Py_ssize_t i1 = list_int(tp, i2 - 1);
+    if (i1 < 0 && PyErr_Occurred()) goto fail;
+    const Py_ssize_t l1 = i2 - i1, l2 = length - l1;
+    if (have_last && last_ci == ci && last_i1 + length > i1) continue;  /* overlaps (bpe.py:1909-1912) */
+    if (!(l1 > 0 && l2 > 0)) {
+      PyErr_SetString(PyExc_AssertionError, "bad split");
+      goto fail;
+    }
+    t12 = pair2(ci, i2);
+    if (!t12) goto fail;
+    PyObject* cur_key = PyDict_GetItemWithError(m.pk, t12);
+    if (!cur_key && PyErr_Occurred()) goto fail;
+    const int same = cur_key ? PyObject_RichCompareBool(cur_key, key, Py_EQ) : 0;
+    if (same < 0) goto fail;
+    if (!same) {  /* bpe.py:1917-1920 */
+      Py_CLEAR(t12);
+      continue;
+    }
+    if (set_in(&m, key, t12, 0) < 0 || PyDict_DelItem(m.pk, t12) < 0 || note(&m, key, -1) < 0) goto fail;
+    Py_ssize_t i0 = 0, l0 = 0, i3 = 0, l3 = 0;
+    const Py_ssize_t ntp = PyList_GET_SIZE(tp);
+    if (i1) {
+      i0 = list_int(tp, i1 - 1);
+      if (i0 < 0 && PyErr_Occurred()) goto fail;
+      l0 = i1 - i0;
+      t01 = pair2(ci, i1);
+      if (!t01) goto fail;
+      left = PyDict_GetItemWithError(m.pk, t01);
+      if (!left) {
+        if (!PyErr_Occurred()) key_error(t01);
+        goto fail;
+      }
+      Py_INCREF(left);
+    }
+    if (i2 + l2 < ntp) {
+      i3 = i2 + l2;
+      l3 = 0;
+      while (i3 + l3 < ntp) {
+        const Py_ssize_t v = list_int(tp, i3 + l3);
+        if (v < 0 && PyErr_Occurred()) goto fail;
+        if (v != i3) break;
+        l3++;
+      }
+      t23 = pair2(ci, i3);
+      if (!t23) goto fail;
+      right = PyDict_GetItemWithError(m.pk, t23);
+      if (!right) {
+        if (!PyErr_Occurred()) key_error(t23);
+        goto fail;
+      }
+      Py_INCREF(right);
+    }
+    if (left && (set_in(&m, left, t01, 0) < 0 || note(&m, left, -1) < 0)) goto fail;
+    if (right && (set_in(&m, right, t23, 0) < 0 || note(&m, right, -1) < 0)) goto fail;
+    {
+      PyObject* vi1 = PyLong_FromSsize_t(i1);
+      if (!vi1) goto fail;
+      for (Py_ssize_t j = i2; j < i2 + l2; j++) {
+        Py_INCREF(vi1);
+        if (PyList_SetItem(tp, j, vi1) < 0) {
+          Py_DECREF(vi1);
+          goto fail;
+        }
+      }
+      PyObject* ki2 = PyLong_FromSsize_t(i2);
+      int rc = ki2 ? PyDict_DelItem(btt, ki2) : -1;
+      Py_XDECREF(ki2);
+      PyObject *tokid = NULL, *val = NULL, *ev = NULL;
+      if (rc == 0) {
+        if (rmsd) {
+          PyObject* a = PyList_GET_ITEM(assigns, q);
+          tokid = PyTuple_Pack(2, nobj, a);
+        } else {
+          tokid = nobj;
+          Py_INCREF(tokid);
+        }
+        val = tokid ? PyTuple_Pack(3, vi1, tokid, lenobj) : NULL;
+        rc = val ? PyDict_SetItem(btt, vi1, val) : -1;
+        if (rc == 0) {
+          PyObject* vi2 = PyLong_FromSsize_t(i2);
+          ev = vi2 ? PyTuple_Pack(3, vi1, vi2, val) : NULL;
+          Py_XDECREF(vi2);
+          rc = ev ? PyList_Append(events, ev) : -1;
+        }
+      }
+      Py_XDECREF(tokid);
+      Py_XDECREF(val);
+      Py_XDECREF(ev);
+      Py_DECREF(vi1);
+      if (rc < 0) goto fail;
+    }
+    if (rmsd) {
+      PyObject* a = PyList_GET_ITEM(assigns, q);
+      PyObject* struc = PyObject_GetItem(vals, a);
+      if (!struc) goto fail;
+      const int rc = apply_geo(chain, cols, init, i1, length, struc);
+      Py_DECREF(struc);
+      if (rc < 0) goto fail;
+    }
+    if (left) {
+      PyObject* k = mpair_key(&m, cols, init, tp, btt, nres, i0, l0, length);
+      if (!k) goto fail;
+      const int rc = (set_in(&m, k, t01, 1) < 0 || PyDict_SetItem(m.pk, t01, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
+      Py_DECREF(k);
+      if (rc < 0) goto fail;
+    }
+    if (right) {
+      PyObject* k = mpair_key(&m, cols, init, tp, btt, nres, i1, length, l3);
+      if (!k) goto fail;
+      const int rc = (set_in(&m, k, t23, 1) < 0 || PyDict_SetItem(m.pk, t23, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
+      Py_DECREF(k);
+      if (rc < 0) goto fail;
+    }
+    if (!rmsd && apply_geo(chain, cols, init, i1, length, vals) < 0) goto fail;
+    last_ci = ci;
+    last_i1 = i1;
+    have_last = 1;
+    Py_CLEAR(t12);
+    Py_CLEAR(t01);
+    Py_CLEAR(t23);
+    Py_CLEAR(left);
+    Py_CLEAR(right);
+  }
+  goto done;
+fail:
+  err = 1;
+done:
+  Py_XDECREF(t12);
+  Py_XDECREF(t01);
+  Py_XDECREF(t23);
+  Py_XDECREF(left);
+  Py_XDECREF(right);
+  Py_XDECREF(cols);
+  Py_XDECREF(init);
+  Py_XDECREF(tp);
+  Py_XDECREF(btt);
+  Py_XDECREF(events);
+  Py_XDECREF(nres_o);
+  Py_XDECREF(nobj);
+  Py_XDECREF(lenobj);
+  if (err) return NULL;
+  Py_RETURN_NONE;
 }
 
 static PyMethodDef METHODS[] = {{"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
                                 {"pack", pack, METH_VARARGS, "whole-residue span geometry, geobpe_nerf layout"},
                                 {"reprs", reprs, METH_VARARGS, "repr(float) of each value (test)"},
                                 {"setgeo", setgeo, METH_VARARGS, "set_token_geo into the chain's column lists"},
+                                {"merge", merge, METH_VARARGS, "the occurrence loop of a merge (RmsdBPE._merge)"},
                                 {NULL, NULL, 0, NULL}};
 static struct PyModuleDef MOD = {PyModuleDef_HEAD_INIT, "_rmsdkey", NULL, -1, METHODS, NULL, NULL, NULL, NULL};
 PyMODINIT_FUNC PyInit__rmsdkey(void) { return PyModule_Create(&MOD); }

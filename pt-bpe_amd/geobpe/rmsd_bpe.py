@@ -59,6 +59,7 @@ _ITEM = {k: (i, 0) for i, k in enumerate(BOND_TYPES)} | {k: (i, 1) for i, k in e
     {k: (i, 2) for i, k in enumerate(DIHEDRALS)}
 _ENC = json.JSONEncoder(sort_keys=True)  # json.dumps(geo, sort_keys=True) (bpe.py:1147-1149)
 _KEY_ORDER = sorted(_ITEM)  # json key order of the nine item types
+_KEY_ORDER_T = tuple(_KEY_ORDER)
 _PACK_ORDER = ["N:CA", "CA:C", "tau", "0C:1N", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"]  # geobpe_nerf's
 
 
@@ -660,6 +661,11 @@ class RmsdBPE:
                 out.append(None)  # (the C key raises only if such a type is binned: then the
         return tuple(out)         #  Python restatement reproduces the reference's error)
 
+    def _edges_store(self, L):
+        """_edges_for(L), cached (called by csrc/rmsdkey.c merge for a length it has not seen)."""
+        e = self._key_edges[L] = self._edges_for(L)
+        return e
+
     def _pair_key_py(self, c, idx1, L, rng):
         """_pair_key in Python: the restatement rmsdkey.c follows (and the path taken for
         its errors, so the reference's exceptions surface unchanged)."""
@@ -788,7 +794,14 @@ class RmsdBPE:
         # every key is derived afresh from the geometry, as the reference does
         stale_ok = not rmsd and len(self.bins) > 1
         last_ci = last_i1 = None
-        for idx in sorted(range(len(occ)), key=occ.__getitem__):
+        order = sorted(range(len(occ)), key=occ.__getitem__)
+        if _KEYC is not None and not stale_ok and not self._py_keys:
+            # the loop below in C (csrc/rmsdkey.c merge), on these same sets / dicts / lists
+            _KEYC.merge((self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T),
+                        [occ[i] for i in order], [assign[i] for i in order] if rmsd else None, key, length, n,
+                        rmsd, self._sphere_dict[key] if rmsd else binned, diff)
+            order = ()
+        for idx in order:
             ci, i2 = occ[idx]
             c = self._chains[ci]
             tp = c.token_pos
