@@ -1599,6 +1599,47 @@ int geobpe_featurize(int device, int64_t n_rows, const int64_t* h_row_off, const
   return rc;
 }
 
+namespace {
+// The context-free entry points (glue opt, NeRF, Kabsch) keep one stream and one scratch arena
+// per (device, entry point) for the process, grown on demand: the RMSD mode calls them once or
+// twice per key and induce once per chain, where a stream and a few allocations per call used
+// to outweigh the kernels.  The lock serialises calls on one arena.
+struct Arena {
+  hipStream_t s = nullptr;
+  char* buf = nullptr;
+  size_t cap = 0;
+};
+std::mutex g_arena_mu;
+std::map<std::pair<int, int>, Arena> g_arena;
+enum { ARENA_GLUE = 0, ARENA_NERF = 1, ARENA_RMSD = 2 };
+
+// the arena's stream and n buffers of sizes[i] bytes (256-B aligned) in ptr[i]; the caller holds g_arena_mu
+int arena_take(int device, int which, int n, const size_t* sizes, void** ptr, hipStream_t* s) {
+  Arena& ar = g_arena[std::make_pair(device, which)];
+  if (!ar.s && hipStreamCreateWithFlags(&ar.s, hipStreamNonBlocking) != hipSuccess) {
+    ar.s = nullptr;
+    return GEOBPE_EHIP;
+  }
+  size_t total = 0;
+  for (int i = 0; i < n; i++) total += (sizes[i] + 255) / 256 * 256;
+  if (ar.cap < total) {
+    if (ar.buf) hipFree(ar.buf);
+    ar.buf = nullptr;
+    ar.cap = 0;
+    const size_t want = total + total / 4;
+    if (hipMalloc(&ar.buf, want) != hipSuccess) return GEOBPE_EHIP;
+    ar.cap = want;
+  }
+  char* q = ar.buf;
+  for (int i = 0; i < n; i++) {
+    ptr[i] = q;
+    q += (sizes[i] + 255) / 256 * 256;
+  }
+  *s = ar.s;
+  return 0;
+}
+}  // namespace
+
 int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const double* h_a, const double* h_b,
                 int symmetric, double* h_out) {
   if (n_a < 0 || n_atoms <= 0 || !h_a || !h_out) return GEOBPE_EARG;
@@ -1609,15 +1650,17 @@ int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const dou
   if (n_b < 0 || !h_b) return GEOBPE_EARG;
   if ((int64_t)n_a * n_b == 0) return 0;
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
-  hipStream_t s;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GEOBPE_EHIP;
   const int64_t la = (int64_t)n_a * n_atoms * 3, lb = (int64_t)n_b * n_atoms * 3, no = (int64_t)n_a * n_b;
   double *d_a = nullptr, *d_b = nullptr, *d_out = nullptr;
-  int rc = 0;
-  if (hipMalloc(&d_a, la * 8) != hipSuccess || (!symmetric && hipMalloc(&d_b, lb * 8) != hipSuccess) ||
-      hipMalloc(&d_out, no * 8) != hipSuccess) {
-    rc = GEOBPE_EHIP;
-  } else {
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  hipStream_t s;
+  const size_t sizes[3] = {(size_t)la * 8, symmetric ? 0 : (size_t)lb * 8, (size_t)no * 8};
+  void* ptr[3];
+  int rc = arena_take(device, ARENA_RMSD, 3, sizes, ptr, &s);
+  if (!rc) {
+    d_a = (double*)ptr[0];
+    d_b = symmetric ? nullptr : (double*)ptr[1];
+    d_out = (double*)ptr[2];
     hipMemcpyAsync(d_a, h_a, la * 8, hipMemcpyHostToDevice, s);
     hipLaunchKernelGGL(k_rmsd_center, dim3((n_a + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, s, d_a, n_a, n_atoms);
     if (!symmetric) {
@@ -1630,10 +1673,6 @@ int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const dou
     if (!rc && hipMemcpyAsync(h_out, d_out, no * 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = GEOBPE_EHIP;
     if (hipStreamSynchronize(s) != hipSuccess) rc = GEOBPE_EHIP;
   }
-  hipFree(d_a);
-  hipFree(d_b);
-  hipFree(d_out);
-  hipStreamDestroy(s);
   return rc;
 }
 
@@ -1643,15 +1682,17 @@ int geobpe_nerf(int device, int64_t n_spans, const int64_t* h_res_off, const dou
   if (R == 0) return 0;
   if (!h_geo || !h_xyz) return GEOBPE_EARG;
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
-  hipStream_t s;
-  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return GEOBPE_EHIP;
   int64_t* d_off = nullptr;
   double *d_geo = nullptr, *d_out = nullptr;
-  int rc = 0;
-  if (hipMalloc(&d_off, (n_spans + 1) * 8) != hipSuccess || hipMalloc(&d_geo, R * 9 * 8) != hipSuccess ||
-      hipMalloc(&d_out, R * 9 * 8) != hipSuccess) {
-    rc = GEOBPE_EHIP;
-  } else {
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  hipStream_t s;
+  const size_t sizes[3] = {(size_t)(n_spans + 1) * 8, (size_t)R * 9 * 8, (size_t)R * 9 * 8};
+  void* ptr[3];
+  int rc = arena_take(device, ARENA_NERF, 3, sizes, ptr, &s);
+  if (!rc) {
+    d_off = (int64_t*)ptr[0];
+    d_geo = (double*)ptr[1];
+    d_out = (double*)ptr[2];
     hipMemcpyAsync(d_off, h_res_off, (n_spans + 1) * 8, hipMemcpyHostToDevice, s);
     hipMemcpyAsync(d_geo, h_geo, R * 9 * 8, hipMemcpyHostToDevice, s);
     hipLaunchKernelGGL(k_nerf, dim3((unsigned)((n_spans + BLOCK - 1) / BLOCK)), dim3(BLOCK), 0, s, n_spans,
@@ -1660,22 +1701,8 @@ int geobpe_nerf(int device, int64_t n_spans, const int64_t* h_res_off, const dou
     if (!rc && hipMemcpyAsync(h_xyz, d_out, R * 9 * 8, hipMemcpyDeviceToHost, s) != hipSuccess) rc = GEOBPE_EHIP;
     if (hipStreamSynchronize(s) != hipSuccess) rc = GEOBPE_EHIP;
   }
-  hipFree(d_off);
-  hipFree(d_geo);
-  hipFree(d_out);
-  hipStreamDestroy(s);
   return rc;
 }
-
-namespace {
-struct GlueArena {  // geobpe_glue_opt's stream and scratch of one device (kept for the process)
-  hipStream_t s = nullptr;
-  char* buf = nullptr;
-  size_t cap = 0;
-};
-std::mutex g_glue_mu;
-std::map<int, GlueArena> g_glue;
-}  // namespace
 
 int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, const double* h_geo, const float* h_x0,
                     const float* h_tgt, const int32_t* h_grid, int32_t n_grid, int32_t kmax, const float* h_prior,
@@ -1699,16 +1726,8 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
   for (int64_t i = 0; i < 3 * (int64_t)n_grid; i++)
     if (h_kcnt[i] <= 0 || h_kcnt[i] > kmax) return GEOBPE_EARG;
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
-  // one stream and one scratch arena per device, kept across calls and grown on demand
-  // (induce with glue opt calls this once per chain and per re-optimisation: a stream and
-  // 14 allocations per call used to outweigh the kernel)
-  std::lock_guard<std::mutex> lock(g_glue_mu);
-  GlueArena& ar = g_glue[device];
-  if (!ar.s && hipStreamCreateWithFlags(&ar.s, hipStreamNonBlocking) != hipSuccess) {
-    ar.s = nullptr;
-    return GEOBPE_EHIP;
-  }
-  hipStream_t s = ar.s;
+  std::lock_guard<std::mutex> lock(g_arena_mu);  // (the per-device arena: see arena_take)
+  hipStream_t s = nullptr;
   const int64_t pmax = 3 * (rmax - 1), S = n_chains;
   GlueProb P{};
   P.S = S;
@@ -1734,26 +1753,9 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
                             (size_t)S * 4, (size_t)n_grid * 6 * kmax * 4, (size_t)n_grid * 3 * 4, (size_t)G * 3 * 4,
                             (size_t)S * 2 * 4, (size_t)S * 2 * 8, (size_t)nx * 8, (size_t)nx * 8,
                             (size_t)GLUE_NVEC * nv * 4, (size_t)2 * GLUE_HIST * nv * 4};
-  size_t total = 0;
-  for (size_t z : sizes) total += (z + 255) / 256 * 256;
-  bool ok = true;
-  if (ar.cap < total) {
-    if (ar.buf) hipFree(ar.buf);
-    ar.buf = nullptr;
-    ar.cap = 0;
-    const size_t want = total + total / 4;
-    if (hipMalloc(&ar.buf, want) == hipSuccess)
-      ar.cap = want;
-    else
-      ok = false;
-  }
+  void* ptr[14];
+  const bool ok = arena_take(device, ARENA_GLUE, 14, sizes, ptr, &s) == 0;
   if (ok) {
-    void* ptr[14];
-    char* q = ar.buf;
-    for (int i = 0; i < 14; i++) {
-      ptr[i] = q;
-      q += (sizes[i] + 255) / 256 * 256;
-    }
     d_off = (int64_t*)ptr[0];
     d_geo = (double*)ptr[1];
     d_x0 = (float*)ptr[2];
