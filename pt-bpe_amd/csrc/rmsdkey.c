@@ -237,8 +237,13 @@ static PyObject* build_key(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ss
         const double q = kind == 0 ? v : py_mod(v + TWO_PI, TWO_PI);
         const long ind = get_ind(q, PyTuple_GET_ITEM(th, 0), PyTuple_GET_ITEM(th, 1));
         if (ind < 0) goto fail;
-        snprintf(num, sizeof num, "%ld", ind);
-        if (buf_str(&b, num) < 0) goto fail;
+        int k = (int)sizeof num;  /* (the bin index in decimal: snprintf cost more than the rest of a key) */
+        long x = ind;
+        do {
+          num[--k] = (char)('0' + x % 10);
+          x /= 10;
+        } while (x);
+        if (buf_put(&b, num + k, (Py_ssize_t)sizeof num - k) < 0) goto fail;
       } else if (put_float(&b, v) < 0) {
         goto fail;
       }
