@@ -752,11 +752,146 @@ done:
   Py_RETURN_NONE;
 }
 
+/* prio(diff, k2p, remove, add, gd, spheres) -- step 7 of BPE.step (bpe.py:2077-2138) as
+ * RmsdBPE._merge runs it: every key whose count changed leaves the priority list and comes
+ * back with its new count (flag = not partitioned, -count, key); a key whose count reached 0
+ * leaves _geo_dict.  remove / add: the SortedList's bound methods. */
+static PyObject* prio(PyObject* self, PyObject* args) {
+  PyObject *diff, *k2p, *remove, *add, *gd, *spheres;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!O!OOOO", &PyDict_Type, &diff, &PyDict_Type, &k2p, &remove, &add, &gd, &spheres))
+    return NULL;
+  Py_ssize_t it = 0;
+  PyObject *k, *d;
+  while (PyDict_Next(diff, &it, &k, &d)) {
+    long count = 0;
+    PyObject* pr = PyDict_GetItemWithError(k2p, k);
+    if (!pr && PyErr_Occurred()) return NULL;
+    if (pr) {
+      Py_INCREF(pr);
+      if (PyDict_DelItem(k2p, k) < 0) {
+        Py_DECREF(pr);
+        return NULL;
+      }
+      PyObject* r = PyObject_CallOneArg(remove, pr);
+      if (!r) {
+        Py_DECREF(pr);
+        return NULL;
+      }
+      Py_DECREF(r);
+      count = -PyLong_AsLong(PyTuple_GET_ITEM(pr, 1));
+      Py_DECREF(pr);
+    }
+    count += PyLong_AsLong(d);
+    if (PyErr_Occurred()) return NULL;
+    PyObject* set = PyObject_GetItem(gd, k);  /* (defaultdict: as len(gd[k])) */
+    if (!set) return NULL;
+    const Py_ssize_t n = PySet_Size(set);
+    Py_DECREF(set);
+    if (n < 0) return NULL;
+    if (count != n) {
+      PyObject* head = PyUnicode_Substring(k, 0, 60);
+      if (head) {
+        PyErr_Format(PyExc_AssertionError, "count of %U out of step", head);
+        Py_DECREF(head);
+      }
+      return NULL;
+    }
+    if (count) {
+      const int in = PySequence_Contains(spheres, k);
+      if (in < 0) return NULL;
+      PyObject* negc = PyLong_FromLong(-count);
+      PyObject* npr = negc ? PyTuple_Pack(3, in ? Py_False : Py_True, negc, k) : NULL;
+      Py_XDECREF(negc);
+      if (!npr) return NULL;
+      if (PyDict_SetItem(k2p, k, npr) < 0) {
+        Py_DECREF(npr);
+        return NULL;
+      }
+      PyObject* r = PyObject_CallOneArg(add, npr);
+      Py_DECREF(npr);
+      if (!r) return NULL;
+      Py_DECREF(r);
+    } else if (PyDict_DelItem(gd, k) < 0) {
+      return NULL;
+    }
+  }
+  Py_RETURN_NONE;
+}
+
+/* packc(chains, orig, spans, out) -- pack() with the spans given as (chain index, q, r): the
+ * chain's columns (cur, or orig) and init are read here (PACK order below) */
+static const char* PACK_NAMES[9] = {"N:CA", "CA:C", "tau", "0C:1N", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"};
+static PyObject* packc(PyObject* self, PyObject* args) {
+  PyObject *chains, *spans, *out;
+  int orig;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!pO!O", &PyList_Type, &chains, &orig, &PyList_Type, &spans, &out)) return NULL;
+  PyObject* items = PyList_New(0);
+  if (!items) return NULL;
+  Py_ssize_t last_ci = -1;
+  PyObject* cols = NULL;
+  PyObject* init = NULL;
+  for (Py_ssize_t i = 0; i < PyList_GET_SIZE(spans); i++) {
+    Py_ssize_t ci, q, r;
+    if (!PyArg_ParseTuple(PyList_GET_ITEM(spans, i), "nnn", &ci, &q, &r)) goto fail;
+    if (ci != last_ci) {
+      Py_CLEAR(cols);
+      Py_CLEAR(init);
+      if (ci < 0 || ci >= PyList_GET_SIZE(chains)) {
+        PyErr_SetString(PyExc_IndexError, "chain index out of range");
+        goto fail;
+      }
+      PyObject* c = PyList_GET_ITEM(chains, ci);
+      PyObject* src = PyObject_GetAttrString(c, orig ? "orig" : "cur");
+      init = PyObject_GetAttrString(c, "init");
+      if (!src || !init) {
+        Py_XDECREF(src);
+        goto fail;
+      }
+      cols = PyTuple_New(9);
+      for (int t = 0; cols && t < 9; t++) {
+        PyObject* col = PyMapping_GetItemString(src, PACK_NAMES[t]);
+        if (!col) {
+          Py_CLEAR(cols);
+          break;
+        }
+        PyTuple_SET_ITEM(cols, t, col);
+      }
+      Py_DECREF(src);
+      if (!cols) goto fail;
+      last_ci = ci;
+    }
+    PyObject* it = Py_BuildValue("(OOnn)", cols, init, q, r);
+    if (!it || PyList_Append(items, it) < 0) {
+      Py_XDECREF(it);
+      goto fail;
+    }
+    Py_DECREF(it);
+  }
+  Py_CLEAR(cols);
+  Py_CLEAR(init);
+  {
+    PyObject* a = Py_BuildValue("(OO)", items, out);
+    PyObject* res = a ? pack(NULL, a) : NULL;
+    Py_XDECREF(a);
+    Py_DECREF(items);
+    return res;
+  }
+fail:
+  Py_XDECREF(cols);
+  Py_XDECREF(init);
+  Py_DECREF(items);
+  return NULL;
+}
+
 static PyMethodDef METHODS[] = {{"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
                                 {"pack", pack, METH_VARARGS, "whole-residue span geometry, geobpe_nerf layout"},
                                 {"reprs", reprs, METH_VARARGS, "repr(float) of each value (test)"},
                                 {"setgeo", setgeo, METH_VARARGS, "set_token_geo into the chain's column lists"},
                                 {"merge", merge, METH_VARARGS, "the occurrence loop of a merge (RmsdBPE._merge)"},
+                                {"prio", prio, METH_VARARGS, "the priority updates of a merge (RmsdBPE._merge)"},
+                                {"packc", packc, METH_VARARGS, "pack() with spans as (chain, q, r)"},
                                 {NULL, NULL, 0, NULL}};
 static struct PyModuleDef MOD = {PyModuleDef_HEAD_INIT, "_rmsdkey", NULL, -1, METHODS, NULL, NULL, NULL, NULL};
 PyMODINIT_FUNC PyInit__rmsdkey(void) { return PyModule_Create(&MOD); }

@@ -352,7 +352,9 @@ class RmsdBPE:
             length = min(length, 3 * c.n - 1 - index)
             start = 3 * (index // 3)
             end = 3 * (((index + length - 1) + 1) // 3) + 1
-            if _KEYC is not None:  # (the span's residues straight into the NeRF layout, csrc/rmsdkey.c)
+            if _KEYC is not None and not isinstance(ci, _Chain):  # (straight into the NeRF layout, csrc/rmsdkey.c)
+                packs.append((ci, start // 3, (end - start + 2) // 3))
+            elif _KEYC is not None:
                 src = c.orig if orig else c.cur
                 packs.append((tuple(src[k] for k in _PACK_ORDER), c.init, start // 3, (end - start + 2) // 3))
             else:
@@ -362,13 +364,22 @@ class RmsdBPE:
             return []
         if _KEYC is not None:
             off = np.zeros(len(packs) + 1, dtype=np.int64)
-            np.cumsum([p[3] for p in packs], out=off[1:])
+            np.cumsum([p[-1] for p in packs], out=off[1:])
             packed = np.zeros((int(off[-1]), 9), dtype=np.float64)
-            _KEYC.pack(packs, packed)
+            if packs and len(packs[0]) == 3 and all(len(p) == 3 for p in packs):
+                _KEYC.packc(self._chains, bool(orig), packs, packed)
+            else:
+                _KEYC.pack([p if len(p) == 4 else self._pack_item(p, orig) for p in packs], packed)
             xyz = _rmsd.nerf_packed(off, packed, device=self.device)
         else:
             xyz = _rmsd.geo_coords(geos, device=self.device)
         return [x[a:len(x) - b] for x, (a, b) in zip(xyz, cuts)]
+
+    def _pack_item(self, p, orig):
+        ci, q, r = p
+        c = self._chains[ci]
+        src = c.orig if orig else c.cur
+        return (tuple(src[k] for k in _PACK_ORDER), c.init, q, r)
 
     def _struc_coords(self, strucs):
         """Tokenizer.key_coords(struc) (tokenizer.py:204-230) for medoid geometries that
@@ -884,6 +895,10 @@ class RmsdBPE:
                         note(new, +1)
         if not recurring:
             self._step += 1
+        if _KEYC is not None and not self._py_keys:  # (step 7 below, in C on the same objects)
+            _KEYC.prio(diff, self._key_to_priority, self._priority.remove, self._priority.add, gd,
+                       getattr(self, "_sphere_dict", {}))
+            diff = {}
         for k, d in diff.items():  # step 7 (bpe.py:2077-2138)
             pr = self._key_to_priority.pop(k, None)
             count = 0
