@@ -80,6 +80,13 @@ def nerf_packed(off, packed) -> list:
     return out
 
 
+def nerf_atoms(off, packed) -> np.ndarray:
+    """nerf_packed's spans back to back, (3 * off[-1], 3) -- the CPU stand-in for
+    geobpe.rmsd.nerf_atoms."""
+    out = nerf_packed(off, packed)
+    return np.concatenate(out).reshape(-1, 3) if out else np.zeros((0, 3))
+
+
 def nerf(geo: dict) -> np.ndarray:
     """Tokenizer.geo_nerf(geo).cartesian_coords (3r - 1 bonds -> 3r atoms)."""
     r = len(geo["N:CA"])

@@ -31,17 +31,20 @@ static const double TWO_PI = 6.283185307179586; /* 2 * np.pi */
 typedef struct {
   char* p;
   Py_ssize_t n, cap;
+  char* stack; /* p's first buffer (the caller's); grown on the heap */
 } Buf;
 
 static int buf_put(Buf* b, const char* s, Py_ssize_t n) {
   if (b->n + n > b->cap) {
     Py_ssize_t c = b->cap ? b->cap : 512;
     while (c < b->n + n) c *= 2;
-    char* q = (char*)PyMem_Realloc(b->p, c);
+    char* q = (char*)PyMem_Malloc(c);
     if (!q) {
       PyErr_NoMemory();
       return -1;
     }
+    memcpy(q, b->p, b->n);
+    if (b->p != b->stack) PyMem_Free(b->p);
     b->p = q;
     b->cap = c;
   }
@@ -188,9 +191,32 @@ static PyObject* key(PyObject* self, PyObject* args) {
   return build_key(cols, init, idx, l, ph, lo, hi, thr);
 }
 
+/* the span's value objects, fetched ahead: a key reads ~25 floats scattered over the heap, and
+ * one after the other each was a dependent cache miss */
+static void prefetch_span(PyObject* cols, Py_ssize_t idx, Py_ssize_t l) {
+  static const int BT[3] = {4, 2, 0}, BA[3] = {8, 3, 1}, DH[3] = {7, 5, 6};
+  for (Py_ssize_t j = idx > 2 ? idx : 2; j < idx + l; j++) {
+    PyObject* col = PyTuple_GET_ITEM(cols, BT[j % 3]);
+    const Py_ssize_t row = (j - 2) / 3;
+    if (row < PyList_GET_SIZE(col)) __builtin_prefetch(PyList_GET_ITEM(col, row));
+  }
+  for (Py_ssize_t j = idx > 1 ? idx : 1; j < idx + l - 1; j++) {
+    PyObject* col = PyTuple_GET_ITEM(cols, BA[j % 3]);
+    const Py_ssize_t row = (j - 1) / 3;
+    if (row < PyList_GET_SIZE(col)) __builtin_prefetch(PyList_GET_ITEM(col, row));
+  }
+  for (Py_ssize_t j = idx; j < idx + l - 2; j++) {
+    PyObject* col = PyTuple_GET_ITEM(cols, DH[j % 3]);
+    const Py_ssize_t row = (j + 1) / 3;
+    if (row < PyList_GET_SIZE(col)) __builtin_prefetch(PyList_GET_ITEM(col, row));
+  }
+}
+
 static PyObject* build_key(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ssize_t l, Py_ssize_t ph,
                            const Py_ssize_t* lo, const Py_ssize_t* hi, PyObject* thr) {
-  Buf b = {NULL, 0, 0};
+  prefetch_span(cols, idx, l);
+  char stack[2048];
+  Buf b = {stack, 0, (Py_ssize_t)sizeof stack, stack};
   int first_key = 1;
   char num[32];
   if (buf_str(&b, "{") < 0) goto fail;
@@ -251,11 +277,12 @@ static PyObject* build_key(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ss
     if (buf_str(&b, "]") < 0) goto fail;
   }
   if (buf_str(&b, "}") < 0) goto fail;
-  PyObject* out = PyUnicode_FromStringAndSize(b.p, b.n);
-  PyMem_Free(b.p);
+  PyObject* out = PyUnicode_New(b.n, 127);  /* (every character is ASCII) */
+  if (out) memcpy(PyUnicode_DATA(out), b.p, b.n);
+  if (b.p != stack) PyMem_Free(b.p);
   return out;
 fail:
-  PyMem_Free(b.p);
+  if (b.p != stack) PyMem_Free(b.p);
   return NULL;
 }
 
@@ -268,6 +295,44 @@ fail:
  * q + k - 1 of N:CA / CA:C / tau (residue 0: init) and row q + k of the junction columns
  * (phi: row q + k + 1) -- bond j -> row (j - 2) // 3, angle a -> (a - 1) // 3, dihedral d ->
  * (d + 1) // 3 (rmsd_bpe._Chain). */
+/* one span into o[9 r]: 0, -1 with IndexError (outside the chain) or another error set */
+static int pack_one(PyObject* cols, PyObject* init, Py_ssize_t q, Py_ssize_t r, double* o) {
+  for (int c = 0; c < 9; c++) {  /* (the value objects first: each read is a cache miss) */
+    PyObject* col = PyTuple_GET_ITEM(cols, c);
+    const Py_ssize_t n = PyList_GET_SIZE(col);
+    for (Py_ssize_t k = 0; k < r; k++) {
+      const Py_ssize_t row = c < 3 ? q + k - 1 : (k + 1 < r ? (c == 8 ? q + k + 1 : q + k) : -1);
+      if (row >= 0 && row < n) __builtin_prefetch(PyList_GET_ITEM(col, row));
+    }
+  }
+  for (Py_ssize_t k = 0; k < r; k++, o += 9) {
+    const Py_ssize_t res = q + k;
+    for (int c = 0; c < 9; c++) {
+      double v = 0.0;
+      if (c < 3) {
+        if (res == 0) {
+          v = PyFloat_AsDouble(PyList_GET_ITEM(init, c));
+        } else {
+          PyObject* col = PyTuple_GET_ITEM(cols, c);
+          if (res - 1 >= PyList_GET_SIZE(col)) goto range;
+          v = PyFloat_AsDouble(PyList_GET_ITEM(col, res - 1));
+        }
+      } else if (k + 1 < r) {
+        PyObject* col = PyTuple_GET_ITEM(cols, c);
+        const Py_ssize_t row = c == 8 ? res + 1 : res;
+        if (row >= PyList_GET_SIZE(col)) goto range;
+        v = PyFloat_AsDouble(PyList_GET_ITEM(col, row));
+      }
+      if (v == -1.0 && PyErr_Occurred()) return -1;
+      o[c] = v;
+    }
+  }
+  return 0;
+range:
+  PyErr_SetString(PyExc_IndexError, "rmsdkey.pack: span outside the chain");
+  return -1;
+}
+
 static PyObject* pack(PyObject* self, PyObject* args) {
   PyObject* spans;
   Py_buffer out;
@@ -285,33 +350,16 @@ static PyObject* pack(PyObject* self, PyObject* args) {
       PyErr_SetString(PyExc_ValueError, "rmsdkey.pack: bad span");
       goto fail;
     }
-    for (Py_ssize_t k = 0; k < r; k++, at += 9) {
-      const Py_ssize_t res = q + k;
-      for (int c = 0; c < 9; c++) {
-        double v = 0.0;
-        if (c < 3) {
-          if (res == 0) {
-            v = PyFloat_AsDouble(PyList_GET_ITEM(init, c));
-          } else {
-            PyObject* col = PyTuple_GET_ITEM(cols, c);
-            if (res - 1 >= PyList_GET_SIZE(col)) goto range;
-            v = PyFloat_AsDouble(PyList_GET_ITEM(col, res - 1));
-          }
-        } else if (k + 1 < r) {
-          PyObject* col = PyTuple_GET_ITEM(cols, c);
-          const Py_ssize_t row = c == 8 ? res + 1 : res;
-          if (row >= PyList_GET_SIZE(col)) goto range;
-          v = PyFloat_AsDouble(PyList_GET_ITEM(col, row));
-        }
-        if (v == -1.0 && PyErr_Occurred()) goto fail;
-        o[at + c] = v;
+    for (int c = 0; c < 9; c++)
+      if (!PyList_Check(PyTuple_GET_ITEM(cols, c))) {
+        PyErr_SetString(PyExc_TypeError, "rmsdkey.pack: columns must be lists");
+        goto fail;
       }
-    }
+    if (pack_one(cols, init, q, r, o + at) < 0) goto fail;
+    at += 9 * r;
   }
   PyBuffer_Release(&out);
   return PyLong_FromSsize_t(at / 9);
-range:
-  PyErr_SetString(PyExc_IndexError, "rmsdkey.pack: span outside the chain");
 fail:
   PyBuffer_Release(&out);
   return NULL;
@@ -579,9 +627,13 @@ static PyObject* merge(PyObject* self, PyObject* args) {
   int have_last = 0, err = 0;
   if (!nobj || !lenobj) goto fail;
   for (Py_ssize_t q = 0; q < PyList_GET_SIZE(occs); q++) {
-    PyObject* oc = PyList_GET_ITEM(occs, q);
-    Py_ssize_t ci, i2;
-    if (!PyArg_ParseTuple(oc, "nn", &ci, &i2)) goto fail;
+    PyObject* oc = PyList_GET_ITEM(occs, q);  /* (the very tuples _geo_dict's sets hold) */
+    if (!PyTuple_CheckExact(oc) || PyTuple_GET_SIZE(oc) != 2) {
+      PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: occurrences must be (chain, index) tuples");
+      goto fail;
+    }
+    const Py_ssize_t ci = PyLong_AsSsize_t(PyTuple_GET_ITEM(oc, 0)), i2 = PyLong_AsSsize_t(PyTuple_GET_ITEM(oc, 1));
+    if ((ci == -1 || i2 == -1) && PyErr_Occurred()) goto fail;
     if (ci != cur_ci) {  /* the chain's objects, kept while its occurrences run */
       Py_CLEAR(cols);
       Py_CLEAR(init);
@@ -616,8 +668,8 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       PyErr_SetString(PyExc_AssertionError, "bad split");
       goto fail;
     }
-    t12 = pair2(ci, i2);
-    if (!t12) goto fail;
+    t12 = oc;
+    Py_INCREF(t12);
     PyObject* cur_key = PyDict_GetItemWithError(m.pk, t12);
     if (!cur_key && PyErr_Occurred()) goto fail;
     const int same = cur_key ? PyObject_RichCompareBool(cur_key, key, Py_EQ) : 0;
@@ -752,14 +804,16 @@ done:
   Py_RETURN_NONE;
 }
 
-/* prio(diff, k2p, remove, add, gd, spheres) -- step 7 of BPE.step (bpe.py:2077-2138) as
- * RmsdBPE._merge runs it: every key whose count changed leaves the priority list and comes
+/* prio(diff, k2p, heap, push, gd, spheres) -- step 7 of BPE.step (bpe.py:2077-2138) as
+ * RmsdBPE._merge runs it: every key whose count changed leaves the priority queue and comes
  * back with its new count (flag = not partitioned, -count, key); a key whose count reached 0
- * leaves _geo_dict.  remove / add: the SortedList's bound methods. */
+ * leaves _geo_dict.  The queue is rmsd_bpe._PrioQueue: k2p is its live map (dropping a key's
+ * entry from k2p removes it), heap / push its heap list and heapq.heappush. */
 static PyObject* prio(PyObject* self, PyObject* args) {
-  PyObject *diff, *k2p, *remove, *add, *gd, *spheres;
+  PyObject *diff, *k2p, *heap, *push, *gd, *spheres;
   (void)self;
-  if (!PyArg_ParseTuple(args, "O!O!OOOO", &PyDict_Type, &diff, &PyDict_Type, &k2p, &remove, &add, &gd, &spheres))
+  if (!PyArg_ParseTuple(args, "O!O!O!OOO", &PyDict_Type, &diff, &PyDict_Type, &k2p, &PyList_Type, &heap, &push, &gd,
+                        &spheres))
     return NULL;
   Py_ssize_t it = 0;
   PyObject *k, *d;
@@ -768,19 +822,8 @@ static PyObject* prio(PyObject* self, PyObject* args) {
     PyObject* pr = PyDict_GetItemWithError(k2p, k);
     if (!pr && PyErr_Occurred()) return NULL;
     if (pr) {
-      Py_INCREF(pr);
-      if (PyDict_DelItem(k2p, k) < 0) {
-        Py_DECREF(pr);
-        return NULL;
-      }
-      PyObject* r = PyObject_CallOneArg(remove, pr);
-      if (!r) {
-        Py_DECREF(pr);
-        return NULL;
-      }
-      Py_DECREF(r);
       count = -PyLong_AsLong(PyTuple_GET_ITEM(pr, 1));
-      Py_DECREF(pr);
+      if (PyDict_DelItem(k2p, k) < 0) return NULL;  /* (pr is gone with it) */
     }
     count += PyLong_AsLong(d);
     if (PyErr_Occurred()) return NULL;
@@ -808,7 +851,7 @@ static PyObject* prio(PyObject* self, PyObject* args) {
         Py_DECREF(npr);
         return NULL;
       }
-      PyObject* r = PyObject_CallOneArg(add, npr);
+      PyObject* r = PyObject_CallFunctionObjArgs(push, heap, npr, NULL);
       Py_DECREF(npr);
       if (!r) return NULL;
       Py_DECREF(r);
@@ -823,13 +866,14 @@ static PyObject* prio(PyObject* self, PyObject* args) {
  * chain's columns (cur, or orig) and init are read here (PACK order below) */
 static const char* PACK_NAMES[9] = {"N:CA", "CA:C", "tau", "0C:1N", "CA:C:1N", "C:1N:1CA", "psi", "omega", "phi"};
 static PyObject* packc(PyObject* self, PyObject* args) {
-  PyObject *chains, *spans, *out;
+  PyObject *chains, *spans;
+  Py_buffer out;
   int orig;
   (void)self;
-  if (!PyArg_ParseTuple(args, "O!pO!O", &PyList_Type, &chains, &orig, &PyList_Type, &spans, &out)) return NULL;
-  PyObject* items = PyList_New(0);
-  if (!items) return NULL;
-  Py_ssize_t last_ci = -1;
+  if (!PyArg_ParseTuple(args, "O!pO!w*", &PyList_Type, &chains, &orig, &PyList_Type, &spans, &out)) return NULL;
+  double* o = (double*)out.buf;
+  const Py_ssize_t cap = out.len / (Py_ssize_t)sizeof(double);
+  Py_ssize_t at = 0, last_ci = -1;
   PyObject* cols = NULL;
   PyObject* init = NULL;
   for (Py_ssize_t i = 0; i < PyList_GET_SIZE(spans); i++) {
@@ -860,28 +904,32 @@ static PyObject* packc(PyObject* self, PyObject* args) {
       }
       Py_DECREF(src);
       if (!cols) goto fail;
+      if (!PyList_Check(init) || PyList_GET_SIZE(init) < 3) {
+        PyErr_SetString(PyExc_TypeError, "rmsdkey.packc: init must be a list of 3");
+        goto fail;
+      }
+      for (int t = 0; t < 9; t++)
+        if (!PyList_Check(PyTuple_GET_ITEM(cols, t))) {
+          PyErr_SetString(PyExc_TypeError, "rmsdkey.packc: columns must be lists");
+          goto fail;
+        }
       last_ci = ci;
     }
-    PyObject* it = Py_BuildValue("(OOnn)", cols, init, q, r);
-    if (!it || PyList_Append(items, it) < 0) {
-      Py_XDECREF(it);
+    if (q < 0 || r < 1 || at + 9 * r > cap) {
+      PyErr_SetString(PyExc_ValueError, "rmsdkey.packc: bad span");
       goto fail;
     }
-    Py_DECREF(it);
+    if (pack_one(cols, init, q, r, o + at) < 0) goto fail;
+    at += 9 * r;
   }
   Py_CLEAR(cols);
   Py_CLEAR(init);
-  {
-    PyObject* a = Py_BuildValue("(OO)", items, out);
-    PyObject* res = a ? pack(NULL, a) : NULL;
-    Py_XDECREF(a);
-    Py_DECREF(items);
-    return res;
-  }
+  PyBuffer_Release(&out);
+  return PyLong_FromSsize_t(at / 9);
 fail:
   Py_XDECREF(cols);
   Py_XDECREF(init);
-  Py_DECREF(items);
+  PyBuffer_Release(&out);
   return NULL;
 }
 

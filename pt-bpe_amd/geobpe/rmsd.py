@@ -168,9 +168,9 @@ def geo_coords(geos, device: int = 0):
     return nerf_packed(off, packed, device)
 
 
-def nerf_packed(off: np.ndarray, packed: np.ndarray, device: int = 0):
+def nerf_atoms(off: np.ndarray, packed: np.ndarray, device: int = 0) -> np.ndarray:
     """geobpe_nerf on spans already packed (9 float64 per residue, off[n + 1] residue
-    offsets): [(3r, 3)] atoms per span."""
+    offsets): the atoms of every span back to back, (3 * off[-1], 3)."""
     L = _native.lib()
     R = int(off[-1])
     xyz = np.empty((max(R, 1), 3, 3), dtype=np.float64)
@@ -179,7 +179,13 @@ def nerf_packed(off: np.ndarray, packed: np.ndarray, device: int = 0):
                            packed.ctypes.data_as(ctypes.c_void_p), xyz.ctypes.data_as(ctypes.c_void_p))
         if rc:
             raise _native.GeoBPEError(f"geobpe_nerf failed (code {rc})")
-    return [xyz[a:b].reshape(3 * (b - a), 3) for a, b in zip(off[:-1], off[1:])]
+    return xyz.reshape(-1, 3)[:3 * R]
+
+
+def nerf_packed(off: np.ndarray, packed: np.ndarray, device: int = 0):
+    """nerf_atoms split per span: [(3r, 3)]."""
+    xyz = nerf_atoms(off, packed, device)
+    return [xyz[3 * a:3 * b] for a, b in zip(off[:-1].tolist(), off[1:].tolist())]
 
 
 def compute_coords(cols: dict, spans, init=None, device: int = 0):

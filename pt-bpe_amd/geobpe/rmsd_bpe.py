@@ -39,6 +39,7 @@ built: ``rmsd_only``.  Free bond lengths
 from __future__ import annotations
 
 import bisect
+import heapq
 import json
 import time
 from collections import defaultdict
@@ -77,6 +78,51 @@ def _load_keyc():
 
 
 _KEYC = _load_keyc()
+
+
+class _PrioQueue:
+    """The reference's priority SortedDict of (not partitioned, -count, key) entries
+    (bpe.py:1431-1474, 2077-2138) as a heap with lazy deletion.  `live` is _key_to_priority
+    itself (key -> its current entry); a heap entry whose key no longer maps to that very tuple
+    is stale and leaves when it reaches the top.  Keys are unique, so the tuple order the heap
+    keeps is the sorted container's order; only [0], len, add, remove and sorted iteration are
+    used.  (A SortedList add/remove cost ~2 us each, a third of a 2000-chain step.)"""
+    __slots__ = ("heap", "live")
+
+    def __init__(self, live: dict):
+        self.live = live
+        self.heap = list(live.values())
+        heapq.heapify(self.heap)
+
+    def add(self, pr):
+        self.live[pr[2]] = pr
+        heapq.heappush(self.heap, pr)
+
+    def remove(self, pr):
+        if self.live.get(pr[2]) is pr:
+            del self.live[pr[2]]
+
+    def _top(self):
+        h, live = self.heap, self.live
+        while h and live.get(h[0][2]) is not h[0]:
+            heapq.heappop(h)
+        if len(h) > 2 * len(live) + 4096:  # (stale entries deep in the heap: rebuild)
+            self.heap = h = list(live.values())
+            heapq.heapify(h)
+        if not h:
+            raise IndexError("priority queue is empty")
+        return h[0]
+
+    def __len__(self):
+        return len(self.live)
+
+    def __getitem__(self, i):
+        if i == 0:
+            return self._top()
+        return sorted(self.live.values())[i]
+
+    def __iter__(self):
+        return iter(sorted(self.live.values()))
 RES_SPHERE_KEY = {3: '{"N:CA": [0], "CA:C": [0], "0C:1N": [0], "tau": [0], "CA:C:1N": [0], "psi": [0]}',
                   2: '{"CA:C": [0], "0C:1N": [0], "CA:C:1N": [0]}'}
 
@@ -346,17 +392,18 @@ class RmsdBPE:
     def _span_coords(self, spans, orig):
         """Tokenizer.compute_coords(index, length, orig) for [(chain, index, length)], one
         device NeRF batch: the span rounded out to whole residues, then its atoms."""
+        if _KEYC is not None and spans and not isinstance(spans[0][0], _Chain):
+            return self._span_coords_idx(spans, orig)
         packs, geos, cuts = [], [], []
         for ci, index, length in spans:
             c = ci if isinstance(ci, _Chain) else self._chains[ci]
             length = min(length, 3 * c.n - 1 - index)
             start = 3 * (index // 3)
             end = 3 * (((index + length - 1) + 1) // 3) + 1
-            if _KEYC is not None and not isinstance(ci, _Chain):  # (straight into the NeRF layout, csrc/rmsdkey.c)
-                packs.append((ci, start // 3, (end - start + 2) // 3))
-            elif _KEYC is not None:
-                src = c.orig if orig else c.cur
-                packs.append((tuple(src[k] for k in _PACK_ORDER), c.init, start // 3, (end - start + 2) // 3))
+            if _KEYC is not None:
+                packs.append(self._pack_item((ci, start // 3, (end - start + 2) // 3), orig) if isinstance(ci, int)
+                             else (tuple((c.orig if orig else c.cur)[k] for k in _PACK_ORDER), c.init, start // 3,
+                                   (end - start + 2) // 3))
             else:
                 geos.append(c.geo(start, end - start + 1, orig))
             cuts.append((index - start, end - (index + length - 1)))
@@ -366,14 +413,35 @@ class RmsdBPE:
             off = np.zeros(len(packs) + 1, dtype=np.int64)
             np.cumsum([p[-1] for p in packs], out=off[1:])
             packed = np.zeros((int(off[-1]), 9), dtype=np.float64)
-            if packs and len(packs[0]) == 3 and all(len(p) == 3 for p in packs):
-                _KEYC.packc(self._chains, bool(orig), packs, packed)
-            else:
-                _KEYC.pack([p if len(p) == 4 else self._pack_item(p, orig) for p in packs], packed)
+            _KEYC.pack(packs, packed)
             xyz = _rmsd.nerf_packed(off, packed, device=self.device)
         else:
             xyz = _rmsd.geo_coords(geos, device=self.device)
         return [x[a:len(x) - b] for x, (a, b) in zip(xyz, cuts)]
+
+    def _span_coords_idx(self, spans, orig):
+        """_span_coords of spans on chains given by index, in arrays: the NeRF layout packed in
+        C (csrc/rmsdkey.c packc), the atoms cut out of the batch's output with one gather.  Spans
+        of one atom count (a merge's occurrences) come back as one (n, atoms, 3) array."""
+        sp = np.asarray(spans, dtype=np.int64).reshape(len(spans), 3)
+        ci, index = sp[:, 0], sp[:, 1]
+        na = self.__dict__.get("_nres_a")
+        if na is None or len(na) != len(self._chains):
+            na = self._nres_a = np.array([c.n for c in self._chains], dtype=np.int64)
+        length = np.minimum(sp[:, 2], 3 * na[ci] - 1 - index)
+        start = 3 * (index // 3)
+        end = 3 * ((index + length) // 3) + 1
+        r = (end - start + 2) // 3
+        off = np.zeros(len(sp) + 1, dtype=np.int64)
+        np.cumsum(r, out=off[1:])
+        packed = np.zeros((int(off[-1]), 9), dtype=np.float64)
+        _KEYC.packc(self._chains, bool(orig), list(zip(ci.tolist(), (start // 3).tolist(), r.tolist())), packed)
+        atoms = _rmsd.nerf_atoms(off, packed, device=self.device)
+        first = 3 * off[:-1] + (index - start)
+        cnt = length + 1
+        if (cnt == cnt[0]).all():
+            return atoms[first[:, None] + np.arange(int(cnt[0]))]
+        return [atoms[f:f + c] for f, c in zip(first.tolist(), cnt.tolist())]
 
     def _pack_item(self, p, orig):
         ci, q, r = p
@@ -407,7 +475,7 @@ class RmsdBPE:
         """_compute_assignment_inner for every occurrence (bpe.py:654-657): argmin over the
         medoids of compute_rmsd(occurrence, medoid) -- one device launch."""
         self.assign_calls += 1
-        if not coords:
+        if len(coords) == 0:
             return []
         return [int(a) for a in _rmsd.assign(coords, medoid_coords, device=self.device)]
 
@@ -606,7 +674,7 @@ class RmsdBPE:
                   else np.arange(N))
         sup = self.rmsd_super_res
         coords = self._span_coords(occ, sup)
-        act = [coords[i] for i in active]
+        act = coords[active] if isinstance(coords, np.ndarray) else [coords[i] for i in active]
         k = self.num_partitions[size]
         medoids = _rmsd.k_medoids(act, k, rng=self.rng, device=self.device)
         if len(medoids) != k:
@@ -706,7 +774,6 @@ class RmsdBPE:
 
     # ------------------------------------------------------------ bin (bpe.py:1431-1474)
     def bin(self):
-        from sortedcontainers import SortedList
         self._geo_dict = defaultdict(set)
         # the key of every live pair by (chain, start of its second token): a pair's key
         # changes only when a merge replaces the pair, so step() reads the old neighbour keys
@@ -719,12 +786,8 @@ class RmsdBPE:
                 self._geo_dict[k].add((ci, i2))
                 self._pk[(ci, i2)] = k
         self._geo_step = {k: 0 for k in self._geo_dict}
-        self._priority = SortedList()
-        self._key_to_priority = {}
-        for key, occ in self._geo_dict.items():
-            pr = (True, -len(occ), key)
-            self._priority.add(pr)
-            self._key_to_priority[key] = pr
+        self._key_to_priority = {key: (True, -len(occ), key) for key, occ in self._geo_dict.items()}
+        self._priority = _PrioQueue(self._key_to_priority)
         self._sphere_keys = {}
 
     @property
@@ -751,7 +814,7 @@ class RmsdBPE:
         spans = [(ci, self._chains[ci].token_pos[index - 1], length) for ci, index in occ]
         sup = self.rmsd_super_res
         coords = self._span_coords(spans, sup)
-        act = [coords[i] for i in active]
+        act = coords[active] if isinstance(coords, np.ndarray) else [coords[i] for i in active]
         medoids = _rmsd.k_medoids(act, self.num_partitions[length], rng=self.rng, device=self.device)
         assign = self._assign(coords, [act[m] for m in medoids])
         strucs = []
@@ -896,7 +959,7 @@ class RmsdBPE:
         if not recurring:
             self._step += 1
         if _KEYC is not None and not self._py_keys:  # (step 7 below, in C on the same objects)
-            _KEYC.prio(diff, self._key_to_priority, self._priority.remove, self._priority.add, gd,
+            _KEYC.prio(diff, self._key_to_priority, self._priority.heap, heapq.heappush, gd,
                        getattr(self, "_sphere_dict", {}))
             diff = {}
         for k, d in diff.items():  # step 7 (bpe.py:2077-2138)

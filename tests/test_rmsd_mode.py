@@ -131,6 +131,7 @@ def host_geometry(monkeypatch):
 
     monkeypatch.setattr(rmsd, "geo_coords", lambda geos, device=0: [orm.nerf(g) for g in geos])
     monkeypatch.setattr(rmsd, "nerf_packed", lambda off, packed, device=0: orm.nerf_packed(off, packed))
+    monkeypatch.setattr(rmsd, "nerf_atoms", lambda off, packed, device=0: orm.nerf_atoms(off, packed))
     monkeypatch.setattr(rmsd, "rmsd_matrix", lambda S, device=0: orm.rmsd_matrix(S))
     monkeypatch.setattr(rmsd, "rmsd_cross", lambda A, B, device=0: np.array([[orm.rmsd(a, b) for b in B] for a in A]))
     monkeypatch.setattr(rmsd_bpe.RmsdBPE, "_grid_thresholds",

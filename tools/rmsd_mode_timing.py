@@ -37,7 +37,7 @@ def run_geobpe(n, lo, hi, steps, p, sup):
     from geobpe.bpe import BPE
     corpus = corpus_of(n, lo, hi)
     dev_t = [0.0]
-    for name in ("geo_coords", "nerf_packed", "rmsd_matrix", "rmsd_cross"):
+    for name in ("nerf_atoms", "rmsd_matrix", "rmsd_cross"):
         f = getattr(rmsd, name)
 
         def timed(*a, _f=f, **k):
