@@ -425,3 +425,63 @@ def test_set_geo_c_matches_python():
             except Exception as e:  # noqa: BLE001
                 errs.append((type(e), str(e)))
         assert errs[0] == errs[1] and errs[0] is not None
+
+
+def test_prio_queue_order_matches_sorted_container():
+    """rmsd_bpe._PrioQueue (a lazy-deletion heap over _key_to_priority) against the reference's
+    sorted container of (not partitioned, -count, key): the same top after every batch of
+    priority updates -- the C path (rmsdkey.prio) and the Python path (remove / add) -- the same
+    sorted iteration and slices."""
+    import heapq
+
+    from sortedcontainers import SortedList
+    from geobpe import rmsd_bpe
+
+    rng = np.random.default_rng(5)
+    keys = [f'{{"k": [{i}]}}' for i in range(400)]
+    k2p = {k: (True, -int(rng.integers(1, 40)), k) for k in keys[:300]}
+    ref = SortedList(k2p.values())
+    q = rmsd_bpe._PrioQueue(k2p)
+    gd = {k: set(range(-p[1])) for k, p in k2p.items()}
+    spheres = {}
+    for step in range(300):
+        diff = {}
+        for k in rng.choice(keys, 12, replace=False):
+            k = str(k)
+            cur = len(gd.get(k, ()))
+            d = int(rng.integers(-cur, 6))
+            gd[k] = set(range(cur + d))
+            diff[k] = diff.get(k, 0) + d
+            if rng.random() < 0.05:
+                spheres[k] = None
+        use_c = rmsd_bpe._KEYC is not None and step % 2 == 0
+        if use_c:
+            for k in diff:  # (what the C call does, on the reference container)
+                pr = next((p for p in ref if p[2] == k), None)
+                if pr is not None:
+                    ref.remove(pr)
+            rmsd_bpe._KEYC.prio(diff, k2p, q.heap, heapq.heappush, gd, spheres)
+            for k in diff:
+                if k in k2p:
+                    ref.add(k2p[k])
+        else:
+            for k, d in diff.items():
+                pr = k2p.pop(k, None)
+                if pr is not None:
+                    q.remove(pr)
+                    ref.remove(pr)
+                n = len(gd[k])
+                if n:
+                    pr = (k not in spheres, -n, k)
+                    k2p[k] = pr
+                    q.add(pr)
+                    ref.add(pr)
+                else:
+                    gd.pop(k)
+        for k in [k for k in list(gd) if not gd[k]]:
+            gd.pop(k)
+        assert len(q) == len(ref)
+        if len(ref):
+            assert q[0] == ref[0]
+        if step % 50 == 0:
+            assert list(q) == list(ref) and q[:7] == list(ref[:7])
