@@ -439,8 +439,10 @@ class RmsdBPE:
         atoms = _rmsd.nerf_atoms(off, packed, device=self.device)
         first = 3 * off[:-1] + (index - start)
         cnt = length + 1
-        if (cnt == cnt[0]).all():
-            return atoms[first[:, None] + np.arange(int(cnt[0]))]
+        if (cnt == cnt[0]).all():  # (one flat take: a row gather of 3-double rows is ~3x slower)
+            c = int(cnt[0])
+            flat = np.ascontiguousarray(atoms).reshape(-1)
+            return flat.take((3 * first)[:, None] + np.arange(3 * c)).reshape(len(first), c, 3)
         return [atoms[f:f + c] for f, c in zip(first.tolist(), cnt.tolist())]
 
     def _pack_item(self, p, orig):
