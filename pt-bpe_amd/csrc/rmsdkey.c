@@ -28,6 +28,13 @@ static const int KIND[9] = {0, 1, 0, 1, 0, 2, 2, 2, 1};
 static const int T0[9] = {2, 2, 1, 1, 0, 1, 2, 0, 0};
 static const double TWO_PI = 6.283185307179586; /* 2 * np.pi */
 
+/* attribute and column names, interned once at import (the ...String() lookups built and
+ * hashed a new str per call, ~10 per chain visited) */
+enum { A_CUR, A_ORIG, A_INIT, A_TOKEN_POS, A_BTT, A_EVENTS, A_N, A_COUNT };
+static const char* ATTR_NAMES[A_COUNT] = {"cur", "orig", "init", "token_pos", "btt", "events", "n"};
+static PyObject* ATTR[A_COUNT];
+static PyObject* PACK_KEYS[9];
+
 typedef struct {
   char* p;
   Py_ssize_t n, cap;
@@ -501,7 +508,7 @@ static PyObject* pair2(Py_ssize_t ci, Py_ssize_t i) {
 
 /* the chain's column lists in json key order (a new tuple) */
 static PyObject* chain_cols(MSt* m, PyObject* chain) {
-  PyObject* cur = PyObject_GetAttrString(chain, "cur");
+  PyObject* cur = PyObject_GetAttr(chain, ATTR[A_CUR]);
   if (!cur) return NULL;
   PyObject* t = PyTuple_New(9);
   for (int i = 0; t && i < 9; i++) {
@@ -647,11 +654,11 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       }
       chain = PyList_GET_ITEM(m.chains, ci);
       cols = chain_cols(&m, chain);
-      init = PyObject_GetAttrString(chain, "init");
-      tp = PyObject_GetAttrString(chain, "token_pos");
-      btt = PyObject_GetAttrString(chain, "btt");
-      events = PyObject_GetAttrString(chain, "events");
-      nres_o = PyObject_GetAttrString(chain, "n");
+      init = PyObject_GetAttr(chain, ATTR[A_INIT]);
+      tp = PyObject_GetAttr(chain, ATTR[A_TOKEN_POS]);
+      btt = PyObject_GetAttr(chain, ATTR[A_BTT]);
+      events = PyObject_GetAttr(chain, ATTR[A_EVENTS]);
+      nres_o = PyObject_GetAttr(chain, ATTR[A_N]);
       if (!cols || !init || !tp || !btt || !events || !nres_o) goto fail;
       if (!PyList_Check(tp) || !PyDict_Check(btt) || !PyList_Check(events) || !PyList_Check(init)) {
         PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: unexpected chain state");
@@ -887,15 +894,15 @@ static PyObject* packc(PyObject* self, PyObject* args) {
         goto fail;
       }
       PyObject* c = PyList_GET_ITEM(chains, ci);
-      PyObject* src = PyObject_GetAttrString(c, orig ? "orig" : "cur");
-      init = PyObject_GetAttrString(c, "init");
+      PyObject* src = PyObject_GetAttr(c, ATTR[orig ? A_ORIG : A_CUR]);
+      init = PyObject_GetAttr(c, ATTR[A_INIT]);
       if (!src || !init) {
         Py_XDECREF(src);
         goto fail;
       }
       cols = PyTuple_New(9);
       for (int t = 0; cols && t < 9; t++) {
-        PyObject* col = PyMapping_GetItemString(src, PACK_NAMES[t]);
+        PyObject* col = PyObject_GetItem(src, PACK_KEYS[t]);
         if (!col) {
           Py_CLEAR(cols);
           break;
@@ -942,4 +949,10 @@ static PyMethodDef METHODS[] = {{"key", key, METH_VARARGS, "the pair key string 
                                 {"packc", packc, METH_VARARGS, "pack() with spans as (chain, q, r)"},
                                 {NULL, NULL, 0, NULL}};
 static struct PyModuleDef MOD = {PyModuleDef_HEAD_INIT, "_rmsdkey", NULL, -1, METHODS, NULL, NULL, NULL, NULL};
-PyMODINIT_FUNC PyInit__rmsdkey(void) { return PyModule_Create(&MOD); }
+PyMODINIT_FUNC PyInit__rmsdkey(void) {
+  for (int i = 0; i < A_COUNT; i++)
+    if (!ATTR[i] && !(ATTR[i] = PyUnicode_InternFromString(ATTR_NAMES[i]))) return NULL;
+  for (int i = 0; i < 9; i++)
+    if (!PACK_KEYS[i] && !(PACK_KEYS[i] = PyUnicode_InternFromString(PACK_NAMES[i]))) return NULL;
+  return PyModule_Create(&MOD);
+}
