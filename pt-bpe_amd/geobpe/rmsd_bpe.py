@@ -39,6 +39,7 @@ built: ``rmsd_only``.  Free bond lengths
 from __future__ import annotations
 
 import bisect
+import gc
 import heapq
 import json
 import time
@@ -799,12 +800,22 @@ class RmsdBPE:
 
     # ------------------------------------------------------------ step (bpe.py:1792-2166)
     def step(self):
-        while True:
-            self._merge()
-            if not len(self._priority):
-                raise IndexError("peekitem on an empty priority dict (bpe.py:2164)")
-            if self._priority[0][0]:
-                return
+        # (the cyclic collector is paused for the step: a step allocates thousands of tracked
+        # tuples, and the full passes they set off over the tracked host state -- millions of
+        # pair tuples, sets and dicts -- were a quarter of a 2000-chain step; nothing here makes
+        # cycles, refcounting frees it all, and the collector resumes as it was)
+        gc_was = gc.isenabled()
+        gc.disable()
+        try:
+            while True:
+                self._merge()
+                if not len(self._priority):
+                    raise IndexError("peekitem on an empty priority dict (bpe.py:2164)")
+                if self._priority[0][0]:
+                    return
+        finally:
+            if gc_was:
+                gc.enable()
 
     def _partition(self, key, length):
         """rmsd_partition (bpe.py:1739-1789): k-medoids over (a sample of) the occurrences,
