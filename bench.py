@@ -52,6 +52,8 @@ MIDFIND_BYTES_PER_OCC = 132  # k_mid_find: list entry 4, token records of g, p, 
                              # 32, merge entry 16, two new-pair entries 16
 MIDSEL_BYTES_PER_OCC = 76    # k_mid_sel's token rewrites: merge entry 16, records of a, b, c 28, two new-pair
                              # entries 16, two pk 8, (+ the appends beside the next find: two entries 8)
+FIND_KREC_BYTES = 48       # k_find per key record it writes for k_commit (content hash, representative, T range)
+FIND_DREC_BYTES = 8        # k_find per decrement record it writes for k_commit (key, delta)
 COMMIT_KREC_BYTES = 56     # k_commit per key record: 48 read + (id, log position) 8 written
 COMMIT_DREC_BYTES = 8      # per decrement record
 COMMIT_KEY_BYTES = 44      # per key: table slot 8 (CAS), count 4, payload (h1, h2, len, representative) 32
@@ -293,43 +295,61 @@ def main():
                           f"{COMMIT_KEY_BYTES} B x keys (avg {cw['commit_key_records']:.0f} / "
                           f"{cw['commit_decrement_records']:.0f} / {cw['commit_keys']:.0f} per launch, counted by an "
                           f"instrumented replay of the same merges)")
-    # the sampled launches (every event_stride-th of each kernel in the timed region) pair
-    # with their own merges' bytes when the window had no rebuild iteration (one launch of
-    # each kernel per merge); the replay's every-launch average pairs with the window average
+    if commit_work:  # k_find also writes the key and decrement records k_commit reads
+        cw = {k: per(v) for k, v in commit_work.items()}
+        fb = (FIND_BYTES_PER_OCC * per(n_merged) + FIND_KREC_BYTES * cw["commit_key_records"]
+              + FIND_DREC_BYTES * cw["commit_decrement_records"])
+        work["find"] = (fb, f"{FIND_BYTES_PER_OCC} B x merged occurrences + {FIND_KREC_BYTES} B x key records + "
+                            f"{FIND_DREC_BYTES} B x decrement records written for k_commit (avg {per(n_merged):.0f} / "
+                            f"{cw['commit_key_records']:.0f} / {cw['commit_decrement_records']:.0f} per launch; the "
+                            f"record counts from the instrumented replay)")
+    # avg_launch_us is the replay's: every launch of the window's merges timed with HIP events
+    # on the engine stream (the rocprof trace of the same window agrees, profiles/); the live
+    # events of the timed region sample every event_stride-th launch and are reported beside
+    # it (live_*), paired with their own merges' bytes when the window had no rebuild iteration
     per_occ = {"find": FIND_BYTES_PER_OCC, "select": PLACE_BYTES_PER_OCC, "mid_find": MIDFIND_BYTES_PER_OCC,
                "mid_sel": MIDSEL_BYTES_PER_OCC}
     src_of = {"find": w_full, "select": prev[:n_full], "mid_find": w_mid, "mid_sel": prev[n_full:]}
     no_skip = st1["nskip"] == st0["nskip"]
     roofs = {}
     for k, (ms, nl) in ktimes.items():
-        live = k in LIVE.split(",")
-        if not nl and not (not live and k in replay_avg):
+        live = k in LIVE.split(",") and nl > 0
+        if not live and k not in replay_avg:
             continue
-        if not nl:  # (not sampled live: the replay's every-launch average)
-            ms, nl = replay_avg[k] / 1000.0, 1
-        avg_s = ms / 1000.0 / nl
         bpl, note = work[k]
-        if not live:
-            note += "; timed by the replay only (no live events on this kernel)"
-        if no_skip and live and k in per_occ:
-            smp = src_of[k][::args.event_stride][:nl]
-            if len(smp) == nl:
-                bpl = per_occ[k] * sum(m[2] for m in smp) / nl
-                note += f"; the {nl} timed launches' own merges: avg {bpl / per_occ[k]:.0f} occurrences"
-        ach = bpl / avg_s / 1e9 if bpl is not None else None
+        live_us = 1000.0 * ms / nl if live else None
+        avg_us = replay_avg.get(k, live_us)
+        src = ("replay: every launch timed" if k in replay_avg
+               else f"live: every {args.event_stride}th launch of the timed region (no replay)")
+        live_ach = None
+        if live and bpl is not None:
+            lb = bpl
+            if no_skip and k in per_occ:
+                smp = src_of[k][::args.event_stride][:nl]
+                if len(smp) == nl:  # (the sampled launches' own merges)
+                    lb = bpl + per_occ[k] * (sum(m[2] for m in smp) / nl - sum(m[2] for m in src_of[k]) / max(len(src_of[k]), 1))
+            live_ach = lb / (live_us * 1e-6) / 1e9
+        ach = bpl / (avg_us * 1e-6) / 1e9 if bpl is not None else None
         traffic, tsrc = pmc_traffic(k, wkey)  # (k_select's dispatches carry k_place)
-        roofs[k] = {"kernel": {"select": "k_select+k_place", "mid_sel": "k_mid_sel"}.get(k, f"k_{k}"), "bound": "hbm", "achieved": round(ach, 2) if ach else None,
-                    "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
+        roofs[k] = {"kernel": {"select": "k_select+k_place", "mid_sel": "k_mid_sel"}.get(k, f"k_{k}"), "bound": "hbm",
+                    "achieved": round(ach, 2) if ach else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
                     "traffic": traffic, "traffic_source": tsrc, "traffic_window": wkey,
-                    "bytes_per_launch": round(bpl, 1) if bpl is not None else None, "avg_launch_us": round(avg_s * 1e6, 3),
-                    "launches_timed": nl if live else 0, "event_stride": args.event_stride if live else None,
+                    "traffic_frac_of_algorithmic": round(traffic / bpl, 2) if traffic and bpl else None,
+                    "bytes_per_launch": round(bpl, 1) if bpl is not None else None,
+                    "avg_launch_us": round(avg_us, 3), "avg_source": src,
+                    "ms_total": kern.get("select+place" if k == "select" else k, {}).get("ms_total"),
                     "algorithmic_bytes": note,
-                    "replay_avg_launch_us": round(replay_avg[k], 3) if k in replay_avg else None,
-                    "replay_achieved": (round(work[k][0] / (replay_avg[k] * 1e-6) / 1e9, 2)
-                                        if k in replay_avg and work[k][0] is not None else None)}
-    if args.roofline_kernel == "auto":  # the slowest live-timed kernel by every launch of the replay
+                    "live_avg_launch_us": round(live_us, 3) if live else None,
+                    "live_launches_timed": nl if live else 0, "event_stride": args.event_stride if live else None,
+                    "live_achieved": round(live_ach, 2) if live_ach else None}
+    if args.roofline_kernel == "auto":
+        # the dominant kernel: the most total time over the window's launches (replay), among
+        # the kernels that can dominate (k_select+k_place rides with a one-workgroup select)
         cand = [k for k in roofs if k in LIVE.split(",")] or list(roofs)
-        dom = max(cand, key=lambda k: replay_avg.get(k, roofs[k]["avg_launch_us"])) if cand else None
+        tot = lambda k: (roofs[k]["ms_total"] if roofs[k]["ms_total"] is not None  # noqa: E731
+                         else roofs[k]["avg_launch_us"] * _launches(k) / 1000.0)
+        dom = max(cand, key=tot) if cand else None
     else:
         dom = args.roofline_kernel if args.roofline_kernel in roofs else None
     roofline = roofs.get(dom) if dom else None
@@ -342,18 +362,27 @@ def main():
         t_pass = sum(bin_ms.values()) / 1000.0
         t_count = bin_ms["pair_count"] / 1000.0
         dense = "bin_claim" in bin_ms
+        ctraffic = pmc_traffic("bin_count" if dense else "pairs_all", wkey, "pre_kernels")[0]
         pair_count = {
             "bytes": bc, "T0": R_local, "U0": U0,
             "count_kernel": {"kernel": "k_bin_count" if dense else "k_pairs_all",
                              "time_us": round(t_count * 1e6, 2), "achieved_GBs": round(bc / t_count / 1e9, 1),
                              "frac": round(bc / t_count / 1e9 / HBM_PEAK_GBS, 4),
-                             "traffic": pmc_traffic("bin_count" if dense else "pairs_all", wkey, "pre_kernels")[0]},
+                             "frac_basis": "SURVEY 8(d) B_count = 20*T + 4*U bytes",
+                             "traffic": ctraffic,
+                             # the counters' own bytes (FETCH + WRITE of this launch) over the same time
+                             "traffic_frac": (round(ctraffic / t_count / 1e9 / HBM_PEAK_GBS, 4) if ctraffic else None)},
             "pass": {"kernels": ("k_bin_sample+k_bin_rank+k_bin_flag+k_bin_precube | k_bin_count | k_bin_reduce | "
                                  "k_bin_ool_stage+k_bin_ool_claim+k_bin_ool_fix") if dense else "k_pairs_all+k_finalize",
                      "time_us": round(t_pass * 1e6, 2), "achieved_GBs": round(bc / t_pass / 1e9, 1),
                      "frac": round(bc / t_pass / 1e9 / HBM_PEAK_GBS, 4),
                      "ms": {k: round(v, 4) for k, v in bin_ms.items()}},
             "layout_pack_us": round(pack_ms * 1000, 2),
+            # k_pack (pk into the token records for the merge loop) follows the bin pass, outside the
+            # timed merges; bin pass + pack together
+            "pack_us": round(pack_ms * 1000, 2),
+            "pass_and_pack": {"time_us": round(t_pass * 1e6 + pack_ms * 1000, 2),
+                              "frac": round(bc / (t_pass + pack_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)},
         }
 
     cpu = None

@@ -281,6 +281,10 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t *h_res_off, cons
                     const float *h_tgt, const int32_t *h_grid, int32_t n_grid, int32_t kmax, const float *h_prior,
                     const int32_t *h_kcnt, float lam, double w_rot, double w_trans, float *h_xout, int32_t *h_stats,
                     double *h_loss);
+/* The context-free entry points above (geobpe_rmsd / geobpe_nerf / geobpe_glue_opt) keep one
+   stream and one grown scratch arena per (device, entry point), each behind its own lock.
+   This frees the arenas of `device` (-1: every device); the next call re-creates them. */
+int geobpe_arena_release(int device);
 int geobpe_set_record_events(geobpe_ctx *ctx, int on);
 int64_t geobpe_events(geobpe_ctx *ctx, int32_t *h_merge, int32_t *h_a, int32_t *h_b);
 

@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <type_traits>
@@ -108,7 +109,7 @@ struct geobpe_ctx {
   int32_t x_world = 1, x_rank = 0;
   uint8_t *x_pbuf = nullptr, *x_gath = nullptr, *x_tmp = nullptr, *x_flat = nullptr;
   int64_t* x_head = nullptr;  // the slot header of the last pipelined iteration (its record count)
-  int64_t x_pcap = 0, x_tmp_bytes = 0, x_flat_bytes = 0;
+  int64_t x_pcap = 0, x_tmp_bytes = 0, x_flat_bytes = 0, x_gath_bytes = 0;
   uint8_t *x_hsend = nullptr, *x_hrecv = nullptr;  // (host callback: pinned staging)
   int64_t x_hbytes = 0;
   int64_t x_ahead = 1, x_capf = 1024, x_fixed = 0;  // poll window and slot size carry over between runs
@@ -1603,19 +1604,28 @@ namespace {
 // The context-free entry points (glue opt, NeRF, Kabsch) keep one stream and one scratch arena
 // per (device, entry point) for the process, grown on demand: the RMSD mode calls them once or
 // twice per key and induce once per chain, where a stream and a few allocations per call used
-// to outweigh the kernels.  The lock serialises calls on one arena.
+// to outweigh the kernels.  Each arena has its own lock (calls on different devices or entry
+// points run concurrently; calls on one arena are serialised); geobpe_arena_release returns
+// the memory and the streams.
 struct Arena {
+  std::mutex mu;
   hipStream_t s = nullptr;
   char* buf = nullptr;
   size_t cap = 0;
 };
-std::mutex g_arena_mu;
-std::map<std::pair<int, int>, Arena> g_arena;
+std::mutex g_arena_mu;  // guards the map only
+std::map<std::pair<int, int>, std::unique_ptr<Arena>> g_arena;
 enum { ARENA_GLUE = 0, ARENA_NERF = 1, ARENA_RMSD = 2 };
 
-// the arena's stream and n buffers of sizes[i] bytes (256-B aligned) in ptr[i]; the caller holds g_arena_mu
-int arena_take(int device, int which, int n, const size_t* sizes, void** ptr, hipStream_t* s) {
-  Arena& ar = g_arena[std::make_pair(device, which)];
+Arena& arena_of(int device, int which) {
+  std::lock_guard<std::mutex> lock(g_arena_mu);
+  std::unique_ptr<Arena>& p = g_arena[std::make_pair(device, which)];
+  if (!p) p.reset(new Arena());
+  return *p;  // (entries are never erased: the reference stays valid)
+}
+
+// the arena's stream and n buffers of sizes[i] bytes (256-B aligned) in ptr[i]; the caller holds ar.mu
+int arena_take(Arena& ar, int n, const size_t* sizes, void** ptr, hipStream_t* s) {
   if (!ar.s && hipStreamCreateWithFlags(&ar.s, hipStreamNonBlocking) != hipSuccess) {
     ar.s = nullptr;
     return GEOBPE_EHIP;
@@ -1640,6 +1650,26 @@ int arena_take(int device, int which, int n, const size_t* sizes, void** ptr, hi
 }
 }  // namespace
 
+int geobpe_arena_release(int device) {
+  std::vector<Arena*> arenas;
+  {
+    std::lock_guard<std::mutex> lock(g_arena_mu);
+    for (auto& kv : g_arena)
+      if (device < 0 || kv.first.first == device) arenas.push_back(kv.second.get());
+  }
+  int rc = 0;
+  for (Arena* ar : arenas) {
+    std::lock_guard<std::mutex> lock(ar->mu);
+    if (ar->s && hipStreamSynchronize(ar->s) != hipSuccess) rc = GEOBPE_EHIP;
+    if (ar->buf) hipFree(ar->buf);
+    if (ar->s) hipStreamDestroy(ar->s);
+    ar->buf = nullptr;
+    ar->cap = 0;
+    ar->s = nullptr;
+  }
+  return rc;
+}
+
 int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const double* h_a, const double* h_b,
                 int symmetric, double* h_out) {
   if (n_a < 0 || n_atoms <= 0 || !h_a || !h_out) return GEOBPE_EARG;
@@ -1652,11 +1682,12 @@ int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const dou
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
   const int64_t la = (int64_t)n_a * n_atoms * 3, lb = (int64_t)n_b * n_atoms * 3, no = (int64_t)n_a * n_b;
   double *d_a = nullptr, *d_b = nullptr, *d_out = nullptr;
-  std::lock_guard<std::mutex> lock(g_arena_mu);
+  Arena& ar = arena_of(device, ARENA_RMSD);
+  std::lock_guard<std::mutex> lock(ar.mu);
   hipStream_t s;
   const size_t sizes[3] = {(size_t)la * 8, symmetric ? 0 : (size_t)lb * 8, (size_t)no * 8};
   void* ptr[3];
-  int rc = arena_take(device, ARENA_RMSD, 3, sizes, ptr, &s);
+  int rc = arena_take(ar, 3, sizes, ptr, &s);
   if (!rc) {
     d_a = (double*)ptr[0];
     d_b = symmetric ? nullptr : (double*)ptr[1];
@@ -1684,11 +1715,12 @@ int geobpe_nerf(int device, int64_t n_spans, const int64_t* h_res_off, const dou
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
   int64_t* d_off = nullptr;
   double *d_geo = nullptr, *d_out = nullptr;
-  std::lock_guard<std::mutex> lock(g_arena_mu);
+  Arena& ar = arena_of(device, ARENA_NERF);
+  std::lock_guard<std::mutex> lock(ar.mu);
   hipStream_t s;
   const size_t sizes[3] = {(size_t)(n_spans + 1) * 8, (size_t)R * 9 * 8, (size_t)R * 9 * 8};
   void* ptr[3];
-  int rc = arena_take(device, ARENA_NERF, 3, sizes, ptr, &s);
+  int rc = arena_take(ar, 3, sizes, ptr, &s);
   if (!rc) {
     d_off = (int64_t*)ptr[0];
     d_geo = (double*)ptr[1];
@@ -1726,7 +1758,8 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
   for (int64_t i = 0; i < 3 * (int64_t)n_grid; i++)
     if (h_kcnt[i] <= 0 || h_kcnt[i] > kmax) return GEOBPE_EARG;
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
-  std::lock_guard<std::mutex> lock(g_arena_mu);  // (the per-device arena: see arena_take)
+  Arena& ar = arena_of(device, ARENA_GLUE);
+  std::lock_guard<std::mutex> lock(ar.mu);  // (the per-device arena: see arena_take)
   hipStream_t s = nullptr;
   const int64_t pmax = 3 * (rmax - 1), S = n_chains;
   GlueProb P{};
@@ -1754,7 +1787,7 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
                             (size_t)S * 2 * 4, (size_t)S * 2 * 8, (size_t)nx * 8, (size_t)nx * 8,
                             (size_t)GLUE_NVEC * nv * 4, (size_t)2 * GLUE_HIST * nv * 4};
   void* ptr[14];
-  const bool ok = arena_take(device, ARENA_GLUE, 14, sizes, ptr, &s) == 0;
+  const bool ok = arena_take(ar, 14, sizes, ptr, &s) == 0;
   if (ok) {
     d_off = (int64_t*)ptr[0];
     d_geo = (double*)ptr[1];
@@ -2036,11 +2069,12 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
   int rc;
   if (!c->x_pbuf) {
     c->x_pcap = 3 * c->R + 65536;
-    const int64_t top = c->x_fixed ? c->x_fixed : CAP_MAX;
     HIPCHK(c, hipMalloc((void**)&c->x_pbuf, (size_t)((1 + c->x_pcap) * REC)));
     HIPCHK(c, hipMemsetAsync(c->x_pbuf, 0, (size_t)((1 + c->x_pcap) * REC), c->stream));
-    HIPCHK(c, hipMalloc((void**)&c->x_gath, (size_t)(W * (1 + top) * REC)));
   }
+  // the gathered slots: W x the largest slot this run can use (geobpe_comm_set_slot may have
+  // raised the fixed size since the last run)
+  if ((rc = grow_dev(c, &c->x_gath, &c->x_gath_bytes, W * (1 + std::max(CAP_MAX, c->x_fixed)) * REC))) return rc;
   if ((rc = geobpe_pipeline_begin(c))) return rc;
   int64_t out[4];
   int64_t done = 0;
@@ -2048,18 +2082,21 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
   const int64_t it0 = out[1];
   int64_t ahead = c->x_ahead, capf = c->x_fixed ? c->x_fixed : c->x_capf;
   while (!rc && done < n_merges) {
-    // the middle regime once this rank's share of a merge is small (a poll is a quiescent
-    // point: the lists are built, or rebuilt after an iteration stalled on them)
+    // the middle regime once the winner's count is small (a poll is a quiescent point: the
+    // lists are built, or rebuilt after an iteration stalled on them).  The decision and the
+    // poll window read only replicated data -- the winner's global count from the replicated
+    // counts, the iteration number -- so every rank switches at the same poll and issues the
+    // same collectives (a rank's own merged count would let ranks part ways)
     int64_t win = ahead;
     if (!c->mid_on && mid_enabled(c) && c->h_state->iter > 0) {
       LogRec lr;
       HIPCHK(c, hipMemcpy(&lr, c->D.log + (c->h_state->iter - 1), sizeof lr, hipMemcpyDeviceToHost));
-      if (lr.nmerged <= c->mid_thresh) {
+      if (lr.count <= c->mid_thresh) {
         c->mid_on = true;
         // the middle regime's records are per (workgroup, key), not per owner and key: a
         // merge of the same size sends up to ~4x as many -- a slot that small would stall
         if (!c->x_fixed) capf = std::min(CAP_MAX, 4 * capf);
-      } else if (lr.nmerged <= 2 * c->mid_thresh) {
+      } else if (lr.count <= 2 * c->mid_thresh) {
         win = std::min<int64_t>(win, 8);  // (close: poll sooner)
       }
     }

@@ -255,8 +255,13 @@ static PyObject* build_key(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ss
       if (m_hi > cnt) m_hi = cnt;
     }
     PyObject* th = PyTuple_GET_ITEM(thr, t);
-    if (m_lo < m_hi && (th == Py_None || !PyTuple_Check(th) || PyTuple_GET_SIZE(th) != 2)) {
-      PyErr_SetString(PyExc_ValueError, "rmsdkey.key: no thresholds for a binned item type");
+    if (m_lo < m_hi && (!PyTuple_Check(th) || PyTuple_GET_SIZE(th) != 2)) {
+      /* the type has no thresholds at this length: _edges_for stored the exception the
+         reference's lookup raised (KeyError / TypeError, bpe.py:1247-1296); raise that one */
+      if (PyExceptionInstance_Check(th))
+        PyErr_SetObject((PyObject*)Py_TYPE(th), th);
+      else
+        PyErr_SetString(PyExc_ValueError, "rmsdkey.key: no thresholds for a binned item type");
       goto fail;
     }
     if (!first_key && buf_str(&b, ", ") < 0) goto fail;

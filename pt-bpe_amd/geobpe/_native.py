@@ -125,6 +125,7 @@ def lib():
                                            ctypes.c_float, ctypes.c_double, ctypes.c_double, P, P, P]),
         "geobpe_rmsd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P, P,
                                        ctypes.c_int, P]),
+        "geobpe_arena_release": (ctypes.c_int, [ctypes.c_int]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -147,7 +148,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_pipeline_import", "geobpe_pipeline_poll", "geobpe_pipeline_resolve", "geobpe_pipeline_end",
     "geobpe_comm_unique_id", "geobpe_comm_init_rccl", "geobpe_comm_error", "geobpe_comm_set_callback",
     "geobpe_comm_set_slot", "geobpe_run_exchange", "geobpe_pdb_backbone", "geobpe_pdb_error",
-    "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf", "geobpe_glue_opt",
+    "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf", "geobpe_glue_opt", "geobpe_arena_release",
 ]
 
 

@@ -52,6 +52,14 @@ def _run(a: np.ndarray, b, symmetric: bool, device: int) -> np.ndarray:
     return out
 
 
+def release_scratch(device: int = -1) -> None:
+    """Free the device scratch arenas of geobpe_rmsd / geobpe_nerf / geobpe_glue_opt
+    (geobpe_arena_release; -1: every device).  The next call re-creates them."""
+    rc = _native.lib().geobpe_arena_release(device)
+    if rc:
+        raise _native.GeoBPEError(f"geobpe_arena_release failed (code {rc})")
+
+
 def rmsd_cross(A, B, device: int = 0) -> np.ndarray:
     """float64 (len(A), len(B)): compute_rmsd(A_i, B_j) (B_j aligned onto A_i)."""
     return _run(_coords(A), _coords(B), False, device)

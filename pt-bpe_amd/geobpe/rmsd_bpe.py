@@ -680,9 +680,10 @@ class RmsdBPE:
         act = coords[active] if isinstance(coords, np.ndarray) else [coords[i] for i in active]
         k = self.num_partitions[size]
         medoids = _rmsd.k_medoids(act, k, rng=self.rng, device=self.device)
-        if len(medoids) != k:
+        if len(medoids) not in (1, k):
             # the reference stores the medoids in a memmap of num_partitions[size] entries
-            # (bpe.py:299-300): fewer structures than partitions fail the write there
+            # (bpe.py:299-300): numpy broadcasts one medoid into it (one structure of the
+            # size: the run goes on with that medoid list), any other shortfall fails the write
             raise ValueError(f"could not broadcast input array from shape ({len(medoids)},) into shape ({k},)")
         assign = self._assign(coords, [act[m] for m in medoids])
         key = RES_SPHERE_KEY[size]
@@ -728,7 +729,9 @@ class RmsdBPE:
 
     def _edges_for(self, L):
         """The (left edges, right edges) lists of every item type's thresholds at span length L,
-        in json key order (rmsdkey.c's layout); None for a type whose thresholds do not exist."""
+        in json key order (rmsdkey.c's layout).  For a type whose thresholds do not exist the
+        entry is the exception the lookup raised: rmsdkey.c raises it when such a type is
+        binned, so the C key and the C merge loop fail as _pair_key_py (the reference) does."""
         thr_all = self._thresholds
         thr_L = self._thr_by_len.get(L)
         if thr_L is None:
@@ -739,9 +742,9 @@ class RmsdBPE:
             try:
                 thr = (thr_all[k] if self.std_bonds else thr_L[k]) if kind == 0 else thr_L[k]
                 out.append(([float(a) for a, _ in thr], [float(b) for _, b in thr]))
-            except (KeyError, TypeError):
-                out.append(None)  # (the C key raises only if such a type is binned: then the
-        return tuple(out)         #  Python restatement reproduces the reference's error)
+            except (KeyError, TypeError) as e:
+                out.append(e.with_traceback(None))
+        return tuple(out)
 
     def _edges_store(self, L):
         """_edges_for(L), cached (called by csrc/rmsdkey.c merge for a length it has not seen)."""

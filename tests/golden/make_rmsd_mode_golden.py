@@ -66,6 +66,10 @@ FIXTURES = {
     # pdb_angles.py) in the README's first run minus glue optimisation: --bins 1-50, p = 0,
     # --num-p 2-2:3-5:5-1:6-2:8-1, max_num_strucs 500, free bonds, rmsd_super_res
     "rm_pdb72_readme": ("pdb72", None, None, 0, 50, 0, True, 500, 20, {2: 2, 3: 5, 5: 1, 6: 2, 8: 1}, False),
+    # one chain: its last residue is the only size-2 structure, k_medoids returns [0] and the
+    # reference's memmap write of num_partitions[2] = 2 entries broadcasts that one medoid
+    # (bpe.py:298-300); the run carries on with one size-2 partition
+    "rm_p0_one_chain": (1, 30, 40, 34, 5, 0, False, 60, 20),
 }
 # BPE.tokenize (bpe.py:1053-1140, the RMSD mode's induce) after the training calls, on: the
 # first three training chains, the first 60 % of chains 3 and 4 (values inside the trained

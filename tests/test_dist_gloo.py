@@ -90,13 +90,22 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
         from geobpe.engine import GeoBPEEngine
         corpus = synth.make_corpus(synth.make_lengths(2000, 20, 300, seed=91), seed=91, repeat_frac=0.05)
         lo, hi = shard_rows(corpus["row_off"], world)[rank]
+        mid = None
+        if mode == "skewed":
+            # rank 0 holds 5 % of the rows: its own merged counts sit far below the others', so
+            # a switch to the middle regime decided per rank would part the ranks' collectives
+            # (ADVICE r3); the switch must follow the replicated winner count (mid = 1500 puts
+            # it inside the run)
+            cuts = [0, 100] + [100 + (1900 * (r + 1)) // (world - 1) for r in range(world - 1)]
+            lo, hi = cuts[rank], cuts[rank + 1]
+            mid = 1500
         shard = slice_corpus(corpus, lo, hi)
         g = TorchGroup(int(shard["row_off"][-1]), device=0)
         if mode == "small-slots":  # most merges overflow the fixed slots: the stall / resolve path
             g.pipe_cap = 16
         if mode == "host-loop":  # the Python-driven loop (geobpe.dist) instead of geobpe_run_exchange
             g.engine_exchange = False
-        e = GeoBPEEngine(shard, 5, device=0, group=g).initialize()
+        e = GeoBPEEngine(shard, 5, device=0, group=g, mid=mid).initialize()
         e.pipelined = mode != "stepwise"
         e.bin()
         done = e.run(70)
@@ -107,6 +116,8 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
         else:
             done += e.run(80)  # a second pipelined run continues the device parity
         s, ids, off = e.segmentation()
+        if mode == "skewed":
+            assert e.merges[0][1] > mid >= e.merges[-1][1], "the run does not cross the middle-regime threshold"
         q.put((rank, done, e.merge_keys(), ids.tolist()))
     except Exception as ex:  # pragma: no cover
         q.put((rank, -1, repr(ex), None))
@@ -116,7 +127,8 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise"),
-                                         (3, "mixed"), (4, "small-slots"), (2, "host-loop")])
+                                         (3, "mixed"), (4, "small-slots"), (2, "host-loop"), (2, "skewed"),
+                                         (3, "skewed")])
 def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
     """The full N>1 path (TorchGroup exchange, one process per rank) with gloo on
     one device: the engine's pipelined loop (geobpe_run_exchange over the group's host

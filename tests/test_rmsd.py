@@ -48,6 +48,18 @@ def test_device_rmsd_matches_reference(ref):
 
 
 @pytest.mark.gpu
+def test_device_scratch_release(ref):
+    """geobpe_arena_release frees the per-device arenas; the next calls re-create them and
+    give the same bits (arenas were kept for the process's lifetime)."""
+    from geobpe import rmsd
+    D1 = rmsd.rmsd_matrix(ref["A"])
+    rmsd.release_scratch(0)
+    D2 = rmsd.rmsd_matrix(ref["A"])
+    rmsd.release_scratch()
+    assert np.array_equal(D1, D2)
+
+
+@pytest.mark.gpu
 def test_device_k_medoids_and_assignment_match_reference(ref):
     from geobpe import rmsd
     m = rmsd.k_medoids(list(ref["A"]), 5, rng=np.random.default_rng(3))

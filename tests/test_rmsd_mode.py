@@ -365,6 +365,39 @@ def test_pair_key_c_matches_python(name, host_geometry):
     assert kc == kp
 
 
+def test_pair_key_missing_thresholds_raises_like_python(host_geometry):
+    """An item type with no thresholds at the span's length: the C key raises the
+    exception the Python restatement (the reference's lookup) raises, type and message."""
+    from geobpe import rmsd_bpe
+    from geobpe.bpe import BPE
+    meta, corpus, arrs = _load("rm_p0")
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()}, rmsd_partition_min_size=0,
+              num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, seed=meta["rng_seed"])
+    bpe.initialize()
+    bpe.bin()
+    c = bpe._chains[0]
+    (i1, _, l1), (_, _, l2) = c.tokens()[0], c.tokens()[1]
+    L = l1 + l2
+
+    class NoOmega(dict):
+        def __getitem__(self, k):
+            if k == "omega":  # (a junction dihedral: binned in every pair key)
+                raise KeyError(k)
+            return dict.__getitem__(self, k)
+
+    bpe._thr_by_len[L] = NoOmega(bpe._thresholds[L])
+    bpe._key_edges.pop(L, None)
+    got = []
+    for py in (False, True):
+        bpe._py_keys = py
+        with pytest.raises(KeyError) as e:
+            bpe._pair_key(0, i1, l1, l2)
+        got.append((type(e.value), e.value.args))
+    bpe._py_keys = False
+    assert rmsd_bpe._KEYC is not None and got[0] == got[1]
+
+
 def test_key_float_repr_matches_python():
     """csrc/frepr.cpp (std::to_chars' shortest digits laid out as float.__repr__ does) against
     Python's repr on 200 000 doubles: random bit patterns (subnormals, huge exponents), scaled

@@ -1,4 +1,4 @@
-# usage: bash tools/r3_ab.sh <tag> lib1.so lib2.so ...   (GPU box)
+# usage: bash tools/ab.sh <tag> lib1.so lib2.so ...   (GPU box)
 # kernel A/B: the driver window (merges 6..25) twice and the default run (merges 11..1000) once
 # per library variant, alternating variants; outputs under gpurun_out/ab_<tag>/
 set -o pipefail

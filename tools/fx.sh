@@ -1,11 +1,11 @@
-# usage: bash tools/r3_fx.sh <tag> [pytest -k expr]: the multi-rank tests (engine-owned exchange over
+# usage: bash tools/fx.sh <tag> [pytest -k expr]: the multi-rank tests (engine-owned exchange over
 # gloo on one GPU), then the 1-GPU RCCL rehearsal of the N > 1 loop (--force-exchange) on the driver
 # window and the default run, and a kernel trace of the default forced-exchange run; outputs under
-# gpurun_out/r3_<tag>/
+# gpurun_out/<tag>/
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-OUT=gpurun_out/r3_$1
+OUT=gpurun_out/$1
 K=${2:-"dist_gloo or pipelined_ranks or test_bench"}
 mkdir -p $OUT
 ( while true; do date +%T >> $OUT/heartbeat; sleep 50; done ) &

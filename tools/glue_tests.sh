@@ -1,8 +1,8 @@
-# usage: bash tools/r3_glue.sh <tag>: the glue-optimisation GPU tests with their printed drift
-# statistics (-s), outputs under gpurun_out/r3_<tag>/
+# usage: bash tools/glue_tests.sh <tag>: the glue-optimisation GPU tests with their printed drift
+# statistics (-s), outputs under gpurun_out/<tag>/
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-OUT=gpurun_out/r3_$1
+OUT=gpurun_out/$1
 mkdir -p $OUT
 ( while true; do date +%T >> $OUT/heartbeat; sleep 50; done ) &
 HB=$!
