@@ -305,6 +305,15 @@ typedef int (*geobpe_allgather_fn)(void *user, const void *send, void *recv, int
 int geobpe_comm_set_callback(geobpe_ctx *ctx, geobpe_allgather_fn fn, void *user, int32_t nranks, int32_t rank);
 /* Fixed slot size in records (0 = sized from the last import; tests force stalls with it). */
 int geobpe_comm_set_slot(geobpe_ctx *ctx, int64_t records);
+/* At the middle-regime switch (the winner's global count <= geobpe_set_mid's threshold),
+ * geobpe_run_exchange stops sharding: every rank gathers every rank's token records once,
+ * re-keys them in its own key table and continues as the one-rank loop over the whole corpus
+ * (no exchange per merge; every rank makes the same merges).  Segmentation / encode / token
+ * counts keep reporting this rank's rows.  on = 0 keeps the sharded exchange to the end.
+ * (No reference counterpart: the reference has no multi-GPU path) */
+int geobpe_set_collapse(geobpe_ctx *ctx, int on);
+/* 1 once the engine has collapsed (then geobpe_step / geobpe_run drive it, as one rank). */
+int geobpe_collapsed(geobpe_ctx *ctx);
 /* n_merges merges of the row-sharded N > 1 loop with no host wait per merge: per iteration
  * the merge kernels and the slot export, one all-gather of the fixed slots on the engine's
  * stream, the import; polls every few iterations; a merge whose records overflowed a slot

@@ -301,10 +301,26 @@ __device__ inline u64 probe_key(u64 h1, u64 h2, int32_t len) {
   return k ? k : 1;
 }
 
+// The first error wins (GEOBPE_E*, and where it happened).  Out of line: its call sites sit
+// on cold paths of the merge kernels, and inlined, their 64-bit constants were hoisted into
+// VGPRs that the 128-VGPR budget of a 1024-thread workgroup then spilled to scratch -- every
+// lane of every launch wrote ~28 B of scratch (k_find / k_mid_find: ~7-8 MB of HBM writes
+// per launch at the kernel end).  A call materialises them in the cold block instead.
+#ifndef SET_ERROR_INLINE
+#define SET_ERROR_INLINE 0  // (A/B: 1 = the inlined form)
+#endif
+#if SET_ERROR_INLINE
 __device__ inline void set_error(const Dev& D, int64_t code, int64_t pos) {
   unsigned long long* p = (unsigned long long*)&D.st->err_code;
   if (atomicCAS(p, 0ULL, (unsigned long long)code) == 0ULL) D.st->err_pos = pos;
 }
+#else
+__device__ __attribute__((noinline, cold)) void set_error_at(State* st, int64_t code, int64_t pos) {
+  unsigned long long* p = (unsigned long long*)&st->err_code;
+  if (atomicCAS(p, 0ULL, (unsigned long long)code) == 0ULL) st->err_pos = pos;
+}
+__device__ inline void set_error(const Dev& D, int64_t code, int64_t pos) { set_error_at(D.st, code, pos); }
+#endif
 
 // Python / numpy  (v + 2*pi) % (2*pi)  in float64 (float_rem / npy_divmod)
 __device__ inline double wrap2pi(double v) {

@@ -113,6 +113,10 @@ struct geobpe_ctx {
   uint8_t *x_hsend = nullptr, *x_hrecv = nullptr;  // (host callback: pinned staging)
   int64_t x_hbytes = 0;
   int64_t x_ahead = 1, x_capf = 1024, x_fixed = 0;  // poll window and slot size carry over between runs
+  // collapse at the middle-regime switch (geobpe_set_collapse): every rank then holds the whole
+  // corpus and runs the one-rank loop; its own rows are [own_row0, own_row1) of it
+  bool collapse_on = true, collapsed = false;
+  int64_t own_row0 = 0, own_row1 = -1;
   // profiling
   bool prof = false;
   int prof_stride = 1;      // time every prof_stride-th launch of each kernel
@@ -159,6 +163,15 @@ int dalloc(geobpe_ctx* c, T** p, int64_t n, int fill = -1) {
     if (e != hipSuccess) return fail(c, GEOBPE_EHIP, "hipMemsetAsync: %s", hipGetErrorString(e));
   }
   return 0;
+}
+
+template <class T>
+void dfree(geobpe_ctx* c, T** p) {
+  if (!*p) return;
+  auto it = std::find(c->allocs.begin(), c->allocs.end(), (void*)*p);
+  if (it != c->allocs.end()) c->allocs.erase(it);
+  hipFree((void*)*p);
+  *p = nullptr;
 }
 
 // ---------------------------------------------------------------- light kernel timing
@@ -404,11 +417,13 @@ int tail_alloc(geobpe_ctx* c) {
   D.TMcap = c->R / 2 + 1024 + MSEG_TM;  // (mid.h: the find workgroups' segments, then the spill list)
   D.THcap = c->R + 2048 + MSEG_TH;
   int rc;
-  // (zero: a key claimed after the list build starts with an empty list of capacity 0)
-  if ((rc = dalloc(c, &D.kp_off, D.HC, 0)) || (rc = dalloc(c, &D.kp_n, D.HC, 0)) || (rc = dalloc(c, &D.kp_cap, D.HC, 0)) ||
-      (rc = dalloc(c, &D.kpool, D.KPOOL, 0xFF)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, 2 * D.THcap)) ||
-      (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)) ||
-      (rc = dalloc(c, &D.mcnt, 2 * NBA_MAX, 0)))
+  // (zero: a key claimed after the list build starts with an empty list of capacity 0; the
+  // key-indexed arrays outlive a collapse, the residue-sized ones are made again for it)
+  if (!D.kp_off && ((rc = dalloc(c, &D.kp_off, D.HC, 0)) || (rc = dalloc(c, &D.kp_n, D.HC, 0)) ||
+                    (rc = dalloc(c, &D.kp_cap, D.HC, 0)) || (rc = dalloc(c, &D.mcnt, 2 * NBA_MAX, 0))))
+    return rc;
+  if ((rc = dalloc(c, &D.kpool, D.KPOOL, 0xFF)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, 2 * D.THcap)) ||
+      (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)))
     return rc;
   c->tail_ready = true;
   return 0;
@@ -1304,13 +1319,21 @@ int64_t geobpe_debug_state(geobpe_ctx* c, int64_t* h_out, int64_t cap) {
   return n;
 }
 
+// the rows this context reports: all of them, or after a collapse its own rank's window
+static void own_rows(const geobpe_ctx* c, int64_t* r0, int64_t* r1) {
+  *r0 = c->collapsed ? c->own_row0 : 0;
+  *r1 = c->collapsed ? c->own_row1 : c->nrows;
+}
+
 int64_t geobpe_num_tokens(geobpe_ctx* c) {
   if (!c || !c->R) return -1;
   std::vector<int64_t> off;
   int64_t* d;
   if (row_token_offsets(c, off, &d)) return -1;
   hipFree(d);
-  return off.back();
+  int64_t r0, r1;
+  own_rows(c, &r0, &r1);
+  return off[r1] - off[r0];
 }
 
 int64_t geobpe_segmentation(geobpe_ctx* c, int32_t* h_start, int32_t* h_id, int64_t* h_row_tok_off) {
@@ -1319,20 +1342,23 @@ int64_t geobpe_segmentation(geobpe_ctx* c, int32_t* h_start, int32_t* h_id, int6
   std::vector<int64_t> off;
   int64_t* d_off;
   if (row_token_offsets(c, off, &d_off)) return -1;
-  const int64_t T = off.back();
-  if (h_row_tok_off) memcpy(h_row_tok_off, off.data(), (c->nrows + 1) * 8);
+  int64_t r0, r1;
+  own_rows(c, &r0, &r1);
+  const int64_t T = off.back(), t0 = off[r0], Tw = off[r1] - off[r0];
+  if (h_row_tok_off)
+    for (int64_t r = r0; r <= r1; r++) h_row_tok_off[r - r0] = off[r] - t0;
   if (h_start || h_id) {
     int32_t *ds, *di;
     if (hipMalloc(&ds, T * 4 + 4) != hipSuccess || hipMalloc(&di, T * 4 + 4) != hipSuccess) return -1;
     hipLaunchKernelGGL(k_row_seg, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (const int64_t*)d_off, ds, di);
-    if (h_start) hipMemcpyAsync(h_start, ds, T * 4, hipMemcpyDeviceToHost, c->stream);
-    if (h_id) hipMemcpyAsync(h_id, di, T * 4, hipMemcpyDeviceToHost, c->stream);
+    if (h_start) hipMemcpyAsync(h_start, ds + t0, Tw * 4, hipMemcpyDeviceToHost, c->stream);
+    if (h_id) hipMemcpyAsync(h_id, di + t0, Tw * 4, hipMemcpyDeviceToHost, c->stream);
     hipStreamSynchronize(c->stream);
     hipFree(ds);
     hipFree(di);
   }
   hipFree(d_off);
-  return T;
+  return Tw;
 }
 
 int64_t geobpe_encode(geobpe_ctx* c, int32_t* h_ids, int64_t* h_row_id_off) {
@@ -1345,19 +1371,22 @@ int64_t geobpe_encode(geobpe_ctx* c, int32_t* h_ids, int64_t* h_row_id_off) {
   if (row_token_offsets(c, off, &d_off)) return -1;
   std::vector<int64_t> ioff(c->nrows + 1, 0);
   for (int64_t r = 0; r < c->nrows; r++) ioff[r + 1] = ioff[r] + 4 * (off[r + 1] - off[r]) - 3;
-  const int64_t T = ioff.back();
-  if (h_row_id_off) memcpy(h_row_id_off, ioff.data(), (c->nrows + 1) * 8);
+  int64_t r0, r1;
+  own_rows(c, &r0, &r1);
+  const int64_t T = ioff.back(), i0 = ioff[r0], Tw = ioff[r1] - ioff[r0];
+  if (h_row_id_off)
+    for (int64_t r = r0; r <= r1; r++) h_row_id_off[r - r0] = ioff[r] - i0;
   if (h_ids) {
     int32_t* di;
     if (hipMalloc(&di, T * 4 + 4) != hipSuccess) return -1;
     hipMemcpyAsync(d_off, ioff.data(), (c->nrows + 1) * 8, hipMemcpyHostToDevice, c->stream);
     hipLaunchKernelGGL(k_row_encode, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (const int64_t*)d_off, di, K);
-    hipMemcpyAsync(h_ids, di, T * 4, hipMemcpyDeviceToHost, c->stream);
+    hipMemcpyAsync(h_ids, di + i0, Tw * 4, hipMemcpyDeviceToHost, c->stream);
     hipStreamSynchronize(c->stream);
     hipFree(di);
   }
   hipFree(d_off);
-  return T;
+  return Tw;
 }
 
 int64_t geobpe_verify_counts(geobpe_ctx* c) {
@@ -1617,11 +1646,11 @@ std::mutex g_arena_mu;  // guards the map only
 std::map<std::pair<int, int>, std::unique_ptr<Arena>> g_arena;
 enum { ARENA_GLUE = 0, ARENA_NERF = 1, ARENA_RMSD = 2 };
 
-Arena& arena_of(int device, int which) {
+Arena* arena_of(int device, int which) {
   std::lock_guard<std::mutex> lock(g_arena_mu);
   std::unique_ptr<Arena>& p = g_arena[std::make_pair(device, which)];
   if (!p) p.reset(new Arena());
-  return *p;  // (entries are never erased: the reference stays valid)
+  return p.get();  // (entries are never erased: the pointer stays valid)
 }
 
 // the arena's stream and n buffers of sizes[i] bytes (256-B aligned) in ptr[i]; the caller holds ar.mu
@@ -1682,7 +1711,7 @@ int geobpe_rmsd(int device, int32_t n_a, int32_t n_b, int32_t n_atoms, const dou
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
   const int64_t la = (int64_t)n_a * n_atoms * 3, lb = (int64_t)n_b * n_atoms * 3, no = (int64_t)n_a * n_b;
   double *d_a = nullptr, *d_b = nullptr, *d_out = nullptr;
-  Arena& ar = arena_of(device, ARENA_RMSD);
+  Arena& ar = *arena_of(device, ARENA_RMSD);
   std::lock_guard<std::mutex> lock(ar.mu);
   hipStream_t s;
   const size_t sizes[3] = {(size_t)la * 8, symmetric ? 0 : (size_t)lb * 8, (size_t)no * 8};
@@ -1715,7 +1744,7 @@ int geobpe_nerf(int device, int64_t n_spans, const int64_t* h_res_off, const dou
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
   int64_t* d_off = nullptr;
   double *d_geo = nullptr, *d_out = nullptr;
-  Arena& ar = arena_of(device, ARENA_NERF);
+  Arena& ar = *arena_of(device, ARENA_NERF);
   std::lock_guard<std::mutex> lock(ar.mu);
   hipStream_t s;
   const size_t sizes[3] = {(size_t)(n_spans + 1) * 8, (size_t)R * 9 * 8, (size_t)R * 9 * 8};
@@ -1758,7 +1787,7 @@ int geobpe_glue_opt(int device, int64_t n_chains, const int64_t* h_res_off, cons
   for (int64_t i = 0; i < 3 * (int64_t)n_grid; i++)
     if (h_kcnt[i] <= 0 || h_kcnt[i] > kmax) return GEOBPE_EARG;
   if (hipSetDevice(device) != hipSuccess) return GEOBPE_EHIP;
-  Arena& ar = arena_of(device, ARENA_GLUE);
+  Arena& ar = *arena_of(device, ARENA_GLUE);
   std::lock_guard<std::mutex> lock(ar.mu);  // (the per-device arena: see arena_take)
   hipStream_t s = nullptr;
   const int64_t pmax = 3 * (rmax - 1), S = n_chains;
@@ -1984,6 +2013,15 @@ int geobpe_comm_set_slot(geobpe_ctx* c, int64_t records) {
   return 0;
 }
 
+int geobpe_set_collapse(geobpe_ctx* c, int on) {
+  if (!c) return GEOBPE_EARG;
+  if (c->collapsed && !on) return fail(c, GEOBPE_EARG, "the engine has collapsed already");
+  c->collapse_on = on != 0;
+  return 0;
+}
+
+int geobpe_collapsed(geobpe_ctx* c) { return c && c->collapsed ? 1 : 0; }
+
 namespace {
 
 int grow_dev(geobpe_ctx* c, uint8_t** p, int64_t* have, int64_t bytes) {
@@ -2010,6 +2048,7 @@ int x_allgather(geobpe_ctx* c, const void* d_send, void* d_recv, int64_t bytes) 
   }
   const int64_t need = bytes * c->x_world;
   if (c->x_hbytes < need) {
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (the last copy out of x_hrecv may be in flight)
     if (c->x_hsend) hipHostFree(c->x_hsend);
     if (c->x_hrecv) hipHostFree(c->x_hrecv);
     HIPCHK(c, hipHostMalloc((void**)&c->x_hsend, (size_t)need, hipHostMallocDefault));
@@ -2052,6 +2091,156 @@ int x_resolve(geobpe_ctx* c) {
   return geobpe_pipeline_resolve(c, c->x_flat, total);
 }
 
+// every rank's `bytes` of host data, rank-major, through the exchange (device staging)
+int x_allgather_host(geobpe_ctx* c, const void* h_send, int64_t bytes, std::vector<uint8_t>& h_recv) {
+  const int64_t W = c->x_world;
+  int rc;
+  if ((rc = grow_dev(c, &c->x_flat, &c->x_flat_bytes, bytes)) ||
+      (rc = grow_dev(c, &c->x_tmp, &c->x_tmp_bytes, W * bytes)))
+    return rc;
+  HIPCHK(c, hipMemcpyAsync(c->x_flat, h_send, (size_t)bytes, hipMemcpyHostToDevice, c->stream));
+  if ((rc = x_allgather(c, c->x_flat, c->x_tmp, bytes))) return rc;
+  h_recv.resize((size_t)(W * bytes));
+  HIPCHK(c, hipMemcpyAsync(h_recv.data(), c->x_tmp, (size_t)(W * bytes), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return 0;
+}
+
+// every rank's block of n[r] elements of `per` bytes (d_src: this rank's) into d_dst at the
+// rank's element base: one all-gather of blocks padded to the largest
+int x_gather_blocks(geobpe_ctx* c, const void* d_src, void* d_dst, const std::vector<int64_t>& n,
+                    const std::vector<int64_t>& base, int64_t per) {
+  const int64_t W = c->x_world;
+  const int64_t nmax = *std::max_element(n.begin(), n.end());
+  int rc;
+  if ((rc = grow_dev(c, &c->x_flat, &c->x_flat_bytes, std::max<int64_t>(nmax * per, 8))) ||
+      (rc = grow_dev(c, &c->x_tmp, &c->x_tmp_bytes, std::max<int64_t>(W * nmax * per, 8))))
+    return rc;
+  if (n[c->x_rank]) HIPCHK(c, hipMemcpyAsync(c->x_flat, d_src, (size_t)(n[c->x_rank] * per), hipMemcpyDeviceToDevice, c->stream));
+  if ((rc = x_allgather(c, c->x_flat, c->x_tmp, nmax * per))) return rc;
+  for (int64_t r = 0; r < W; r++)
+    if (n[r])
+      HIPCHK(c, hipMemcpyAsync((uint8_t*)d_dst + base[r] * per, c->x_tmp + r * nmax * per, (size_t)(n[r] * per),
+                               hipMemcpyDeviceToDevice, c->stream));
+  return 0;
+}
+
+// The middle-regime switch of the row-sharded loop: stop sharding.  Below mid_thresh
+// occurrences a merge is a fixed chain of dependent round trips whatever a rank holds, so
+// the per-merge exchange (all-gather + import) is pure overhead there (N > 1
+// slower than N = 1 in that regime).  Every rank gathers every rank's token records (and
+// the junction symbols and row offsets) once, re-keys the foreign blocks' pairs in its own
+// key table (k_collapse_fix) and continues as the one-rank loop over the whole corpus --
+// every rank making the same merges with no exchange, its own rows a window of the whole.
+// The counts need no change: they were global (replicated) already.  Called at a poll of
+// geobpe_run_exchange, after geobpe_pipeline_end (nothing in flight, nothing stalled).
+int x_collapse(geobpe_ctx* c) {
+  const int64_t W = c->x_world, me = c->x_rank;
+  int rc;
+  if ((rc = sync_state(c))) return rc;  // (flushes the last merge's place)
+  const int64_t mine[3] = {c->R, c->nrows, c->Lmax};
+  std::vector<uint8_t> raw;
+  if ((rc = x_allgather_host(c, mine, sizeof mine, raw))) return rc;
+  const int64_t* all = reinterpret_cast<const int64_t*>(raw.data());
+  std::vector<int64_t> nR(W), nN(W), bR(W + 1, 0), bN(W + 1, 0);
+  int64_t Lmax = 1;
+  for (int64_t r = 0; r < W; r++) {
+    nR[r] = all[3 * r];
+    nN[r] = all[3 * r + 1];
+    Lmax = std::max(Lmax, all[3 * r + 2]);
+    bR[r + 1] = bR[r] + nR[r];
+    bN[r + 1] = bN[r] + nN[r];
+  }
+  if (nR[me] != c->R || nN[me] != c->nrows) return fail(c, GEOBPE_EARG, "collapse: rank sizes disagree");
+  const int64_t Rt = bR[W], Nt = bN[W];
+  if (Rt >= INT32_MAX / 4) return fail(c, GEOBPE_EARG, "collapse: too many residues for int32 indexing");
+  Dev& D = c->D;
+  int4* tok2 = nullptr;
+  int32_t* gsym2 = nullptr;
+  uint16_t* gs16_2 = nullptr;
+  int64_t* row2 = nullptr;
+  if ((rc = dalloc(c, &tok2, Rt + 8, 0xFF)) || (rc = dalloc(c, &gsym2, Rt + 8, 0)) || (rc = dalloc(c, &row2, Nt + 1)) ||
+      (D.gs16 && (rc = dalloc(c, &gs16_2, Rt + 8, 0xFF))))
+    return rc;
+  if ((rc = x_gather_blocks(c, D.tok, tok2, nR, bR, sizeof(int4))) ||
+      (rc = x_gather_blocks(c, D.gsym, gsym2, nR, bR, sizeof(int32_t))) ||
+      (D.gs16 && (rc = x_gather_blocks(c, D.gs16, gs16_2, nR, bR, sizeof(uint16_t)))))
+    return rc;
+  // row offsets: every rank's (local, then moved to its residue base), the total at the end
+  std::vector<int64_t> rows_full(Nt + 1);
+  {
+    const int64_t nmax = *std::max_element(nN.begin(), nN.end());
+    std::vector<int64_t> send(std::max<int64_t>(nmax, 1), 0);
+    std::copy(c->row_off.begin(), c->row_off.begin() + c->nrows, send.begin());
+    if ((rc = x_allgather_host(c, send.data(), (int64_t)send.size() * 8, raw))) return rc;
+    const int64_t* ro = reinterpret_cast<const int64_t*>(raw.data());
+    for (int64_t r = 0; r < W; r++)
+      for (int64_t i = 0; i < nN[r]; i++) rows_full[bN[r] + i] = bR[r] + ro[r * (int64_t)send.size() + i];
+    rows_full[Nt] = Rt;
+  }
+  HIPCHK(c, hipMemcpyAsync(row2, rows_full.data(), (Nt + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  // the longest chain anywhere bounds the token lengths the content hashes combine
+  if (Lmax > c->Lmax) {
+    const int64_t pwn = 2 * Lmax + 8;
+    std::vector<u64> p1(pwn), p2(pwn);
+    p1[0] = p2[0] = 1;
+    for (int64_t i = 1; i < pwn; i++) {
+      p1[i] = mulmod61(p1[i - 1], HP1);
+      p2[i] = mulmod61(p2[i - 1], HP2);
+    }
+    u64 *dp1, *dp2;
+    if ((rc = dalloc(c, &dp1, pwn)) || (rc = dalloc(c, &dp2, pwn))) return rc;
+    HIPCHK(c, hipMemcpyAsync(dp1, p1.data(), pwn * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dp2, p2.data(), pwn * 8, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));  // (the host vectors go out of scope)
+    D.pw1 = dp1;
+    D.pw2 = dp2;
+    D.pwn = pwn;
+    c->Lmax = Lmax;
+  }
+  // the whole corpus from here on
+  dfree(c, &D.tok);
+  dfree(c, &D.gsym);
+  if (D.gs16) dfree(c, &D.gs16);
+  dfree(c, &c->d_row_off);
+  D.tok = tok2;
+  D.gsym = gsym2;
+  D.gs16 = gs16_2;
+  c->d_row_off = row2;
+  D.row_off = row2;
+  c->row_off = rows_full;
+  c->own_row0 = bN[me];
+  c->own_row1 = bN[me + 1];
+  c->R = Rt;
+  D.R = Rt;
+  c->nrows = Nt;
+  D.nrows = Nt;
+  int64_t* d_base;
+  if ((rc = dalloc(c, &d_base, W + 1))) return rc;
+  HIPCHK(c, hipMemcpyAsync(d_base, bR.data(), (W + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  hipLaunchKernelGGL(k_collapse_fix, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (const int64_t*)d_base, (int)W,
+                     (int)me);
+  HIPCHK(c, hipGetLastError());
+  if ((rc = sync_state(c))) return rc;
+  dfree(c, &d_base);
+  // the per-key lists and the middle regime's buffers are sized by the residues: made again
+  if (c->tail_ready) {
+    dfree(c, &D.kpool);
+    dfree(c, &D.TM);
+    dfree(c, &D.TH);
+    dfree(c, &D.TS);
+    dfree(c, &D.TR);
+    dfree(c, &D.TK);
+    c->tail_ready = false;
+  }
+  c->h_state->kp_valid = 0;
+  HIPCHK(c, hipMemsetAsync(&D.st->kp_valid, 0, 4, c->stream));
+  c->distributed = false;
+  c->collapsed = true;
+  c->mid_on = true;
+  return 0;
+}
+
 }  // namespace
 
 // the pipelined N > 1 loop with the engine's own exchange (TorchGroup.run_pipelined in C++):
@@ -2061,6 +2250,7 @@ int x_resolve(geobpe_ctx* c) {
 // the same polls, so every rank issues the same collectives.
 int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
   if (!c || n_merges < 0) return GEOBPE_EARG;
+  if (c->collapsed) return geobpe_run(c, n_merges, n_done);  // (every rank holds the whole corpus)
   if (!c->distributed || !c->keys_ready) return fail(c, GEOBPE_EARG, "run_exchange needs a distributed, binned engine");
   if (!c->x_kind) return fail(c, GEOBPE_EARG, "no exchange set up (geobpe_comm_init_rccl / geobpe_comm_set_callback)");
   HIPCHK(c, hipSetDevice(c->device));
@@ -2091,6 +2281,14 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
     if (!c->mid_on && mid_enabled(c) && c->h_state->iter > 0) {
       LogRec lr;
       HIPCHK(c, hipMemcpy(&lr, c->D.log + (c->h_state->iter - 1), sizeof lr, hipMemcpyDeviceToHost));
+      if (lr.count <= c->mid_thresh && c->collapse_on && !c->ev) {
+        // stop sharding: every rank takes the whole corpus and goes on alone (x_collapse)
+        if ((rc = geobpe_pipeline_end(c)) || (rc = x_collapse(c))) return rc;
+        int64_t more = 0;
+        rc = geobpe_run(c, n_merges - done, &more);
+        if (n_done) *n_done = done + more;
+        return rc;
+      }
       if (lr.count <= c->mid_thresh) {
         c->mid_on = true;
         // the middle regime's records are per (workgroup, key), not per owner and key: a

@@ -1185,6 +1185,55 @@ __global__ __launch_bounds__(ABLOCK) void k_import_fixed(Dev D, const uint8_t* i
   if (threadIdx.x == 0) D.chkcnt[blockIdx.x] = min(s_chk, (int32_t)D.RC);
 }
 
+// collapse of the row-sharded loop at the middle-regime switch (geobpe_run_exchange): every
+// rank now holds every rank's token records, each block at its rank's residue base (rbase,
+// W + 1 entries).  Links (tprev) move to global slots; a foreign block's pair keys are looked
+// up again by content, in this rank's key table -- key ids are rank-local, and every rank
+// holds every key (the exchange claimed each one on every rank, with its global count).
+// A pair whose content is absent, or whose hashes differ from the key's, is an error.
+__global__ __launch_bounds__(BLOCK) void k_collapse_fix(Dev D, const int64_t* rbase, int W, int own) {
+  const u64 mask = (u64)D.HC - 1;
+  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
+    int r = 0;
+    while (r + 1 < W && g >= rbase[r + 1]) r++;
+    int4 t = D.tok[g];
+    if (t.x < 0) continue;  // (not a token start)
+    bool ch = false;
+    if (t.z >= 0 && rbase[r]) {
+      t.z += (int32_t)rbase[r];
+      ch = true;
+    }
+    if (r != own && t.w >= 0) {
+      const int32_t xlen = tok_len(t.y);
+      const int64_t e = g + xlen - 1;
+      const int4 te = D.tok[e + 1];  // (its x / y are never rewritten here)
+      const int32_t gl = next_glue(D, t.y, e), ylen = tok_len(te.y);
+      u64 h1, h2;
+      combine(D, D.vh1[t.x], D.vh2[t.x], gl, D.vh1[te.x], D.vh2[te.x], ylen, h1, h2);
+      const int32_t len = xlen + ylen;
+      const u64 k = probe_key(h1, h2, len);
+      u64 s = ht_first_slot(D, k);
+      int32_t d = -1;
+      for (int64_t probe = 0; probe < D.HC; probe++) {
+        const u64 cur = D.ht_key[s];
+        if (cur == k) {
+          d = (int32_t)s;
+          break;
+        }
+        if (cur == 0) break;
+        s = (s + 1) & mask;
+      }
+      if (d < 0 || D.kh1[d] != h1 || D.kh2[d] != h2 || D.klen[d] != len) {
+        set_error(D, d < 0 ? GEOBPE_ESTATE : GEOBPE_EHASH, g);
+        d = -1;
+      }
+      t.w = d;
+      ch = true;
+    }
+    if (ch) D.tok[g] = t;
+  }
+}
+
 // ====================================================================== exports / checks
 __global__ __launch_bounds__(BLOCK) void k_row_ntok(Dev D, int64_t* ntok) {
   for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < D.nrows; r += (int64_t)gridDim.x * blockDim.x) {

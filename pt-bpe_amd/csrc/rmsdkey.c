@@ -483,6 +483,32 @@ typedef struct {
   PyObject *chains, *gd, *pk, *edges, *edges_fn, *names, *diff;
 } MSt;
 
+/* RMSDKEY_PROF=1 (a profiling build): nanoseconds per section of merge(), read by prof() */
+#ifndef RMSDKEY_PROF
+#define RMSDKEY_PROF 0
+#endif
+#if RMSDKEY_PROF
+#include <time.h>
+static double g_prof[8];
+static long g_prof_n[8];
+static double now_ns(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e9 + ts.tv_nsec;
+}
+#define PROF_T(v) double v = now_ns()
+#define PROF_ADD(i, t0)           \
+  do {                            \
+    double t1_ = now_ns();        \
+    g_prof[i] += t1_ - (t0);      \
+    g_prof_n[i]++;                \
+    t0 = t1_;                     \
+  } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(i, t0)
+#endif
+
 static int key_error(PyObject* k) {
   PyObject* a = PyTuple_Pack(1, k);
   if (a) {
@@ -672,6 +698,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       nres = PyLong_AsSsize_t(nres_o);
       cur_ci = ci;
     }
+    PROF_T(pt0);
     const Py_ssize_t i1 = list_int(tp, i2 - 1);
     if (i1 < 0 && PyErr_Occurred()) goto fail;
     const Py_ssize_t l1 = i2 - i1, l2 = length - l1;
@@ -726,6 +753,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
     }
     if (left && (set_in(&m, left, t01, 0) < 0 || note(&m, left, -1) < 0)) goto fail;
     if (right && (set_in(&m, right, t23, 0) < 0 || note(&m, right, -1) < 0)) goto fail;
+    PROF_ADD(0, pt0);
     {
       PyObject* vi1 = PyLong_FromSsize_t(i1);
       if (!vi1) goto fail;
@@ -763,6 +791,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       Py_DECREF(vi1);
       if (rc < 0) goto fail;
     }
+    PROF_ADD(1, pt0);
     if (rmsd) {
       PyObject* a = PyList_GET_ITEM(assigns, q);
       PyObject* struc = PyObject_GetItem(vals, a);
@@ -771,21 +800,27 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       Py_DECREF(struc);
       if (rc < 0) goto fail;
     }
+    PROF_ADD(2, pt0);
     if (left) {
       PyObject* k = mpair_key(&m, cols, init, tp, btt, nres, i0, l0, length);
+      PROF_ADD(3, pt0);
       if (!k) goto fail;
       const int rc = (set_in(&m, k, t01, 1) < 0 || PyDict_SetItem(m.pk, t01, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
       Py_DECREF(k);
+      PROF_ADD(4, pt0);
       if (rc < 0) goto fail;
     }
     if (right) {
       PyObject* k = mpair_key(&m, cols, init, tp, btt, nres, i1, length, l3);
+      PROF_ADD(3, pt0);
       if (!k) goto fail;
       const int rc = (set_in(&m, k, t23, 1) < 0 || PyDict_SetItem(m.pk, t23, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
       Py_DECREF(k);
+      PROF_ADD(4, pt0);
       if (rc < 0) goto fail;
     }
     if (!rmsd && apply_geo(chain, cols, init, i1, length, vals) < 0) goto fail;
+    PROF_ADD(5, pt0);
     last_ci = ci;
     last_i1 = i1;
     have_last = 1;
@@ -945,7 +980,21 @@ fail:
   return NULL;
 }
 
-static PyMethodDef METHODS[] = {{"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
+#if RMSDKEY_PROF
+static PyObject* prof(PyObject* self, PyObject* args) {
+  (void)self;
+  (void)args;
+  PyObject* l = PyList_New(8);
+  for (int i = 0; i < 8; i++) PyList_SET_ITEM(l, i, Py_BuildValue("(dl)", g_prof[i], g_prof_n[i]));
+  return l;
+}
+#endif
+
+static PyMethodDef METHODS[] = {
+#if RMSDKEY_PROF
+                                {"prof", prof, METH_NOARGS, "merge() section times (ns, count)"},
+#endif
+                                {"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
                                 {"pack", pack, METH_VARARGS, "whole-residue span geometry, geobpe_nerf layout"},
                                 {"reprs", reprs, METH_VARARGS, "repr(float) of each value (test)"},
                                 {"setgeo", setgeo, METH_VARARGS, "set_token_geo into the chain's column lists"},

@@ -126,6 +126,8 @@ def lib():
         "geobpe_rmsd": (ctypes.c_int, [ctypes.c_int, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, P, P,
                                        ctypes.c_int, P]),
         "geobpe_arena_release": (ctypes.c_int, [ctypes.c_int]),
+        "geobpe_set_collapse": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_collapsed": (ctypes.c_int, [P]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -149,6 +151,7 @@ EXPORTED_SYMBOLS = [
     "geobpe_comm_unique_id", "geobpe_comm_init_rccl", "geobpe_comm_error", "geobpe_comm_set_callback",
     "geobpe_comm_set_slot", "geobpe_run_exchange", "geobpe_pdb_backbone", "geobpe_pdb_error",
     "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf", "geobpe_glue_opt", "geobpe_arena_release",
+    "geobpe_set_collapse", "geobpe_collapsed",
 ]
 
 

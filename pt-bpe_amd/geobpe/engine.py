@@ -83,13 +83,14 @@ class GeoBPEEngine:
     def __init__(self, corpus: dict, bins: int, device: int = 0, max_vocab: int = 1 << 20,
                  group=None, stream=None, use_torch_stream: bool = True, cover: bool = False,
                  bin_dense: bool = True, strategy: Optional[str] = None, tail: Optional[int] = None,
-                 mid: Optional[int] = None):
+                 mid: Optional[int] = None, collapse: bool = True):
         """``corpus``: ``{column: float64[R]}`` + ``row_off`` (geobpe.synth layout) for
         THIS shard.  ``group``: an exchange group (geobpe.dist) for multi-rank runs.
         ``tail``: merges of at most this count run in the one-workgroup late-merge
         kernel (include/geobpe.h geobpe_set_tail; None = the library default, 0 = never);
         ``mid``: merges of at most this count run in the two-launch middle-regime kernels
-        (geobpe_set_mid)."""
+        (geobpe_set_mid); ``collapse``: multi-rank runs stop sharding at that switch, every
+        rank going on with the whole corpus (geobpe_set_collapse)."""
         self.L = _native.lib()
         self.B = int(bins)
         self.device = int(device)
@@ -124,6 +125,8 @@ class GeoBPEEngine:
             self._chk(self.L.geobpe_set_tail(self._ctx, int(tail)))
         if mid is not None:
             self._chk(self.L.geobpe_set_mid(self._ctx, int(mid)))
+        self._chk(self.L.geobpe_set_collapse(self._ctx, 1 if collapse else 0))
+        self._collapsed = False
         self.K0 = 0
         self.merges = []  # [(new_id, count, n_merged)]
         self.thresholds = None
@@ -138,7 +141,14 @@ class GeoBPEEngine:
 
     @property
     def distributed(self) -> bool:
-        return self.group is not None and (self.group.world_size > 1 or getattr(self.group, "force", False))
+        """Row-sharded with an exchange per merge (until a collapse: then every rank holds the
+        whole corpus and runs the one-rank loop)."""
+        return (self.group is not None and (self.group.world_size > 1 or getattr(self.group, "force", False))
+                and not self._collapsed)
+
+    @property
+    def collapsed(self) -> bool:
+        return self._collapsed
 
     def close(self):
         if self._ctx:
@@ -300,6 +310,7 @@ class GeoBPEEngine:
         if self.distributed:
             if self.pipelined and hasattr(self.group, "run_pipelined"):
                 done = self.group.run_pipelined(self, int(n_merges))
+                self._collapsed = bool(self.L.geobpe_collapsed(self._ctx))
                 self._refresh_log()
                 if done < n_merges:
                     self._done = True

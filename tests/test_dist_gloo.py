@@ -91,7 +91,10 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
         corpus = synth.make_corpus(synth.make_lengths(2000, 20, 300, seed=91), seed=91, repeat_frac=0.05)
         lo, hi = shard_rows(corpus["row_off"], world)[rank]
         mid = None
-        if mode == "skewed":
+        # the sharded exchange to the end, or (modes "collapse*", "skewed", "mixed-collapse") the
+        # collapse at the middle-regime switch: every rank goes on with the whole corpus
+        collapse = mode.startswith("collapse") or mode in ("skewed", "mixed-collapse")
+        if mode.startswith("skewed"):
             # rank 0 holds 5 % of the rows: its own merged counts sit far below the others', so
             # a switch to the middle regime decided per rank would part the ranks' collectives
             # (ADVICE r3); the switch must follow the replicated winner count (mid = 1500 puts
@@ -105,19 +108,23 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
             g.pipe_cap = 16
         if mode == "host-loop":  # the Python-driven loop (geobpe.dist) instead of geobpe_run_exchange
             g.engine_exchange = False
-        e = GeoBPEEngine(shard, 5, device=0, group=g, mid=mid).initialize()
+        e = GeoBPEEngine(shard, 5, device=0, group=g, mid=mid, collapse=collapse).initialize()
         e.pipelined = mode != "stepwise"
         e.bin()
         done = e.run(70)
-        if mode == "mixed":  # pipelined -> host-synchronised step() -> pipelined: the parity hand-offs
+        if mode.startswith("mixed"):  # pipelined -> host-synchronised step() -> pipelined: the parity hand-offs
             for _ in range(20):
                 done += e.step(want_merged=False) is not None
             done += e.run(60)
         else:
             done += e.run(80)  # a second pipelined run continues the device parity
         s, ids, off = e.segmentation()
-        if mode == "skewed":
+        if mode.startswith("skewed"):
             assert e.merges[0][1] > mid >= e.merges[-1][1], "the run does not cross the middle-regime threshold"
+        assert e.collapsed == collapse, "collapse expected" if collapse else "no collapse expected"
+        if collapse:  # the whole corpus on every rank: its counts are the global ones
+            assert e.verify_counts() == 0, "counts after the collapse differ from a full recount"
+            assert len(off) == hi - lo + 1 and e.encode()[1].shape == off.shape  # (this rank's rows only)
         q.put((rank, done, e.merge_keys(), ids.tolist()))
     except Exception as ex:  # pragma: no cover
         q.put((rank, -1, repr(ex), None))
@@ -127,14 +134,18 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise"),
-                                         (3, "mixed"), (4, "small-slots"), (2, "host-loop"), (2, "skewed"),
-                                         (3, "skewed")])
+                                         (3, "mixed"), (4, "small-slots"), (2, "host-loop"),
+                                         (2, "skewed-nocollapse"), (3, "skewed-nocollapse"), (2, "skewed"),
+                                         (3, "skewed"), (2, "collapse"), (4, "collapse"), (2, "mixed-collapse")])
 def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
     """The full N>1 path (TorchGroup exchange, one process per rank) with gloo on
     one device: the engine's pipelined loop (geobpe_run_exchange over the group's host
     collective: fixed slots, stall + full re-exchange of an overflowing merge), the same
     with tiny slots, the Python-driven loop, and the host-synchronised per-merge
-    exchange; merge list and segmentation equal the oracle's."""
+    exchange; skewed shards whose own merged counts cross the middle-regime threshold far
+    apart (the switch follows the replicated count); the collapse at that switch (every
+    rank gathers the whole corpus and goes on alone) early, mid-run and before host steps.
+    Merge list and segmentation equal the oracle's."""
     import multiprocessing as mp
     from geobpe import synth
     ctx = mp.get_context("spawn")

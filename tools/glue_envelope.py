@@ -1,0 +1,220 @@
+"""The reference glue optimiser's own sensitivity envelope: how far its
+result moves under input perturbations far below anything physical, so that the device
+optimiser's tolerance is stated in the reference's own terms instead of the device's tails.
+
+The reference optimiser is oracle/glue.py (a torch restatement that reproduces the
+reference's LBFGS optimum bit for bit on the fixtures: tests/test_glue.py::
+test_oracle_matches_reference_optimum).  Each variant runs the fixture's whole reference
+sequence on the host -- RmsdBPE with the oracle's numpy NeRF / Kabsch and this optimiser in
+place of the device batches, exactly tests/test_glue.py's host path -- with ONE change to the
+optimiser's inputs:
+
+  ref        none (must reproduce the fixture exactly: the control)
+  x0_up/dn   every start value x0 moved 1 float32 ulp up / down
+  tgt_up     every target frame value (R, t; float32 in the optimiser) 1 ulp up
+  geo_up     every fixed geometry value of the chain (float32 in the optimiser) 1 ulp up
+  threads    torch.set_num_threads(8) instead of 1 (summation order of torch's kernels)
+
+Recorded per (fixture, variant): after glue_opt_all, the glued geometry against the
+fixture's (the reference's): glues in another bin, their distance (rad), how many further
+than 0.02 / 0.1 rad, per glue type; then the merges popped by bin() + step() and how many
+leading merges equal the fixture's.  And for the 120-chain drift set (tools/glue_drift.py,
+prior off) the raw optimum's drift quantiles and same-bin share against the unperturbed
+optimum.
+
+  python tools/glue_envelope.py [--jobs N] [--no-steps] OUT.json [fixture ...]
+
+CPU only, run in the build container (torch on the CPU); the output is committed as
+tests/golden/glue_envelope.json and tests/test_glue.py derives its device bounds from it.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "pt-bpe_amd"))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+
+FIXTURES = ["gl_all_p0", "gl_all_p0_prior", "gl_pdb72_readme", "gl_syn120_pareto"]
+VARIANTS = ["ref", "x0_up", "x0_dn", "tgt_up", "geo_up", "threads"]
+GLUE_COLS = ["omega", "C:1N:1CA", "phi"]
+COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
+
+
+def _up(a):
+    a = np.asarray(a, dtype=np.float32)
+    return np.nextafter(a, np.float32(np.inf)).astype(np.float32)
+
+
+def _dn(a):
+    a = np.asarray(a, dtype=np.float32)
+    return np.nextafter(a, np.float32(-np.inf)).astype(np.float32)
+
+
+def perturbed_optimize(variant):
+    """oracle.glue.optimize with the variant's input change."""
+    from oracle import glue as og
+
+    def opt(g, x0, R, t, prior=None, lam=0.0):
+        if variant == "x0_up":
+            x0 = _up(x0)
+        elif variant == "x0_dn":
+            x0 = _dn(x0)
+        elif variant == "tgt_up":
+            R, t = _up(R), _up(t)
+        elif variant == "geo_up":
+            g = _up(np.asarray(g, dtype=np.float32)).astype(np.float64)
+        return og.optimize(g, x0, R, t, prior, lam)
+    return opt
+
+
+def install_host(variant):
+    """tests/test_glue.py's host_glue fixture without pytest: the oracle's NeRF / Kabsch /
+    thresholds and the (perturbed) optimiser in place of the device batches."""
+    import oracle.prologue as prologue
+    import oracle.rmsd as orm
+    from geobpe import glue, rmsd, rmsd_bpe
+    rmsd.geo_coords = lambda geos, device=0: [orm.nerf(g) for g in geos]
+    rmsd.nerf_packed = lambda off, packed, device=0: orm.nerf_packed(off, packed)
+    rmsd.nerf_atoms = lambda off, packed, device=0: orm.nerf_atoms(off, packed)
+    rmsd.rmsd_matrix = lambda S, device=0: orm.rmsd_matrix(S)
+    rmsd.rmsd_cross = lambda A, B, device=0: np.array([[orm.rmsd(a, b) for b in B] for a in A])
+    rmsd_bpe.RmsdBPE._grid_thresholds = lambda self: {s: prologue.thresholds(self._corpus, b) for s, b in self.bins.items()}
+    opt1 = perturbed_optimize(variant)
+
+    def opt_chains(geos, x0s, targets, grids, prior, lam, device=0, w_rot=1.0, w_trans=0.1):
+        table, counts = prior
+        outs = []
+        for g, x0, (R, t), gi in zip(geos, x0s, targets, grids):
+            pr = [(table[gi, k, 0, :counts[gi, k]], table[gi, k, 1, :counts[gi, k]]) for k in range(3)]
+            outs.append(opt1(g, x0, R, t, pr, lam)[0])
+        return outs, None, None
+    glue.optimize_chains = opt_chains
+
+
+def glued_stats(a, b, thr):
+    """a (this run) vs b (the fixture) for one glue column: tests/test_glue.py::_glue_close's
+    numbers without its asserts."""
+    bad = ~((a == b) | (np.isnan(a) & np.isnan(b)))
+    n = int(np.sum(~np.isnan(b)))
+    e = np.asarray(thr, dtype=np.float64)
+    width = float(np.max(e[:, 1] - e[:, 0]))
+    d = np.abs(a[bad] - b[bad])
+    d = np.minimum(d, 2 * np.pi - d)
+    return {"glues": n, "other_bin": int(bad.sum()), "bin_width": width,
+            "max_rad": float(d.max()) if d.size else 0.0,
+            "past_0.02": int(np.sum(d > 0.02)), "past_0.1": int(np.sum(d > 0.1))}
+
+
+def run_fixture(name, variant, steps=True):
+    import torch
+    torch.set_num_threads(8 if variant == "threads" else 1)
+    install_host(variant)
+    from test_glue import _load
+    from geobpe.bpe import BPE
+    meta, arrs = _load(name)
+    corpus = {k: arrs[k] for k in COLS + ["row_off"]}
+    t0 = time.time()
+    bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()},
+              rmsd_partition_min_size=meta["rmsd_partition_min_size"], rmsd_super_res=meta["rmsd_super_res"],
+              num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta["std_bonds"],
+              glue_opt=True, glue_opt_prior=meta["glue_opt_prior"], glue_opt_every=meta["glue_opt_every"],
+              glue_opt_method=meta["glue_opt_method"], seed=meta["rng_seed"])
+    popped = []
+    inner = bpe._merge
+
+    def recording():
+        popped.append(list(bpe._priority[0]))
+        return inner()
+    bpe._merge = recording
+    bpe.initialize()
+    bpe.glue_opt_all()
+    g = bpe.geometry()
+    out = {"fixture": name, "variant": variant,
+           "glued": {c: glued_stats(g[c], arrs[f"glued_{c}"], bpe._thresholds[1][c]) for c in GLUE_COLS}}
+    if steps:
+        want = [p for call in meta["calls"] for p in call["popped"]]
+        bpe.bin()
+        for _ in meta["calls"]:
+            bpe.step()
+        same = next((i for i, (a, b) in enumerate(zip(popped, want)) if a != b), min(len(popped), len(want)))
+        out["merges"] = {"total": len(want), "shared_prefix": same}
+    out["seconds"] = round(time.time() - t0, 1)
+    return out
+
+
+def drift_variant(variant, n=120):
+    """The drift set of tools/glue_drift.py: the variant's raw optimum against the unperturbed
+    one (both the reference optimiser)."""
+    import torch
+    torch.set_num_threads(8 if variant == "threads" else 1)
+    import glue_drift
+    from geobpe import glue
+    geos, x0s, R, T, thr = glue_drift.problems(n)
+    z = np.load(os.path.join(REPO, "tests", "golden", "glue_drift_oracle.npz"))
+    opt = perturbed_optimize(variant)
+    outs, loss = [], []
+    for g, x0, r, t in zip(geos, x0s, R, T):
+        o = opt(g, x0, r, t)
+        outs.append(o[0])
+        loss.append(o[4])
+    dev = np.concatenate(outs).astype(np.float64)
+    ref = z["opt"].astype(np.float64)
+    d = np.abs(dev - ref)
+    d = np.minimum(d, 2 * np.pi - d).ravel()
+    same = np.array([[glue.snap_bin(thr[t], a[t]) == glue.snap_bin(thr[t], b[t]) for t in range(3)]
+                     for a, b in zip(dev, ref)])
+    lr = np.array(loss) / z["loss"]
+    return {"fixture": "drift120", "variant": variant, "glues": int(len(dev)),
+            "drift_rad": {q: float(np.quantile(d, p)) for q, p in (("p50", .5), ("p90", .9), ("p99", .99), ("max", 1.0))},
+            "exact": float(np.mean(d == 0)), "same_bin": float(same.mean()),
+            "loss_ratio": {"min": float(lr.min()), "max": float(lr.max())}}
+
+
+def _job(args):
+    kind, name, variant, steps = args
+    try:
+        if kind == "drift":
+            return drift_variant(variant)
+        return run_fixture(name, variant, steps)
+    except Exception as e:  # the reference's own failures are data too
+        return {"fixture": name, "variant": variant, "raised": f"{type(e).__name__}: {e}"}
+
+
+def main(argv):
+    import multiprocessing as mp
+    jobs, steps = 6, True
+    while argv and argv[0].startswith("--"):
+        if argv[0] == "--jobs":
+            jobs = int(argv[1])
+            argv = argv[2:]
+        elif argv[0] == "--no-steps":
+            steps = False
+            argv = argv[1:]
+    out_path, names = argv[0], (argv[1:] or FIXTURES + ["drift120"])
+    work = []
+    for name in names:
+        for v in VARIANTS:
+            work.append(("drift", name, v, steps) if name == "drift120" else ("fixture", name, v, steps))
+    # the longest first (the pareto fixture's runs)
+    work.sort(key=lambda w: 0 if "pareto" in w[1] else (1 if "readme" in w[1] else 2))
+    res = []
+    with mp.get_context("spawn").Pool(jobs) as pool:
+        for r in pool.imap_unordered(_job, work):
+            res.append(r)
+            print(json.dumps(r), flush=True)
+    res.sort(key=lambda r: (r["fixture"], VARIANTS.index(r["variant"])))
+    with open(out_path, "w") as f:
+        json.dump({"generator": "tools/glue_envelope.py", "variants": VARIANTS, "results": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:])
