@@ -38,6 +38,12 @@
 #include "rmsd.h"
 #include "glue.h"
 
+namespace gb {
+// kp_sort.hip (its own translation unit): stable radix sort of (key, value) int32 pairs
+hipError_t kp_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* keys_in, int32_t* keys_out,
+                         const int32_t* vals_in, int32_t* vals_out, int64_t n, int end_bit, hipStream_t s);
+}  // namespace gb
+
 using namespace gb;
 
 // RCCL entry points, resolved with dlsym from the RCCL library the process already uses
@@ -116,6 +122,10 @@ struct geobpe_ctx {
   // collapse at the middle-regime switch (geobpe_set_collapse): every rank then holds the whole
   // corpus and runs the one-rank loop; its own rows are [own_row0, own_row1) of it
   bool collapse_on = true, collapsed = false;
+  // per-key list build (tail_build): radix-sort scratch; kp_atomic: the atomic counting build (A/B)
+  void* kps = nullptr;
+  int64_t kps_bytes = 0;
+  bool kp_atomic = false;
   int64_t own_row0 = 0, own_row1 = -1;
   // profiling
   bool prof = false;
@@ -429,10 +439,49 @@ int tail_alloc(geobpe_ctx* c) {
   return 0;
 }
 
-// per-key posting lists of the live pairs (a counting sort by key), after any pending place
+// per-key posting lists of the live pairs, after any pending place: a stable radix sort of
+// the (key, slot) pairs (kp_sort.hip) -> runs -> list space -> placement; GEOBPE_KP_ATOMIC=1
+// (A/B) or a failed scratch allocation: the counting build with a global atomic per pair
+int tail_build_sorted(geobpe_ctx* c) {
+  Dev& D = c->D;
+  const int64_t n = c->R;
+  if (n <= 0 || n >= INT32_MAX) return 1;
+  int end_bit = 1;
+  while (end_bit < 31 && (1LL << end_bit) <= D.HC) end_bit++;
+  const int32_t none = (int32_t)((1LL << end_bit) - 1);  // (> every key id: sorts last)
+  size_t tb = 0;
+  if (kp_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, c->stream) != hipSuccess) return 1;
+  const int64_t need = 4 * n * 4 + (int64_t)tb + 1024;
+  if (c->kps_bytes < need) {
+    if (c->kps) {
+      hipStreamSynchronize(c->stream);
+      hipFree(c->kps);
+      c->kps = nullptr;
+      c->kps_bytes = 0;
+    }
+    if (hipMalloc(&c->kps, (size_t)need) != hipSuccess) return 1;
+    c->kps_bytes = need;
+  }
+  int32_t* kin = reinterpret_cast<int32_t*>(c->kps);
+  int32_t* vin = kin + n;
+  int32_t* kout = vin + n;
+  int32_t* vout = kout + n;
+  void* temp = reinterpret_cast<char*>(vout + n) + 256 - (reinterpret_cast<uintptr_t>(vout + n) & 255);
+  hipLaunchKernelGGL(k_kp_reset, dim3(c->nb), dim3(BLOCK), 0, c->stream, D);
+  hipLaunchKernelGGL(k_kp_keys, dim3(c->nb), dim3(BLOCK), 0, c->stream, D, kin, vin, none);
+  if (kp_sort_pairs(temp, &tb, kin, kout, vin, vout, n, end_bit, c->stream) != hipSuccess) return 1;
+  hipLaunchKernelGGL(k_kp_runs, dim3(c->nb), dim3(BLOCK), 0, c->stream, D, (const int32_t*)kout, none);
+  hipLaunchKernelGGL(k_kp_alloc_runs, dim3(c->nb), dim3(BLOCK), 0, c->stream, D);
+  hipLaunchKernelGGL(k_kp_fill_runs, dim3(c->nb), dim3(BLOCK), 0, c->stream, D, (const int32_t*)kout,
+                     (const int32_t*)vout, none);
+  hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, D);  // (nothing pending)
+  return 0;
+}
+
 void tail_build(geobpe_ctx* c) {
   flush_place(c);
   Timed t(c, "tail_build");
+  if (!c->kp_atomic && tail_build_sorted(c) == 0) return;
   if (c->distributed) {  // (a rank's counts are global: count its own live pairs)
     hipLaunchKernelGGL(k_kp_reset, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
     hipLaunchKernelGGL(k_kp_count, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
@@ -554,6 +603,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   }
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
+  if (const char* e = getenv("GEOBPE_KP_ATOMIC")) c->kp_atomic = atoi(e) == 1;  // (A/B: the atomic list build)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
@@ -575,6 +625,7 @@ void geobpe_destroy(geobpe_ctx* c) {
   if (c->comm && c->rccl.CommDestroy) c->rccl.CommDestroy(c->comm);
   for (uint8_t* p : {c->x_pbuf, c->x_gath, c->x_tmp, c->x_flat})
     if (p) hipFree(p);
+  if (c->kps) hipFree(c->kps);
   if (c->x_hsend) hipHostFree(c->x_hsend);
   if (c->x_hrecv) hipHostFree(c->x_hrecv);
   for (auto e : c->evall) hipEventDestroy(e);

@@ -32,6 +32,32 @@ static const double TWO_PI = 6.283185307179586; /* 2 * np.pi */
  * hashed a new str per call, ~10 per chain visited) */
 enum { A_CUR, A_ORIG, A_INIT, A_TOKEN_POS, A_BTT, A_EVENTS, A_N, A_COUNT };
 static const char* ATTR_NAMES[A_COUNT] = {"cur", "orig", "init", "token_pos", "btt", "events", "n"};
+/* RMSDKEY_PROF=1 (a profiling build): nanoseconds per section of merge(), read by prof() */
+#ifndef RMSDKEY_PROF
+#define RMSDKEY_PROF 0
+#endif
+#if RMSDKEY_PROF
+#include <time.h>
+static double g_prof[8];
+static long g_prof_n[8];
+static double now_ns(void) {
+  struct timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return ts.tv_sec * 1e9 + ts.tv_nsec;
+}
+#define PROF_T(v) double v = now_ns()
+#define PROF_ADD(i, t0)           \
+  do {                            \
+    double t1_ = now_ns();        \
+    g_prof[i] += t1_ - (t0);      \
+    g_prof_n[i]++;                \
+    t0 = t1_;                     \
+  } while (0)
+#else
+#define PROF_T(v)
+#define PROF_ADD(i, t0)
+#endif
+
 static PyObject* ATTR[A_COUNT];
 static PyObject* PACK_KEYS[9];
 
@@ -289,8 +315,10 @@ static PyObject* build_key(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ss
     if (buf_str(&b, "]") < 0) goto fail;
   }
   if (buf_str(&b, "}") < 0) goto fail;
+  PROF_T(uk0);
   PyObject* out = PyUnicode_New(b.n, 127);  /* (every character is ASCII) */
   if (out) memcpy(PyUnicode_DATA(out), b.p, b.n);
+  PROF_ADD(7, uk0);
   if (b.p != stack) PyMem_Free(b.p);
   return out;
 fail:
@@ -483,32 +511,6 @@ typedef struct {
   PyObject *chains, *gd, *pk, *edges, *edges_fn, *names, *diff;
 } MSt;
 
-/* RMSDKEY_PROF=1 (a profiling build): nanoseconds per section of merge(), read by prof() */
-#ifndef RMSDKEY_PROF
-#define RMSDKEY_PROF 0
-#endif
-#if RMSDKEY_PROF
-#include <time.h>
-static double g_prof[8];
-static long g_prof_n[8];
-static double now_ns(void) {
-  struct timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return ts.tv_sec * 1e9 + ts.tv_nsec;
-}
-#define PROF_T(v) double v = now_ns()
-#define PROF_ADD(i, t0)           \
-  do {                            \
-    double t1_ = now_ns();        \
-    g_prof[i] += t1_ - (t0);      \
-    g_prof_n[i]++;                \
-    t0 = t1_;                     \
-  } while (0)
-#else
-#define PROF_T(v)
-#define PROF_ADD(i, t0)
-#endif
-
 static int key_error(PyObject* k) {
   PyObject* a = PyTuple_Pack(1, k);
   if (a) {
@@ -615,7 +617,9 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
     PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: edges must be a 9-tuple");
     return NULL;
   }
+  PROF_T(pk0);
   PyObject* k = build_key(cols, init, i1, L, i1 % 3, lo, hi, thr);
+  PROF_ADD(6, pk0);
   Py_DECREF(thr);
   return k;
 }

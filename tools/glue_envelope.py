@@ -14,6 +14,10 @@ optimiser's inputs:
   tgt_up     every target frame value (R, t; float32 in the optimiser) 1 ulp up
   geo_up     every fixed geometry value of the chain (float32 in the optimiser) 1 ulp up
   threads    torch.set_num_threads(8) instead of 1 (summation order of torch's kernels)
+  grad_s<k>  at EVERY evaluation the gradient the closure returns moved 1 float32 ulp up or
+             down per element (random signs, seed k): another float32 gradient of the same
+             loss, as a different summation order or rounding point gives one -- the model of
+             an independent float32 implementation of the optimiser (such as the device's)
 
 Recorded per (fixture, variant): after glue_opt_all, the glued geometry against the
 fixture's (the reference's): glues in another bin, their distance (rad), how many further
@@ -22,7 +26,7 @@ leading merges equal the fixture's.  And for the 120-chain drift set (tools/glue
 prior off) the raw optimum's drift quantiles and same-bin share against the unperturbed
 optimum.
 
-  python tools/glue_envelope.py [--jobs N] [--no-steps] OUT.json [fixture ...]
+  python tools/glue_envelope.py [--jobs N] [--no-steps] [--variants a,b] OUT.json [fixture ...]
 
 CPU only, run in the build container (torch on the CPU); the output is committed as
 tests/golden/glue_envelope.json and tests/test_glue.py derives its device bounds from it.
@@ -43,7 +47,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 FIXTURES = ["gl_all_p0", "gl_all_p0_prior", "gl_pdb72_readme", "gl_syn120_pareto"]
-VARIANTS = ["ref", "x0_up", "x0_dn", "tgt_up", "geo_up", "threads"]
+VARIANTS = ["ref", "x0_up", "x0_dn", "tgt_up", "geo_up", "threads", "grad_s0", "grad_s1", "grad_s2"]
 GLUE_COLS = ["omega", "C:1N:1CA", "phi"]
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
@@ -58,11 +62,46 @@ def _dn(a):
     return np.nextafter(a, np.float32(-np.inf)).astype(np.float32)
 
 
+def optimize_grad_ulp(geo, x0, R_occs, t_occs, prior, lam, rng):
+    """oracle.glue.optimize with every gradient the closure hands LBFGS moved 1 float32 ulp
+    (random direction per element)."""
+    import torch
+    from oracle import glue as og
+    geo32 = torch.tensor(np.asarray(geo, dtype=np.float32))
+    R = [torch.tensor(np.asarray(x, dtype=np.float32)) for x in R_occs]
+    T = [torch.tensor(np.asarray(x, dtype=np.float32)) for x in t_occs]
+    pr = None
+    if prior is not None:
+        pr = [(torch.tensor(np.asarray(c, dtype=np.float32)), torch.tensor(np.asarray(w, dtype=np.float32)))
+              for c, w in prior]
+    raw = torch.nn.Parameter(torch.tensor(np.ascontiguousarray(x0, dtype=np.float32)))
+    opt = torch.optim.LBFGS([raw], max_iter=20, line_search_fn="strong_wolfe")
+    losses = []
+
+    def closure():
+        opt.zero_grad()
+        loss = og.chain_loss(geo32, raw, R, T, pr, lam)
+        loss.backward()
+        g = raw.grad.numpy()
+        up = rng.random(g.shape) < 0.5
+        g2 = np.where(up, np.nextafter(g, np.float32(np.inf)), np.nextafter(g, np.float32(-np.inf))).astype(np.float32)
+        raw.grad.copy_(torch.from_numpy(g2))
+        losses.append(loss.item())
+        return loss
+
+    opt.step(closure)
+    st = opt.state[raw]
+    return og.wrap(raw.detach()).numpy(), int(st["n_iter"]), int(st["func_evals"]), losses[0], losses[-1]
+
+
 def perturbed_optimize(variant):
     """oracle.glue.optimize with the variant's input change."""
     from oracle import glue as og
+    rng = np.random.default_rng(int(variant[6:]) if variant.startswith("grad_s") else 0)
 
     def opt(g, x0, R, t, prior=None, lam=0.0):
+        if variant.startswith("grad_s"):
+            return optimize_grad_ulp(g, x0, R, t, prior, lam, rng)
         if variant == "x0_up":
             x0 = _up(x0)
         elif variant == "x0_dn":
@@ -199,10 +238,14 @@ def main(argv):
         elif argv[0] == "--no-steps":
             steps = False
             argv = argv[1:]
+    variants = VARIANTS
+    if argv and argv[0] == "--variants":
+        variants = argv[1].split(",")
+        argv = argv[2:]
     out_path, names = argv[0], (argv[1:] or FIXTURES + ["drift120"])
     work = []
     for name in names:
-        for v in VARIANTS:
+        for v in variants:
             work.append(("drift", name, v, steps) if name == "drift120" else ("fixture", name, v, steps))
     # the longest first (the pareto fixture's runs)
     work.sort(key=lambda w: 0 if "pareto" in w[1] else (1 if "readme" in w[1] else 2))
@@ -211,7 +254,12 @@ def main(argv):
         for r in pool.imap_unordered(_job, work):
             res.append(r)
             print(json.dumps(r), flush=True)
-    res.sort(key=lambda r: (r["fixture"], VARIANTS.index(r["variant"])))
+    if os.path.exists(out_path):  # (merged with an earlier run's other variants)
+        with open(out_path) as f:
+            old = json.load(f)["results"]
+        have = {(r["fixture"], r["variant"]) for r in res}
+        res += [r for r in old if (r["fixture"], r["variant"]) not in have]
+    res.sort(key=lambda r: (r["fixture"], VARIANTS.index(r["variant"]) if r["variant"] in VARIANTS else 99))
     with open(out_path, "w") as f:
         json.dump({"generator": "tools/glue_envelope.py", "variants": VARIANTS, "results": res}, f, indent=1)
 
