@@ -507,8 +507,22 @@ static PyObject* setgeo(PyObject* self, PyObject* args) {
  *   occs    the occurrences (ci, i2) in sorted order; assigns: their medoids (rmsd) or None
  *   vals    rmsd: the medoid geometries of the key; else the binned geometry
  *   diff    note(): key -> count change                                                  */
+static int g_memo_check = 0;  /* memo_check(1): every memo hit is derived again and compared */
+static long long g_memo_hits = 0;
+
+static PyObject* memo_check(PyObject* self, PyObject* args) {
+  int on;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "p", &on)) return NULL;
+  g_memo_check = on;
+  const long long h = g_memo_hits;
+  g_memo_hits = 0;
+  return PyLong_FromLongLong(h);
+}
+
 typedef struct {
   PyObject *chains, *gd, *pk, *edges, *edges_fn, *names, *diff;
+  PyObject* memo; /* dict signature -> key string, or NULL (see mpair_key) */
 } MSt;
 
 static int key_error(PyObject* k) {
@@ -602,6 +616,66 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
     PyErr_Format(PyExc_ValueError, "idx+l cannot exceed %zd", 3 * nres - 1);
     return NULL;
   }
+  /* Memo (m->memo, the RMSD mode without glue optimisation): a pair of two partitioned tokens
+   * keys on raw values everywhere but the junction -- the angle at span position la - 1 and
+   * the dihedrals at la - 2, la - 1 (lo / hi above) -- and each token's raw values are its
+   * medoid geometry, written whole by set_token_geo when the token was made (bpe.py:1974-1985,
+   * 294-330) and never touched again.  So the key string is a function of (token ids, span
+   * length, phase, the three junction values): a merge's occurrences share most of them. */
+  PyObject* sig = NULL;
+  if (m->memo && pt1 && pt2 && la >= 2 && i1 + la - 2 >= 0) {
+    static const int BA[3] = {8, 3, 1}, DH[3] = {7, 5, 6};
+    long long w[9];
+    PyObject *id1 = PyTuple_GET_ITEM(t1, 1), *id2 = PyTuple_GET_ITEM(t2, 1);
+    int ok = PyTuple_GET_SIZE(id1) == 2 && PyTuple_GET_SIZE(id2) == 2;
+    for (int q = 0; ok && q < 2; q++) {
+      w[q] = PyLong_AsLongLong(PyTuple_GET_ITEM(id1, q));
+      w[2 + q] = PyLong_AsLongLong(PyTuple_GET_ITEM(id2, q));
+    }
+    if (PyErr_Occurred()) return NULL;
+    w[4] = (long long)L;
+    w[5] = (long long)(i1 % 3);
+    const Py_ssize_t a = i1 + la - 1, d0 = i1 + la - 2;
+    double v[3];
+    for (int q = 0; ok && q < 3; q++) {
+      PyObject* col;
+      Py_ssize_t row;
+      if (q == 0) {
+        if (a == 0) { /* (the init angle) */
+          v[0] = PyFloat_AsDouble(PyList_GET_ITEM(init, 2));
+          continue;
+        }
+        col = PyTuple_GET_ITEM(cols, BA[a % 3]);
+        row = (a - 1) / 3;
+      } else {
+        const Py_ssize_t d = d0 + (q - 1);
+        col = PyTuple_GET_ITEM(cols, DH[d % 3]);
+        row = (d + 1) / 3;
+      }
+      if (row < 0 || row >= PyList_GET_SIZE(col)) {
+        ok = 0;
+        break;
+      }
+      v[q] = PyFloat_AsDouble(PyList_GET_ITEM(col, row));
+    }
+    if (PyErr_Occurred()) return NULL;
+    if (ok) {
+      memcpy(&w[6], v, sizeof v);
+      sig = PyBytes_FromStringAndSize((const char*)w, sizeof w);
+      if (!sig) return NULL;
+      PyObject* hit = PyDict_GetItemWithError(m->memo, sig);
+      if (hit && !g_memo_check) {
+        Py_DECREF(sig);
+        Py_INCREF(hit);
+        return hit;
+      }
+      if (hit) g_memo_hits++;  /* (check mode: derived below and compared) */
+      if (PyErr_Occurred()) {
+        Py_DECREF(sig);
+        return NULL;
+      }
+    }
+  }
   PyObject* kL = PyLong_FromSsize_t(L);
   if (!kL) return NULL;
   PyObject* thr = PyDict_GetItemWithError(m->edges, kL);
@@ -611,9 +685,13 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
     thr = PyObject_CallOneArg(m->edges_fn, kL);  /* (computes and caches it) */
   }
   Py_DECREF(kL);
-  if (!thr) return NULL;
+  if (!thr) {
+    Py_XDECREF(sig);
+    return NULL;
+  }
   if (!PyTuple_Check(thr) || PyTuple_GET_SIZE(thr) != 9) {
     Py_DECREF(thr);
+    Py_XDECREF(sig);
     PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: edges must be a 9-tuple");
     return NULL;
   }
@@ -621,6 +699,19 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
   PyObject* k = build_key(cols, init, i1, L, i1 % 3, lo, hi, thr);
   PROF_ADD(6, pk0);
   Py_DECREF(thr);
+  if (sig) {
+    PyObject* hit = k && g_memo_check ? PyDict_GetItemWithError(m->memo, sig) : NULL;
+    if (hit) {
+      const int eq = PyUnicode_Compare(hit, k) == 0;
+      if (!eq) {
+        PyErr_Format(PyExc_AssertionError, "rmsdkey: memo key %R differs from the derived key %R", hit, k);
+        Py_CLEAR(k);
+      }
+    } else if (k && PyDict_SetItem(m->memo, sig, k) < 0) {
+      Py_CLEAR(k);
+    }
+    Py_DECREF(sig);
+  }
   return k;
 }
 
@@ -657,9 +748,15 @@ static PyObject* merge(PyObject* self, PyObject* args) {
                         &rmsd, &vals, &PyDict_Type, &diff))
     return NULL;
   MSt m;
-  if (!PyArg_ParseTuple(st, "O!OO!O!OO!", &PyList_Type, &m.chains, &m.gd, &PyDict_Type, &m.pk, &PyDict_Type, &m.edges,
-                        &m.edges_fn, &PyTuple_Type, &m.names))
+  m.memo = NULL;
+  if (!PyArg_ParseTuple(st, "O!OO!O!OO!|O", &PyList_Type, &m.chains, &m.gd, &PyDict_Type, &m.pk, &PyDict_Type, &m.edges,
+                        &m.edges_fn, &PyTuple_Type, &m.names, &m.memo))
     return NULL;
+  if (m.memo == Py_None) m.memo = NULL;
+  if (m.memo && !PyDict_Check(m.memo)) {
+    PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: the key memo must be a dict");
+    return NULL;
+  }
   m.diff = diff;
   PyObject* nobj = PyLong_FromSsize_t(n);
   PyObject* lenobj = PyLong_FromSsize_t(length);
@@ -1003,6 +1100,8 @@ static PyMethodDef METHODS[] = {
                                 {"reprs", reprs, METH_VARARGS, "repr(float) of each value (test)"},
                                 {"setgeo", setgeo, METH_VARARGS, "set_token_geo into the chain's column lists"},
                                 {"merge", merge, METH_VARARGS, "the occurrence loop of a merge (RmsdBPE._merge)"},
+                                {"memo_check", memo_check, METH_VARARGS,
+                                 "memo_check(on) -> memo hits compared since the last call (test)"},
                                 {"prio", prio, METH_VARARGS, "the priority updates of a merge (RmsdBPE._merge)"},
                                 {"packc", packc, METH_VARARGS, "pack() with spans as (chain, q, r)"},
                                 {NULL, NULL, 0, NULL}};

@@ -332,6 +332,7 @@ class RmsdBPE:
     Constructed by ``geobpe.bpe.BPE(...)`` when the arguments ask for this mode."""
 
     _py_keys = False  # True: the pair keys in Python (_pair_key_py) instead of csrc/rmsdkey.c
+    _no_key_memo = False  # True: rmsdkey.c merge derives every pair key (no memo; A/B and tests)
 
     def __init__(self, structures, bins, bin_strategy="histogram", save_dir="./plots/bpe",
                  compute_sec_structs=False, plot_iou_with_sec_structs=False, res_init=False, std_bonds=True,
@@ -887,7 +888,12 @@ class RmsdBPE:
         order = sorted(range(len(occ)), key=occ.__getitem__)
         if _KEYC is not None and not stale_ok and not self._py_keys:
             # the loop below in C (csrc/rmsdkey.c merge), on these same sets / dicts / lists
-            _KEYC.merge((self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T),
+            # (the pair-key memo of rmsdkey.c: partitioned tokens keep their medoid geometry
+            # unless glue optimisation rewrites the glues inside them)
+            memo = None
+            if not self.glue_opt and not self._no_key_memo:
+                memo = self.__dict__.setdefault("_key_memo", {})
+            _KEYC.merge((self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T, memo),
                         [occ[i] for i in order], [assign[i] for i in order] if rmsd else None, key, length, n,
                         rmsd, self._sphere_dict[key] if rmsd else binned, diff)
             order = ()

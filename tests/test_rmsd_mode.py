@@ -365,6 +365,23 @@ def test_pair_key_c_matches_python(name, host_geometry):
     assert kc == kp
 
 
+@pytest.mark.parametrize("name", ["rm_p0", "rm_p0_super", "rm_p0_b1_one_partition", "rm_p0_multigrid"])
+def test_pair_key_memo_equals_derived_keys(name, host_geometry):
+    """rmsdkey.c's pair-key memo (partitioned tokens keep their medoid geometry, so a pair's key
+    is a function of the two token ids and the junction's three values): with memo_check on,
+    every memo hit is derived again from the geometry and must be the same string; the run
+    equals the reference's fixture (run_and_compare) and the memo was actually used."""
+    from geobpe import rmsd_bpe
+    assert rmsd_bpe._KEYC is not None
+    rmsd_bpe._KEYC.memo_check(True)
+    try:
+        bpe = run_and_compare(name)
+        hits = rmsd_bpe._KEYC.memo_check(False)
+    finally:
+        rmsd_bpe._KEYC.memo_check(False)
+    assert len(bpe._key_memo) > 0 and hits > 0, (len(bpe._key_memo), hits)
+
+
 def test_pair_key_missing_thresholds_raises_like_python(host_geometry):
     """An item type with no thresholds at the span's length: the C key raises the
     exception the Python restatement (the reference's lookup) raises, type and message."""

@@ -134,8 +134,12 @@ def install_host(variant):
         for g, x0, (R, t), gi in zip(geos, x0s, targets, grids):
             pr = [(table[gi, k, 0, :counts[gi, k]], table[gi, k, 1, :counts[gi, k]]) for k in range(3)]
             outs.append(opt1(g, x0, R, t, pr, lam)[0])
+        FIRST_OPT.append(outs)
         return outs, None, None
     glue.optimize_chains = opt_chains
+
+
+FIRST_OPT = []  # the raw optima of every optimize_chains call (glue_opt_all first)
 
 
 def glued_stats(a, b, thr):
@@ -156,6 +160,7 @@ def run_fixture(name, variant, steps=True):
     import torch
     torch.set_num_threads(8 if variant == "threads" else 1)
     install_host(variant)
+    FIRST_OPT.clear()  # (a pool worker runs several jobs)
     from test_glue import _load
     from geobpe.bpe import BPE
     meta, arrs = _load(name)
@@ -179,6 +184,10 @@ def run_fixture(name, variant, steps=True):
     g = bpe.geometry()
     out = {"fixture": name, "variant": variant,
            "glued": {c: glued_stats(g[c], arrs[f"glued_{c}"], bpe._thresholds[1][c]) for c in GLUE_COLS}}
+    if "lbfgs_opt" in arrs and FIRST_OPT:  # the raw optimum of glue_opt_all against the reference's
+        d = np.abs(np.concatenate(FIRST_OPT[0]).astype(np.float64) - arrs["lbfgs_opt"])
+        d = np.minimum(d, 2 * np.pi - d)
+        out["raw_drift_rad"] = {"p50": float(np.median(d)), "p99": float(np.quantile(d, 0.99)), "max": float(d.max())}
     if steps:
         want = [p for call in meta["calls"] for p in call["popped"]]
         bpe.bin()
