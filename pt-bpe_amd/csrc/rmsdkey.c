@@ -60,6 +60,7 @@ static double now_ns(void) {
 
 static PyObject* ATTR[A_COUNT];
 static PyObject* PACK_KEYS[9];
+static PyObject* NAME_KEYS[9]; /* NAMES interned: a struc dict's keys are found by identity first */
 
 typedef struct {
   char* p;
@@ -429,7 +430,9 @@ static int setgeo_impl(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ssize_
   Py_ssize_t it = 0;
   while (PyDict_Next(vals, &it, &k, &v)) {
     int t = -1;
-    for (int q = 0; q < 9; q++)
+    for (int q = 0; q < 9 && t < 0; q++)
+      if (k == NAME_KEYS[q]) t = q;
+    for (int q = 0; q < 9 && t < 0; q++)
       if (PyUnicode_Check(k) && PyUnicode_CompareWithASCIIString(k, NAMES[q]) == 0) t = q;
     if (t < 0) {
       ok = Py_False;
@@ -551,6 +554,23 @@ static PyObject* pair2(Py_ssize_t ci, Py_ssize_t i) {
   Py_XDECREF(a);
   Py_XDECREF(b);
   return t;
+}
+
+/* the stored key of the pair starting at bond i of the chain (pk row: the chain's list;
+ * None = no pair), borrowed; NULL without an error when there is none */
+static PyObject* pk_get(PyObject* row, Py_ssize_t i) {
+  if (i < 0 || i >= PyList_GET_SIZE(row)) return NULL;
+  PyObject* k = PyList_GET_ITEM(row, i);
+  return k == Py_None ? NULL : k;
+}
+static int pk_set(PyObject* row, Py_ssize_t i, PyObject* k) {
+  if (i < 0 || i >= PyList_GET_SIZE(row)) {
+    PyErr_SetString(PyExc_IndexError, "rmsdkey.merge: pair position outside the chain");
+    return -1;
+  }
+  PyObject* v = k ? k : Py_None;
+  Py_INCREF(v);
+  return PyList_SetItem(row, i, v);
 }
 
 /* the chain's column lists in json key order (a new tuple) */
@@ -749,7 +769,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
     return NULL;
   MSt m;
   m.memo = NULL;
-  if (!PyArg_ParseTuple(st, "O!OO!O!OO!|O", &PyList_Type, &m.chains, &m.gd, &PyDict_Type, &m.pk, &PyDict_Type, &m.edges,
+  if (!PyArg_ParseTuple(st, "O!OO!O!OO!|O", &PyList_Type, &m.chains, &m.gd, &PyList_Type, &m.pk, &PyDict_Type, &m.edges,
                         &m.edges_fn, &PyTuple_Type, &m.names, &m.memo))
     return NULL;
   if (m.memo == Py_None) m.memo = NULL;
@@ -761,7 +781,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
   PyObject* nobj = PyLong_FromSsize_t(n);
   PyObject* lenobj = PyLong_FromSsize_t(length);
   PyObject *chain = NULL, *cols = NULL, *init = NULL, *tp = NULL, *btt = NULL, *events = NULL, *nres_o = NULL;
-  PyObject *t12 = NULL, *t01 = NULL, *t23 = NULL, *left = NULL, *right = NULL;
+  PyObject *t12 = NULL, *t01 = NULL, *t23 = NULL, *left = NULL, *right = NULL, *pkrow = NULL;
   Py_ssize_t cur_ci = -1, nres = 0, last_ci = -1, last_i1 = 0;
   int have_last = 0, err = 0;
   if (!nobj || !lenobj) goto fail;
@@ -797,6 +817,11 @@ static PyObject* merge(PyObject* self, PyObject* args) {
         goto fail;
       }
       nres = PyLong_AsSsize_t(nres_o);
+      if (ci >= PyList_GET_SIZE(m.pk) || !PyList_Check(PyList_GET_ITEM(m.pk, ci))) {
+        PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: the pair keys must be one list per chain");
+        goto fail;
+      }
+      pkrow = PyList_GET_ITEM(m.pk, ci);  /* (borrowed: m.pk holds it) */
       cur_ci = ci;
     }
     PROF_T(pt0);
@@ -810,15 +835,14 @@ static PyObject* merge(PyObject* self, PyObject* args) {
     }
     t12 = oc;
     Py_INCREF(t12);
-    PyObject* cur_key = PyDict_GetItemWithError(m.pk, t12);
-    if (!cur_key && PyErr_Occurred()) goto fail;
+    PyObject* cur_key = pk_get(pkrow, i2);
     const int same = cur_key ? PyObject_RichCompareBool(cur_key, key, Py_EQ) : 0;
     if (same < 0) goto fail;
     if (!same) {  /* bpe.py:1917-1920 */
       Py_CLEAR(t12);
       continue;
     }
-    if (set_in(&m, key, t12, 0) < 0 || PyDict_DelItem(m.pk, t12) < 0 || note(&m, key, -1) < 0) goto fail;
+    if (set_in(&m, key, t12, 0) < 0 || pk_set(pkrow, i2, NULL) < 0 || note(&m, key, -1) < 0) goto fail;
     Py_ssize_t i0 = 0, l0 = 0, i3 = 0, l3 = 0;
     const Py_ssize_t ntp = PyList_GET_SIZE(tp);
     if (i1) {
@@ -827,9 +851,9 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       l0 = i1 - i0;
       t01 = pair2(ci, i1);
       if (!t01) goto fail;
-      left = PyDict_GetItemWithError(m.pk, t01);
+      left = pk_get(pkrow, i1);
       if (!left) {
-        if (!PyErr_Occurred()) key_error(t01);
+        key_error(t01);
         goto fail;
       }
       Py_INCREF(left);
@@ -845,9 +869,9 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       }
       t23 = pair2(ci, i3);
       if (!t23) goto fail;
-      right = PyDict_GetItemWithError(m.pk, t23);
+      right = pk_get(pkrow, i3);
       if (!right) {
-        if (!PyErr_Occurred()) key_error(t23);
+        key_error(t23);
         goto fail;
       }
       Py_INCREF(right);
@@ -906,7 +930,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       PyObject* k = mpair_key(&m, cols, init, tp, btt, nres, i0, l0, length);
       PROF_ADD(3, pt0);
       if (!k) goto fail;
-      const int rc = (set_in(&m, k, t01, 1) < 0 || PyDict_SetItem(m.pk, t01, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
+      const int rc = (set_in(&m, k, t01, 1) < 0 || pk_set(pkrow, i1, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
       Py_DECREF(k);
       PROF_ADD(4, pt0);
       if (rc < 0) goto fail;
@@ -915,7 +939,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       PyObject* k = mpair_key(&m, cols, init, tp, btt, nres, i1, length, l3);
       PROF_ADD(3, pt0);
       if (!k) goto fail;
-      const int rc = (set_in(&m, k, t23, 1) < 0 || PyDict_SetItem(m.pk, t23, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
+      const int rc = (set_in(&m, k, t23, 1) < 0 || pk_set(pkrow, i3, k) < 0 || note(&m, k, 1) < 0) ? -1 : 0;
       Py_DECREF(k);
       PROF_ADD(4, pt0);
       if (rc < 0) goto fail;
@@ -1111,5 +1135,7 @@ PyMODINIT_FUNC PyInit__rmsdkey(void) {
     if (!ATTR[i] && !(ATTR[i] = PyUnicode_InternFromString(ATTR_NAMES[i]))) return NULL;
   for (int i = 0; i < 9; i++)
     if (!PACK_KEYS[i] && !(PACK_KEYS[i] = PyUnicode_InternFromString(PACK_NAMES[i]))) return NULL;
+  for (int i = 0; i < 9; i++)
+    if (!NAME_KEYS[i] && !(NAME_KEYS[i] = PyUnicode_InternFromString(NAMES[i]))) return NULL;
   return PyModule_Create(&MOD);
 }

@@ -131,6 +131,15 @@ RES_SPHERE_KEY = {3: '{"N:CA": [0], "CA:C": [0], "0C:1N": [0], "tau": [0], "CA:C
 _LEFT = {}
 
 
+def _pk_at(pk, ci, i):
+    """The stored key of the pair starting at bond i of chain ci (pk: that chain's list);
+    KeyError((ci, i)) when no pair starts there, as the reference's dict lookup raises."""
+    k = pk[i] if i < len(pk) else None
+    if k is None:
+        raise KeyError((ci, i))
+    return k
+
+
 def _get_ind(v, values):
     """BPE.get_ind (bpe.py:1164-1189), with the left edges of each threshold list cached."""
     left = _LEFT.get(id(values))
@@ -784,14 +793,17 @@ class RmsdBPE:
         self._geo_dict = defaultdict(set)
         # the key of every live pair by (chain, start of its second token): a pair's key
         # changes only when a merge replaces the pair, so step() reads the old neighbour keys
-        # from here instead of re-deriving them from the geometry (bpe.py:1917, 1933, 1941)
-        self._pk = {}
+        # from here instead of re-deriving them from the geometry (bpe.py:1917, 1933, 1941).
+        # One list per chain indexed by bond (None: no pair starts there) -- a merge's
+        # occurrences read and write their chain's list instead of hashing (chain, bond)
+        # tuples into one dict of every pair
+        self._pk = [[None] * (3 * c.n) for c in self._chains]
         for ci, c in enumerate(self._chains):
             toks = c.tokens()
             for (i1, _, l1), (i2, _, l2) in zip(toks, toks[1:]):
                 k = self._pair_key(ci, i1, l1, l2)
                 self._geo_dict[k].add((ci, i2))
-                self._pk[(ci, i2)] = k
+                self._pk[ci][i2] = k
         self._geo_step = {k: 0 for k in self._geo_dict}
         self._key_to_priority = {key: (True, -len(occ), key) for key, occ in self._geo_dict.items()}
         self._priority = _PrioQueue(self._key_to_priority)
@@ -911,25 +923,25 @@ class RmsdBPE:
                 continue
             if not (l1 > 0 and l2 > 0):
                 raise AssertionError("bad split")
-            pk = self._pk
-            if pk.get((ci, i2)) != key or (stale_ok and self._pair_key(ci, i1, l1, l2) != key):
+            pk = self._pk[ci]
+            if pk[i2] != key or (stale_ok and self._pair_key(ci, i1, l1, l2) != key):
                 # bpe.py:1917-1920 (breakpoint(); continue): the stored key is the pair's key
                 # unless a multi-grid re-snap made it stale (no RMSD partitioning)
                 continue
             gd[key].remove((ci, i2))
-            del pk[(ci, i2)]
+            pk[i2] = None
             note(key, -1)
             left = right = None
             if i1:
                 i0 = tp[i1 - 1]
                 l0 = i1 - i0
-                left = self._pair_key(ci, i0, l0, l1) if stale_ok else pk[(ci, i1)]
+                left = self._pair_key(ci, i0, l0, l1) if stale_ok else _pk_at(pk, ci, i1)
             if i2 + l2 < len(tp):
                 i3 = i2 + l2
                 l3 = 0
                 while i3 + l3 < len(tp) and tp[i3 + l3] == i3:
                     l3 += 1
-                right = self._pair_key(ci, i2, l2, l3) if stale_ok else pk[(ci, i3)]
+                right = self._pair_key(ci, i2, l2, l3) if stale_ok else _pk_at(pk, ci, i3)
             if left:
                 gd[left].remove((ci, i1))
                 note(left, -1)
@@ -946,12 +958,12 @@ class RmsdBPE:
             if left:
                 k = self._pair_key(ci, i0, l0, length)
                 gd[k].add((ci, i1))
-                pk[(ci, i1)] = k
+                pk[i1] = k
                 note(k, +1)
             if right:
                 k = self._pair_key(ci, i1, length, l3)
                 gd[k].add((ci, i3))
-                pk[(ci, i3)] = k
+                pk[i3] = k
                 note(k, +1)
             if not rmsd:
                 c.set_geo(i1, length, binned)
@@ -961,22 +973,22 @@ class RmsdBPE:
         if (rmsd and self.glue_opt and not self.rmsd_only and self.glue_opt_method == "all"
                 and self._step % self.glue_opt_every == 0):
             uniq = set(ci for ci, _ in occ)
-            pk = self._pk
             for ci in self._glue_opt(list(uniq)):
                 btt = self._chains[ci].btt
+                pk = self._pk[ci]
                 last = 3 * self._chains[ci].n - 1
                 for i1, (_, _, l1) in list(btt.items()):
                     if i1 + l1 == last:
                         continue
                     i2 = i1 + l1
                     l2 = btt[i2][2]
-                    old = pk[(ci, i2)]
+                    old = _pk_at(pk, ci, i2)
                     new = self._pair_key(ci, i1, l1, l2)
                     if new != old:
                         gd[old].remove((ci, i2))
                         note(old, -1)
                         gd[new].add((ci, i2))
-                        pk[(ci, i2)] = new
+                        pk[i2] = new
                         note(new, +1)
         if not recurring:
             self._step += 1
