@@ -125,7 +125,10 @@ struct geobpe_ctx {
   // per-key list build (tail_build): radix-sort scratch; kp_atomic: the atomic counting build (A/B)
   void* kps = nullptr;
   int64_t kps_bytes = 0;
-  bool kp_atomic = false;
+#ifndef KP_ATOMIC_DEFAULT
+#define KP_ATOMIC_DEFAULT 0  // (A/B builds: 1 = the atomic counting build by default)
+#endif
+  bool kp_atomic = KP_ATOMIC_DEFAULT != 0;
   int64_t own_row0 = 0, own_row1 = -1;
   // profiling
   bool prof = false;
@@ -603,7 +606,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   }
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
-  if (const char* e = getenv("GEOBPE_KP_ATOMIC")) c->kp_atomic = atoi(e) == 1;  // (A/B: the atomic list build)
+  if (const char* e = getenv("GEOBPE_KP_ATOMIC")) c->kp_atomic = atoi(e) == 1;  // (A/B: 1 = the atomic list build)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
