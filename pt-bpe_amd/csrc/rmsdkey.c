@@ -510,6 +510,87 @@ static PyObject* setgeo(PyObject* self, PyObject* args) {
  *   occs    the occurrences (ci, i2) in sorted order; assigns: their medoids (rmsd) or None
  *   vals    rmsd: the medoid geometries of the key; else the binned geometry
  *   diff    note(): key -> count change                                                  */
+/* The pair-key memo (mpair_key): an open-addressing table of 9-word signatures -> key str,
+ * owned by a capsule per RmsdBPE instance (a Python dict keyed by bytes cost an allocation
+ * and a 72-byte hash per lookup) */
+typedef struct {
+  long long w[9];
+  PyObject* v; /* NULL: empty */
+} MemoEnt;
+typedef struct {
+  Py_ssize_t n, cap; /* cap: a power of two */
+  MemoEnt* e;
+} Memo;
+static const char* MEMO_NAME = "rmsdkey.memo";
+
+static void memo_destroy(PyObject* capsule) {
+  Memo* m = (Memo*)PyCapsule_GetPointer(capsule, MEMO_NAME);
+  if (!m) return;
+  for (Py_ssize_t i = 0; i < m->cap; i++) Py_XDECREF(m->e[i].v);
+  PyMem_Free(m->e);
+  PyMem_Free(m);
+}
+static PyObject* memo_new(PyObject* self, PyObject* noargs) {
+  (void)self;
+  (void)noargs;
+  Memo* m = (Memo*)PyMem_Calloc(1, sizeof(Memo));
+  if (!m) return PyErr_NoMemory();
+  m->cap = 1 << 12;
+  m->e = (MemoEnt*)PyMem_Calloc((size_t)m->cap, sizeof(MemoEnt));
+  if (!m->e) {
+    PyMem_Free(m);
+    return PyErr_NoMemory();
+  }
+  PyObject* c = PyCapsule_New(m, MEMO_NAME, memo_destroy);
+  if (!c) {
+    PyMem_Free(m->e);
+    PyMem_Free(m);
+  }
+  return c;
+}
+static PyObject* memo_len(PyObject* self, PyObject* capsule) {
+  (void)self;
+  Memo* m = (Memo*)PyCapsule_GetPointer(capsule, MEMO_NAME);
+  return m ? PyLong_FromSsize_t(m->n) : NULL;
+}
+static unsigned long long memo_hash(const long long* w) {
+  unsigned long long h = 0x9E3779B97F4A7C15ULL;
+  for (int i = 0; i < 9; i++) {
+    h ^= (unsigned long long)w[i];
+    h *= 0xBF58476D1CE4E5B9ULL;
+    h ^= h >> 31;
+  }
+  return h;
+}
+static MemoEnt* memo_slot(Memo* m, const long long* w) { /* the entry holding w, or the empty one it goes to */
+  Py_ssize_t i = (Py_ssize_t)(memo_hash(w) & (unsigned long long)(m->cap - 1));
+  for (;;) {
+    MemoEnt* e = &m->e[i];
+    if (!e->v || memcmp(e->w, w, sizeof e->w) == 0) return e;
+    i = (i + 1) & (m->cap - 1);
+  }
+}
+static int memo_put(Memo* m, const long long* w, PyObject* v) {
+  if (2 * (m->n + 1) > m->cap) { /* grow to keep the load under 1/2 */
+    Memo big = {0, 2 * m->cap, (MemoEnt*)PyMem_Calloc((size_t)(2 * m->cap), sizeof(MemoEnt))};
+    if (!big.e) {
+      PyErr_NoMemory();
+      return -1;
+    }
+    for (Py_ssize_t i = 0; i < m->cap; i++)
+      if (m->e[i].v) *memo_slot(&big, m->e[i].w) = m->e[i];
+    PyMem_Free(m->e);
+    m->e = big.e;
+    m->cap = big.cap;
+  }
+  MemoEnt* e = memo_slot(m, w);
+  if (!e->v) m->n++;
+  memcpy(e->w, w, sizeof e->w);
+  Py_INCREF(v);
+  Py_XSETREF(e->v, v);
+  return 0;
+}
+
 static int g_memo_check = 0;  /* memo_check(1): every memo hit is derived again and compared */
 static long long g_memo_hits = 0;
 
@@ -525,7 +606,7 @@ static PyObject* memo_check(PyObject* self, PyObject* args) {
 
 typedef struct {
   PyObject *chains, *gd, *pk, *edges, *edges_fn, *names, *diff;
-  PyObject* memo; /* dict signature -> key string, or NULL (see mpair_key) */
+  Memo* memo; /* the pair-key memo, or NULL (see mpair_key) */
 } MSt;
 
 static int key_error(PyObject* k) {
@@ -642,10 +723,10 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
    * medoid geometry, written whole by set_token_geo when the token was made (bpe.py:1974-1985,
    * 294-330) and never touched again.  So the key string is a function of (token ids, span
    * length, phase, the three junction values): a merge's occurrences share most of them. */
-  PyObject* sig = NULL;
+  int use_memo = 0;
+  long long w[9];
   if (m->memo && pt1 && pt2 && la >= 2 && i1 + la - 2 >= 0) {
     static const int BA[3] = {8, 3, 1}, DH[3] = {7, 5, 6};
-    long long w[9];
     PyObject *id1 = PyTuple_GET_ITEM(t1, 1), *id2 = PyTuple_GET_ITEM(t2, 1);
     int ok = PyTuple_GET_SIZE(id1) == 2 && PyTuple_GET_SIZE(id2) == 2;
     for (int q = 0; ok && q < 2; q++) {
@@ -681,19 +762,13 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
     if (PyErr_Occurred()) return NULL;
     if (ok) {
       memcpy(&w[6], v, sizeof v);
-      sig = PyBytes_FromStringAndSize((const char*)w, sizeof w);
-      if (!sig) return NULL;
-      PyObject* hit = PyDict_GetItemWithError(m->memo, sig);
+      use_memo = 1;
+      PyObject* hit = memo_slot(m->memo, w)->v;
       if (hit && !g_memo_check) {
-        Py_DECREF(sig);
         Py_INCREF(hit);
         return hit;
       }
       if (hit) g_memo_hits++;  /* (check mode: derived below and compared) */
-      if (PyErr_Occurred()) {
-        Py_DECREF(sig);
-        return NULL;
-      }
     }
   }
   PyObject* kL = PyLong_FromSsize_t(L);
@@ -705,13 +780,9 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
     thr = PyObject_CallOneArg(m->edges_fn, kL);  /* (computes and caches it) */
   }
   Py_DECREF(kL);
-  if (!thr) {
-    Py_XDECREF(sig);
-    return NULL;
-  }
+  if (!thr) return NULL;
   if (!PyTuple_Check(thr) || PyTuple_GET_SIZE(thr) != 9) {
     Py_DECREF(thr);
-    Py_XDECREF(sig);
     PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: edges must be a 9-tuple");
     return NULL;
   }
@@ -719,18 +790,16 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
   PyObject* k = build_key(cols, init, i1, L, i1 % 3, lo, hi, thr);
   PROF_ADD(6, pk0);
   Py_DECREF(thr);
-  if (sig) {
-    PyObject* hit = k && g_memo_check ? PyDict_GetItemWithError(m->memo, sig) : NULL;
-    if (hit) {
-      const int eq = PyUnicode_Compare(hit, k) == 0;
-      if (!eq) {
+  if (use_memo && k) {
+    PyObject* hit = memo_slot(m->memo, w)->v;
+    if (hit) { /* (check mode) */
+      if (PyUnicode_Compare(hit, k) != 0) {
         PyErr_Format(PyExc_AssertionError, "rmsdkey: memo key %R differs from the derived key %R", hit, k);
         Py_CLEAR(k);
       }
-    } else if (k && PyDict_SetItem(m->memo, sig, k) < 0) {
+    } else if (memo_put(m->memo, w, k) < 0) {
       Py_CLEAR(k);
     }
-    Py_DECREF(sig);
   }
   return k;
 }
@@ -768,14 +837,14 @@ static PyObject* merge(PyObject* self, PyObject* args) {
                         &rmsd, &vals, &PyDict_Type, &diff))
     return NULL;
   MSt m;
-  m.memo = NULL;
+  PyObject* memo = NULL;
   if (!PyArg_ParseTuple(st, "O!OO!O!OO!|O", &PyList_Type, &m.chains, &m.gd, &PyList_Type, &m.pk, &PyDict_Type, &m.edges,
-                        &m.edges_fn, &PyTuple_Type, &m.names, &m.memo))
+                        &m.edges_fn, &PyTuple_Type, &m.names, &memo))
     return NULL;
-  if (m.memo == Py_None) m.memo = NULL;
-  if (m.memo && !PyDict_Check(m.memo)) {
-    PyErr_SetString(PyExc_TypeError, "rmsdkey.merge: the key memo must be a dict");
-    return NULL;
+  m.memo = NULL;
+  if (memo && memo != Py_None) {
+    m.memo = (Memo*)PyCapsule_GetPointer(memo, MEMO_NAME);
+    if (!m.memo) return NULL;
   }
   m.diff = diff;
   PyObject* nobj = PyLong_FromSsize_t(n);
@@ -1124,6 +1193,8 @@ static PyMethodDef METHODS[] = {
                                 {"reprs", reprs, METH_VARARGS, "repr(float) of each value (test)"},
                                 {"setgeo", setgeo, METH_VARARGS, "set_token_geo into the chain's column lists"},
                                 {"merge", merge, METH_VARARGS, "the occurrence loop of a merge (RmsdBPE._merge)"},
+                                {"memo_new", memo_new, METH_NOARGS, "a new pair-key memo (merge's 7th state item)"},
+                                {"memo_len", memo_len, METH_O, "keys in a pair-key memo"},
                                 {"memo_check", memo_check, METH_VARARGS,
                                  "memo_check(on) -> memo hits compared since the last call (test)"},
                                 {"prio", prio, METH_VARARGS, "the priority updates of a merge (RmsdBPE._merge)"},

@@ -904,7 +904,9 @@ class RmsdBPE:
             # unless glue optimisation rewrites the glues inside them)
             memo = None
             if not self.glue_opt and not self._no_key_memo:
-                memo = self.__dict__.setdefault("_key_memo", {})
+                memo = self.__dict__.get("_key_memo")
+                if memo is None:
+                    memo = self._key_memo = _KEYC.memo_new()
             _KEYC.merge((self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T, memo),
                         [occ[i] for i in order], [assign[i] for i in order] if rmsd else None, key, length, n,
                         rmsd, self._sphere_dict[key] if rmsd else binned, diff)

@@ -379,7 +379,8 @@ def test_pair_key_memo_equals_derived_keys(name, host_geometry):
         hits = rmsd_bpe._KEYC.memo_check(False)
     finally:
         rmsd_bpe._KEYC.memo_check(False)
-    assert len(bpe._key_memo) > 0 and hits > 0, (len(bpe._key_memo), hits)
+    n = rmsd_bpe._KEYC.memo_len(bpe._key_memo)
+    assert n > 0 and hits > 0, (n, hits)
 
 
 def test_pair_key_missing_thresholds_raises_like_python(host_geometry):
