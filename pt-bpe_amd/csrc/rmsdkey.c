@@ -629,8 +629,20 @@ static int note(MSt* m, PyObject* k, long d) {
   return rc;
 }
 
+/* small non-negative ints (chain and bond indices) from a cache: PyLong_FromSsize_t allocates
+ * every value above 256, twice or more per key and per occurrence here */
+static PyObject* g_ints[1 << 16];
+static PyObject* cint(Py_ssize_t v) {
+  if (v >= 0 && v < (Py_ssize_t)(sizeof g_ints / sizeof g_ints[0])) {
+    if (!g_ints[v] && !(g_ints[v] = PyLong_FromSsize_t(v))) return NULL;
+    Py_INCREF(g_ints[v]);
+    return g_ints[v];
+  }
+  return PyLong_FromSsize_t(v);
+}
+
 static PyObject* pair2(Py_ssize_t ci, Py_ssize_t i) {
-  PyObject *a = PyLong_FromSsize_t(ci), *b = PyLong_FromSsize_t(i);
+  PyObject *a = cint(ci), *b = cint(i);
   PyObject* t = (a && b) ? PyTuple_Pack(2, a, b) : NULL;
   Py_XDECREF(a);
   Py_XDECREF(b);
@@ -684,7 +696,7 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
                            Py_ssize_t i1, Py_ssize_t la, Py_ssize_t lb) {
   const Py_ssize_t p1 = list_int(tp, i1), p2 = p1 < 0 ? -1 : list_int(tp, i1 + la);
   if (p1 < 0 || p2 < 0) return NULL;
-  PyObject *k1 = PyLong_FromSsize_t(p1), *k2 = PyLong_FromSsize_t(p2);
+  PyObject *k1 = cint(p1), *k2 = cint(p2);
   PyObject* t1 = k1 ? PyDict_GetItemWithError(btt, k1) : NULL;
   PyObject* t2 = (t1 && k2) ? PyDict_GetItemWithError(btt, k2) : NULL;
   if (!t1 || !t2) {
@@ -771,7 +783,7 @@ static PyObject* mpair_key(MSt* m, PyObject* cols, PyObject* init, PyObject* tp,
       if (hit) g_memo_hits++;  /* (check mode: derived below and compared) */
     }
   }
-  PyObject* kL = PyLong_FromSsize_t(L);
+  PyObject* kL = cint(L);
   if (!kL) return NULL;
   PyObject* thr = PyDict_GetItemWithError(m->edges, kL);
   if (thr) {
@@ -949,7 +961,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
     if (right && (set_in(&m, right, t23, 0) < 0 || note(&m, right, -1) < 0)) goto fail;
     PROF_ADD(0, pt0);
     {
-      PyObject* vi1 = PyLong_FromSsize_t(i1);
+      PyObject* vi1 = cint(i1);
       if (!vi1) goto fail;
       for (Py_ssize_t j = i2; j < i2 + l2; j++) {
         Py_INCREF(vi1);
@@ -958,7 +970,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
           goto fail;
         }
       }
-      PyObject* ki2 = PyLong_FromSsize_t(i2);
+      PyObject* ki2 = cint(i2);
       int rc = ki2 ? PyDict_DelItem(btt, ki2) : -1;
       Py_XDECREF(ki2);
       PyObject *tokid = NULL, *val = NULL, *ev = NULL;
@@ -973,7 +985,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
         val = tokid ? PyTuple_Pack(3, vi1, tokid, lenobj) : NULL;
         rc = val ? PyDict_SetItem(btt, vi1, val) : -1;
         if (rc == 0) {
-          PyObject* vi2 = PyLong_FromSsize_t(i2);
+          PyObject* vi2 = cint(i2);
           ev = vi2 ? PyTuple_Pack(3, vi1, vi2, val) : NULL;
           Py_XDECREF(vi2);
           rc = ev ? PyList_Append(events, ev) : -1;
