@@ -126,7 +126,7 @@ struct geobpe_ctx {
   void* kps = nullptr;
   int64_t kps_bytes = 0;
 #ifndef KP_ATOMIC_DEFAULT
-#define KP_ATOMIC_DEFAULT 0  // (A/B builds: 1 = the atomic counting build by default)
+#define KP_ATOMIC_DEFAULT 1  // (the atomic counting build; A/B builds: 0 = the radix-sorted build)
 #endif
   bool kp_atomic = KP_ATOMIC_DEFAULT != 0;
   int64_t own_row0 = 0, own_row1 = -1;
@@ -442,9 +442,10 @@ int tail_alloc(geobpe_ctx* c) {
   return 0;
 }
 
-// per-key posting lists of the live pairs, after any pending place: a stable radix sort of
-// the (key, slot) pairs (kp_sort.hip) -> runs -> list space -> placement; GEOBPE_KP_ATOMIC=1
-// (A/B) or a failed scratch allocation: the counting build with a global atomic per pair
+// per-key posting lists of the live pairs, after any pending place.  Default: the counting
+// build with a global atomic per pair (k_kp_alloc / k_kp_fill).  GEOBPE_KP_ATOMIC=0 (A/B): a
+// stable radix sort of the (key, slot) pairs (kp_sort.hip) -> runs -> list space ->
+// placement; measured slower end to end at C3 (25.3k vs 28.6k merges/s)
 int tail_build_sorted(geobpe_ctx* c) {
   Dev& D = c->D;
   const int64_t n = c->R;
@@ -546,6 +547,17 @@ void tail_check_switch(geobpe_ctx* c) {
   if (tail_enabled(c) && m <= c->tail_thresh) c->tail_on = true;
 }
 
+// the middle / late regimes' arrays (per-key lists, pool, merged-occurrence and new-pair
+// lists: ~90 B per residue) reserved with the key arrays, after the bin pass, so that the
+// switch itself allocates nothing (hipMalloc + fill of ~1 GB at C3, inside the merge loop
+// otherwise).  A sharded run reserves at its collapse, for the gathered corpus.
+int regime_reserve(geobpe_ctx* c) {
+  if (c->distributed || (c->mid_thresh <= 0 && c->tail_thresh <= 0)) return 0;
+  int rc;
+  if ((rc = tail_alloc(c))) return rc;
+  return sync_state(c);
+}
+
 // per-key lists usable by the middle regime: built at the switch, rebuilt when a place
 // lost entries (the stalled iterations merged nothing) or the pool is 3/4 used
 int mid_prepare(geobpe_ctx* c) {
@@ -606,7 +618,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   }
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
-  if (const char* e = getenv("GEOBPE_KP_ATOMIC")) c->kp_atomic = atoi(e) == 1;  // (A/B: 1 = the atomic list build)
+  if (const char* e = getenv("GEOBPE_KP_ATOMIC")) c->kp_atomic = atoi(e) != 0;  // (A/B: 0 = the sorted list build)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
@@ -986,7 +998,7 @@ int geobpe_bin(geobpe_ctx* c) {
       c->bin_cube[1] = shape[1];
     }
     for (void* q : tmp) hipFree(q);
-    return rc;
+    return rc ? rc : regime_reserve(c);
   }
   if ((rc = reset_region_counters(c))) return rc;
   {
@@ -997,7 +1009,8 @@ int geobpe_bin(geobpe_ctx* c) {
   enqueue_commit(c, c->distributed);
   enqueue_pack(c);
   HIPCHK(c, hipGetLastError());
-  return sync_state(c);
+  if ((rc = sync_state(c))) return rc;
+  return regime_reserve(c);
 }
 
 int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {

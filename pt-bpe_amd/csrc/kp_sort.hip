@@ -3,10 +3,12 @@
 // key's pairs form one run in slot order.  hipCUB's onesweep radix sort (rocPRIM) in a
 // translation unit of its own (its templates would triple the main unit's compile time).
 //
-// The build it replaces counted and placed every live pair with a returning global atomic
-// on its key's list counter (k_kp_fill: ~25 M atomics, 4.7 GB of memory-side traffic and
-// 1.46 ms at the C3 middle-regime switch); the sorted runs place every pair with plain
-// loads and stores.
+// The alternative to the default build, which counts and places every live pair with a
+// returning global atomic on its key's list counter (k_kp_fill: ~25 M atomics, 4.7 GB of
+// memory-side traffic and 1.46 ms at the C3 middle-regime switch).  The sorted runs place
+// every pair with plain loads and stores, but the sort over every residue slot plus its
+// scratch cost more end to end (C3 default run 25.3k vs 28.6k merges/s), so it is the A/B
+// leg (GEOBPE_KP_ATOMIC=0), not the default.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 

@@ -239,7 +239,7 @@ def _job(args):
 
 def main(argv):
     import multiprocessing as mp
-    jobs, steps = 6, True
+    jobs, steps, variants = 6, True, VARIANTS
     while argv and argv[0].startswith("--"):
         if argv[0] == "--jobs":
             jobs = int(argv[1])
@@ -247,10 +247,11 @@ def main(argv):
         elif argv[0] == "--no-steps":
             steps = False
             argv = argv[1:]
-    variants = VARIANTS
-    if argv and argv[0] == "--variants":
-        variants = argv[1].split(",")
-        argv = argv[2:]
+        elif argv[0] == "--variants":
+            variants = argv[1].split(",")
+            argv = argv[2:]
+        else:
+            raise SystemExit(f"unknown option {argv[0]}")
     out_path, names = argv[0], (argv[1:] or FIXTURES + ["drift120"])
     work = []
     for name in names:

@@ -48,6 +48,21 @@ def main(d):
                            "p50_us": round(q[len(q) // 2], 2), "min_us": round(q[0], 2), "max_us": round(q[-1], 2)}
     if tr:
         out["window_wall_us"] = round((int(tr[-1]["End_Timestamp"]) - int(tr[0]["Start_Timestamp"])) / 1000, 2)
+        # the GPU's idle time inside the window: the gaps between consecutive dispatches (host
+        # waits, allocations, launch latency), by the kernel pair around them
+        gaps, by_pair = [], collections.defaultdict(list)
+        t = sorted(tr, key=lambda r: int(r["Start_Timestamp"]))
+        end = int(t[0]["End_Timestamp"])
+        for a, b in zip(t, t[1:]):
+            g = (int(b["Start_Timestamp"]) - end) / 1000
+            end = max(end, int(b["End_Timestamp"]))
+            if g > 0:
+                gaps.append((g, short(a["Kernel_Name"]), short(b["Kernel_Name"])))
+                by_pair[short(a["Kernel_Name"]) + " -> " + short(b["Kernel_Name"])].append(g)
+        out["idle"] = {"total_us": round(sum(g for g, _, _ in gaps), 2),
+                       "by_pair": {k: {"n": len(v), "total_us": round(sum(v), 2), "max_us": round(max(v), 2)}
+                                   for k, v in sorted(by_pair.items(), key=lambda kv: -sum(kv[1]))[:12]},
+                       "largest": [[round(g, 2), a, b] for g, a, b in sorted(gaps, reverse=True)[:12]]}
     for c, name in (("fetch", "FETCH_SIZE"), ("write", "WRITE_SIZE")):
         p = f"{d}/pmc_{c}/run_counter_collection.csv"
         if not os.path.exists(p):
