@@ -190,8 +190,15 @@ void dfree(geobpe_ctx* c, T** p) {
 // ---------------------------------------------------------------- light kernel timing
 hipEvent_t take_event(geobpe_ctx* c) {
   if (c->evpool.empty()) {
+    // timing-only events: no system-scope fence (an L2 writeback + invalidate) when one
+    // completes -- with it, each sampled launch opened a 7-20 us gap in the merge loop
+    // (GEOBPE_EVENT_FENCE=1: the default events, A/B)
+    static const bool fence = getenv("GEOBPE_EVENT_FENCE") && atoi(getenv("GEOBPE_EVENT_FENCE")) == 1;
     hipEvent_t e;
-    hipEventCreate(&e);
+    if (fence)
+      hipEventCreate(&e);
+    else
+      hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
     c->evall.push_back(e);
     return e;
   }

@@ -998,7 +998,7 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       if (rc < 0) goto fail;
     }
     PROF_ADD(1, pt0);
-    if (rmsd) {
+    if (rmsd && vals != Py_None) {  /* (None: rmsd_only, the merge keeps its own geometry) */
       PyObject* a = PyList_GET_ITEM(assigns, q);
       PyObject* struc = PyObject_GetItem(vals, a);
       if (!struc) goto fail;

@@ -32,8 +32,9 @@ the residues at initialize() and every merge; p >= 4 never creates ``_sphere_dic
 first merge of >= p bonds raises AttributeError there, as it does here.  Glue optimisation
 (``glue_opt=True``, ``glue_opt_method="all"``, bpe.py:106-135, 192-229, 2027-2071) runs as one
 device L-BFGS launch over the chains (geobpe/glue.py, csrc/glue.h).  The "each" method
-stops where the reference's does (an AssertionError in initialize(), bpe.py:761).  Not
-built: ``rmsd_only``.  Free bond lengths
+stops where the reference's does (an AssertionError in initialize(), bpe.py:761).
+``rmsd_only`` (bpe.py:1977, 2027) keeps a partitioned merge's own geometry: the medoid's is
+not written over it, and no glue is re-optimised.  Free bond lengths
 (``std_bonds=False``) run where the reference runs them (p <= 2; p >= 3 raises its KeyError).
 """
 from __future__ import annotations
@@ -359,8 +360,8 @@ class RmsdBPE:
             raise NotImplementedError("free bonds with uniform (equal-count) bins are not built")
         if glue_opt and glue_opt_method not in ("all", "each"):
             raise ValueError(f"glue_opt_method must be 'all' or 'each', not {glue_opt_method!r}")
-        if rmsd_only or compute_sec_structs:
-            raise NotImplementedError("rmsd_only / secondary-structure priorities are not built")
+        if compute_sec_structs:
+            raise NotImplementedError("secondary-structure priorities are not built")
         if isinstance(structures, dict) and "row_off" in structures:
             corpus = structures
             fnames = list(structures["fnames"]) if structures.get("fnames") is not None else None
@@ -903,13 +904,13 @@ class RmsdBPE:
             # (the pair-key memo of rmsdkey.c: partitioned tokens keep their medoid geometry
             # unless glue optimisation rewrites the glues inside them)
             memo = None
-            if not self.glue_opt and not self._no_key_memo:
+            if not self.glue_opt and not self.rmsd_only and not self._no_key_memo:
                 memo = self.__dict__.get("_key_memo")
                 if memo is None:
                     memo = self._key_memo = _KEYC.memo_new()
             _KEYC.merge((self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T, memo),
                         [occ[i] for i in order], [assign[i] for i in order] if rmsd else None, key, length, n,
-                        rmsd, self._sphere_dict[key] if rmsd else binned, diff)
+                        rmsd, (None if self.rmsd_only else self._sphere_dict[key]) if rmsd else binned, diff)
             order = ()
         for idx in order:
             ci, i2 = occ[idx]
@@ -955,7 +956,7 @@ class RmsdBPE:
             c.btt.pop(i2)
             c.btt[i1] = (i1, (n, assign[idx]) if rmsd else n, length)
             c.events.append((i1, i2, c.btt[i1]))
-            if rmsd:
+            if rmsd and not self.rmsd_only:  # (bpe.py:1977)
                 c.set_geo(i1, length, self._sphere_dict[key][assign[idx]])
             if left:
                 k = self._pair_key(ci, i0, l0, length)
@@ -1337,8 +1338,6 @@ class RmsdBPE:
             setattr(self, k, getattr(obj, k, None))
         self.rmsd_super_res = bool(self.rmsd_super_res)
         self.std_bonds = True if self.std_bonds is None else bool(self.std_bonds)
-        if self.rmsd_only:
-            raise NotImplementedError("checkpoints trained with rmsd_only")
         if self.glue_opt:  # the prior tables from the checkpoint's _bin_centers / _bin_weights
             from .glue import GLUE
 

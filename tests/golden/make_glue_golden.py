@@ -50,6 +50,9 @@ FIXTURES = {
     "gl_pdb72_pareto": ("pdb72", None, None, 0, 500, 0, True, "all", 1.0, 1, 4, PARETO),
     # ... so the pareto setting itself runs on a synthetic corpus with more than 100 chains
     "gl_syn120_pareto": (120, 30, 60, 44, 500, 0, True, "all", 1.0, 1, 4, PARETO),
+    # rmsd_only (bpe.py:1977, 2027): glue_opt_all still runs, the merges neither write the
+    # medoid geometry nor re-optimise glues
+    "gl_all_p0_rmsd_only": (6, 12, 30, 41, 5, 0, False, "all", 0.0, 1, 12, {"rmsd_only": True}),
 }
 # BPE.tokenize (the RMSD mode's induce, bpe.py:1053-1140, with glue_opt "all") of these
 # training chains after the steps
@@ -112,21 +115,22 @@ def run_one(name):
     meta = {"name": name, "n_chains": nch, "len_lo": lo, "len_hi": hi, "seed": seed, "bins": {"1": B},
             "rmsd_partition_min_size": p, "rmsd_super_res": sup, "glue_opt_method": method,
             "glue_opt_prior": prior, "glue_opt_every": every, "num_partitions": {str(k): v for k, v in num_p.items()},
-            "max_num_strucs": maxs, "std_bonds": std, "rng_seed": 0, "calls": [], "raised": None,
+            "max_num_strucs": maxs, "std_bonds": std, "rmsd_only": extra.get("rmsd_only", False), "rng_seed": 0,
+            "calls": [], "raised": None,
             "generator": "tests/golden/make_glue_golden.py (reference: /root/reference foldingdiff/bpe.py, "
                          "run in the build container)"}
     arrays = dict(corpus)
     bpe = RB.BPE(structs, bins={1: B}, save_dir=tempfile.mkdtemp(prefix="geobpe_glue_golden_"),
                  rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(num_p), max_num_strucs=maxs,
                  res_init=True, std_bonds=std, glue_opt=True, glue_opt_prior=prior, glue_opt_every=every,
-                 glue_opt_method=method, seed=0)
+                 glue_opt_method=method, rmsd_only=extra.get("rmsd_only", False), seed=0)
     stage = "initialize"
     try:
         bpe.initialize()
         geometry(bpe, "init", arrays)
         meta["init_segmentation"] = segmentation(bpe)
         stage = "glue_opt_all"
-        if method == "all" and not extra:  # (the optimiser's own view: the small corpora only)
+        if method == "all" and not set(extra) - {"rmsd_only"}:  # (the optimiser's own view: the small corpora only)
             lbfgs_record(RB, bpe, meta, arrays)
         if method == "all":
             bpe.glue_opt_all()

@@ -70,7 +70,14 @@ FIXTURES = {
     # reference's memmap write of num_partitions[2] = 2 entries broadcasts that one medoid
     # (bpe.py:298-300); the run carries on with one size-2 partition
     "rm_p0_one_chain": (1, 30, 40, 34, 5, 0, False, 60, 20),
+    # rmsd_only (bpe.py:1977, 2027): a partitioned merge keeps its own geometry (no medoid
+    # written over it), so later keys see the chains' raw values
+    "rm_p0_rmsd_only": (10, 20, 40, 21, 5, 0, False, 60, 25),
+    "rm_p3_super_rmsd_only": (8, 15, 35, 22, 4, 3, True, 50, 20),
+    "rm_p0_b2_long_rmsd_only": (16, 12, 30, 25, 2, 0, False, 80, 120),
 }
+# further BPE(...) arguments of a fixture
+EXTRA = {n: {"rmsd_only": True} for n in FIXTURES if n.endswith("_rmsd_only")}
 # BPE.tokenize (bpe.py:1053-1140, the RMSD mode's induce) after the training calls, on: the
 # first three training chains, the first 60 % of chains 3 and 4 (values inside the trained
 # bins), and new synthetic chains (chains, len_lo, len_hi, seed) -- those usually hold a value
@@ -144,12 +151,13 @@ def run_one(name):
             "bins": {str(k): v for k, v in bins.items()},
             "rmsd_partition_min_size": p, "rmsd_super_res": sup, "max_num_strucs": maxs, "std_bonds": std,
             "num_partitions": {str(k): v for k, v in num_p.items()}, "rng_seed": 0, "calls": [],
+            "extra": EXTRA.get(name, {}),
             "raised": None, "generator": "tests/golden/make_rmsd_mode_golden.py (reference: /root/reference "
                                          "foldingdiff/bpe.py, run in the build container)"}
     arrays = dict(corpus)
     bpe = RB.BPE(structs, bins=bins, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_golden_"),
                  rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(num_p),
-                 max_num_strucs=maxs, res_init=True, std_bonds=std, seed=0)
+                 max_num_strucs=maxs, res_init=True, std_bonds=std, seed=0, **EXTRA.get(name, {}))
     try:
         bpe.initialize()
         geometry(bpe, "init", arrays)

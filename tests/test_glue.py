@@ -301,7 +301,7 @@ def run_and_compare(name, device=False):
               num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
               max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta["std_bonds"],
               glue_opt=True, glue_opt_prior=meta["glue_opt_prior"], glue_opt_every=meta["glue_opt_every"],
-              glue_opt_method=meta["glue_opt_method"], seed=meta["rng_seed"])
+              glue_opt_method=meta["glue_opt_method"], rmsd_only=meta.get("rmsd_only", False), seed=meta["rng_seed"])
     assert isinstance(bpe, RmsdBPE)
     popped = []
     inner = bpe._merge
@@ -402,9 +402,11 @@ def host_glue(monkeypatch):
     monkeypatch.setattr(glue, "optimize_chains", opt_chains)
 
 
-@pytest.mark.parametrize("name", NAMES)
+@pytest.mark.parametrize("name", NAMES + ["gl_all_p0_rmsd_only"])
 def test_rmsd_mode_glue_opt_host_logic_matches_reference(name, host_glue):
-    run_and_compare(name)
+    bpe = run_and_compare(name)
+    if bpe.rmsd_only:  # (glue_opt_all only: the merges re-optimise nothing, bpe.py:2027)
+        assert bpe.glue_calls == 1
 
 
 @pytest.mark.skipif(os.environ.get("GEOBPE_SLOW_TESTS") != "1", reason="~20 min on one CPU core (GEOBPE_SLOW_TESTS=1)")

@@ -55,7 +55,7 @@ def run_and_compare(name, device=True):
     bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()}, rmsd_partition_min_size=meta["rmsd_partition_min_size"],
               rmsd_super_res=meta["rmsd_super_res"], num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
               max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta.get("std_bonds", True),
-              seed=meta["rng_seed"])
+              seed=meta["rng_seed"], **meta.get("extra", {}))
     assert isinstance(bpe, RmsdBPE)
     if "init_tokens" not in meta:  # the reference raised in initialize()
         with pytest.raises(Exception) as ei:
@@ -149,7 +149,7 @@ def test_rmsd_mode_dispatch_and_scope():
     _, corpus, _ = _load(NAMES[0])
     assert isinstance(BPE(corpus, bins={1: 5}, res_init=True), RmsdBPE)  # the reference's default p = 4
     with pytest.raises(NotImplementedError):
-        BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=3, rmsd_only=True)
+        BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=3, compute_sec_structs=True)
     assert not isinstance(BPE.__new__(BPE, corpus, bins={1: 5}, res_init=True,
                                       rmsd_partition_min_size=float("inf")), RmsdBPE)
 
