@@ -106,7 +106,7 @@ int geobpe_run(geobpe_ctx *ctx, int64_t n_iters, int64_t *n_done);
 int geobpe_set_tail(geobpe_ctx *ctx, int64_t max_count);
 /* Middle regime (same results): once a merge's count is <= max_count, merges run as two
  * launches (select + the previous merge's place, then find) over the per-key posting lists
- * (0 = never; default 16384; environment GEOBPE_MID overrides at create).  Single rank. */
+ * (0 = never; default 49152; environment GEOBPE_MID overrides at create).  Single rank. */
 int geobpe_set_mid(geobpe_ctx *ctx, int64_t max_count);
 /* The merge list so far: 3 int64 per merge (new id, count, merges applied);
  * returns the number of merges (copies at most cap). */

@@ -103,7 +103,7 @@ struct geobpe_ctx {
   bool tail_ready = false;     // its arrays are allocated
   int64_t hold_us = 0;         // geobpe_set_hold: a k_hold launch before each batch of iterations
   // middle regime (mid.h): merges whose count is <= mid_thresh run as k_mid_sel + k_mid_find
-  int64_t mid_thresh = 16384;  // 0: never
+  int64_t mid_thresh = 49152;  // 0: never (C3 merges 11..1000: 16384 -> 29.2k, 32768 -> 30.7k, 49152 -> 31.0k, 65536 -> 30.8k, 98304 -> 29.2k merges/s)
   bool mid_on = false;         // switched (one way)
   bool place_mid = false;      // the pending place is k_mid_sel's (else k_place's)
   // the multi-rank exchange owned by the engine (geobpe_comm_*, geobpe_run_exchange)
@@ -453,13 +453,13 @@ int tail_alloc(geobpe_ctx* c) {
 // build with a global atomic per pair (k_kp_alloc / k_kp_fill).  GEOBPE_KP_ATOMIC=0 (A/B): a
 // stable radix sort of the (key, slot) pairs (kp_sort.hip) -> runs -> list space ->
 // placement; measured slower end to end at C3 (25.3k vs 28.6k merges/s)
-int tail_build_sorted(geobpe_ctx* c) {
-  Dev& D = c->D;
+// the sorted build's scratch: keys / slots in and out + the sort's own (reserved with the
+// regime arrays when that build is selected)
+int kp_sort_scratch(geobpe_ctx* c, int* end_bit_out, size_t* tb_out) {
   const int64_t n = c->R;
   if (n <= 0 || n >= INT32_MAX) return 1;
   int end_bit = 1;
-  while (end_bit < 31 && (1LL << end_bit) <= D.HC) end_bit++;
-  const int32_t none = (int32_t)((1LL << end_bit) - 1);  // (> every key id: sorts last)
+  while (end_bit < 31 && (1LL << end_bit) <= c->D.HC) end_bit++;
   size_t tb = 0;
   if (kp_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, c->stream) != hipSuccess) return 1;
   const int64_t need = 4 * n * 4 + (int64_t)tb + 1024;
@@ -473,6 +473,18 @@ int tail_build_sorted(geobpe_ctx* c) {
     if (hipMalloc(&c->kps, (size_t)need) != hipSuccess) return 1;
     c->kps_bytes = need;
   }
+  *end_bit_out = end_bit;
+  *tb_out = tb;
+  return 0;
+}
+
+int tail_build_sorted(geobpe_ctx* c) {
+  Dev& D = c->D;
+  const int64_t n = c->R;
+  int end_bit;
+  size_t tb;
+  if (kp_sort_scratch(c, &end_bit, &tb)) return 1;
+  const int32_t none = (int32_t)((1LL << end_bit) - 1);  // (> every key id: sorts last)
   int32_t* kin = reinterpret_cast<int32_t*>(c->kps);
   int32_t* vin = kin + n;
   int32_t* kout = vin + n;
@@ -562,6 +574,16 @@ int regime_reserve(geobpe_ctx* c) {
   if (c->distributed || (c->mid_thresh <= 0 && c->tail_thresh <= 0)) return 0;
   int rc;
   if ((rc = tail_alloc(c))) return rc;
+  int end_bit;
+  size_t tb;
+  if (!c->kp_atomic && kp_sort_scratch(c, &end_bit, &tb)) c->kp_atomic = true;  // (no scratch: the atomic build)
+  if (!c->kp_atomic) {  // one tiny sort now: the sort's code object loads here (~4.6 ms at first use), not at the switch
+    int32_t* k = reinterpret_cast<int32_t*>(c->kps);
+    size_t tb1 = 0;
+    kp_sort_pairs(nullptr, &tb1, nullptr, nullptr, nullptr, nullptr, 1, end_bit, c->stream);
+    if (tb1 + 64 <= (size_t)c->kps_bytes - 16 * 4)
+      kp_sort_pairs(k + 16, &tb1, k, k + 4, k + 8, k + 12, 1, end_bit, c->stream);
+  }
   return sync_state(c);
 }
 

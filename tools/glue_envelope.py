@@ -16,8 +16,11 @@ optimiser's inputs:
   threads    torch.set_num_threads(8) instead of 1 (summation order of torch's kernels)
   grad_s<k>  at EVERY evaluation the gradient the closure returns moved 1 float32 ulp up or
              down per element (random signs, seed k): another float32 gradient of the same
-             loss, as a different summation order or rounding point gives one -- the model of
-             an independent float32 implementation of the optimiser (such as the device's)
+             loss, as a different summation order or rounding point gives one
+  eval_s<k>  as grad_s<k>, and the loss value the closure returns moved 1 ulp too (random
+             sign): another float32 evaluation of loss AND gradient -- the model of an
+             independent float32 implementation of the optimiser (such as the device's),
+             whose loss feeds the strong-Wolfe line search's comparisons
 
 Recorded per (fixture, variant): after glue_opt_all, the glued geometry against the
 fixture's (the reference's): glues in another bin, their distance (rad), how many further
@@ -47,7 +50,8 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 
 FIXTURES = ["gl_all_p0", "gl_all_p0_prior", "gl_pdb72_readme", "gl_syn120_pareto"]
-VARIANTS = ["ref", "x0_up", "x0_dn", "tgt_up", "geo_up", "threads", "grad_s0", "grad_s1", "grad_s2"]
+VARIANTS = ["ref", "x0_up", "x0_dn", "tgt_up", "geo_up", "threads", "grad_s0", "grad_s1", "grad_s2",
+            "eval_s0", "eval_s1", "eval_s2"]
 GLUE_COLS = ["omega", "C:1N:1CA", "phi"]
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
@@ -62,9 +66,9 @@ def _dn(a):
     return np.nextafter(a, np.float32(-np.inf)).astype(np.float32)
 
 
-def optimize_grad_ulp(geo, x0, R_occs, t_occs, prior, lam, rng):
+def optimize_grad_ulp(geo, x0, R_occs, t_occs, prior, lam, rng, loss_too=False):
     """oracle.glue.optimize with every gradient the closure hands LBFGS moved 1 float32 ulp
-    (random direction per element)."""
+    (random direction per element); loss_too: the loss value it returns as well."""
     import torch
     from oracle import glue as og
     geo32 = torch.tensor(np.asarray(geo, dtype=np.float32))
@@ -87,6 +91,10 @@ def optimize_grad_ulp(geo, x0, R_occs, t_occs, prior, lam, rng):
         g2 = np.where(up, np.nextafter(g, np.float32(np.inf)), np.nextafter(g, np.float32(-np.inf))).astype(np.float32)
         raw.grad.copy_(torch.from_numpy(g2))
         losses.append(loss.item())
+        if loss_too:
+            lv = np.float32(loss.item())
+            lv = np.nextafter(lv, np.float32(np.inf if rng.random() < 0.5 else -np.inf)).astype(np.float32)
+            return torch.tensor(lv)
         return loss
 
     opt.step(closure)
@@ -97,11 +105,11 @@ def optimize_grad_ulp(geo, x0, R_occs, t_occs, prior, lam, rng):
 def perturbed_optimize(variant):
     """oracle.glue.optimize with the variant's input change."""
     from oracle import glue as og
-    rng = np.random.default_rng(int(variant[6:]) if variant.startswith("grad_s") else 0)
+    rng = np.random.default_rng(int(variant[6:]) if variant[:6] in ("grad_s", "eval_s") else 0)
 
     def opt(g, x0, R, t, prior=None, lam=0.0):
-        if variant.startswith("grad_s"):
-            return optimize_grad_ulp(g, x0, R, t, prior, lam, rng)
+        if variant[:6] in ("grad_s", "eval_s"):
+            return optimize_grad_ulp(g, x0, R, t, prior, lam, rng, loss_too=variant.startswith("eval_s"))
         if variant == "x0_up":
             x0 = _up(x0)
         elif variant == "x0_dn":
