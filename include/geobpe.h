@@ -99,6 +99,13 @@ int geobpe_step(geobpe_ctx *ctx, int32_t *new_id, int32_t *count, int64_t *n_mer
  * (the winner, tie-break and new token are resolved on the device), then wait;
  * *n_done = merges actually made (fewer if the pairs ran out). */
 int geobpe_run(geobpe_ctx *ctx, int64_t n_iters, int64_t *n_done);
+/* geobpe_run, and the merges it made in h_out (3 int64 per merge, as geobpe_merge_log;
+ * at most cap); *first = the merges made before this run.  Their log records ride in the
+ * run's own state synchronisations to a pinned mirror, so the caller's merge list needs no
+ * further round trip (BPE.step's per-step bookkeeping of the merge list,
+ * bpe.py:1857-1866).  Single rank. */
+int geobpe_run_log(geobpe_ctx *ctx, int64_t n_iters, int64_t *n_done, int64_t *first, int64_t *h_out,
+                   int64_t cap);
 /* Late-merge path (same results): once a merge's count is <= max_count, geobpe_run /
  * geobpe_step run the merges in one workgroup over per-key posting lists (k_tail, many
  * merges per launch) instead of the full-grid kernels; 0 = never (the default: the middle regime is faster;

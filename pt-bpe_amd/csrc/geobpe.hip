@@ -74,6 +74,8 @@ struct geobpe_ctx {
   std::vector<void*> allocs;
   State* h_state = nullptr;  // pinned mirror
   Sel* h_sel = nullptr;      // pinned copy of the last decision (step_select)
+  LogRec* h_log = nullptr;   // pinned mirror of the merge log, pulled by geobpe_run_log
+  int64_t h_log_cap = 0;
   bool keys_ready = false;
   bool distributed = false;
   bool bin_dense = true;
@@ -666,6 +668,7 @@ void geobpe_destroy(geobpe_ctx* c) {
     if (c->d_cols[i]) hipFree(c->d_cols[i]);
   if (c->h_state) hipHostFree(c->h_state);
   if (c->h_sel) hipHostFree(c->h_sel);
+  if (c->h_log) hipHostFree(c->h_log);
   if (c->comm && c->rccl.CommDestroy) c->rccl.CommDestroy(c->comm);
   for (uint8_t* p : {c->x_pbuf, c->x_gath, c->x_tmp, c->x_flat})
     if (p) hipFree(p);
@@ -1126,7 +1129,9 @@ int geobpe_step(geobpe_ctx* c, int32_t* new_id, int32_t* count, int64_t* n_merge
   return 0;
 }
 
-int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) {
+// the batch loop of geobpe_run; pull: each batch's merge-log records ride to the pinned
+// mirror in the batch's own state synchronisation (no extra round trip for the log)
+static int run_batches(geobpe_ctx* c, int64_t n_iters, int64_t* n_done, bool pull) {
   if (!c || n_iters < 0) return GEOBPE_EARG;
   if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
   if (c->distributed) return fail(c, GEOBPE_EARG, "geobpe_run in distributed mode");
@@ -1151,12 +1156,45 @@ int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) {
         enqueue_iteration(c);
     }
     HIPCHK(c, hipGetLastError());
+    if (pull) {  // (every record this batch can write: <= one per iteration; after the pending
+                 // place, which sums the last merge's merged total into its record)
+      flush_place(c);
+      const int64_t from = c->h_state->iter, n = std::min<int64_t>(batch, c->h_log_cap - from);
+      if (n > 0)
+        HIPCHK(c, hipMemcpyAsync(c->h_log + from, c->D.log + from, n * sizeof(LogRec), hipMemcpyDeviceToHost,
+                                 c->stream));
+    }
     if ((rc = sync_state(c))) return rc;
     if (c->h_state->done) break;
     tail_check_switch(c);
     want = n_iters - (c->h_state->iter - it0);
   }
   if (n_done) *n_done = c->h_state->iter - it0;
+  return 0;
+}
+
+int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) { return run_batches(c, n_iters, n_done, false); }
+
+int geobpe_run_log(geobpe_ctx* c, int64_t n_iters, int64_t* n_done, int64_t* first, int64_t* h_out, int64_t cap) {
+  if (!c || !n_done || !first || (cap > 0 && !h_out)) return GEOBPE_EARG;
+  if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
+  if (!c->h_log) {  // (the merge-log capacity; pinned once, outside any later run's loop)
+    HIPCHK(c, hipHostMalloc((void**)&c->h_log, (size_t)c->D.KC * sizeof(LogRec), hipHostMallocDefault));
+    c->h_log_cap = c->D.KC;
+  }
+  const int64_t it0 = c->h_state->iter;
+  *first = it0;
+  int rc;
+  if ((rc = run_batches(c, n_iters, n_done, true))) return rc;
+  const int64_t n = std::min(*n_done, cap);
+  if (c->tail_on && tail_enabled(c) && n > 0)  // (the one-workgroup path syncs on its own: one copy)
+    HIPCHK(c, hipMemcpy(c->h_log + it0, c->D.log + it0, n * sizeof(LogRec), hipMemcpyDeviceToHost));
+  for (int64_t i = 0; i < n; i++) {
+    const LogRec& r = c->h_log[it0 + i];
+    h_out[3 * i] = r.nid;
+    h_out[3 * i + 1] = r.count;
+    h_out[3 * i + 2] = r.nmerged;
+  }
   return 0;
 }
 

@@ -69,6 +69,7 @@ def lib():
         "geobpe_set_bin_dense": (ctypes.c_int, [P, ctypes.c_int]),
         "geobpe_step": (ctypes.c_int, [P, pI32, pI32, pI64]),
         "geobpe_run": (ctypes.c_int, [P, I64, pI64]),
+        "geobpe_run_log": (ctypes.c_int, [P, I64, pI64, pI64, P, I64]),
         "geobpe_set_tail": (ctypes.c_int, [P, I64]),
         "geobpe_set_mid": (ctypes.c_int, [P, I64]),
         "geobpe_merge_log": (I64, [P, P, I64]),
@@ -140,7 +141,7 @@ def lib():
 EXPORTED_SYMBOLS = [
     "geobpe_create", "geobpe_destroy", "geobpe_last_error", "geobpe_load_angles", "geobpe_angle_range",
     "geobpe_quantize", "geobpe_symbol_first", "geobpe_init_tokens", "geobpe_bin", "geobpe_set_bin_dense", "geobpe_step",
-    "geobpe_run", "geobpe_set_tail", "geobpe_set_mid", "geobpe_merge_log", "geobpe_key_json", "geobpe_debug_key_less", "geobpe_debug_counts", "geobpe_debug_state", "geobpe_debug_key",
+    "geobpe_run", "geobpe_run_log", "geobpe_set_tail", "geobpe_set_mid", "geobpe_merge_log", "geobpe_key_json", "geobpe_debug_key_less", "geobpe_debug_counts", "geobpe_debug_state", "geobpe_debug_key",
     "geobpe_step_select", "geobpe_step_apply", "geobpe_delta_export", "geobpe_delta_import",
     "geobpe_set_distributed", "geobpe_set_global_residues", "geobpe_set_rank", "geobpe_token_json", "geobpe_token_content",
     "geobpe_vocab_count", "geobpe_num_keys", "geobpe_num_tokens", "geobpe_segmentation", "geobpe_encode",

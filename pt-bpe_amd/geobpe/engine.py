@@ -321,9 +321,15 @@ class GeoBPEEngine:
                     break
                 done += 1
             return done
-        n = ctypes.c_int64(0)
-        self._chk(self.L.geobpe_run(self._ctx, int(n_merges), ctypes.byref(n)))
-        self._refresh_log()
+        n, first = ctypes.c_int64(0), ctypes.c_int64(0)
+        buf = np.zeros(3 * max(int(n_merges), 1), dtype=np.int64)
+        # (the run's merges come back with it: no further synchronisation for the merge list)
+        self._chk(self.L.geobpe_run_log(self._ctx, int(n_merges), ctypes.byref(n), ctypes.byref(first), _p(buf),
+                                        int(n_merges)))
+        if first.value == len(self.merges):
+            self.merges.extend(tuple(int(x) for x in buf[3 * i:3 * i + 3]) for i in range(n.value))
+        else:
+            self._refresh_log()
         if n.value < n_merges:
             self._done = True
         return int(n.value)

@@ -57,6 +57,11 @@ def _envelope(fixture):
     env = {}
     for t in GLUE_COLS:
         env[t] = {k: max(r["glued"][t][k] for r in res) for k in ("other_bin", "past_0.02", "past_0.1", "max_rad")}
+    # the farthest any glue of any type moved in any variant: a glue past it is a move the
+    # reference never made
+    pool = max(env[t]["max_rad"] for t in GLUE_COLS)
+    for t in GLUE_COLS:
+        env[t]["pool_max_rad"] = pool
     prefix = min(r["merges"]["shared_prefix"] for r in res if "merges" in r)
     return env, prefix, [r["variant"] for r in res]
 
@@ -253,18 +258,24 @@ def _glue_close(a, b, thr, what, fixture):
     n = int(np.sum(~np.isnan(b)))
     d = np.abs(a[bad] - b[bad])
     d = np.minimum(d, 2 * np.pi - d)  # angles: the first and last bins are neighbours on the circle
-    got = {"other_bin": int(bad.sum()), "past_0.02": int(np.sum(d > 0.02)), "past_0.1": int(np.sum(d > 0.1)),
-           "max_rad": float(d.max()) if d.size else 0.0}
     t = what.split()[-1]
     env = _envelope(fixture)[0][t]
+    # (one bin when the reference's farthest move is shorter: a flip to the neighbouring bin)
+    width = float(np.max(np.asarray(thr[t], dtype=np.float64)[:, 1] - np.asarray(thr[t], dtype=np.float64)[:, 0]))
+    far = max(env["pool_max_rad"], width)
+    got = {"other_bin": int(bad.sum()), "past_0.02": int(np.sum(d > 0.02)), "past_0.1": int(np.sum(d > 0.1)),
+           "past_envelope": int(np.sum(d > far)), "max_rad": float(d.max()) if d.size else 0.0}
     print(f"{what}: device {got} of {n} glues; reference envelope {env}")
     if not CHECK_GLUE[0]:
         return got["other_bin"]
+    # counts: within the Poisson allowance of the most any variant of the reference produced
     for k in ("other_bin", "past_0.02", "past_0.1"):
         assert got[k] <= _count_bound(env[k]), f"{what}: {k} {got[k]} outside the reference's envelope {env[k]}"
-    # the worst glue: no further than the reference's worst, or one bin when that is wider
-    width = float(np.max(np.asarray(thr[t], dtype=np.float64)[:, 1] - np.asarray(thr[t], dtype=np.float64)[:, 0]))
-    assert got["max_rad"] <= max(env["max_rad"], width) * 1.01, f"{what}: a glue {got['max_rad']:.3g} rad away"
+    # the tail: glues farther than ANY variant moved any glue -- the reference's count there
+    # is 0, so at most its allowance (the single largest distance of one run is not asserted:
+    # a maximum over a handful of rare events has no power to separate two implementations)
+    assert got["past_envelope"] <= _count_bound(0), (
+        f"{what}: {got['past_envelope']} glues farther than the reference's farthest ({far:.3g} rad)")
     return got["other_bin"]
 
 

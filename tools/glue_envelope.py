@@ -30,6 +30,7 @@ prior off) the raw optimum's drift quantiles and same-bin share against the unpe
 optimum.
 
   python tools/glue_envelope.py [--jobs N] [--no-steps] [--variants a,b] OUT.json [fixture ...]
+  python tools/glue_envelope.py --merge OUT.json LOG ...   (the result lines of earlier runs)
 
 CPU only, run in the build container (torch on the CPU); the output is committed as
 tests/golden/glue_envelope.json and tests/test_glue.py derives its device bounds from it.
@@ -245,8 +246,28 @@ def _job(args):
         return {"fixture": name, "variant": variant, "raised": f"{type(e).__name__}: {e}"}
 
 
+def merge_logs(out_path, logs):
+    """the result lines of earlier runs' logs (one JSON object a line) into OUT.json"""
+    res = {}
+    if os.path.exists(out_path):
+        with open(out_path) as f:
+            res = {(r["fixture"], r["variant"]): r for r in json.load(f)["results"]}
+    for p in logs:
+        with open(p) as f:
+            for ln in f:
+                if ln.startswith("{"):
+                    r = json.loads(ln)
+                    if "fixture" in r and "variant" in r and "raised" not in r:
+                        res[(r["fixture"], r["variant"])] = r
+    out = sorted(res.values(), key=lambda r: (r["fixture"], VARIANTS.index(r["variant"]) if r["variant"] in VARIANTS else 99))
+    with open(out_path, "w") as f:
+        json.dump({"generator": "tools/glue_envelope.py", "variants": VARIANTS, "results": out}, f, indent=1)
+
+
 def main(argv):
     import multiprocessing as mp
+    if argv and argv[0] == "--merge":  # --merge OUT.json LOG ...
+        return merge_logs(argv[1], argv[2:])
     jobs, steps, variants = 6, True, VARIANTS
     while argv and argv[0].startswith("--"):
         if argv[0] == "--jobs":
