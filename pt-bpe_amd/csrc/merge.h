@@ -968,9 +968,17 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   if (mine0) COMMIT_INSERT(r0);
   if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
   const int32_t nE = s_preE[nba], nF = s_preF[nba], nKO = S.nKO;
+  // (this thread's first extra record stays in registers for round 2: an owner with extras
+  // otherwise paid one more dependent global round trip there, ~3 us, on the kernel's tail)
+  KRec e0;
+  int64_t at0 = 0;
   for (int32_t i = t; i < nE + nKO; i += ABLOCK) {  // extras, then the overflow list
     const int64_t at = extra_at(D, s_preE, nba, j, PER, nE, i);
     const KRec k = D.KS[at];
+    if (i == t) {
+      e0 = k;
+      at0 = at;
+    }
     if (i < nE || owner_of_key(D, k.pkey) == j) COMMIT_INSERT(k);
   }
   for (int32_t i = t; i < nF; i += ABLOCK) {
@@ -1060,11 +1068,24 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   // and the log entries of its occurrence slots); the first PER records per finder
   // are still in registers
   commit_publish(D, S, mine0, r0, seg * SK + k0);
+  dbg_stamp(D, 53);
+  dbg_val(D, 54, nE);
+  dbg_val(D, 55, nKO);
   for (int32_t i0 = 0; i0 < nE + nKO; i0 += ABLOCK) {  // block-uniform
     const int32_t i = i0 + t;
-    const int64_t at = i < nE + nKO ? extra_at(D, s_preE, nba, j, PER, nE, i) : 0;
-    const KRec k = D.KS[at];
-    const bool mine = i < nE + nKO && (i < nE || owner_of_key(D, k.pkey) == j);
+    const bool in = i < nE + nKO;
+    KRec k;
+    int64_t at = 0;
+    if (i0 == 0) {  // (round 1's first iteration loaded exactly these)
+      if (in) {
+        k = e0;
+        at = at0;
+      }
+    } else if (in) {
+      at = extra_at(D, s_preE, nba, j, PER, nE, i);
+      k = D.KS[at];
+    }
+    const bool mine = in && (i < nE || owner_of_key(D, k.pkey) == j);
     commit_publish(D, S, mine, k, at);
   }
   dbg_stamp(D, 4);
