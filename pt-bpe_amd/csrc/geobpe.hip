@@ -1178,11 +1178,21 @@ int geobpe_run(geobpe_ctx* c, int64_t n_iters, int64_t* n_done) { return run_bat
 int geobpe_run_log(geobpe_ctx* c, int64_t n_iters, int64_t* n_done, int64_t* first, int64_t* h_out, int64_t cap) {
   if (!c || !n_done || !first || (cap > 0 && !h_out)) return GEOBPE_EARG;
   if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
-  if (!c->h_log) {  // (the merge-log capacity; pinned once, outside any later run's loop)
-    HIPCHK(c, hipHostMalloc((void**)&c->h_log, (size_t)c->D.KC * sizeof(LogRec), hipHostMallocDefault));
-    c->h_log_cap = c->D.KC;
-  }
   const int64_t it0 = c->h_state->iter;
+  // the pinned mirror covers every record this run can write (grown by doubling, at most the
+  // log's capacity): a run of K merges from merge it0 needs it0 + K + 1
+  const int64_t need = std::min<int64_t>(c->D.KC, it0 + n_iters + 1);
+  if (need > c->h_log_cap) {
+    const int64_t cap = std::min<int64_t>(c->D.KC, std::max<int64_t>({need, 2 * c->h_log_cap, 4096}));
+    LogRec* p = nullptr;
+    HIPCHK(c, hipHostMalloc((void**)&p, (size_t)cap * sizeof(LogRec), hipHostMallocDefault));
+    if (c->h_log) {
+      memcpy(p, c->h_log, (size_t)c->h_log_cap * sizeof(LogRec));
+      hipHostFree(c->h_log);
+    }
+    c->h_log = p;
+    c->h_log_cap = cap;
+  }
   *first = it0;
   int rc;
   if ((rc = run_batches(c, n_iters, n_done, true))) return rc;
