@@ -103,6 +103,30 @@ def _prior(meta, arrs):
     return [(c[t], w[t]) for t in range(3)], float(meta["glue_opt_prior"])
 
 
+def test_glue_close_uses_the_envelope():
+    """The device-vs-reference glue criterion (_glue_close) on synthetic columns against the
+    committed pareto envelope: the reference itself passes; a column with more glues past
+    0.02 rad than the Poisson allowance of the variants' largest count fails; three glues
+    farther than any variant's farthest move fail, two pass."""
+    env = _envelope("gl_syn120_pareto")[0]
+    thr = {t: [(i * 0.0125, (i + 1) * 0.0125) for i in range(503)] for t in GLUE_COLS}
+    rng = np.random.default_rng(0)
+    b = rng.uniform(0, 6.28, 5000)
+    assert _glue_close(b.copy(), b, thr, "glued geometry phi", "gl_syn120_pareto") == 0
+    a = b.copy()
+    n = int(_count_bound(env["phi"]["past_0.02"])) + 1
+    a[:n] += 0.03
+    with pytest.raises(AssertionError, match="past_0.02"):
+        _glue_close(a, b, thr, "glued geometry phi", "gl_syn120_pareto")
+    far = env["phi"]["pool_max_rad"] + 0.01
+    a = b.copy()
+    a[:2] += far
+    _glue_close(a, b, thr, "glued geometry phi", "gl_syn120_pareto")
+    a[2] += far
+    with pytest.raises(AssertionError, match="farther than"):
+        _glue_close(a, b, thr, "glued geometry phi", "gl_syn120_pareto")
+
+
 @pytest.mark.parametrize("name", NAMES)
 def test_oracle_matches_reference_optimum(name):
     from oracle import glue as og
