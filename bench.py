@@ -102,12 +102,16 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
     ap.add_argument("--no-replay", action="store_true", help="skip the profiled replay (per-kernel table)")
     ap.add_argument("--roofline-kernel", default="auto", help="auto: the slowest merge-loop kernel")
-    ap.add_argument("--event-stride", type=int, default=8,
+    ap.add_argument("--event-stride", type=int, default=0,
                     help="time every k-th launch of the merge-loop kernels in the timed region (event records "
-                         "are host work: at stride 1 the host, not the GPU, sets the pace)")
+                         "are host work: at stride 1 the host, not the GPU, sets the pace); 0 = auto: "
+                         "max(8, steps // 32), about 32 samples per kernel at most")
     ap.add_argument("--emit-merges", action="store_true",
                     help="add the merge list ([key string, count] of every merge so far) to the JSON line")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.event_stride <= 0:  # (each sampled launch costs the timed region a few us of event packets)
+        args.event_stride = max(8, args.steps // 32)
+    return args
 
 
 def _free_port() -> int:
