@@ -254,6 +254,8 @@ struct Dev {
   int4* TM;       // merged occurrences {a, ya, b, c}
   int2* TH;       // new pairs {slot, key} (mid.h: two buffers of THcap, by launch parity)
   int4* mcnt;     // mid.h: per find workgroup {TM count, TH count, merged, -} by parity [2][NBA_MAX]
+  int32_t* mbk;   // mid.h: per find workgroup, its TH segment's runs by appending workgroup
+                  // (bucket k at [mbk[k], mbk[k + 1])), by parity [2][NBA_MAX][MID_APP + 1]
   int4* TS;       // posting entries past a list's capacity {key, position, slot}
   int32_t* TR;    // keys whose list is regrown
   NewPair* TK;    // keys found (not claimed): EHASH check

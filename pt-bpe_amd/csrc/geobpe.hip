@@ -442,7 +442,8 @@ int tail_alloc(geobpe_ctx* c) {
   // (zero: a key claimed after the list build starts with an empty list of capacity 0; the
   // key-indexed arrays outlive a collapse, the residue-sized ones are made again for it)
   if (!D.kp_off && ((rc = dalloc(c, &D.kp_off, D.HC, 0)) || (rc = dalloc(c, &D.kp_n, D.HC, 0)) ||
-                    (rc = dalloc(c, &D.kp_cap, D.HC, 0)) || (rc = dalloc(c, &D.mcnt, 2 * NBA_MAX, 0))))
+                    (rc = dalloc(c, &D.kp_cap, D.HC, 0)) || (rc = dalloc(c, &D.mcnt, 2 * NBA_MAX, 0)) ||
+                    (rc = dalloc(c, &D.mbk, 2 * NBA_MAX * (MID_APP + 1), 0))))
     return rc;
   if ((rc = dalloc(c, &D.kpool, D.KPOOL, 0xFF)) || (rc = dalloc(c, &D.TM, D.TMcap)) || (rc = dalloc(c, &D.TH, 2 * D.THcap)) ||
       (rc = dalloc(c, &D.TS, D.THcap)) || (rc = dalloc(c, &D.TR, D.THcap)) || (rc = dalloc(c, &D.TK, D.THcap)))

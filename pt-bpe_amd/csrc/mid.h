@@ -56,10 +56,12 @@ struct MidFindLds {
   int4 tm[MTM];
   int2 th[MTH];
   int32_t kl[MKL];
+  int32_t bcnt[MID_APP + 1];  // the new pairs per appending workgroup, then their runs' starts
   int32_t red[ABLOCK / 64];
   int32_t nocc, nm, chk, ntm, nth, nkl;
   int64_t xbase, bk;
 };
+static_assert(MTH <= 2 * ABLOCK, "mid_flush_lists: two new pairs per thread");
 
 constexpr int MAE = 6144;  // appends: this bucket's entries kept from pass 1 (LDS)
 static_assert(MPK <= 2048, "an append entry packs its key slot in 11 bits");
@@ -69,7 +71,8 @@ struct MidAppLds {
   int32_t occ[MPK];
   int2 ent[MAE];  // this bucket's new pairs {slot, key}, then {slot, key slot << 21 | rank (as uint32)}
   int32_t big_old[TAIL_BIG], big_new[TAIL_BIG], big_pre[TAIL_BIG + 1];
-  int32_t pre[NBA_MAX + 1];  // prefix of the find workgroups' TH segment counts
+  int32_t pre[NBA_MAX + 1];  // prefix of this bucket's run lengths over the find workgroups' TH segments
+  int32_t rb[NBA_MAX];       // this bucket's run start in each segment
   int32_t red[ABLOCK / 64];
   int32_t nocc, nbig, full, nent;
   int64_t pbase;
@@ -81,6 +84,11 @@ struct MidCtx {
   u64 w1, w2;
   u64 pa1, pb1, pa2, pb2;
 };
+
+// the appending workgroup (of A) that takes key d's posting entries
+__device__ inline uint32_t mid_bucket(int32_t d, int32_t A) {
+  return (uint32_t)(((u64)((uint32_t)d * 2654435761u) * (u64)A) >> 32);
+}
 
 // one LDS slot per active lane, one LDS atomic per wave instruction
 __device__ inline int32_t lds_reserve(int32_t* n) {
@@ -160,8 +168,36 @@ __device__ inline void mid_flush_lists(const Dev& D, MidFindLds& S, int par, int
   }
   int4* tm = D.TM + (int64_t)w * MTM;
   for (int32_t i = t; i < a; i += ABLOCK) tm[i] = S.tm[i];
+  // the new pairs grouped by the appending workgroup that takes them (the hash bucket of the
+  // key, mid_bucket): bucket k's run is [bcnt[k], bcnt[k + 1]) of the segment, so an appender
+  // reads its own runs only (round 3: every appender read every new pair, ~16 MB a launch at
+  // 30 k occurrences, and the appenders set the launch's length above ~10 k occurrences)
   int2* th = mid_th(D, par) + (int64_t)w * MTH;
-  for (int32_t i = t; i < b; i += ABLOCK) th[i] = S.th[i];
+  if (t <= MID_APP) S.bcnt[t] = 0;
+  __syncthreads();
+  int32_t k0 = 0, k1 = 0, r0 = -1, r1 = -1;
+  if (t < b) {
+    k0 = (int32_t)mid_bucket(max(S.th[t].y, 0), MID_APP);
+    r0 = atomicAdd(&S.bcnt[k0], 1);
+  }
+  if (t + ABLOCK < b) {
+    k1 = (int32_t)mid_bucket(max(S.th[t + ABLOCK].y, 0), MID_APP);
+    r1 = atomicAdd(&S.bcnt[k1], 1);
+  }
+  __syncthreads();
+  if (t == 0) {
+    int32_t run = 0;
+    for (int k = 0; k < MID_APP; k++) {
+      const int32_t n = S.bcnt[k];
+      S.bcnt[k] = run;
+      run += n;
+    }
+    S.bcnt[MID_APP] = run;
+  }
+  __syncthreads();
+  if (t <= MID_APP) D.mbk[((int64_t)par * NBA_MAX + w) * (MID_APP + 1) + t] = S.bcnt[t];
+  if (r0 >= 0) th[S.bcnt[k0] + r0] = S.th[t];
+  if (r1 >= 0) th[S.bcnt[k1] + r1] = S.th[t + ABLOCK];
   if (c) {
     __syncthreads();
     for (int32_t i = t; i < c; i += ABLOCK) klist_put(D, S.bk + i, S.kl[i]);
@@ -599,9 +635,6 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
 }
 
 // ---------------------------------------------------------------------- appends
-__device__ inline uint32_t mid_bucket(int32_t d, int32_t A) {
-  return (uint32_t)(((u64)((uint32_t)d * 2654435761u) * (u64)A) >> 32);
-}
 
 // the key's slot in the append table (insert: claim an empty one); -1: not there / full
 __device__ inline int32_t mpk_slot(MidAppLds& S, int32_t d, bool insert, bool* ins) {
@@ -665,24 +698,22 @@ template <int PASS>
 __device__ __attribute__((always_inline)) inline void mid_app_pass(const Dev& D, MidAppLds& S, int32_t pp,
                                                                    int32_t skip, int32_t b, int32_t A) {
   const int2* th = mid_th(D, pp);
-  const int32_t NS = mid_G(D), t = threadIdx.x, lane = t & 63;
-  constexpr int NWV = ABLOCK / 64;
-  for (int32_t s0 = t >> 6; s0 < NS; s0 += NWV * MP_UNR) {  // (wave-uniform)
-    int32_t n[MP_UNR], nmax = 0;
+  const int32_t NS = mid_G(D), t = threadIdx.x;
+  const int32_t tot = S.pre[NS];  // (this bucket's runs of every segment, flattened)
+  for (int32_t q0 = t; q0 < tot; q0 += MP_UNR * ABLOCK) {
+    int2 h[MP_UNR];
 #pragma unroll
     for (int u = 0; u < MP_UNR; u++) {
-      const int32_t sg = s0 + u * NWV;
-      n[u] = sg < NS ? S.pre[sg] : 0;
-      nmax = max(nmax, n[u]);
+      const int32_t q = q0 + u * ABLOCK;
+      if (q < tot) {
+        const int32_t w = seg_of(S.pre, NS, q);
+        h[u] = th[(int64_t)w * MTH + S.rb[w] + (q - S.pre[w])];
+      } else {
+        h[u] = make_int2(-1, -1);
+      }
     }
-    for (int32_t c = lane; c < nmax; c += 64) {
-      int2 h[MP_UNR];
 #pragma unroll
-      for (int u = 0; u < MP_UNR; u++)
-        h[u] = c < n[u] ? th[(int64_t)(s0 + u * NWV) * MTH + c] : make_int2(-1, -1);
-#pragma unroll
-      for (int u = 0; u < MP_UNR; u++) mid_app_one<PASS>(D, S, h[u], skip, b, A);
-    }
+    for (int u = 0; u < MP_UNR; u++) mid_app_one<PASS>(D, S, h[u], skip, b, A);
   }
   const int64_t nsp = min(D.st->mid_nh[pp], D.THcap - MSEG_TH);
   const int2* sp = th + MSEG_TH;
@@ -699,13 +730,31 @@ __device__ __attribute__((always_inline)) inline void mid_append_body(const Dev&
   State* st = D.st;
   const int32_t t = threadIdx.x;
   dbg_stamp(D, 30);
+  if (A != MID_APP) {  // (the segments' runs are by MID_APP buckets: any other split rebuilds the lists)
+    if (t == 0) st->kp_valid = 0;
+    return;
+  }
   for (int i = t; i < MPK; i += ABLOCK) {
     S.key[i] = -1;
     S.cnt[i] = 0;
     S.cur[i] = 0;
   }
   if (t == 0) S.nocc = S.nbig = S.full = S.nent = 0;
-  if (t < mid_G(D)) S.pre[t] = min(D.mcnt[pp * NBA_MAX + t].y, MTH);  // (the segment counts)
+  {  // this bucket's run in every find workgroup's TH segment (mid_flush_lists grouped them)
+    const int32_t NS = mid_G(D);
+    int32_t len = 0;
+    if (t < NS && b <= MID_APP - 1) {
+      const int32_t cnt = min(D.mcnt[pp * NBA_MAX + t].y, MTH);
+      const int32_t* bo = D.mbk + ((int64_t)pp * NBA_MAX + t) * (MID_APP + 1);
+      const int32_t o0 = min(max(bo[b], 0), cnt), o1 = min(max(bo[b + 1], o0), cnt);
+      S.rb[t] = o0;
+      len = o1 - o0;
+    }
+    int32_t tot;
+    const int32_t ex = block_excl_scan(len, &tot, S.red);
+    if (t < NS) S.pre[t] = ex;
+    if (t == 0) S.pre[NS] = tot;
+  }
   __syncthreads();
   // ---- pass 1: this bucket's new pairs compacted into LDS, then counted per key (dense)
   mid_app_pass<0>(D, S, pp, skip, b, A);
