@@ -428,6 +428,31 @@ __device__ inline int32_t mkc_slot(MidFindLds& S, const MidHalf& h, bool* ins) {
   return -1;
 }
 
+// _tokens[n] = json.loads(key) (the new token's content in vsym) and the state the next select
+// reads -- by appending workgroup 0 (it starts with nothing to wait for; on find workgroup 0
+// these two dependent round trips delayed that workgroup's walk, the launch's last to end)
+__device__ inline void mid_new_token(const Dev& D, const Sel& sel) {
+  State* st = D.st;
+  const int32_t t = threadIdx.x;
+  const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
+  const int64_t vL = D.voff[L], vR = D.voff[Rr];
+  const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
+  const int64_t pos = D.voff[sel.nid], ln = nL + 1 + nR;
+  if (pos + ln > D.VSC) {
+    if (t == 0) set_error(D, GEOBPE_ECAPACITY, -9);
+  } else {
+    for (int64_t i = t; i < ln; i += ABLOCK)
+      D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
+    if (t == 0) D.voff[sel.nid + 1] = pos + ln;
+  }
+  if (t == 0) {
+    st->iter = sel.iter + 1;
+    st->K = sel.nid + 1;
+    st->maxc = sel.maxc;
+    st->ncand = sel.ncand;
+  }
+}
+
 // find workgroup w of G (merge parity par, decision sel)
 __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w,
                                                                     int32_t G, MidFindLds& S) {
@@ -479,25 +504,9 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
   const int2* segp = thp + (int64_t)w * MTH;
   const int2* spp = thp + MSEG_TH + s0;
   const int64_t ncand = nl + nsg + ns;
-  if (w == 0) {  // _tokens[n] = json.loads(key); state the next select reads
-    const int32_t L = sel.widL, g = sel.wg, Rr = sel.widR;
-    const int64_t vL = D.voff[L], vR = D.voff[Rr];
-    const int64_t nL = D.voff[L + 1] - vL, nR = D.voff[Rr + 1] - vR;
-    const int64_t pos = D.voff[F.nid], ln = nL + 1 + nR;
-    if (pos + ln > D.VSC) {
-      if (t == 0) set_error(D, GEOBPE_ECAPACITY, -9);
-    } else {
-      for (int64_t i = t; i < ln; i += ABLOCK)
-        D.vsym[pos + i] = i < nL ? D.vsym[vL + i] : (i == nL ? g : D.vsym[vR + i - nL - 1]);
-      if (t == 0) D.voff[F.nid + 1] = pos + ln;
-    }
-    if (t == 0) {
-      st->iter = sel.iter + 1;
-      st->K = sel.nid + 1;
-      st->maxc = sel.maxc;
-      st->ncand = sel.ncand;
-    }
-  }
+  // (round 0's list candidate of this thread, loaded beside the hash powers: both depend only
+  // on the Sel record, and the barrier below waits for every outstanding load anyway)
+  const int32_t g0 = t < nl ? D.kpool[offW + t] : -1;
   for (int i = t; i < MKC; i += ABLOCK) {
     S.key[i] = 0;
     S.cnt[i] = 0;
@@ -520,7 +529,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     if (i < ncand) {
       int32_t g = -1;
       if (i < nl) {
-        g = D.kpool[offW + i];
+        g = c0 == 0 ? g0 : D.kpool[offW + i];
       } else {
         const int2 e = i < nl + nsg ? segp[i - nl] : spp[i - nl - nsg];
         if (e.y == F.W) g = e.x;
@@ -886,6 +895,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int 
     mid_find_body(D, sel, par, blockIdx.x, G, U.f);
     return;
   }
+  if ((int)blockIdx.x == G && sel.decision == SEL_MERGE) mid_new_token(D, sel);
   const int32_t pp = st->place_par_prev;
   if (pp < 0 || !valid) return;
   const int32_t skip = sel.decision == SEL_MERGE ? sel.W : -1;
