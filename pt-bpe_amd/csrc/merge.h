@@ -967,6 +967,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const bool mine0 = lane_ok && k0 < min(cK, SK);
   if (mine0) COMMIT_INSERT(r0);
   if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
+  dbg_stamp(D, 56);
   const int32_t nE = s_preE[nba], nF = s_preF[nba], nKO = S.nKO;
   // (this thread's first extra record stays in registers for round 2: an owner with extras
   // otherwise paid one more dependent global round trip there, ~3 us, on the kernel's tail)
@@ -981,11 +982,14 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     }
     if (i < nE || owner_of_key(D, k.pkey) == j) COMMIT_INSERT(k);
   }
+  dbg_stamp(D, 57);
+  dbg_val(D, 59, nF);
   for (int32_t i = t; i < nF; i += ABLOCK) {
     const int32_t ww = seg_of(s_preF, nba, i);
     const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
     if (!agg_stage(S.u.agg, x.x, x.y)) commit_add(D, x.x, x.y, tod);
   }
+  dbg_stamp(D, 58);
   __syncthreads();
   dbg_stamp(D, 2);
   if (D.dbg) {  // (debug timeline: this owner's work, block-uniform)

@@ -21,7 +21,7 @@ L = _native.lib()
 names = {0: "C.start", 1: "C.init", 2: "C.records", 3: "C.resolved", 4: "C.published", 5: "C.flush+klist", 6: "C.end",
          10: "F.start", 11: "F.setup", 14: "F.r0.queued", 15: "F.r0.walked", 16: "F.r0.grouped", 12: "F.walked",
          13: "F.end", 40: "F.w.T1", 41: "F.w.T2", 42: "F.w.T3", 43: "F.w.emitted", 44: "F.w.hashed", 30: "P.start", 31: "P.tokens", 32: "P.slots", 33: "P.end",
-         50: "C.i.loaded", 51: "C.i.zeroed", 53: "C.published0", 20: "S.start", 21: "S.scanned", 22: "S.max", 23: "S.ties", 24: "S.staged", 25: "S.tourn", 26: "S.end"}
+         50: "C.i.loaded", 51: "C.i.zeroed", 53: "C.published0", 56: "C.r.first", 57: "C.r.extras", 58: "C.r.decs", 20: "S.start", 21: "S.scanned", 22: "S.max", 23: "S.ties", 24: "S.staged", 25: "S.tourn", 26: "S.end"}
 done = 0
 for it in iters:
     eng.run(it - done - 1)
@@ -36,8 +36,9 @@ for it in iters:
     if len(t) == 0:
         print(f"merge {it}: (no stamps)")
         continue
-    vals = {7: "C.records(n)", 8: "C.decrements(n)", 9: "C.keys(n)", 54: "C.extras(n)", 55: "C.overflow(n)"}
-    vv = t[:, [7, 8, 9, 54, 55]].copy()
+    vals = {7: "C.records(n)", 8: "C.decrements(n)", 9: "C.keys(n)", 54: "C.extras(n)", 55: "C.overflow(n)",
+            59: "C.dec_extras(n)"}
+    vv = t[:, [7, 8, 9, 54, 55, 59]].copy()
     for k, nm in vals.items():  # values, not times
         v = t[:, k][t[:, k] > 0]
         if len(v):
@@ -54,9 +55,10 @@ for it in iters:
         print(f"  {names.get(k, str(k)):14s} min {np.nanmin(col):8.1f}  med {np.nanmedian(col):8.1f}  max {np.nanmax(col):8.1f}")
     if not np.all(np.isnan(rel[:, 6])):  # the slowest commit workgroups and their work
         order = np.argsort(-np.nan_to_num(rel[:, 6], nan=-1e9))[:6]
-        print("  slowest commit workgroups: wg  init  records  resolved  pub0  published  end | krec  drec  keys  extras  ovf")
+        print("  slowest commit workgroups: wg  init  r.first r.extras r.decs records  resolved  pub0  published  end"
+              " | krec  drec  keys  extras  ovf  dec_extras")
         for w in order:
-            print(f"    {w:4d} " + " ".join(f"{rel[w, k]:7.1f}" for k in (1, 2, 3, 53, 4, 6))
-                  + f" | {vv[w, 0]:5d} {vv[w, 1]:5d} {vv[w, 2]:5d} {vv[w, 3]:5d} {vv[w, 4]:5d}")
+            print(f"    {w:4d} " + " ".join(f"{rel[w, k]:7.1f}" for k in (1, 56, 57, 58, 2, 3, 53, 4, 6))
+                  + f" | {vv[w, 0]:5d} {vv[w, 1]:5d} {vv[w, 2]:5d} {vv[w, 3]:5d} {vv[w, 4]:5d} {vv[w, 5]:5d}")
         print(f"  median work: krec {int(np.median(vv[:, 0]))} drec {int(np.median(vv[:, 1]))} keys {int(np.median(vv[:, 2]))}")
 eng.close()
