@@ -909,40 +909,84 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
   State* st = D.st;
   const int32_t t = threadIdx.x;
   dbg_stamp(D, 36);
-  if (b < D.NBA) {  // (then consumed: the next find writes region b afresh)
-    check_found(D, b);
-    __syncthreads();
+  // The loads go out in three rounds, each depending only on the one before: (1) the check's
+  // record count and the merge's parity; (2) this thread's check record, the Sel record, the
+  // segment counts; (3) the check key's hashes and this thread's first merged occurrence and
+  // new pair.  (Round 3's version ran the EHASH check's three dependent rounds, a barrier and
+  // then the place's own three: this launch's place workgroups set its length.)
+  const bool chk = b < D.NBA;  // (then consumed: the next find writes region b afresh)
+  const int32_t nchk = chk ? min(D.chkcnt[b], (int32_t)D.RC) : 0;
+  const int32_t par = st->place_par;
+  const NewPair* reg = D.chk + (int64_t)b * D.RC;
+  NewPair c0;
+  const bool hc = t < nchk;
+  if (hc) c0 = reg[t];
+  const int32_t G = mid_G(D);
+  Sel sel;
+  sel.decision = SEL_STALL;
+  int4 mc = make_int4(0, 0, 0, 0);
+  int64_t nms = 0, nhs = 0;
+  int32_t v0 = 0;  // (workgroup 0: the find workgroups' merged counts, summed below)
+  if (par >= 0) {
+    sel = D.sel[par];
+    if (b < G) mc = D.mcnt[par * NBA_MAX + b];
+    nms = min(st->mid_nm[par], D.TMcap - MSEG_TM);
+    nhs = min(st->mid_nh[par], D.THcap - MSEG_TH);
+    if (b == 0 && t < G) v0 = D.mcnt[par * NBA_MAX + t].z;
+  }
+  const bool go = par >= 0 && sel.decision == SEL_MERGE;  // (block-uniform)
+  // find workgroup b's segments (b < G), share b of the spill lists
+  const int4* tms = D.TM + (int64_t)b * MTM;
+  const int2* th = mid_th(D, par >= 0 ? par : 0);
+  const int2* ths = th + (int64_t)b * MTH;
+  int64_t m0 = 0, nm = 0, h0 = 0, nh = 0;
+  const int32_t sm = min(mc.x, MTM), sh = min(mc.y, MTH);
+  int4 e = make_int4(0, 0, 0, 0);
+  int2 h = make_int2(0, 0);
+  if (go) {
+    m0 = nms * b / P;
+    nm = sm + (nms * (b + 1) / P - m0);
+    h0 = nhs * b / P;
+    nh = sh + (nhs * (b + 1) / P - h0);
+    if (t < nm) e = t < sm ? tms[t] : D.TM[MSEG_TM + m0 + t - sm];
+    if (t < nh) h = t < sh ? ths[t] : th[MSEG_TH + h0 + t - sh];
+  }
+  u64 kh1 = 0, kh2 = 0;
+  int32_t kln = 0;
+  if (hc) {
+    kh1 = D.kh1[c0.target];
+    kh2 = D.kh2[c0.target];
+    kln = D.klen[c0.target];
+  }
+  const int32_t nid = sel.nid;
+  auto place_tm = [&](const int4& x) {  // a merged occurrence's token rewrites
+    *reinterpret_cast<int2*>(D.tok + x.x) = make_int2(nid, x.y);
+    D.tok[x.z] = make_int4(-1, 0, -1, -1);
+    if (x.w >= 0)
+      *tok_f(D, x.w, 2) = x.x;
+    else
+      *tok_f(D, x.x, 3) = -1;
+  };
+  if (t < nm) place_tm(e);
+  if (t < nh) *tok_f(D, h.x, 3) = h.y;
+  if (hc && (kh1 != c0.h1 || kh2 != c0.h2 || kln != c0.len)) set_error(D, GEOBPE_EHASH, t);
+  for (int64_t i = t + ABLOCK; i < nm; i += ABLOCK) place_tm(i < sm ? tms[i] : D.TM[MSEG_TM + m0 + i - sm]);
+  for (int64_t i = t + ABLOCK; i < nh; i += ABLOCK) {
+    const int2 x = i < sh ? ths[i] : th[MSEG_TH + h0 + i - sh];
+    *tok_f(D, x.x, 3) = x.y;
+  }
+  for (int32_t i = t + ABLOCK; i < nchk; i += ABLOCK) {
+    const NewPair x = reg[i];
+    const int32_t d = x.target;
+    if (D.kh1[d] != x.h1 || D.kh2[d] != x.h2 || D.klen[d] != x.len) set_error(D, GEOBPE_EHASH, i);
+  }
+  if (chk) {
+    __syncthreads();  // (every thread has read the count)
     if (t == 0) D.chkcnt[b] = 0;
   }
-  const int32_t par = st->place_par;
-  if (par < 0) return;
-  const Sel sel = D.sel[par];
-  if (sel.decision != SEL_MERGE) return;
-  // find workgroup b's segments (b < G), share b of the spill lists
-  const int32_t G = mid_G(D);
-  const int4 mc = b < G ? D.mcnt[par * NBA_MAX + b] : make_int4(0, 0, 0, 0);
-  const int64_t nms = min(st->mid_nm[par], D.TMcap - MSEG_TM), nhs = min(st->mid_nh[par], D.THcap - MSEG_TH);
-  const int4* tms = D.TM + (int64_t)b * MTM;
-  const int64_t m0 = nms * b / P, nm = min(mc.x, MTM) + (nms * (b + 1) / P - m0);
-  for (int64_t i = t; i < nm; i += ABLOCK) {
-    const int4 e = i < min(mc.x, MTM) ? tms[i] : D.TM[MSEG_TM + m0 + i - min(mc.x, MTM)];
-    *reinterpret_cast<int2*>(D.tok + e.x) = make_int2(sel.nid, e.y);
-    D.tok[e.z] = make_int4(-1, 0, -1, -1);
-    if (e.w >= 0)
-      *tok_f(D, e.w, 2) = e.x;
-    else
-      *tok_f(D, e.x, 3) = -1;
-  }
-  const int2* th = mid_th(D, par);
-  const int2* ths = th + (int64_t)b * MTH;
-  const int64_t h0 = nhs * b / P, nh = min(mc.y, MTH) + (nhs * (b + 1) / P - h0);
-  for (int64_t i = t; i < nh; i += ABLOCK) {
-    const int2 h = i < min(mc.y, MTH) ? ths[i] : th[MSEG_TH + h0 + i - min(mc.y, MTH)];
-    *tok_f(D, h.x, 3) = h.y;
-  }
-  if (b == 0) {  // the merge's merged occurrences: the find workgroups' counts, summed
-    int32_t v = 0;
-    for (int32_t i = t; i < G; i += ABLOCK) v += D.mcnt[par * NBA_MAX + i].z;
+  if (go && b == 0) {  // the merge's merged occurrences: the find workgroups' counts, summed
+    int32_t v = v0;
+    for (int32_t i = t + ABLOCK; i < G; i += ABLOCK) v += D.mcnt[par * NBA_MAX + i].z;
     __shared__ int32_t s_red[ABLOCK / 64];
     int32_t tot;
     block_excl_scan(v, &tot, s_red);
