@@ -1193,13 +1193,20 @@ __device__ inline void place_record(const Dev& D, const PlaceLds& S, int32_t j, 
 // values (the pipelined exchange may run it again behind a stall).
 __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   State* st = D.st;
+  const int32_t t = threadIdx.x;
+  // first round: what depends on nothing -- the merge's parity, this region's merge-entry count
+  // and (speculatively) its first entry per thread, the record counts finder j sent each owner
+  // (round 3's version loaded them after the Sel record: two more dependent rounds on the
+  // select launch's critical path)
   const int32_t par = st->place_par;
+  const int32_t nA = D.Lcnt[j];
+  const LEntry eA = D.L[(int64_t)j * D.LC + min((int64_t)t, D.LC - 1)];
+  const int32_t cK = t < D.NBA ? D.cntK[(int64_t)t * D.NBA + j] : 0;
   if (par < 0) return;
   const Sel sel = D.sel[par];
   if (sel.decision != SEL_MERGE) return;
   dbg_stamp(D, 30);
   const int32_t nid = sel.nid;
-  const int32_t nA = D.Lcnt[j];
   const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
   const int64_t oper = (novf + D.NBA - 1) / D.NBA;
   const int64_t o_lo = (int64_t)j * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
@@ -1207,9 +1214,8 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   const int64_t kper = (nko + D.NBA - 1) / D.NBA;
   const int64_t k_lo = (int64_t)j * kper, k_n = max((int64_t)0, min(nko, k_lo + kper) - k_lo);
   {
-    const int32_t c = threadIdx.x < D.NBA ? D.cntK[(int64_t)threadIdx.x * D.NBA + j] : 0;
     int32_t tot;
-    const int32_t e = block_excl_scan(c, &tot, S.red);
+    const int32_t e = block_excl_scan(cK, &tot, S.red);
     if (threadIdx.x < D.NBA) S.pre[threadIdx.x] = e;
     if (threadIdx.x == 0) S.pre[D.NBA] = tot;
   }
@@ -1224,7 +1230,7 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   }
 #endif
   for (int64_t i = threadIdx.x; i < nA + o_n; i += ABLOCK) {
-    const LEntry e = i < nA ? D.L[(int64_t)j * D.LC + i] : D.Lovf[o_lo + (i - nA)];
+    const LEntry e = i < nA ? (i == t ? eA : D.L[(int64_t)j * D.LC + i]) : D.Lovf[o_lo + (i - nA)];
     *reinterpret_cast<int2*>(D.tok + e.a) = make_int2(nid, e.ya);
     D.tok[e.b] = make_int4(-1, 0, -1, -1);  // (no other occurrence writes b's record)
     if (e.c >= 0)
