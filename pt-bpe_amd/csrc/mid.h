@@ -453,9 +453,28 @@ __device__ inline void mid_new_token(const Dev& D, const Sel& sel) {
   }
 }
 
+// what a find workgroup reads that depends on neither the Sel record nor each other, loaded
+// in the launch's first round beside the Sel record (both parities' segment counts: the
+// previous merge's parity is itself one of these loads)
+struct MidPre {  // (scalars: an indexed pair would be a private array, which the compiler puts in LDS)
+  int32_t pp, theta, seg0, seg1;
+  int64_t spill0, spill1;
+};
+__device__ inline MidPre mid_pre(const Dev& D, int32_t w) {
+  MidPre m;
+  const State* st = D.st;
+  m.pp = st->place_par_prev;
+  m.theta = st->theta;
+  m.seg0 = D.mcnt[w].y;
+  m.seg1 = D.mcnt[NBA_MAX + w].y;
+  m.spill0 = st->mid_nh[0];
+  m.spill1 = st->mid_nh[1];
+  return m;
+}
+
 // find workgroup w of G (merge parity par, decision sel)
 __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w,
-                                                                    int32_t G, MidFindLds& S) {
+                                                                    int32_t G, MidFindLds& S, const MidPre& M) {
   State* st = D.st;
   const int32_t t = threadIdx.x;
   dbg_stamp(D, 10);
@@ -481,7 +500,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
   F.wl = sel.wl;
   F.w1 = sel.w1;
   F.w2 = sel.w2;
-  F.th = st->theta;
+  F.th = M.theta;
   F.par = par;
   F.iter = sel.iter;
   {
@@ -494,12 +513,12 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
   // candidates: share w of the winner's list, then the previous merge's new pairs of key W
   // (find workgroup w's segment of them, and share w of the spill list)
   const int32_t nW = sel.kpn;
-  const int32_t pp = st->place_par_prev;  // the previous merge's parity (-1: its pairs are in the lists)
+  const int32_t pp = M.pp;  // the previous merge's parity (-1: its pairs are in the lists)
   const int2* thp = mid_th(D, pp >= 0 ? pp : 0);
   const int64_t l0 = (int64_t)nW * w / G, nl = (int64_t)nW * (w + 1) / G - l0;
   const int64_t offW = sel.kpoff + l0;
-  const int64_t nsg = pp >= 0 ? min(D.mcnt[pp * NBA_MAX + w].y, MTH) : 0;
-  const int64_t nsp = pp >= 0 ? min(st->mid_nh[pp], D.THcap - MSEG_TH) : 0;
+  const int64_t nsg = pp >= 0 ? min((pp & 1) ? M.seg1 : M.seg0, MTH) : 0;
+  const int64_t nsp = pp >= 0 ? min((pp & 1) ? M.spill1 : M.spill0, D.THcap - MSEG_TH) : 0;
   const int64_t s0 = nsp * w / G, ns = nsp * (w + 1) / G - s0;
   const int2* segp = thp + (int64_t)w * MTH;
   const int2* spp = thp + MSEG_TH + s0;
@@ -881,6 +900,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int 
     MidAppLds a;
   } U;
   State* st = D.st;
+  const MidPre pre = (int)blockIdx.x < G ? mid_pre(D, blockIdx.x) : MidPre{};
   if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
     if (st->stall) return;
     par = st->dgen & 1;
@@ -892,7 +912,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int 
   const bool valid = st->kp_valid != 0;
   if (!find || !valid) sel.decision = SEL_STALL;
   if ((int)blockIdx.x < G) {
-    mid_find_body(D, sel, par, blockIdx.x, G, U.f);
+    mid_find_body(D, sel, par, blockIdx.x, G, U.f, pre);
     return;
   }
   if ((int)blockIdx.x == G && sel.decision == SEL_MERGE) mid_new_token(D, sel);
