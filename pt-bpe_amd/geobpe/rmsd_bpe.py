@@ -70,7 +70,8 @@ def _load_keyc():
     """The C pair-key builder (csrc/rmsdkey.c, built in-tree by geobpe/build.py)."""
     import importlib.util
     import os
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_rmsdkey.so")
+    # (GEOBPE_RMSDKEY: another build of the same extension, e.g. tools/asan_host.sh's sanitizer build)
+    path = os.environ.get("GEOBPE_RMSDKEY") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_rmsdkey.so")
     if not os.path.exists(path):
         return None
     spec = importlib.util.spec_from_file_location("_rmsdkey", path)
