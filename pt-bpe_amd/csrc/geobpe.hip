@@ -16,6 +16,7 @@
 // The bin pass is k_pairs_all + k_finalize.
 
 #include <dlfcn.h>
+#include <hip/hip_ext.h>
 #include <rccl/rccl.h>  // types only: the functions are resolved at run time (the process's RCCL)
 
 #include <algorithm>
@@ -230,6 +231,27 @@ struct Timed {
   }
 };
 
+// a sampled single-kernel launch of the merge loop: the start / stop stamps ride on the kernel's
+// own dispatch packet (hipExtLaunchKernelGGL) -- no marker packets in the stream, where a pair
+// of hipEventRecord around the launch opened an 8-15 us gap before it (profiles/r4_final/)
+bool sample_events(geobpe_ctx* c, const char* n, hipEvent_t* a, hipEvent_t* b) {
+  if (!c->prof) return false;
+  if (!c->prof_filter.empty() && c->prof_filter.find("," + std::string(n) + ",") == std::string::npos) return false;
+  if (c->prof_stride > 1 && (c->prof_seen[n]++ % c->prof_stride) != 0) return false;
+  *a = take_event(c);
+  *b = take_event(c);
+  c->pending.push_back({n, *a, *b});
+  return true;
+}
+#define LAUNCH_T(c, name, kernel, grid, block, shmem, ...)                                         \
+  do {                                                                                           \
+    hipEvent_t ea_ = nullptr, eb_ = nullptr;                                                     \
+    if (sample_events((c), (name), &ea_, &eb_))                                                  \
+      hipExtLaunchKernelGGL(kernel, grid, block, shmem, (c)->stream, ea_, eb_, 0, __VA_ARGS__); \
+    else                                                                                         \
+      hipLaunchKernelGGL(kernel, grid, block, shmem, (c)->stream, __VA_ARGS__);                  \
+  } while (0)
+
 void collect_events(geobpe_ctx* c) {
   if (c->pending.empty()) return;
   hipStreamSynchronize(c->stream);
@@ -361,21 +383,15 @@ void enqueue_select(geobpe_ctx* c) {
     return;
   }
   if (c->place_pending && c->place_mid) flush_place(c);
-  Timed t(c, "select");  // (+ the previous merge's k_place in workgroups 1..nba)
-  const int grid = c->place_pending ? 1 + c->nba : 1;
+  const int grid = c->place_pending ? 1 + c->nba : 1;  // (+ the previous merge's k_place in workgroups 1..nba)
   c->place_pending = false;
-  hipLaunchKernelGGL(k_select, dim3(grid), dim3(SBLOCK), 0, c->stream, c->D, (int)(c->gen & 1));
+  LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, (int)(c->gen & 1));
 }
 void enqueue_mark(geobpe_ctx* c) {
-  Timed t(c, "find");
-  hipLaunchKernelGGL(k_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
+  LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
 }
 void enqueue_apply(geobpe_ctx* c) {
-  {
-    Timed t(c, "commit");
-    hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, c->distributed ? 1 : 0,
-                       (int)(c->gen & 1));
-  }
+  LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
   c->place_pending = true;
   c->place_mid = false;
 #ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
@@ -396,16 +412,14 @@ void enqueue_iteration(geobpe_ctx* c) {
 void enqueue_iteration_mid(geobpe_ctx* c) {
   const int par = (int)(c->gen & 1);
   {
-    Timed t(c, "mid_sel");  // (+ the previous merge's token rewrites in workgroups 1..nba)
-    const bool carry = c->place_pending && c->place_mid;
+    const bool carry = c->place_pending && c->place_mid;  // (+ the previous merge's token rewrites in workgroups 1..nba)
     if (c->place_pending && !c->place_mid) flush_place(c);
     c->place_pending = false;
-    hipLaunchKernelGGL(k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->stream, c->D, par);
+    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->D, par);
   }
   {
-    Timed t(c, "mid_find");  // (+ the previous merge's posting entries in MID_APP more workgroups)
-    const int G = c->nba - MID_APP;
-    hipLaunchKernelGGL(k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, par, G, 1);
+    const int G = c->nba - MID_APP;  // (+ the previous merge's posting entries in MID_APP more workgroups)
+    LAUNCH_T(c, "mid_find", k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->D, par, G, 1);
   }
   c->place_pending = true;
   c->place_mid = true;
@@ -1309,15 +1323,9 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   D.xcnt = head;  // the records are counted in the slot header: final when the iteration's last kernel ends
   if (c->mid_on && mid_enabled(c)) {  // the middle regime (mid.h), device parity
     if (c->place_pending && !c->place_mid) flush_place(c);
-    {
-      Timed t(c, "mid_sel");
-      c->place_pending = false;
-      hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, D, -1);
-    }
-    {
-      Timed t(c, "mid_find");
-      hipLaunchKernelGGL(k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D, -1, c->nba - MID_APP, 1);
-    }
+    c->place_pending = false;
+    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, D, -1);
+    LAUNCH_T(c, "mid_find", k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, D, -1, c->nba - MID_APP, 1);
     c->place_pending = true;
     c->place_mid = true;
     HIPCHK(c, hipGetLastError());
@@ -1325,19 +1333,12 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   }
   if (c->place_pending && c->place_mid) flush_place(c);
   {
-    Timed t(c, "select");  // (+ the previous merge's k_place)
-    const int grid = c->place_pending ? 1 + c->nba : 1;
+    const int grid = c->place_pending ? 1 + c->nba : 1;  // (+ the previous merge's k_place)
     c->place_pending = false;
-    hipLaunchKernelGGL(k_select, dim3(grid), dim3(SBLOCK), 0, c->stream, c->D, -1);
+    LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, -1);
   }
-  {
-    Timed t(c, "find");
-    hipLaunchKernelGGL(k_find, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D, 1, -1);
-  }
-  {
-    Timed t(c, "commit");
-    hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D, 1, -1);
-  }
+  LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
+  LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
   c->place_pending = true;
 #ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
   flush_place(c);
