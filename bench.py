@@ -324,12 +324,13 @@ def main():
         live_us = 1000.0 * ms / nl if live else None
         avg_us = replay_avg.get(k, live_us)
         src = ("replay: every launch timed" if k in replay_avg
-               else f"live: every {args.event_stride}th launch of the timed region (no replay)")
+               else f"live: every {args.event_stride}th launch of the timed region, from the "
+               f"{args.event_stride // 2 + 1}th (no replay)")
         live_ach = None
         if live and bpl is not None:
             lb = bpl
             if no_skip and k in per_occ:
-                smp = src_of[k][::args.event_stride][:nl]
+                smp = src_of[k][args.event_stride // 2::args.event_stride][:nl]  # (the engine samples mid-stride)
                 if len(smp) == nl:  # (the sampled launches' own merges)
                     lb = bpl + per_occ[k] * (sum(m[2] for m in smp) / nl - sum(m[2] for m in src_of[k]) / max(len(src_of[k]), 1))
             live_ach = lb / (live_us * 1e-6) / 1e9

@@ -199,8 +199,9 @@ int64_t geobpe_verify_counts(geobpe_ctx *ctx);
  * "select" (+ the previous merge's place), "find", "commit", "place" (a place
  * launched on its own), "recount".  The merge loop's k_commit also counts its work
  * (key / decrement records, keys: geobpe_debug_state) when on = 1.  on = 0: off; on = 1: every
- * launch; on = k > 1: every k-th launch of each kernel (sampling keeps the event
- * packets from stretching the stream they measure). */
+ * launch; on = k > 1: every k-th launch of each kernel, from launch k / 2 (a run's first
+ * launch starts cold).  The merge loop's single-kernel launches carry their events on their
+ * own dispatch (hipExtLaunchKernelGGL: kernel start / end, no marker packets). */
 int geobpe_set_profiling(geobpe_ctx *ctx, int on);
 /* k_commit's work counters (key records, decrement records, keys: geobpe_debug_state
  * slots 10-12) on or off; geobpe_set_profiling with stride 1 turns them on (they slow

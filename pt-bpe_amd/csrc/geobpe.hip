@@ -237,7 +237,8 @@ struct Timed {
 bool sample_events(geobpe_ctx* c, const char* n, hipEvent_t* a, hipEvent_t* b) {
   if (!c->prof) return false;
   if (!c->prof_filter.empty() && c->prof_filter.find("," + std::string(n) + ",") == std::string::npos) return false;
-  if (c->prof_stride > 1 && (c->prof_seen[n]++ % c->prof_stride) != 0) return false;
+  // (the middle launch of every stride: a run's first launch of a kernel starts cold)
+  if (c->prof_stride > 1 && (c->prof_seen[n]++ % c->prof_stride) != c->prof_stride / 2) return false;
   *a = take_event(c);
   *b = take_event(c);
   c->pending.push_back({n, *a, *b});
