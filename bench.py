@@ -105,12 +105,13 @@ def parse():
     ap.add_argument("--event-stride", type=int, default=0,
                     help="time every k-th launch of the merge-loop kernels in the timed region (event records "
                          "are host work: at stride 1 the host, not the GPU, sets the pace); 0 = auto: "
-                         "max(8, steps // 32), about 32 samples per kernel at most")
+                         "one sample per kernel (its middle launch) below 256 steps, else max(8, steps // 32): "
+                         "about 32 samples per kernel")
     ap.add_argument("--emit-merges", action="store_true",
                     help="add the merge list ([key string, count] of every merge so far) to the JSON line")
     args = ap.parse_args()
-    if args.event_stride <= 0:  # (each sampled launch costs the timed region a few us of event packets)
-        args.event_stride = max(8, args.steps // 32)
+    if args.event_stride <= 0:  # (each sampled launch costs the timed region ~10 us of GPU idle)
+        args.event_stride = max(1, args.steps) if args.steps < 256 else max(8, args.steps // 32)
     return args
 
 

@@ -191,20 +191,21 @@ void dfree(geobpe_ctx* c, T** p) {
 }
 
 // ---------------------------------------------------------------- light kernel timing
+// timing-only events: no system-scope fence (an L2 writeback + invalidate) when one
+// completes -- with it, each sampled launch opened a 7-20 us gap in the merge loop
+// (GEOBPE_EVENT_FENCE=1: the default events, A/B)
+hipEvent_t make_event(geobpe_ctx* c) {
+  static const bool fence = getenv("GEOBPE_EVENT_FENCE") && atoi(getenv("GEOBPE_EVENT_FENCE")) == 1;
+  hipEvent_t e;
+  if (fence)
+    hipEventCreate(&e);
+  else
+    hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+  c->evall.push_back(e);
+  return e;
+}
 hipEvent_t take_event(geobpe_ctx* c) {
-  if (c->evpool.empty()) {
-    // timing-only events: no system-scope fence (an L2 writeback + invalidate) when one
-    // completes -- with it, each sampled launch opened a 7-20 us gap in the merge loop
-    // (GEOBPE_EVENT_FENCE=1: the default events, A/B)
-    static const bool fence = getenv("GEOBPE_EVENT_FENCE") && atoi(getenv("GEOBPE_EVENT_FENCE")) == 1;
-    hipEvent_t e;
-    if (fence)
-      hipEventCreate(&e);
-    else
-      hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
-    c->evall.push_back(e);
-    return e;
-  }
+  if (c->evpool.empty()) return make_event(c);
   hipEvent_t e = c->evpool.back();
   c->evpool.pop_back();
   return e;
@@ -1661,6 +1662,14 @@ int geobpe_set_profiling(geobpe_ctx* c, int on) {
   c->D.stats = c->prof && c->prof_stride == 1 ? 1 : 0;  // (work counters only under full profiling)
   c->prof_seen.clear();
   c->ktime.clear();
+  // events made now, not at the first sampled launches (hipEventCreate is host work inside
+  // the loop being measured)
+  if (c->prof) {
+    const size_t have = c->evpool.size();
+    std::vector<hipEvent_t> made;
+    for (size_t i = have; i < 128; i++) made.push_back(make_event(c));
+    c->evpool.insert(c->evpool.end(), made.begin(), made.end());
+  }
   return 0;
 }
 
