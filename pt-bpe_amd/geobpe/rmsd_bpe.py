@@ -1164,7 +1164,8 @@ class RmsdBPE:
             c.btt.pop(i2)
             c.btt[i1] = (i1, (n, assign[idx]), length)
             c.events.append((i1, i2, c.btt[i1]))
-            c.set_geo(i1, length, self._sphere_dict[key][assign[idx]])
+            if not self.rmsd_only:  # bpe.py:1386: rmsd_only keeps the occurrence's own geometry
+                c.set_geo(i1, length, self._sphere_dict[key][assign[idx]])
             if left:
                 geo_dict[self._pair_key(c, i0, l0, length)].add(i1)
             if right:

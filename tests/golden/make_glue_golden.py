@@ -50,13 +50,18 @@ FIXTURES = {
     "gl_pdb72_pareto": ("pdb72", None, None, 0, 500, 0, True, "all", 1.0, 1, 4, PARETO),
     # ... so the pareto setting itself runs on a synthetic corpus with more than 100 chains
     "gl_syn120_pareto": (120, 30, 60, 44, 500, 0, True, "all", 1.0, 1, 4, PARETO),
+    # held out: the same setting on a new seed, made after the envelope's
+    # variants and allowances were frozen, to check the device bound out of sample
+    "gl_syn120b_pareto": (120, 30, 60, 45, 500, 0, True, "all", 1.0, 1, 4, PARETO),
     # rmsd_only (bpe.py:1977, 2027): glue_opt_all still runs, the merges neither write the
     # medoid geometry nor re-optimise glues
     "gl_all_p0_rmsd_only": (6, 12, 30, 41, 5, 0, False, "all", 0.0, 1, 12, {"rmsd_only": True}),
 }
 # BPE.tokenize (the RMSD mode's induce, bpe.py:1053-1140, with glue_opt "all") of these
 # training chains after the steps
-INDUCE = {"gl_all_p0": [0, 3], "gl_all_p0_prior": [1, 4]}
+INDUCE = {"gl_all_p0": [0, 3], "gl_all_p0_prior": [1, 4],
+          # rmsd_only: step_helper keeps each occurrence's own (glue-optimised) geometry (bpe.py:1386)
+          "gl_all_p0_rmsd_only": [0, 3]}
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 
 

@@ -90,6 +90,9 @@ INDUCE = {
     "rm_p2_super_b3": (6, 10, 30, 97),
     "rm_p0_super_freebonds": (5, 15, 45, 96),
     "rm_pdb72_readme": (4, 40, 120, 95),
+    # rmsd_only: step_helper keeps each occurrence's own geometry (bpe.py:1386)
+    "rm_p0_rmsd_only": (5, 15, 45, 94),
+    "rm_p0_b2_long_rmsd_only": (5, 12, 30, 93),
 }
 COLS = ["0C:1N", "N:CA", "CA:C", "phi", "psi", "omega", "tau", "CA:C:1N", "C:1N:1CA"]
 

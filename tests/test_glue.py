@@ -41,6 +41,8 @@ NAMES = ["gl_all_p0", "gl_all_p0_prior"]
 # 2 sqrt(n) + 2 (the envelope is itself a sample of a few variants) -- and at least as long a
 # shared merge prefix as the shortest variant's.
 ENVELOPE = os.path.join(GOLDEN, "glue_envelope.json")
+DEVICE_PREFIX = {"gl_all_p0": 12, "gl_all_p0_prior": 5}  # merges the device run shares (of 12 / 7)
+ABS_CAP_RAD = 0.2    # backstop on any one glue's distance (the envelopes' farthest: 0.11-0.13 rad)
 GLUE_LOSS = 0.05     # relative, final loss of a chain (the envelope's loss ratios: tools/glue_envelope.py)
 
 
@@ -52,8 +54,8 @@ def _envelope(fixture):
         with open(ENVELOPE) as f:
             res = [r for r in json.load(f)["results"] if r["fixture"] == fixture and r["variant"] != "ref"
                    and "glued" in r]
-    if not res:
-        pytest.skip(f"no envelope for {fixture} in {ENVELOPE} (tools/glue_envelope.py)")
+    if not res:  # the envelope is committed: a missing entry is a failure, not a skip
+        pytest.fail(f"no envelope for {fixture} in {ENVELOPE} (tools/glue_envelope.py)")
     env = {}
     for t in GLUE_COLS:
         env[t] = {k: max(r["glued"][t][k] for r in res) for k in ("other_bin", "past_0.02", "past_0.1", "max_rad")}
@@ -256,7 +258,7 @@ def test_device_glue_drift_statistics():
             env = [r for r in json.load(f)["results"] if r["fixture"] == "drift120" and r["variant"] != "ref"
                    and "drift_rad" in r]
     if not env:
-        pytest.skip("no drift120 envelope (tools/glue_envelope.py)")
+        pytest.fail("no drift120 envelope in tests/golden/glue_envelope.json (tools/glue_envelope.py)")
     st = glue_drift.device_stats(os.path.join(GOLDEN, "glue_drift_oracle.npz"))
     print(json.dumps(st))
     print("reference envelope:", json.dumps({r["variant"]: [r["drift_rad"], r["same_bin"], r["loss_ratio"]] for r in env}))
@@ -300,6 +302,10 @@ def _glue_close(a, b, thr, what, fixture):
     # a maximum over a handful of rare events has no power to separate two implementations)
     assert got["past_envelope"] <= _count_bound(0), (
         f"{what}: {got['past_envelope']} glues farther than the reference's farthest ({far:.3g} rad)")
+    # absolute backstop, independent of the envelope: no glue farther than ABS_CAP_RAD, or than
+    # one bin on a grid coarser than that (a flip to the neighbouring bin at most)
+    assert got["max_rad"] <= max(ABS_CAP_RAD, width) + 1e-9, (
+        f"{what}: a glue {got['max_rad']:.3g} rad from the reference's (cap {max(ABS_CAP_RAD, width):.3g})")
     return got["other_bin"]
 
 
@@ -369,6 +375,8 @@ def run_and_compare(name, device=False):
         assert bpe._step == meta["step"]
         if CHECK_GLUE[0]:
             assert same >= prefix, f"{name}: the device shares {same} merges, the reference's own envelope {prefix}"
+            # the deterministic device kernel's own prefix (gl_device_golden.json pins its bits)
+            assert same >= DEVICE_PREFIX.get(name, 0), f"{name}: the device shares {same} merges, it shared {DEVICE_PREFIX[name]}"
         return bpe
     assert [[list(s) for s in x] for x in _segmentation(bpe)] == meta["segmentation"]
     _geometry_equal(bpe, arrs, "final")
@@ -440,8 +448,8 @@ def host_glue(monkeypatch):
 @pytest.mark.parametrize("name", NAMES + ["gl_all_p0_rmsd_only"])
 def test_rmsd_mode_glue_opt_host_logic_matches_reference(name, host_glue):
     bpe = run_and_compare(name)
-    if bpe.rmsd_only:  # (glue_opt_all only: the merges re-optimise nothing, bpe.py:2027)
-        assert bpe.glue_calls == 1
+    if bpe.rmsd_only:  # glue_opt_all, then one per tokenize(): the merges re-optimise nothing (bpe.py:1406, 2027)
+        assert bpe.glue_calls == 1 + len(_load(name)[0].get("induce", []))
 
 
 @pytest.mark.skipif(os.environ.get("GEOBPE_SLOW_TESTS") != "1", reason="~20 min on one CPU core (GEOBPE_SLOW_TESTS=1)")
