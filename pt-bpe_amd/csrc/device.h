@@ -98,7 +98,9 @@ struct State {
   int32_t post_valid, plog_ovf;
   int64_t pool_used, npost;   // pool chunks handed out since the last rebuild; rebuilds so far
   int64_t nko2[2];            // key records past the fixed slots, by launch parity
-  int32_t place_par, pad3;    // launch parity of the merge k_place writes out (-1: none)
+  int32_t place_par;          // launch parity of the merge k_place writes out (-1: none)
+  int32_t place_nid;          // ... its new token id, merge entries / key records past the fixed slots:
+  int64_t place_novf, place_nko;  // k_commit copies them here, so k_place has them in its first round
   int64_t stat_krec, stat_drec, stat_keys;
   int64_t nxovf;  // entries of Dev.xovf (pipelined exchange)  // k_commit work (profiling only): key records, decrement records, keys
   int64_t slot_max;    // pipelined exchange: the largest slot count of the imports since the last poll (every rank)
@@ -116,6 +118,9 @@ struct State {
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
 // and the host read it).  Every mark workgroup computes the same decision.
 constexpr int SEL_MERGE = 0, SEL_SKIP = 1, SEL_DONE = 2, SEL_STALL = 3;  // STALL: mid.h, lists being rebuilt
+// IDLE: the run's target merge count is reached -- an iteration the host enqueued past it (so
+// that a rebuild iteration inside the batch needs no host round trip to top up) does nothing
+constexpr int SEL_IDLE = 4;
 struct Sel {
   int32_t decision;
   int32_t skip;       // SKIP_* bits of a rebuild iteration

@@ -105,6 +105,11 @@ struct geobpe_ctx {
   bool tail_on = false;        // switched (one way: the full-grid kernels' posting index goes stale)
   bool tail_ready = false;     // its arrays are allocated
   int64_t hold_us = 0;         // geobpe_set_hold: a k_hold launch before each batch of iterations
+  // run_batches: iterations past a batch's target idle on the device (SEL_IDLE), so a rebuild
+  // iteration inside the batch costs no host round trip; run_end = target merges + 1 (0: off)
+  int32_t run_end = 0;
+  int spec = 1;                // iterations enqueued past each batch's target
+  double decay = 0;            // maxc ratio per merge over the last pulled batch (0: unknown)
   // middle regime (mid.h): merges whose count is <= mid_thresh run as k_mid_sel + k_mid_find
   int64_t mid_thresh = 49152;  // 0: never (C3 merges 11..1000: 16384 -> 29.2k, 32768 -> 30.7k, 49152 -> 31.0k, 65536 -> 30.8k, 98304 -> 29.2k merges/s)
   bool mid_on = false;         // switched (one way)
@@ -293,7 +298,7 @@ void flush_place(geobpe_ctx* c) {
   c->place_pending = false;
   Timed t(c, "place");
   if (c->place_mid) {  // token rewrites, then the posting entries, then nothing is pending
-    hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, c->D, INT32_MIN);
+    hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, c->D, INT32_MIN, 0);
     hipLaunchKernelGGL(k_mid_find, dim3(MID_APP), dim3(ABLOCK), 0, c->stream, c->D, (int)(c->gen & 1), 0, 0);
     hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, c->D);
   } else {
@@ -387,7 +392,7 @@ void enqueue_select(geobpe_ctx* c) {
   if (c->place_pending && c->place_mid) flush_place(c);
   const int grid = c->place_pending ? 1 + c->nba : 1;  // (+ the previous merge's k_place in workgroups 1..nba)
   c->place_pending = false;
-  LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, (int)(c->gen & 1));
+  LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, (int)(c->gen & 1), c->run_end);
 }
 void enqueue_mark(geobpe_ctx* c) {
   LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
@@ -417,7 +422,7 @@ void enqueue_iteration_mid(geobpe_ctx* c) {
     const bool carry = c->place_pending && c->place_mid;  // (+ the previous merge's token rewrites in workgroups 1..nba)
     if (c->place_pending && !c->place_mid) flush_place(c);
     c->place_pending = false;
-    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->D, par);
+    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->D, par, c->run_end);
   }
   {
     const int G = c->nba - MID_APP;  // (+ the previous merge's posting entries in MID_APP more workgroups)
@@ -569,14 +574,25 @@ bool mid_enabled(const geobpe_ctx* c) {
   return c->mid_thresh > 0 && !c->replay && (!c->distributed || c->pipelined) && c->nba > MID_APP;
 }
 
-// the next batch of iterations before the regime switches are checked: long while the
-// merges are far above the next threshold (the check costs a synchronisation)
+// the next batch of iterations before the regime switches are checked (the check is a host
+// round trip, ~33 us).  A merge's count falls roughly geometrically, so the merges left before
+// the switch are predicted from the last pulled batch's decay, and the batch runs to that
+// prediction + 8: overshooting the middle-regime threshold by a few merges costs nothing
+// measurable (the regimes run equally fast between 32 768 and 65 536 occurrences),
+// while round 4's 8-merge batches near it put three round trips into the driver's window
 int64_t tail_batch(const geobpe_ctx* c, int64_t want) {
   const bool mid = mid_enabled(c) && !c->mid_on, tail = tail_enabled(c);
   if (!mid && !tail) return want;
   const int64_t th = mid ? c->mid_thresh : c->tail_thresh;
   const int64_t m = c->h_state->maxc;
-  return std::min<int64_t>(want, m == 0 ? 16 : (m > 8 * th ? 64 : 8));
+  if (m == 0) return std::min<int64_t>(want, 16);
+  if (m > 8 * th) return std::min<int64_t>(want, 64);
+  int64_t b = m > 4 * th ? 32 : (m > 2 * th ? 16 : 8);
+  if (c->decay > 0 && c->decay < 1 && m > th) {
+    const double k = std::log((double)th / (double)m) / std::log(c->decay);
+    b = std::max<int64_t>(b, std::min<int64_t>(64, (int64_t)k + 8));
+  }
+  return std::min(want, b);
 }
 void tail_check_switch(geobpe_ctx* c) {
   const int64_t m = c->h_state->maxc;
@@ -666,6 +682,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   }
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
+  if (const char* e = getenv("GEOBPE_SPEC")) c->spec = std::max(0, atoi(e));  // (A/B: 0 = no idle iterations)
   if (const char* e = getenv("GEOBPE_KP_ATOMIC")) c->kp_atomic = atoi(e) != 0;  // (A/B: 0 = the sorted list build)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
@@ -1165,13 +1182,18 @@ static int run_batches(geobpe_ctx* c, int64_t n_iters, int64_t* n_done, bool pul
     const bool mid = c->mid_on && mid_enabled(c);
     if (mid && (rc = mid_prepare(c))) return rc;
     const int64_t batch = tail_batch(c, want);
+    // the run's last batch: spec more iterations, which idle on the device once the batch's
+    // merges are made (a hot-list rebuild iteration inside the batch then needs no top-up)
+    const int64_t extra = batch == want && !c->replay ? c->spec : 0;
+    c->run_end = extra ? (int32_t)(c->h_state->iter + batch + 1) : 0;
     if (c->hold_us > 0) hipLaunchKernelGGL(k_hold, dim3(1), dim3(64), 0, c->stream, (int64_t)(100 * c->hold_us));
-    for (int64_t i = 0; i < batch; i++) {
+    for (int64_t i = 0; i < batch + extra; i++) {
       if (mid)
         enqueue_iteration_mid(c);
       else
         enqueue_iteration(c);
     }
+    c->run_end = 0;
     HIPCHK(c, hipGetLastError());
     if (pull) {  // (every record this batch can write: <= one per iteration; after the pending
                  // place, which sums the last merge's merged total into its record)
@@ -1181,7 +1203,13 @@ static int run_batches(geobpe_ctx* c, int64_t n_iters, int64_t* n_done, bool pul
         HIPCHK(c, hipMemcpyAsync(c->h_log + from, c->D.log + from, n * sizeof(LogRec), hipMemcpyDeviceToHost,
                                  c->stream));
     }
+    const int32_t before = pull ? (int32_t)std::min<int64_t>(c->h_state->iter, c->h_log_cap) : 0;
     if ((rc = sync_state(c))) return rc;
+    if (pull) {  // the count's decay over the batch's merges (the next batch's size)
+      const int32_t a = before, z = (int32_t)std::min<int64_t>(c->h_state->iter, c->h_log_cap) - 1;
+      if (z > a && c->h_log[a].count > 0 && c->h_log[z].count > 0)
+        c->decay = std::pow((double)c->h_log[z].count / (double)c->h_log[a].count, 1.0 / (double)(z - a));
+    }
     if (c->h_state->done) break;
     tail_check_switch(c);
     want = n_iters - (c->h_state->iter - it0);
@@ -1326,7 +1354,7 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   if (c->mid_on && mid_enabled(c)) {  // the middle regime (mid.h), device parity
     if (c->place_pending && !c->place_mid) flush_place(c);
     c->place_pending = false;
-    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, D, -1);
+    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, D, -1, 0);
     LAUNCH_T(c, "mid_find", k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, D, -1, c->nba - MID_APP, 1);
     c->place_pending = true;
     c->place_mid = true;
@@ -1337,7 +1365,7 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   {
     const int grid = c->place_pending ? 1 + c->nba : 1;  // (+ the previous merge's k_place)
     c->place_pending = false;
-    LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, -1);
+    LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, -1, 0);
   }
   LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
   LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);

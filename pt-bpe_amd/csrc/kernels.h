@@ -698,7 +698,7 @@ __device__ inline T ldc(const T* p) {
 // the argmax + tie-break of one iteration (every thread of the workgroup calls it): the
 // decision goes to Sel[par] and, when lsel is given, to LDS (thread 0 writes both)
 template <bool COH>
-__device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, Sel* lsel) {
+__device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, Sel* lsel, int32_t run_end = 0) {
   State* st = D.st;
   Sel* out = D.sel + par;
   const bool rec = threadIdx.x == 0;
@@ -720,6 +720,13 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
   if (ldc<COH>(&st->done)) {
     if (rec) {
       o.decision = SEL_DONE;
+      publish();
+    }
+    return;
+  }
+  if (run_end > 0 && iter >= run_end - 1) {  // the run's merges are made: an idle iteration
+    if (rec) {
+      o.decision = SEL_IDLE;
       publish();
     }
     return;
@@ -920,7 +927,7 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
   dbg_stamp(D, 26);
 }
 
-__global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
+__global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par, int run_end) {
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
   State* st = D.st;
@@ -937,7 +944,7 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par) {
     __syncthreads();  // every thread has read dgen
     if (threadIdx.x == 0) st->dgen = g;
   }
-  select_core<false>(D, par, S, s_red, nullptr);
+  select_core<false>(D, par, S, s_red, nullptr, run_end);
 }
 
 // merge replay (bin/induce.py): merge t is the trained

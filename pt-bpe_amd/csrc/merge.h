@@ -721,6 +721,40 @@ __device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nb
   return (int64_t)nba * nba * SK + (i - nE);
 }
 
+// commit_resolve with the key's count added in the same round trip: the add to the count of
+// the key's first slot goes out beside the CAS (the key is there unless another key took the
+// slot first: then the add is undone and the key resolved onward).  An unclaimed slot's count
+// is 0, so a claim's count is its occurrence total either way.  The undone add may have hidden
+// a theta crossing of the slot's own key from the thread that made it: that key joins the hot
+// list unconditionally (a listed key under theta is a stale entry the select skips)
+__device__ __attribute__((always_inline)) inline int32_t commit_resolve_counted(const Dev& D, CommitLds& S, HotApp& hot,
+                                                                                const KRec& k, int32_t n, int32_t th) {
+  bool claimed = false;
+  const u64 s0 = ht_first_slot(D, k.pkey);
+  const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s0], 0ULL, (unsigned long long)k.pkey);
+  const int32_t c0 = atomicAdd(&D.count[s0], n);
+  int32_t d;
+  if (old == 0 || old == k.pkey) {
+    claimed = old == 0;
+    d = (int32_t)s0;
+    if (th > 0 && c0 < th && c0 + n >= th) hot_push(D, hot, d);
+  } else {
+    atomicAdd(&D.count[s0], -n);
+    if (th > 0) hot_push(D, hot, (int32_t)s0);
+    const u64 s1 = (s0 + 1) & ((u64)D.HC - 1);
+    d = ht_resolve(D, k.pkey, s1, ht_probe(D, s1), &claimed);
+    if (d >= 0) count_add_hot(D, hot, d, n, th);
+  }
+  if (d < 0) return -1;
+  if (claimed) {
+    claim_payload(D, d, k.h1, k.h2, k.len, k.idL, k.g, k.idR);
+    note_claim(D, &S.ns, d);
+  } else {
+    emit_check(D, &S.chk, d, k.len, k.h1, k.h2);
+  }
+  return d;
+}
+
 // a count change k_commit could not stage: a record (pipelined), the global count or the delta
 __device__ inline void commit_add(const Dev& D, int32_t d, int32_t v, bool tod) {
   if (tod && D.xrec)
@@ -863,6 +897,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const int32_t th = st->theta;
   const int32_t pn = D.pnch[j], pf = D.pfill[j];
   const int64_t nko_raw = st->nko2[par];
+  const int64_t novf_raw = j == 0 ? st->L_ovf2[par] : 0;
 #if EARLY_KCHUNK
   const int64_t kl0 = D.kchunk[2 * j], kl1 = D.kchunk[2 * j + 1];  // (this owner's klist chunk)
 #endif
@@ -872,6 +907,9 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     st->L_ovf2[par ^ 1] = 0;  // the next find's overflow counters (idle since the last pair)
     st->nko2[par ^ 1] = 0;
     st->place_par = sel.decision == SEL_MERGE ? par : -1;  // k_place's merge (with the next select)
+    st->place_nid = sel.nid;
+    st->place_novf = min(novf_raw, D.Lovf_cap);
+    st->place_nko = min(nko_raw, D.KO_cap);
     if (sel.decision == SEL_DONE) {
       st->done = 1;
       st->maxc = 0;
@@ -879,7 +917,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       st->nskip += 1;
     }
   }
-  if (sel.decision == SEL_DONE) return;
+  if (sel.decision == SEL_DONE || sel.decision == SEL_IDLE) return;
   if (sel.decision == SEL_SKIP) {
     if (sel.skip & SKIP_MEASURE) measure_max(D);
     if (sel.skip & SKIP_HOT) rebuild_hot_list(D, sel.theta_new, sel.build);
@@ -965,26 +1003,36 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     }                                                             \
   } while (0)
   const bool mine0 = lane_ok && k0 < min(cK, SK);
+  const int32_t nE = s_preE[nba], nF = s_preF[nba], nKO = S.nKO;
+  // this thread's first record past a slot's first PER (extras, then the overflow list) and
+  // its first extra decrement record go out in the same round as r0 / d0: the owners with
+  // extras -- the ones holding the most hot keys, which end the launch -- paid one more
+  // dependent round trip for them (~3 us, profiles/r4_final/merge_timeline_heavy.txt).  The
+  // first extra stays in registers for the publish round as well.
+  KRec e0;
+  int64_t at0 = 0;
+  const bool he = t < nE + nKO;
+  if (he) {
+    at0 = extra_at(D, s_preE, nba, j, PER, nE, t);
+    e0 = D.KS[at0];
+  }
+  int2 x0 = make_int2(-1, 0);
+  if (t < nF) {
+    const int32_t ww = seg_of(s_preF, nba, t);
+    x0 = D.DS[((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww])];
+  }
   if (mine0) COMMIT_INSERT(r0);
   if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
   dbg_stamp(D, 56);
-  const int32_t nE = s_preE[nba], nF = s_preF[nba], nKO = S.nKO;
-  // (this thread's first extra record stays in registers for round 2: an owner with extras
-  // otherwise paid one more dependent global round trip there, ~3 us, on the kernel's tail)
-  KRec e0;
-  int64_t at0 = 0;
-  for (int32_t i = t; i < nE + nKO; i += ABLOCK) {  // extras, then the overflow list
-    const int64_t at = extra_at(D, s_preE, nba, j, PER, nE, i);
-    const KRec k = D.KS[at];
-    if (i == t) {
-      e0 = k;
-      at0 = at;
-    }
+  if (he && (t < nE || owner_of_key(D, e0.pkey) == j)) COMMIT_INSERT(e0);
+  for (int32_t i = t + ABLOCK; i < nE + nKO; i += ABLOCK) {  // (rare: more than ABLOCK extras)
+    const KRec k = D.KS[extra_at(D, s_preE, nba, j, PER, nE, i)];
     if (i < nE || owner_of_key(D, k.pkey) == j) COMMIT_INSERT(k);
   }
   dbg_stamp(D, 57);
   dbg_val(D, 59, nF);
-  for (int32_t i = t; i < nF; i += ABLOCK) {
+  if (t < nF && !agg_stage(S.u.agg, x0.x, x0.y)) commit_add(D, x0.x, x0.y, tod);
+  for (int32_t i = t + ABLOCK; i < nF; i += ABLOCK) {
     const int32_t ww = seg_of(s_preF, nba, i);
     const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
     if (!agg_stage(S.u.agg, x.x, x.y)) commit_add(D, x.x, x.y, tod);
@@ -997,9 +1045,15 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     dbg_val(D, 7, nr + nE + nKO);
     dbg_val(D, 8, nd + nF);
   }
+  // ---- decrements of this owner's keys: one atomic per key, in flight under the resolves
+  // (a decrement cannot hide a theta crossing: a positive add that follows sees less)
+  if (!tod)
+    for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+      const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
+      if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
+    }
   // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
   int32_t nlog = 0, nkeys = 0;
-  const bool alone = S.fbn == 0;  // no key of this owner was resolved outside the table
   for (int32_t s = t; s < CKC; s += ABLOCK) {
     const u64 key = S.ckey[s];
     if (key == 0) continue;
@@ -1012,19 +1066,11 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     k.idL = rp.y;
     k.g = rp.z;
     k.idR = rp.w;
-    bool claimed;
-    const int32_t d = commit_resolve(D, S, k, &claimed);
+    const int32_t n = S.cn[s];
+    const int32_t d = tod ? commit_resolve(D, S, k) : commit_resolve_counted(D, S, hot, k, n, th);
     S.cid[s] = d >= 0 ? d : -2;
     if (d >= 0) {
-      const int32_t n = S.cn[s];
-      if (tod) {
-        if (!D.xrec) touch_add(D, tb, d, n);  // (direct records: written below)
-      } else if (claimed && alone) {  // a new key only this thread adds to: its count is n
-        D.count[d] = n;
-        if (th > 0 && n >= th) hot_push(D, hot, d);
-      } else {
-        count_add_hot(D, hot, d, n, th);
-      }
+      if (tod && !D.xrec) touch_add(D, tb, d, n);  // (direct records: written below)
       nlog += n;
       nkeys++;
     }
@@ -1093,15 +1139,12 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     commit_publish(D, S, mine, k, at);
   }
   dbg_stamp(D, 4);
-  // ---- decrements of this owner's keys: one atomic per key
-  for (int i = t; i < AggT<12>::N; i += ABLOCK) {
-    const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
-    if (k < 0 || v == 0) continue;
-    if (!tod)
-      atomicAdd(&D.count[k], v);
-    else if (!D.xrec)
-      touch_add(D, tb, k, v);
-  }
+  // ---- decrements of this owner's keys (multi-rank: into the touched list / the records)
+  if (tod && !D.xrec)
+    for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+      const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
+      if (k >= 0 && v != 0) touch_add(D, tb, k, v);
+    }
   if (tod && !D.xrec) touch_flush(D, tb);  // (block-uniform)
   if (tod && D.xrec) commit_export(D, S);  // (block-uniform)
   hot_flush(D, hot);  // (syncs the workgroup first)
@@ -1198,19 +1241,18 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   // and (speculatively) its first entry per thread, the record counts finder j sent each owner
   // (round 3's version loaded them after the Sel record: two more dependent rounds on the
   // select launch's critical path)
+  // (the merge's parity, token id and overflow counts come from k_commit's copy in the state:
+  // no dependent load of the Sel record)
   const int32_t par = st->place_par;
+  const int32_t nid = st->place_nid;
+  const int64_t novf = st->place_novf, nko = st->place_nko;
   const int32_t nA = D.Lcnt[j];
   const LEntry eA = D.L[(int64_t)j * D.LC + min((int64_t)t, D.LC - 1)];
   const int32_t cK = t < D.NBA ? D.cntK[(int64_t)t * D.NBA + j] : 0;
-  if (par < 0) return;
-  const Sel sel = D.sel[par];
-  if (sel.decision != SEL_MERGE) return;
+  if (par < 0) return;  // (k_commit sets par only for a merge)
   dbg_stamp(D, 30);
-  const int32_t nid = sel.nid;
-  const int64_t novf = min(st->L_ovf2[par], D.Lovf_cap);
   const int64_t oper = (novf + D.NBA - 1) / D.NBA;
   const int64_t o_lo = (int64_t)j * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
-  const int64_t nko = min(st->nko2[par], D.KO_cap);
   const int64_t kper = (nko + D.NBA - 1) / D.NBA;
   const int64_t k_lo = (int64_t)j * kper, k_n = max((int64_t)0, min(nko, k_lo + kper) - k_lo);
   {

@@ -80,7 +80,7 @@ struct MidAppLds {
 
 // ---------------------------------------------------------------------- find
 struct MidCtx {
-  int32_t W, nid, wl, th, par, iter;
+  int32_t W, nid, wl, th, par, iter, maxc;
   u64 w1, w2;
   u64 pa1, pb1, pa2, pb2;
 };
@@ -279,6 +279,29 @@ __device__ inline int32_t mid_resolve(const Dev& D, u64 h1, u64 h2, int32_t len,
   if (old == 0 || old == k) return (int32_t)s0;
   const u64 s1 = (s0 + 1) & ((u64)D.HC - 1);
   return ht_resolve(D, k, s1, ht_probe(D, s1), claimed);
+}
+
+// mid_resolve with the key's count (+n) added in the same round trip (one rank): the add to
+// the first slot's count goes out beside the CAS, as k_commit's commit_resolve_counted does --
+// undone when another key holds the slot, whose key then joins the hot list (the undone add
+// may have hidden its theta crossing from the thread that made it)
+__device__ inline int32_t mid_resolve_counted(const Dev& D, HotApp& hot, u64 h1, u64 h2, int32_t len, int32_t n,
+                                              int32_t th, bool* claimed) {
+  const u64 k = probe_key(h1, h2, len);
+  const u64 s0 = ht_first_slot(D, k);
+  const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s0], 0ULL, (unsigned long long)k);
+  const int32_t c0 = atomicAdd(&D.count[s0], n);
+  *claimed = old == 0;
+  if (old == 0 || old == k) {
+    if (th > 0 && c0 < th && c0 + n >= th) hot_push(D, hot, (int32_t)s0);
+    return (int32_t)s0;
+  }
+  atomicAdd(&D.count[s0], -n);
+  if (th > 0) hot_push(D, hot, (int32_t)s0);
+  const u64 s1 = (s0 + 1) & ((u64)D.HC - 1);
+  const int32_t d = ht_resolve(D, k, s1, ht_probe(D, s1), claimed);
+  if (d >= 0) count_add_hot(D, hot, d, n, th);
+  return d;
 }
 
 // a new pair resolved on its own (a run's later occurrence, or the round's table is full)
@@ -487,7 +510,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       st->nskip += 1;
     }
   }
-  if (sel.decision == SEL_DONE || sel.decision == SEL_STALL) return;
+  if (sel.decision == SEL_DONE || sel.decision == SEL_STALL || sel.decision == SEL_IDLE) return;
   if (sel.decision == SEL_SKIP) {
     if (t == 0) D.chkcnt[w] = 0;
     if (sel.skip & SKIP_MEASURE) measure_max(D, w, G);
@@ -503,6 +526,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
   F.th = M.theta;
   F.par = par;
   F.iter = sel.iter;
+  F.maxc = sel.maxc;
   {
     const int64_t nw = 2 * (int64_t)max(F.wl, 1) - 1;
     F.pa1 = D.pw1[nw + 1];
@@ -590,7 +614,8 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       const int4 rp = S.rep[s];
       bool claimed;
       const u64 h1 = S.h1[s], h2 = S.h2[s];
-      const int32_t d = mid_resolve(D, h1, h2, rp.x, &claimed);
+      const int32_t d = D.xrec ? mid_resolve(D, h1, h2, rp.x, &claimed)
+                               : mid_resolve_counted(D, S.hot, h1, h2, rp.x, S.cnt[s], F.th, &claimed);
       S.did[s] = d;
       if (d < 0) {
         if (D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, 0, -1);  // (no-op record)
@@ -602,10 +627,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       } else {
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
-      if (D.xrec)
-        mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
-      else
-        count_add_hot(D, S.hot, d, S.cnt[s], F.th);
+      if (D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
     }
     __syncthreads();
     if (c0 == 0) dbg_stamp(D, 17);
@@ -654,7 +676,9 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       const int32_t k = S.agg.key[i], v = S.agg.val[i];
       if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
     }
-    if (w == 0 && t == 0) D.count[F.W] = 0;  // (mid_dec_agg: every pair of W is gone)
+    // (mid_dec_agg: every pair of W is gone; an add, not a store: another key's speculative
+    // add to this slot and its undo may straddle it, mid_resolve_counted)
+    if (w == 0 && t == 0) atomicAdd(&D.count[F.W], -F.maxc);
   }
   // (the merge's merged total: the next place sums the workgroups' counts into the log)
   hot_flush(D, S.hot);  // (syncs the workgroup first)
@@ -1019,7 +1043,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
 // rewrites of merge st->place_par.  Workgroup 0 records which merge's new pairs the next
 // find's appends take (place_par_prev) and resets its parity's list cursors (nothing else
 // in this launch reads them).
-__global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par) {
+__global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par, int run_end) {
   if (blockIdx.x > 0) {
     mid_place_body(D, blockIdx.x - 1, gridDim.x - 1);
     return;
@@ -1048,7 +1072,7 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par) {
     }
     return;
   }
-  select_core<false>(D, par, S, s_red, nullptr);
+  select_core<false>(D, par, S, s_red, nullptr, run_end);
 }
 
 // after a flush (k_mid_sel place-only + k_mid_find appends-only): nothing is pending
