@@ -130,6 +130,13 @@ struct geobpe_ctx {
   // collapse at the middle-regime switch (geobpe_set_collapse): every rank then holds the whole
   // corpus and runs the one-rank loop; its own rows are [own_row0, own_row1) of it
   bool collapse_on = true, collapsed = false;
+  // x_collapse_prepare: every rank's sizes and bases, the gathered junction symbols and row offsets
+  bool cg_ready = false;
+  std::vector<int64_t> cg_nR, cg_nN, cg_bR, cg_bN, cg_rows;
+  int64_t cg_Lmax = 1;
+  int32_t* cg_gsym = nullptr;
+  uint16_t* cg_gs16 = nullptr;
+  int64_t* cg_row = nullptr;
   // per-key list build (tail_build): radix-sort scratch; kp_atomic: the atomic counting build (A/B)
   void* kps = nullptr;
   int64_t kps_bytes = 0;
@@ -451,7 +458,19 @@ int sync_state_sel(geobpe_ctx* c, Sel* out) {
 }
 
 // ---------------------------------------------------------------- late-merge path (tail.h)
-bool tail_enabled(const geobpe_ctx* c) { return c->tail_thresh > 0 && !c->distributed && !c->replay; }
+bool tail_enabled(const geobpe_ctx* c) {
+  return c->tail_thresh > 0 && !c->distributed && !c->replay && !c->collapsed;
+}
+
+// device bytes tail_alloc takes for R residues (a collapse checks them before it commits)
+int64_t tail_bytes(const geobpe_ctx* c, int64_t R) {
+  const int64_t kpool = std::min<int64_t>(6 * R + 65536, INT32_MAX - 1) * 4;
+  const int64_t tm = (R / 2 + 1024 + MSEG_TM) * (int64_t)sizeof(int4);
+  const int64_t thc = R + 2048 + MSEG_TH;
+  const int64_t th = thc * (2 * (int64_t)sizeof(int2) + (int64_t)sizeof(int4) + 4 + (int64_t)sizeof(NewPair));
+  const int64_t keyed = c->D.kp_off ? 0 : 3 * c->D.HC * 4 + 2 * NBA_MAX * (int64_t)sizeof(int4) + 2 * NBA_MAX * (MID_APP + 1) * 4;
+  return kpool + tm + th + keyed;
+}
 
 int tail_alloc(geobpe_ctx* c) {
   if (c->tail_ready) return 0;
@@ -574,6 +593,13 @@ bool mid_enabled(const geobpe_ctx* c) {
   return c->mid_thresh > 0 && !c->replay && (!c->distributed || c->pipelined) && c->nba > MID_APP;
 }
 
+// a collapsed engine (x_collapse) holds the whole corpus in the token records, the junction
+// symbols and the row offsets only: every other residue-sized buffer (rsym, pk, posting index,
+// find regions, ...) and the capacities derived from them keep the shard's size, so the
+// full-grid kernels (k_select / k_find / k_commit / k_place, the bin pass) must never run on
+// it -- only the middle regime, whose arrays are made again for the whole corpus
+bool collapsed_grid(const geobpe_ctx* c) { return c->collapsed && !(c->mid_on && mid_enabled(c)); }
+
 // the next batch of iterations before the regime switches are checked (the check is a host
 // round trip, ~33 us).  A merge's count falls roughly geometrically, so the merges left before
 // the switch are predicted from the last pulled batch's decay, and the batch runs to that
@@ -587,7 +613,9 @@ int64_t tail_batch(const geobpe_ctx* c, int64_t want) {
   const int64_t m = c->h_state->maxc;
   if (m == 0) return std::min<int64_t>(want, 16);
   if (m > 8 * th) return std::min<int64_t>(want, 64);
-  int64_t b = m > 4 * th ? 32 : (m > 2 * th ? 16 : 8);
+  // (2 th -> th takes ~20 merges on C3, each 0.964 of the last: 32 overshoots by ~12 merges into
+  // the range where the two regimes run equally fast)
+  int64_t b = m > 4 * th ? 48 : (m > 2 * th ? 32 : (4 * m > 5 * th ? 16 : 8));
   if (c->decay > 0 && c->decay < 1 && m > th) {
     const double k = std::log((double)th / (double)m) / std::log(c->decay);
     b = std::max<int64_t>(b, std::min<int64_t>(64, (int64_t)k + 8));
@@ -966,6 +994,7 @@ int geobpe_set_tail(geobpe_ctx* c, int64_t max_count) {
 
 int geobpe_set_mid(geobpe_ctx* c, int64_t max_count) {
   if (!c || max_count < 0) return GEOBPE_EARG;
+  if (c->collapsed && !max_count) return fail(c, GEOBPE_EARG, "a collapsed engine runs the middle regime only");
   c->mid_thresh = max_count;
   if (!max_count && c->mid_on) return fail(c, GEOBPE_EARG, "the middle-regime path is already in use");
   return 0;
@@ -1081,6 +1110,7 @@ int geobpe_bin(geobpe_ctx* c) {
 
 int geobpe_step_select(geobpe_ctx* c, int32_t* new_id, int32_t* count) {
   if (!c || !c->keys_ready || !new_id) return GEOBPE_EARG;
+  if (c->collapsed) return fail(c, GEOBPE_EARG, "a collapsed engine runs the middle regime only (geobpe_run)");
   if (c->mark_pending) return fail(c, GEOBPE_EARG, "step_select twice without step_apply");
   if (c->pipelined) return fail(c, GEOBPE_EARG, "step_select inside a pipelined exchange");
   HIPCHK(c, hipSetDevice(c->device));
@@ -1127,6 +1157,7 @@ int geobpe_step_apply(geobpe_ctx* c, int64_t* n_merged) {
 int geobpe_step(geobpe_ctx* c, int32_t* new_id, int32_t* count, int64_t* n_merged) {
   if (!c || !new_id) return GEOBPE_EARG;
   if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
+  if (collapsed_grid(c)) return fail(c, GEOBPE_EARG, "a collapsed engine runs the middle regime only");
   if (c->distributed) return fail(c, GEOBPE_EARG, "geobpe_step in distributed mode: use step_select/apply + deltas");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
@@ -1169,6 +1200,7 @@ static int run_batches(geobpe_ctx* c, int64_t n_iters, int64_t* n_done, bool pul
   if (!c || n_iters < 0) return GEOBPE_EARG;
   if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
   if (c->distributed) return fail(c, GEOBPE_EARG, "geobpe_run in distributed mode");
+  if (collapsed_grid(c)) return fail(c, GEOBPE_EARG, "a collapsed engine runs the middle regime only");
   HIPCHK(c, hipSetDevice(c->device));
   const int32_t it0 = c->h_state->iter;
   int rc;
@@ -1735,7 +1767,7 @@ int geobpe_replay_load(geobpe_ctx* c, const uint64_t* h_h1, const uint64_t* h_h2
                        const int32_t* h_idL, const int32_t* h_g, const int32_t* h_idR, int64_t n) {
   if (!c || n < 0 || (n && (!h_h1 || !h_h2 || !h_len || !h_idL || !h_g || !h_idR))) return GEOBPE_EARG;
   if (!c->keys_ready) return fail(c, GEOBPE_EARG, "bin() first");
-  if (c->distributed) return fail(c, GEOBPE_EARG, "merge replay is single-rank");
+  if (c->distributed || c->collapsed) return fail(c, GEOBPE_EARG, "merge replay is single-rank");
   if (c->h_state->iter > 0) return fail(c, GEOBPE_EARG, "merge replay must start before the first merge");
   if (c->K0 + n > c->max_vocab) return fail(c, GEOBPE_ECAPACITY, "K0 + %lld merges exceed max_vocab", (long long)n);
   std::vector<ReplayRec> r((size_t)n);
@@ -2309,71 +2341,151 @@ int x_gather_blocks(geobpe_ctx* c, const void* d_src, void* d_dst, const std::ve
   return 0;
 }
 
-// The middle-regime switch of the row-sharded loop: stop sharding.  Below mid_thresh
-// occurrences a merge is a fixed chain of dependent round trips whatever a rank holds, so
-// the per-merge exchange (all-gather + import) is pure overhead there (VERDICT r3: N > 1
-// slower than N = 1 in that regime).  Every rank gathers every rank's token records (and
-// the junction symbols and row offsets) once, re-keys the foreign blocks' pairs in its own
-// key table (k_collapse_fix) and continues as the one-rank loop over the whole corpus --
-// every rank making the same merges with no exchange, its own rows a window of the whole.
-// The counts need no change: they were global (replicated) already.  Called at a poll of
-// geobpe_run_exchange, after geobpe_pipeline_end (nothing in flight, nothing stalled).
-int x_collapse(geobpe_ctx* c) {
+// every rank's yes: a collective every rank reaches (the decisions that lead here read only
+// replicated data), so a rank that cannot go on says so instead of leaving its peers blocked in
+// the next collective (the collapse's allocations could fail between gathers)
+int x_agree(geobpe_ctx* c, bool mine, bool* all) {
+  const int32_t v = mine ? 1 : 0;
+  std::vector<uint8_t> raw;
+  int rc;
+  if ((rc = x_allgather_host(c, &v, 4, raw))) return rc;
+  *all = true;
+  for (int64_t r = 0; r < c->x_world; r++) *all = *all && reinterpret_cast<const int32_t*>(raw.data())[r] != 0;
+  return 0;
+}
+
+// device memory still free, less a margin for the runtime and RCCL
+bool x_fits(int64_t bytes) {
+  size_t fr = 0, tot = 0;
+  if (hipMemGetInfo(&fr, &tot) != hipSuccess) return false;
+  return (int64_t)fr - bytes > (int64_t)(1LL << 30);
+}
+
+// Before the first pipelined merge: what a collapse moves that never changes after
+// initialize() -- every rank's junction symbols (int32 and 16-bit copies) and row offsets -- is
+// gathered once, off the switch (the collapse then moves only the 16-B token
+// records).  Every step that can fail on one rank (the sizes, the allocations) is agreed on by
+// every rank before the gathers; a rank that cannot hold them turns the collapse off on all.
+int x_collapse_prepare(geobpe_ctx* c) {
+  if (c->cg_ready || !c->collapse_on) return 0;
   const int64_t W = c->x_world, me = c->x_rank;
   int rc;
-  if ((rc = sync_state(c))) return rc;  // (flushes the last merge's place)
   const int64_t mine[3] = {c->R, c->nrows, c->Lmax};
   std::vector<uint8_t> raw;
   if ((rc = x_allgather_host(c, mine, sizeof mine, raw))) return rc;
   const int64_t* all = reinterpret_cast<const int64_t*>(raw.data());
-  std::vector<int64_t> nR(W), nN(W), bR(W + 1, 0), bN(W + 1, 0);
-  int64_t Lmax = 1;
+  c->cg_nR.assign(W, 0);
+  c->cg_nN.assign(W, 0);
+  c->cg_bR.assign(W + 1, 0);
+  c->cg_bN.assign(W + 1, 0);
+  c->cg_Lmax = 1;
   for (int64_t r = 0; r < W; r++) {
-    nR[r] = all[3 * r];
-    nN[r] = all[3 * r + 1];
-    Lmax = std::max(Lmax, all[3 * r + 2]);
-    bR[r + 1] = bR[r] + nR[r];
-    bN[r + 1] = bN[r] + nN[r];
+    c->cg_nR[r] = all[3 * r];
+    c->cg_nN[r] = all[3 * r + 1];
+    c->cg_Lmax = std::max(c->cg_Lmax, all[3 * r + 2]);
+    c->cg_bR[r + 1] = c->cg_bR[r] + c->cg_nR[r];
+    c->cg_bN[r + 1] = c->cg_bN[r] + c->cg_nN[r];
   }
-  if (nR[me] != c->R || nN[me] != c->nrows) return fail(c, GEOBPE_EARG, "collapse: rank sizes disagree");
-  const int64_t Rt = bR[W], Nt = bN[W];
-  if (Rt >= INT32_MAX / 4) return fail(c, GEOBPE_EARG, "collapse: too many residues for int32 indexing");
+  const int64_t Rt = c->cg_bR[W], Nt = c->cg_bN[W];
+  const int64_t nmax = *std::max_element(c->cg_nR.begin(), c->cg_nR.end());
+  const int64_t per = c->D.gs16 ? 6 : 4;
+  bool ok = c->cg_nR[me] == c->R && c->cg_nN[me] == c->nrows && Rt < INT32_MAX / 4 &&
+            x_fits(Rt * per + (Nt + 1) * 8 + (W + 1) * nmax * 4 + 16 * Rt + tail_bytes(c, Rt));
   Dev& D = c->D;
-  int4* tok2 = nullptr;
-  int32_t* gsym2 = nullptr;
-  uint16_t* gs16_2 = nullptr;
-  int64_t* row2 = nullptr;
-  if ((rc = dalloc(c, &tok2, Rt + 8, 0xFF)) || (rc = dalloc(c, &gsym2, Rt + 8, 0)) || (rc = dalloc(c, &row2, Nt + 1)) ||
-      (D.gs16 && (rc = dalloc(c, &gs16_2, Rt + 8, 0xFF))))
-    return rc;
-  if ((rc = x_gather_blocks(c, D.tok, tok2, nR, bR, sizeof(int4))) ||
-      (rc = x_gather_blocks(c, D.gsym, gsym2, nR, bR, sizeof(int32_t))) ||
-      (D.gs16 && (rc = x_gather_blocks(c, D.gs16, gs16_2, nR, bR, sizeof(uint16_t)))))
+  if (ok) ok = !dalloc(c, &c->cg_gsym, Rt + 8, 0) && !dalloc(c, &c->cg_row, Nt + 1) &&
+               !(D.gs16 && dalloc(c, &c->cg_gs16, Rt + 8, 0xFF)) &&
+               !grow_dev(c, &c->x_flat, &c->x_flat_bytes, std::max<int64_t>(nmax * 4, 8)) &&
+               !grow_dev(c, &c->x_tmp, &c->x_tmp_bytes, std::max<int64_t>(W * nmax * 4, 8));
+  bool every = false;
+  if ((rc = x_agree(c, ok, &every))) return rc;
+  if (!every) {  // (consistent on every rank: the sharded middle regime instead)
+    dfree(c, &c->cg_gsym);
+    dfree(c, &c->cg_row);
+    if (c->cg_gs16) dfree(c, &c->cg_gs16);
+    c->collapse_on = false;
+    return 0;
+  }
+  if ((rc = x_gather_blocks(c, D.gsym, c->cg_gsym, c->cg_nR, c->cg_bR, sizeof(int32_t))) ||
+      (D.gs16 && (rc = x_gather_blocks(c, D.gs16, c->cg_gs16, c->cg_nR, c->cg_bR, sizeof(uint16_t)))))
     return rc;
   // row offsets: every rank's (local, then moved to its residue base), the total at the end
-  std::vector<int64_t> rows_full(Nt + 1);
-  {
-    const int64_t nmax = *std::max_element(nN.begin(), nN.end());
-    std::vector<int64_t> send(std::max<int64_t>(nmax, 1), 0);
-    std::copy(c->row_off.begin(), c->row_off.begin() + c->nrows, send.begin());
-    if ((rc = x_allgather_host(c, send.data(), (int64_t)send.size() * 8, raw))) return rc;
-    const int64_t* ro = reinterpret_cast<const int64_t*>(raw.data());
-    for (int64_t r = 0; r < W; r++)
-      for (int64_t i = 0; i < nN[r]; i++) rows_full[bN[r] + i] = bR[r] + ro[r * (int64_t)send.size() + i];
-    rows_full[Nt] = Rt;
+  const int64_t nNmax = *std::max_element(c->cg_nN.begin(), c->cg_nN.end());
+  std::vector<int64_t> send(std::max<int64_t>(nNmax, 1), 0);
+  std::copy(c->row_off.begin(), c->row_off.begin() + c->nrows, send.begin());
+  if ((rc = x_allgather_host(c, send.data(), (int64_t)send.size() * 8, raw))) return rc;
+  const int64_t* ro = reinterpret_cast<const int64_t*>(raw.data());
+  c->cg_rows.assign(Nt + 1, 0);
+  for (int64_t r = 0; r < W; r++)
+    for (int64_t i = 0; i < c->cg_nN[r]; i++) c->cg_rows[c->cg_bN[r] + i] = c->cg_bR[r] + ro[r * (int64_t)send.size() + i];
+  c->cg_rows[Nt] = Rt;
+  HIPCHK(c, hipMemcpyAsync(c->cg_row, c->cg_rows.data(), (Nt + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->cg_ready = true;
+  return 0;
+}
+
+// the collapse as a cost decision: it pays once -- the token records' all-gather
+// (16 B a residue at ~200 GB/s per rank over xGMI), the re-keying pass (~0.5 ms) and the
+// whole-corpus list build (~1.5 ms) at C3's 30 M residues, ~0.2 ms of synchronisations and
+// launches -- and saves the exchange of every later merge of the run (~25 us a merge: the
+// record export, the all-gather and the import of the world-1 rehearsal), so it is
+// taken when the run has enough merges left to earn it back (C3: ~190)
+bool x_collapse_pays(const geobpe_ctx* c, int64_t left) {
+  if (!c->cg_ready || c->cg_bR.empty()) return false;
+  const double Rt = (double)c->cg_bR.back();
+  const double cost_us = 200.0 + Rt * (16.0 / 200e3 + 2.0e3 / 30e6);
+  return (double)left * 25.0 > cost_us;
+}
+
+// The middle-regime switch of the row-sharded loop: stop sharding.  Below mid_thresh
+// occurrences a merge is a fixed chain of dependent round trips whatever a rank holds, so
+// the per-merge exchange (all-gather + import) is pure overhead there (VERDICT r3: N > 1
+// slower than N = 1 in that regime).  Every rank gathers every rank's token records once (the
+// junction symbols and row offsets were gathered before the loop, x_collapse_prepare), re-keys
+// the foreign blocks' pairs in its own key table (k_collapse_fix) and continues as the one-rank
+// loop over the whole corpus -- every rank making the same merges with no exchange, its own
+// rows a window of the whole.  The counts need no change: they were global (replicated)
+// already.  Called at a poll of geobpe_run_exchange, after geobpe_pipeline_end (nothing in
+// flight, nothing stalled).  Every allocation comes first and every rank agrees before the
+// gather (x_agree): *done = false on every rank when one of them cannot take the whole corpus,
+// and the loop goes on sharded.
+int x_collapse(geobpe_ctx* c, bool* done) {
+  *done = false;
+  if (!c->cg_ready) return 0;
+  const int64_t W = c->x_world, me = c->x_rank;
+  int rc;
+  if ((rc = sync_state(c))) return rc;  // (flushes the last merge's place)
+  Dev& D = c->D;
+  const int64_t Rt = c->cg_bR[W], Nt = c->cg_bN[W], Lmax = c->cg_Lmax;
+  const int64_t nmax = *std::max_element(c->cg_nR.begin(), c->cg_nR.end());
+  int4* tok2 = nullptr;
+  int64_t* d_base = nullptr;
+  u64 *dp1 = nullptr, *dp2 = nullptr;
+  const int64_t pwn = 2 * Lmax + 8;
+  bool ok = x_fits(16 * Rt + 2 * W * nmax * 16 + tail_bytes(c, Rt)) && !dalloc(c, &tok2, Rt + 8, 0xFF) &&
+            !dalloc(c, &d_base, W + 1) &&
+            (Lmax <= c->Lmax || (!dalloc(c, &dp1, pwn) && !dalloc(c, &dp2, pwn))) &&
+            !grow_dev(c, &c->x_flat, &c->x_flat_bytes, std::max<int64_t>(nmax * 16, 8)) &&
+            !grow_dev(c, &c->x_tmp, &c->x_tmp_bytes, std::max<int64_t>(W * nmax * 16, 8));
+  bool every = false;
+  if ((rc = x_agree(c, ok, &every))) return rc;
+  if (!every) {
+    dfree(c, &tok2);
+    dfree(c, &d_base);
+    if (dp1) dfree(c, &dp1);
+    if (dp2) dfree(c, &dp2);
+    c->collapse_on = false;
+    return 0;
   }
-  HIPCHK(c, hipMemcpyAsync(row2, rows_full.data(), (Nt + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  if ((rc = x_gather_blocks(c, D.tok, tok2, c->cg_nR, c->cg_bR, sizeof(int4)))) return rc;
   // the longest chain anywhere bounds the token lengths the content hashes combine
   if (Lmax > c->Lmax) {
-    const int64_t pwn = 2 * Lmax + 8;
     std::vector<u64> p1(pwn), p2(pwn);
     p1[0] = p2[0] = 1;
     for (int64_t i = 1; i < pwn; i++) {
       p1[i] = mulmod61(p1[i - 1], HP1);
       p2[i] = mulmod61(p2[i - 1], HP2);
     }
-    u64 *dp1, *dp2;
-    if ((rc = dalloc(c, &dp1, pwn)) || (rc = dalloc(c, &dp2, pwn))) return rc;
     HIPCHK(c, hipMemcpyAsync(dp1, p1.data(), pwn * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipMemcpyAsync(dp2, p2.data(), pwn * 8, hipMemcpyHostToDevice, c->stream));
     HIPCHK(c, hipStreamSynchronize(c->stream));  // (the host vectors go out of scope)
@@ -2388,20 +2500,21 @@ int x_collapse(geobpe_ctx* c) {
   if (D.gs16) dfree(c, &D.gs16);
   dfree(c, &c->d_row_off);
   D.tok = tok2;
-  D.gsym = gsym2;
-  D.gs16 = gs16_2;
-  c->d_row_off = row2;
-  D.row_off = row2;
-  c->row_off = rows_full;
-  c->own_row0 = bN[me];
-  c->own_row1 = bN[me + 1];
+  D.gsym = c->cg_gsym;
+  D.gs16 = c->cg_gs16;
+  c->d_row_off = c->cg_row;
+  D.row_off = c->cg_row;
+  c->cg_gsym = nullptr;
+  c->cg_gs16 = nullptr;
+  c->cg_row = nullptr;
+  c->row_off = c->cg_rows;
+  c->own_row0 = c->cg_bN[me];
+  c->own_row1 = c->cg_bN[me + 1];
   c->R = Rt;
   D.R = Rt;
   c->nrows = Nt;
   D.nrows = Nt;
-  int64_t* d_base;
-  if ((rc = dalloc(c, &d_base, W + 1))) return rc;
-  HIPCHK(c, hipMemcpyAsync(d_base, bR.data(), (W + 1) * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(d_base, c->cg_bR.data(), (W + 1) * 8, hipMemcpyHostToDevice, c->stream));
   hipLaunchKernelGGL(k_collapse_fix, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, (const int64_t*)d_base, (int)W,
                      (int)me);
   HIPCHK(c, hipGetLastError());
@@ -2422,6 +2535,7 @@ int x_collapse(geobpe_ctx* c) {
   c->distributed = false;
   c->collapsed = true;
   c->mid_on = true;
+  *done = true;
   return 0;
 }
 
@@ -2449,6 +2563,7 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
   // the gathered slots: W x the largest slot this run can use (geobpe_comm_set_slot may have
   // raised the fixed size since the last run)
   if ((rc = grow_dev(c, &c->x_gath, &c->x_gath_bytes, W * (1 + std::max(CAP_MAX, c->x_fixed)) * REC))) return rc;
+  if (!c->ev && (rc = x_collapse_prepare(c))) return rc;  // (once: the collapse's static arrays)
   if ((rc = geobpe_pipeline_begin(c))) return rc;
   int64_t out[4];
   int64_t done = 0;
@@ -2462,23 +2577,28 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
     // counts, the iteration number -- so every rank switches at the same poll and issues the
     // same collectives (a rank's own merged count would let ranks part ways)
     int64_t win = ahead;
-    if (!c->mid_on && mid_enabled(c) && c->h_state->iter > 0) {
+    const bool may_collapse = c->collapse_on && c->cg_ready && !c->ev && x_collapse_pays(c, n_merges - done);
+    if ((!c->mid_on || may_collapse) && mid_enabled(c) && c->h_state->iter > 0) {
       LogRec lr;
       HIPCHK(c, hipMemcpy(&lr, c->D.log + (c->h_state->iter - 1), sizeof lr, hipMemcpyDeviceToHost));
-      if (lr.count <= c->mid_thresh && c->collapse_on && !c->ev) {
+      if (lr.count <= c->mid_thresh && may_collapse) {
         // stop sharding: every rank takes the whole corpus and goes on alone (x_collapse)
-        if ((rc = geobpe_pipeline_end(c)) || (rc = x_collapse(c))) return rc;
-        int64_t more = 0;
-        rc = geobpe_run(c, n_merges - done, &more);
-        if (n_done) *n_done = done + more;
-        return rc;
+        bool collapsed = false;
+        if ((rc = geobpe_pipeline_end(c)) || (rc = x_collapse(c, &collapsed))) return rc;
+        if (collapsed) {
+          int64_t more = 0;
+          rc = geobpe_run(c, n_merges - done, &more);
+          if (n_done) *n_done = done + more;
+          return rc;
+        }
+        if ((rc = geobpe_pipeline_begin(c))) return rc;  // (some rank declined: sharded, as before)
       }
-      if (lr.count <= c->mid_thresh) {
+      if (!c->mid_on && lr.count <= c->mid_thresh) {
         c->mid_on = true;
         // the middle regime's records are per (workgroup, key), not per owner and key: a
         // merge of the same size sends up to ~4x as many -- a slot that small would stall
         if (!c->x_fixed) capf = std::min(CAP_MAX, 4 * capf);
-      } else if (lr.count <= 2 * c->mid_thresh) {
+      } else if (!c->mid_on && lr.count <= 2 * c->mid_thresh) {
         win = std::min<int64_t>(win, 8);  // (close: poll sooner)
       }
     }

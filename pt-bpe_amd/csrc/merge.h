@@ -54,6 +54,16 @@ __device__ inline void out_store(V* p, const V& v) {
 #endif
 }
 
+// the record counts finder r sent owner o (cntK / cntD).  CNT_T = 1 keeps them finder-major,
+// so a finder's end writes whole lines (owner-major, its 2 x NBA counts were NBA-strided 4-B
+// writes: 2 x 65 536 partial lines a launch written back at k_find's end)
+#ifndef CNT_T
+#define CNT_T 0
+#endif
+__device__ inline int64_t cnt_at(const Dev& D, int32_t o, int32_t r) {
+  return CNT_T ? (int64_t)r * D.NBA + o : (int64_t)o * D.NBA + r;
+}
+
 // chunked per-owner posting log: entry k of owner o
 __device__ inline int64_t log_addr(const Dev& D, int o, int64_t k) {
   return (int64_t)D.pch[(int64_t)o * D.MAXCH + k / D.CHUNK] * D.CHUNK + k % D.CHUNK;
@@ -598,8 +608,8 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   }
   __syncthreads();
   for (int i = threadIdx.x; i < D.NBA; i += ABLOCK) {
-    D.cntK[(int64_t)i * D.NBA + r] = min(S.curK[i], SK);
-    D.cntD[(int64_t)i * D.NBA + r] = min(S.curD[i], SD);
+    D.cntK[cnt_at(D, i, r)] = min(S.curK[i], SK);
+    D.cntD[cnt_at(D, i, r)] = min(S.curD[i], SD);
   }
   if (threadIdx.x == 0) D.Lcnt[r] = min(S.n, (int32_t)D.LC);
 #if EARLY_LOADS
@@ -886,7 +896,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const int32_t w = t % nba, k0 = t / nba;
   const bool lane_ok = k0 < PER;
   const int64_t seg = (int64_t)j * nba + w;
-  const int32_t cK = D.cntK[seg], cD = D.cntD[seg];
+  const int32_t cK = D.cntK[cnt_at(D, j, w)], cD = D.cntD[cnt_at(D, j, w)];
 #if COMMIT_SPEC
   // speculative: the first PER records of every finder's slot in the first round
   // (~15 MB per launch, mostly empty slots; it held the prefix scans below ~4 us)
@@ -1248,7 +1258,7 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   const int64_t novf = st->place_novf, nko = st->place_nko;
   const int32_t nA = D.Lcnt[j];
   const LEntry eA = D.L[(int64_t)j * D.LC + min((int64_t)t, D.LC - 1)];
-  const int32_t cK = t < D.NBA ? D.cntK[(int64_t)t * D.NBA + j] : 0;
+  const int32_t cK = t < D.NBA ? D.cntK[cnt_at(D, t, j)] : 0;
   if (par < 0) return;  // (k_commit sets par only for a merge)
   dbg_stamp(D, 30);
   const int64_t oper = (novf + D.NBA - 1) / D.NBA;

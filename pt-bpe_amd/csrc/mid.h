@@ -25,6 +25,9 @@
 #pragma once
 // (included inside namespace gb)
 
+#ifndef MID_SPEC
+#define MID_SPEC 0
+#endif
 constexpr int MKC = 1024;   // k_mid_find: new-key dedupe slots per round (LDS)
 constexpr int MPK = 2048;   // appends: key grouping slots (LDS)
 constexpr int MID_APP = 32; // appending workgroups of k_mid_find (hash buckets of the keys)
@@ -281,7 +284,9 @@ __device__ inline int32_t mid_resolve(const Dev& D, u64 h1, u64 h2, int32_t len,
   return ht_resolve(D, k, s1, ht_probe(D, s1), claimed);
 }
 
-// mid_resolve with the key's count (+n) added in the same round trip (one rank): the add to
+// MID_SPEC = 1 (A/B; measured slower: default run 32.9 k -> 29.9 k merges/s, k_mid_find 18.2 ->
+// 19.1 us, profiles/r5_s1/): mid_resolve with the key's count (+n) added in the same round trip
+// (one rank): the add to
 // the first slot's count goes out beside the CAS, as k_commit's commit_resolve_counted does --
 // undone when another key holds the slot, whose key then joins the hot list (the undone add
 // may have hidden its theta crossing from the thread that made it)
@@ -614,8 +619,8 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       const int4 rp = S.rep[s];
       bool claimed;
       const u64 h1 = S.h1[s], h2 = S.h2[s];
-      const int32_t d = D.xrec ? mid_resolve(D, h1, h2, rp.x, &claimed)
-                               : mid_resolve_counted(D, S.hot, h1, h2, rp.x, S.cnt[s], F.th, &claimed);
+      const int32_t d = D.xrec || !MID_SPEC ? mid_resolve(D, h1, h2, rp.x, &claimed)
+                                            : mid_resolve_counted(D, S.hot, h1, h2, rp.x, S.cnt[s], F.th, &claimed);
       S.did[s] = d;
       if (d < 0) {
         if (D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, 0, -1);  // (no-op record)
@@ -627,7 +632,10 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       } else {
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
-      if (D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
+      if (D.xrec)
+        mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
+      else if (!MID_SPEC)
+        count_add_hot(D, S.hot, d, S.cnt[s], F.th);
     }
     __syncthreads();
     if (c0 == 0) dbg_stamp(D, 17);
