@@ -58,7 +58,7 @@ __device__ inline void out_store(V* p, const V& v) {
 // so a finder's end writes whole lines (owner-major, its 2 x NBA counts were NBA-strided 4-B
 // writes: 2 x 65 536 partial lines a launch written back at k_find's end)
 #ifndef CNT_T
-#define CNT_T 0
+#define CNT_T 1
 #endif
 __device__ inline int64_t cnt_at(const Dev& D, int32_t o, int32_t r) {
   return CNT_T ? (int64_t)r * D.NBA + o : (int64_t)o * D.NBA + r;
@@ -731,6 +731,9 @@ __device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nb
   return (int64_t)nba * nba * SK + (i - nE);
 }
 
+#ifndef COMMIT_CSPEC
+#define COMMIT_CSPEC 1
+#endif
 // commit_resolve with the key's count added in the same round trip: the add to the count of
 // the key's first slot goes out beside the CAS (the key is there unless another key took the
 // slot first: then the add is undone and the key resolved onward).  An unclaimed slot's count
@@ -787,23 +790,39 @@ __device__ __attribute__((always_inline)) inline void commit_fallback(const Dev&
   }
 }
 
+// the key id of a record this owner resolved (-1: none)
+__device__ __attribute__((always_inline)) inline int32_t commit_id_of(const Dev& D, CommitLds& S, const KRec& k) {
+  bool res;
+  const int32_t s = ckc_slot(S, k.pkey, false, &res);
+  if (s >= 0) {
+    if (S.ch1[s] != k.h1) {  // same probe key, other content
+      set_error(D, GEOBPE_EHASH, -13);
+      return -1;
+    }
+    return S.cid[s];
+  }
+  bool claimed;  // (round 1 resolved it on its own: find it again)
+  return ht_resolve(D, k.pkey, ht_first_slot(D, k.pkey), ht_probe(D, ht_first_slot(D, k.pkey)), &claimed);
+}
+
+// two records per thread in ONE publish round (r0 and the first extra e0): an owner with a
+// single record past a slot's first PER paid a whole second round (block scan, barrier,
+// ~3.5 us, profiles/r5_s2/timeline_ab_b.so.txt) -- and such owners end the launch
+__device__ __attribute__((always_inline)) inline void commit_publish2(const Dev& D, CommitLds& S, bool m0, const KRec& k0,
+                                                                      int64_t at0, bool m1, const KRec& k1, int64_t at1) {
+  const int32_t d0 = m0 ? commit_id_of(D, S, k0) : -1, d1 = m1 ? commit_id_of(D, S, k1) : -1;
+  const int32_t n0 = m0 && d0 >= 0 ? k0.n : 0, n1 = m1 && d1 >= 0 ? k1.n : 0;
+  int32_t tot;
+  const int32_t ex = block_excl_scan(n0 + n1, &tot, S.red);
+  if (m0) D.KSid[at0] = make_int2(d0 >= 0 ? d0 : -1, S.logok && d0 >= 0 ? (int32_t)(S.logpos + ex) : -1);
+  if (m1) D.KSid[at1] = make_int2(d1 >= 0 ? d1 : -1, S.logok && d1 >= 0 ? (int32_t)(S.logpos + ex + n0) : -1);
+  __syncthreads();
+  if (threadIdx.x == 0) S.logpos += tot;
+}
+
 // a record's key id and posting-log position (block-uniform: every thread calls it)
 __device__ __attribute__((always_inline)) inline void commit_publish(const Dev& D, CommitLds& S, bool mine, const KRec& k, int64_t at) {
-  int32_t d = -1;
-  if (mine) {
-    bool res;
-    const int32_t s = ckc_slot(S, k.pkey, false, &res);
-    if (s >= 0) {
-      d = S.cid[s];
-      if (S.ch1[s] != k.h1) {  // same probe key, other content
-        set_error(D, GEOBPE_EHASH, -13);
-        d = -1;
-      }
-    } else {  // (round 1 resolved it on its own: find it again)
-      bool claimed;
-      d = ht_resolve(D, k.pkey, ht_first_slot(D, k.pkey), ht_probe(D, ht_first_slot(D, k.pkey)), &claimed);
-    }
-  }
+  const int32_t d = mine ? commit_id_of(D, S, k) : -1;
   const int32_t n = mine && d >= 0 ? k.n : 0;
   int32_t tot;
   const int32_t ex = block_excl_scan(n, &tot, S.red);
@@ -1055,13 +1074,6 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     dbg_val(D, 7, nr + nE + nKO);
     dbg_val(D, 8, nd + nF);
   }
-  // ---- decrements of this owner's keys: one atomic per key, in flight under the resolves
-  // (a decrement cannot hide a theta crossing: a positive add that follows sees less)
-  if (!tod)
-    for (int i = t; i < AggT<12>::N; i += ABLOCK) {
-      const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
-      if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
-    }
   // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
   int32_t nlog = 0, nkeys = 0;
   for (int32_t s = t; s < CKC; s += ABLOCK) {
@@ -1077,7 +1089,14 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     k.g = rp.z;
     k.idR = rp.w;
     const int32_t n = S.cn[s];
-    const int32_t d = tod ? commit_resolve(D, S, k) : commit_resolve_counted(D, S, hot, k, n, th);
+    int32_t d;
+    if (tod || !COMMIT_CSPEC) {
+      bool claimed;
+      d = commit_resolve(D, S, k, &claimed);
+      if (d >= 0 && !tod) count_add_hot(D, hot, d, n, th);
+    } else {
+      d = commit_resolve_counted(D, S, hot, k, n, th);
+    }
     S.cid[s] = d >= 0 ? d : -2;
     if (d >= 0) {
       if (tod && !D.xrec) touch_add(D, tb, d, n);  // (direct records: written below)
@@ -1085,6 +1104,14 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       nkeys++;
     }
   }
+  // ---- decrements of this owner's keys: one atomic per key, in flight under the log
+  // reservation and the publish round (a decrement cannot hide a theta crossing: a positive
+  // add that follows sees less; before the resolves they queued ahead of them)
+  if (!tod)
+    for (int i = t; i < AggT<12>::N; i += ABLOCK) {
+      const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
+      if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
+    }
   if (D.dbg) {
     int32_t tk;
     block_excl_scan(nkeys, &tk, S.red);
@@ -1127,21 +1154,16 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   // ---- round 2: every record's key id and posting-log position (k_place writes pk
   // and the log entries of its occurrence slots); the first PER records per finder
   // are still in registers
-  commit_publish(D, S, mine0, r0, seg * SK + k0);
+  commit_publish2(D, S, mine0, r0, seg * SK + k0, he && (t < nE || owner_of_key(D, e0.pkey) == j), e0, at0);
   dbg_stamp(D, 53);
   dbg_val(D, 54, nE);
   dbg_val(D, 55, nKO);
-  for (int32_t i0 = 0; i0 < nE + nKO; i0 += ABLOCK) {  // block-uniform
+  for (int32_t i0 = ABLOCK; i0 < nE + nKO; i0 += ABLOCK) {  // block-uniform (rare: more than ABLOCK extras)
     const int32_t i = i0 + t;
     const bool in = i < nE + nKO;
     KRec k;
     int64_t at = 0;
-    if (i0 == 0) {  // (round 1's first iteration loaded exactly these)
-      if (in) {
-        k = e0;
-        at = at0;
-      }
-    } else if (in) {
+    if (in) {
       at = extra_at(D, s_preE, nba, j, PER, nE, i);
       k = D.KS[at];
     }

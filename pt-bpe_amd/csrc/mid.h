@@ -150,15 +150,15 @@ __device__ inline void mid_claimed(const Dev& D, MidFindLds& S, int32_t d) {
 // counts beside them, the claimed keys from this workgroup's klist chunk (a reservation only
 // when the chunk runs out) -- no shared counter, so the find workgroups ending together do not
 // queue on one address
-__device__ inline void mid_flush_lists(const Dev& D, MidFindLds& S, int par, int32_t w) {
+__device__ inline void mid_flush_lists(const Dev& D, MidFindLds& S, int par, int32_t w, int64_t kc0, int64_t kc1) {
   State* st = D.st;
   const int32_t t = threadIdx.x;
   __syncthreads();
   const int32_t a = min(S.ntm, MTM), b = min(S.nth, MTH), c = min(S.nkl, MKL);
   if (t == 0) {
     D.mcnt[par * NBA_MAX + w] = make_int4(a, b, S.nm, 0);
-    if (c) {
-      int64_t k0 = D.kchunk[2 * w], k1 = D.kchunk[2 * w + 1];
+    if (c) {  // (the chunk state came with the launch's first loads: no round trip here)
+      int64_t k0 = kc0, k1 = kc1;
       if (k1 - k0 < c) {
         const int64_t sz = max((int64_t)KL_CHUNK, (int64_t)c);
         k0 = (int64_t)atomicAdd((unsigned long long*)&st->U, (unsigned long long)sz);
@@ -487,6 +487,7 @@ __device__ inline void mid_new_token(const Dev& D, const Sel& sel) {
 struct MidPre {  // (scalars: an indexed pair would be a private array, which the compiler puts in LDS)
   int32_t pp, theta, seg0, seg1;
   int64_t spill0, spill1;
+  int64_t kc0, kc1;  // this workgroup's klist chunk (its claims' list positions, mid_flush_lists)
 };
 __device__ inline MidPre mid_pre(const Dev& D, int32_t w) {
   MidPre m;
@@ -497,6 +498,8 @@ __device__ inline MidPre mid_pre(const Dev& D, int32_t w) {
   m.seg1 = D.mcnt[NBA_MAX + w].y;
   m.spill0 = st->mid_nh[0];
   m.spill1 = st->mid_nh[1];
+  m.kc0 = D.kchunk[2 * w];
+  m.kc1 = D.kchunk[2 * w + 1];
   return m;
 }
 
@@ -612,6 +615,14 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     if (vr && sr < 0) mid_single(D, S, F, hr.h1, hr.h2, hr.len, hr.idL, hr.g, hr.idR, hr.target);
     __syncthreads();
     if (c0 == 0) dbg_stamp(D, 16);
+    // the last round's walks are done, so every decrement is staged: out now, one atomic per
+    // key, in flight under the resolves and the list flush (at the launch's end they were the
+    // last memory operations to drain)
+    if (!D.xrec && c0 + ABLOCK >= ncand)
+      for (int i = t; i < AggT<11>::N; i += ABLOCK) {
+        const int32_t k = S.agg.key[i], v = S.agg.val[i];
+        if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
+      }
     const int32_t nocc = S.nocc;
     const int64_t xb = D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
     for (int32_t q = t; q < nocc; q += ABLOCK) {
@@ -656,7 +667,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     if (t == 0) S.nocc = 0;
     __syncthreads();
   }
-  mid_flush_lists(D, S, F.par, w);
+  mid_flush_lists(D, S, F.par, w, M.kc0, M.kc1);
   dbg_stamp(D, 12);
   // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
   if (D.xrec) {  // as records: the nonzero slots, compacted behind one reservation
@@ -679,11 +690,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       const int32_t k = S.agg.key[i], v = S.agg.val[i];
       if (k >= 0 && v != 0) mid_put_id(D, j++, k, v);
     }
-  } else {
-    for (int i = t; i < AggT<11>::N; i += ABLOCK) {
-      const int32_t k = S.agg.key[i], v = S.agg.val[i];
-      if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
-    }
+  } else {  // (the decrements went out with the last round)
     // (mid_dec_agg: every pair of W is gone; an add, not a store: another key's speculative
     // add to this slot and its undo may straddle it, mid_resolve_counted)
     if (w == 0 && t == 0) atomicAdd(&D.count[F.W], -F.maxc);

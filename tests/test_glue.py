@@ -467,7 +467,7 @@ def test_rmsd_mode_glue_opt_host_logic_matches_reference(name, host_glue):
 
 
 @pytest.mark.skipif(os.environ.get("GEOBPE_SLOW_TESTS") != "1", reason="~20 min on one CPU core (GEOBPE_SLOW_TESTS=1)")
-@pytest.mark.parametrize("name", PARETO)
+@pytest.mark.parametrize("name", PARETO + HELD_OUT)
 def test_rmsd_mode_pareto_host_logic_matches_reference(name, host_glue):
     """The pareto fixture exactly, with the torch optimiser restatement on the CPU (600 chain
     optimisations): passed in the build container (19.5 min); the device run of the same

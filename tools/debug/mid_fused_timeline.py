@@ -8,6 +8,8 @@ import ctypes
 import os
 import sys
 
+os.environ.setdefault("GEOBPE_SPEC", "0")  # (no idle iteration after each run: it would stamp over the merge's rows)
+
 import numpy as np
 
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "pt-bpe_amd"))
