@@ -384,9 +384,10 @@ def main():
                      "frac": round(bc / t_pass / 1e9 / HBM_PEAK_GBS, 4),
                      "ms": {k: round(v, 4) for k, v in bin_ms.items()}},
             "layout_pack_us": round(pack_ms * 1000, 2),
-            # k_pack (pk into the token records for the merge loop) follows the bin pass, outside the
-            # timed merges; bin pass + pack together
+            # the merge loop's token records: k_bin_count writes them itself since round 5
+            # (FUSE_PACK: pack_us 0); before, k_pack copied pk into them after the pass
             "pack_us": round(pack_ms * 1000, 2),
+            "pack_fused": pack_ms == 0,
             "pass_and_pack": {"time_us": round(t_pass * 1e6 + pack_ms * 1000, 2),
                               "frac": round(bc / (t_pass + pack_ms / 1000.0) / 1e9 / HBM_PEAK_GBS, 4)},
         }

@@ -28,13 +28,21 @@
 // (inside namespace gb: kernels.h includes this file)
 
 constexpr int BIN_VEC = 4;        // residue slots per int4 group
+#ifndef FUSE_PACK
+#define FUSE_PACK 1
+#endif
 #ifndef BIN_GPT_DEF
-#define BIN_GPT_DEF 4
+#define BIN_GPT_DEF (FUSE_PACK ? 3 : 4)  // (4 with the fused record writes spills 12 VGPRs)
 #endif
 #ifndef BIN_EXP
 #define BIN_EXP 0
 #endif
 constexpr int BIN_GPT = BIN_GPT_DEF;  // groups per thread per step (loads in flight together)
+// FUSE_PACK = 1: k_bin_count writes the merge loop's token records itself ({label, 1 | 16-bit
+// junction symbol << 16, previous slot, pair key}: one 64-B line per group of 4 residues) and
+// the 16-bit junction symbols, and the list kernels write the listed pairs' keys into the
+// records -- no pk / fp arrays and no k_pack pass over them afterwards (VERDICT r4 item 5:
+// k_pack was ~285 us after a ~300 us bin pass)
 constexpr int BIN_NC = 1 << 14;   // max cube cells (64 KB of LDS counts)
 constexpr int BIN_SAMPLE = 16;    // the sample: the first 1/16 of each workgroup's range
 constexpr int BIN_MAXSYM = 2048;  // label / junction-symbol tables (K0, B^3 <= 2048)
@@ -309,11 +317,28 @@ __global__ __launch_bounds__(BLOCK) void k_bin_precube(Dev D, BinWork W) {
 
 __device__ inline uint16_t bin_fp(int32_t k) { return k >= 0 ? key_fp(k) : (uint16_t)0xFFFF; }
 
+// a listed pair's key: into its token record (FUSE_PACK), else the streamed pk / fp for k_pack
+__device__ inline void bin_set_pk(const Dev& D, int64_t g, int32_t k) {
+  if (FUSE_PACK) {
+    D.tok[g].w = k;
+  } else {
+    D.pk[g] = k;
+    D.fp[g] = bin_fp(k);
+  }
+}
+
 // a pair of k_bin_count outside the pre-claimed cube: this workgroup's list
 __device__ inline void bin_list(const BinWork& W, int32_t* s_nool, int2* ool, int32_t la, int32_t gs, int32_t lb,
                                 int64_t g) {
   const int32_t j = atomicAdd(s_nool, 1);
   if (j < W.ool_cap) ool[j] = make_int2((int32_t)g, bin_triple(la, gs, lb, W.G, W.K0));
+}
+
+// token record of residue g at the initial state (every token one residue): pair key k, junction
+// symbol gs (-1: chain end), junction symbol of g - 1 (-1: g starts its chain)
+__device__ inline int4 bin_tok(const Dev& D, int64_t g, int32_t lab, int32_t gs, int32_t gprev, int32_t k) {
+  const uint32_t g16 = gs < 0 ? 0xFFFFu : (uint32_t)gs;
+  return make_int4(lab, D.gs16 ? (int32_t)(1u | (g16 << 16)) : 1, gprev >= 0 ? (int32_t)(g - 1) : -1, k);
 }
 
 // the pass over every pair.  LDS: the cube's key ids and counts, the cube
@@ -394,7 +419,24 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
         else if (ss[q][u] >= 0)
           bin_list(W, &s_nool, ool, ts[q][u], ss[q][u], ts[q][u + 1], v * BIN_VEC + u);
       }
-      if (v < hi) {
+      if (FUSE_PACK) {
+        // the junction symbol before the group: the previous lane's group (DPP wave_shr:1), the
+        // wave's first lane loads it
+        int32_t gp = __builtin_amdgcn_update_dpp(-2, ss[q][BIN_VEC - 1], 0x138, 0xF, 0xF, false);
+        if (wave_lane() == 0 && v < hi) gp = v > 0 ? D.gsym[v * BIN_VEC - 1] : -1;
+        if (v < hi) {
+          const int64_t g = v * BIN_VEC;
+          int4* tk = D.tok + g;
+          tk[0] = bin_tok(D, g, ts[q][0], ss[q][0], gp, k[q][0]);
+          tk[1] = bin_tok(D, g + 1, ts[q][1], ss[q][1], ss[q][0], k[q][1]);
+          tk[2] = bin_tok(D, g + 2, ts[q][2], ss[q][2], ss[q][1], k[q][2]);
+          tk[3] = bin_tok(D, g + 3, ts[q][3], ss[q][3], ss[q][2], k[q][3]);
+          if (D.gs16) {
+            auto h16 = [](int32_t s) { return (uint16_t)(s < 0 ? 0xFFFFu : (uint32_t)s); };
+            reinterpret_cast<ushort4*>(D.gs16)[v] = make_ushort4(h16(ss[q][0]), h16(ss[q][1]), h16(ss[q][2]), h16(ss[q][3]));
+          }
+        }
+      } else if (v < hi) {
         pv[v] = make_int4(k[q][0], k[q][1], k[q][2], k[q][3]);
         if (!(BIN_EXP & 1)) fv[v] = make_ushort4(bin_fp(k[q][0]), bin_fp(k[q][1]), bin_fp(k[q][2]), bin_fp(k[q][3]));
       }
@@ -413,8 +455,13 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
         else
           bin_list(W, &s_nool, ool, la, sy, lb, g);
       }
-      D.pk[g] = k;
-      D.fp[g] = bin_fp(k);
+      if (FUSE_PACK) {
+        D.tok[g] = bin_tok(D, g, D.lab0[g], sy, g > 0 ? D.gsym[g - 1] : -1, k);
+        if (D.gs16) D.gs16[g] = (uint16_t)(sy < 0 ? 0xFFFFu : (uint32_t)sy);
+      } else {
+        D.pk[g] = k;
+        D.fp[g] = bin_fp(k);
+      }
     }
   }
   __syncthreads();
@@ -522,8 +569,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_ool_fix(Dev D, BinWork W) {
   for (int32_t j = threadIdx.x; j < n; j += ABLOCK) {
     const int2 e = ool[j];
     const int32_t k = W.dcnt[e.y];
-    D.pk[e.x] = k;
-    D.fp[e.x] = bin_fp(k);
+    bin_set_pk(D, e.x, k);
   }
 }
 
@@ -575,8 +621,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_ool(Dev D, BinWork W, int to_del
         }
         global_add(D, slot, 1, to_delta != 0);
       }
-      D.pk[e.x] = slot;
-      D.fp[e.x] = bin_fp(slot);
+      bin_set_pk(D, e.x, slot);
       ool[j].y = -1;
     } else {
       ool[j].y = at;
@@ -610,8 +655,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_ool(Dev D, BinWork W, int to_del
     const int2 e = ool[j];
     if (e.y < 0) continue;
     const int32_t k = s_id[e.y];
-    D.pk[e.x] = k;
-    D.fp[e.x] = bin_fp(k);
+    bin_set_pk(D, e.x, k);
   }
   cb_flush(D, cb);
   if (threadIdx.x == 0) {

@@ -115,6 +115,18 @@ struct State {
   int32_t pad6;
 };
 
+// k_select -> k_find (FIND_HDR): region r's candidates of the winner, found by the select's
+// workgroup once the winner is known -- the bucket bounds in r's posting index, r's share of the
+// winner owner's posting log and the pool chunks that share lies in -- so that k_find's first
+// round of loads holds them and its second the candidates themselves (round 4's k_find loaded
+// the bucket offsets and log length, then the chunk table, then the candidates: two more rounds)
+constexpr int FH_CH = 4;  // chunk ids carried (a share spanning more reads the chunk table)
+struct FindHdr {
+  int32_t lo, n1;    // the bucket of W in region r's posting index: post[r * PR + lo .. + n1)
+  int32_t ls0, ls1;  // region r's share of the owner's log: entries [ls0, ls1)
+  int32_t ch[FH_CH]; // pool chunks of log chunks ls0 / CHUNK, + 1, ...
+};
+
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
 // and the host read it).  Every mark workgroup computes the same decision.
 constexpr int SEL_MERGE = 0, SEL_SKIP = 1, SEL_DONE = 2, SEL_STALL = 3;  // STALL: mid.h, lists being rebuilt
@@ -237,7 +249,8 @@ struct Dev {
   KRec* KO;         // overflow: key records past their fixed slots
   int64_t KO_cap;
   int2 *KSid, *KOid;  // k_commit -> k_place: (key id, posting-log position) per record
-  int32_t* T;       // [find wg][TC]: occurrence slots grouped by new key
+  int2* T;          // [find wg][TC]: {occurrence slot, its key record (KS index)} grouped by new key
+  int32_t* Tcnt;    // [find wg]: T entries
   int64_t TC;
   // optional phase timeline (geobpe_debug_timeline): DBG_SLOTS wall-clock stamps per workgroup
   int64_t* dbg;
@@ -273,6 +286,7 @@ struct Dev {
   LogRec* log;
   State* st;
   Sel* sel;  // [2], by launch parity
+  struct FindHdr* fh;  // [NBA]: k_select's per-region candidate bounds for k_find (FIND_HDR)
 };
 
 // ------------------------------------------------------------------ arithmetic

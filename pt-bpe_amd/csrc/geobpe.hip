@@ -698,7 +698,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   memset(c->h_state, 0, sizeof(State));
   c->h_state->place_par = -1;
   int rc;
-  if ((rc = dalloc(c, &c->D.st, 1, 0)) || (rc = dalloc(c, &c->D.sel, 2, 0))) return rc;
+  if ((rc = dalloc(c, &c->D.st, 1, 0)) || (rc = dalloc(c, &c->D.sel, 2, 0)) || (rc = dalloc(c, &c->D.fh, NBA_MAX, 0))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->D.st, c->h_state, sizeof(State), hipMemcpyHostToDevice, c->stream));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -804,7 +804,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
       (rc = dalloc(c, &D.pnch, c->nba, 0)) || (rc = dalloc(c, &D.pfill, c->nba, 0)) ||
       (rc = dalloc(c, &D.KS, (int64_t)c->nba * c->nba * SK + D.KO_cap)) || (rc = dalloc(c, &D.cntK, (int64_t)c->nba * c->nba, 0)) ||
       (rc = dalloc(c, &D.DS, (int64_t)c->nba * c->nba * SD)) || (rc = dalloc(c, &D.cntD, (int64_t)c->nba * c->nba, 0)) ||
-      (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) ||
+      (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) || (rc = dalloc(c, &D.Tcnt, c->nba, 0)) ||
       (rc = dalloc(c, &D.KSid, (int64_t)c->nba * c->nba * SK + D.KO_cap)))
     return rc;
   D.KO = D.KS + (int64_t)c->nba * c->nba * SK;  // (one allocation: a record index into KS covers both)
@@ -1083,7 +1083,7 @@ int geobpe_bin(geobpe_ctx* c) {
         hipLaunchKernelGGL(k_bin_verify, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
       }
     }
-    enqueue_pack(c);
+    if (!FUSE_PACK) enqueue_pack(c);  // (fused: k_bin_count wrote the token records)
     HIPCHK(c, hipGetLastError());
     rc = sync_state(c);
     if (!rc) {

@@ -927,6 +927,9 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
   dbg_stamp(D, 26);
 }
 
+#ifndef FIND_HDR
+#define FIND_HDR 1
+#endif
 __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par, int run_end) {
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
@@ -944,7 +947,29 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par, int run_end) 
     __syncthreads();  // every thread has read dgen
     if (threadIdx.x == 0) st->dgen = g;
   }
-  select_core<false>(D, par, S, s_red, nullptr, run_end);
+  __shared__ Sel s_sel;
+  select_core<false>(D, par, S, s_red, &s_sel, run_end);
+#if FIND_HDR
+  __syncthreads();  // (s_sel)
+  if (s_sel.decision == SEL_MERGE && !s_sel.rebuild && s_sel.W >= 0 && (int32_t)threadIdx.x < D.NBA) {
+    // region t's candidates of the winner for k_find (struct FindHdr)
+    const int32_t t = threadIdx.x, W = s_sel.W, o = s_sel.wown;
+    const int32_t* off = D.poff + (int64_t)t * (NBKT + 1);
+    const uint32_t bk = post_bkt(W);
+    const int32_t lo = off[bk], hi = off[bk + 1];
+    const int64_t nlog = log_len(D, o);
+    FindHdr h;
+    h.lo = lo;
+    h.n1 = hi - lo;
+    h.ls0 = (int32_t)(nlog * t / D.NBA);
+    h.ls1 = (int32_t)(nlog * (t + 1) / D.NBA);
+    const int64_t c0 = h.ls0 / D.CHUNK;
+#pragma unroll
+    for (int k = 0; k < FH_CH; k++)
+      h.ch[k] = h.ls1 > h.ls0 && c0 + k <= (h.ls1 - 1) / D.CHUNK ? D.pch[(int64_t)o * D.MAXCH + c0 + k] : -1;
+    D.fh[t] = h;
+  }
+#endif
 }
 
 // merge replay (bin/induce.py): merge t is the trained

@@ -188,6 +188,7 @@ struct FindLds {
       u64 kh1[FKC];
       int32_t kcnt[FKC];
       int32_t kst[FKC];
+      int32_t kat[FKC];  // the key's record (KS index) this round: T entries carry it (k_place)
       AggT<12> agg;  // count decrements of this workgroup
     } m;
   } u;
@@ -223,8 +224,9 @@ __device__ inline void emit_occ(const Dev& D, FindCtx& F, int32_t* s_n, int32_t 
 }
 
 // a key record into its owner's slot of this finder (or the overflow list)
-__device__ inline void emit_krec(const Dev& D, const FindCtx& F, int32_t* curK, const FHalf& h, int32_t n,
-                                 int32_t tstart) {
+// (returns the record's index in KS -- the overflow list KO is KS's tail -- or -1)
+__device__ inline int32_t emit_krec(const Dev& D, const FindCtx& F, int32_t* curK, const FHalf& h, int32_t n,
+                                    int32_t tstart) {
   KRec k;
   k.pkey = h.pkey;
   k.h1 = h.h1;
@@ -238,14 +240,17 @@ __device__ inline void emit_krec(const Dev& D, const FindCtx& F, int32_t* curK, 
   const int o = owner_of_key(D, h.pkey);
   const int32_t j = atomicAdd(&curK[o], 1);
   if (j < SK) {
-    out_store(&D.KS[((int64_t)o * D.NBA + F.r) * SK + j], k);
-  } else {
-    const int64_t x = atomicAdd((unsigned long long*)&D.st->nko2[F.par], 1ULL);
-    if (x < D.KO_cap)
-      D.KO[x] = k;
-    else
-      set_error(D, GEOBPE_ECAPACITY, -41);
+    const int64_t at = ((int64_t)o * D.NBA + F.r) * SK + j;
+    out_store(&D.KS[at], k);
+    return (int32_t)at;
   }
+  const int64_t x = atomicAdd((unsigned long long*)&D.st->nko2[F.par], 1ULL);
+  if (x < D.KO_cap) {
+    D.KO[x] = k;
+    return (int32_t)((int64_t)D.NBA * D.NBA * SK + x);
+  }
+  set_error(D, GEOBPE_ECAPACITY, -41);
+  return -1;
 }
 __device__ inline void emit_single(const Dev& D, const FindCtx& F, int32_t* curK, const FHalf& h) {
   emit_krec(D, F, curK, h, 1, -(h.target + 1));
@@ -409,6 +414,9 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   const int32_t r = blockIdx.x;
   dbg_stamp(D, 10);
   const Sel sel = D.sel[par];
+#if FIND_HDR
+  const FindHdr fh = D.fh[r];  // (valid for a merge without a posting rebuild: k_select wrote it)
+#endif
 #if EARLY_LOADS
   // EHASH check of the keys the previous commit / import found: the first ABLOCK records
   // are loaded now and compared after the merge work (their two dependent rounds used to
@@ -467,15 +475,27 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
     }
     queued = S.qn <= FMQ;
   }
+  bool hdr = false;  // (the log chunks of the share from k_select's header)
   if (W >= 0 && !queued) {
-    const int32_t* off = D.poff + (int64_t)r * (NBKT + 1);
-    const uint32_t bk = post_bkt(W);
-    lo = off[bk];
-    n1 = off[bk + 1] - lo;
+#if FIND_HDR
     if (!sel.rebuild) {
-      const int64_t nlog = log_len(D, o);
-      ls0 = nlog * r / D.NBA;
-      ls1 = nlog * (r + 1) / D.NBA;
+      lo = fh.lo;
+      n1 = fh.n1;
+      ls0 = fh.ls0;
+      ls1 = fh.ls1;
+      hdr = ls1 <= ls0 || (ls1 - 1) / D.CHUNK - ls0 / D.CHUNK < FH_CH;
+    } else
+#endif
+    {
+      const int32_t* off = D.poff + (int64_t)r * (NBKT + 1);
+      const uint32_t bk = post_bkt(W);
+      lo = off[bk];
+      n1 = off[bk + 1] - lo;
+      if (!sel.rebuild) {
+        const int64_t nlog = log_len(D, o);
+        ls0 = nlog * r / D.NBA;
+        ls1 = nlog * (r + 1) / D.NBA;
+      }
     }
   }
   // dedupe + aggregation state
@@ -501,7 +521,19 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       __syncthreads();
       const int64_t c1 = min(ntot, c0 + FMQ);
       for (int64_t i = c0 + threadIdx.x; i < c1; i += ABLOCK) {
-        const int2 e = i < n1 ? P[i] : D.pool[log_addr(D, o, ls0 + (i - n1))];
+        int2 e;
+        if (i < n1) {
+          e = P[i];
+        } else {
+          const int64_t k = ls0 + (i - n1);
+#if FIND_HDR
+          if (hdr) {
+            const int32_t ch = fh.ch[k / D.CHUNK - ls0 / D.CHUNK];
+            e = D.pool[(int64_t)ch * D.CHUNK + k % D.CHUNK];
+          } else
+#endif
+            e = D.pool[log_addr(D, o, k)];
+        }
         if (e.x == W) S.q[atomicAdd(&S.qn, 1)] = e.y;
       }
       __syncthreads();
@@ -564,21 +596,23 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       const int64_t tbase = (int64_t)r * D.TC + S.tb;
       if (vl) {
         if (sl >= 0 && fits) {
-          out_store(&D.T[tbase + S.u.m.kst[sl] + kl], hl.target);
-          if (rl) emit_krec(D, F, S.curK, hl, S.u.m.kcnt[sl], (int32_t)(tbase + S.u.m.kst[sl]));
+          if (rl) S.u.m.kat[sl] = emit_krec(D, F, S.curK, hl, S.u.m.kcnt[sl], (int32_t)(tbase + S.u.m.kst[sl]));
         } else {
           emit_single(D, F, S.curK, hl);
         }
       }
       if (vr) {
         if (sr >= 0 && fits) {
-          out_store(&D.T[tbase + S.u.m.kst[sr] + kr], hr.target);
-          if (rr) emit_krec(D, F, S.curK, hr, S.u.m.kcnt[sr], (int32_t)(tbase + S.u.m.kst[sr]));
+          if (rr) S.u.m.kat[sr] = emit_krec(D, F, S.curK, hr, S.u.m.kcnt[sr], (int32_t)(tbase + S.u.m.kst[sr]));
         } else {
           emit_single(D, F, S.curK, hr);
         }
       }
       __syncthreads();
+      // T entries {occurrence slot, the key's record}: k_place joins them with the record's key
+      // id without first loading the record (one dependent round less on the select launch)
+      if (vl && sl >= 0 && fits) out_store(&D.T[tbase + S.u.m.kst[sl] + kl], make_int2(hl.target, S.u.m.kat[sl]));
+      if (vr && sr >= 0 && fits) out_store(&D.T[tbase + S.u.m.kst[sr] + kr], make_int2(hr.target, S.u.m.kat[sr]));
       if (rl && sl >= 0) {
         S.u.m.kkey[sl] = 0;
         S.u.m.kcnt[sl] = 0;
@@ -611,7 +645,10 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
     D.cntK[cnt_at(D, i, r)] = min(S.curK[i], SK);
     D.cntD[cnt_at(D, i, r)] = min(S.curD[i], SD);
   }
-  if (threadIdx.x == 0) D.Lcnt[r] = min(S.n, (int32_t)D.LC);
+  if (threadIdx.x == 0) {
+    D.Lcnt[r] = min(S.n, (int32_t)D.LC);
+    D.Tcnt[r] = S.tb;  // (T entries of this region: [r * TC, + Tcnt))
+  }
 #if EARLY_LOADS
   check_found_tail(D, r, nchk, chk0);
 #endif
@@ -740,12 +777,11 @@ __device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nb
 // is 0, so a claim's count is its occurrence total either way.  The undone add may have hidden
 // a theta crossing of the slot's own key from the thread that made it: that key joins the hot
 // list unconditionally (a listed key under theta is a stale entry the select skips)
-__device__ __attribute__((always_inline)) inline int32_t commit_resolve_counted(const Dev& D, CommitLds& S, HotApp& hot,
-                                                                                const KRec& k, int32_t n, int32_t th) {
+// (the second half: the CAS and the add were issued by the caller, old / c0 their results)
+__device__ __attribute__((always_inline)) inline int32_t commit_resolve_finish(const Dev& D, CommitLds& S, HotApp& hot,
+                                                                               const KRec& k, int32_t n, int32_t th,
+                                                                               u64 s0, u64 old, int32_t c0) {
   bool claimed = false;
-  const u64 s0 = ht_first_slot(D, k.pkey);
-  const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s0], 0ULL, (unsigned long long)k.pkey);
-  const int32_t c0 = atomicAdd(&D.count[s0], n);
   int32_t d;
   if (old == 0 || old == k.pkey) {
     claimed = old == 0;
@@ -766,6 +802,22 @@ __device__ __attribute__((always_inline)) inline int32_t commit_resolve_counted(
     emit_check(D, &S.chk, d, k.len, k.h1, k.h2);
   }
   return d;
+}
+
+// the key record of table slot s (LDS)
+__device__ inline KRec commit_key_at(const CommitLds& S, int32_t s) {
+  KRec k;
+  k.pkey = S.ckey[s];
+  k.h1 = S.ch1[s];
+  k.h2 = S.ch2[s];
+  const int4 rp = S.crep[s];
+  k.len = rp.x;
+  k.idL = rp.y;
+  k.g = rp.z;
+  k.idR = rp.w;
+  k.n = S.cn[s];
+  k.tstart = 0;
+  return k;
 }
 
 // a count change k_commit could not stage: a record (pipelined), the global count or the delta
@@ -925,6 +977,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const Sel sel = D.sel[par];
   const int32_t th = st->theta;
   const int32_t pn = D.pnch[j], pf = D.pfill[j];
+  const int32_t plog_ovf0 = st->plog_ovf;  // (read with the first round: the log reservation needs it)
   const int64_t nko_raw = st->nko2[par];
   const int64_t novf_raw = j == 0 ? st->L_ovf2[par] : 0;
 #if EARLY_KCHUNK
@@ -1074,9 +1127,61 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     dbg_val(D, 7, nr + nE + nKO);
     dbg_val(D, 8, nd + nF);
   }
+  // ---- posting-log space for this merge's new pairs of this owner (one reservation), sized from
+  // round 1's occurrence totals (a key that then fails to resolve only leaves its space unused):
+  // the reservation's returning atomic on the pool cursor is in flight under the resolves, not
+  // after them (~2-4 us on the owners that open a chunk)
+  int64_t lbase = 0;
+  int32_t lneed = 0, lc1 = 0;
+  {
+    int32_t mine_n = 0;
+    for (int32_t s = t; s < CKC; s += ABLOCK) mine_n += S.ckey[s] != 0 ? S.cn[s] : 0;
+    int32_t tot;
+    block_excl_scan(mine_n, &tot, S.red);
+    if (t == 0) {
+      const int64_t add = (int64_t)tot + S.fbn;  // (+ records whose key did not fit the dedupe table)
+      const int64_t p0 = pn > 0 ? (int64_t)(pn - 1) * D.CHUNK + pf : 0;
+      S.logpos = p0;
+      S.logok = 0;
+      lc1 = (int32_t)((p0 + add + D.CHUNK - 1) / D.CHUNK);  // chunks [0, lc1) hold the log
+      if (!plog_ovf0 && lc1 - (int32_t)(p0 / D.CHUNK) <= LOG_CH_MAX && lc1 <= D.MAXCH) {
+        lneed = max(0, lc1 - pn);
+        lbase = lneed ? (int64_t)atomicAdd((unsigned long long*)&st->pool_used, (unsigned long long)lneed) : 0;
+      } else {
+        lneed = -1;
+      }
+    }
+  }
   // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
-  int32_t nlog = 0, nkeys = 0;
-  for (int32_t s = t; s < CKC; s += ABLOCK) {
+  int32_t nkeys = 0;
+  if (!tod && COMMIT_CSPEC) {
+    // this thread's two table slots: both keys' CAS and count add out before any result is used
+    static_assert(CKC == 2 * ABLOCK, "two commit table slots per thread");
+    const u64 ka = S.ckey[t], kb = S.ckey[t + ABLOCK];
+    const int32_t na = S.cn[t], nb = S.cn[t + ABLOCK];
+    const u64 sa = ht_first_slot(D, ka), sb = ht_first_slot(D, kb);
+    u64 oa = 0, ob = 0;
+    int32_t ca = 0, cb = 0;
+    if (ka) {
+      oa = atomicCAS((unsigned long long*)&D.ht_key[sa], 0ULL, (unsigned long long)ka);
+      ca = atomicAdd(&D.count[sa], na);
+    }
+    if (kb) {
+      ob = atomicCAS((unsigned long long*)&D.ht_key[sb], 0ULL, (unsigned long long)kb);
+      cb = atomicAdd(&D.count[sb], nb);
+    }
+    if (ka) {
+      const int32_t d = commit_resolve_finish(D, S, hot, commit_key_at(S, t), na, th, sa, oa, ca);
+      S.cid[t] = d >= 0 ? d : -2;
+      if (d >= 0) nkeys++;
+    }
+    if (kb) {
+      const int32_t d = commit_resolve_finish(D, S, hot, commit_key_at(S, t + ABLOCK), nb, th, sb, ob, cb);
+      S.cid[t + ABLOCK] = d >= 0 ? d : -2;
+      if (d >= 0) nkeys++;
+    }
+  }
+  for (int32_t s = t; s < CKC && (tod || !COMMIT_CSPEC); s += ABLOCK) {
     const u64 key = S.ckey[s];
     if (key == 0) continue;
     KRec k;
@@ -1089,18 +1194,12 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     k.g = rp.z;
     k.idR = rp.w;
     const int32_t n = S.cn[s];
-    int32_t d;
-    if (tod || !COMMIT_CSPEC) {
-      bool claimed;
-      d = commit_resolve(D, S, k, &claimed);
-      if (d >= 0 && !tod) count_add_hot(D, hot, d, n, th);
-    } else {
-      d = commit_resolve_counted(D, S, hot, k, n, th);
-    }
+    bool claimed;
+    const int32_t d = commit_resolve(D, S, k, &claimed);
+    if (d >= 0 && !tod) count_add_hot(D, hot, d, n, th);
     S.cid[s] = d >= 0 ? d : -2;
     if (d >= 0) {
       if (tod && !D.xrec) touch_add(D, tb, d, n);  // (direct records: written below)
-      nlog += n;
       nkeys++;
     }
   }
@@ -1128,26 +1227,13 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       atomicAdd((unsigned long long*)&st->stat_drec, (unsigned long long)(td + nF));
     }
   }
-  // posting-log space for this merge's new pairs of this owner (one reservation)
-  {
-    int32_t tot;
-    block_excl_scan(nlog, &tot, S.red);
-    if (t == 0) {
-      const int64_t add = (int64_t)tot + S.fbn;  // (+ records whose key did not fit the dedupe table)
-      const int64_t p0 = pn > 0 ? (int64_t)(pn - 1) * D.CHUNK + pf : 0;
-      S.logpos = p0;
-      S.logok = 0;
-      const int32_t c1 = (int32_t)((p0 + add + D.CHUNK - 1) / D.CHUNK);  // chunks [0, c1) hold the log
-      if (!st->plog_ovf && c1 - (int32_t)(p0 / D.CHUNK) <= LOG_CH_MAX && c1 <= D.MAXCH) {
-        const int32_t need = max(0, c1 - pn);
-        const int64_t base = need ? (int64_t)atomicAdd((unsigned long long*)&st->pool_used, (unsigned long long)need) : 0;
-        if (base + need <= D.POOL_CH) {
-          for (int32_t c = pn; c < c1; c++) D.pch[(int64_t)j * D.MAXCH + c] = (int32_t)(base + (c - pn));
-          S.logok = 1;
-        }
-      }
-      if (!S.logok) st->plog_ovf = 1;  // the next merge rebuilds the posting index first
+  // the reservation made before the resolves: the new chunks into the owner's chunk table
+  if (t == 0) {
+    if (lneed >= 0 && lbase + lneed <= D.POOL_CH) {
+      for (int32_t c = pn; c < lc1; c++) D.pch[(int64_t)j * D.MAXCH + c] = (int32_t)(lbase + (c - pn));
+      S.logok = 1;
     }
+    if (!S.logok) st->plog_ovf = 1;  // the next merge rebuilds the posting index first
   }
   __syncthreads();
   dbg_stamp(D, 3);
@@ -1233,54 +1319,65 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
 // posting-log entries -- balanced by region, whatever the key skew.
 struct PlaceLds {
   int32_t pre[NBA_MAX + 1];
-  int32_t tpre[ABLOCK + 1];  // this round's records: prefix of their slot counts
-  int32_t rts[ABLOCK], rid[ABLOCK], rlp[ABLOCK], rown[ABLOCK];
   int32_t red[ABLOCK / 64];
 };
 
+// the owner whose posting log a record's occurrences join: the owner slot of a KS index, the
+// key's owner for an overflow record (KO, KS's tail)
+__device__ inline int32_t place_owner(const Dev& D, int32_t at) {
+  const int64_t base = (int64_t)D.NBA * D.NBA * SK;
+  return at < base ? (int32_t)(at / ((int64_t)D.NBA * SK)) : owner_of_key(D, D.KS[at].pkey);
+}
+
 // record i of finder region j's records (the owners' slots, then its share k_lo.. of the
-// overflow list): occurrence count, T start, key id, posting-log position, owner
-__device__ inline void place_record(const Dev& D, const PlaceLds& S, int32_t j, int32_t i, int32_t nk, int64_t k_lo,
-                                    int32_t& n, int32_t& ts, int32_t& id, int32_t& lp, int32_t& ow) {
-  int2 v;
+// overflow list): its KS index
+__device__ inline int32_t place_rec_at(const Dev& D, const PlaceLds& S, int32_t j, int32_t i, int32_t nk, int64_t k_lo) {
   if (i < nk) {
-    ow = seg_of(S.pre, D.NBA, i);
-    const int64_t at = ((int64_t)ow * D.NBA + j) * SK + (i - S.pre[ow]);
-    const int2 nt = *reinterpret_cast<const int2*>(&D.KS[at].n);
-    v = D.KSid[at];
-    n = nt.x;
-    ts = nt.y;
-  } else {
-    const int64_t x = k_lo + (i - nk);
-    const KRec k = D.KO[x];
-    v = D.KOid[x];
-    ow = owner_of_key(D, k.pkey);
-    n = k.n;
-    ts = k.tstart;
+    const int32_t ow = seg_of(S.pre, D.NBA, i);
+    return (int32_t)(((int64_t)ow * D.NBA + j) * SK + (i - S.pre[ow]));
   }
-  id = v.x;
-  lp = v.y;
-  if (id < 0) n = 0;
+  return (int32_t)((int64_t)D.NBA * D.NBA * SK + k_lo + (i - nk));
+}
+
+// a single record (one occurrence, its slot in tstart as -(slot + 1)) of finder region j: pk
+// of the slot and its posting-log entry.  Grouped records are written through their T entries.
+__device__ inline void place_single(const Dev& D, int32_t at, int2 nt, int2 v) {
+  if (nt.y >= 0 || v.x < 0) return;
+  const int32_t t = -(nt.y + 1);
+  *tok_f(D, t, 3) = v.x;
+  if (v.y >= 0) D.pool[log_addr(D, place_owner(D, at), v.y)] = make_int2(v.x, t);
+}
+
+// T entry {slot, record} at T index q: pk of the slot and its posting-log entry (its position
+// in the record's range: the record's log position + q - tstart)
+__device__ inline void place_tentry(const Dev& D, int64_t q, int2 e, int2 v, int32_t tstart) {
+  if (e.y < 0 || v.x < 0) return;
+  *tok_f(D, e.x, 3) = v.x;
+  if (v.y >= 0) D.pool[log_addr(D, place_owner(D, e.y), (int64_t)v.y + (q - tstart))] = make_int2(v.x, e.x);
 }
 
 // place the merge committed with launch parity st->place_par (k_commit sets it; -1:
 // nothing to place).  Idempotent until the next k_find: a re-run writes the same
 // values (the pipelined exchange may run it again behind a stall).
+//
+// Two dependent rounds of loads.  Round 1: the merge's header (k_commit's copy in the state),
+// this region's merge entries, the record counts finder j sent each owner, and its T entries
+// {occurrence slot, key record} (up to 2 per thread).  Round 2: every record's (n, tstart) and
+// (key id, log position), and for every T entry its record's (key id, log position) and tstart
+// -- the T entries carry their record, so they need no record first (round 4's place loaded the
+// records, then the T ranges: three rounds on the select launch's critical path).
 __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   State* st = D.st;
   const int32_t t = threadIdx.x;
-  // first round: what depends on nothing -- the merge's parity, this region's merge-entry count
-  // and (speculatively) its first entry per thread, the record counts finder j sent each owner
-  // (round 3's version loaded them after the Sel record: two more dependent rounds on the
-  // select launch's critical path)
-  // (the merge's parity, token id and overflow counts come from k_commit's copy in the state:
-  // no dependent load of the Sel record)
   const int32_t par = st->place_par;
   const int32_t nid = st->place_nid;
   const int64_t novf = st->place_novf, nko = st->place_nko;
   const int32_t nA = D.Lcnt[j];
   const LEntry eA = D.L[(int64_t)j * D.LC + min((int64_t)t, D.LC - 1)];
   const int32_t cK = t < D.NBA ? D.cntK[cnt_at(D, t, j)] : 0;
+  const int32_t nT = min((int64_t)D.Tcnt[j], D.TC);
+  const int2* Tj = D.T + (int64_t)j * D.TC;
+  const int2 te0 = Tj[min(t, (int32_t)D.TC - 1)], te1 = Tj[min(t + ABLOCK, (int32_t)D.TC - 1)];
   if (par < 0) return;  // (k_commit sets par only for a merge)
   dbg_stamp(D, 30);
   const int64_t oper = (novf + D.NBA - 1) / D.NBA;
@@ -1293,17 +1390,30 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
     if (threadIdx.x < D.NBA) S.pre[threadIdx.x] = e;
     if (threadIdx.x == 0) S.pre[D.NBA] = tot;
   }
-  // this thread's record of the first round, loaded before the token rewrites so that its
-  // latency hides behind them (PLACE_PRE; the records depend only on k_commit)
-  int32_t p_n = 0, p_ts = 0, p_id = -1, p_lp = -1, p_ow = 0;
-#if PLACE_PRE
   __syncthreads();  // S.pre
-  {
-    const int32_t i = threadIdx.x, nk = S.pre[D.NBA];
-    if (i < nk + (int32_t)k_n) place_record(D, S, j, i, nk, k_lo, p_n, p_ts, p_id, p_lp, p_ow);
+  const int32_t nk = S.pre[D.NBA];
+  const int32_t nrec = nk + (int32_t)k_n;
+  // ---- round 2, all issued before any result is used
+  int32_t ra = -1;
+  int2 rnt = make_int2(0, 0), rv = make_int2(-1, -1);
+  if (t < nrec) {
+    ra = place_rec_at(D, S, j, t, nk, k_lo);
+    rnt = *reinterpret_cast<const int2*>(&D.KS[ra].n);
+    rv = D.KSid[ra];
   }
-#endif
-  for (int64_t i = threadIdx.x; i < nA + o_n; i += ABLOCK) {
+  const bool h0 = t < nT && te0.y >= 0, h1 = t + ABLOCK < nT && te1.y >= 0;
+  int2 v0 = make_int2(-1, -1), v1 = make_int2(-1, -1);
+  int32_t ts0 = 0, ts1 = 0;
+  if (h0) {
+    v0 = D.KSid[te0.y];
+    ts0 = D.KS[te0.y].tstart;
+  }
+  if (h1) {
+    v1 = D.KSid[te1.y];
+    ts1 = D.KS[te1.y].tstart;
+  }
+  // ---- the token rewrites of find region j (round 1's data)
+  for (int64_t i = t; i < nA + o_n; i += ABLOCK) {
     const LEntry e = i < nA ? (i == t ? eA : D.L[(int64_t)j * D.LC + i]) : D.Lovf[o_lo + (i - nA)];
     *reinterpret_cast<int2*>(D.tok + e.a) = make_int2(nid, e.ya);
     D.tok[e.b] = make_int4(-1, 0, -1, -1);  // (no other occurrence writes b's record)
@@ -1312,39 +1422,19 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
     else
       *tok_f(D, e.a, 3) = -1;
   }
-  __syncthreads();
   dbg_stamp(D, 31);
-  const int32_t nrec2 = S.pre[D.NBA] + (int32_t)k_n;
-  for (int32_t i0 = 0; i0 < nrec2; i0 += ABLOCK) {  // block-uniform rounds of records
-    const int32_t i = i0 + threadIdx.x;
-    int32_t n = 0, ts = 0, id = -1, lp = -1, ow = 0;
-    if (PLACE_PRE && i0 == 0) {
-      n = p_n, ts = p_ts, id = p_id, lp = p_lp, ow = p_ow;
-    } else if (i < nrec2) {
-      place_record(D, S, j, i, S.pre[D.NBA], k_lo, n, ts, id, lp, ow);
-    }
-    int32_t tot;
-    const int32_t ex = block_excl_scan(n, &tot, S.red);
-    S.tpre[threadIdx.x] = ex;
-    S.rts[threadIdx.x] = ts;
-    S.rid[threadIdx.x] = id;
-    S.rlp[threadIdx.x] = lp;
-    S.rown[threadIdx.x] = ow;
-    if (threadIdx.x == 0) S.tpre[ABLOCK] = tot;
-    __syncthreads();
-    for (int32_t q = threadIdx.x; q < tot; q += ABLOCK) {  // every occurrence slot of the round
-      const int32_t r = seg_of(S.tpre, ABLOCK, q);
-      const int32_t k = q - S.tpre[r];
-      const int32_t tsr = S.rts[r], d = S.rid[r];
-      const int32_t t = tsr >= 0 ? D.T[tsr + k] : -(tsr + 1);
-      *tok_f(D, t, 3) = d;
-      const int32_t l = S.rlp[r];
-      if (l >= 0) {
-        const int64_t pos = (int64_t)l + k;
-        D.pool[log_addr(D, S.rown[r], pos)] = make_int2(d, t);
-      }
-    }
-    __syncthreads();
+  // ---- pk of every new pair and its posting-log entry
+  const int64_t qbase = (int64_t)j * D.TC;
+  if (t < nrec) place_single(D, ra, rnt, rv);
+  if (h0) place_tentry(D, qbase + t, te0, v0, ts0);
+  if (h1) place_tentry(D, qbase + t + ABLOCK, te1, v1, ts1);
+  for (int32_t i = t + ABLOCK; i < nrec; i += ABLOCK) {  // (rare: more records than threads)
+    const int32_t at = place_rec_at(D, S, j, i, nk, k_lo);
+    place_single(D, at, *reinterpret_cast<const int2*>(&D.KS[at].n), D.KSid[at]);
+  }
+  for (int32_t q = t + 2 * ABLOCK; q < nT; q += ABLOCK) {  // (rare: more than 2 per thread)
+    const int2 e = Tj[q];
+    if (e.y >= 0) place_tentry(D, qbase + q, e, D.KSid[e.y], D.KS[e.y].tstart);
   }
   dbg_stamp(D, 32);
 }
