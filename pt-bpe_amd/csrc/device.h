@@ -120,6 +120,9 @@ struct State {
 // winner owner's posting log and the pool chunks that share lies in -- so that k_find's first
 // round of loads holds them and its second the candidates themselves (round 4's k_find loaded
 // the bucket offsets and log length, then the chunk table, then the candidates: two more rounds)
+#ifndef FIND_HDR
+#define FIND_HDR 1
+#endif
 constexpr int FH_CH = 4;  // chunk ids carried (a share spanning more reads the chunk table)
 struct FindHdr {
   int32_t lo, n1;    // the bucket of W in region r's posting index: post[r * PR + lo .. + n1)

@@ -108,7 +108,10 @@ struct geobpe_ctx {
   // run_batches: iterations past a batch's target idle on the device (SEL_IDLE), so a rebuild
   // iteration inside the batch costs no host round trip; run_end = target merges + 1 (0: off)
   int32_t run_end = 0;
-  int spec = 1;                // iterations enqueued past each batch's target
+#ifndef SPEC_DEF
+#define SPEC_DEF 1
+#endif
+  int spec = SPEC_DEF;         // iterations enqueued past the run's last batch target (GEOBPE_SPEC)
   double decay = 0;            // maxc ratio per merge over the last pulled batch (0: unknown)
   // middle regime (mid.h): merges whose count is <= mid_thresh run as k_mid_sel + k_mid_find
   int64_t mid_thresh = 49152;  // 0: never (C3 merges 11..1000: 16384 -> 29.2k, 32768 -> 30.7k, 49152 -> 31.0k, 65536 -> 30.8k, 98304 -> 29.2k merges/s)

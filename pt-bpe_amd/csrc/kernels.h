@@ -927,9 +927,6 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
   dbg_stamp(D, 26);
 }
 
-#ifndef FIND_HDR
-#define FIND_HDR 1
-#endif
 __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par, int run_end) {
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;

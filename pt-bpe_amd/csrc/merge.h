@@ -527,8 +527,9 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
         } else {
           const int64_t k = ls0 + (i - n1);
 #if FIND_HDR
-          if (hdr) {
-            const int32_t ch = fh.ch[k / D.CHUNK - ls0 / D.CHUNK];
+          if (hdr) {  // (a select chain, not an indexed private array: that one went to LDS)
+            const int64_t ci = k / D.CHUNK - ls0 / D.CHUNK;
+            const int32_t ch = ci == 0 ? fh.ch[0] : ci == 1 ? fh.ch[1] : ci == 2 ? fh.ch[2] : fh.ch[3];
             e = D.pool[(int64_t)ch * D.CHUNK + k % D.CHUNK];
           } else
 #endif
@@ -1033,6 +1034,14 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   hot_init(hot);
   if (t == 0) tb.n = 0;
   dbg_stamp(D, 51);
+#if !COMMIT_SPEC
+  // the first PER records of each finder's slot, only where they exist: issued as soon as the
+  // record counts are in, under the prefix scans below (they depend on nothing else)
+  KRec r0;
+  int2 d0 = make_int2(0, 0);
+  if (lane_ok && k0 < min(cK, SK)) r0 = D.KS[seg * SK + k0];
+  if (lane_ok && k0 < min(cD, SD)) d0 = D.DS[seg * SD + k0];
+#endif
   {  // records past the first PER of a finder's slot: prefix sums
     const int32_t eK = t < nba ? max(0, min(cK, SK) - PER) : 0;
     const int32_t eD = t < nba ? max(0, min(cD, SD) - PER) : 0;
@@ -1061,13 +1070,6 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   }
   __syncthreads();
   dbg_stamp(D, 1);
-#if !COMMIT_SPEC
-  // the first PER records of each finder's slot, only where they exist
-  KRec r0;
-  int2 d0 = make_int2(0, 0);
-  if (lane_ok && k0 < min(cK, SK)) r0 = D.KS[seg * SK + k0];
-  if (lane_ok && k0 < min(cD, SD)) d0 = D.DS[seg * SD + k0];
-#endif
   // ---- round 1: key records -> LDS dedupe (occurrence totals per key); decrements -> LDS
 #define COMMIT_INSERT(k)                                          \
   do {                                                            \
@@ -1441,5 +1443,9 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
 
 __global__ __launch_bounds__(ABLOCK) void k_place(Dev D) {
   __shared__ PlaceLds S;
+  // (the standalone launch flushes a run's last place, usually already done by an idle
+  // iteration's select launch: nothing to wait for then -- the place's own first round of
+  // loads took ~13 us to drain before its workgroups could see par < 0)
+  if (D.st->place_par < 0) return;
   place_body(D, blockIdx.x, S);
 }
