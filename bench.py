@@ -45,9 +45,9 @@ CONFIGS = {
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
 LIVE = "find,commit,mid_find"  # merge-loop kernels timed live (sampled) inside the timed region
 # algorithmic bytes
-FIND_BYTES_PER_OCC = 128   # k_find per merged occurrence: posting entry 8, token records of p, g, b, c 64,
-                           # vocab hashes of p and c 32, merge entry 16, two occurrence slots (T) 8
-PLACE_BYTES_PER_OCC = 76   # k_place: merge entry 16, T 8, token rewrites 28, two pk 8, two log entries 16
+FIND_BYTES_PER_OCC = 136   # k_find per merged occurrence: posting entry 8, token records of p, g, b, c 64,
+                           # vocab hashes of p and c 32, merge entry 16, two T entries {slot, record} 16
+PLACE_BYTES_PER_OCC = 84   # k_place: merge entry 16, two T entries 16, token rewrites 28, two pk 8, two log entries 16
 MIDFIND_BYTES_PER_OCC = 132  # k_mid_find: list entry 4, token records of g, p, b, c 64, vocab hashes of p and c
                              # 32, merge entry 16, two new-pair entries 16
 MIDSEL_BYTES_PER_OCC = 76    # k_mid_sel's token rewrites: merge entry 16, records of a, b, c 28, two new-pair

@@ -121,7 +121,7 @@ struct State {
 // round of loads holds them and its second the candidates themselves (round 4's k_find loaded
 // the bucket offsets and log length, then the chunk table, then the candidates: two more rounds)
 #ifndef FIND_HDR
-#define FIND_HDR 1
+#define FIND_HDR 0  // (A/B, profiles/r5_s5: the select workgroup's two extra rounds outweigh the find's gain)
 #endif
 constexpr int FH_CH = 4;  // chunk ids carried (a share spanning more reads the chunk table)
 struct FindHdr {

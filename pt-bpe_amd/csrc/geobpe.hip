@@ -114,7 +114,7 @@ struct geobpe_ctx {
   int spec = SPEC_DEF;         // iterations enqueued past the run's last batch target (GEOBPE_SPEC)
   double decay = 0;            // maxc ratio per merge over the last pulled batch (0: unknown)
   // middle regime (mid.h): merges whose count is <= mid_thresh run as k_mid_sel + k_mid_find
-  int64_t mid_thresh = 49152;  // 0: never (C3 merges 11..1000: 16384 -> 29.2k, 32768 -> 30.7k, 49152 -> 31.0k, 65536 -> 30.8k, 98304 -> 29.2k merges/s)
+  int64_t mid_thresh = 65536;  // 0: never (C3 merges 11..1000, round 5 kernels: 32768 -> 32.2k, 49152 -> 32.6k, 65536 -> 32.8k, 98304 -> 32.8k merges/s)
   bool mid_on = false;         // switched (one way)
   bool place_mid = false;      // the pending place is k_mid_sel's (else k_place's)
   // the multi-rank exchange owned by the engine (geobpe_comm_*, geobpe_run_exchange)

@@ -404,6 +404,50 @@ __device__ inline int32_t fkc_find(FindLds& S, const Dev& D, u64 k, u64 h1, bool
   return -1;
 }
 
+#ifndef FAGG
+#define FAGG 0  // k_find: wave-aggregated LDS dedupe of the new keys (iterations; 0: off)
+#endif
+// the round's dedupe slot (s), insert flag and rank within the slot of one new key per lane;
+// lanes of a wave holding the same key (a common neighbour token: the same new key for many
+// occurrences of a region) take one LDS probe and one counter add between them, up to FAGG
+// keys per wave -- the rest probe on their own
+__device__ inline void fkc_group(FindLds& S, const Dev& D, bool v, const FHalf& h, int32_t& s, bool& ins, int32_t& rank) {
+  s = -1;
+  ins = false;
+  rank = 0;
+  bool done = false;
+#if FAGG
+  u64 pend = __ballot(v);
+  const int lane = wave_lane();
+  for (int it = 0; it < FAGG && pend; it++) {  // (wave-uniform)
+    const int leader = __ffsll((long long)pend) - 1;
+    const u64 lk = __shfl((unsigned long long)h.pkey, leader, 64);
+    const bool same = v && !done && h.pkey == lk;
+    const u64 m = __ballot(same);
+    if (__popcll(m) < 2) break;
+    int32_t ss = -1, base = 0;
+    bool r = false;
+    if (lane == leader) {
+      ss = fkc_find(S, D, h.pkey, h.h1, &r);
+      if (ss >= 0) base = atomicAdd(&S.u.m.kcnt[ss], (int32_t)__popcll(m));
+    }
+    ss = __shfl(ss, leader, 64);
+    base = __shfl(base, leader, 64);
+    if (same) {
+      s = ss;
+      rank = base + (int32_t)__popcll(m & ((1ULL << lane) - 1));
+      ins = lane == leader && r;
+    }
+    done = done || same;
+    pend &= ~m;
+  }
+#endif
+  if (v && !done) {
+    s = fkc_find(S, D, h.pkey, h.h1, &ins);
+    if (s >= 0) rank = atomicAdd(&S.u.m.kcnt[s], 1);
+  }
+}
+
 __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   __shared__ FindLds S;
   State* st = D.st;
@@ -550,14 +594,8 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       // group the new keys of this round: LDS slot, rank within the slot
       bool rl = false, rr = false;
       int32_t sl = -1, sr = -1, kl = 0, kr = 0;
-      if (vl) {
-        sl = fkc_find(S, D, hl.pkey, hl.h1, &rl);
-        if (sl >= 0) kl = atomicAdd(&S.u.m.kcnt[sl], 1);
-      }
-      if (vr) {
-        sr = fkc_find(S, D, hr.pkey, hr.h1, &rr);
-        if (sr >= 0) kr = atomicAdd(&S.u.m.kcnt[sr], 1);
-      }
+      fkc_group(S, D, vl, hl, sl, rl, kl);
+      fkc_group(S, D, vr, hr, sr, rr, kr);
       __syncthreads();
       if (vl && sl >= 0 && S.u.m.kh1[sl] != hl.h1) {  // same probe key, other content
         set_error(D, GEOBPE_EHASH, -13);
@@ -771,6 +809,9 @@ __device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nb
 
 #ifndef COMMIT_CSPEC
 #define COMMIT_CSPEC 1
+#endif
+#ifndef CAGG
+#define CAGG 0  // k_commit: wave-aggregated inserts of the first records (iterations; 0: off)
 #endif
 // commit_resolve with the key's count added in the same round trip: the add to the count of
 // the key's first slot goes out beside the CAS (the key is there unless another key took the
@@ -1034,14 +1075,6 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   hot_init(hot);
   if (t == 0) tb.n = 0;
   dbg_stamp(D, 51);
-#if !COMMIT_SPEC
-  // the first PER records of each finder's slot, only where they exist: issued as soon as the
-  // record counts are in, under the prefix scans below (they depend on nothing else)
-  KRec r0;
-  int2 d0 = make_int2(0, 0);
-  if (lane_ok && k0 < min(cK, SK)) r0 = D.KS[seg * SK + k0];
-  if (lane_ok && k0 < min(cD, SD)) d0 = D.DS[seg * SD + k0];
-#endif
   {  // records past the first PER of a finder's slot: prefix sums
     const int32_t eK = t < nba ? max(0, min(cK, SK) - PER) : 0;
     const int32_t eD = t < nba ? max(0, min(cD, SD) - PER) : 0;
@@ -1070,6 +1103,14 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   }
   __syncthreads();
   dbg_stamp(D, 1);
+#if !COMMIT_SPEC
+  // the first PER records of each finder's slot, only where they exist (issuing them before the
+  // prefix scans above measured ~1 % slower on the window, profiles/r5_s5/)
+  KRec r0;
+  int2 d0 = make_int2(0, 0);
+  if (lane_ok && k0 < min(cK, SK)) r0 = D.KS[seg * SK + k0];
+  if (lane_ok && k0 < min(cD, SD)) d0 = D.DS[seg * SD + k0];
+#endif
   // ---- round 1: key records -> LDS dedupe (occurrence totals per key); decrements -> LDS
 #define COMMIT_INSERT(k)                                          \
   do {                                                            \
@@ -1105,7 +1146,32 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     const int32_t ww = seg_of(s_preF, nba, t);
     x0 = D.DS[((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww])];
   }
+#if CAGG
+  {  // a hot key reaches its owner once per finder -- up to 64 times in a wave's r0, each one an
+     // atomic on the same LDS counter: the lanes holding the wave's first pending key add their
+     // totals once (a few keys per wave; the rest insert on their own)
+    u64 pend = __ballot(mine0);
+    bool agg = false;
+    for (int it = 0; it < CAGG && pend; it++) {  // (wave-uniform)
+      const int leader = __ffsll((long long)pend) - 1;
+      const u64 lk = __shfl((unsigned long long)r0.pkey, leader, 64);
+      const bool same = mine0 && !agg && r0.pkey == lk;
+      const u64 m = __ballot(same);
+      if (__popcll(m) < 2) break;
+      const int32_t v = wave_sum(same ? r0.n : 0);
+      if (wave_lane() == leader) {
+        KRec k = r0;
+        k.n = v;
+        COMMIT_INSERT(k);
+      }
+      agg = agg || same;
+      pend &= ~m;
+    }
+    if (mine0 && !agg) COMMIT_INSERT(r0);
+  }
+#else
   if (mine0) COMMIT_INSERT(r0);
+#endif
   if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
   dbg_stamp(D, 56);
   if (he && (t < nE || owner_of_key(D, e0.pkey) == j)) COMMIT_INSERT(e0);
