@@ -29,20 +29,25 @@
 
 constexpr int BIN_VEC = 4;        // residue slots per int4 group
 #ifndef FUSE_PACK
-#define FUSE_PACK 1
+#define FUSE_PACK 0  // (A/B, profiles/r5_suite1: the fused count kernel 287 us against 133 + a 285 us k_pack)
 #endif
 #ifndef BIN_GPT_DEF
 #define BIN_GPT_DEF (FUSE_PACK ? 3 : 4)  // (4 with the fused record writes spills 12 VGPRs)
+#endif
+#ifndef BIN_FP
+#define BIN_FP 0  // the 16-bit pair fingerprints (fp): written, never read since round 2's token records
 #endif
 #ifndef BIN_EXP
 #define BIN_EXP 0
 #endif
 constexpr int BIN_GPT = BIN_GPT_DEF;  // groups per thread per step (loads in flight together)
-// FUSE_PACK = 1: k_bin_count writes the merge loop's token records itself ({label, 1 | 16-bit
-// junction symbol << 16, previous slot, pair key}: one 64-B line per group of 4 residues) and
-// the 16-bit junction symbols, and the list kernels write the listed pairs' keys into the
-// records -- no pk / fp arrays and no k_pack pass over them afterwards (VERDICT r4 item 5:
-// k_pack was ~285 us after a ~300 us bin pass)
+// FUSE_PACK = 1 (A/B): k_bin_count writes the merge loop's token records itself ({label, 1 |
+// 16-bit junction symbol << 16, previous slot, pair key}: one 64-B line per group of 4 residues,
+// lane-strided) and the 16-bit junction symbols, and the list kernels write the listed pairs'
+// keys into the records -- no pk array and no k_pack pass.  Measured: the count kernel 133 ->
+// 287 us (its stores touch 64 lines per instruction), pass + pack 585 -> 454 us, but the
+// pair-count kernel at 0.26 of HBM peak.  Default: the lean count kernel and a coalesced k_pack
+// (kernels.h) that writes whole records lane by lane
 constexpr int BIN_NC = 1 << 14;   // max cube cells (64 KB of LDS counts)
 constexpr int BIN_SAMPLE = 16;    // the sample: the first 1/16 of each workgroup's range
 constexpr int BIN_MAXSYM = 2048;  // label / junction-symbol tables (K0, B^3 <= 2048)
@@ -438,7 +443,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
         }
       } else if (v < hi) {
         pv[v] = make_int4(k[q][0], k[q][1], k[q][2], k[q][3]);
-        if (!(BIN_EXP & 1)) fv[v] = make_ushort4(bin_fp(k[q][0]), bin_fp(k[q][1]), bin_fp(k[q][2]), bin_fp(k[q][3]));
+        if (BIN_FP && !(BIN_EXP & 1)) fv[v] = make_ushort4(bin_fp(k[q][0]), bin_fp(k[q][1]), bin_fp(k[q][2]), bin_fp(k[q][3]));
       }
     }
   }

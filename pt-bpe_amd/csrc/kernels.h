@@ -131,17 +131,18 @@ __global__ __launch_bounds__(BLOCK) void k_first(Dev D, int64_t row_base, u64* f
   }
 }
 
-// after the bin pass: the pair keys join the token records (tok.w = pk), and the
-// 16-bit junction symbols the merge loop reads
+// after the bin pass: the merge loop's token records, whole ({label, 1 | 16-bit junction
+// symbol << 16, previous slot, pair key}: one 16-B store per residue, consecutive lanes on
+// consecutive records), and the 16-bit junction symbols.  Round 4's k_pack stored pk and the
+// length word into the records' 2nd and 4th words, 4-B stores at a 16-B lane stride, ~285 us
+// at C3.  (Every token is one residue here; g starts its chain iff gsym[g - 1] < 0.)
 __global__ __launch_bounds__(BLOCK) void k_pack(Dev D) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
-    *tok_f(D, g, 3) = D.pk[g];
-    if (D.gs16) {  // (every token is one residue here)
-      const int32_t v = D.gsym[g];
-      const uint32_t g16 = v < 0 ? 0xFFFFu : (uint32_t)v;
-      D.gs16[g] = (uint16_t)g16;
-      *tok_f(D, g, 1) = (int32_t)(1u | (g16 << 16));
-    }
+    const int32_t lab = D.lab0[g], gs = D.gsym[g], k = D.pk[g];
+    const int32_t gp = g > 0 ? D.gsym[g - 1] : -1;  // (the previous lane's line: a cache hit)
+    const uint32_t g16 = gs < 0 ? 0xFFFFu : (uint32_t)gs;
+    D.tok[g] = make_int4(lab, D.gs16 ? (int32_t)(1u | (g16 << 16)) : 1, gp >= 0 ? (int32_t)(g - 1) : -1, k);
+    if (D.gs16) D.gs16[g] = (uint16_t)g16;
   }
 }
 

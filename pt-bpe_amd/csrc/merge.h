@@ -519,7 +519,9 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
     }
     queued = S.qn <= FMQ;
   }
+#if FIND_HDR
   bool hdr = false;  // (the log chunks of the share from k_select's header)
+#endif
   if (W >= 0 && !queued) {
 #if FIND_HDR
     if (!sel.rebuild) {

@@ -615,14 +615,6 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     if (vr && sr < 0) mid_single(D, S, F, hr.h1, hr.h2, hr.len, hr.idL, hr.g, hr.idR, hr.target);
     __syncthreads();
     if (c0 == 0) dbg_stamp(D, 16);
-    // the last round's walks are done, so every decrement is staged: out now, one atomic per
-    // key, in flight under the resolves and the list flush (at the launch's end they were the
-    // last memory operations to drain)
-    if (!D.xrec && c0 + ABLOCK >= ncand)
-      for (int i = t; i < AggT<11>::N; i += ABLOCK) {
-        const int32_t k = S.agg.key[i], v = S.agg.val[i];
-        if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
-      }
     const int32_t nocc = S.nocc;
     const int64_t xb = D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
     for (int32_t q = t; q < nocc; q += ABLOCK) {
@@ -648,6 +640,15 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       else if (!MID_SPEC)
         count_add_hot(D, S.hot, d, S.cnt[s], F.th);
     }
+    // the last round's walks are done, so every decrement is staged: out now, one atomic per
+    // key, in flight under the new pairs' grouping and the list flush (at the launch's end they
+    // were the last memory operations to drain; issued before the resolves they queued ahead of
+    // the resolves' atomics: merge 100 +2 us, profiles/r5_s6/)
+    if (!D.xrec && c0 + ABLOCK >= ncand)
+      for (int i = t; i < AggT<11>::N; i += ABLOCK) {
+        const int32_t k = S.agg.key[i], v = S.agg.val[i];
+        if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
+      }
     __syncthreads();
     if (c0 == 0) dbg_stamp(D, 17);
     if (vl && sl >= 0) {
