@@ -455,11 +455,15 @@ static int setgeo_impl(PyObject* cols, PyObject* init, Py_ssize_t idx, Py_ssize_
       if ((j + 1) / 3 >= PyList_GET_SIZE(PyTuple_GET_ITEM(cols, DH[j % 3]))) ok = Py_False;
   }
   if (ok == Py_True) {
+/* (a cell that already holds the very object is left alone: a partitioned token's medoid
+   geometry is mostly its parts' medoid values, the objects the span already holds) */
 #define SETGEO_PUT(LIST, ROW, T)                                     \
   do {                                                              \
     PyObject* x_ = PySequence_Fast_GET_ITEM(seq[T], pos[T]++);      \
-    Py_INCREF(x_);                                                  \
-    PyList_SetItem((LIST), (ROW), x_);                              \
+    if (PyList_GET_ITEM((LIST), (ROW)) != x_) {                     \
+      Py_INCREF(x_);                                                \
+      PyList_SetItem((LIST), (ROW), x_);                            \
+    }                                                               \
   } while (0)
     for (Py_ssize_t j = idx; j < idx + l; j++) {
       const int t = BT[j % 3];
@@ -604,9 +608,90 @@ static PyObject* memo_check(PyObject* self, PyObject* args) {
   return PyLong_FromLongLong(h);
 }
 
+/* note()'s count changes, gathered per key OBJECT in C and added to the diff dict once per
+ * object at the merge's end, in first-note order -- the dict then gains its keys in the order
+ * the per-call updates gave (a string's first object is noted when the string first is) and
+ * the same sums, without a dict update and an int allocation per call (~5 per occurrence).
+ * Each object is held while noted, so its address is not reused by another key. */
+typedef struct {
+  PyObject* k;
+  long d;
+} NoteEnt;
+typedef struct {
+  NoteEnt* t;        /* open addressing on the object address */
+  Py_ssize_t* order; /* slots in first-note order */
+  Py_ssize_t cap, n;
+} Notes;
+
+static Py_ssize_t notes_slot(const Notes* s, PyObject* k) {
+  size_t h = ((size_t)(uintptr_t)k >> 4) * 0x9E3779B97F4A7C15ull;
+  for (size_t i = h & (size_t)(s->cap - 1);; i = (i + 1) & (size_t)(s->cap - 1))
+    if (s->t[i].k == k || !s->t[i].k) return (Py_ssize_t)i;
+}
+
+static int notes_add(Notes* s, PyObject* k, long d) {
+  if (2 * (s->n + 1) > s->cap) {
+    Notes g = {NULL, NULL, s->cap ? 2 * s->cap : 1024, 0};
+    g.t = PyMem_Calloc(g.cap, sizeof *g.t);
+    g.order = PyMem_Malloc(g.cap * sizeof *g.order);
+    if (!g.t || !g.order) {
+      PyMem_Free(g.t);
+      PyMem_Free(g.order);
+      PyErr_NoMemory();
+      return -1;
+    }
+    for (Py_ssize_t i = 0; i < s->n; i++) {
+      const NoteEnt e = s->t[s->order[i]];
+      const Py_ssize_t j = notes_slot(&g, e.k);
+      g.t[j] = e;
+      g.order[g.n++] = j;
+    }
+    PyMem_Free(s->t);
+    PyMem_Free(s->order);
+    *s = g;
+  }
+  const Py_ssize_t i = notes_slot(s, k);
+  if (!s->t[i].k) {
+    Py_INCREF(k);
+    s->t[i].k = k;
+    s->t[i].d = 0;
+    s->order[s->n++] = i;
+  }
+  s->t[i].d += d;
+  return 0;
+}
+
+/* diff[k] = diff.get(k, 0) + d for every noted object in first-note order, then release them;
+ * with diff NULL only release (an error path) */
+static int notes_flush(Notes* s, PyObject* diff) {
+  int rc = 0;
+  for (Py_ssize_t i = 0; i < s->n; i++) {
+    NoteEnt* e = &s->t[s->order[i]];
+    if (diff && rc == 0) {
+      PyObject* old = PyDict_GetItemWithError(diff, e->k);
+      if (!old && PyErr_Occurred()) {
+        rc = -1;
+      } else {
+        const long v = (old ? PyLong_AsLong(old) : 0) + e->d;
+        PyObject* nv = (v == -1 && PyErr_Occurred()) ? NULL : PyLong_FromLong(v);
+        rc = nv ? PyDict_SetItem(diff, e->k, nv) : -1;
+        Py_XDECREF(nv);
+      }
+    }
+    Py_DECREF(e->k);
+  }
+  PyMem_Free(s->t);
+  PyMem_Free(s->order);
+  s->t = NULL;
+  s->order = NULL;
+  s->cap = s->n = 0;
+  return rc;
+}
+
 typedef struct {
   PyObject *chains, *gd, *pk, *edges, *edges_fn, *names, *diff;
   Memo* memo; /* the pair-key memo, or NULL (see mpair_key) */
+  Notes notes;
 } MSt;
 
 static int key_error(PyObject* k) {
@@ -618,16 +703,7 @@ static int key_error(PyObject* k) {
   return -1;
 }
 
-static int note(MSt* m, PyObject* k, long d) {
-  PyObject* old = PyDict_GetItemWithError(m->diff, k);
-  if (!old && PyErr_Occurred()) return -1;
-  long v = (old ? PyLong_AsLong(old) : 0) + d;
-  PyObject* nv = PyLong_FromLong(v);
-  if (!nv) return -1;
-  const int rc = PyDict_SetItem(m->diff, k, nv);
-  Py_DECREF(nv);
-  return rc;
-}
+static int note(MSt* m, PyObject* k, long d) { return notes_add(&m->notes, k, d); }
 
 /* small non-negative ints (chain and bond indices) from a cache: PyLong_FromSsize_t allocates
  * every value above 256, twice or more per key and per occurrence here */
@@ -859,12 +935,18 @@ static PyObject* merge(PyObject* self, PyObject* args) {
     if (!m.memo) return NULL;
   }
   m.diff = diff;
+  m.notes = (Notes){NULL, NULL, 0, 0};
   PyObject* nobj = PyLong_FromSsize_t(n);
   PyObject* lenobj = PyLong_FromSsize_t(length);
   PyObject *chain = NULL, *cols = NULL, *init = NULL, *tp = NULL, *btt = NULL, *events = NULL, *nres_o = NULL;
   PyObject *t12 = NULL, *t01 = NULL, *t23 = NULL, *left = NULL, *right = NULL, *pkrow = NULL;
   Py_ssize_t cur_ci = -1, nres = 0, last_ci = -1, last_i1 = 0;
   int have_last = 0, err = 0;
+  /* the merged key's set, looked up once (every removal below is from it); NULL: per call */
+  PyObject* kset = PyDict_Check(m.gd) ? PyDict_GetItemWithError(m.gd, key) : NULL;
+  if (!kset && PyErr_Occurred()) goto fail;
+  if (kset && !PySet_Check(kset)) kset = NULL;
+  Py_XINCREF(kset);
   if (!nobj || !lenobj) goto fail;
   for (Py_ssize_t q = 0; q < PyList_GET_SIZE(occs); q++) {
     PyObject* oc = PyList_GET_ITEM(occs, q);  /* (the very tuples _geo_dict's sets hold) */
@@ -923,7 +1005,13 @@ static PyObject* merge(PyObject* self, PyObject* args) {
       Py_CLEAR(t12);
       continue;
     }
-    if (set_in(&m, key, t12, 0) < 0 || pk_set(pkrow, i2, NULL) < 0 || note(&m, key, -1) < 0) goto fail;
+    if (kset) {
+      const int rc = PySet_Discard(kset, t12);
+      if (rc < 0 || (rc == 0 && key_error(t12) < 0)) goto fail;
+    } else if (set_in(&m, key, t12, 0) < 0) {
+      goto fail;
+    }
+    if (pk_set(pkrow, i2, NULL) < 0 || note(&m, key, -1) < 0) goto fail;
     Py_ssize_t i0 = 0, l0 = 0, i3 = 0, l3 = 0;
     const Py_ssize_t ntp = PyList_GET_SIZE(tp);
     if (i1) {
@@ -1040,6 +1128,8 @@ static PyObject* merge(PyObject* self, PyObject* args) {
 fail:
   err = 1;
 done:
+  if (notes_flush(&m.notes, err ? NULL : diff) < 0) err = 1;
+  Py_XDECREF(kset);
   Py_XDECREF(t12);
   Py_XDECREF(t01);
   Py_XDECREF(t23);
@@ -1186,6 +1276,239 @@ fail:
   return NULL;
 }
 
+/* packa(chains, orig, spans, out) -- packc() with the spans an int64 (n, 3) buffer of
+ * (chain index, q, r) rows (no tuple per span) */
+static PyObject* packa(PyObject* self, PyObject* args) {
+  PyObject* chains;
+  Py_buffer sb, out;
+  int orig;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!py*w*", &PyList_Type, &chains, &orig, &sb, &out)) return NULL;
+  double* o = (double*)out.buf;
+  const Py_ssize_t cap = out.len / (Py_ssize_t)sizeof(double);
+  const int64_t* sp = (const int64_t*)sb.buf;
+  const Py_ssize_t ns = sb.len / (3 * (Py_ssize_t)sizeof(int64_t));
+  Py_ssize_t at = 0, last_ci = -1;
+  PyObject* cols = NULL;
+  PyObject* init = NULL;
+  int err = 0;
+  for (Py_ssize_t i = 0; i < ns && !err; i++) {
+    const Py_ssize_t ci = (Py_ssize_t)sp[3 * i], q = (Py_ssize_t)sp[3 * i + 1], r = (Py_ssize_t)sp[3 * i + 2];
+    if (ci != last_ci) {
+      Py_CLEAR(cols);
+      Py_CLEAR(init);
+      if (ci < 0 || ci >= PyList_GET_SIZE(chains)) {
+        PyErr_SetString(PyExc_IndexError, "chain index out of range");
+        err = 1;
+        break;
+      }
+      PyObject* c = PyList_GET_ITEM(chains, ci);
+      PyObject* src = PyObject_GetAttr(c, ATTR[orig ? A_ORIG : A_CUR]);
+      init = PyObject_GetAttr(c, ATTR[A_INIT]);
+      cols = (src && init) ? PyTuple_New(9) : NULL;
+      for (int t = 0; cols && t < 9; t++) {
+        PyObject* col = PyObject_GetItem(src, PACK_KEYS[t]);
+        if (!col || !PyList_Check(col)) {
+          if (col) PyErr_SetString(PyExc_TypeError, "rmsdkey.packa: columns must be lists");
+          Py_XDECREF(col);
+          Py_CLEAR(cols);
+          break;
+        }
+        PyTuple_SET_ITEM(cols, t, col);
+      }
+      Py_XDECREF(src);
+      if (!cols || !PyList_Check(init) || PyList_GET_SIZE(init) < 3) {
+        if (cols) PyErr_SetString(PyExc_TypeError, "rmsdkey.packa: init must be a list of 3");
+        err = 1;
+        break;
+      }
+      last_ci = ci;
+    }
+    if (q < 0 || r < 1 || at + 9 * r > cap) {
+      PyErr_SetString(PyExc_ValueError, "rmsdkey.packa: bad span");
+      err = 1;
+      break;
+    }
+    if (pack_one(cols, init, q, r, o + at) < 0) err = 1;
+    at += 9 * r;
+  }
+  Py_XDECREF(cols);
+  Py_XDECREF(init);
+  PyBuffer_Release(&sb);
+  PyBuffer_Release(&out);
+  return err ? NULL : PyLong_FromSsize_t(at / 9);
+}
+
+/* spans_occ(chains, occ, length, out) -- [(ci, chains[ci].token_pos[i2 - 1], length) for ci, i2
+ * in occ] (RmsdBPE._partition / the recurring merge, bpe.py:1759-1763) into an int64 (n, 3)
+ * buffer */
+static PyObject* spans_occ(PyObject* self, PyObject* args) {
+  PyObject *chains, *occ;
+  Py_ssize_t length;
+  Py_buffer out;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!O!nw*", &PyList_Type, &chains, &PyList_Type, &occ, &length, &out)) return NULL;
+  int64_t* o = (int64_t*)out.buf;
+  const Py_ssize_t n = PyList_GET_SIZE(occ);
+  int err = out.len < 3 * n * (Py_ssize_t)sizeof(int64_t);
+  if (err) PyErr_SetString(PyExc_ValueError, "rmsdkey.spans_occ: output too small");
+  for (Py_ssize_t i = 0; i < n && !err; i++) {
+    PyObject* oc = PyList_GET_ITEM(occ, i);
+    if (!PyTuple_Check(oc) || PyTuple_GET_SIZE(oc) != 2) {
+      PyErr_SetString(PyExc_TypeError, "rmsdkey.spans_occ: occurrences must be (chain, index) tuples");
+      err = 1;
+      break;
+    }
+    const Py_ssize_t ci = PyLong_AsSsize_t(PyTuple_GET_ITEM(oc, 0)), i2 = PyLong_AsSsize_t(PyTuple_GET_ITEM(oc, 1));
+    if (PyErr_Occurred()) {
+      err = 1;
+      break;
+    }
+    if (ci < 0 || ci >= PyList_GET_SIZE(chains)) {
+      PyErr_SetString(PyExc_IndexError, "chain index out of range");
+      err = 1;
+      break;
+    }
+    PyObject* tp = PyObject_GetAttr(PyList_GET_ITEM(chains, ci), ATTR[A_TOKEN_POS]);
+    if (!tp || !PyList_Check(tp)) {
+      if (tp) PyErr_SetString(PyExc_TypeError, "rmsdkey.spans_occ: token_pos must be a list");
+      Py_XDECREF(tp);
+      err = 1;
+      break;
+    }
+    /* (Python's tp[i2 - 1]: a negative index counts from the end) */
+    const Py_ssize_t j = i2 - 1 < 0 ? i2 - 1 + PyList_GET_SIZE(tp) : i2 - 1;
+    const Py_ssize_t i1 = list_int(tp, j);
+    Py_DECREF(tp);
+    if (i1 == -1 && PyErr_Occurred()) {
+      err = 1;
+      break;
+    }
+    o[3 * i] = ci, o[3 * i + 1] = i1, o[3 * i + 2] = length;
+  }
+  PyBuffer_Release(&out);
+  if (err) return NULL;
+  Py_RETURN_NONE;
+}
+
+/* ---------------------------------------------------------------- k-medoids
+ * kmed_step(D, medoids, assign) -> list -- the body of one iteration of algo.k_medoids
+ * (algo.py:191-213) as rmsd.k_medoids_from_matrix runs it on the float32 (N, N) matrix D:
+ * assign[i] = argmin_j D[i, medoids[j]] (np.argmin over D[:, medoids], axis 1), then per
+ * cluster j the member minimising D[np.ix_(members, members)].sum(axis=1), or -1 for an
+ * empty cluster (the caller draws its rng.integers(N) in j order, as there).  The row sums
+ * follow numpy's float32 reduction order exactly (pairwise summation over the gathered row:
+ * below 8 items a running sum, up to 128 eight accumulators, above that halves cut at a
+ * multiple of 8), and argmin keeps numpy's rules (the first minimum; a NaN wins), so the
+ * medoids are the numpy loop's bit for bit (tests/test_rmsd.py checks both on random and
+ * tied matrices).  The numpy path gathered the members x members block per cluster (~0.7 ms
+ * of a 2 000-chain RMSD step). */
+static float pw_sum(const float* row, const Py_ssize_t* ix, Py_ssize_t n) {
+  if (n < 8) {
+    float r = 0.f;
+    for (Py_ssize_t i = 0; i < n; i++) r += row[ix[i]];
+    return r;
+  }
+  if (n <= 128) {
+    float r[8];
+    for (int j = 0; j < 8; j++) r[j] = row[ix[j]];
+    Py_ssize_t i;
+    for (i = 8; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; j++) r[j] += row[ix[i + j]];
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; i++) res += row[ix[i]];
+    return res;
+  }
+  Py_ssize_t n2 = n / 2;
+  n2 -= n2 % 8;
+  const float a = pw_sum(row, ix, n2);
+  return a + pw_sum(row, ix + n2, n - n2);
+}
+
+/* np.argmin's pick among v[0..n): the first NaN, else the first minimum */
+static Py_ssize_t argmin_f32(const float* v, Py_ssize_t n) {
+  Py_ssize_t b = 0;
+  if (v[0] != v[0]) return 0;
+  for (Py_ssize_t i = 1; i < n; i++) {
+    if (v[i] != v[i]) return i;
+    if (v[i] < v[b]) b = i;
+  }
+  return b;
+}
+
+static PyObject* kmed_step(PyObject* self, PyObject* args) {
+  Py_buffer Db, Ab;
+  PyObject* med;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "y*O!w*", &Db, &PyList_Type, &med, &Ab)) return NULL;
+  PyObject* out = NULL;
+  Py_ssize_t *mi = NULL, *cnt = NULL, *mem = NULL, *start = NULL;
+  float *vals = NULL, *intra = NULL;
+  const Py_ssize_t k = PyList_GET_SIZE(med);
+  const Py_ssize_t N = Ab.len / (Py_ssize_t)sizeof(int64_t);
+  if (Db.len != N * N * (Py_ssize_t)sizeof(float) || k < 1 || N < 1) {
+    PyErr_SetString(PyExc_ValueError, "rmsdkey.kmed_step: D must be float32 (N, N) and assign int64 (N,)");
+    goto done;
+  }
+  const float* D = (const float*)Db.buf;
+  int64_t* as = (int64_t*)Ab.buf;
+  mi = PyMem_Malloc(k * sizeof *mi);
+  cnt = PyMem_Calloc(k + 1, sizeof *cnt);
+  start = PyMem_Malloc((k + 1) * sizeof *start);
+  mem = PyMem_Malloc(N * sizeof *mem);
+  vals = PyMem_Malloc(k * sizeof *vals);
+  intra = PyMem_Malloc(N * sizeof *intra);
+  if (!mi || !cnt || !start || !mem || !vals || !intra) {
+    PyErr_NoMemory();
+    goto done;
+  }
+  for (Py_ssize_t j = 0; j < k; j++) {
+    mi[j] = PyLong_AsSsize_t(PyList_GET_ITEM(med, j));
+    if (mi[j] == -1 && PyErr_Occurred()) goto done;
+    if (mi[j] < 0) mi[j] += N;  /* (numpy's negative index) */
+    if (mi[j] < 0 || mi[j] >= N) {
+      PyErr_SetString(PyExc_IndexError, "rmsdkey.kmed_step: medoid index out of range");
+      goto done;
+    }
+  }
+  for (Py_ssize_t i = 0; i < N; i++) {
+    const float* row = D + i * N;
+    for (Py_ssize_t j = 0; j < k; j++) vals[j] = row[mi[j]];
+    as[i] = (int64_t)argmin_f32(vals, k);
+    cnt[as[i] + 1]++;
+  }
+  start[0] = 0;
+  for (Py_ssize_t j = 0; j < k; j++) start[j + 1] = start[j] + cnt[j + 1];
+  for (Py_ssize_t j = 0; j <= k; j++) cnt[j] = start[j];
+  for (Py_ssize_t i = 0; i < N; i++) mem[cnt[as[i]]++] = i;  /* (np.where order: ascending) */
+  out = PyList_New(k);
+  for (Py_ssize_t j = 0; out && j < k; j++) {
+    const Py_ssize_t n = start[j + 1] - start[j];
+    Py_ssize_t pick = -1;
+    if (n) {
+      const Py_ssize_t* ix = mem + start[j];
+      for (Py_ssize_t a = 0; a < n; a++) intra[a] = pw_sum(D + ix[a] * N, ix, n);
+      pick = ix[argmin_f32(intra, n)];
+    }
+    PyObject* v = PyLong_FromSsize_t(pick);
+    if (!v) {
+      Py_CLEAR(out);
+      break;
+    }
+    PyList_SET_ITEM(out, j, v);
+  }
+done:
+  PyMem_Free(mi);
+  PyMem_Free(cnt);
+  PyMem_Free(start);
+  PyMem_Free(mem);
+  PyMem_Free(vals);
+  PyMem_Free(intra);
+  PyBuffer_Release(&Db);
+  PyBuffer_Release(&Ab);
+  return out;
+}
+
 #if RMSDKEY_PROF
 static PyObject* prof(PyObject* self, PyObject* args) {
   (void)self;
@@ -1211,6 +1534,9 @@ static PyMethodDef METHODS[] = {
                                  "memo_check(on) -> memo hits compared since the last call (test)"},
                                 {"prio", prio, METH_VARARGS, "the priority updates of a merge (RmsdBPE._merge)"},
                                 {"packc", packc, METH_VARARGS, "pack() with spans as (chain, q, r)"},
+                                {"kmed_step", kmed_step, METH_VARARGS, "one k-medoids iteration (algo.py:191-213)"},
+                                {"packa", packa, METH_VARARGS, "pack() with spans as an int64 (n, 3) buffer"},
+                                {"spans_occ", spans_occ, METH_VARARGS, "the spans of a key's occurrences"},
                                 {NULL, NULL, 0, NULL}};
 static struct PyModuleDef MOD = {PyModuleDef_HEAD_INIT, "_rmsdkey", NULL, -1, METHODS, NULL, NULL, NULL, NULL};
 PyMODINIT_FUNC PyInit__rmsdkey(void) {

@@ -82,6 +82,14 @@ def k_medoids(strucs, k, max_iterations: int = 10, tol: float = 1e-4, *, rng=Non
     return k_medoids_from_matrix(rmsd_matrix(strucs, device=device), k, max_iterations, tol, rng=rng)
 
 
+KMED_C = True  # (False: the numpy loop below; tests compare the two)
+
+
+def _keyc():
+    from .rmsd_bpe import _KEYC
+    return _KEYC
+
+
 def k_medoids_from_matrix(D: np.ndarray, k, max_iterations: int = 10, tol: float = 1e-4, *, rng=None):
     """The iterations of algo.k_medoids (algo.py:191-213) on a given distance matrix."""
     N = len(D)
@@ -90,6 +98,24 @@ def k_medoids_from_matrix(D: np.ndarray, k, max_iterations: int = 10, tol: float
         rng = np.random.default_rng(None)
     medoid_indices = rng.choice(np.arange(N), size=k, replace=False)
     assignments = np.zeros(N, dtype=int)
+    keyc = _keyc() if KMED_C else None
+    if keyc is not None:  # (the iteration's assignment and medoid update in C, csrc/rmsdkey.c kmed_step)
+        Dc = np.ascontiguousarray(D, dtype=np.float32)
+        asg = np.zeros(N, dtype=np.int64)
+        for iteration in range(max_iterations):
+            picks = keyc.kmed_step(Dc, [int(m) for m in medoid_indices], asg)
+            total_shift = 0.0
+            new_medoid_indices = []
+            for j in range(k):
+                new_idx = picks[j] if picks[j] >= 0 else rng.integers(N)  # (empty cluster, j order)
+                shift = D[medoid_indices[j], new_idx]
+                total_shift += shift
+                new_medoid_indices.append(new_idx)
+            medoid_indices = new_medoid_indices
+            if total_shift < tol:
+                print(f"Converged in {iteration + 1} iterations with total shift {total_shift:.6f}.")
+                break
+        return medoid_indices
     for iteration in range(max_iterations):
         # (the reference's per-row np.argmin, all rows at once: the same float32 values, the
         # same first-minimum rule)

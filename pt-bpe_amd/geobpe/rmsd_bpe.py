@@ -405,6 +405,8 @@ class RmsdBPE:
     def _span_coords(self, spans, orig):
         """Tokenizer.compute_coords(index, length, orig) for [(chain, index, length)], one
         device NeRF batch: the span rounded out to whole residues, then its atoms."""
+        if isinstance(spans, np.ndarray):  # (_occ_spans' int64 rows)
+            return self._span_coords_idx(spans, orig) if len(spans) else []
         if _KEYC is not None and spans and not isinstance(spans[0][0], _Chain):
             return self._span_coords_idx(spans, orig)
         packs, geos, cuts = [], [], []
@@ -436,7 +438,7 @@ class RmsdBPE:
         """_span_coords of spans on chains given by index, in arrays: the NeRF layout packed in
         C (csrc/rmsdkey.c packc), the atoms cut out of the batch's output with one gather.  Spans
         of one atom count (a merge's occurrences) come back as one (n, atoms, 3) array."""
-        sp = np.asarray(spans, dtype=np.int64).reshape(len(spans), 3)
+        sp = spans if isinstance(spans, np.ndarray) else np.asarray(spans, dtype=np.int64).reshape(len(spans), 3)
         ci, index = sp[:, 0], sp[:, 1]
         na = self.__dict__.get("_nres_a")
         if na is None or len(na) != len(self._chains):
@@ -448,7 +450,7 @@ class RmsdBPE:
         off = np.zeros(len(sp) + 1, dtype=np.int64)
         np.cumsum(r, out=off[1:])
         packed = np.zeros((int(off[-1]), 9), dtype=np.float64)
-        _KEYC.packc(self._chains, bool(orig), list(zip(ci.tolist(), (start // 3).tolist(), r.tolist())), packed)
+        _KEYC.packa(self._chains, bool(orig), np.ascontiguousarray(np.stack([ci, start // 3, r], axis=1)), packed)
         atoms = _rmsd.nerf_atoms(off, packed, device=self.device)
         first = 3 * off[:-1] + (index - start)
         cnt = length + 1
@@ -457,6 +459,15 @@ class RmsdBPE:
             flat = np.ascontiguousarray(atoms).reshape(-1)
             return flat.take((3 * first)[:, None] + np.arange(3 * c)).reshape(len(first), c, 3)
         return [atoms[f:f + c] for f, c in zip(first.tolist(), cnt.tolist())]
+
+    def _occ_spans(self, occ, length):
+        """[(ci, token_pos[i2 - 1], length) for (ci, i2) in occ] (bpe.py:1759-1763), as int64
+        rows built in C when the extension is there"""
+        if _KEYC is not None:
+            sp = np.empty((len(occ), 3), dtype=np.int64)
+            _KEYC.spans_occ(self._chains, occ, length, sp)
+            return sp
+        return [(ci, self._chains[ci].token_pos[index - 1], length) for ci, index in occ]
 
     def _pack_item(self, p, orig):
         ci, q, r = p
@@ -842,7 +853,7 @@ class RmsdBPE:
         N = len(occ)
         active = (self.rng.choice(N, self.max_num_strucs, replace=False) if N > self.max_num_strucs
                   else np.arange(N))
-        spans = [(ci, self._chains[ci].token_pos[index - 1], length) for ci, index in occ]
+        spans = self._occ_spans(occ, length)
         sup = self.rmsd_super_res
         coords = self._span_coords(spans, sup)
         act = coords[active] if isinstance(coords, np.ndarray) else [coords[i] for i in active]
@@ -850,7 +861,7 @@ class RmsdBPE:
         assign = self._assign(coords, [act[m] for m in medoids])
         strucs = []
         for m in medoids:
-            ci, i1, _ = spans[int(active[m])]
+            ci, i1 = (int(x) for x in spans[int(active[m])][:2])
             strucs.append(self._chains[ci].geo(i1, length, sup))
         self._sphere_dict[key] = strucs
         return occ, assign
@@ -871,7 +882,7 @@ class RmsdBPE:
                 raise AttributeError("'BPE' object has no attribute '_sphere_dict'")
             if recurring:
                 occ = list(self._geo_dict[key])
-                spans = [(ci, self._chains[ci].token_pos[index - 1], length) for ci, index in occ]
+                spans = self._occ_spans(occ, length)
                 assign = self._assign(self._span_coords(spans, self.rmsd_super_res),
                                       self._struc_coords(self._sphere_dict[key]))
             else:

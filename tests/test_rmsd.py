@@ -36,6 +36,59 @@ def test_k_medoids_loop_matches_reference(ref):
     assert [int(x) for x in m3] == ref["medoids3_ref"].tolist()
 
 
+def _kmed_both(D, k, seed, max_iterations=10):
+    from geobpe import rmsd
+    out = []
+    for c in (False, True):
+        rmsd.KMED_C = c
+        try:
+            out.append([int(x) for x in rmsd.k_medoids_from_matrix(D, k, max_iterations,
+                                                                   rng=np.random.default_rng(seed))])
+        finally:
+            rmsd.KMED_C = True
+    return out
+
+
+def test_k_medoids_c_step_equals_numpy_loop(ref):
+    """csrc/rmsdkey.c kmed_step (numpy's float32 pairwise row sums and argmin rules in C)
+    gives the numpy loop's medoids: the reference's matrices, random ones of every size the
+    summation splits differently (below 8, up to 128, halves above), tied and quantised
+    values, empty clusters (rng re-seeds) and a NaN."""
+    from geobpe import rmsd
+    if rmsd._keyc() is None:
+        pytest.skip("_rmsdkey.so not built")
+    for D, k, s in ((ref["D_ref"], 5, 3), (ref["D3_ref"], 4, 5)):
+        a, b = _kmed_both(D, k, s)
+        assert a == b
+    g = np.random.default_rng(11)
+    for n in (1, 2, 3, 7, 8, 9, 15, 16, 17, 100, 127, 128, 129, 136, 255, 256, 257, 300, 500):
+        for trial in range(3):
+            X = g.random((n, 3)) * 10
+            D = np.sqrt(((X[:, None] - X[None]) ** 2).sum(-1)).astype(np.float32)
+            if trial == 1:
+                D = np.round(D * 2) / 2  # (ties everywhere)
+            if trial == 2:
+                D = g.random((n, n)).astype(np.float32) * 1e4  # (asymmetric, large sums)
+            for k in (1, 2, 5, 9):
+                a, b = _kmed_both(D, k, 100 * n + trial)
+                assert a == b, (n, trial, k)
+    for n in (9, 40, 128, 200, 333):  # (every row a permutation of one multiset: the medoid is
+        #                                decided by the summation order's rounding alone)
+        v = (g.random(n) * 1e3).astype(np.float32)
+        D = np.stack([g.permutation(v) for _ in range(n)])
+        a, b = _kmed_both(D, 1, n)
+        assert a == b, n
+        sums = D.sum(axis=1)
+        assert len(set(sums.tolist())) > 1 or n < 16  # (the order does change the sums)
+    D = np.zeros((12, 12), dtype=np.float32)  # (every row ties: all to medoid 0, the rest empty)
+    a, b = _kmed_both(D, 4, 1)
+    assert a == b
+    D = g.random((40, 40)).astype(np.float32)
+    D[5, 7] = np.nan
+    a, b = _kmed_both(D, 3, 2)
+    assert a == b
+
+
 @pytest.mark.gpu
 def test_device_rmsd_matches_reference(ref):
     from geobpe import rmsd
