@@ -26,11 +26,36 @@
 #pragma once
 // (included inside namespace gb)
 
+// a store written through to memory (gfx950 `global_store ... sc1`: 8-B relaxed agent-scope
+// atomic stores; a 4-B value as one 4-B store): the line leaves the XCD's L2 during the kernel,
+// so the kernel's end has no dirty bytes of it to write back (the boundary costs ~bytes / 6 TB/s
+// on top of ~1.5 us)
+template <typename V>
+__device__ inline void wt_store(V* p, const V& v) {
+  static_assert(sizeof(V) % 8 == 0 || sizeof(V) == 4, "store width");
+  if constexpr (sizeof(V) % 8 == 0) {
+    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&v);
+    unsigned long long* dst = reinterpret_cast<unsigned long long*>(p);
+#pragma unroll
+    for (int i = 0; i < (int)(sizeof(V) / 8); i++)
+      __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), *reinterpret_cast<const uint32_t*>(&v), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // k_find's outputs (merge entries, key / decrement records, T slots) are read once, by
-// k_commit / k_place on other XCDs: FIND_NT=1 stores them non-temporal (A/B)
+// k_commit / k_place on other XCDs: FIND_NT=1 stores them non-temporal (A/B), FIND_WT=1
+// write-through
+#ifndef FIND_WT
+#define FIND_WT 0
+#endif
 template <typename V>
 __device__ inline void out_store(V* p, const V& v) {
-#if FIND_NT
+#if FIND_WT
+  wt_store(p, v);
+#elif FIND_NT
   static_assert(sizeof(V) % 16 == 0 || sizeof(V) == 8 || sizeof(V) == 4, "store width");
   if constexpr (sizeof(V) % 16 == 0) {
     const int4* src = reinterpret_cast<const int4*>(&v);
@@ -683,12 +708,12 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   }
   __syncthreads();
   for (int i = threadIdx.x; i < D.NBA; i += ABLOCK) {
-    D.cntK[cnt_at(D, i, r)] = min(S.curK[i], SK);
-    D.cntD[cnt_at(D, i, r)] = min(S.curD[i], SD);
+    out_store(&D.cntK[cnt_at(D, i, r)], min(S.curK[i], SK));
+    out_store(&D.cntD[cnt_at(D, i, r)], min(S.curD[i], SD));
   }
   if (threadIdx.x == 0) {
-    D.Lcnt[r] = min(S.n, (int32_t)D.LC);
-    D.Tcnt[r] = S.tb;  // (T entries of this region: [r * TC, + Tcnt))
+    out_store(&D.Lcnt[r], min(S.n, (int32_t)D.LC));
+    out_store(&D.Tcnt[r], S.tb);  // (T entries of this region: [r * TC, + Tcnt))
   }
 #if EARLY_LOADS
   check_found_tail(D, r, nchk, chk0);
@@ -1409,21 +1434,35 @@ __device__ inline int32_t place_rec_at(const Dev& D, const PlaceLds& S, int32_t 
   return (int32_t)((int64_t)D.NBA * D.NBA * SK + k_lo + (i - nk));
 }
 
+// k_place's token rewrites, pk and posting-log entries (read by the next k_find on every XCD):
+// PLACE_WT=1 stores them write-through (A/B)
+#ifndef PLACE_WT
+#define PLACE_WT 0
+#endif
+template <typename V>
+__device__ inline void pl_store(V* p, const V& v) {
+#if PLACE_WT
+  wt_store(p, v);
+#else
+  *p = v;
+#endif
+}
+
 // a single record (one occurrence, its slot in tstart as -(slot + 1)) of finder region j: pk
 // of the slot and its posting-log entry.  Grouped records are written through their T entries.
 __device__ inline void place_single(const Dev& D, int32_t at, int2 nt, int2 v) {
   if (nt.y >= 0 || v.x < 0) return;
   const int32_t t = -(nt.y + 1);
-  *tok_f(D, t, 3) = v.x;
-  if (v.y >= 0) D.pool[log_addr(D, place_owner(D, at), v.y)] = make_int2(v.x, t);
+  pl_store(tok_f(D, t, 3), v.x);
+  if (v.y >= 0) pl_store(&D.pool[log_addr(D, place_owner(D, at), v.y)], make_int2(v.x, t));
 }
 
 // T entry {slot, record} at T index q: pk of the slot and its posting-log entry (its position
 // in the record's range: the record's log position + q - tstart)
 __device__ inline void place_tentry(const Dev& D, int64_t q, int2 e, int2 v, int32_t tstart) {
   if (e.y < 0 || v.x < 0) return;
-  *tok_f(D, e.x, 3) = v.x;
-  if (v.y >= 0) D.pool[log_addr(D, place_owner(D, e.y), (int64_t)v.y + (q - tstart))] = make_int2(v.x, e.x);
+  pl_store(tok_f(D, e.x, 3), v.x);
+  if (v.y >= 0) pl_store(&D.pool[log_addr(D, place_owner(D, e.y), (int64_t)v.y + (q - tstart))], make_int2(v.x, e.x));
 }
 
 // place the merge committed with launch parity st->place_par (k_commit sets it; -1:
@@ -1485,12 +1524,12 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   // ---- the token rewrites of find region j (round 1's data)
   for (int64_t i = t; i < nA + o_n; i += ABLOCK) {
     const LEntry e = i < nA ? (i == t ? eA : D.L[(int64_t)j * D.LC + i]) : D.Lovf[o_lo + (i - nA)];
-    *reinterpret_cast<int2*>(D.tok + e.a) = make_int2(nid, e.ya);
-    D.tok[e.b] = make_int4(-1, 0, -1, -1);  // (no other occurrence writes b's record)
+    pl_store(reinterpret_cast<int2*>(D.tok + e.a), make_int2(nid, e.ya));
+    pl_store(D.tok + e.b, make_int4(-1, 0, -1, -1));  // (no other occurrence writes b's record)
     if (e.c >= 0)
-      *tok_f(D, e.c, 2) = e.a;
+      pl_store(tok_f(D, e.c, 2), e.a);
     else
-      *tok_f(D, e.a, 3) = -1;
+      pl_store(tok_f(D, e.a, 3), (int32_t)-1);
   }
   dbg_stamp(D, 31);
   // ---- pk of every new pair and its posting-log entry

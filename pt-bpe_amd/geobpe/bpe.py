@@ -199,16 +199,19 @@ def _check_scope(bins, bin_strategy, res_init, std_bonds, rmsd_partition_min_siz
 class BPE:
     def __new__(cls, *args, **kwargs):
         """A finite rmsd_partition_min_size (the reference's default is 4) selects the
-        RMSD-partitioned mode, geobpe.rmsd_bpe.RmsdBPE."""
+        RMSD-partitioned mode, geobpe.rmsd_bpe.RmsdBPE; so do a multi-grid
+        schedule and bond-level init (res_init=False)."""
         if cls is BPE:
             import inspect
             ba = inspect.signature(BPE.__init__).bind(None, *args, **kwargs)
             ba.apply_defaults()
             p = ba.arguments["rmsd_partition_min_size"]
             bins = ba.arguments["bins"]
-            if (p != float("inf") and p < 10 ** 9) or (isinstance(bins, dict) and len(bins) > 1 and 1 in bins):
-                # the host mirror: RMSD partitioning, or a multi-grid schedule without it (the
-                # reference's stale-key semantics, DESIGN §7); the device engine runs bins={1: B}
+            if (p != float("inf") and p < 10 ** 9) or (isinstance(bins, dict) and len(bins) > 1 and 1 in bins) \
+                    or not ba.arguments["res_init"]:
+                # the host mirror: RMSD partitioning, a multi-grid schedule without it (the
+                # reference's stale-key semantics, DESIGN §7), or bond-level init (res_init=False,
+                # bpe.py:397-420); the device engine runs bins={1: B} from residue tokens
                 from .rmsd_bpe import RmsdBPE
                 return RmsdBPE(*args, **kwargs)
         return super().__new__(cls)

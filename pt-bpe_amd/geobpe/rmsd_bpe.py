@@ -355,8 +355,10 @@ class RmsdBPE:
             raise NotImplementedError("the RMSD mode runs on one GPU (no row sharding)")
         if not isinstance(bins, dict) or 1 not in bins:
             raise KeyError("bins must be a dict with key 1 (quantize/capacity need bins[1], bpe.py:896,909,952)")
-        if not res_init:
-            raise NotImplementedError("the RMSD mode needs res_init=True (bond-level init is not built)")
+        if not res_init and not std_bonds:  # (no reference fixture pins it)
+            raise NotImplementedError("bond-level init (res_init=False) with free bond lengths is not built")
+        if not res_init and glue_opt:  # (glue optimisation works on residue tokens' exit frames)
+            raise NotImplementedError("glue optimisation with bond-level init (res_init=False) is not built")
         if not std_bonds and bin_strategy == "uniform":
             raise NotImplementedError("free bonds with uniform (equal-count) bins are not built")
         if glue_opt and glue_opt_method not in ("all", "each"):
@@ -526,8 +528,26 @@ class RmsdBPE:
         for r in range(self.n):
             cols = {c: np.asarray(self._corpus[c][ro[r]:ro[r + 1]], dtype=np.float64) for c in COLUMNS}
             self._chains.append(_Chain(cols, init, self._fnames[r] if self._fnames else None))
-        self._init_residues()
+        if self.res_init:
+            self._init_residues()
+        else:
+            self._init_bonds()
         return self
+
+    def _init_bonds(self):
+        """_init_tokens (bpe.py:397-420), res_init=False: every bond its own initial token --
+        token ids 0, 1, 2 = {N:CA: [0]}, {CA:C: [0]}, {0C:1N: [0]} by the bond's type
+        (Tokenizer.bond_labels, tokenizer.py:49) -- each bond set to its type's standard length
+        (std_bonds); the angles stay raw (the glue snap is the residue init's, bpe.py:381-391)."""
+        self._tokens = {i: {BOND_TYPES[i]: [0]} for i in range(3)}
+        std = {bt: sum(self._thresholds[bt][0]) / 2 for bt in BOND_TYPES}
+        for c in self._chains:
+            c.init[0], c.init[1] = std["N:CA"], std["CA:C"]
+            for bt in BOND_TYPES:
+                c.cur[bt][:max(c.n - 1, 0)] = [std[bt]] * max(c.n - 1, 0)
+            c.btt = {j: (j, j % 3, 1) for j in range(3 * c.n - 1)}
+            c.token_pos = list(range(3 * c.n - 1))
+            c.tokens0 = list(c.btt.values())
 
     def _grid_thresholds(self):
         """{size: thresholds} of the six angle types for every grid of ``bins``

@@ -75,9 +75,16 @@ FIXTURES = {
     "rm_p0_rmsd_only": (10, 20, 40, 21, 5, 0, False, 60, 25),
     "rm_p3_super_rmsd_only": (8, 15, 35, 22, 4, 3, True, 50, 20),
     "rm_p0_b2_long_rmsd_only": (16, 12, 30, 25, 2, 0, False, 80, 120),
+    # bond-level init (res_init=False): every bond its own token, pairs of bonds first
+    "rm_p0_bondinit": (8, 15, 30, 35, 5, 0, False, 60, 40),
+    "rm_p3_super_bondinit": (8, 15, 30, 36, 4, 3, True, 60, 40),
+    "rm_pinf_bondinit": (8, 15, 30, 37, 5, float("inf"), False, 60, 40),
+    "rm_pinf_bondinit_b3_long": (12, 20, 40, 38, 3, float("inf"), False, 60, 250),
 }
 # further BPE(...) arguments of a fixture
 EXTRA = {n: {"rmsd_only": True} for n in FIXTURES if n.endswith("_rmsd_only")}
+# bond-level init (res_init=False, bpe.py:397-420): every bond its own initial token
+EXTRA.update({n: {"res_init": False} for n in FIXTURES if "_bondinit" in n})
 # BPE.tokenize (bpe.py:1053-1140, the RMSD mode's induce) after the training calls, on: the
 # first three training chains, the first 60 % of chains 3 and 4 (values inside the trained
 # bins), and new synthetic chains (chains, len_lo, len_hi, seed) -- those usually hold a value
@@ -160,7 +167,7 @@ def run_one(name):
     arrays = dict(corpus)
     bpe = RB.BPE(structs, bins=bins, save_dir=tempfile.mkdtemp(prefix="geobpe_rmsd_golden_"),
                  rmsd_partition_min_size=p, rmsd_super_res=sup, num_partitions=dict(num_p),
-                 max_num_strucs=maxs, res_init=True, std_bonds=std, seed=0, **EXTRA.get(name, {}))
+                 max_num_strucs=maxs, std_bonds=std, seed=0, **({"res_init": True} | EXTRA.get(name, {})))
     try:
         bpe.initialize()
         geometry(bpe, "init", arrays)

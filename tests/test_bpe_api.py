@@ -16,7 +16,6 @@ def _bpe(meta, corpus):
 
 
 @pytest.mark.parametrize("kw, exc", [
-    (dict(res_init=False), NotImplementedError),
     (dict(rmsd_partition_min_size=3, glue_opt=True, glue_opt_method="other"), ValueError),
     (dict(rmsd_partition_min_size=2, compute_sec_structs=True), NotImplementedError),
     (dict(glue_opt=True), NotImplementedError),  # glue opt without RMSD partitioning (bpe.py:2027)

@@ -54,8 +54,8 @@ def run_and_compare(name, device=True):
     meta, corpus, arrs = _load(name)
     bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()}, rmsd_partition_min_size=meta["rmsd_partition_min_size"],
               rmsd_super_res=meta["rmsd_super_res"], num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
-              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta.get("std_bonds", True),
-              seed=meta["rng_seed"], **meta.get("extra", {}))
+              max_num_strucs=meta["max_num_strucs"], std_bonds=meta.get("std_bonds", True),
+              seed=meta["rng_seed"], **({"res_init": True} | meta.get("extra", {})))
     assert isinstance(bpe, RmsdBPE)
     if "init_tokens" not in meta:  # the reference raised in initialize()
         with pytest.raises(Exception) as ei:
@@ -152,6 +152,12 @@ def test_rmsd_mode_dispatch_and_scope():
         BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=3, compute_sec_structs=True)
     assert not isinstance(BPE.__new__(BPE, corpus, bins={1: 5}, res_init=True,
                                       rmsd_partition_min_size=float("inf")), RmsdBPE)
+    # bond-level init (res_init=False, bpe.py:397-420) runs in the host mirror at any p; with
+    # free bonds or glue optimisation it is not built
+    assert isinstance(BPE(corpus, bins={1: 5}, res_init=False, rmsd_partition_min_size=float("inf")), RmsdBPE)
+    for kw in (dict(std_bonds=False), dict(glue_opt=True)):
+        with pytest.raises(NotImplementedError):
+            BPE(corpus, bins={1: 5}, res_init=False, rmsd_partition_min_size=3, **kw)
 
 
 @pytest.mark.gpu
@@ -192,7 +198,12 @@ def resume(bpe, n):
         calls.append({"popped": popped[n0:], "step": bpe._step, "n_tokens": len(bpe._tokens)})
     return {"calls": calls,
             "segmentation": [[[int(s), tid(v[1]), int(v[2])] for s, v in t.bond_to_token.items()] for t in bpe.tokenizers],
-            "quantize": [[int(x) for x in bpe.quantize(t)] for t in bpe.tokenizers], "vocab_size": bpe.vocab_size}
+            "quantize": [quant(bpe, t) for t in bpe.tokenizers], "vocab_size": bpe.vocab_size}
+def quant(bpe, t):
+    try:
+        return [int(x) for x in bpe.quantize(t)]
+    except ValueError as e:  # (a NaN or out-of-range angle between tokens: recorded, as the fixtures do)
+        return {"raised": type(e).__name__}
 name, k, rest = sys.argv[4], int(sys.argv[5]), int(sys.argv[6])
 m = json.load(open(f"{sys.argv[2]}/{name}.json"))
 z = np.load(f"{sys.argv[2]}/{name}.npz")
@@ -207,7 +218,7 @@ for i, row in enumerate(synth.corpus_rows(corpus)):
 ref = B.BPE(structs, bins={int(a): b for a, b in m["bins"].items()}, save_dir=tempfile.mkdtemp(),
             rmsd_partition_min_size=m["rmsd_partition_min_size"], rmsd_super_res=m["rmsd_super_res"],
             num_partitions={int(a): b for a, b in m["num_partitions"].items()}, max_num_strucs=m["max_num_strucs"],
-            res_init=True, std_bonds=m.get("std_bonds", True), seed=0)
+            std_bonds=m.get("std_bonds", True), seed=0, **({"res_init": True} | m.get("extra", {})))
 ref.initialize()
 ref.bin()
 for _ in range(k):
@@ -219,7 +230,7 @@ print("JSON" + json.dumps({"own": own, "ours": ours}))
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference/foldingdiff"), reason="reference not present (GPU box)")
-@pytest.mark.parametrize("name", ["rm_p0", "rm_p0_multigrid", "rm_p0_super"])
+@pytest.mark.parametrize("name", ["rm_p0", "rm_p0_multigrid", "rm_p0_super", "rm_pinf_bondinit"])
 def test_reference_resumes_rmsd_mode_checkpoint(name, host_geometry, tmp_path):
     """bpe_iter=*.pkl of the RMSD mode: the reference unpickles this build's checkpoint
     taken after 10 step() calls and keeps training.  Its merges, segmentation, quantize ids
@@ -237,8 +248,8 @@ def test_reference_resumes_rmsd_mode_checkpoint(name, host_geometry, tmp_path):
     bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()},
               rmsd_partition_min_size=meta["rmsd_partition_min_size"], rmsd_super_res=meta["rmsd_super_res"],
               num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
-              max_num_strucs=meta["max_num_strucs"], res_init=True, std_bonds=meta.get("std_bonds", True),
-              seed=meta["rng_seed"])
+              max_num_strucs=meta["max_num_strucs"], std_bonds=meta.get("std_bonds", True),
+              seed=meta["rng_seed"], **({"res_init": True} | meta.get("extra", {})))
     bpe.initialize()
     bpe.bin()
     k = 10
