@@ -338,6 +338,38 @@ class RmsdTokenizer:
         return out
 
 
+class _RmsdGroup:
+    """The RMSD mode over several processes (``RmsdBPE(group=...)``): every rank holds the whole
+    corpus and the same host state (the bookkeeping is replicated and deterministic), and the
+    per-merge assignment batch is split across the ranks.  ``group``: a torch.distributed
+    process group, ``True`` for the default one, or an object carrying one as ``.pg``
+    (geobpe.dist.TorchGroup)."""
+
+    def __init__(self, group):
+        import torch
+        import torch.distributed as dist
+        pg = None if group is True else getattr(group, "pg", group)
+        self.torch, self.dist, self.pg = torch, dist, pg
+        self.rank = dist.get_rank(pg)
+        self.world = dist.get_world_size(pg)
+        self.dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(pg) == "nccl" \
+            else torch.device("cpu")
+
+    def gather_chunks(self, mine: np.ndarray, n: int) -> np.ndarray:
+        """The ranks' contiguous chunks [n * r // world, n * (r + 1) // world) of an int64
+        array of n, all-gathered in rank order"""
+        torch = self.torch
+        w = self.world
+        cap = -(-n // w) + 1
+        t = torch.full((cap,), -1, dtype=torch.int64)
+        t[:len(mine)] = torch.from_numpy(mine)
+        t = t.to(self.dev)
+        outs = [torch.empty_like(t) for _ in range(w)]
+        self.dist.all_gather(outs, t, group=self.pg)
+        parts = [outs[r][:n * (r + 1) // w - n * r // w].cpu().numpy() for r in range(w)]
+        return np.concatenate(parts)
+
+
 class RmsdBPE:
     """foldingdiff.bpe.BPE with a finite rmsd_partition_min_size (see the module docstring).
     Constructed by ``geobpe.bpe.BPE(...)`` when the arguments ask for this mode."""
@@ -351,8 +383,6 @@ class RmsdBPE:
                  max_num_strucs=500, glue_opt=False, glue_opt_prior=0.0, glue_opt_every=10,
                  glue_opt_method="all", seed=None, device: int = 0, group=None, **_unused):
         from .bpe import ThresholdDict, structures_to_corpus
-        if group is not None:
-            raise NotImplementedError("the RMSD mode runs on one GPU (no row sharding)")
         if not isinstance(bins, dict) or 1 not in bins:
             raise KeyError("bins must be a dict with key 1 (quantize/capacity need bins[1], bpe.py:896,909,952)")
         if not res_init and not std_bonds:  # (no reference fixture pins it)
@@ -402,6 +432,7 @@ class RmsdBPE:
         self._chains = []
         self._merge_log = []  # [key, count] of every merge popped, recurring repeats included
         self.assign_calls = 0  # device assignment batches (tests check the GPU path ran)
+        self._group = _RmsdGroup(group) if group is not None else None
 
     # ------------------------------------------------------------ geometry on the device
     def _span_coords(self, spans, orig):
@@ -501,11 +532,20 @@ class RmsdBPE:
 
     def _assign(self, coords, medoid_coords):
         """_compute_assignment_inner for every occurrence (bpe.py:654-657): argmin over the
-        medoids of compute_rmsd(occurrence, medoid) -- one device launch."""
+        medoids of compute_rmsd(occurrence, medoid) -- one device launch.  With a process
+        group each rank takes a contiguous 1/world of the occurrences on its own GPU and the
+        assignments are all-gathered (the reference fans this out over a process pool,
+        bpe.py:1766-1777); every rank then holds all of them."""
         self.assign_calls += 1
         if len(coords) == 0:
             return []
-        return [int(a) for a in _rmsd.assign(coords, medoid_coords, device=self.device)]
+        g = self._group
+        if g is None or g.world == 1:
+            return [int(a) for a in _rmsd.assign(coords, medoid_coords, device=self.device)]
+        n = len(coords)
+        lo, hi = n * g.rank // g.world, n * (g.rank + 1) // g.world
+        mine = _rmsd.assign(coords[lo:hi], medoid_coords, device=self.device) if hi > lo else []
+        return [int(a) for a in g.gather_chunks(np.asarray(mine, dtype=np.int64), n)]
 
     # ------------------------------------------------------------ initialize (bpe.py:91-103)
     def initialize(self, path=None):
@@ -1432,10 +1472,13 @@ class RmsdBPE:
         return out
 
     def save_checkpoint(self, path: str) -> None:
-        """``bpe_iter=t.pkl`` in the reference's format (bin/encode.py:427), written atomically."""
+        """``bpe_iter=t.pkl`` in the reference's format (bin/encode.py:427), written atomically
+        (with a process group by rank 0 only: every rank holds the same state)."""
         import os
 
         from . import refpickle as R
+        if self._group is not None and self._group.rank != 0:
+            return
         tmp = path + ".tmp"
         with open(tmp, "wb") as f:
             R.dump(self.checkpoint_object(), f)

@@ -548,3 +548,86 @@ def test_prio_queue_order_matches_sorted_container():
             assert q[0] == ref[0]
         if step % 50 == 0:
             assert list(q) == list(ref) and q[:7] == list(ref[:7])
+
+
+def _group_worker(rank, world, port, names, q, device=False):
+    """one rank of a gloo group running the RMSD mode on the whole corpus: on the GPU (device)
+    or with the oracle's stand-ins for the device batches (the host_geometry fixture, by hand:
+    no pytest here)"""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "pt-bpe_amd"))
+    sys.path.insert(0, os.path.dirname(here))
+    sys.path.insert(0, here)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle.prologue as prologue
+        import oracle.rmsd as orm
+        from geobpe import rmsd, rmsd_bpe
+        from geobpe.bpe import BPE
+        if not device:
+            rmsd.nerf_atoms = lambda off, packed, device=0: orm.nerf_atoms(off, packed)
+            rmsd.nerf_packed = lambda off, packed, device=0: orm.nerf_packed(off, packed)
+            rmsd.geo_coords = lambda geos, device=0: [orm.nerf(g) for g in geos]
+            rmsd.rmsd_matrix = lambda S, device=0: orm.rmsd_matrix(S)
+            rmsd.rmsd_cross = lambda A, B, device=0: np.array([[orm.rmsd(a, b) for b in B] for a in A])
+            rmsd_bpe.RmsdBPE._grid_thresholds = lambda self: {s: prologue.thresholds(self._corpus, b)
+                                                              for s, b in self.bins.items()}
+        for name in names:
+            meta, corpus, _ = _load(name)
+            bpe = BPE(corpus, bins={int(k): v for k, v in meta["bins"].items()},
+                      rmsd_partition_min_size=meta["rmsd_partition_min_size"], rmsd_super_res=meta["rmsd_super_res"],
+                      num_partitions={int(k): v for k, v in meta["num_partitions"].items()},
+                      max_num_strucs=meta["max_num_strucs"], std_bonds=meta.get("std_bonds", True),
+                      seed=meta["rng_seed"], group=True, **({"res_init": True} | meta.get("extra", {})))
+            calls = []
+            bpe.initialize()
+            bpe.bin()
+            for _ in meta["calls"]:
+                n0 = len(bpe._merge_log)
+                bpe.step()
+                calls.append([[k, c] for k, c in bpe._merge_log[n0:]])
+            want = [[[p[2], -p[1]] for p in c["popped"]] for c in meta["calls"]]
+            assert calls == want, f"{name}: merges differ"
+            assert _segmentation(bpe) == meta["segmentation"], f"{name}: segmentation"
+            assert bpe.assign_calls > 0
+        q.put((rank, "ok"))
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rmsd_mode_process_group_gloo():
+    """RmsdBPE(group=...) at world size 2 over gloo: each rank assigns half of every merge's
+    occurrences and the halves are all-gathered; both ranks reproduce the reference's merges and
+    segmentation (the single-process fixtures)."""
+    _group_run(False)
+
+
+@pytest.mark.gpu
+def test_rmsd_mode_process_group_device():
+    """The same with the device batches: two ranks on one GPU, gloo for the all-gather."""
+    _group_run(True)
+
+
+def _group_run(device):
+    import multiprocessing as mp
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    names = ["rm_p0_super", "rm_p2_super_b3"]
+    ps = [ctx.Process(target=_group_worker, args=(r, 2, port, names, q, device)) for r in range(2)]
+    for p in ps:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in ps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res == {0: "ok", 1: "ok"}, res
