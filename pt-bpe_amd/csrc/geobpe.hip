@@ -805,7 +805,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   if ((rc = dalloc(c, &D.post, (int64_t)c->nba * D.PR)) || (rc = dalloc(c, &D.poff, (int64_t)c->nba * (NBKT + 1), 0)) ||
       (rc = dalloc(c, &D.pool, D.POOL_CH * D.CHUNK)) || (rc = dalloc(c, &D.pch, (int64_t)c->nba * D.MAXCH)) ||
       (rc = dalloc(c, &D.pnch, c->nba, 0)) || (rc = dalloc(c, &D.pfill, c->nba, 0)) ||
-      (rc = dalloc(c, &D.KS, (int64_t)c->nba * c->nba * SK + D.KO_cap)) || (rc = dalloc(c, &D.cntK, (int64_t)c->nba * c->nba, 0)) ||
+      (rc = dalloc(c, &D.KS, (int64_t)c->nba * c->nba * SK + D.KO_cap)) || (rc = dalloc(c, &D.cntK, 2 * (int64_t)c->nba * c->nba, 0)) ||
       (rc = dalloc(c, &D.DS, (int64_t)c->nba * c->nba * SD)) || (rc = dalloc(c, &D.cntD, (int64_t)c->nba * c->nba, 0)) ||
       (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) || (rc = dalloc(c, &D.Tcnt, c->nba, 0)) ||
       (rc = dalloc(c, &D.KSid, (int64_t)c->nba * c->nba * SK + D.KO_cap)))

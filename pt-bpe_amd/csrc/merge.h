@@ -88,6 +88,18 @@ __device__ inline void out_store(V* p, const V& v) {
 __device__ inline int64_t cnt_at(const Dev& D, int32_t o, int32_t r) {
   return CNT_T ? (int64_t)r * D.NBA + o : (int64_t)o * D.NBA + r;
 }
+// CNT_PAIR = 1: the two counts of a (finder, owner) as one int2 in cntK (allocated 2 x NBA^2),
+// so an owner's first round loads one strided line set instead of two
+#ifndef CNT_PAIR
+#define CNT_PAIR 1
+#endif
+__device__ inline int2 cnt_pair(const Dev& D, int32_t o, int32_t r) {
+#if CNT_PAIR
+  return reinterpret_cast<const int2*>(D.cntK)[cnt_at(D, o, r)];
+#else
+  return make_int2(D.cntK[cnt_at(D, o, r)], D.cntD[cnt_at(D, o, r)]);
+#endif
+}
 
 // chunked per-owner posting log: entry k of owner o
 __device__ inline int64_t log_addr(const Dev& D, int o, int64_t k) {
@@ -221,6 +233,7 @@ struct FindLds {
   int32_t curK[NBA_MAX], curD[NBA_MAX];
   int32_t red[ABLOCK / 64];
   int32_t qn, n, tb, fits, ktot;
+  int32_t qsteal;  // FIND_STEAL: the round's next unclaimed candidate
 };
 
 __device__ inline void emit_occ(const Dev& D, FindCtx& F, int32_t* s_n, int32_t a, int32_t ya, int32_t b, int32_t c) {
@@ -306,12 +319,13 @@ __device__ inline void right_half(const Dev& D, const FindCtx& F, const FindLds&
 // run start's left neighbour p is a right part iff the W-run ending at (pp, p) has
 // odd length.  The first occurrence's new keys are returned (grouped by the caller),
 // a run's later occurrences send theirs as single records.
-__device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf& hl, bool& vl, FHalf& hr,
+// (returns true when g is no occurrence to walk: a stale posting or not a run start)
+__device__ bool find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf& hl, bool& vl, FHalf& hr,
                           bool& vr) {
   vl = vr = false;
   const int32_t W = F.W;
   const int4 tg = D.tok[g];  // {tid, tlen, tprev, pk}
-  if (tg.w != W) return;
+  if (tg.w != W) return true;
   dbg_stamp(D, 40);
   const int32_t p = tg.z;
   const int32_t b = g + tok_len(tg.y);
@@ -319,7 +333,7 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
   const int32_t ip = p >= 0 ? p : g;
   const int4 tp = D.tok[ip];
   const int4 tb = D.tok[b];
-  if (p >= 0 && tp.w == W) return;  // not a run start: its run's start walks it
+  if (p >= 0 && tp.w == W) return true;  // not a run start: its run's start walks it
   dbg_stamp(D, 41);
   const int32_t glL = p >= 0 ? next_glue(D, tp.y, g - 1) : 0;
   const int32_t glR = next_glue(D, tb.y, g + F.wl - 1);
@@ -403,6 +417,7 @@ __device__ void find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
     cur_cL = cL2;
     lcur_c = tok_len(tc2.y);
   }
+  return false;
 }
 
 // LDS dedupe slot of a new key (*res: this thread inserted it); -1 when the probes
@@ -429,6 +444,9 @@ __device__ inline int32_t fkc_find(FindLds& S, const Dev& D, u64 k, u64 h1, bool
   return -1;
 }
 
+#ifndef FIND_STEAL
+#define FIND_STEAL 1
+#endif
 #ifndef FAGG
 #define FAGG 0  // k_find: wave-aggregated LDS dedupe of the new keys (iterations; 0: off)
 #endif
@@ -582,6 +600,8 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   dbg_stamp(D, 11);
   const int64_t ntot = queued ? (int64_t)S.qn : n1 + (ls1 - ls0);
   const int2* P = D.post + (int64_t)r * D.PR + lo;
+  dbg_val(D, 60, ntot + 1);  // (debug timeline: posting entries scanned, +1)
+  int64_t dbg_nq = 0;
   for (int64_t c0 = 0; c0 < ntot; c0 += FMQ) {  // block-uniform
     int32_t nq;
     if (queued) {
@@ -612,11 +632,21 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       nq = S.qn;
     }
     if (c0 == 0) dbg_stamp(D, 14);
-    for (int32_t q0 = 0; q0 < nq; q0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
-      const int32_t qi = q0 + threadIdx.x;
+    dbg_nq += nq;
+    for (int32_t q0 = 0; q0 < nq;) {  // block-uniform rounds, one walked candidate per thread
+      int32_t qi = q0 + threadIdx.x;
       FHalf hl, hr;
       bool vl = false, vr = false;
+#if FIND_STEAL
+      // a thread whose candidate turns out stale or inside a run (~1/3 of them, known after one or
+      // two loads) takes the next candidate past the round's first ABLOCK: a workgroup with a few
+      // more candidates than threads walks them in this round instead of a second one (~10 us)
+      if (threadIdx.x == 0) S.qsteal = q0 + ABLOCK;
+      __syncthreads();
+      while (qi < nq && find_walk(D, F, S, S.q[qi], hl, vl, hr, vr)) qi = atomicAdd(&S.qsteal, 1);
+#else
       if (qi < nq) find_walk(D, F, S, S.q[qi], hl, vl, hr, vr);
+#endif
       if (c0 == 0 && q0 == 0) dbg_stamp(D, 15);
       // group the new keys of this round: LDS slot, rank within the slot
       bool rl = false, rr = false;
@@ -689,9 +719,17 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       }
       if (threadIdx.x == 0 && fits) S.tb += S.ktot;
       __syncthreads();
+#if FIND_STEAL
+      q0 = min(S.qsteal, nq);  // (block-uniform: read after the barrier above)
+      __syncthreads();  // (before thread 0 resets it for the next round)
+#else
+      q0 += ABLOCK;
+#endif
     }
   }
   dbg_stamp(D, 12);
+  dbg_val(D, 61, dbg_nq + 1);  // (candidates walked, +1)
+  dbg_val(D, 62, S.n + 1);     // (occurrences merged, +1)
   // step 1 (the merged pair, -1 on W per occurrence: S.n counts them) and the
   // decrements -> owners
   if (threadIdx.x == 0 && S.n && W >= 0) dec_add(D, F, S.u.m.agg, W, -S.n);
@@ -708,8 +746,12 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   }
   __syncthreads();
   for (int i = threadIdx.x; i < D.NBA; i += ABLOCK) {
+#if CNT_PAIR
+    out_store(reinterpret_cast<int2*>(D.cntK) + cnt_at(D, i, r), make_int2(min(S.curK[i], SK), min(S.curD[i], SD)));
+#else
     out_store(&D.cntK[cnt_at(D, i, r)], min(S.curK[i], SK));
     out_store(&D.cntD[cnt_at(D, i, r)], min(S.curD[i], SD));
+#endif
   }
   if (threadIdx.x == 0) {
     out_store(&D.Lcnt[r], min(S.n, (int32_t)D.LC));
@@ -1036,7 +1078,8 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const int32_t w = t % nba, k0 = t / nba;
   const bool lane_ok = k0 < PER;
   const int64_t seg = (int64_t)j * nba + w;
-  const int32_t cK = D.cntK[cnt_at(D, j, w)], cD = D.cntD[cnt_at(D, j, w)];
+  const int2 cKD = cnt_pair(D, j, w);
+  const int32_t cK = cKD.x, cD = cKD.y;
 #if COMMIT_SPEC
   // speculative: the first PER records of every finder's slot in the first round
   // (~15 MB per launch, mostly empty slots; it held the prefix scans below ~4 us)
@@ -1483,7 +1526,7 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   const int64_t novf = st->place_novf, nko = st->place_nko;
   const int32_t nA = D.Lcnt[j];
   const LEntry eA = D.L[(int64_t)j * D.LC + min((int64_t)t, D.LC - 1)];
-  const int32_t cK = t < D.NBA ? D.cntK[cnt_at(D, t, j)] : 0;
+  const int32_t cK = t < D.NBA ? cnt_pair(D, t, j).x : 0;
   const int32_t nT = min((int64_t)D.Tcnt[j], D.TC);
   const int2* Tj = D.T + (int64_t)j * D.TC;
   const int2 te0 = Tj[min(t, (int32_t)D.TC - 1)], te1 = Tj[min(t + ABLOCK, (int32_t)D.TC - 1)];

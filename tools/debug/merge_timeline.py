@@ -39,8 +39,9 @@ for it in iters:
         print(f"merge {it}: (no stamps)")
         continue
     vals = {7: "C.records(n)", 8: "C.decrements(n)", 9: "C.keys(n)", 54: "C.extras(n)", 55: "C.overflow(n)",
-            59: "C.dec_extras(n)"}
+            59: "C.dec_extras(n)", 60: "F.scanned(n+1)", 61: "F.cands(n+1)", 62: "F.occs(n+1)"}
     vv = t[:, [7, 8, 9, 54, 55, 59]].copy()
+    fv = t[:, [60, 61, 62]].copy() - 1
     for k, nm in vals.items():  # values, not times
         v = t[:, k][t[:, k] > 0]
         if len(v):
@@ -63,4 +64,12 @@ for it in iters:
             print(f"    {w:4d} " + " ".join(f"{rel[w, k]:7.1f}" for k in (1, 56, 57, 58, 2, 3, 53, 4, 6))
                   + f" | {vv[w, 0]:5d} {vv[w, 1]:5d} {vv[w, 2]:5d} {vv[w, 3]:5d} {vv[w, 4]:5d} {vv[w, 5]:5d}")
         print(f"  median work: krec {int(np.median(vv[:, 0]))} drec {int(np.median(vv[:, 1]))} keys {int(np.median(vv[:, 2]))}")
+    if not np.all(np.isnan(rel[:, 13])):  # the slowest find workgroups and their work
+        order = np.argsort(-np.nan_to_num(rel[:, 13], nan=-1e9))[:6]
+        print("  slowest find workgroups: wg  start  setup  queued  T1  r0.walked  grouped  walked  end | scanned  cands  occs")
+        for w in order:
+            print(f"    {w:4d} " + " ".join(f"{rel[w, k]:7.1f}" for k in (10, 11, 14, 40, 15, 16, 12, 13))
+                  + f" | {fv[w, 0]:6d} {fv[w, 1]:6d} {fv[w, 2]:6d}")
+        print(f"  median find work: scanned {int(np.median(fv[:, 0]))} cands {int(np.median(fv[:, 1]))} "
+              f"occs {int(np.median(fv[:, 2]))}")
 eng.close()
