@@ -376,6 +376,7 @@ class RmsdBPE:
 
     _py_keys = False  # True: the pair keys in Python (_pair_key_py) instead of csrc/rmsdkey.c
     _no_key_memo = False  # True: rmsdkey.c merge derives every pair key (no memo; A/B and tests)
+    _group = None  # _RmsdGroup with a process group (also what a checkpoint-loaded instance has)
 
     def __init__(self, structures, bins, bin_strategy="histogram", save_dir="./plots/bpe",
                  compute_sec_structs=False, plot_iou_with_sec_structs=False, res_init=False, std_bonds=True,
