@@ -34,9 +34,6 @@ constexpr int BIN_VEC = 4;        // residue slots per int4 group
 #ifndef BIN_GPT_DEF
 #define BIN_GPT_DEF (FUSE_PACK ? 3 : 4)  // (4 with the fused record writes spills 12 VGPRs)
 #endif
-#ifndef BIN_FP
-#define BIN_FP 0  // the 16-bit pair fingerprints (fp): written, never read since round 2's token records
-#endif
 #ifndef BIN_EXP
 #define BIN_EXP 0
 #endif
@@ -70,6 +67,7 @@ struct BinWork {
   int32_t* partial;       // [nbc][BIN_NC] per-workgroup cube counts
   int2* ool;              // [nbc][ool_cap] (slot, triple) of out-of-cube pairs
   int32_t* ooln;          // [nbc]
+  int32_t enc_ool;        // BIN_OOLPACK: listed pairs' pk = -2 - triple (k_pack reads the key from dcnt)
   int2* found;            // [nbc][AggOol::N] (key id, triple) of keys a list found (sparse form)
   int32_t* foundn;        // [nbc]
   int64_t ool_cap;        // entries per list region
@@ -328,7 +326,7 @@ __device__ inline void bin_set_pk(const Dev& D, int64_t g, int32_t k) {
     D.tok[g].w = k;
   } else {
     D.pk[g] = k;
-    D.fp[g] = bin_fp(k);
+    if (BIN_FP) D.fp[g] = bin_fp(k);
   }
 }
 
@@ -419,10 +417,12 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
 #pragma unroll
       for (int u = 0; u < BIN_VEC; u++) {
         if (BIN_EXP & 2) continue;
-        if (k[q][u] >= 0)
+        if (k[q][u] >= 0) {
           atomicAdd(&s_cnt[c[q][u]], 1);
-        else if (ss[q][u] >= 0)
+        } else if (ss[q][u] >= 0) {
           bin_list(W, &s_nool, ool, ts[q][u], ss[q][u], ts[q][u + 1], v * BIN_VEC + u);
+          if (W.enc_ool) k[q][u] = -2 - bin_triple(ts[q][u], ss[q][u], ts[q][u + 1], G, K0);
+        }
       }
       if (FUSE_PACK) {
         // the junction symbol before the group: the previous lane's group (DPP wave_shr:1), the
@@ -455,17 +455,19 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
         const int32_t la = D.lab0[g], lb = D.lab0[g + 1];
         const int32_t cc = bin_cell(cl, cg, CL, CG, la, sy, lb);
         k = cc >= 0 ? s_map[cc] : -1;
-        if (k >= 0)
+        if (k >= 0) {
           atomicAdd(&s_cnt[cc], 1);
-        else
+        } else {
           bin_list(W, &s_nool, ool, la, sy, lb, g);
+          if (W.enc_ool) k = -2 - bin_triple(la, sy, lb, G, K0);
+        }
       }
       if (FUSE_PACK) {
         D.tok[g] = bin_tok(D, g, D.lab0[g], sy, g > 0 ? D.gsym[g - 1] : -1, k);
         if (D.gs16) D.gs16[g] = (uint16_t)(sy < 0 ? 0xFFFFu : (uint32_t)sy);
       } else {
         D.pk[g] = k;
-        D.fp[g] = bin_fp(k);
+        if (BIN_FP) D.fp[g] = bin_fp(k);
       }
     }
   }

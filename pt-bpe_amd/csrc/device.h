@@ -47,6 +47,12 @@ constexpr int NBA_MAX = 256;
 #ifndef PLACE_PRE
 #define PLACE_PRE 1  // k_place: the first round's records loaded before the token rewrites
 #endif
+#ifndef BIN_FP
+#define BIN_FP 0  // the 16-bit pair fingerprints (fp): written, never read since round 2's token records
+#endif  // (device.h: k_init_tokens and the import write them too)
+#ifndef BIN_OOLPACK
+#define BIN_OOLPACK 0  // k_pack reads the out-of-cube pairs' keys (no k_bin_ool_fix); 0: the fix-up kernel
+#endif
 #ifndef FIND_NT
 #define FIND_NT 0  // k_find: non-temporal stores of its outputs (A/B)
 #endif

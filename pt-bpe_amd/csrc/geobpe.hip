@@ -377,9 +377,9 @@ int alloc_keys(geobpe_ctx* c) {
 }
 
 // after the bin pass: pair keys into the token records, 16-bit junction symbols
-void enqueue_pack(geobpe_ctx* c) {
+void enqueue_pack(geobpe_ctx* c, const int32_t* dcnt = nullptr) {
   Timed t(c, "bin_pack");
-  hipLaunchKernelGGL(k_pack, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  hipLaunchKernelGGL(k_pack, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, dcnt);
 }
 
 // the launches of one merge iteration (no host synchronisation)
@@ -770,7 +770,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   if ((rc = dalloc(c, &c->d_row_off, n_rows + 1)) || (rc = dalloc(c, &D.rsym, Rp, 0)) ||
       (rc = dalloc(c, &D.gsym, Rp, 0)) || (rc = dalloc(c, &D.tok, Rp, 0xFF)) || (rc = dalloc(c, &D.lab0, Rp, 0xFF)) ||
       (rc = dalloc(c, &D.pk, Rp, 0xFF)) ||
-      (rc = dalloc(c, &D.fp, Rp + 16, 0xFF)))
+      (BIN_FP && (rc = dalloc(c, &D.fp, Rp + 16, 0xFF))))  // (fp: only the BIN_FP=1 build writes it)
     return rc;
   D.row_off = c->d_row_off;
   HIPCHK(c, hipMemcpyAsync(c->d_row_off, h_row_off, (n_rows + 1) * 8, hipMemcpyHostToDevice, c->stream));
@@ -1048,6 +1048,9 @@ int geobpe_bin(geobpe_ctx* c) {
     HIPCHK(c, hipMemsetAsync(W.flag, 0, (size_t)BIN_NC * 4, c->stream));
     const int64_t DS = K0 * G * K0;
     const bool dense_lists = DS <= (1LL << 26);
+    // (BIN_OOLPACK: with the dense lists and a separate k_pack, the listed pairs' keys are read by
+    // k_pack from the triple counts' cells, and k_bin_ool_fix does not run)
+    W.enc_ool = BIN_OOLPACK && dense_lists && !FUSE_PACK ? 1 : 0;
     if (dense_lists) {
       W.DS = DS;
       W.newcap = std::min<int64_t>(DS, c->R + 1);
@@ -1080,13 +1083,13 @@ int geobpe_bin(geobpe_ctx* c) {
         hipLaunchKernelGGL(k_bin_ool_stage, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
         hipLaunchKernelGGL(k_bin_ool_claim, dim3(4 * c->ncu), dim3(BLOCK), 0, c->stream, c->D, W,
                            c->distributed ? 1 : 0);
-        hipLaunchKernelGGL(k_bin_ool_fix, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+        if (!W.enc_ool) hipLaunchKernelGGL(k_bin_ool_fix, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
       } else {
         hipLaunchKernelGGL(k_bin_ool, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W, c->distributed ? 1 : 0);
         hipLaunchKernelGGL(k_bin_verify, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
       }
     }
-    if (!FUSE_PACK) enqueue_pack(c);  // (fused: k_bin_count wrote the token records)
+    if (!FUSE_PACK) enqueue_pack(c, W.enc_ool ? W.dcnt : nullptr);  // (fused: k_bin_count wrote the records)
     HIPCHK(c, hipGetLastError());
     rc = sync_state(c);
     if (!rc) {

@@ -136,14 +136,56 @@ __global__ __launch_bounds__(BLOCK) void k_first(Dev D, int64_t row_base, u64* f
 // consecutive records), and the 16-bit junction symbols.  Round 4's k_pack stored pk and the
 // length word into the records' 2nd and 4th words, 4-B stores at a 16-B lane stride, ~285 us
 // at C3.  (Every token is one residue here; g starts its chain iff gsym[g - 1] < 0.)
-__global__ __launch_bounds__(BLOCK) void k_pack(Dev D) {
+// dcnt (BIN_OOLPACK, the dense bin lists): a pair k_bin_count listed has pk = -2 - its triple, whose
+// key id k_bin_ool_claim left in dcnt -- read here instead of a fix-up kernel rewriting pk first
+// PACK_VEC = 1: four consecutive residues per thread (16-B loads of labels, junction symbols and
+// pair keys, four 16-B record stores and one 8-B symbol store: a quarter of the memory
+// instructions)
+#ifndef PACK_VEC
+#define PACK_VEC 0
+#endif
+__device__ inline int4 pack_rec(const Dev& D, int64_t g, int32_t lab, int32_t gs, int32_t gp, int32_t k0,
+                                const int32_t* dcnt) {
+  const int32_t k = dcnt && k0 <= -2 ? dcnt[-2 - k0] : k0;
+  const uint32_t g16 = gs < 0 ? 0xFFFFu : (uint32_t)gs;
+  return make_int4(lab, D.gs16 ? (int32_t)(1u | (g16 << 16)) : 1, gp >= 0 ? (int32_t)(g - 1) : -1, k);
+}
+__global__ __launch_bounds__(BLOCK) void k_pack(Dev D, const int32_t* dcnt) {
+#if PACK_VEC
+  const int64_t nv = D.R / 4;
+  const int4* lv = reinterpret_cast<const int4*>(D.lab0);
+  const int4* sv = reinterpret_cast<const int4*>(D.gsym);
+  const int4* kv = reinterpret_cast<const int4*>(D.pk);
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
+    const int4 lab = lv[v], gs = sv[v], k = kv[v];
+    const int64_t g = 4 * v;
+    const int32_t gp = g > 0 ? D.gsym[g - 1] : -1;  // (the previous lane's line: a cache hit)
+    int4* t = D.tok + g;
+    t[0] = pack_rec(D, g, lab.x, gs.x, gp, k.x, dcnt);
+    t[1] = pack_rec(D, g + 1, lab.y, gs.y, gs.x, k.y, dcnt);
+    t[2] = pack_rec(D, g + 2, lab.z, gs.z, gs.y, k.z, dcnt);
+    t[3] = pack_rec(D, g + 3, lab.w, gs.w, gs.z, k.w, dcnt);
+    if (D.gs16) {
+      auto h16 = [](int32_t x) { return (uint16_t)(x < 0 ? 0xFFFFu : (uint32_t)x); };
+      reinterpret_cast<ushort4*>(D.gs16)[v] = make_ushort4(h16(gs.x), h16(gs.y), h16(gs.z), h16(gs.w));
+    }
+  }
+  for (int64_t g = 4 * nv + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R;
+       g += (int64_t)gridDim.x * blockDim.x) {  // (the < 4 residues past the last full group)
+    const int32_t gs = D.gsym[g];
+    D.tok[g] = pack_rec(D, g, D.lab0[g], gs, g > 0 ? D.gsym[g - 1] : -1, D.pk[g], dcnt);
+    if (D.gs16) D.gs16[g] = (uint16_t)(gs < 0 ? 0xFFFFu : (uint32_t)gs);
+  }
+#else
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t lab = D.lab0[g], gs = D.gsym[g], k = D.pk[g];
+    const int32_t lab = D.lab0[g], gs = D.gsym[g], k0 = D.pk[g];
+    const int32_t k = dcnt && k0 <= -2 ? dcnt[-2 - k0] : k0;
     const int32_t gp = g > 0 ? D.gsym[g - 1] : -1;  // (the previous lane's line: a cache hit)
     const uint32_t g16 = gs < 0 ? 0xFFFFu : (uint32_t)gs;
     D.tok[g] = make_int4(lab, D.gs16 ? (int32_t)(1u | (g16 << 16)) : 1, gp >= 0 ? (int32_t)(g - 1) : -1, k);
     if (D.gs16) D.gs16[g] = (uint16_t)g16;
   }
+#endif
 }
 
 __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_of_sym) {
@@ -155,7 +197,7 @@ __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_
       D.tok[g] = make_int4(lab, 1, (g == a) ? -1 : (int32_t)(g - 1), 0);
       D.lab0[g] = lab;
       D.pk[g] = -1;
-      D.fp[g] = 0xFFFF;
+      if (BIN_FP) D.fp[g] = 0xFFFF;
     }
   }
 }
@@ -283,7 +325,7 @@ __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, cons
   }
   if (e.target >= 0) {
     D.pk[e.target] = d;
-    D.fp[e.target] = key_fp(d);
+    if (BIN_FP) D.fp[e.target] = key_fp(d);
   }
   agg_add_hot(agg, D, hot, d, e.delta, to_delta, th);
 }

@@ -26,6 +26,9 @@ def rows(d):
         for n, v in (j.get("roofline_other") or {}).items():
             if (v or {}).get("avg_launch_us") is not None:
                 k.setdefault(n, v["avg_launch_us"])
+        pp = (j.get("pair_count_pass") or {}).get("pass_and_pack") or {}
+        if pp.get("time_us") is not None:  # (the bin pass + k_pack, once per run, outside the timed merges)
+            k["pass+pack"] = pp["time_us"]
         out.append((f[:-4], j["value"], k))
     return out
 
