@@ -452,6 +452,14 @@ __device__ inline void dbg_val(const Dev& D, int k, int64_t v) {
   if (D.dbg && threadIdx.x == 0 && k < DBG_SLOTS) D.dbg[(int64_t)blockIdx.x * DBG_SLOTS + k] = v;
 }
 
+// key d's stored content equals (h1, h2, len): the three loads issued together and compared
+// without short-circuit (`a != x || b != y || ...` loaded them one after another, a round trip each)
+__device__ inline bool key_is(const Dev& D, int32_t d, u64 h1, u64 h2, int32_t len) {
+  const u64 a = D.kh1[d], b = D.kh2[d];
+  const int32_t c = D.klen[d];
+  return (a == h1) & (b == h2) & (c == len);
+}
+
 __device__ inline uint32_t post_bkt(int32_t d) { return ((uint32_t)d * 2654435761u) >> (32 - NBKT_LOG2); }
 
 // token record fields (int4 tok[s] = {tid, tlen, tprev, pk})

@@ -319,7 +319,7 @@ __global__ __launch_bounds__(ABLOCK) void k_pairs_all(Dev D) {
 __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, const NewPair& e, int64_t j, bool to_delta,
                                     int32_t th) {
   const int32_t d = e.slot;
-  if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) {
+  if (!key_is(D, d, e.h1, e.h2, e.len)) {
     set_error(D, GEOBPE_EHASH, j);
     return;
   }

@@ -79,6 +79,36 @@ __device__ inline void out_store(V* p, const V& v) {
 #endif
 }
 
+// a load the compiler issues where it stands: a relaxed workgroup-scope atomic load (a plain
+// global_load in the ISA), which it does not sink into the branch that uses the value -- a plain
+// load only one path uses was moved there and waited for at once
+__device__ inline int2 ld_now(const int2* p) {
+  const unsigned long long v = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+  return make_int2((int32_t)(v & 0xFFFFFFFFu), (int32_t)(v >> 32));
+}
+__device__ inline int32_t ld_now(const int32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ inline KRec ld_rec(const KRec* p) {  // (six 8-B loads)
+  KRec r;
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+  unsigned long long* o = reinterpret_cast<unsigned long long*>(&r);
+#pragma unroll
+  for (int i = 0; i < 6; i++) o[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return r;
+}
+
+// COMMIT_EARLY = 1: k_commit's first round of record loads issued without waits (as PLACE_EARLY)
+#ifndef COMMIT_EARLY
+#define COMMIT_EARLY 1
+#endif
+// PLACE_EARLY = 1: k_place's second round issued without waits (the T entries' records before the
+// scan, unconditional loads, the token stores not behind a conditional load); 0: round 4's order
+#ifndef PLACE_EARLY
+#define PLACE_EARLY 1
+#endif
+
 // the record counts finder r sent owner o (cntK / cntD).  CNT_T = 1 keeps them finder-major,
 // so a finder's end writes whole lines (owner-major, its 2 x NBA counts were NBA-strided 4-B
 // writes: 2 x 65 536 partial lines a launch written back at k_find's end)
@@ -189,7 +219,7 @@ __device__ inline void check_found(const Dev& D, int32_t r) {
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
     const NewPair e = reg[i];
     const int32_t d = e.target;
-    if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) set_error(D, GEOBPE_EHASH, i);
+    if (!key_is(D, d, e.h1, e.h2, e.len)) set_error(D, GEOBPE_EHASH, i);
   }
 }
 
@@ -199,7 +229,7 @@ __device__ inline void check_found_tail(const Dev& D, int32_t r, int32_t n, cons
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
     const NewPair e = i < (int32_t)blockDim.x ? e0 : reg[i];
     const int32_t d = e.target;
-    if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) set_error(D, GEOBPE_EHASH, i);
+    if (!key_is(D, d, e.h1, e.h2, e.len)) set_error(D, GEOBPE_EHASH, i);
   }
 }
 
@@ -1178,8 +1208,19 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   // prefix scans above measured ~1 % slower on the window, profiles/r5_s5/)
   KRec r0;
   int2 d0 = make_int2(0, 0);
+#if COMMIT_EARLY
+  // (unconditional loads from clamped slots, all of this round's loads issued before any wait: a
+  // load inside `if` made the compiler wait for it at the join, r0 / d0 / e0 / x0 one after another)
+  {
+    const bool hk = lane_ok && k0 < min(cK, SK), hd = lane_ok && k0 < min(cD, SD);
+    r0 = ld_rec(&D.KS[seg * SK + (hk ? k0 : 0)]);
+    const int2 d0r = ld_now(&D.DS[seg * SD + (hd ? k0 : 0)]);
+    d0 = hd ? d0r : make_int2(0, 0);
+  }
+#else
   if (lane_ok && k0 < min(cK, SK)) r0 = D.KS[seg * SK + k0];
   if (lane_ok && k0 < min(cD, SD)) d0 = D.DS[seg * SD + k0];
+#endif
 #endif
   // ---- round 1: key records -> LDS dedupe (occurrence totals per key); decrements -> LDS
 #define COMMIT_INSERT(k)                                          \
@@ -1207,15 +1248,29 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   KRec e0;
   int64_t at0 = 0;
   const bool he = t < nE + nKO;
+  int2 x0 = make_int2(-1, 0);
+#if COMMIT_EARLY
+  {
+    if (he) at0 = extra_at(D, s_preE, nba, j, PER, nE, t);
+    int64_t xa = 0;
+    if (t < nF) {
+      const int32_t ww = seg_of(s_preF, nba, t);
+      xa = ((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww]);
+    }
+    e0 = ld_rec(&D.KS[at0]);
+    const int2 x0r = ld_now(&D.DS[xa]);
+    x0 = t < nF ? x0r : make_int2(-1, 0);
+  }
+#else
   if (he) {
     at0 = extra_at(D, s_preE, nba, j, PER, nE, t);
     e0 = D.KS[at0];
   }
-  int2 x0 = make_int2(-1, 0);
   if (t < nF) {
     const int32_t ww = seg_of(s_preF, nba, t);
     x0 = D.DS[((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww])];
   }
+#endif
 #if CAGG
   {  // a hot key reaches its owner once per finder -- up to 64 times in a wave's r0, each one an
      // atomic on the same LDS counter: the lanes holding the wave's first pending key add their
@@ -1477,6 +1532,7 @@ __device__ inline int32_t place_rec_at(const Dev& D, const PlaceLds& S, int32_t 
   return (int32_t)((int64_t)D.NBA * D.NBA * SK + k_lo + (i - nk));
 }
 
+
 // k_place's token rewrites, pk and posting-log entries (read by the next k_find on every XCD):
 // PLACE_WT=1 stores them write-through (A/B)
 #ifndef PLACE_WT
@@ -1489,6 +1545,17 @@ __device__ inline void pl_store(V* p, const V& v) {
 #else
   *p = v;
 #endif
+}
+
+// the token rewrites of one merged occurrence (a, b) with right neighbour c: a becomes the new
+// token, b's record is cleared, c's previous slot is a (or a ends its chain)
+__device__ inline void place_tokens(const Dev& D, const LEntry& e, int32_t nid) {
+  pl_store(reinterpret_cast<int2*>(D.tok + e.a), make_int2(nid, e.ya));
+  pl_store(D.tok + e.b, make_int4(-1, 0, -1, -1));  // (no other occurrence writes b's record)
+  if (e.c >= 0)
+    pl_store(tok_f(D, e.c, 2), e.a);
+  else
+    pl_store(tok_f(D, e.a, 3), (int32_t)-1);
 }
 
 // a single record (one occurrence, its slot in tstart as -(slot + 1)) of finder region j: pk
@@ -1532,6 +1599,19 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   const int2 te0 = Tj[min(t, (int32_t)D.TC - 1)], te1 = Tj[min(t + ABLOCK, (int32_t)D.TC - 1)];
   if (par < 0) return;  // (k_commit sets par only for a merge)
   dbg_stamp(D, 30);
+  // ---- round 2, part 1: every T entry's record (key id, log position, tstart) -- they need only
+  // round 1's T entries, so they go out before the scan below (issued after it, behind the
+  // records' loads, the compiler waited for each group in turn: three round trips, ~4.5 us)
+  // (unconditional loads from a clamped index: a load inside `if` into a register the other path
+  // sets made the compiler wait for it at the join, one group after the other)
+  const bool h0 = t < nT && te0.y >= 0, h1 = t + ABLOCK < nT && te1.y >= 0;
+#if PLACE_EARLY
+  const int32_t a0 = h0 ? te0.y : 0, a1 = h1 ? te1.y : 0;
+  const int2 v0r = ld_now(&D.KSid[a0]), v1r = ld_now(&D.KSid[a1]);
+  const int32_t ts0r = ld_now(&D.KS[a0].tstart), ts1r = ld_now(&D.KS[a1].tstart);
+  const int2 v0 = h0 ? v0r : make_int2(-1, -1), v1 = h1 ? v1r : make_int2(-1, -1);
+  const int32_t ts0 = h0 ? ts0r : 0, ts1 = h1 ? ts1r : 0;
+#endif
   const int64_t oper = (novf + D.NBA - 1) / D.NBA;
   const int64_t o_lo = (int64_t)j * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
   const int64_t kper = (nko + D.NBA - 1) / D.NBA;
@@ -1543,9 +1623,24 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
     if (threadIdx.x == 0) S.pre[D.NBA] = tot;
   }
   __syncthreads();  // S.pre
+  dbg_stamp(D, 38);
   const int32_t nk = S.pre[D.NBA];
   const int32_t nrec = nk + (int32_t)k_n;
-  // ---- round 2, all issued before any result is used
+  // ---- round 2, part 2: the records of this finder's slots (their ranges need the scan)
+#if PLACE_EARLY
+  const bool hr = t < nrec;
+  const int32_t ra = hr ? place_rec_at(D, S, j, t, nk, k_lo) : 0;
+  const int2 rnt_r = ld_now(reinterpret_cast<const int2*>(&D.KS[ra].n)), rv_r = ld_now(&D.KSid[ra]);
+  const int2 rnt = hr ? rnt_r : make_int2(0, 0), rv = hr ? rv_r : make_int2(-1, -1);
+  dbg_stamp(D, 37);
+  // ---- the token rewrites of find region j (round 1's data).  The thread's first entry comes from
+  // registers with no load on its path (a conditional load there made the compiler wait for every
+  // outstanding load, round 2's included, before the first store); the rest -- more entries than
+  // threads, the overflow list -- are rare
+  if (t < nA) place_tokens(D, eA, nid);
+  for (int64_t i = t + ABLOCK; i < nA; i += ABLOCK) place_tokens(D, D.L[(int64_t)j * D.LC + i], nid);
+  for (int64_t i = t; i < o_n; i += ABLOCK) place_tokens(D, D.Lovf[o_lo + i], nid);
+#else
   int32_t ra = -1;
   int2 rnt = make_int2(0, 0), rv = make_int2(-1, -1);
   if (t < nrec) {
@@ -1553,7 +1648,6 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
     rnt = *reinterpret_cast<const int2*>(&D.KS[ra].n);
     rv = D.KSid[ra];
   }
-  const bool h0 = t < nT && te0.y >= 0, h1 = t + ABLOCK < nT && te1.y >= 0;
   int2 v0 = make_int2(-1, -1), v1 = make_int2(-1, -1);
   int32_t ts0 = 0, ts1 = 0;
   if (h0) {
@@ -1564,16 +1658,10 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
     v1 = D.KSid[te1.y];
     ts1 = D.KS[te1.y].tstart;
   }
-  // ---- the token rewrites of find region j (round 1's data)
-  for (int64_t i = t; i < nA + o_n; i += ABLOCK) {
-    const LEntry e = i < nA ? (i == t ? eA : D.L[(int64_t)j * D.LC + i]) : D.Lovf[o_lo + (i - nA)];
-    pl_store(reinterpret_cast<int2*>(D.tok + e.a), make_int2(nid, e.ya));
-    pl_store(D.tok + e.b, make_int4(-1, 0, -1, -1));  // (no other occurrence writes b's record)
-    if (e.c >= 0)
-      pl_store(tok_f(D, e.c, 2), e.a);
-    else
-      pl_store(tok_f(D, e.a, 3), (int32_t)-1);
-  }
+  dbg_stamp(D, 37);
+  for (int64_t i = t; i < nA + o_n; i += ABLOCK)
+    place_tokens(D, i < nA ? (i == t ? eA : D.L[(int64_t)j * D.LC + i]) : D.Lovf[o_lo + (i - nA)], nid);
+#endif
   dbg_stamp(D, 31);
   // ---- pk of every new pair and its posting-log entry
   const int64_t qbase = (int64_t)j * D.TC;

@@ -1038,7 +1038,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
   for (int32_t i = t + ABLOCK; i < nchk; i += ABLOCK) {
     const NewPair x = reg[i];
     const int32_t d = x.target;
-    if (D.kh1[d] != x.h1 || D.kh2[d] != x.h2 || D.klen[d] != x.len) set_error(D, GEOBPE_EHASH, i);
+    if (!key_is(D, d, x.h1, x.h2, x.len)) set_error(D, GEOBPE_EHASH, i);
   }
   if (chk) {
     __syncthreads();  // (every thread has read the count)

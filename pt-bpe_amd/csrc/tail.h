@@ -352,7 +352,7 @@ __global__ __launch_bounds__(SBLOCK) void k_tail(Dev D, int par, int64_t n_max) 
     for (int32_t i = t; i < nC; i += SBLOCK) {
       const NewPair e = D.TK[i];
       const int32_t d = e.target;
-      if (D.kh1[d] != e.h1 || D.kh2[d] != e.h2 || D.klen[d] != e.len) set_error(D, GEOBPE_EHASH, i);
+      if (!key_is(D, d, e.h1, e.h2, e.len)) set_error(D, GEOBPE_EHASH, i);
     }
     if (D.ev) {  // merge events (record mode): (merge, left start, right start)
       __shared__ int64_t s_ev;

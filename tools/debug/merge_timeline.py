@@ -22,7 +22,7 @@ eng.bin()
 L = _native.lib()
 names = {0: "C.start", 1: "C.init", 2: "C.records", 3: "C.resolved", 4: "C.published", 5: "C.flush+klist", 6: "C.end",
          10: "F.start", 11: "F.setup", 14: "F.r0.queued", 15: "F.r0.walked", 16: "F.r0.grouped", 12: "F.walked",
-         13: "F.end", 40: "F.w.T1", 41: "F.w.T2", 42: "F.w.T3", 43: "F.w.emitted", 44: "F.w.hashed", 30: "P.start", 31: "P.tokens", 32: "P.slots", 33: "P.end",
+         13: "F.end", 40: "F.w.T1", 41: "F.w.T2", 42: "F.w.T3", 43: "F.w.emitted", 44: "F.w.hashed", 30: "P.start", 38: "P.scanned", 37: "P.issued", 31: "P.tokens", 32: "P.slots", 33: "P.end",
          50: "C.i.loaded", 51: "C.i.zeroed", 53: "C.published0", 56: "C.r.first", 57: "C.r.extras", 58: "C.r.decs", 20: "S.start", 21: "S.scanned", 22: "S.max", 23: "S.ties", 24: "S.staged", 25: "S.tourn", 26: "S.end"}
 done = 0
 for it in iters:
