@@ -25,6 +25,9 @@
 #pragma once
 // (included inside namespace gb)
 
+#ifndef MID_DEFER
+#define MID_DEFER 0  // k_mid_find: a resolved key's count add returns under the pair writes (its
+#endif               // hot-list check after them), not before the round's barrier
 #ifndef MID_SPEC
 #define MID_SPEC 0
 #endif
@@ -617,6 +620,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     if (c0 == 0) dbg_stamp(D, 16);
     const int32_t nocc = S.nocc;
     const int64_t xb = D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
+    int32_t def_d = -1, def_old = 0, def_v = 0;  // (MID_DEFER: this thread's first count add)
     for (int32_t q = t; q < nocc; q += ABLOCK) {
       const int32_t s = S.occ[q];
       const int4 rp = S.rep[s];
@@ -635,10 +639,18 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       } else {
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
-      if (D.xrec)
+      if (D.xrec) {
         mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
-      else if (!MID_SPEC)
-        count_add_hot(D, S.hot, d, S.cnt[s], F.th);
+      } else if (!MID_SPEC) {
+        const int32_t v = S.cnt[s];
+        if (MID_DEFER && q == t && v > 0 && F.th > 0) {  // the hot-list check waits for it later
+          def_old = atomicAdd(&D.count[d], v);
+          def_d = d;
+          def_v = v;
+        } else {
+          count_add_hot(D, S.hot, d, v, F.th);
+        }
+      }
     }
     // the last round's walks are done, so every decrement is staged: out now, one atomic per
     // key, in flight under the new pairs' grouping and the list flush (at the launch's end they
@@ -659,6 +671,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       if (S.h1[sr] != hr.h1) set_error(D, GEOBPE_EHASH, -13);
       if (S.did[sr] >= 0) mid_pair(D, S, F, hr.target, S.did[sr]);
     }
+    if (def_d >= 0 && def_old < F.th && def_old + def_v >= F.th) hot_push(D, S.hot, def_d);
     __syncthreads();
     for (int32_t q = t; q < nocc; q += ABLOCK) {  // clear the round's slots
       const int32_t s = S.occ[q];
