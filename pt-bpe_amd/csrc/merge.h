@@ -90,6 +90,18 @@ __device__ inline int2 ld_now(const int2* p) {
 __device__ inline int32_t ld_now(const int32_t* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
+template <typename T>
+__device__ inline T ld_now_t(const T* p) {  // (any 8-B multiple, 8 B at a time)
+  static_assert(sizeof(T) % 8 == 0, "8-B multiple");
+  T r;
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);
+  unsigned long long* o = reinterpret_cast<unsigned long long*>(&r);
+#pragma unroll
+  for (int i = 0; i < (int)(sizeof(T) / 8); i++)
+    o[i] = __hip_atomic_load(q + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return r;
+}
+__device__ inline u64 ld_now(const u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
 __device__ inline KRec ld_rec(const KRec* p) {  // (six 8-B loads)
   KRec r;
   const unsigned long long* q = reinterpret_cast<const unsigned long long*>(p);

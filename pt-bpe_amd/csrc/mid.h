@@ -28,6 +28,9 @@
 #ifndef MID_DEFER
 #define MID_DEFER 0  // k_mid_find: a resolved key's count add returns under the pair writes (its
 #endif               // hot-list check after them), not before the round's barrier
+#ifndef MID_PLACE_EARLY
+#define MID_PLACE_EARLY 0  // k_mid_sel's place: 1 = check loads unconditional, 2 = every round (both slower)
+#endif
 #ifndef MID_SPEC
 #define MID_SPEC 0
 #endif
@@ -988,12 +991,64 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
   // new pair.  (Round 3's version ran the EHASH check's three dependent rounds, a barrier and
   // then the place's own three: this launch's place workgroups set its length.)
   const bool chk = b < D.NBA;  // (then consumed: the next find writes region b afresh)
+#if MID_PLACE_EARLY
+  // (every load of a round unconditional, from clamped indices, as relaxed workgroup-scope atomic
+  // loads the compiler neither sinks into the branch using them nor waits for at a join: round 1
+  // is the check count, the parity and, speculatively, this thread's check record; round 2 the
+  // Sel record, the segment counts and the check key's hashes; round 3 the merged occurrence and
+  // new pair -- written as `if (x) v = load`, the rounds went out as about six round trips)
+  // (atomic loads keep their source order, so each group is written before any value is used)
+  // (the record first: a use of a value loaded before it was scheduled between the loads)
+  const NewPair* reg = D.chk + (int64_t)b * D.RC;
+  const NewPair c0 = ld_now_t(&reg[t < D.RC ? t : 0]);
+  const int32_t nchk_raw = ld_now(&D.chkcnt[b < D.NBA ? b : 0]);
+#if MID_PLACE_EARLY >= 2
+  const int32_t par = ld_now(&st->place_par);
+#else
+  const int32_t par = st->place_par;
+#endif
+  // round 2 (the check count and the record both came in round 1; threads past the count load
+  // slot 0 rather than a stale record's slot; the parity clamped to 0 when no merge is placed)
+  const int32_t nchk = chk ? min(nchk_raw, (int32_t)D.RC) : 0;
+  const bool hc = t < nchk;
+  const int32_t ct = hc ? c0.target : 0;
+  const u64 kh1 = ld_now(&D.kh1[ct]), kh2 = ld_now(&D.kh2[ct]);
+  const int32_t kln = ld_now(&D.klen[ct]);
+#endif
+#if MID_PLACE_EARLY >= 2
+  const int32_t pc = par >= 0 ? par : 0;
+  const int32_t G = mid_G(D);
+  const Sel* sp = D.sel + pc;
+  const int32_t s_dec = ld_now(&sp->decision), s_nid = ld_now(&sp->nid), s_iter = ld_now(&sp->iter);
+  const int4 mc_r = ld_now_t(&D.mcnt[pc * NBA_MAX + (b < G ? b : 0)]);
+  const int64_t nm_r = (int64_t)ld_now((const u64*)&st->mid_nm[pc]);
+  const int64_t nh_r = (int64_t)ld_now((const u64*)&st->mid_nh[pc]);
+  const int32_t v0_r = ld_now(&D.mcnt[pc * NBA_MAX + (t < G ? t : 0)].z);
+  Sel sel;
+  sel.decision = SEL_STALL;
+  sel.nid = 0;
+  sel.iter = 0;
+  int4 mc = make_int4(0, 0, 0, 0);
+  int64_t nms = 0, nhs = 0;
+  int32_t v0 = 0;  // (workgroup 0: the find workgroups' merged counts, summed below)
+  if (par >= 0) {
+    sel.decision = s_dec;
+    sel.nid = s_nid;
+    sel.iter = s_iter;
+    if (b < G) mc = mc_r;
+    nms = min(nm_r, D.TMcap - MSEG_TM);
+    nhs = min(nh_r, D.THcap - MSEG_TH);
+    if (b == 0 && t < G) v0 = v0_r;
+  }
+#else
+#if !MID_PLACE_EARLY
   const int32_t nchk = chk ? min(D.chkcnt[b], (int32_t)D.RC) : 0;
   const int32_t par = st->place_par;
   const NewPair* reg = D.chk + (int64_t)b * D.RC;
   NewPair c0;
   const bool hc = t < nchk;
   if (hc) c0 = reg[t];
+#endif
   const int32_t G = mid_G(D);
   Sel sel;
   sel.decision = SEL_STALL;
@@ -1007,6 +1062,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
     nhs = min(st->mid_nh[par], D.THcap - MSEG_TH);
     if (b == 0 && t < G) v0 = D.mcnt[par * NBA_MAX + t].z;
   }
+#endif
   const bool go = par >= 0 && sel.decision == SEL_MERGE;  // (block-uniform)
   // find workgroup b's segments (b < G), share b of the spill lists
   const int4* tms = D.TM + (int64_t)b * MTM;
@@ -1016,6 +1072,22 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
   const int32_t sm = min(mc.x, MTM), sh = min(mc.y, MTH);
   int4 e = make_int4(0, 0, 0, 0);
   int2 h = make_int2(0, 0);
+#if MID_PLACE_EARLY >= 2
+  if (go) {
+    m0 = nms * b / P;
+    nm = sm + (nms * (b + 1) / P - m0);
+    h0 = nhs * b / P;
+    nh = sh + (nhs * (b + 1) / P - h0);
+  }
+  {
+    const int4* ea = t < sm ? tms + t : D.TM + (MSEG_TM + m0 + t - sm);
+    const int2* ha = t < sh ? ths + t : th + (MSEG_TH + h0 + t - sh);
+    const int4 er = ld_now_t(t < nm ? ea : tms);
+    const int2 hr = ld_now(t < nh ? ha : ths);
+    if (t < nm) e = er;
+    if (t < nh) h = hr;
+  }
+#else
   if (go) {
     m0 = nms * b / P;
     nm = sm + (nms * (b + 1) / P - m0);
@@ -1024,6 +1096,8 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
     if (t < nm) e = t < sm ? tms[t] : D.TM[MSEG_TM + m0 + t - sm];
     if (t < nh) h = t < sh ? ths[t] : th[MSEG_TH + h0 + t - sh];
   }
+#endif
+#if !MID_PLACE_EARLY
   u64 kh1 = 0, kh2 = 0;
   int32_t kln = 0;
   if (hc) {
@@ -1031,6 +1105,7 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
     kh2 = D.kh2[c0.target];
     kln = D.klen[c0.target];
   }
+#endif
   const int32_t nid = sel.nid;
   auto place_tm = [&](const int4& x) {  // a merged occurrence's token rewrites
     *reinterpret_cast<int2*>(D.tok + x.x) = make_int2(nid, x.y);
