@@ -112,6 +112,9 @@ __device__ inline KRec ld_rec(const KRec* p) {  // (six 8-B loads)
 }
 
 // COMMIT_EARLY = 1: k_commit's first round of record loads issued without waits (as PLACE_EARLY)
+#ifndef COMMIT_X1
+#define COMMIT_X1 0  // k_commit: each thread's second extra records (t + ABLOCK) with its first (slower, r5_cx2)
+#endif
 #ifndef COMMIT_EARLY
 #define COMMIT_EARLY 1
 #endif
@@ -1261,6 +1264,15 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   int64_t at0 = 0;
   const bool he = t < nE + nKO;
   int2 x0 = make_int2(-1, 0);
+#if COMMIT_X1
+  // (and its second ones, t + ABLOCK: the owners holding the hottest keys have a few hundred
+  // extras, and their second records were one more dependent round trip; the publish loads them
+  // again -- kept in registers to then, the launch spilled 800 B a thread)
+  KRec e1;
+  int64_t at1 = 0;
+  const bool he1 = t + ABLOCK < nE + nKO;
+  int2 x1 = make_int2(-1, 0);
+#endif
 #if COMMIT_EARLY
   {
     if (he) at0 = extra_at(D, s_preE, nba, j, PER, nE, t);
@@ -1269,8 +1281,21 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       const int32_t ww = seg_of(s_preF, nba, t);
       xa = ((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww]);
     }
+#if COMMIT_X1
+    if (he1) at1 = extra_at(D, s_preE, nba, j, PER, nE, t + ABLOCK);
+    int64_t xa1 = 0;
+    if (t + ABLOCK < nF) {
+      const int32_t ww = seg_of(s_preF, nba, t + ABLOCK);
+      xa1 = ((int64_t)j * nba + ww) * SD + PER + (t + ABLOCK - s_preF[ww]);
+    }
+#endif
     e0 = ld_rec(&D.KS[at0]);
     const int2 x0r = ld_now(&D.DS[xa]);
+#if COMMIT_X1
+    e1 = ld_rec(&D.KS[at1]);
+    const int2 x1r = ld_now(&D.DS[xa1]);
+    x1 = t + ABLOCK < nF ? x1r : make_int2(-1, 0);
+#endif
     x0 = t < nF ? x0r : make_int2(-1, 0);
   }
 #else
@@ -1311,15 +1336,30 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
 #endif
   if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
   dbg_stamp(D, 56);
+#if COMMIT_X1 && COMMIT_EARLY
+#pragma unroll 1
+  for (int u = 0; u < 2; u++) {  // (one insert site: a second one inlined its fallback again and spilled)
+    const KRec k = u ? e1 : e0;
+    if (u ? he1 && (t + ABLOCK < nE || owner_of_key(D, e1.pkey) == j) : he && (t < nE || owner_of_key(D, e0.pkey) == j))
+      COMMIT_INSERT(k);
+  }
+  for (int32_t i = t + 2 * ABLOCK; i < nE + nKO; i += ABLOCK) {  // (rare: more than 2 ABLOCK extras)
+#else
   if (he && (t < nE || owner_of_key(D, e0.pkey) == j)) COMMIT_INSERT(e0);
   for (int32_t i = t + ABLOCK; i < nE + nKO; i += ABLOCK) {  // (rare: more than ABLOCK extras)
+#endif
     const KRec k = D.KS[extra_at(D, s_preE, nba, j, PER, nE, i)];
     if (i < nE || owner_of_key(D, k.pkey) == j) COMMIT_INSERT(k);
   }
   dbg_stamp(D, 57);
   dbg_val(D, 59, nF);
   if (t < nF && !agg_stage(S.u.agg, x0.x, x0.y)) commit_add(D, x0.x, x0.y, tod);
+#if COMMIT_X1 && COMMIT_EARLY
+  if (t + ABLOCK < nF && !agg_stage(S.u.agg, x1.x, x1.y)) commit_add(D, x1.x, x1.y, tod);
+  for (int32_t i = t + 2 * ABLOCK; i < nF; i += ABLOCK) {
+#else
   for (int32_t i = t + ABLOCK; i < nF; i += ABLOCK) {
+#endif
     const int32_t ww = seg_of(s_preF, nba, i);
     const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
     if (!agg_stage(S.u.agg, x.x, x.y)) commit_add(D, x.x, x.y, tod);
