@@ -144,6 +144,9 @@ __global__ __launch_bounds__(BLOCK) void k_first(Dev D, int64_t row_base, u64* f
 #ifndef PACK_VEC
 #define PACK_VEC 0
 #endif
+#ifndef PACK_UNR
+#define PACK_UNR 1  // (2, 4, 8 measured slower: profiles/r5_ab/r5_pu.txt)
+#endif
 __device__ inline int4 pack_rec(const Dev& D, int64_t g, int32_t lab, int32_t gs, int32_t gp, int32_t k0,
                                 const int32_t* dcnt) {
   const int32_t k = dcnt && k0 <= -2 ? dcnt[-2 - k0] : k0;
@@ -175,6 +178,30 @@ __global__ __launch_bounds__(BLOCK) void k_pack(Dev D, const int32_t* dcnt) {
     const int32_t gs = D.gsym[g];
     D.tok[g] = pack_rec(D, g, D.lab0[g], gs, g > 0 ? D.gsym[g - 1] : -1, D.pk[g], dcnt);
     if (D.gs16) D.gs16[g] = (uint16_t)(gs < 0 ? 0xFFFFu : (uint32_t)gs);
+  }
+#elif PACK_UNR > 1
+  // PACK_UNR residues per thread a grid stride apart (coalesced as above), every load of the
+  // group issued before any store: ~4x the bytes in flight of one residue per iteration, which
+  // left the kernel latency-bound at ~0.7 of HBM peak
+  const int64_t S = (int64_t)gridDim.x * blockDim.x, R = D.R;
+  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g0 < R; g0 += PACK_UNR * S) {
+    int32_t lab[PACK_UNR], gs[PACK_UNR], k0[PACK_UNR], gp[PACK_UNR];
+#pragma unroll
+    for (int u = 0; u < PACK_UNR; u++) {
+      const int64_t g = g0 + u * S;
+      const int64_t i = g < R ? g : 0;  // (clamped: unconditional loads)
+      lab[u] = D.lab0[i];
+      gs[u] = D.gsym[i];
+      k0[u] = D.pk[i];
+      gp[u] = D.gsym[i > 0 ? i - 1 : 0];  // (the previous lane's line: a cache hit)
+    }
+#pragma unroll
+    for (int u = 0; u < PACK_UNR; u++) {
+      const int64_t g = g0 + u * S;
+      if (g >= R) break;
+      D.tok[g] = pack_rec(D, g, lab[u], gs[u], g > 0 ? gp[u] : -1, k0[u], dcnt);
+      if (D.gs16) D.gs16[g] = (uint16_t)(gs[u] < 0 ? 0xFFFFu : (uint32_t)gs[u]);
+    }
   }
 #else
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
