@@ -96,3 +96,31 @@ def nerf(geo: dict) -> np.ndarray:
         out.append(place(out[-3], out[-2], out[-1], geo["C:1N:1CA"][i], geo["N:CA"][i + 1], geo["omega"][i]))
         out.append(place(out[-3], out[-2], out[-1], geo["tau"][i + 1], geo["CA:C"][i + 1], geo["phi"][i]))
     return np.array(out)
+
+
+def k_medoids_from_matrix(D: np.ndarray, k, max_iterations: int = 10, tol: float = 1e-4, *, rng=None):
+    """The host iterations of algo.k_medoids (foldingdiff/algo.py:191-213) on a given distance
+    matrix, in numpy: the comparator of the product's C step (csrc/rmsdkey.c kmed_step,
+    geobpe.rmsd.k_medoids_from_matrix).  The same Generator draws in the same order, the
+    per-row argmin (first minimum) and each cluster's float32 member sums."""
+    N = len(D)
+    k = min(N, k)
+    if rng is None:
+        rng = np.random.default_rng(None)
+    medoid_indices = rng.choice(np.arange(N), size=k, replace=False)
+    for iteration in range(max_iterations):
+        assignments = np.argmin(D[:, medoid_indices], axis=1)  # (all rows at once: the same values)
+        total_shift = 0.0
+        new_medoid_indices = []
+        for j in range(k):
+            members = np.where(assignments == j)[0]
+            if members.size == 0:
+                new_idx = rng.integers(N)
+            else:
+                new_idx = members[np.argmin(D[np.ix_(members, members)].sum(axis=1))]
+            total_shift += D[medoid_indices[j], new_idx]
+            new_medoid_indices.append(new_idx)
+        medoid_indices = new_medoid_indices
+        if total_shift < tol:
+            break
+    return medoid_indices

@@ -6,7 +6,7 @@
 // the triple space is a "cube" of CL x CG x CL cells over the most frequent
 // labels / junction symbols (<= 16384 cells: one LDS array), and the keys of
 // its sampled cells are claimed BEFORE the count pass, so that pass writes the
-// final pk / fp of an in-cube pair directly and counts it with a plain LDS add.
+// final pk of an in-cube pair directly and counts it with a plain LDS add.
 // At C3 (B=5) the cube holds ~94 % of all pairs; the rest go to a per-workgroup
 // list that a second, non-divergent kernel counts through an LDS hash table.
 //
@@ -15,36 +15,23 @@
 //                  sampled mass it covers; cube coordinate tables
 //   k_bin_flag     cube cells that occur in the sample
 //   k_bin_precube  each flagged cell claims its key (table slot = key id)
-//   k_bin_count    the pass over every pair: 8 B in (tid, gsym), 6 B out (pk,
-//                  fp) for in-cube pairs; per-workgroup cube counts (LDS) ->
+//   k_bin_count    the pass over every pair: 8 B in (tid, gsym), 4 B out (pk)
+//                  for in-cube pairs; per-workgroup cube counts (LDS) ->
 //                  one coalesced partial row per workgroup; the other pairs ->
 //                  this workgroup's (slot, triple) list
 //   k_bin_reduce   cube counts = sums of the partial rows
 //   k_bin_ool      per list: LDS-staged counts per triple, one find-or-claim of
-//                  each distinct triple's key, one count add, pk / fp
+//                  each distinct triple's key, one count add, pk
 //   k_bin_verify   every key a list found (not claimed) has this content
 // The pair at residue slot g exists iff gsym[g] >= 0 (k_quantize: -1 = chain end).
 #pragma once
 // (inside namespace gb: kernels.h includes this file)
 
 constexpr int BIN_VEC = 4;        // residue slots per int4 group
-#ifndef FUSE_PACK
-#define FUSE_PACK 0  // (A/B, profiles/r5_suite1: the fused count kernel 287 us against 133 + a 285 us k_pack)
-#endif
-#ifndef BIN_GPT_DEF
-#define BIN_GPT_DEF (FUSE_PACK ? 3 : 4)  // (4 with the fused record writes spills 12 VGPRs)
-#endif
-#ifndef BIN_EXP
-#define BIN_EXP 0
-#endif
-constexpr int BIN_GPT = BIN_GPT_DEF;  // groups per thread per step (loads in flight together)
-// FUSE_PACK = 1 (A/B): k_bin_count writes the merge loop's token records itself ({label, 1 |
-// 16-bit junction symbol << 16, previous slot, pair key}: one 64-B line per group of 4 residues,
-// lane-strided) and the 16-bit junction symbols, and the list kernels write the listed pairs'
-// keys into the records -- no pk array and no k_pack pass.  Measured: the count kernel 133 ->
-// 287 us (its stores touch 64 lines per instruction), pass + pack 585 -> 454 us, but the
-// pair-count kernel at 0.26 of HBM peak.  Default: the lean count kernel and a coalesced k_pack
-// (kernels.h) that writes whole records lane by lane
+constexpr int BIN_GPT = 4;        // groups per thread per step (loads in flight together)
+// (round 5 A/B: a count kernel that also wrote the merge loop's token records -- lane-strided
+// 64-B record groups, 64 lines per store instruction -- took 287 us against 133 + a coalesced
+// k_pack; the lean count kernel and k_pack stay)
 constexpr int BIN_NC = 1 << 14;   // max cube cells (64 KB of LDS counts)
 constexpr int BIN_SAMPLE = 16;    // the sample: the first 1/16 of each workgroup's range
 constexpr int BIN_MAXSYM = 2048;  // label / junction-symbol tables (K0, B^3 <= 2048)
@@ -67,7 +54,6 @@ struct BinWork {
   int32_t* partial;       // [nbc][BIN_NC] per-workgroup cube counts
   int2* ool;              // [nbc][ool_cap] (slot, triple) of out-of-cube pairs
   int32_t* ooln;          // [nbc]
-  int32_t enc_ool;        // BIN_OOLPACK: listed pairs' pk = -2 - triple (k_pack reads the key from dcnt)
   int2* found;            // [nbc][AggOol::N] (key id, triple) of keys a list found (sparse form)
   int32_t* foundn;        // [nbc]
   int64_t ool_cap;        // entries per list region
@@ -318,30 +304,14 @@ __global__ __launch_bounds__(BLOCK) void k_bin_precube(Dev D, BinWork W) {
   cb_flush(D, cb);
 }
 
-__device__ inline uint16_t bin_fp(int32_t k) { return k >= 0 ? key_fp(k) : (uint16_t)0xFFFF; }
-
-// a listed pair's key: into its token record (FUSE_PACK), else the streamed pk / fp for k_pack
-__device__ inline void bin_set_pk(const Dev& D, int64_t g, int32_t k) {
-  if (FUSE_PACK) {
-    D.tok[g].w = k;
-  } else {
-    D.pk[g] = k;
-    if (BIN_FP) D.fp[g] = bin_fp(k);
-  }
-}
+// a listed pair's key: the streamed pk that k_pack copies into the token record
+__device__ inline void bin_set_pk(const Dev& D, int64_t g, int32_t k) { D.pk[g] = k; }
 
 // a pair of k_bin_count outside the pre-claimed cube: this workgroup's list
 __device__ inline void bin_list(const BinWork& W, int32_t* s_nool, int2* ool, int32_t la, int32_t gs, int32_t lb,
                                 int64_t g) {
   const int32_t j = atomicAdd(s_nool, 1);
   if (j < W.ool_cap) ool[j] = make_int2((int32_t)g, bin_triple(la, gs, lb, W.G, W.K0));
-}
-
-// token record of residue g at the initial state (every token one residue): pair key k, junction
-// symbol gs (-1: chain end), junction symbol of g - 1 (-1: g starts its chain)
-__device__ inline int4 bin_tok(const Dev& D, int64_t g, int32_t lab, int32_t gs, int32_t gprev, int32_t k) {
-  const uint32_t g16 = gs < 0 ? 0xFFFFu : (uint32_t)gs;
-  return make_int4(lab, D.gs16 ? (int32_t)(1u | (g16 << 16)) : 1, gprev >= 0 ? (int32_t)(g - 1) : -1, k);
 }
 
 // the pass over every pair.  LDS: the cube's key ids and counts, the cube
@@ -369,7 +339,6 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
   const int4* tv = (const int4*)D.lab0;
   const int4* gv = (const int4*)D.gsym;
   int4* pv = (int4*)D.pk;
-  ushort4* fv = (ushort4*)D.fp;
   int2* ool = W.ool + (int64_t)blockIdx.x * W.ool_cap;
   for (int64_t v0 = lo; v0 < hi; v0 += BIN_GPT * ABLOCK) {
     int32_t ts[BIN_GPT][BIN_VEC + 1], ss[BIN_GPT][BIN_VEC];
@@ -410,41 +379,18 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
 #pragma unroll
     for (int q = 0; q < BIN_GPT; q++)
 #pragma unroll
-      for (int u = 0; u < BIN_VEC; u++) k[q][u] = (BIN_EXP & 2) ? ts[q][u] : c[q][u] >= 0 ? s_map[c[q][u]] : -1;
+      for (int u = 0; u < BIN_VEC; u++) k[q][u] = c[q][u] >= 0 ? s_map[c[q][u]] : -1;
 #pragma unroll
     for (int q = 0; q < BIN_GPT; q++) {
       const int64_t v = v0 + q * ABLOCK + threadIdx.x;
 #pragma unroll
       for (int u = 0; u < BIN_VEC; u++) {
-        if (BIN_EXP & 2) continue;
-        if (k[q][u] >= 0) {
+        if (k[q][u] >= 0)
           atomicAdd(&s_cnt[c[q][u]], 1);
-        } else if (ss[q][u] >= 0) {
+        else if (ss[q][u] >= 0)
           bin_list(W, &s_nool, ool, ts[q][u], ss[q][u], ts[q][u + 1], v * BIN_VEC + u);
-          if (W.enc_ool) k[q][u] = -2 - bin_triple(ts[q][u], ss[q][u], ts[q][u + 1], G, K0);
-        }
       }
-      if (FUSE_PACK) {
-        // the junction symbol before the group: the previous lane's group (DPP wave_shr:1), the
-        // wave's first lane loads it
-        int32_t gp = __builtin_amdgcn_update_dpp(-2, ss[q][BIN_VEC - 1], 0x138, 0xF, 0xF, false);
-        if (wave_lane() == 0 && v < hi) gp = v > 0 ? D.gsym[v * BIN_VEC - 1] : -1;
-        if (v < hi) {
-          const int64_t g = v * BIN_VEC;
-          int4* tk = D.tok + g;
-          tk[0] = bin_tok(D, g, ts[q][0], ss[q][0], gp, k[q][0]);
-          tk[1] = bin_tok(D, g + 1, ts[q][1], ss[q][1], ss[q][0], k[q][1]);
-          tk[2] = bin_tok(D, g + 2, ts[q][2], ss[q][2], ss[q][1], k[q][2]);
-          tk[3] = bin_tok(D, g + 3, ts[q][3], ss[q][3], ss[q][2], k[q][3]);
-          if (D.gs16) {
-            auto h16 = [](int32_t s) { return (uint16_t)(s < 0 ? 0xFFFFu : (uint32_t)s); };
-            reinterpret_cast<ushort4*>(D.gs16)[v] = make_ushort4(h16(ss[q][0]), h16(ss[q][1]), h16(ss[q][2]), h16(ss[q][3]));
-          }
-        }
-      } else if (v < hi) {
-        pv[v] = make_int4(k[q][0], k[q][1], k[q][2], k[q][3]);
-        if (BIN_FP && !(BIN_EXP & 1)) fv[v] = make_ushort4(bin_fp(k[q][0]), bin_fp(k[q][1]), bin_fp(k[q][2]), bin_fp(k[q][3]));
-      }
+      if (v < hi) pv[v] = make_int4(k[q][0], k[q][1], k[q][2], k[q][3]);
     }
   }
   if (blockIdx.x == gridDim.x - 1) {  // the < 4 slots past the last full group
@@ -455,20 +401,12 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_count(Dev D, BinWork W) {
         const int32_t la = D.lab0[g], lb = D.lab0[g + 1];
         const int32_t cc = bin_cell(cl, cg, CL, CG, la, sy, lb);
         k = cc >= 0 ? s_map[cc] : -1;
-        if (k >= 0) {
+        if (k >= 0)
           atomicAdd(&s_cnt[cc], 1);
-        } else {
+        else
           bin_list(W, &s_nool, ool, la, sy, lb, g);
-          if (W.enc_ool) k = -2 - bin_triple(la, sy, lb, G, K0);
-        }
       }
-      if (FUSE_PACK) {
-        D.tok[g] = bin_tok(D, g, D.lab0[g], sy, g > 0 ? D.gsym[g - 1] : -1, k);
-        if (D.gs16) D.gs16[g] = (uint16_t)(sy < 0 ? 0xFFFFu : (uint32_t)sy);
-      } else {
-        D.pk[g] = k;
-        if (BIN_FP) D.fp[g] = bin_fp(k);
-      }
+      D.pk[g] = k;
     }
   }
   __syncthreads();
@@ -503,8 +441,8 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_reduce(Dev D, BinWork W, int to_
 // triple.  k_bin_ool_stage: LDS-staged counts per list, one atomic per
 // (list, triple); the add that finds a cell at 0 lists the triple as new.
 // k_bin_ool_claim: one thread per new triple claims its key (a found key is a
-// hash collision: every other bin key is a distinct triple).  k_bin_ool_fix: pk /
-// fp of every listed pair from the cell (now the key id).
+// hash collision: every other bin key is a distinct triple).  k_bin_ool_fix: pk
+// of every listed pair from the cell (now the key id).
 __device__ inline void bin_stage_list(const Dev& D, AggOol& agg, int2* ool, int32_t n) {
   for (int32_t j = threadIdx.x; j < n; j += ABLOCK) {
     const int32_t d = ool[j].y;
@@ -582,7 +520,7 @@ __global__ __launch_bounds__(ABLOCK) void k_bin_ool_fix(Dev D, BinWork W) {
 
 // ---- the lists, sparse form (larger triple spaces): per list, LDS-staged counts
 // per triple, then one find-or-claim and one count add per distinct triple,
-// then pk / fp of every listed pair.  A list holding more than AggOol::N
+// then pk of every listed pair.  A list holding more than AggOol::N
 // distinct triples sends the rest through the key table one by one.
 __global__ __launch_bounds__(ABLOCK) void k_bin_ool(Dev D, BinWork W, int to_delta) {
   __shared__ AggOol agg;

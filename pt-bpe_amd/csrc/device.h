@@ -24,48 +24,15 @@ constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per re
 constexpr int NBKT = 1 << NBKT_LOG2;
 constexpr int SKIP_HOT = 1, SKIP_MEASURE = 4;  // what a rebuild iteration does
 constexpr int DBG_SLOTS = 64;
-#ifndef PW_LDS_DEF
-#define PW_LDS_DEF 2048
-#endif
-constexpr int PW_LDS = PW_LDS_DEF;  // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
+constexpr int PW_LDS = 2048;  // hash powers staged in LDS by k_apply (chains up to ~1000 residues)
 constexpr int KL_CHUNK = 4096;  // klist entries a commit workgroup reserves at a time
 // merge find -> commit hand-off (merge.h): per (owner, find workgroup) fixed record
 // slots, overflow to one global list
 constexpr int NBA_MAX = 256;
-#ifndef GB_SK
-#define GB_SK 48
-#endif
-#ifndef GB_FKC
-#define GB_FKC 2048
-#endif
-#ifndef EARLY_LOADS
-#define EARLY_LOADS 0  // k_find: the EHASH-check records loaded first, compared last (A/B: spills, slower)
-#endif
-#ifndef EARLY_KCHUNK
-#define EARLY_KCHUNK 1  // k_commit: the owner's klist chunk loaded with the first round
-#endif
-#ifndef PLACE_PRE
-#define PLACE_PRE 1  // k_place: the first round's records loaded before the token rewrites
-#endif
-#ifndef BIN_FP
-#define BIN_FP 0  // the 16-bit pair fingerprints (fp): written, never read since round 2's token records
-#endif  // (device.h: k_init_tokens and the import write them too)
-#ifndef BIN_OOLPACK
-#define BIN_OOLPACK 0  // k_pack reads the out-of-cube pairs' keys (no k_bin_ool_fix); 0: the fix-up kernel
-#endif
-#ifndef FIND_NT
-#define FIND_NT 0  // k_find: non-temporal stores of its outputs (A/B)
-#endif
-#ifndef COMMIT_SPEC
-#define COMMIT_SPEC 0  // k_commit: 1 = load every finder slot's first records before the scans
-#endif
-#ifndef GB_CKC
-#define GB_CKC 2048
-#endif
-constexpr int SK = GB_SK;    // key records per (owner, find workgroup)
-constexpr int SD = GB_SK;    // decrement records per (owner, find workgroup)
-constexpr int FKC = GB_FKC;  // find: new-key dedupe slots (LDS) per round
-constexpr int CKC = GB_CKC;  // commit: key dedupe slots (LDS) per owner
+constexpr int SK = 48;      // key records per (owner, find workgroup)
+constexpr int SD = 48;      // decrement records per (owner, find workgroup)
+constexpr int FKC = 2048;   // find: new-key dedupe slots (LDS) per round
+constexpr int CKC = 2048;   // commit: key dedupe slots (LDS) per owner
 constexpr int FMQ = 4096;    // find: candidate queue (LDS) per chunk of posting entries
 constexpr int LOG_CH_MAX = 64;  // posting-log chunks one owner may add in one merge
 
@@ -119,21 +86,6 @@ struct State {
   int64_t mid_nm[2], mid_nh[2];  // mid.h: merged occurrences / new pairs of k_mid_find, by launch parity
   int32_t place_par_prev;        // mid.h: parity of the merge whose new pairs the next find appends (-1: none)
   int32_t pad6;
-};
-
-// k_select -> k_find (FIND_HDR): region r's candidates of the winner, found by the select's
-// workgroup once the winner is known -- the bucket bounds in r's posting index, r's share of the
-// winner owner's posting log and the pool chunks that share lies in -- so that k_find's first
-// round of loads holds them and its second the candidates themselves (round 4's k_find loaded
-// the bucket offsets and log length, then the chunk table, then the candidates: two more rounds)
-#ifndef FIND_HDR
-#define FIND_HDR 0  // (A/B, profiles/r5_s5: the select workgroup's two extra rounds outweigh the find's gain)
-#endif
-constexpr int FH_CH = 4;  // chunk ids carried (a share spanning more reads the chunk table)
-struct FindHdr {
-  int32_t lo, n1;    // the bucket of W in region r's posting index: post[r * PR + lo .. + n1)
-  int32_t ls0, ls1;  // region r's share of the owner's log: entries [ls0, ls1)
-  int32_t ch[FH_CH]; // pool chunks of log chunks ls0 / CHUNK, + 1, ...
 };
 
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
@@ -205,7 +157,6 @@ struct Dev {
   int4* tok;
   int32_t* pk;    // the bin pass's pair keys (streamed there; k_pack copies them into tok.w)
   int32_t* lab0;  // initial residue labels (= tok[s].x before any merge): the bin pass streams these
-  uint16_t* fp;  // 16-bit fingerprint of pk (0xFFFF = none), written by the bin pass
   // vocab (token id indexed)
   u64 *vh1, *vh2;
   int32_t* vlen;
@@ -295,7 +246,6 @@ struct Dev {
   LogRec* log;
   State* st;
   Sel* sel;  // [2], by launch parity
-  struct FindHdr* fh;  // [NBA]: k_select's per-region candidate bounds for k_find (FIND_HDR)
 };
 
 // ------------------------------------------------------------------ arithmetic
@@ -336,21 +286,11 @@ __device__ inline u64 probe_key(u64 h1, u64 h2, int32_t len) {
 // VGPRs that the 128-VGPR budget of a 1024-thread workgroup then spilled to scratch -- every
 // lane of every launch wrote ~28 B of scratch (k_find / k_mid_find: ~7-8 MB of HBM writes
 // per launch at the kernel end).  A call materialises them in the cold block instead.
-#ifndef SET_ERROR_INLINE
-#define SET_ERROR_INLINE 0  // (A/B: 1 = the inlined form)
-#endif
-#if SET_ERROR_INLINE
-__device__ inline void set_error(const Dev& D, int64_t code, int64_t pos) {
-  unsigned long long* p = (unsigned long long*)&D.st->err_code;
-  if (atomicCAS(p, 0ULL, (unsigned long long)code) == 0ULL) D.st->err_pos = pos;
-}
-#else
 __device__ __attribute__((noinline, cold)) void set_error_at(State* st, int64_t code, int64_t pos) {
   unsigned long long* p = (unsigned long long*)&st->err_code;
   if (atomicCAS(p, 0ULL, (unsigned long long)code) == 0ULL) st->err_pos = pos;
 }
 __device__ inline void set_error(const Dev& D, int64_t code, int64_t pos) { set_error_at(D.st, code, pos); }
-#endif
 
 // Python / numpy  (v + 2*pi) % (2*pi)  in float64 (float_rem / npy_divmod)
 __device__ inline double wrap2pi(double v) {
@@ -742,10 +682,6 @@ __device__ inline void agg_flush_hot(A& s, const Dev& D, HotApp& h, bool to_delt
 #pragma unroll
     for (int u = 0; u < U; u++) {
       old[u] = 0;
-#ifdef GB_FLUSH_NORET  // (diagnostic A/B only: no theta-crossing check)
-      if (v[u] != 0) atomicAdd(&D.count[k[u]], v[u]);
-      continue;
-#endif
       if (v[u] > 0 && th > 0)
         old[u] = atomicAdd(&D.count[k[u]], v[u]);
       else if (v[u] != 0)

@@ -39,12 +39,6 @@
 #include "rmsd.h"
 #include "glue.h"
 
-namespace gb {
-// kp_sort.hip (its own translation unit): stable radix sort of (key, value) int32 pairs
-hipError_t kp_sort_pairs(void* temp, size_t* temp_bytes, const int32_t* keys_in, int32_t* keys_out,
-                         const int32_t* vals_in, int32_t* vals_out, int64_t n, int end_bit, hipStream_t s);
-}  // namespace gb
-
 using namespace gb;
 
 // RCCL entry points, resolved with dlsym from the RCCL library the process already uses
@@ -108,10 +102,7 @@ struct geobpe_ctx {
   // run_batches: iterations past a batch's target idle on the device (SEL_IDLE), so a rebuild
   // iteration inside the batch costs no host round trip; run_end = target merges + 1 (0: off)
   int32_t run_end = 0;
-#ifndef SPEC_DEF
-#define SPEC_DEF 1
-#endif
-  int spec = SPEC_DEF;         // iterations enqueued past the run's last batch target (GEOBPE_SPEC)
+  int spec = 1;                // iterations enqueued past the run's last batch target (GEOBPE_SPEC)
   double decay = 0;            // maxc ratio per merge over the last pulled batch (0: unknown)
   // middle regime (mid.h): merges whose count is <= mid_thresh run as k_mid_sel + k_mid_find
   int64_t mid_thresh = 65536;  // 0: never (C3 merges 11..1000, round 5 kernels: 32768 -> 32.2k, 49152 -> 32.6k, 65536 -> 32.8k, 98304 -> 32.8k merges/s)
@@ -140,13 +131,6 @@ struct geobpe_ctx {
   int32_t* cg_gsym = nullptr;
   uint16_t* cg_gs16 = nullptr;
   int64_t* cg_row = nullptr;
-  // per-key list build (tail_build): radix-sort scratch; kp_atomic: the atomic counting build (A/B)
-  void* kps = nullptr;
-  int64_t kps_bytes = 0;
-#ifndef KP_ATOMIC_DEFAULT
-#define KP_ATOMIC_DEFAULT 1  // (the atomic counting build; A/B builds: 0 = the radix-sorted build)
-#endif
-  bool kp_atomic = KP_ATOMIC_DEFAULT != 0;
   int64_t own_row0 = 0, own_row1 = -1;
   // profiling
   bool prof = false;
@@ -377,9 +361,9 @@ int alloc_keys(geobpe_ctx* c) {
 }
 
 // after the bin pass: pair keys into the token records, 16-bit junction symbols
-void enqueue_pack(geobpe_ctx* c, const int32_t* dcnt = nullptr) {
+void enqueue_pack(geobpe_ctx* c) {
   Timed t(c, "bin_pack");
-  hipLaunchKernelGGL(k_pack, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, dcnt);
+  hipLaunchKernelGGL(k_pack, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
 }
 
 // the launches of one merge iteration (no host synchronisation)
@@ -411,9 +395,6 @@ void enqueue_apply(geobpe_ctx* c) {
   LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
   c->place_pending = true;
   c->place_mid = false;
-#ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
-  flush_place(c);
-#endif
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, (int)(c->gen & 1), c->ev, c->ev_cap,
                        c->ev_n);
@@ -495,62 +476,13 @@ int tail_alloc(geobpe_ctx* c) {
   return 0;
 }
 
-// per-key posting lists of the live pairs, after any pending place.  Default: the counting
-// build with a global atomic per pair (k_kp_alloc / k_kp_fill).  GEOBPE_KP_ATOMIC=0 (A/B): a
-// stable radix sort of the (key, slot) pairs (kp_sort.hip) -> runs -> list space ->
-// placement; measured slower end to end at C3 (25.3k vs 28.6k merges/s)
-// the sorted build's scratch: keys / slots in and out + the sort's own (reserved with the
-// regime arrays when that build is selected)
-int kp_sort_scratch(geobpe_ctx* c, int* end_bit_out, size_t* tb_out) {
-  const int64_t n = c->R;
-  if (n <= 0 || n >= INT32_MAX) return 1;
-  int end_bit = 1;
-  while (end_bit < 31 && (1LL << end_bit) <= c->D.HC) end_bit++;
-  size_t tb = 0;
-  if (kp_sort_pairs(nullptr, &tb, nullptr, nullptr, nullptr, nullptr, n, end_bit, c->stream) != hipSuccess) return 1;
-  const int64_t need = 4 * n * 4 + (int64_t)tb + 1024;
-  if (c->kps_bytes < need) {
-    if (c->kps) {
-      hipStreamSynchronize(c->stream);
-      hipFree(c->kps);
-      c->kps = nullptr;
-      c->kps_bytes = 0;
-    }
-    if (hipMalloc(&c->kps, (size_t)need) != hipSuccess) return 1;
-    c->kps_bytes = need;
-  }
-  *end_bit_out = end_bit;
-  *tb_out = tb;
-  return 0;
-}
-
-int tail_build_sorted(geobpe_ctx* c) {
-  Dev& D = c->D;
-  const int64_t n = c->R;
-  int end_bit;
-  size_t tb;
-  if (kp_sort_scratch(c, &end_bit, &tb)) return 1;
-  const int32_t none = (int32_t)((1LL << end_bit) - 1);  // (> every key id: sorts last)
-  int32_t* kin = reinterpret_cast<int32_t*>(c->kps);
-  int32_t* vin = kin + n;
-  int32_t* kout = vin + n;
-  int32_t* vout = kout + n;
-  void* temp = reinterpret_cast<char*>(vout + n) + 256 - (reinterpret_cast<uintptr_t>(vout + n) & 255);
-  hipLaunchKernelGGL(k_kp_reset, dim3(c->nb), dim3(BLOCK), 0, c->stream, D);
-  hipLaunchKernelGGL(k_kp_keys, dim3(c->nb), dim3(BLOCK), 0, c->stream, D, kin, vin, none);
-  if (kp_sort_pairs(temp, &tb, kin, kout, vin, vout, n, end_bit, c->stream) != hipSuccess) return 1;
-  hipLaunchKernelGGL(k_kp_runs, dim3(c->nb), dim3(BLOCK), 0, c->stream, D, (const int32_t*)kout, none);
-  hipLaunchKernelGGL(k_kp_alloc_runs, dim3(c->nb), dim3(BLOCK), 0, c->stream, D);
-  hipLaunchKernelGGL(k_kp_fill_runs, dim3(c->nb), dim3(BLOCK), 0, c->stream, D, (const int32_t*)kout,
-                     (const int32_t*)vout, none);
-  hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, D);  // (nothing pending)
-  return 0;
-}
-
+// per-key posting lists of the live pairs, after any pending place: a counting build with a
+// global atomic per pair (k_kp_alloc / k_kp_fill).  (Round 4 A/B: a stable radix sort of the
+// (key, slot) pairs -> runs -> list space -> placement took as long, and its first call loaded
+// the sort's code object inside the loop: 25.3k vs 28.6k merges/s end to end)
 void tail_build(geobpe_ctx* c) {
   flush_place(c);
   Timed t(c, "tail_build");
-  if (!c->kp_atomic && tail_build_sorted(c) == 0) return;
   if (c->distributed) {  // (a rank's counts are global: count its own live pairs)
     hipLaunchKernelGGL(k_kp_reset, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
     hipLaunchKernelGGL(k_kp_count, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
@@ -640,16 +572,6 @@ int regime_reserve(geobpe_ctx* c) {
   if (c->distributed || (c->mid_thresh <= 0 && c->tail_thresh <= 0)) return 0;
   int rc;
   if ((rc = tail_alloc(c))) return rc;
-  int end_bit;
-  size_t tb;
-  if (!c->kp_atomic && kp_sort_scratch(c, &end_bit, &tb)) c->kp_atomic = true;  // (no scratch: the atomic build)
-  if (!c->kp_atomic) {  // one tiny sort now: the sort's code object loads here (~4.6 ms at first use), not at the switch
-    int32_t* k = reinterpret_cast<int32_t*>(c->kps);
-    size_t tb1 = 0;
-    kp_sort_pairs(nullptr, &tb1, nullptr, nullptr, nullptr, nullptr, 1, end_bit, c->stream);
-    if (tb1 + 64 <= (size_t)c->kps_bytes - 16 * 4)
-      kp_sort_pairs(k + 16, &tb1, k, k + 4, k + 8, k + 12, 1, end_bit, c->stream);
-  }
   return sync_state(c);
 }
 
@@ -701,7 +623,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   memset(c->h_state, 0, sizeof(State));
   c->h_state->place_par = -1;
   int rc;
-  if ((rc = dalloc(c, &c->D.st, 1, 0)) || (rc = dalloc(c, &c->D.sel, 2, 0)) || (rc = dalloc(c, &c->D.fh, NBA_MAX, 0))) return rc;
+  if ((rc = dalloc(c, &c->D.st, 1, 0)) || (rc = dalloc(c, &c->D.sel, 2, 0))) return rc;
   HIPCHK(c, hipMemcpyAsync(c->D.st, c->h_state, sizeof(State), hipMemcpyHostToDevice, c->stream));
   hipDeviceProp_t prop;
   if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
@@ -714,7 +636,6 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_SPEC")) c->spec = std::max(0, atoi(e));  // (A/B: 0 = no idle iterations)
-  if (const char* e = getenv("GEOBPE_KP_ATOMIC")) c->kp_atomic = atoi(e) != 0;  // (A/B: 0 = the sorted list build)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
   c->D.NBA = c->nba;
@@ -737,7 +658,6 @@ void geobpe_destroy(geobpe_ctx* c) {
   if (c->comm && c->rccl.CommDestroy) c->rccl.CommDestroy(c->comm);
   for (uint8_t* p : {c->x_pbuf, c->x_gath, c->x_tmp, c->x_flat})
     if (p) hipFree(p);
-  if (c->kps) hipFree(c->kps);
   if (c->x_hsend) hipHostFree(c->x_hsend);
   if (c->x_hrecv) hipHostFree(c->x_hrecv);
   for (auto e : c->evall) hipEventDestroy(e);
@@ -769,8 +689,7 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
   const int64_t Rp = c->R + 8;  // int4 padding for the pk scan
   if ((rc = dalloc(c, &c->d_row_off, n_rows + 1)) || (rc = dalloc(c, &D.rsym, Rp, 0)) ||
       (rc = dalloc(c, &D.gsym, Rp, 0)) || (rc = dalloc(c, &D.tok, Rp, 0xFF)) || (rc = dalloc(c, &D.lab0, Rp, 0xFF)) ||
-      (rc = dalloc(c, &D.pk, Rp, 0xFF)) ||
-      (BIN_FP && (rc = dalloc(c, &D.fp, Rp + 16, 0xFF))))  // (fp: only the BIN_FP=1 build writes it)
+      (rc = dalloc(c, &D.pk, Rp, 0xFF)))
     return rc;
   D.row_off = c->d_row_off;
   HIPCHK(c, hipMemcpyAsync(c->d_row_off, h_row_off, (n_rows + 1) * 8, hipMemcpyHostToDevice, c->stream));
@@ -1048,9 +967,6 @@ int geobpe_bin(geobpe_ctx* c) {
     HIPCHK(c, hipMemsetAsync(W.flag, 0, (size_t)BIN_NC * 4, c->stream));
     const int64_t DS = K0 * G * K0;
     const bool dense_lists = DS <= (1LL << 26);
-    // (BIN_OOLPACK: with the dense lists and a separate k_pack, the listed pairs' keys are read by
-    // k_pack from the triple counts' cells, and k_bin_ool_fix does not run)
-    W.enc_ool = BIN_OOLPACK && dense_lists && !FUSE_PACK ? 1 : 0;
     if (dense_lists) {
       W.DS = DS;
       W.newcap = std::min<int64_t>(DS, c->R + 1);
@@ -1083,13 +999,13 @@ int geobpe_bin(geobpe_ctx* c) {
         hipLaunchKernelGGL(k_bin_ool_stage, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
         hipLaunchKernelGGL(k_bin_ool_claim, dim3(4 * c->ncu), dim3(BLOCK), 0, c->stream, c->D, W,
                            c->distributed ? 1 : 0);
-        if (!W.enc_ool) hipLaunchKernelGGL(k_bin_ool_fix, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
+        hipLaunchKernelGGL(k_bin_ool_fix, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
       } else {
         hipLaunchKernelGGL(k_bin_ool, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W, c->distributed ? 1 : 0);
         hipLaunchKernelGGL(k_bin_verify, dim3(nbc), dim3(ABLOCK), 0, c->stream, c->D, W);
       }
     }
-    if (!FUSE_PACK) enqueue_pack(c, W.enc_ool ? W.dcnt : nullptr);  // (fused: k_bin_count wrote the records)
+    enqueue_pack(c);
     HIPCHK(c, hipGetLastError());
     rc = sync_state(c);
     if (!rc) {
@@ -1408,9 +1324,6 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
   LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
   c->place_pending = true;
-#ifdef GB_NO_FUSE  // (A/B: k_place as its own launch right after k_commit)
-  flush_place(c);
-#endif
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
   HIPCHK(c, hipGetLastError());
@@ -2475,11 +2388,15 @@ int x_collapse(geobpe_ctx* c, bool* done) {
             !grow_dev(c, &c->x_tmp, &c->x_tmp_bytes, std::max<int64_t>(W * nmax * 16, 8));
   bool every = false;
   if ((rc = x_agree(c, ok, &every))) return rc;
-  if (!every) {
+  if (!every) {  // (declined for good: the whole-corpus static arrays of x_collapse_prepare go too)
     dfree(c, &tok2);
     dfree(c, &d_base);
     if (dp1) dfree(c, &dp1);
     if (dp2) dfree(c, &dp2);
+    dfree(c, &c->cg_gsym);
+    dfree(c, &c->cg_row);
+    if (c->cg_gs16) dfree(c, &c->cg_gs16);
+    c->cg_ready = false;
     c->collapse_on = false;
     return 0;
   }

@@ -52,19 +52,11 @@ struct GlueProb {
 // the CPU (glibc / SLEEF, ~correctly rounded) are matched more closely than by the ~1-2 ulp
 // single-precision device library, and the trajectory of 20 L-BFGS iterations amplifies
 // every ulp
-#ifdef GLUE_DEVICE_TRIG  // A/B build switch: the single-precision device library
-__device__ inline float f_sin(float a) { return sinf(a); }
-__device__ inline float f_cos(float a) { return cosf(a); }
-__device__ inline float f_atan2(float y, float x) { return atan2f(y, x); }
-__device__ inline float f_exp(float a) { return expf(a); }
-__device__ inline float f_log(float a) { return logf(a); }
-#else
 __device__ inline float f_sin(float a) { return (float)sin((double)a); }
 __device__ inline float f_cos(float a) { return (float)cos((double)a); }
 __device__ inline float f_atan2(float y, float x) { return (float)atan2((double)y, (double)x); }
 __device__ inline float f_exp(float a) { return (float)exp((double)a); }
 __device__ inline float f_log(float a) { return (float)log((double)a); }
-#endif
 
 struct IV {  // a strided float vector of one chain
   float* p;

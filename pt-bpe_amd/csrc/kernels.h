@@ -135,84 +135,17 @@ __global__ __launch_bounds__(BLOCK) void k_first(Dev D, int64_t row_base, u64* f
 // symbol << 16, previous slot, pair key}: one 16-B store per residue, consecutive lanes on
 // consecutive records), and the 16-bit junction symbols.  Round 4's k_pack stored pk and the
 // length word into the records' 2nd and 4th words, 4-B stores at a 16-B lane stride, ~285 us
-// at C3.  (Every token is one residue here; g starts its chain iff gsym[g - 1] < 0.)
-// dcnt (BIN_OOLPACK, the dense bin lists): a pair k_bin_count listed has pk = -2 - its triple, whose
-// key id k_bin_ool_claim left in dcnt -- read here instead of a fix-up kernel rewriting pk first
-// PACK_VEC = 1: four consecutive residues per thread (16-B loads of labels, junction symbols and
-// pair keys, four 16-B record stores and one 8-B symbol store: a quarter of the memory
-// instructions)
-#ifndef PACK_VEC
-#define PACK_VEC 0
-#endif
-#ifndef PACK_UNR
-#define PACK_UNR 1  // (2, 4, 8 measured slower: profiles/r5_ab/r5_pu.txt)
-#endif
-__device__ inline int4 pack_rec(const Dev& D, int64_t g, int32_t lab, int32_t gs, int32_t gp, int32_t k0,
-                                const int32_t* dcnt) {
-  const int32_t k = dcnt && k0 <= -2 ? dcnt[-2 - k0] : k0;
-  const uint32_t g16 = gs < 0 ? 0xFFFFu : (uint32_t)gs;
-  return make_int4(lab, D.gs16 ? (int32_t)(1u | (g16 << 16)) : 1, gp >= 0 ? (int32_t)(g - 1) : -1, k);
-}
-__global__ __launch_bounds__(BLOCK) void k_pack(Dev D, const int32_t* dcnt) {
-#if PACK_VEC
-  const int64_t nv = D.R / 4;
-  const int4* lv = reinterpret_cast<const int4*>(D.lab0);
-  const int4* sv = reinterpret_cast<const int4*>(D.gsym);
-  const int4* kv = reinterpret_cast<const int4*>(D.pk);
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nv; v += (int64_t)gridDim.x * blockDim.x) {
-    const int4 lab = lv[v], gs = sv[v], k = kv[v];
-    const int64_t g = 4 * v;
-    const int32_t gp = g > 0 ? D.gsym[g - 1] : -1;  // (the previous lane's line: a cache hit)
-    int4* t = D.tok + g;
-    t[0] = pack_rec(D, g, lab.x, gs.x, gp, k.x, dcnt);
-    t[1] = pack_rec(D, g + 1, lab.y, gs.y, gs.x, k.y, dcnt);
-    t[2] = pack_rec(D, g + 2, lab.z, gs.z, gs.y, k.z, dcnt);
-    t[3] = pack_rec(D, g + 3, lab.w, gs.w, gs.z, k.w, dcnt);
-    if (D.gs16) {
-      auto h16 = [](int32_t x) { return (uint16_t)(x < 0 ? 0xFFFFu : (uint32_t)x); };
-      reinterpret_cast<ushort4*>(D.gs16)[v] = make_ushort4(h16(gs.x), h16(gs.y), h16(gs.z), h16(gs.w));
-    }
-  }
-  for (int64_t g = 4 * nv + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R;
-       g += (int64_t)gridDim.x * blockDim.x) {  // (the < 4 residues past the last full group)
-    const int32_t gs = D.gsym[g];
-    D.tok[g] = pack_rec(D, g, D.lab0[g], gs, g > 0 ? D.gsym[g - 1] : -1, D.pk[g], dcnt);
-    if (D.gs16) D.gs16[g] = (uint16_t)(gs < 0 ? 0xFFFFu : (uint32_t)gs);
-  }
-#elif PACK_UNR > 1
-  // PACK_UNR residues per thread a grid stride apart (coalesced as above), every load of the
-  // group issued before any store: ~4x the bytes in flight of one residue per iteration, which
-  // left the kernel latency-bound at ~0.7 of HBM peak
-  const int64_t S = (int64_t)gridDim.x * blockDim.x, R = D.R;
-  for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g0 < R; g0 += PACK_UNR * S) {
-    int32_t lab[PACK_UNR], gs[PACK_UNR], k0[PACK_UNR], gp[PACK_UNR];
-#pragma unroll
-    for (int u = 0; u < PACK_UNR; u++) {
-      const int64_t g = g0 + u * S;
-      const int64_t i = g < R ? g : 0;  // (clamped: unconditional loads)
-      lab[u] = D.lab0[i];
-      gs[u] = D.gsym[i];
-      k0[u] = D.pk[i];
-      gp[u] = D.gsym[i > 0 ? i - 1 : 0];  // (the previous lane's line: a cache hit)
-    }
-#pragma unroll
-    for (int u = 0; u < PACK_UNR; u++) {
-      const int64_t g = g0 + u * S;
-      if (g >= R) break;
-      D.tok[g] = pack_rec(D, g, lab[u], gs[u], g > 0 ? gp[u] : -1, k0[u], dcnt);
-      if (D.gs16) D.gs16[g] = (uint16_t)(gs[u] < 0 ? 0xFFFFu : (uint32_t)gs[u]);
-    }
-  }
-#else
+// at C3.  (Every token is one residue here; g starts its chain iff gsym[g - 1] < 0.)  Measured
+// and dropped: reading the listed pairs' keys here instead of a fix-up kernel, four
+// residues per thread, 2-8 residues per thread in flight.
+__global__ __launch_bounds__(BLOCK) void k_pack(Dev D) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t lab = D.lab0[g], gs = D.gsym[g], k0 = D.pk[g];
-    const int32_t k = dcnt && k0 <= -2 ? dcnt[-2 - k0] : k0;
+    const int32_t lab = D.lab0[g], gs = D.gsym[g], k = D.pk[g];
     const int32_t gp = g > 0 ? D.gsym[g - 1] : -1;  // (the previous lane's line: a cache hit)
     const uint32_t g16 = gs < 0 ? 0xFFFFu : (uint32_t)gs;
     D.tok[g] = make_int4(lab, D.gs16 ? (int32_t)(1u | (g16 << 16)) : 1, gp >= 0 ? (int32_t)(g - 1) : -1, k);
     if (D.gs16) D.gs16[g] = (uint16_t)g16;
   }
-#endif
 }
 
 __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_of_sym) {
@@ -224,7 +157,6 @@ __global__ __launch_bounds__(64) void k_init_tokens(Dev D, const int32_t* label_
       D.tok[g] = make_int4(lab, 1, (g == a) ? -1 : (int32_t)(g - 1), 0);
       D.lab0[g] = lab;
       D.pk[g] = -1;
-      if (BIN_FP) D.fp[g] = 0xFFFF;
     }
   }
 }
@@ -350,10 +282,7 @@ __device__ inline void finalize_one(const Dev& D, AggBig& agg, HotApp& hot, cons
     set_error(D, GEOBPE_EHASH, j);
     return;
   }
-  if (e.target >= 0) {
-    D.pk[e.target] = d;
-    if (BIN_FP) D.fp[e.target] = key_fp(d);
-  }
+  if (e.target >= 0) D.pk[e.target] = d;
   agg_add_hot(agg, D, hot, d, e.delta, to_delta, th);
 }
 
@@ -692,10 +621,7 @@ __device__ inline KSeq key_seq(const Dev& D, int32_t d) {
 // long keys of late merges; a 64-workgroup scan with a last-arriver reduction
 // paid ~6 us of release/acquire fences and tickets for nothing at these lengths.)
 constexpr int SBLOCK = 1024;
-#ifndef SEL_UNR_DEF
-#define SEL_UNR_DEF 4
-#endif
-constexpr int SEL_UNR = SEL_UNR_DEF;  // list entries in flight per thread (A/B: 8 is no faster)
+constexpr int SEL_UNR = 4;  // list entries in flight per thread (A/B: 8 is no faster)
 constexpr int SEL_TMAX = SBLOCK;  // staged candidates
 constexpr int SEL_SYMS = 6144;    // staged content symbols (24 KB)
 
@@ -1016,27 +942,6 @@ __global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par, int run_end) 
   }
   __shared__ Sel s_sel;
   select_core<false>(D, par, S, s_red, &s_sel, run_end);
-#if FIND_HDR
-  __syncthreads();  // (s_sel)
-  if (s_sel.decision == SEL_MERGE && !s_sel.rebuild && s_sel.W >= 0 && (int32_t)threadIdx.x < D.NBA) {
-    // region t's candidates of the winner for k_find (struct FindHdr)
-    const int32_t t = threadIdx.x, W = s_sel.W, o = s_sel.wown;
-    const int32_t* off = D.poff + (int64_t)t * (NBKT + 1);
-    const uint32_t bk = post_bkt(W);
-    const int32_t lo = off[bk], hi = off[bk + 1];
-    const int64_t nlog = log_len(D, o);
-    FindHdr h;
-    h.lo = lo;
-    h.n1 = hi - lo;
-    h.ls0 = (int32_t)(nlog * t / D.NBA);
-    h.ls1 = (int32_t)(nlog * (t + 1) / D.NBA);
-    const int64_t c0 = h.ls0 / D.CHUNK;
-#pragma unroll
-    for (int k = 0; k < FH_CH; k++)
-      h.ch[k] = h.ls1 > h.ls0 && c0 + k <= (h.ls1 - 1) / D.CHUNK ? D.pch[(int64_t)o * D.MAXCH + c0 + k] : -1;
-    D.fh[t] = h;
-  }
-#endif
 }
 
 // merge replay (bin/induce.py): merge t is the trained

@@ -26,57 +26,13 @@
 #pragma once
 // (included inside namespace gb)
 
-// a store written through to memory (gfx950 `global_store ... sc1`: 8-B relaxed agent-scope
-// atomic stores; a 4-B value as one 4-B store): the line leaves the XCD's L2 during the kernel,
-// so the kernel's end has no dirty bytes of it to write back (the boundary costs ~bytes / 6 TB/s
-// on top of ~1.5 us)
-template <typename V>
-__device__ inline void wt_store(V* p, const V& v) {
-  static_assert(sizeof(V) % 8 == 0 || sizeof(V) == 4, "store width");
-  if constexpr (sizeof(V) % 8 == 0) {
-    const unsigned long long* src = reinterpret_cast<const unsigned long long*>(&v);
-    unsigned long long* dst = reinterpret_cast<unsigned long long*>(p);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(V) / 8); i++)
-      __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  } else {
-    __hip_atomic_store(reinterpret_cast<uint32_t*>(p), *reinterpret_cast<const uint32_t*>(&v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-
 // k_find's outputs (merge entries, key / decrement records, T slots) are read once, by
-// k_commit / k_place on other XCDs: FIND_NT=1 stores them non-temporal (A/B), FIND_WT=1
-// write-through
-#ifndef FIND_WT
-#define FIND_WT 0
-#endif
+// k_commit / k_place on other XCDs.  Plain stores: non-temporal (round 2) and write-through
+// (round 5: each scattered 4-16-B store then goes to memory, k_find 29.5 -> 41.3 us) stores
+// were measured slower
 template <typename V>
 __device__ inline void out_store(V* p, const V& v) {
-#if FIND_WT
-  wt_store(p, v);
-#elif FIND_NT
-  static_assert(sizeof(V) % 16 == 0 || sizeof(V) == 8 || sizeof(V) == 4, "store width");
-  if constexpr (sizeof(V) % 16 == 0) {
-    const int4* src = reinterpret_cast<const int4*>(&v);
-    int4* dst = reinterpret_cast<int4*>(p);
-#pragma unroll
-    for (int i = 0; i < (int)(sizeof(V) / 16); i++) {
-      __builtin_nontemporal_store(src[i].x, &dst[i].x);
-      __builtin_nontemporal_store(src[i].y, &dst[i].y);
-      __builtin_nontemporal_store(src[i].z, &dst[i].z);
-      __builtin_nontemporal_store(src[i].w, &dst[i].w);
-    }
-  } else if constexpr (sizeof(V) == 8) {
-    const int2 x = *reinterpret_cast<const int2*>(&v);
-    __builtin_nontemporal_store(x.x, &reinterpret_cast<int2*>(p)->x);
-    __builtin_nontemporal_store(x.y, &reinterpret_cast<int2*>(p)->y);
-  } else {
-    __builtin_nontemporal_store(*reinterpret_cast<const int32_t*>(&v), reinterpret_cast<int32_t*>(p));
-  }
-#else
   *p = v;
-#endif
 }
 
 // a load the compiler issues where it stands: a relaxed workgroup-scope atomic load (a plain
@@ -111,39 +67,14 @@ __device__ inline KRec ld_rec(const KRec* p) {  // (six 8-B loads)
   return r;
 }
 
-// COMMIT_EARLY = 1: k_commit's first round of record loads issued without waits (as PLACE_EARLY)
-#ifndef COMMIT_X1
-#define COMMIT_X1 0  // k_commit: each thread's second extra records (t + ABLOCK) with its first (slower, r5_cx2)
-#endif
-#ifndef COMMIT_EARLY
-#define COMMIT_EARLY 1
-#endif
-// PLACE_EARLY = 1: k_place's second round issued without waits (the T entries' records before the
-// scan, unconditional loads, the token stores not behind a conditional load); 0: round 4's order
-#ifndef PLACE_EARLY
-#define PLACE_EARLY 1
-#endif
-
-// the record counts finder r sent owner o (cntK / cntD).  CNT_T = 1 keeps them finder-major,
-// so a finder's end writes whole lines (owner-major, its 2 x NBA counts were NBA-strided 4-B
-// writes: 2 x 65 536 partial lines a launch written back at k_find's end)
-#ifndef CNT_T
-#define CNT_T 1
-#endif
-__device__ inline int64_t cnt_at(const Dev& D, int32_t o, int32_t r) {
-  return CNT_T ? (int64_t)r * D.NBA + o : (int64_t)o * D.NBA + r;
-}
-// CNT_PAIR = 1: the two counts of a (finder, owner) as one int2 in cntK (allocated 2 x NBA^2),
-// so an owner's first round loads one strided line set instead of two
-#ifndef CNT_PAIR
-#define CNT_PAIR 1
-#endif
+// the record counts finder r sent owner o, finder-major, so a finder's end writes whole lines
+// (owner-major, its 2 x NBA counts were NBA-strided 4-B writes: 2 x 65 536 partial lines a
+// launch written back at k_find's end)
+__device__ inline int64_t cnt_at(const Dev& D, int32_t o, int32_t r) { return (int64_t)r * D.NBA + o; }
+// the two counts of a (finder, owner) as one int2 in cntK (allocated 2 x NBA^2), so an owner's
+// first round loads one strided line set instead of two
 __device__ inline int2 cnt_pair(const Dev& D, int32_t o, int32_t r) {
-#if CNT_PAIR
   return reinterpret_cast<const int2*>(D.cntK)[cnt_at(D, o, r)];
-#else
-  return make_int2(D.cntK[cnt_at(D, o, r)], D.cntD[cnt_at(D, o, r)]);
-#endif
 }
 
 // chunked per-owner posting log: entry k of owner o
@@ -238,16 +169,6 @@ __device__ inline void check_found(const Dev& D, int32_t r) {
   }
 }
 
-// check_found with this thread's first record already loaded (EARLY_LOADS)
-__device__ inline void check_found_tail(const Dev& D, int32_t r, int32_t n, const NewPair& e0) {
-  const NewPair* reg = D.chk + (int64_t)r * D.RC;
-  for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const NewPair e = i < (int32_t)blockDim.x ? e0 : reg[i];
-    const int32_t d = e.target;
-    if (!key_is(D, d, e.h1, e.h2, e.len)) set_error(D, GEOBPE_EHASH, i);
-  }
-}
-
 // ---------------------------------------------------------------------- k_find
 struct FHalf {  // a new neighbour pair of a merged occurrence
   u64 pkey, h1, h2;
@@ -278,7 +199,7 @@ struct FindLds {
   int32_t curK[NBA_MAX], curD[NBA_MAX];
   int32_t red[ABLOCK / 64];
   int32_t qn, n, tb, fits, ktot;
-  int32_t qsteal;  // FIND_STEAL: the round's next unclaimed candidate
+  int32_t qsteal;  // the round's next unclaimed candidate (candidate stealing)
 };
 
 __device__ inline void emit_occ(const Dev& D, FindCtx& F, int32_t* s_n, int32_t a, int32_t ya, int32_t b, int32_t c) {
@@ -489,48 +410,14 @@ __device__ inline int32_t fkc_find(FindLds& S, const Dev& D, u64 k, u64 h1, bool
   return -1;
 }
 
-#ifndef FIND_STEAL
-#define FIND_STEAL 1
-#endif
-#ifndef FAGG
-#define FAGG 0  // k_find: wave-aggregated LDS dedupe of the new keys (iterations; 0: off)
-#endif
-// the round's dedupe slot (s), insert flag and rank within the slot of one new key per lane;
-// lanes of a wave holding the same key (a common neighbour token: the same new key for many
-// occurrences of a region) take one LDS probe and one counter add between them, up to FAGG
-// keys per wave -- the rest probe on their own
+// the round's dedupe slot (s), insert flag and rank within the slot of one new key per lane
+// (round 5 A/B: lanes of a wave holding the same key sharing one probe and one counter add
+// were slower, DESIGN 8 -- the same-key LDS atomics were not the cost)
 __device__ inline void fkc_group(FindLds& S, const Dev& D, bool v, const FHalf& h, int32_t& s, bool& ins, int32_t& rank) {
   s = -1;
   ins = false;
   rank = 0;
-  bool done = false;
-#if FAGG
-  u64 pend = __ballot(v);
-  const int lane = wave_lane();
-  for (int it = 0; it < FAGG && pend; it++) {  // (wave-uniform)
-    const int leader = __ffsll((long long)pend) - 1;
-    const u64 lk = __shfl((unsigned long long)h.pkey, leader, 64);
-    const bool same = v && !done && h.pkey == lk;
-    const u64 m = __ballot(same);
-    if (__popcll(m) < 2) break;
-    int32_t ss = -1, base = 0;
-    bool r = false;
-    if (lane == leader) {
-      ss = fkc_find(S, D, h.pkey, h.h1, &r);
-      if (ss >= 0) base = atomicAdd(&S.u.m.kcnt[ss], (int32_t)__popcll(m));
-    }
-    ss = __shfl(ss, leader, 64);
-    base = __shfl(base, leader, 64);
-    if (same) {
-      s = ss;
-      rank = base + (int32_t)__popcll(m & ((1ULL << lane) - 1));
-      ins = lane == leader && r;
-    }
-    done = done || same;
-    pend &= ~m;
-  }
-#endif
-  if (v && !done) {
+  if (v) {
     s = fkc_find(S, D, h.pkey, h.h1, &ins);
     if (s >= 0) rank = atomicAdd(&S.u.m.kcnt[s], 1);
   }
@@ -546,24 +433,8 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   const int32_t r = blockIdx.x;
   dbg_stamp(D, 10);
   const Sel sel = D.sel[par];
-#if FIND_HDR
-  const FindHdr fh = D.fh[r];  // (valid for a merge without a posting rebuild: k_select wrote it)
-#endif
-#if EARLY_LOADS
-  // EHASH check of the keys the previous commit / import found: the first ABLOCK records
-  // are loaded now and compared after the merge work (their two dependent rounds used to
-  // precede the candidate loads)
-  const int32_t nchk = D.chkcnt[r];
-  NewPair chk0;
-  if ((int32_t)threadIdx.x < nchk) chk0 = D.chk[(int64_t)r * D.RC + threadIdx.x];
-  if (sel.decision != SEL_MERGE) {
-    check_found_tail(D, r, nchk, chk0);
-    return;
-  }
-#else
   check_found(D, r);
   if (sel.decision != SEL_MERGE) return;
-#endif
   FindCtx F;
   F.W = sel.W;
   F.nid = sel.nid;
@@ -607,19 +478,7 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
     }
     queued = S.qn <= FMQ;
   }
-#if FIND_HDR
-  bool hdr = false;  // (the log chunks of the share from k_select's header)
-#endif
   if (W >= 0 && !queued) {
-#if FIND_HDR
-    if (!sel.rebuild) {
-      lo = fh.lo;
-      n1 = fh.n1;
-      ls0 = fh.ls0;
-      ls1 = fh.ls1;
-      hdr = ls1 <= ls0 || (ls1 - 1) / D.CHUNK - ls0 / D.CHUNK < FH_CH;
-    } else
-#endif
     {
       const int32_t* off = D.poff + (int64_t)r * (NBKT + 1);
       const uint32_t bk = post_bkt(W);
@@ -662,13 +521,6 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
           e = P[i];
         } else {
           const int64_t k = ls0 + (i - n1);
-#if FIND_HDR
-          if (hdr) {  // (a select chain, not an indexed private array: that one went to LDS)
-            const int64_t ci = k / D.CHUNK - ls0 / D.CHUNK;
-            const int32_t ch = ci == 0 ? fh.ch[0] : ci == 1 ? fh.ch[1] : ci == 2 ? fh.ch[2] : fh.ch[3];
-            e = D.pool[(int64_t)ch * D.CHUNK + k % D.CHUNK];
-          } else
-#endif
             e = D.pool[log_addr(D, o, k)];
         }
         if (e.x == W) S.q[atomicAdd(&S.qn, 1)] = e.y;
@@ -682,16 +534,12 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       int32_t qi = q0 + threadIdx.x;
       FHalf hl, hr;
       bool vl = false, vr = false;
-#if FIND_STEAL
       // a thread whose candidate turns out stale or inside a run (~1/3 of them, known after one or
       // two loads) takes the next candidate past the round's first ABLOCK: a workgroup with a few
       // more candidates than threads walks them in this round instead of a second one (~10 us)
       if (threadIdx.x == 0) S.qsteal = q0 + ABLOCK;
       __syncthreads();
       while (qi < nq && find_walk(D, F, S, S.q[qi], hl, vl, hr, vr)) qi = atomicAdd(&S.qsteal, 1);
-#else
-      if (qi < nq) find_walk(D, F, S, S.q[qi], hl, vl, hr, vr);
-#endif
       if (c0 == 0 && q0 == 0) dbg_stamp(D, 15);
       // group the new keys of this round: LDS slot, rank within the slot
       bool rl = false, rr = false;
@@ -764,12 +612,8 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
       }
       if (threadIdx.x == 0 && fits) S.tb += S.ktot;
       __syncthreads();
-#if FIND_STEAL
       q0 = min(S.qsteal, nq);  // (block-uniform: read after the barrier above)
       __syncthreads();  // (before thread 0 resets it for the next round)
-#else
-      q0 += ABLOCK;
-#endif
     }
   }
   dbg_stamp(D, 12);
@@ -791,20 +635,12 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   }
   __syncthreads();
   for (int i = threadIdx.x; i < D.NBA; i += ABLOCK) {
-#if CNT_PAIR
     out_store(reinterpret_cast<int2*>(D.cntK) + cnt_at(D, i, r), make_int2(min(S.curK[i], SK), min(S.curD[i], SD)));
-#else
-    out_store(&D.cntK[cnt_at(D, i, r)], min(S.curK[i], SK));
-    out_store(&D.cntD[cnt_at(D, i, r)], min(S.curD[i], SD));
-#endif
   }
   if (threadIdx.x == 0) {
     out_store(&D.Lcnt[r], min(S.n, (int32_t)D.LC));
     out_store(&D.Tcnt[r], S.tb);  // (T entries of this region: [r * TC, + Tcnt))
   }
-#if EARLY_LOADS
-  check_found_tail(D, r, nchk, chk0);
-#endif
   dbg_stamp(D, 13);
 }
 
@@ -921,12 +757,6 @@ __device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nb
   return (int64_t)nba * nba * SK + (i - nE);
 }
 
-#ifndef COMMIT_CSPEC
-#define COMMIT_CSPEC 1
-#endif
-#ifndef CAGG
-#define CAGG 0  // k_commit: wave-aggregated inserts of the first records (iterations; 0: off)
-#endif
 // commit_resolve with the key's count added in the same round trip: the add to the count of
 // the key's first slot goes out beside the CAS (the key is there unless another key took the
 // slot first: then the add is undone and the key resolved onward).  An unclaimed slot's count
@@ -1125,21 +955,13 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   const int64_t seg = (int64_t)j * nba + w;
   const int2 cKD = cnt_pair(D, j, w);
   const int32_t cK = cKD.x, cD = cKD.y;
-#if COMMIT_SPEC
-  // speculative: the first PER records of every finder's slot in the first round
-  // (~15 MB per launch, mostly empty slots; it held the prefix scans below ~4 us)
-  const KRec r0 = D.KS[seg * SK + min(k0, SK - 1)];
-  const int2 d0 = D.DS[seg * SD + min(k0, SD - 1)];
-#endif
   const Sel sel = D.sel[par];
   const int32_t th = st->theta;
   const int32_t pn = D.pnch[j], pf = D.pfill[j];
   const int32_t plog_ovf0 = st->plog_ovf;  // (read with the first round: the log reservation needs it)
   const int64_t nko_raw = st->nko2[par];
   const int64_t novf_raw = j == 0 ? st->L_ovf2[par] : 0;
-#if EARLY_KCHUNK
   const int64_t kl0 = D.kchunk[2 * j], kl1 = D.kchunk[2 * j + 1];  // (this owner's klist chunk)
-#endif
   int32_t lc = 0;
   if (j == 0 && t < nba) lc = D.Lcnt[t];
   if (j == 0 && t == 0) {
@@ -1207,23 +1029,16 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       S.ns = 0;
       S.chk = 0;
       S.fbn = 0;
-#if EARLY_KCHUNK
       s_kl[0] = kl0;
       s_kl[1] = kl1;
-#else
-      s_kl[0] = D.kchunk[2 * j];
-      s_kl[1] = D.kchunk[2 * j + 1];
-#endif
     }
   }
   __syncthreads();
   dbg_stamp(D, 1);
-#if !COMMIT_SPEC
   // the first PER records of each finder's slot, only where they exist (issuing them before the
   // prefix scans above measured ~1 % slower on the window, profiles/r5_s5/)
   KRec r0;
   int2 d0 = make_int2(0, 0);
-#if COMMIT_EARLY
   // (unconditional loads from clamped slots, all of this round's loads issued before any wait: a
   // load inside `if` made the compiler wait for it at the join, r0 / d0 / e0 / x0 one after another)
   {
@@ -1232,11 +1047,6 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     const int2 d0r = ld_now(&D.DS[seg * SD + (hd ? k0 : 0)]);
     d0 = hd ? d0r : make_int2(0, 0);
   }
-#else
-  if (lane_ok && k0 < min(cK, SK)) r0 = D.KS[seg * SK + k0];
-  if (lane_ok && k0 < min(cD, SD)) d0 = D.DS[seg * SD + k0];
-#endif
-#endif
   // ---- round 1: key records -> LDS dedupe (occurrence totals per key); decrements -> LDS
 #define COMMIT_INSERT(k)                                          \
   do {                                                            \
@@ -1264,16 +1074,6 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   int64_t at0 = 0;
   const bool he = t < nE + nKO;
   int2 x0 = make_int2(-1, 0);
-#if COMMIT_X1
-  // (and its second ones, t + ABLOCK: the owners holding the hottest keys have a few hundred
-  // extras, and their second records were one more dependent round trip; the publish loads them
-  // again -- kept in registers to then, the launch spilled 800 B a thread)
-  KRec e1;
-  int64_t at1 = 0;
-  const bool he1 = t + ABLOCK < nE + nKO;
-  int2 x1 = make_int2(-1, 0);
-#endif
-#if COMMIT_EARLY
   {
     if (he) at0 = extra_at(D, s_preE, nba, j, PER, nE, t);
     int64_t xa = 0;
@@ -1281,85 +1081,22 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       const int32_t ww = seg_of(s_preF, nba, t);
       xa = ((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww]);
     }
-#if COMMIT_X1
-    if (he1) at1 = extra_at(D, s_preE, nba, j, PER, nE, t + ABLOCK);
-    int64_t xa1 = 0;
-    if (t + ABLOCK < nF) {
-      const int32_t ww = seg_of(s_preF, nba, t + ABLOCK);
-      xa1 = ((int64_t)j * nba + ww) * SD + PER + (t + ABLOCK - s_preF[ww]);
-    }
-#endif
     e0 = ld_rec(&D.KS[at0]);
     const int2 x0r = ld_now(&D.DS[xa]);
-#if COMMIT_X1
-    e1 = ld_rec(&D.KS[at1]);
-    const int2 x1r = ld_now(&D.DS[xa1]);
-    x1 = t + ABLOCK < nF ? x1r : make_int2(-1, 0);
-#endif
     x0 = t < nF ? x0r : make_int2(-1, 0);
   }
-#else
-  if (he) {
-    at0 = extra_at(D, s_preE, nba, j, PER, nE, t);
-    e0 = D.KS[at0];
-  }
-  if (t < nF) {
-    const int32_t ww = seg_of(s_preF, nba, t);
-    x0 = D.DS[((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww])];
-  }
-#endif
-#if CAGG
-  {  // a hot key reaches its owner once per finder -- up to 64 times in a wave's r0, each one an
-     // atomic on the same LDS counter: the lanes holding the wave's first pending key add their
-     // totals once (a few keys per wave; the rest insert on their own)
-    u64 pend = __ballot(mine0);
-    bool agg = false;
-    for (int it = 0; it < CAGG && pend; it++) {  // (wave-uniform)
-      const int leader = __ffsll((long long)pend) - 1;
-      const u64 lk = __shfl((unsigned long long)r0.pkey, leader, 64);
-      const bool same = mine0 && !agg && r0.pkey == lk;
-      const u64 m = __ballot(same);
-      if (__popcll(m) < 2) break;
-      const int32_t v = wave_sum(same ? r0.n : 0);
-      if (wave_lane() == leader) {
-        KRec k = r0;
-        k.n = v;
-        COMMIT_INSERT(k);
-      }
-      agg = agg || same;
-      pend &= ~m;
-    }
-    if (mine0 && !agg) COMMIT_INSERT(r0);
-  }
-#else
   if (mine0) COMMIT_INSERT(r0);
-#endif
   if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
   dbg_stamp(D, 56);
-#if COMMIT_X1 && COMMIT_EARLY
-#pragma unroll 1
-  for (int u = 0; u < 2; u++) {  // (one insert site: a second one inlined its fallback again and spilled)
-    const KRec k = u ? e1 : e0;
-    if (u ? he1 && (t + ABLOCK < nE || owner_of_key(D, e1.pkey) == j) : he && (t < nE || owner_of_key(D, e0.pkey) == j))
-      COMMIT_INSERT(k);
-  }
-  for (int32_t i = t + 2 * ABLOCK; i < nE + nKO; i += ABLOCK) {  // (rare: more than 2 ABLOCK extras)
-#else
   if (he && (t < nE || owner_of_key(D, e0.pkey) == j)) COMMIT_INSERT(e0);
   for (int32_t i = t + ABLOCK; i < nE + nKO; i += ABLOCK) {  // (rare: more than ABLOCK extras)
-#endif
     const KRec k = D.KS[extra_at(D, s_preE, nba, j, PER, nE, i)];
     if (i < nE || owner_of_key(D, k.pkey) == j) COMMIT_INSERT(k);
   }
   dbg_stamp(D, 57);
   dbg_val(D, 59, nF);
   if (t < nF && !agg_stage(S.u.agg, x0.x, x0.y)) commit_add(D, x0.x, x0.y, tod);
-#if COMMIT_X1 && COMMIT_EARLY
-  if (t + ABLOCK < nF && !agg_stage(S.u.agg, x1.x, x1.y)) commit_add(D, x1.x, x1.y, tod);
-  for (int32_t i = t + 2 * ABLOCK; i < nF; i += ABLOCK) {
-#else
   for (int32_t i = t + ABLOCK; i < nF; i += ABLOCK) {
-#endif
     const int32_t ww = seg_of(s_preF, nba, i);
     const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
     if (!agg_stage(S.u.agg, x.x, x.y)) commit_add(D, x.x, x.y, tod);
@@ -1399,7 +1136,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
   }
   // ---- every distinct key once: find or claim, its count (+ hot-list crossing)
   int32_t nkeys = 0;
-  if (!tod && COMMIT_CSPEC) {
+  if (!tod) {
     // this thread's two table slots: both keys' CAS and count add out before any result is used
     static_assert(CKC == 2 * ABLOCK, "two commit table slots per thread");
     const u64 ka = S.ckey[t], kb = S.ckey[t + ABLOCK];
@@ -1426,7 +1163,7 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
       if (d >= 0) nkeys++;
     }
   }
-  for (int32_t s = t; s < CKC && (tod || !COMMIT_CSPEC); s += ABLOCK) {
+  for (int32_t s = t; s < CKC && tod; s += ABLOCK) {
     const u64 key = S.ckey[s];
     if (key == 0) continue;
     KRec k;
@@ -1587,16 +1324,9 @@ __device__ inline int32_t place_rec_at(const Dev& D, const PlaceLds& S, int32_t 
 
 // k_place's token rewrites, pk and posting-log entries (read by the next k_find on every XCD):
 // PLACE_WT=1 stores them write-through (A/B)
-#ifndef PLACE_WT
-#define PLACE_WT 0
-#endif
 template <typename V>
 __device__ inline void pl_store(V* p, const V& v) {
-#if PLACE_WT
-  wt_store(p, v);
-#else
   *p = v;
-#endif
 }
 
 // the token rewrites of one merged occurrence (a, b) with right neighbour c: a becomes the new
@@ -1657,13 +1387,11 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   // (unconditional loads from a clamped index: a load inside `if` into a register the other path
   // sets made the compiler wait for it at the join, one group after the other)
   const bool h0 = t < nT && te0.y >= 0, h1 = t + ABLOCK < nT && te1.y >= 0;
-#if PLACE_EARLY
   const int32_t a0 = h0 ? te0.y : 0, a1 = h1 ? te1.y : 0;
   const int2 v0r = ld_now(&D.KSid[a0]), v1r = ld_now(&D.KSid[a1]);
   const int32_t ts0r = ld_now(&D.KS[a0].tstart), ts1r = ld_now(&D.KS[a1].tstart);
   const int2 v0 = h0 ? v0r : make_int2(-1, -1), v1 = h1 ? v1r : make_int2(-1, -1);
   const int32_t ts0 = h0 ? ts0r : 0, ts1 = h1 ? ts1r : 0;
-#endif
   const int64_t oper = (novf + D.NBA - 1) / D.NBA;
   const int64_t o_lo = (int64_t)j * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
   const int64_t kper = (nko + D.NBA - 1) / D.NBA;
@@ -1679,7 +1407,6 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   const int32_t nk = S.pre[D.NBA];
   const int32_t nrec = nk + (int32_t)k_n;
   // ---- round 2, part 2: the records of this finder's slots (their ranges need the scan)
-#if PLACE_EARLY
   const bool hr = t < nrec;
   const int32_t ra = hr ? place_rec_at(D, S, j, t, nk, k_lo) : 0;
   const int2 rnt_r = ld_now(reinterpret_cast<const int2*>(&D.KS[ra].n)), rv_r = ld_now(&D.KSid[ra]);
@@ -1692,28 +1419,6 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   if (t < nA) place_tokens(D, eA, nid);
   for (int64_t i = t + ABLOCK; i < nA; i += ABLOCK) place_tokens(D, D.L[(int64_t)j * D.LC + i], nid);
   for (int64_t i = t; i < o_n; i += ABLOCK) place_tokens(D, D.Lovf[o_lo + i], nid);
-#else
-  int32_t ra = -1;
-  int2 rnt = make_int2(0, 0), rv = make_int2(-1, -1);
-  if (t < nrec) {
-    ra = place_rec_at(D, S, j, t, nk, k_lo);
-    rnt = *reinterpret_cast<const int2*>(&D.KS[ra].n);
-    rv = D.KSid[ra];
-  }
-  int2 v0 = make_int2(-1, -1), v1 = make_int2(-1, -1);
-  int32_t ts0 = 0, ts1 = 0;
-  if (h0) {
-    v0 = D.KSid[te0.y];
-    ts0 = D.KS[te0.y].tstart;
-  }
-  if (h1) {
-    v1 = D.KSid[te1.y];
-    ts1 = D.KS[te1.y].tstart;
-  }
-  dbg_stamp(D, 37);
-  for (int64_t i = t; i < nA + o_n; i += ABLOCK)
-    place_tokens(D, i < nA ? (i == t ? eA : D.L[(int64_t)j * D.LC + i]) : D.Lovf[o_lo + (i - nA)], nid);
-#endif
   dbg_stamp(D, 31);
   // ---- pk of every new pair and its posting-log entry
   const int64_t qbase = (int64_t)j * D.TC;

@@ -25,15 +25,6 @@
 #pragma once
 // (included inside namespace gb)
 
-#ifndef MID_DEFER
-#define MID_DEFER 0  // k_mid_find: a resolved key's count add returns under the pair writes (its
-#endif               // hot-list check after them), not before the round's barrier
-#ifndef MID_PLACE_EARLY
-#define MID_PLACE_EARLY 0  // k_mid_sel's place: 1 = check loads unconditional, 2 = every round (both slower)
-#endif
-#ifndef MID_SPEC
-#define MID_SPEC 0
-#endif
 constexpr int MKC = 1024;   // k_mid_find: new-key dedupe slots per round (LDS)
 constexpr int MPK = 2048;   // appends: key grouping slots (LDS)
 constexpr int MID_APP = 32; // appending workgroups of k_mid_find (hash buckets of the keys)
@@ -288,31 +279,6 @@ __device__ inline int32_t mid_resolve(const Dev& D, u64 h1, u64 h2, int32_t len,
   if (old == 0 || old == k) return (int32_t)s0;
   const u64 s1 = (s0 + 1) & ((u64)D.HC - 1);
   return ht_resolve(D, k, s1, ht_probe(D, s1), claimed);
-}
-
-// MID_SPEC = 1 (A/B; measured slower: default run 32.9 k -> 29.9 k merges/s, k_mid_find 18.2 ->
-// 19.1 us, profiles/r5_s1/): mid_resolve with the key's count (+n) added in the same round trip
-// (one rank): the add to
-// the first slot's count goes out beside the CAS, as k_commit's commit_resolve_counted does --
-// undone when another key holds the slot, whose key then joins the hot list (the undone add
-// may have hidden its theta crossing from the thread that made it)
-__device__ inline int32_t mid_resolve_counted(const Dev& D, HotApp& hot, u64 h1, u64 h2, int32_t len, int32_t n,
-                                              int32_t th, bool* claimed) {
-  const u64 k = probe_key(h1, h2, len);
-  const u64 s0 = ht_first_slot(D, k);
-  const u64 old = atomicCAS((unsigned long long*)&D.ht_key[s0], 0ULL, (unsigned long long)k);
-  const int32_t c0 = atomicAdd(&D.count[s0], n);
-  *claimed = old == 0;
-  if (old == 0 || old == k) {
-    if (th > 0 && c0 < th && c0 + n >= th) hot_push(D, hot, (int32_t)s0);
-    return (int32_t)s0;
-  }
-  atomicAdd(&D.count[s0], -n);
-  if (th > 0) hot_push(D, hot, (int32_t)s0);
-  const u64 s1 = (s0 + 1) & ((u64)D.HC - 1);
-  const int32_t d = ht_resolve(D, k, s1, ht_probe(D, s1), claimed);
-  if (d >= 0) count_add_hot(D, hot, d, n, th);
-  return d;
 }
 
 // a new pair resolved on its own (a run's later occurrence, or the round's table is full)
@@ -623,14 +589,14 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     if (c0 == 0) dbg_stamp(D, 16);
     const int32_t nocc = S.nocc;
     const int64_t xb = D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
-    int32_t def_d = -1, def_old = 0, def_v = 0;  // (MID_DEFER: this thread's first count add)
     for (int32_t q = t; q < nocc; q += ABLOCK) {
       const int32_t s = S.occ[q];
       const int4 rp = S.rep[s];
       bool claimed;
       const u64 h1 = S.h1[s], h2 = S.h2[s];
-      const int32_t d = D.xrec || !MID_SPEC ? mid_resolve(D, h1, h2, rp.x, &claimed)
-                                            : mid_resolve_counted(D, S.hot, h1, h2, rp.x, S.cnt[s], F.th, &claimed);
+      // (round 5 A/Bs, DESIGN 3: the count add beside the CAS, or its hot-list check deferred
+      // under the pair writes, were both slower)
+      const int32_t d = mid_resolve(D, h1, h2, rp.x, &claimed);
       S.did[s] = d;
       if (d < 0) {
         if (D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, 0, -1);  // (no-op record)
@@ -642,18 +608,10 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       } else {
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
-      if (D.xrec) {
+      if (D.xrec)
         mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
-      } else if (!MID_SPEC) {
-        const int32_t v = S.cnt[s];
-        if (MID_DEFER && q == t && v > 0 && F.th > 0) {  // the hot-list check waits for it later
-          def_old = atomicAdd(&D.count[d], v);
-          def_d = d;
-          def_v = v;
-        } else {
-          count_add_hot(D, S.hot, d, v, F.th);
-        }
-      }
+      else
+        count_add_hot(D, S.hot, d, S.cnt[s], F.th);
     }
     // the last round's walks are done, so every decrement is staged: out now, one atomic per
     // key, in flight under the new pairs' grouping and the list flush (at the launch's end they
@@ -674,7 +632,6 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       if (S.h1[sr] != hr.h1) set_error(D, GEOBPE_EHASH, -13);
       if (S.did[sr] >= 0) mid_pair(D, S, F, hr.target, S.did[sr]);
     }
-    if (def_d >= 0 && def_old < F.th && def_old + def_v >= F.th) hot_push(D, S.hot, def_d);
     __syncthreads();
     for (int32_t q = t; q < nocc; q += ABLOCK) {  // clear the round's slots
       const int32_t s = S.occ[q];
@@ -708,8 +665,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       if (k >= 0 && v != 0) mid_put_id(D, j++, k, v);
     }
   } else {  // (the decrements went out with the last round)
-    // (mid_dec_agg: every pair of W is gone; an add, not a store: another key's speculative
-    // add to this slot and its undo may straddle it, mid_resolve_counted)
+    // (mid_dec_agg: every pair of W is gone)
     if (w == 0 && t == 0) atomicAdd(&D.count[F.W], -F.maxc);
   }
   // (the merge's merged total: the next place sums the workgroups' counts into the log)
@@ -991,64 +947,12 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
   // new pair.  (Round 3's version ran the EHASH check's three dependent rounds, a barrier and
   // then the place's own three: this launch's place workgroups set its length.)
   const bool chk = b < D.NBA;  // (then consumed: the next find writes region b afresh)
-#if MID_PLACE_EARLY
-  // (every load of a round unconditional, from clamped indices, as relaxed workgroup-scope atomic
-  // loads the compiler neither sinks into the branch using them nor waits for at a join: round 1
-  // is the check count, the parity and, speculatively, this thread's check record; round 2 the
-  // Sel record, the segment counts and the check key's hashes; round 3 the merged occurrence and
-  // new pair -- written as `if (x) v = load`, the rounds went out as about six round trips)
-  // (atomic loads keep their source order, so each group is written before any value is used)
-  // (the record first: a use of a value loaded before it was scheduled between the loads)
-  const NewPair* reg = D.chk + (int64_t)b * D.RC;
-  const NewPair c0 = ld_now_t(&reg[t < D.RC ? t : 0]);
-  const int32_t nchk_raw = ld_now(&D.chkcnt[b < D.NBA ? b : 0]);
-#if MID_PLACE_EARLY >= 2
-  const int32_t par = ld_now(&st->place_par);
-#else
-  const int32_t par = st->place_par;
-#endif
-  // round 2 (the check count and the record both came in round 1; threads past the count load
-  // slot 0 rather than a stale record's slot; the parity clamped to 0 when no merge is placed)
-  const int32_t nchk = chk ? min(nchk_raw, (int32_t)D.RC) : 0;
-  const bool hc = t < nchk;
-  const int32_t ct = hc ? c0.target : 0;
-  const u64 kh1 = ld_now(&D.kh1[ct]), kh2 = ld_now(&D.kh2[ct]);
-  const int32_t kln = ld_now(&D.klen[ct]);
-#endif
-#if MID_PLACE_EARLY >= 2
-  const int32_t pc = par >= 0 ? par : 0;
-  const int32_t G = mid_G(D);
-  const Sel* sp = D.sel + pc;
-  const int32_t s_dec = ld_now(&sp->decision), s_nid = ld_now(&sp->nid), s_iter = ld_now(&sp->iter);
-  const int4 mc_r = ld_now_t(&D.mcnt[pc * NBA_MAX + (b < G ? b : 0)]);
-  const int64_t nm_r = (int64_t)ld_now((const u64*)&st->mid_nm[pc]);
-  const int64_t nh_r = (int64_t)ld_now((const u64*)&st->mid_nh[pc]);
-  const int32_t v0_r = ld_now(&D.mcnt[pc * NBA_MAX + (t < G ? t : 0)].z);
-  Sel sel;
-  sel.decision = SEL_STALL;
-  sel.nid = 0;
-  sel.iter = 0;
-  int4 mc = make_int4(0, 0, 0, 0);
-  int64_t nms = 0, nhs = 0;
-  int32_t v0 = 0;  // (workgroup 0: the find workgroups' merged counts, summed below)
-  if (par >= 0) {
-    sel.decision = s_dec;
-    sel.nid = s_nid;
-    sel.iter = s_iter;
-    if (b < G) mc = mc_r;
-    nms = min(nm_r, D.TMcap - MSEG_TM);
-    nhs = min(nh_r, D.THcap - MSEG_TH);
-    if (b == 0 && t < G) v0 = v0_r;
-  }
-#else
-#if !MID_PLACE_EARLY
   const int32_t nchk = chk ? min(D.chkcnt[b], (int32_t)D.RC) : 0;
   const int32_t par = st->place_par;
   const NewPair* reg = D.chk + (int64_t)b * D.RC;
   NewPair c0;
   const bool hc = t < nchk;
   if (hc) c0 = reg[t];
-#endif
   const int32_t G = mid_G(D);
   Sel sel;
   sel.decision = SEL_STALL;
@@ -1062,7 +966,6 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
     nhs = min(st->mid_nh[par], D.THcap - MSEG_TH);
     if (b == 0 && t < G) v0 = D.mcnt[par * NBA_MAX + t].z;
   }
-#endif
   const bool go = par >= 0 && sel.decision == SEL_MERGE;  // (block-uniform)
   // find workgroup b's segments (b < G), share b of the spill lists
   const int4* tms = D.TM + (int64_t)b * MTM;
@@ -1072,22 +975,6 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
   const int32_t sm = min(mc.x, MTM), sh = min(mc.y, MTH);
   int4 e = make_int4(0, 0, 0, 0);
   int2 h = make_int2(0, 0);
-#if MID_PLACE_EARLY >= 2
-  if (go) {
-    m0 = nms * b / P;
-    nm = sm + (nms * (b + 1) / P - m0);
-    h0 = nhs * b / P;
-    nh = sh + (nhs * (b + 1) / P - h0);
-  }
-  {
-    const int4* ea = t < sm ? tms + t : D.TM + (MSEG_TM + m0 + t - sm);
-    const int2* ha = t < sh ? ths + t : th + (MSEG_TH + h0 + t - sh);
-    const int4 er = ld_now_t(t < nm ? ea : tms);
-    const int2 hr = ld_now(t < nh ? ha : ths);
-    if (t < nm) e = er;
-    if (t < nh) h = hr;
-  }
-#else
   if (go) {
     m0 = nms * b / P;
     nm = sm + (nms * (b + 1) / P - m0);
@@ -1096,8 +983,6 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
     if (t < nm) e = t < sm ? tms[t] : D.TM[MSEG_TM + m0 + t - sm];
     if (t < nh) h = t < sh ? ths[t] : th[MSEG_TH + h0 + t - sh];
   }
-#endif
-#if !MID_PLACE_EARLY
   u64 kh1 = 0, kh2 = 0;
   int32_t kln = 0;
   if (hc) {
@@ -1105,7 +990,6 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
     kh2 = D.kh2[c0.target];
     kln = D.klen[c0.target];
   }
-#endif
   const int32_t nid = sel.nid;
   auto place_tm = [&](const int4& x) {  // a merged occurrence's token rewrites
     *reinterpret_cast<int2*>(D.tok + x.x) = make_int2(nid, x.y);

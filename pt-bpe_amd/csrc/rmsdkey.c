@@ -33,30 +33,8 @@ static const double TWO_PI = 6.283185307179586; /* 2 * np.pi */
 enum { A_CUR, A_ORIG, A_INIT, A_TOKEN_POS, A_BTT, A_EVENTS, A_N, A_COUNT };
 static const char* ATTR_NAMES[A_COUNT] = {"cur", "orig", "init", "token_pos", "btt", "events", "n"};
 /* RMSDKEY_PROF=1 (a profiling build): nanoseconds per section of merge(), read by prof() */
-#ifndef RMSDKEY_PROF
-#define RMSDKEY_PROF 0
-#endif
-#if RMSDKEY_PROF
-#include <time.h>
-static double g_prof[8];
-static long g_prof_n[8];
-static double now_ns(void) {
-  struct timespec ts;
-  clock_gettime(CLOCK_MONOTONIC, &ts);
-  return ts.tv_sec * 1e9 + ts.tv_nsec;
-}
-#define PROF_T(v) double v = now_ns()
-#define PROF_ADD(i, t0)           \
-  do {                            \
-    double t1_ = now_ns();        \
-    g_prof[i] += t1_ - (t0);      \
-    g_prof_n[i]++;                \
-    t0 = t1_;                     \
-  } while (0)
-#else
 #define PROF_T(v)
 #define PROF_ADD(i, t0)
-#endif
 
 static PyObject* ATTR[A_COUNT];
 static PyObject* PACK_KEYS[9];
@@ -1509,20 +1487,8 @@ done:
   return out;
 }
 
-#if RMSDKEY_PROF
-static PyObject* prof(PyObject* self, PyObject* args) {
-  (void)self;
-  (void)args;
-  PyObject* l = PyList_New(8);
-  for (int i = 0; i < 8; i++) PyList_SET_ITEM(l, i, Py_BuildValue("(dl)", g_prof[i], g_prof_n[i]));
-  return l;
-}
-#endif
 
 static PyMethodDef METHODS[] = {
-#if RMSDKEY_PROF
-                                {"prof", prof, METH_NOARGS, "merge() section times (ns, count)"},
-#endif
                                 {"key", key, METH_VARARGS, "the pair key string of a span (RmsdBPE._pair_key)"},
                                 {"pack", pack, METH_VARARGS, "whole-residue span geometry, geobpe_nerf layout"},
                                 {"reprs", reprs, METH_VARARGS, "repr(float) of each value (test)"},

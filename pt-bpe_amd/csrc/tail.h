@@ -433,67 +433,6 @@ __global__ __launch_bounds__(BLOCK) void k_kp_alloc(Dev D, int from_count) {
   }
 }
 
-// ---- the same lists from a stable radix sort of the live pairs by key (kp_sort.hip; the
-// default build): key runs in slot order, so every pair's place in its list is its offset
-// in its run -- no atomic per pair.  Scratch: keys / slots in and out (R each), the run
-// starts in D.scratch (per key id).
-__global__ __launch_bounds__(BLOCK) void k_kp_keys(Dev D, int32_t* keys, int32_t* vals, int32_t none) {
-  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t d = tok_pk(D, g);
-    keys[g] = d >= 0 ? d : none;
-    vals[g] = (int32_t)g;
-  }
-}
-// run start of key d -> D.scratch[d], run end -> kp_n[d] (k_kp_reset zeroed it)
-__global__ __launch_bounds__(BLOCK) void k_kp_runs(Dev D, const int32_t* keys, int32_t none) {
-  const int64_t n = D.R;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t d = keys[i];
-    if (d == none) continue;
-    if (i == 0 || keys[i - 1] != d) D.scratch[d] = (int32_t)i;
-    if (i + 1 == n || keys[i + 1] != d) D.kp_n[d] = (int32_t)(i + 1);
-  }
-}
-// list space as k_kp_alloc (n + n/2 + 4 per key), n = the key's run length; kp_n = n
-__global__ __launch_bounds__(BLOCK) void k_kp_alloc_runs(Dev D) {
-  __shared__ int32_t s_red[BLOCK / 64];
-  __shared__ int64_t s_base;
-  const int64_t U = min(D.st->U, D.KCAP);
-  const int64_t per = (U + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = (int64_t)blockIdx.x * per, hi = min(U, lo + per);
-  for (int64_t i0 = lo; i0 < hi; i0 += BLOCK) {  // block-uniform
-    const int64_t i = i0 + threadIdx.x;
-    const int32_t d = i < hi ? D.klist[i] : -1;
-    const int32_t end = d >= 0 ? D.kp_n[d] : 0;
-    const int32_t n = end > 0 ? end - D.scratch[d] : 0;
-    const int32_t cap = n > 0 ? n + (n >> 1) + 4 : 0;
-    int32_t tot;
-    const int32_t ex = block_excl_scan(cap, &tot, s_red);
-    if (threadIdx.x == 0) s_base = tot ? (int64_t)atomicAdd((unsigned long long*)&D.st->kpool_used, (unsigned long long)tot) : 0;
-    __syncthreads();
-    if (d >= 0) {
-      const bool fits = s_base + ex + cap <= D.KPOOL;
-      if (!fits) set_error(D, GEOBPE_ECAPACITY, -61);
-      D.kp_off[d] = (int32_t)(s_base + ex);
-      D.kp_cap[d] = fits ? cap : 0;
-      D.kp_n[d] = fits ? n : 0;
-    }
-    __syncthreads();
-  }
-}
-__global__ __launch_bounds__(BLOCK) void k_kp_fill_runs(Dev D, const int32_t* keys, const int32_t* vals, int32_t none) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < D.R; i += (int64_t)gridDim.x * blockDim.x) {
-    const int32_t d = keys[i];
-    if (d == none) continue;
-    const int32_t r = (int32_t)i - D.scratch[d];
-    if (r < D.kp_cap[d]) D.kpool[(int64_t)D.kp_off[d] + r] = vals[i];
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    D.st->kp_valid = 1;
-    D.st->tail_exit = 0;
-  }
-}
-
 __global__ __launch_bounds__(BLOCK) void k_kp_fill(Dev D) {
   for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < D.R; g += (int64_t)gridDim.x * blockDim.x) {
     const int32_t d = tok_pk(D, g);

@@ -82,55 +82,35 @@ def k_medoids(strucs, k, max_iterations: int = 10, tol: float = 1e-4, *, rng=Non
     return k_medoids_from_matrix(rmsd_matrix(strucs, device=device), k, max_iterations, tol, rng=rng)
 
 
-KMED_C = True  # (False: the numpy loop below; tests compare the two)
-
-
 def _keyc():
     from .rmsd_bpe import _KEYC
     return _KEYC
 
 
 def k_medoids_from_matrix(D: np.ndarray, k, max_iterations: int = 10, tol: float = 1e-4, *, rng=None):
-    """The iterations of algo.k_medoids (algo.py:191-213) on a given distance matrix."""
-    N = len(D)
+    """The iterations of algo.k_medoids (algo.py:191-213) on a given distance matrix: the
+    assignment argmin and every cluster's member sums in C (csrc/rmsdkey.c kmed_step, numpy's
+    float32 pairwise summation order and first-minimum rule, so the medoids are the reference's
+    bit for bit; tests compare it with the numpy loop of oracle/rmsd.py), the Generator draws
+    here in the reference's order.  The reference's matrix is float32 (algo.py:179-189): D is
+    taken as float32 once, for the step and the shifts alike."""
+    keyc = _keyc()
+    if keyc is None:
+        raise RuntimeError("the RMSD mode's C extension (_rmsdkey.so) is not built: geobpe.build.build_keys()")
+    Dc = np.ascontiguousarray(D, dtype=np.float32)
+    N = len(Dc)
     k = min(N, k)
     if rng is None:
         rng = np.random.default_rng(None)
     medoid_indices = rng.choice(np.arange(N), size=k, replace=False)
-    assignments = np.zeros(N, dtype=int)
-    keyc = _keyc() if KMED_C else None
-    if keyc is not None:  # (the iteration's assignment and medoid update in C, csrc/rmsdkey.c kmed_step)
-        Dc = np.ascontiguousarray(D, dtype=np.float32)
-        asg = np.zeros(N, dtype=np.int64)
-        for iteration in range(max_iterations):
-            picks = keyc.kmed_step(Dc, [int(m) for m in medoid_indices], asg)
-            total_shift = 0.0
-            new_medoid_indices = []
-            for j in range(k):
-                new_idx = picks[j] if picks[j] >= 0 else rng.integers(N)  # (empty cluster, j order)
-                shift = D[medoid_indices[j], new_idx]
-                total_shift += shift
-                new_medoid_indices.append(new_idx)
-            medoid_indices = new_medoid_indices
-            if total_shift < tol:
-                print(f"Converged in {iteration + 1} iterations with total shift {total_shift:.6f}.")
-                break
-        return medoid_indices
+    asg = np.zeros(N, dtype=np.int64)
     for iteration in range(max_iterations):
-        # (the reference's per-row np.argmin, all rows at once: the same float32 values, the
-        # same first-minimum rule)
-        assignments[:] = np.argmin(D[:, medoid_indices], axis=1)
+        picks = keyc.kmed_step(Dc, [int(m) for m in medoid_indices], asg)
         total_shift = 0.0
         new_medoid_indices = []
         for j in range(k):
-            members = np.where(assignments == j)[0]
-            if members.size == 0:
-                new_idx = rng.integers(N)
-            else:
-                intra = D[np.ix_(members, members)].sum(axis=1)
-                new_idx = members[np.argmin(intra)]
-            shift = D[medoid_indices[j], new_idx]
-            total_shift += shift
+            new_idx = picks[j] if picks[j] >= 0 else rng.integers(N)  # (empty cluster, j order)
+            total_shift += Dc[medoid_indices[j], new_idx]
             new_medoid_indices.append(new_idx)
         medoid_indices = new_medoid_indices
         if total_shift < tol:

@@ -43,6 +43,7 @@ import bisect
 import gc
 import heapq
 import json
+import os
 import time
 from collections import defaultdict
 
@@ -345,15 +346,25 @@ class _RmsdGroup:
     process group, ``True`` for the default one, or an object carrying one as ``.pg``
     (geobpe.dist.TorchGroup)."""
 
-    def __init__(self, group):
+    def __init__(self, group, device: int):
         import torch
         import torch.distributed as dist
         pg = None if group is True else getattr(group, "pg", group)
         self.torch, self.dist, self.pg = torch, dist, pg
         self.rank = dist.get_rank(pg)
         self.world = dist.get_world_size(pg)
-        self.dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(pg) == "nccl" \
-            else torch.device("cpu")
+        # (NCCL gathers on the GPU this rank's batches run on, not torch's current device)
+        self.dev = torch.device("cuda", device) if dist.get_backend(pg) == "nccl" else torch.device("cpu")
+
+    def shared_seed(self):
+        """a seed drawn by rank 0 and broadcast: with seed=None (the reference's default) every
+        rank's Generator must still make the same draws (k-medoids' picks are replicated state)"""
+        box = [int(np.random.SeedSequence().entropy) if self.rank == 0 else None]
+        self.dist.broadcast_object_list(box, src=0, group=self.pg)
+        return box[0]
+
+    def barrier(self):
+        self.dist.barrier(group=self.pg)
 
     def gather_chunks(self, mine: np.ndarray, n: int) -> np.ndarray:
         """The ranks' contiguous chunks [n * r // world, n * (r + 1) // world) of an int64
@@ -382,7 +393,7 @@ class RmsdBPE:
                  compute_sec_structs=False, plot_iou_with_sec_structs=False, res_init=False, std_bonds=True,
                  rmsd_partition_min_size=4, rmsd_super_res=False, rmsd_only=False, num_partitions=3,
                  max_num_strucs=500, glue_opt=False, glue_opt_prior=0.0, glue_opt_every=10,
-                 glue_opt_method="all", seed=None, device: int = 0, group=None, **_unused):
+                 glue_opt_method="all", seed=None, device=None, group=None, **_unused):
         from .bpe import ThresholdDict, structures_to_corpus
         if not isinstance(bins, dict) or 1 not in bins:
             raise KeyError("bins must be a dict with key 1 (quantize/capacity need bins[1], bpe.py:896,909,952)")
@@ -423,8 +434,12 @@ class RmsdBPE:
         self.glue_opt_every = glue_opt_every
         self.glue_opt_method = glue_opt_method
         self.seed = seed
-        self.rng = np.random.default_rng(seed)
+        if device is None:  # (with a process group: this rank's own GPU, torchrun's LOCAL_RANK)
+            device = int(os.environ.get("LOCAL_RANK", 0)) if group is not None else 0
         self.device = int(device)
+        self._group = _RmsdGroup(group, self.device) if group is not None else None
+        self.rng = np.random.default_rng(self._group.shared_seed() if self._group is not None and seed is None
+                                         else seed)
         self.n = len(corpus["row_off"]) - 1
         self._step = 0
         self._times = []
@@ -433,7 +448,6 @@ class RmsdBPE:
         self._chains = []
         self._merge_log = []  # [key, count] of every merge popped, recurring repeats included
         self.assign_calls = 0  # device assignment batches (tests check the GPU path ran)
-        self._group = _RmsdGroup(group) if group is not None else None
 
     # ------------------------------------------------------------ geometry on the device
     def _span_coords(self, spans, orig):
@@ -1398,12 +1412,16 @@ class RmsdBPE:
         return R._new(C["BPE"], attrs)
 
     @classmethod
-    def from_checkpoint(cls, obj, device: int = 0):
+    def from_checkpoint(cls, obj, device: int = 0, group=None):
         """The trained state tokenize() needs, from a checkpoint of this mode (this build's or
         the reference's, read by geobpe.refpickle.load): settings, _thresholds, _tokens,
-        _sphere_dict.  bin/induce.py's RMSD-mode path."""
+        _sphere_dict.  bin/induce.py's RMSD-mode path.  ``group`` as in the constructor (the
+        assignment batches split over the ranks); every attribute __init__ sets is set here too
+        (tests/test_rmsd_mode.py compares the two)."""
         from .bpe import ThresholdDict
         self = cls.__new__(cls)
+        self.device = int(device)
+        self._group = _RmsdGroup(group, self.device) if group is not None else None
         self.bins = dict(obj.bins)
         self.B = int(self.bins[1])
         for k in ("bin_strategy", "res_init", "std_bonds", "rmsd_partition_min_size", "rmsd_super_res",
@@ -1436,9 +1454,12 @@ class RmsdBPE:
         self._tokens = dict(obj._tokens)
         self._sphere_dict = dict(obj._sphere_dict)
         self.num_partitions = getattr(obj, "num_partitions", 3)
-        self.device = int(device)
         self.assign_calls = 0
         self._chains, self._times, self._merge_log, self._step = [], [], [], int(getattr(obj, "_step", 0))
+        self._ious = list(getattr(obj, "_ious", []) or [])
+        self._corpus, self._fnames, self.n = None, None, 0  # (no training corpus: tokenize() brings chains)
+        rng = getattr(obj, "rng", None)  # (the checkpoint's Generator in its saved state, else a fresh one)
+        self.rng = rng if isinstance(rng, np.random.Generator) else np.random.default_rng(self.seed)
         return self
 
     def _grid_only(self, size):
@@ -1478,12 +1499,14 @@ class RmsdBPE:
         import os
 
         from . import refpickle as R
-        if self._group is not None and self._group.rank != 0:
-            return
-        tmp = path + ".tmp"
-        with open(tmp, "wb") as f:
-            R.dump(self.checkpoint_object(), f)
-        os.replace(tmp, path)
+        g = self._group
+        if g is None or g.rank == 0:
+            tmp = path + ".tmp"
+            with open(tmp, "wb") as f:
+                R.dump(self.checkpoint_object(), f)
+            os.replace(tmp, path)
+        if g is not None:  # (no rank returns before the file is there)
+            g.barrier()
 
     def geometry(self):
         """Every chain's current 9 columns, concatenated (the reference's DataFrames)."""

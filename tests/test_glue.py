@@ -239,6 +239,28 @@ def test_device_glue_opt_matches_reference(name):
 
 
 @pytest.mark.gpu
+def test_device_glue_opt_thread_kernel(monkeypatch):
+    """The one-thread-per-chain optimiser (k_glue_opt, selected at run time by
+    GEOBPE_GLUE_THREAD=1; the default is the wave-per-chain k_glue_wave) on the first glue
+    fixture: the same loss at x0, the optimum's loss and its snapped bins within the tolerances
+    the wave kernel is held to."""
+    monkeypatch.setenv("GEOBPE_GLUE_THREAD", "1")
+    name = NAMES[0]
+    rec, (meta, arrs, x0s, outs, stats, loss) = device_opt_record(name)
+    thr = [[tuple(e) for e in arrs["thresholds"][t]] for t in range(3)]
+    env = _envelope(name)[0]
+    flips = [0, 0, 0]
+    for ci, (opt, x0) in enumerate(zip(outs, x0s)):
+        rec_ = meta["lbfgs"][ci]
+        assert abs(loss[ci, 0] - rec_["loss0"]) <= 1e-6 * abs(rec_["loss0"])
+        assert abs(loss[ci, 1] - rec_["loss"]) <= GLUE_LOSS * abs(rec_["loss"])
+        for k, t in zip(*np.nonzero(_snap_all(opt, thr) != _glued(arrs, ci, len(x0) + 1))):
+            flips[t] += 1
+    for t in range(3):
+        assert flips[t] <= _count_bound(env[GLUE_COLS[t]]["other_bin"]), (GLUE_COLS[t], flips)
+
+
+@pytest.mark.gpu
 def test_device_glue_drift_statistics():
     """The device optimiser against the reference's (oracle/glue.py, bit-exact with it) on 120
     synthetic chains, 3462 glues, prior off (tools/glue_drift.py; the oracle's optimum is

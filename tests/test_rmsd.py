@@ -37,16 +37,11 @@ def test_k_medoids_loop_matches_reference(ref):
 
 
 def _kmed_both(D, k, seed, max_iterations=10):
+    """the numpy loop of oracle/rmsd.py and the product's C step, from the same seed"""
     from geobpe import rmsd
-    out = []
-    for c in (False, True):
-        rmsd.KMED_C = c
-        try:
-            out.append([int(x) for x in rmsd.k_medoids_from_matrix(D, k, max_iterations,
-                                                                   rng=np.random.default_rng(seed))])
-        finally:
-            rmsd.KMED_C = True
-    return out
+    from oracle import rmsd as orm
+    return [[int(x) for x in f(D, k, max_iterations, rng=np.random.default_rng(seed))]
+            for f in (orm.k_medoids_from_matrix, rmsd.k_medoids_from_matrix)]
 
 
 def test_k_medoids_c_step_equals_numpy_loop(ref):
@@ -54,9 +49,6 @@ def test_k_medoids_c_step_equals_numpy_loop(ref):
     gives the numpy loop's medoids: the reference's matrices, random ones of every size the
     summation splits differently (below 8, up to 128, halves above), tied and quantised
     values, empty clusters (rng re-seeds) and a NaN."""
-    from geobpe import rmsd
-    if rmsd._keyc() is None:
-        pytest.skip("_rmsdkey.so not built")
     for D, k, s in ((ref["D_ref"], 5, 3), (ref["D3_ref"], 4, 5)):
         a, b = _kmed_both(D, k, s)
         assert a == b
