@@ -92,11 +92,16 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=990)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="c3", choices=sorted(CONFIGS) + ["rmsd"],
+                    help="rmsd: the RMSD-partitioned mode in the README's downstream setting (bench_rmsd)")
+    ap.add_argument("--rmsd-chains", type=int, default=2000, help="--config rmsd: synthetic chains")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-exchange", action="store_true",
                     help="run the multi-rank exchange (RCCL) even at world size 1: a 1-GPU rehearsal of the N>1 path")
     ap.add_argument("--cpu-budget-s", type=float, default=30.0)
+    ap.add_argument("--shard-of", type=int, default=1,
+                    help="rehearsal at world size 1: run rank 0's shard of an N-way row sharding (the work one "
+                         "rank of N does per merge; DESIGN 5's N > 1 prediction), not the whole corpus")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: RCCL (default); gloo puts every rank on GPU 0 (a one-GPU rehearsal of the N > 1 path)")
     ap.add_argument("--no-profile", action="store_true", help="skip the per-kernel HIP-event timing")
@@ -134,8 +139,80 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+def bench_rmsd(args):
+    """--config rmsd: the RMSD-partitioned mode (geobpe/rmsd_bpe.py) in the
+    README's suggested downstream setting (README.md:45, scripts/encode.sh): bins {1: 50}, histogram,
+    rmsd_partition_min_size 0, --num-p 2-2:3-5:5-1:6-2:8-1, max_num_strucs 500, free bonds,
+    rmsd_super_res, glue optimisation ("all", prior 0, every 10 steps).  Synthetic chains of the C3
+    length law (U{40..560}, seed 0), since the PDB pretrain set is not here.  A step is one
+    BPE.step() (bpe.py:1792-2166: a merge, its occurrences' k-medoids partition and assignment, the
+    neighbour keys, every 10th step the glue re-optimisation); W untimed steps, then K timed.
+    Per phase: initialize (thresholds, residue partitions), glue_opt_all, bin, the steps -- each
+    split into the device batches (NeRF, Kabsch RMSD matrices / assignments, L-BFGS glue launches,
+    timed by wrapping their entry points; each returns its result to the host) and the host
+    bookkeeping (the rest)."""
+    import torch
+    from geobpe import glue, rmsd, synth
+    from geobpe.bpe import BPE
+    torch.cuda.set_device(0)
+    n = args.rmsd_chains
+    corpus = synth.make_corpus(synth.make_lengths(n, 40, 560, seed=0), seed=0)
+    dev = {"s": 0.0, "calls": 0}
+    for mod, names in ((rmsd, ("nerf_atoms", "nerf_packed", "geo_coords", "rmsd_matrix", "rmsd_cross")),
+                       (glue, ("optimize_chains", "exit_frames"))):
+        for name in names:
+            f = getattr(mod, name)
+
+            def timed(*a, _f=f, **k):
+                t0 = time.perf_counter()
+                r = _f(*a, **k)
+                dev["s"] += time.perf_counter() - t0
+                dev["calls"] += 1
+                return r
+            setattr(mod, name, timed)
+    bpe = BPE(corpus, bins={1: 50}, bin_strategy="histogram", res_init=True, std_bonds=False,
+              rmsd_partition_min_size=0, rmsd_super_res=True, num_partitions={2: 2, 3: 5, 5: 1, 6: 2, 8: 1},
+              max_num_strucs=500, glue_opt=True, glue_opt_prior=0.0, glue_opt_every=10, glue_opt_method="all",
+              seed=0, device=0)
+    phases = {}
+
+    def phase(name, fn):
+        d0, t0 = dev["s"], time.perf_counter()
+        r = fn()
+        T = time.perf_counter() - t0
+        phases[name] = {"s": round(T, 4), "device_s": round(dev["s"] - d0, 4), "host_s": round(T - (dev["s"] - d0), 4)}
+        return r
+    phase("initialize", bpe.initialize)
+    phase("glue_opt_all", bpe.glue_opt_all)
+    phase("bin", bpe.bin)
+    phase("warmup_steps", lambda: bpe.run(args.warmup))
+    d0, c0 = dev["s"], dev["calls"]
+    t0 = time.perf_counter()
+    done = bpe.run(args.steps)
+    T = time.perf_counter() - t0
+    dsec = dev["s"] - d0
+    out = {
+        "metric": "RMSD-mode BPE merge iters/sec (README downstream setting, synthetic chains)",
+        "value": round(done / T, 3) if T > 0 else None, "unit": "merges/s", "n_gpus": 1, "steps": done,
+        "warmup": args.warmup, "ms_per_step": round(1000 * T / max(done, 1), 3), "higher_is_better": True,
+        "scaling": "none", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"RMSD-partitioned mode, README.md:45 setting: {n} synthetic chains, len U{{40..560}}, "
+                               f"{int(corpus['row_off'][-1])} residues, bins {{1: 50}}, p_min_size 0, num_p "
+                               "2-2:3-5:5-1:6-2:8-1, max_num_strucs 500, free bonds, rmsd_super_res, glue opt all "
+                               f"(prior 0, every 10), steps {args.warmup + 1}..{args.warmup + done}",
+                   "chains": n, "residues": int(corpus["row_off"][-1])},
+        "steps_split": {"device_s": round(dsec, 4), "host_s": round(T - dsec, 4),
+                        "device_share": round(dsec / T, 4) if T > 0 else None, "device_calls": dev["calls"] - c0},
+        "phases": phases,
+        "final": {"vocab_size": bpe.vocab_size, "merges": len(bpe._merge_log)},
+    }
+    print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.config == "rmsd":
+        return bench_rmsd(args)
     if args.gpus < 1:
         sys.exit("--gpus must be >= 1")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -172,9 +249,13 @@ def main():
     t_gen = time.time() - t0
     shard = corpus
     group = None
-    if world > 1 or args.force_exchange:
-        lo_r, hi_r = shard_rows(corpus["row_off"], world)[rank]
+    if args.shard_of > 1 and world == 1:  # (one rank's share of an N-way run, alone on the GPU)
+        lo_r, hi_r = shard_rows(corpus["row_off"], args.shard_of)[0]
         shard = slice_corpus(corpus, lo_r, hi_r)
+    if world > 1 or args.force_exchange:
+        if world > 1:
+            lo_r, hi_r = shard_rows(corpus["row_off"], world)[rank]
+            shard = slice_corpus(corpus, lo_r, hi_r)
         group = TorchGroup(int(shard["row_off"][-1]), device=local)
         group.force = args.force_exchange
     eng = GeoBPEEngine(shard, B, device=local, group=group, max_vocab=1 << 20)
@@ -418,7 +499,10 @@ def main():
                                 f"bins {{1: {B}}}, merges {args.warmup + 1}..{args.warmup + done}")
                    if args.config in ("c3", "c5") else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
                    "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}",
-                   "rank_residues": rank_res, "backend": (args.dist_backend if world > 1 else None)},
+                   "rank_residues": rank_res, "backend": (args.dist_backend if world > 1 else None),
+                   **({"shard_of": args.shard_of} if args.shard_of > 1 else {}),
+                   **({"exchange": "rehearsal (world 1)" + (", all-gather" if os.environ.get("GEOBPE_PEER") == "0"
+                                                             else ", peer")} if args.force_exchange else {})},
         "roofline": roofline,
         "roofline_other": roofline_other,
         "cpu_baseline": cpu,

@@ -313,6 +313,15 @@ typedef int (*geobpe_allgather_fn)(void *user, const void *send, void *recv, int
 int geobpe_comm_set_callback(geobpe_ctx *ctx, geobpe_allgather_fn fn, void *user, int32_t nranks, int32_t rank);
 /* Fixed slot size in records (0 = sized from the last import; tests force stalls with it). */
 int geobpe_comm_set_slot(geobpe_ctx *ctx, int64_t records);
+/* The peer exchange (default on for up to 8 ranks; off: the all-gather of fixed slots): every
+ * rank's receive area is IPC-mapped into every other rank once, the merge kernels store their
+ * delta records straight into the peers' areas and publish a {count, seq} header, the stream
+ * waits for the peers' headers (hipStreamWaitValue32) and the next select launch imports them.
+ * GEOBPE_PEER=0 in the environment turns it off too.  Set before the first geobpe_run_exchange.
+ * (No reference counterpart: the reference has no multi-GPU path) */
+int geobpe_comm_peer(geobpe_ctx *ctx, int on);
+/* 1 when geobpe_run_exchange runs the peer exchange (set up and agreed on by every rank). */
+int geobpe_comm_peer_active(geobpe_ctx *ctx);
 /* At the middle-regime switch (the winner's global count <= geobpe_set_mid's threshold),
  * geobpe_run_exchange stops sharding: every rank gathers every rank's token records once,
  * re-keys them in its own key table and continues as the one-rank loop over the whole corpus
@@ -323,10 +332,19 @@ int geobpe_set_collapse(geobpe_ctx *ctx, int on);
 /* 1 once the engine has collapsed (then geobpe_step / geobpe_run drive it, as one rank). */
 int geobpe_collapsed(geobpe_ctx *ctx);
 /* n_merges merges of the row-sharded N > 1 loop with no host wait per merge: per iteration
- * the merge kernels and the slot export, one all-gather of the fixed slots on the engine's
- * stream, the import; polls every few iterations; a merge whose records overflowed a slot
- * is re-exchanged in full.  *n_done = merges made. */
+ * the merge kernels and the records' exchange (the peer exchange above, or the slot export,
+ * one all-gather of the fixed slots on the engine's stream and the import); polls every few
+ * iterations; a merge whose records overflowed a slot is re-exchanged in full.  A rank runs
+ * the middle regime once its share of the winner's count (count / nranks) is below the
+ * geobpe_set_mid threshold; the collapse comes below GEOBPE_COLLAPSE_AT (32768) with the peer
+ * exchange, below the threshold itself without it.  *n_done = merges made. */
 int geobpe_run_exchange(geobpe_ctx *ctx, int64_t n_merges, int64_t *n_done);
+/* geobpe_run_exchange with the run's merge records ({new id, count, merged occurrences} per merge,
+ * as geobpe_run_log; the reference's BPE._tokens / step log, bpe.py:1857-1866) pulled inside the
+ * run's last synchronisation.  *first = the run's first merge index, or -1 when the run went on
+ * in the one-rank loop after a collapse (geobpe_merge_log then has them). */
+int geobpe_run_exchange_log(geobpe_ctx *ctx, int64_t n_merges, int64_t *n_done, int64_t *first, int64_t *h_out,
+                            int64_t cap);
 
 #ifdef __cplusplus
 }

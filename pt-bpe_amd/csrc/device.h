@@ -18,8 +18,10 @@ constexpr u64 KMIX = 0x9E3779B97F4A7C15ULL;
 constexpr double TWO_PI = 6.283185307179586;  // 2*np.pi
 constexpr int BLOCK = 256;
 constexpr int ABLOCK = 1024;  // region kernels (bin pairs, finalize, apply, import): 16 waves per CU
-constexpr int CL_MIN_SHRINK = 4096;
-constexpr int PIPE_MAX_WORLD = 64;   // ranks of a pipelined exchange  // hot-list length above which a 4x drop of theta re-scans
+constexpr int CL_MIN_SHRINK = 4096;  // hot-list length above which a 4x drop of theta re-scans
+constexpr int PIPE_MAX_WORLD = 64;  // ranks of a pipelined exchange
+constexpr int XPEER_MAX = 8;        // peer exchange: ranks (one node)
+constexpr int XHDR = 64;            // peer exchange: slot header bytes {int64 count, int32 seq}
 constexpr int NBKT_LOG2 = 14;        // key buckets of the posting index (per region)
 constexpr int NBKT = 1 << NBKT_LOG2;
 constexpr int SKIP_HOT = 1, SKIP_MEASURE = 4;  // what a rebuild iteration does
@@ -86,6 +88,15 @@ struct State {
   int64_t mid_nm[2], mid_nh[2];  // mid.h: merged occurrences / new pairs of k_mid_find, by launch parity
   int32_t place_par_prev;        // mid.h: parity of the merge whose new pairs the next find appends (-1: none)
   int32_t pad6;
+  // peer exchange (Dev.xw > 0, exchange.h): the producer launch's last workgroup to arrive
+  // publishes its record count; the next select launch's import workgroups take every rank's
+  // records and the select workgroup waits for them
+  int32_t xarr;   // producer workgroups arrived
+  int32_t xiarr;  // import workgroups arrived
+  int32_t xpend;  // 1: records published and not yet imported
+  int32_t xppar;  // their receive-slot parity
+  int64_t xpcnt;  // this rank's record count of them
+  int32_t xpseq, pad7;
 };
 
 // The decision of one k_mark launch (its workgroup 0 writes Sel[parity]; k_apply
@@ -224,6 +235,17 @@ struct Dev {
   // into the slot header, which is then final when k_mid_find ends (no header pass)
   int64_t* xcnt;
   int2* xovf;  // (key, delta) of the rare unstaged adds of a pipelined iteration
+  // peer exchange (geobpe_comm_peer; exchange.h): every record j < xcapf is also stored straight
+  // into rank q's receive area (xpeer[q]: IPC-mapped, over xGMI on a node; this launch's parity
+  // half) at the slot of this rank; xrecv = this rank's own area (parity 0).  xw = 0: off
+  uint8_t* xpeer[XPEER_MAX];
+  uint8_t* xrecv;
+  int64_t xslot, xcapf;  // bytes per source slot (XHDR + xcapf records), records per slot
+  int32_t xw, xme;       // ranks, this rank
+  int32_t xseq, xpar;    // this launch's sequence number and slot parity
+  NewPair* xchk;         // per import workgroup: the keys its import found (not claimed), checked
+  int32_t* xchkcnt;      // against their stored content by the next import (EHASH; exchange.h)
+  int64_t xchkcap;
   int64_t ovf_cap;
   // late-merge path (tail.h): key d's posting list is kpool[kp_off[d] .. + kp_n[d]) (capacity
   // kp_cap[d]; entries whose token no longer carries the key are skipped); per-merge scratch
@@ -465,6 +487,31 @@ __device__ inline void global_add(const Dev& D, int32_t d, int32_t v, bool to_de
   if (atomicAdd(&D.dcount[d], v) == 0) touched_append(D, d);
 }
 
+// delta record j of this rank: its local list (xrec: what a stalled merge's full re-exchange
+// reads) and, with the peer exchange, rank q's receive slot of this rank for every other q --
+// direct stores into the peer's memory, no collective (j < xcapf; a count past it stalls the
+// pipeline on every rank and the merge is re-exchanged in full)
+__device__ __attribute__((always_inline)) inline void x_put_rec(const Dev& D, int64_t j, const DeltaRec& r, int32_t err) {
+  if (j >= D.xcap) {
+    set_error(D, GEOBPE_ECAPACITY, err);
+    return;
+  }
+  D.xrec[j] = r;
+  if (D.xw > 1 && j < D.xcapf) {
+    const unsigned long long* v = reinterpret_cast<const unsigned long long*>(&r);
+#pragma unroll
+    for (int q = 0; q < XPEER_MAX; q++) {  // (static indices: a runtime index into the kernel-argument
+      if (q >= D.xw || q == D.xme) continue;  // array copies the whole Dev to scratch)
+      // written through to the peer's memory (system-scope stores: no dirty line left in this
+      // XCD's L2, so the producer's end needs no L2 write-back before the header)
+      unsigned long long* o =
+          reinterpret_cast<unsigned long long*>(reinterpret_cast<DeltaRec*>(D.xpeer[q] + (int64_t)D.xme * D.xslot + XHDR) + j);
+#pragma unroll
+      for (int i = 0; i < 5; i++) __hip_atomic_store(o + i, v[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 // pipelined exchange, k_commit's rare unstaged adds: a delta record straight into the
 // rank's slot (one reservation per wave instruction on the record counter)
 __device__ inline void rec_add(const Dev& D, int32_t d, int32_t v) {
@@ -485,10 +532,7 @@ __device__ inline void rec_add(const Dev& D, int32_t d, int32_t v) {
   r.idR = D.krep[3 * (int64_t)d + 2];
   r.delta = v;
   r.pad = d + 1;
-  if (j < D.xcap)
-    D.xrec[j] = r;
-  else
-    set_error(D, GEOBPE_ECAPACITY, -33);
+  x_put_rec(D, j, r, -33);
 }
 
 // rank-local deltas of one workgroup whose keys join the touched list: buffered in

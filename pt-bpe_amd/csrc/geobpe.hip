@@ -121,6 +121,24 @@ struct geobpe_ctx {
   uint8_t *x_hsend = nullptr, *x_hrecv = nullptr;  // (host callback: pinned staging)
   int64_t x_hbytes = 0;
   int64_t x_ahead = 1, x_capf = 1024, x_fixed = 0;  // poll window and slot size carry over between runs
+  // peer exchange (exchange.h; geobpe_comm_peer): this rank's receive area (2 parities x
+  // x_world slots), every rank's area as mapped here (IPC handles; [x_rank] = x_recv), the
+  // host's count of producer launches (each launch's sequence number, the same on every rank)
+  bool x_peer_want = true, x_peer_ready = false, x_pending = false, x_cpwait = true;
+  uint8_t* x_recv = nullptr;
+  uint8_t* x_peers[XPEER_MAX] = {};
+  int64_t x_slot = 0, x_rcapf = 0;
+  int64_t x_hseq = 1, x_prev_seq = 0;
+  LogRec* x_hlog = nullptr;  // (pinned: a batch's merge records, pulled with its poll)
+  int32_t* x_hbeg = nullptr; // (pinned: dgen / stall for a pipeline begin without a synchronisation)
+  int64_t enq = 0, enq_synced = -1;  // merge iterations enqueued; the count at the last state sync
+  double x_decay = 0;        // the winner count's decay per merge over the last batch (0: unknown)
+  LogRec x_last{};           // the last merge's record seen by an exchange run's poll, and its index
+  int64_t x_last_i = -1;
+  NewPair* x_chk = nullptr;  // the imports' found keys, checked by the next import (exchange.h)
+  int32_t* x_chkcnt = nullptr;
+  int64_t x_chkcap = 0;
+  int64_t x_collapse_at = 32768;  // the sharded loop collapses below this count (GEOBPE_COLLAPSE_AT)
   // collapse at the middle-regime switch (geobpe_set_collapse): every rank then holds the whole
   // corpus and runs the one-rank loop; its own rows are [own_row0, own_row1) of it
   bool collapse_on = true, collapsed = false;
@@ -292,7 +310,7 @@ void flush_place(geobpe_ctx* c) {
   c->place_pending = false;
   Timed t(c, "place");
   if (c->place_mid) {  // token rewrites, then the posting entries, then nothing is pending
-    hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, c->D, INT32_MIN, 0);
+    hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, c->D, INT32_MIN, 0, 0);
     hipLaunchKernelGGL(k_mid_find, dim3(MID_APP), dim3(ABLOCK), 0, c->stream, c->D, (int)(c->gen & 1), 0, 0);
     hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, c->D);
   } else {
@@ -304,6 +322,7 @@ int sync_state(geobpe_ctx* c) {
   flush_place(c);
   HIPCHK(c, hipMemcpyAsync(c->h_state, c->D.st, sizeof(State), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  c->enq_synced = c->enq;  // (h_state holds the state after every iteration enqueued so far)
   return check_device_error(c);
 }
 
@@ -376,6 +395,7 @@ void enqueue_commit(geobpe_ctx* c, bool to_delta) {
 // k_apply, on launch parity gen & 1 (the double-buffered Sel record and
 // merge-overflow counter)
 void enqueue_select(geobpe_ctx* c) {
+  c->enq++;
   if (c->replay) {
     flush_place(c);
     Timed t(c, "select");
@@ -386,7 +406,7 @@ void enqueue_select(geobpe_ctx* c) {
   if (c->place_pending && c->place_mid) flush_place(c);
   const int grid = c->place_pending ? 1 + c->nba : 1;  // (+ the previous merge's k_place in workgroups 1..nba)
   c->place_pending = false;
-  LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, (int)(c->gen & 1), c->run_end);
+  LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, (int)(c->gen & 1), c->run_end, grid > 1 ? 1 : 0, 0);
 }
 void enqueue_mark(geobpe_ctx* c) {
   LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
@@ -408,12 +428,13 @@ void enqueue_iteration(geobpe_ctx* c) {
 
 // one merge iteration of the middle regime (mid.h): select (+ the previous place) -> find
 void enqueue_iteration_mid(geobpe_ctx* c) {
+  c->enq++;
   const int par = (int)(c->gen & 1);
   {
     const bool carry = c->place_pending && c->place_mid;  // (+ the previous merge's token rewrites in workgroups 1..nba)
     if (c->place_pending && !c->place_mid) flush_place(c);
     c->place_pending = false;
-    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->D, par, c->run_end);
+    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(carry ? 1 + c->nba : 1), dim3(ABLOCK), 0, c->D, par, c->run_end, 0);
   }
   {
     const int G = c->nba - MID_APP;  // (+ the previous merge's posting entries in MID_APP more workgroups)
@@ -497,6 +518,7 @@ void tail_build(geobpe_ctx* c) {
 // up to n merges in k_tail (one workgroup, one launch for many merges); a hot-list rebuild
 // or the end is run by k_commit on the parity the tail stopped at; stale lists are rebuilt
 int tail_run(geobpe_ctx* c, int64_t n) {
+  c->enq++;
   int rc;
   if ((rc = tail_alloc(c)) || (rc = sync_state(c))) return rc;
   const int32_t it0 = c->h_state->iter;
@@ -635,6 +657,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   }
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
+  if (const char* e = getenv("GEOBPE_COLLAPSE_AT")) c->x_collapse_at = atoll(e);  // (A/B: the collapse count)
   if (const char* e = getenv("GEOBPE_SPEC")) c->spec = std::max(0, atoi(e));  // (A/B: 0 = no idle iterations)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
@@ -655,10 +678,15 @@ void geobpe_destroy(geobpe_ctx* c) {
   if (c->h_state) hipHostFree(c->h_state);
   if (c->h_sel) hipHostFree(c->h_sel);
   if (c->h_log) hipHostFree(c->h_log);
+  for (int q = 0; q < XPEER_MAX; q++)  // (the peers' areas, mapped here by IPC handle)
+    if (c->x_peers[q] && c->x_peers[q] != c->x_recv) hipIpcCloseMemHandle(c->x_peers[q]);
+  if (c->x_recv) hipFree(c->x_recv);
   if (c->comm && c->rccl.CommDestroy) c->rccl.CommDestroy(c->comm);
   for (uint8_t* p : {c->x_pbuf, c->x_gath, c->x_tmp, c->x_flat})
     if (p) hipFree(p);
   if (c->x_hsend) hipHostFree(c->x_hsend);
+  if (c->x_hlog) hipHostFree(c->x_hlog);
+  if (c->x_hbeg) hipHostFree(c->x_hbeg);
   if (c->x_hrecv) hipHostFree(c->x_hrecv);
   for (auto e : c->evall) hipEventDestroy(e);
   if (c->own_stream) hipStreamDestroy(c->stream);
@@ -1279,11 +1307,27 @@ int geobpe_delta_export_async(geobpe_ctx* c, void* d_out, int64_t cap, void* d_c
 // records), a collective by the caller, and the import of the gathered slots.
 // A slot that overflowed stalls every pipelined kernel until the host resolves
 // that merge with a sized exchange; the host polls every few iterations.
-int geobpe_pipeline_begin(geobpe_ctx* c) {
+}  // extern "C"
+namespace {
+// the pipeline's start: the device's parity counter from the host's, no stall.  lite: without a
+// synchronisation when the host state is current (no iteration enqueued since the last sync) --
+// the two writes then go out from a pinned pair, stream-ordered before the first select
+int pipeline_begin_impl(geobpe_ctx* c, bool lite) {
   if (!c || !c->distributed || !c->keys_ready) return GEOBPE_EARG;
   if (c->mark_pending) return fail(c, GEOBPE_EARG, "pipeline_begin between step_select and step_apply");
   HIPCHK(c, hipSetDevice(c->device));
   int rc;
+  if (lite && !c->x_hbeg) HIPCHK(c, hipHostMalloc((void**)&c->x_hbeg, 2 * sizeof(int32_t), hipHostMallocDefault));
+  if (lite && c->enq == c->enq_synced && !c->place_pending) {
+    c->x_hbeg[0] = (int32_t)c->gen - 1;
+    c->x_hbeg[1] = 0;
+    c->h_state->dgen = c->x_hbeg[0];
+    c->h_state->stall = 0;
+    HIPCHK(c, hipMemcpyAsync(&c->D.st->dgen, &c->x_hbeg[0], 4, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(&c->D.st->stall, &c->x_hbeg[1], 4, hipMemcpyHostToDevice, c->stream));
+    c->pipelined = true;
+    return 0;
+  }
   if ((rc = sync_state(c))) return rc;
   c->h_state->dgen = (int32_t)c->gen - 1;  // the next device iteration takes parity gen & 1
   c->h_state->stall = 0;
@@ -1293,9 +1337,87 @@ int geobpe_pipeline_begin(geobpe_ctx* c) {
   c->pipelined = true;
   return 0;
 }
+}  // namespace
+extern "C" {
 
-int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
-  if (!c || !c->pipelined || !d_buf) return GEOBPE_EARG;
+int geobpe_pipeline_begin(geobpe_ctx* c) { return pipeline_begin_impl(c, false); }
+
+}  // extern "C"
+namespace {
+// geobpe_pipeline_end when the last poll has synchronised everything (nothing enqueued since)
+int pipeline_end_lite(geobpe_ctx* c) {
+  if (c->h_state->stall) return fail(c, GEOBPE_EARG, "pipeline_end while stalled");
+  c->gen = (int64_t)c->h_state->dgen + 1;  // host parity continues the device's
+  c->pipelined = false;
+  return 0;
+}
+}  // namespace
+extern "C" {
+
+}  // extern "C"
+namespace {
+
+// the peer exchange's view of producer launch h (exchange.h): every rank's receive area at
+// parity h & 1 as mapped here, the launch's sequence number
+Dev x_peer_dev(const geobpe_ctx* c, Dev D, int64_t h) {
+  D.xw = c->x_world;
+  D.xme = c->x_rank;
+  D.xrecv = c->x_recv;
+  D.xslot = c->x_slot;
+  D.xcapf = c->x_rcapf;
+  D.xseq = (int32_t)h;
+  D.xpar = (int32_t)(h & 1);
+  D.xchk = c->x_chk;
+  D.xchkcnt = c->x_chkcnt;
+  D.xchkcap = c->x_chkcap;
+  for (int q = 0; q < c->x_world; q++) D.xpeer[q] = c->x_peers[q] + (h & 1) * c->x_world * c->x_slot;
+  return D;
+}
+
+// before the import of the last producer launch (the next select launch, or the drain): the
+// stream waits until every peer's slot header carries that launch's sequence number -- on the
+// command processor (hipStreamWaitValue32), or where the device lacks it a one-wave kernel
+// with a bounded spin
+__global__ void k_xwait(Dev D, int32_t par, int32_t seq) {
+  const int q = threadIdx.x;
+  if (q >= D.xw || q == D.xme) return;
+  const XHdr* h = x_hdr(D.xrecv + (int64_t)par * D.xw * D.xslot, D.xslot, q);
+  const uint64_t t0 = wall_clock64();
+  // (relaxed system-scope loads in the loop -- they miss the caches -- and one acquire after it:
+  // an acquire per iteration would invalidate this XCD's L2 under everything else running)
+  while (__hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+    __builtin_amdgcn_s_sleep(2);
+    if (wall_clock64() - t0 > (uint64_t)200000000) {  // (~2 s: a peer that never publishes)
+      set_error(D, GEOBPE_ESTATE, -83);
+      D.st->stall = 1;
+      return;
+    }
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+}
+int x_wait_prev(geobpe_ctx* c, const Dev& D) {
+  if (!c->x_pending || c->x_world < 2) return 0;
+  const int64_t par = c->x_prev_seq & 1;
+  if (!c->x_cpwait) {
+    hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, c->stream, D, (int32_t)par, (int32_t)c->x_prev_seq);
+    HIPCHK(c, hipGetLastError());
+    return 0;
+  }
+  for (int q = 0; q < c->x_world; q++) {
+    if (q == c->x_rank) continue;
+    void* seqp = c->x_recv + (par * c->x_world + q) * c->x_slot + offsetof(XHdr, seq);
+    HIPCHK(c, hipStreamWaitValue32(c->stream, seqp, (uint32_t)c->x_prev_seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
+  }
+  return 0;
+}
+
+// the select launch's import workgroups: the place workgroups that share the chip with the
+// select workgroup (one 1024-thread workgroup per CU: the launch's last one waits for a CU)
+int x_nimp(const geobpe_ctx* c) { return std::max(1, c->nba - 1); }
+
+// one pipelined iteration (geobpe_pipeline_iter); peer: the engine's peer exchange
+int pipeline_iter_impl(geobpe_ctx* c, void* d_buf, int64_t cap_total, bool peer, int32_t run_end = 0) {
+  c->enq++;
   Dev D = c->D;  // find and commit write this rank's delta records into the slot buffer
   D.xrec = reinterpret_cast<DeltaRec*>(d_buf) + 1;  // record 0 is the slot header
   D.xcap = cap_total;
@@ -1305,10 +1427,20 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     c->x_head = head;
   }
   D.xcnt = head;  // the records are counted in the slot header: final when the iteration's last kernel ends
+  int nimp = 0;
+  if (peer) {
+    const int64_t h = c->x_hseq++;
+    int rc;
+    if ((rc = x_wait_prev(c, x_peer_dev(c, D, c->x_prev_seq)))) return rc;
+    D = x_peer_dev(c, D, h);
+    nimp = x_nimp(c);
+    c->x_pending = true;  // (this launch's headers: the next select launch or the drain waits for them)
+    c->x_prev_seq = h;
+  }
   if (c->mid_on && mid_enabled(c)) {  // the middle regime (mid.h), device parity
     if (c->place_pending && !c->place_mid) flush_place(c);
     c->place_pending = false;
-    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, D, -1, 0);
+    LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, D, -1, run_end, nimp);
     LAUNCH_T(c, "mid_find", k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, D, -1, c->nba - MID_APP, 1);
     c->place_pending = true;
     c->place_mid = true;
@@ -1317,9 +1449,10 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
   }
   if (c->place_pending && c->place_mid) flush_place(c);
   {
-    const int grid = c->place_pending ? 1 + c->nba : 1;  // (+ the previous merge's k_place)
+    const bool place = c->place_pending;  // (+ the previous merge's k_place)
+    const int grid = place || nimp ? 1 + c->nba : 1;
     c->place_pending = false;
-    LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, c->D, -1, 0);
+    LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, D, -1, run_end, place ? 1 : 0, nimp);
   }
   LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
   LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
@@ -1328,6 +1461,39 @@ int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);
   HIPCHK(c, hipGetLastError());
   return 0;
+}
+
+// the last producer launch's records imported on their own (the end of a batch: the host then
+// sees complete counts at its poll)
+int x_drain(geobpe_ctx* c) {
+  if (!c->x_peer_ready || !c->x_pending) return 0;
+  Dev D = x_peer_dev(c, c->D, c->x_prev_seq);
+  D.xrec = reinterpret_cast<DeltaRec*>(c->x_pbuf) + 1;
+  D.xcap = c->x_pcap;
+  D.xcnt = reinterpret_cast<int64_t*>(c->x_pbuf);
+  int rc;
+  if ((rc = x_wait_prev(c, D))) return rc;
+  {
+    Timed t(c, "xdrain");
+    hipLaunchKernelGGL(k_xdrain, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D);
+  }
+  HIPCHK(c, hipGetLastError());
+  c->x_pending = false;
+  return 0;
+}
+
+// every import region's found keys checked (the end of a peer-exchange run, or its collapse)
+void x_check_all(geobpe_ctx* c) {
+  Dev D = x_peer_dev(c, c->D, c->x_prev_seq);
+  hipLaunchKernelGGL(k_xcheck, dim3(c->nba), dim3(ABLOCK), 0, c->stream, D);
+}
+
+}  // namespace
+extern "C" {
+
+int geobpe_pipeline_iter(geobpe_ctx* c, void* d_buf, int64_t cap_total) {
+  if (!c || !c->pipelined || !d_buf) return GEOBPE_EARG;
+  return pipeline_iter_impl(c, d_buf, cap_total, false);
 }
 
 int geobpe_pipeline_import(geobpe_ctx* c, const void* d_slots, int32_t world, int64_t cap_fixed) {
@@ -1361,6 +1527,7 @@ int geobpe_pipeline_resolve(geobpe_ctx* c, const void* d_in, int64_t n_records) 
   int rc;
   if ((rc = delta_import(c, d_in, n_records))) return rc;
   if (c->x_head) HIPCHK(c, hipMemsetAsync(c->x_head, 0, 8, c->stream));  // (the stalled merge's count, consumed)
+  HIPCHK(c, hipMemsetAsync(&c->D.st->xpend, 0, 4, c->stream));            // (peer exchange: nothing pending)
   HIPCHK(c, hipMemsetAsync(&c->D.st->stall, 0, 4, c->stream));
   return sync_state(c);
 }
@@ -2157,6 +2324,15 @@ int geobpe_set_collapse(geobpe_ctx* c, int on) {
 
 int geobpe_collapsed(geobpe_ctx* c) { return c && c->collapsed ? 1 : 0; }
 
+int geobpe_comm_peer(geobpe_ctx* c, int on) {
+  if (!c) return GEOBPE_EARG;
+  if (c->x_peer_ready && !on) return fail(c, GEOBPE_EARG, "the peer exchange is set up already");
+  c->x_peer_want = on != 0;
+  return 0;
+}
+
+int geobpe_comm_peer_active(geobpe_ctx* c) { return c && c->x_peer_ready ? 1 : 0; }
+
 namespace {
 
 int grow_dev(geobpe_ctx* c, uint8_t** p, int64_t* have, int64_t bytes) {
@@ -2280,6 +2456,75 @@ bool x_fits(int64_t bytes) {
   return (int64_t)fr - bytes > (int64_t)(1LL << 30);
 }
 
+// The peer exchange (exchange.h), once per engine: this rank's receive area (2 parities x W
+// slots of XHDR + capf records), its IPC handle all-gathered, every other rank's area opened
+// here (same node: xGMI peer memory; ranks sharing a GPU: the same device).  Every rank's yes is
+// agreed on; a rank that cannot map every peer turns the peer exchange off on every rank (the
+// all-gather exchange stays).  capf: the fixed slot size when geobpe_comm_set_slot set one (tests
+// force stalls with tiny slots), else the all-gather path's largest (65 536 records).
+int x_peer_setup(geobpe_ctx* c, int64_t capf) {
+  if (c->x_peer_ready || !c->x_peer_want) return 0;
+  // (records per slot: the all-gather path's 65 536 made the heaviest C3 merges stall at world 1;
+  // 2^19 x 40 B x 2 parities x 8 ranks = 336 MB of the 288 GB)
+  const int64_t W = c->x_world, me = c->x_rank;
+  int rc;
+  bool ok = W >= 1 && W <= XPEER_MAX;
+  c->x_rcapf = capf;
+  c->x_slot = ((XHDR + capf * (int64_t)sizeof(DeltaRec)) + 255) / 256 * 256;
+  hipIpcMemHandle_t mine;
+  memset(&mine, 0, sizeof mine);
+  if (ok) ok = hipMalloc((void**)&c->x_recv, (size_t)(2 * W * c->x_slot)) == hipSuccess;
+  c->x_chkcap = (W * capf + c->nba - 2) / std::max(1, c->nba - 1) + 64;  // (one import share of every rank's slot)
+  if (ok) ok = !dalloc(c, &c->x_chk, (int64_t)c->nba * c->x_chkcap) && !dalloc(c, &c->x_chkcnt, c->nba, 0);
+  if (ok) ok = hipMemsetAsync(c->x_recv, 0, (size_t)(2 * W * c->x_slot), c->stream) == hipSuccess &&
+               hipStreamSynchronize(c->stream) == hipSuccess;
+  if (ok && W > 1) ok = hipIpcGetMemHandle(&mine, c->x_recv) == hipSuccess;
+  if (W > 1) {  // every rank's {ok, handle}; a handle is opened only when every rank made one
+    struct {
+      int64_t ok;
+      hipIpcMemHandle_t h;
+    } rec;
+    rec.ok = ok ? 1 : 0;
+    rec.h = mine;
+    std::vector<uint8_t> all;
+    if ((rc = x_allgather_host(c, &rec, sizeof rec, all))) return rc;
+    for (int64_t q = 0; q < W; q++) ok = ok && reinterpret_cast<const decltype(rec)*>(all.data())[q].ok != 0;
+    for (int64_t q = 0; q < W && ok; q++) {
+      if (q == me) continue;
+      void* p = nullptr;
+      ok = hipIpcOpenMemHandle(&p, reinterpret_cast<const decltype(rec)*>(all.data())[q].h,
+                               hipIpcMemLazyEnablePeerAccess) == hipSuccess;
+      c->x_peers[q] = (uint8_t*)p;
+    }
+  }
+  int can = 0;
+  c->x_cpwait = hipDeviceGetAttribute(&can, hipDeviceAttributeCanUseStreamWaitValue, c->device) == hipSuccess && can;
+  // (the stream waits on the command processor for ONE peer; with more, one waiter kernel: each
+  // hipStreamWaitValue32 costs the host ~2.8 us to enqueue, probe tools/probe/waitvalue.hip --
+  // at 7 peers more than a merge's kernels take on the device)
+  c->x_cpwait = c->x_cpwait && W == 2;
+  if (const char* e = getenv("GEOBPE_PEER_WAIT")) c->x_cpwait = atoi(e) != 0;  // (1: command processor, 0: waiter kernel)
+  bool every = ok;
+  if (W > 1 && (rc = x_agree(c, ok, &every))) return rc;
+  if (!every) {
+    for (int64_t q = 0; q < W; q++)
+      if (q != me && c->x_peers[q]) hipIpcCloseMemHandle(c->x_peers[q]);
+    if (c->x_recv) hipFree(c->x_recv);
+    c->x_recv = nullptr;
+    dfree(c, &c->x_chk);
+    dfree(c, &c->x_chkcnt);
+    for (auto& p : c->x_peers) p = nullptr;
+    c->x_peer_want = false;
+    return 0;
+  }
+  c->x_peers[me] = c->x_recv;
+  c->x_hseq = 1;
+  c->x_prev_seq = 0;
+  c->x_pending = false;
+  c->x_peer_ready = true;
+  return 0;
+}
+
 // Before the first pipelined merge: what a collapse moves that never changes after
 // initialize() -- every rank's junction symbols (int32 and 16-bit copies) and row offsets -- is
 // gathered once, off the switch (the collapse then moves only the 16-B token
@@ -2353,7 +2598,7 @@ bool x_collapse_pays(const geobpe_ctx* c, int64_t left) {
   if (!c->cg_ready || c->cg_bR.empty()) return false;
   const double Rt = (double)c->cg_bR.back();
   const double cost_us = 200.0 + Rt * (16.0 / 200e3 + 2.0e3 / 30e6);
-  return (double)left * 25.0 > cost_us;
+  return (double)left * (c->x_peer_ready ? 10.0 : 25.0) > cost_us;  // (the peer exchange's ~10 us a merge)
 }
 
 // The middle-regime switch of the row-sharded loop: stop sharding.  Below mid_thresh
@@ -2469,7 +2714,53 @@ int x_collapse(geobpe_ctx* c, bool* done) {
 // slots on the engine's stream, the import; a poll every few iterations (the window doubles
 // up to 64, back to 1 after a stall), a stalled merge re-exchanged in full.  Every rank sees
 // the same polls, so every rank issues the same collectives.
+}  // extern "C"
+namespace {
+// the pinned merge-log mirror grown to hold records [0, need) (geobpe_run_log's)
+int grow_h_log(geobpe_ctx* c, int64_t need) {
+  need = std::min<int64_t>(c->D.KC, need);
+  if (need <= c->h_log_cap) return 0;
+  const int64_t cap = std::min<int64_t>(c->D.KC, std::max<int64_t>({need, 2 * c->h_log_cap, 4096}));
+  LogRec* p = nullptr;
+  HIPCHK(c, hipHostMalloc((void**)&p, (size_t)cap * sizeof(LogRec), hipHostMallocDefault));
+  if (c->h_log) {
+    memcpy(p, c->h_log, (size_t)c->h_log_cap * sizeof(LogRec));
+    hipHostFree(c->h_log);
+  }
+  c->h_log = p;
+  c->h_log_cap = cap;
+  return 0;
+}
+int run_exchange_impl(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t* log_first);
+}  // namespace
+extern "C" {
+
 int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
+  return run_exchange_impl(c, n_merges, n_done, nullptr);
+}
+
+// geobpe_run_exchange with the run's merge records ({new id, count, merged} per merge, as
+// geobpe_run_log) pulled inside its last synchronisation; *first = the first merge's index, or -1
+// when the run ended in the one-rank loop (a collapse: then geobpe_merge_log has them)
+int geobpe_run_exchange_log(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t* first, int64_t* h_out,
+                            int64_t cap) {
+  if (!c || !first || !n_done || (cap > 0 && !h_out)) return GEOBPE_EARG;
+  int rc = run_exchange_impl(c, n_merges, n_done, first);
+  if (rc || *first < 0) return rc;
+  const int64_t n = std::min(*n_done, cap);
+  for (int64_t i = 0; i < n; i++) {
+    const LogRec& r = c->h_log[*first + i];
+    h_out[3 * i] = r.nid;
+    h_out[3 * i + 1] = r.count;
+    h_out[3 * i + 2] = r.nmerged;
+  }
+  return 0;
+}
+
+}  // extern "C"
+namespace {
+int run_exchange_impl(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t* log_first) {
+  if (log_first) *log_first = -1;
   if (!c || n_merges < 0) return GEOBPE_EARG;
   if (c->collapsed) return geobpe_run(c, n_merges, n_done);  // (every rank holds the whole corpus)
   if (!c->distributed || !c->keys_ready) return fail(c, GEOBPE_EARG, "run_exchange needs a distributed, binned engine");
@@ -2487,26 +2778,59 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
   // raised the fixed size since the last run)
   if ((rc = grow_dev(c, &c->x_gath, &c->x_gath_bytes, W * (1 + std::max(CAP_MAX, c->x_fixed)) * REC))) return rc;
   if (!c->ev && (rc = x_collapse_prepare(c))) return rc;  // (once: the collapse's static arrays)
-  if ((rc = geobpe_pipeline_begin(c))) return rc;
+  // (once: the peer exchange, unless GEOBPE_PEER=0 or more ranks than one node holds)
+  if (const char* e = getenv("GEOBPE_PEER")) c->x_peer_want = c->x_peer_want && atoi(e) != 0;
+  if (W > XPEER_MAX) c->x_peer_want = false;
+  if ((rc = x_peer_setup(c, c->x_fixed ? c->x_fixed : (int64_t)1 << 19))) return rc;
+  const bool peer = c->x_peer_ready;
+  // the regimes of the sharded loop: a rank runs the middle regime once ITS share of
+  // the winner's occurrences (count / W) is below the one-rank threshold, and the ranks collapse
+  // into the one-rank loop only below x_collapse_at, where one rank's late merge costs about what
+  // a sharded merge plus its exchange does.  Both read only replicated data (the winner's global
+  // count), so every rank switches at the same poll.
+  const int64_t mid_at = c->mid_thresh * W;
+  const int64_t collapse_at = peer ? c->x_collapse_at : c->mid_thresh;  // (the all-gather's ~30 us a merge: sooner)
+  if (!c->x_hlog) HIPCHK(c, hipHostMalloc((void**)&c->x_hlog, (size_t)(AHEAD_MAX + 2) * sizeof(LogRec), hipHostMallocDefault));
+  if ((rc = pipeline_begin_impl(c, true))) return rc;
   int64_t out[4];
   int64_t done = 0;
-  rc = geobpe_pipeline_poll(c, out);
-  const int64_t it0 = out[1];
-  int64_t ahead = c->x_ahead, capf = c->x_fixed ? c->x_fixed : c->x_capf;
+  if (!peer) rc = geobpe_pipeline_poll(c, out);  // (the slot sizing's largest count starts again)
+  const int64_t it0 = c->h_state->iter;  // (pipeline_begin synchronised the state)
+  int64_t ahead = peer && c->x_ahead > 1 ? AHEAD_MAX : c->x_ahead, capf = c->x_fixed ? c->x_fixed : c->x_capf;
+  // the last merge's record: the host's copy of the log range the last batch could write, pulled
+  // with its poll (round 5 paid another host round trip per poll for it)
+  int64_t lfrom = -1, ln = 0;
+  bool pulled = false;  // (the run's merge records pulled by the last poll)
+  auto last_rec = [&](LogRec* lr) -> int {
+    const int64_t i = (int64_t)c->h_state->iter - 1;
+    if (i >= lfrom && i < lfrom + ln) {
+      *lr = c->x_hlog[i - lfrom];
+    } else if (i == c->x_last_i) {  // (the previous run's last poll pulled it)
+      *lr = c->x_last;
+    } else {
+      HIPCHK(c, hipMemcpy(lr, c->D.log + i, sizeof *lr, hipMemcpyDeviceToHost));
+    }
+    c->x_last = *lr;
+    c->x_last_i = i;
+    return 0;
+  };
   while (!rc && done < n_merges) {
     // the middle regime once the winner's count is small (a poll is a quiescent point: the
     // lists are built, or rebuilt after an iteration stalled on them).  The decision and the
     // poll window read only replicated data -- the winner's global count from the replicated
     // counts, the iteration number -- so every rank switches at the same poll and issues the
     // same collectives (a rank's own merged count would let ranks part ways)
+    // (the peer exchange stalls only past 2^19 records a rank: its batches run to the next
+    // predicted switch, as the one-rank loop's do, instead of doubling from 1)
     int64_t win = ahead;
     const bool may_collapse = c->collapse_on && c->cg_ready && !c->ev && x_collapse_pays(c, n_merges - done);
     if ((!c->mid_on || may_collapse) && mid_enabled(c) && c->h_state->iter > 0) {
       LogRec lr;
-      HIPCHK(c, hipMemcpy(&lr, c->D.log + (c->h_state->iter - 1), sizeof lr, hipMemcpyDeviceToHost));
-      if (lr.count <= c->mid_thresh && may_collapse) {
+      if ((rc = last_rec(&lr))) break;
+      if (lr.count <= collapse_at && may_collapse) {
         // stop sharding: every rank takes the whole corpus and goes on alone (x_collapse)
         bool collapsed = false;
+        if (peer) x_check_all(c);
         if ((rc = geobpe_pipeline_end(c)) || (rc = x_collapse(c, &collapsed))) return rc;
         if (collapsed) {
           int64_t more = 0;
@@ -2516,31 +2840,73 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
         }
         if ((rc = geobpe_pipeline_begin(c))) return rc;  // (some rank declined: sharded, as before)
       }
-      if (!c->mid_on && lr.count <= c->mid_thresh) {
+      if (!c->mid_on && lr.count <= mid_at) {
         c->mid_on = true;
         // the middle regime's records are per (workgroup, key), not per owner and key: a
         // merge of the same size sends up to ~4x as many -- a slot that small would stall
         if (!c->x_fixed) capf = std::min(CAP_MAX, 4 * capf);
-      } else if (!c->mid_on && lr.count <= 2 * c->mid_thresh) {
-        win = std::min<int64_t>(win, 8);  // (close: poll sooner)
+      } else if ((!c->mid_on && lr.count <= 2 * mid_at) || (may_collapse && lr.count <= 2 * collapse_at)) {
+        // (close to a switch: poll sooner -- at the predicted merge + 8 when the decay is known)
+        const int64_t th = !c->mid_on && lr.count <= 2 * mid_at ? mid_at : collapse_at;
+        int64_t w = 8;
+        if (peer && c->x_decay > 0 && c->x_decay < 1 && lr.count > th)
+          w = std::max<int64_t>(8, std::min<int64_t>(AHEAD_MAX, (int64_t)(std::log((double)th / lr.count) /
+                                                                             std::log(c->x_decay)) + 8));
+        win = std::min<int64_t>(win, w);
       }
     }
     if (c->mid_on && (rc = mid_prepare(c))) break;
     const int64_t slot = (1 + capf) * REC;
     const int64_t k = std::min(win, n_merges - done);  // an iteration merges at most once
-    for (int64_t i = 0; i < k && !rc; i++) {
-      if ((rc = geobpe_pipeline_iter(c, c->x_pbuf, c->x_pcap))) break;
+    // the run's last batch (peer exchange): spec more iterations, idle on the device once the
+    // batch's merges are made -- a hot-list rebuild iteration inside the batch then needs no
+    // top-up batch and poll (run_batches' rule; the select's run_end)
+    const int64_t extra = peer && k == n_merges - done ? c->spec : 0;
+    const int32_t run_end = extra ? (int32_t)(c->h_state->iter + k + 1) : 0;
+    for (int64_t i = 0; i < k + extra && !rc; i++) {
+      if ((rc = pipeline_iter_impl(c, c->x_pbuf, c->x_pcap, peer, run_end))) break;
+      if (peer) continue;  // (the records went to every peer inside the kernels; exchange.h)
       if ((rc = x_allgather(c, c->x_pbuf, c->x_gath, slot))) break;
       rc = geobpe_pipeline_import(c, c->x_gath, (int32_t)W, capf);
+    }
+    if (!rc && peer) rc = x_drain(c);  // (the batch's last records: the poll sees complete counts)
+    const bool last = k == n_merges - done;  // (the run ends at this poll unless merges fell short)
+    pulled = false;
+    if (!rc && last) {  // (the end's work inside this poll's synchronisation: no second one)
+      if (peer) x_check_all(c);
+      if (log_first && !(rc = grow_h_log(c, it0 + n_merges + 1))) {
+        flush_place(c);  // (the last place sums the last merge's merged occurrences into its record)
+        const int64_t m = std::min<int64_t>(n_merges, c->h_log_cap - it0);
+        if (m > 0) {
+          const hipError_t e = hipMemcpyAsync(c->h_log + it0, c->D.log + it0, m * sizeof(LogRec),
+                                              hipMemcpyDeviceToHost, c->stream);
+          if (e != hipSuccess) rc = fail(c, GEOBPE_EHIP, "log pull: %s", hipGetErrorString(e));
+        }
+        pulled = true;
+      }
+    }
+    if (!rc) {  // (the records the batch could write, pulled with the poll's synchronisation)
+      lfrom = c->h_state->iter;
+      ln = std::max<int64_t>(0, std::min<int64_t>({k, AHEAD_MAX + 2, c->D.KC - lfrom}));
+      if (ln > 0) {
+        const hipError_t e = hipMemcpyAsync(c->x_hlog, c->D.log + lfrom, ln * sizeof(LogRec), hipMemcpyDeviceToHost,
+                                            c->stream);
+        if (e != hipSuccess) rc = fail(c, GEOBPE_EHIP, "log pull: %s", hipGetErrorString(e));
+      }
     }
     if (rc || (rc = geobpe_pipeline_poll(c, out))) break;
     const bool stalled = out[0] != 0, fin = out[2] != 0;
     const int64_t it = out[1], smax = out[3];
+    {  // the winner count's decay over the batch (the next batch's length near a switch)
+      const int64_t z = std::min<int64_t>(it - 1, lfrom + ln - 1);
+      if (ln > 0 && z > lfrom && c->x_hlog[0].count > 0 && c->x_hlog[z - lfrom].count > 0)
+        c->x_decay = std::pow((double)c->x_hlog[z - lfrom].count / (double)c->x_hlog[0].count, 1.0 / (double)(z - lfrom));
+    }
     if (stalled) {
       if ((rc = x_resolve(c))) break;
       ahead = 1;
     } else {
-      ahead = std::min<int64_t>(2 * ahead, AHEAD_MAX);
+      ahead = peer ? AHEAD_MAX : std::min<int64_t>(2 * ahead, AHEAD_MAX);
     }
     if (!c->x_fixed) {
       int64_t p2 = 1;
@@ -2552,11 +2918,26 @@ int geobpe_run_exchange(geobpe_ctx* c, int64_t n_merges, int64_t* n_done) {
     c->x_capf = capf;
     if (fin) break;
   }
-  const int rc_end = geobpe_pipeline_end(c);
+  // (the last poll synchronised everything when the run ended with the batch it planned as its last)
+  const bool fresh = pulled || (!log_first && c->enq == c->enq_synced && !c->place_pending);
+  if (!rc && peer && !fresh) x_check_all(c);  // (the last imports' found keys: checked now, not by the next run)
+  if (!rc && log_first && !pulled && !(rc = grow_h_log(c, it0 + n_merges + 1))) {
+    // (the run's records in the end's own synchronisation; after the last place, which sums the
+    // last merge's merged occurrences into its record)
+    flush_place(c);
+    const int64_t m = std::min<int64_t>(n_merges, c->h_log_cap - it0);
+    if (m > 0) {
+      const hipError_t e = hipMemcpyAsync(c->h_log + it0, c->D.log + it0, m * sizeof(LogRec), hipMemcpyDeviceToHost,
+                                          c->stream);
+      if (e != hipSuccess) rc = fail(c, GEOBPE_EHIP, "log pull: %s", hipGetErrorString(e));
+    }
+  }
+  if (!rc && log_first) *log_first = it0;
+  const int rc_end = fresh && !rc ? pipeline_end_lite(c) : geobpe_pipeline_end(c);
   if (rc) return rc;  // (an error in flight is the one to report)
   if (rc_end) return rc_end;
   if (n_done) *n_done = done;
   return 0;
 }
 
-}  // extern "C"
+}  // namespace

@@ -368,6 +368,7 @@ __global__ __launch_bounds__(ABLOCK) void k_finalize(Dev D, int to_delta) {
   agg_flush_hot(agg, D, hot, to_delta != 0, th);
 }
 
+#include "exchange.h"
 #include "merge.h"
 
 // ====================================================================== argmax + tie-break
@@ -923,18 +924,32 @@ __device__ void select_core(const Dev& D, int par, SelStage& S, int32_t* s_red, 
   dbg_stamp(D, 26);
 }
 
-__global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par, int run_end) {
+// workgroup 0: the select; workgroups 1..: the previous merge's k_place (place != 0: it needs
+// only k_commit's output) and, with the peer exchange (nimp > 0, exchange.h), first the import
+// of the previous launch's records in workgroups 1..nimp, which the select waits for
+__global__ __launch_bounds__(SBLOCK) void k_select(Dev D, int par, int run_end, int place, int nimp) {
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
   State* st = D.st;
-  if (blockIdx.x > 0) {  // the previous merge's k_place rides along (it needs only k_commit's output)
-    __shared__ PlaceLds P;
-    place_body(D, blockIdx.x - 1, P);
+  if (blockIdx.x > 0) {
+    const int32_t b = blockIdx.x - 1;
+    if (b < nimp) {
+      __shared__ XImpLds X;
+      x_import_share(D, X, b, nimp, false);
+    }
+    if (place && b < D.NBA) {
+      __shared__ PlaceLds P;
+      place_body(D, b, P);
+    }
     return;
   }
   if (par == INT32_MIN) return;  // place only
   if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
-    if (st->stall) return;
+    if (nimp > 0) {
+      if (!x_import_wait(D, st->xpend != 0, nimp)) return;
+    } else if (st->stall) {
+      return;
+    }
     const int32_t g = st->dgen + 1;
     par = g & 1;
     __syncthreads();  // every thread has read dgen

@@ -646,7 +646,7 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
 
 // ---------------------------------------------------------------------- k_commit
 struct CommitLds;
-__device__ void commit_export(const Dev& D, CommitLds& S);
+__device__ __attribute__((always_inline)) inline void commit_export(const Dev& D, CommitLds& S);
 struct CommitLds {
   union {
     AggT<12> agg;  // decrements of this owner's keys
@@ -877,7 +877,7 @@ __device__ __attribute__((always_inline)) inline void commit_publish(const Dev& 
 // k_find's side list -- straight into the rank's slot, one reservation per workgroup on
 // the slot header's count (final when k_commit ends: no header pass).  The import adds
 // every rank's records (this rank's included) to the replicated counts.
-__device__ void commit_export(const Dev& D, CommitLds& S) {
+__device__ __attribute__((always_inline)) inline void commit_export(const Dev& D, CommitLds& S) {  // (inlined: a call takes D's address, and the whole Dev goes to scratch)
   __shared__ unsigned long long s_xb;
   const int t = threadIdx.x;
   const int64_t nx = min(D.st->nxovf, D.KCAP);  // (k_find's; k_commit adds none)
@@ -904,7 +904,7 @@ __device__ void commit_export(const Dev& D, CommitLds& S) {
     r.idR = rp.w;
     r.delta = S.cn[s];
     r.pad = S.cid[s] + 1;  // (the import of this rank's own slot uses it instead of probing)
-    if (j < D.xcap) D.xrec[j] = r;
+    x_put_rec(D, j, r, -30);
     j++;
   }
   auto put_id = [&](int32_t k, int32_t v) {
@@ -917,7 +917,7 @@ __device__ void commit_export(const Dev& D, CommitLds& S) {
     r.idR = D.krep[3 * (int64_t)k + 2];
     r.delta = v;
     r.pad = k + 1;
-    if (j < D.xcap) D.xrec[j] = r;
+    x_put_rec(D, j, r, -30);
     j++;
   };
   for (int i = t; i < AggT<12>::N; i += ABLOCK) {
@@ -928,10 +928,9 @@ __device__ void commit_export(const Dev& D, CommitLds& S) {
     const int2 e = D.xovf[i];
     put_id(e.x, e.y);
   }
-  if (t == 0 && (int64_t)s_xb + tot > D.xcap) set_error(D, GEOBPE_ECAPACITY, -30);
 }
 
-__global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par) {
+__device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, int to_delta, int par) {
   __shared__ CommitLds S;
   __shared__ HotApp hot;
   __shared__ int64_t s_kl[2];
@@ -1291,6 +1290,11 @@ __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par)
     }
   }
   dbg_stamp(D, 6);
+}
+
+__global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par) {
+  commit_main(D, to_delta, par);
+  x_arrive(D);  // (the peer exchange: this launch's records are out, exchange.h)
 }
 
 // ---------------------------------------------------------------------- k_place

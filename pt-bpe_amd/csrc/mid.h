@@ -223,10 +223,7 @@ __device__ inline void mid_put(const Dev& D, int64_t j, u64 h1, u64 h2, int32_t 
   r.idR = idR;
   r.delta = delta;
   r.pad = d + 1;
-  if (j < D.xcap)
-    D.xrec[j] = r;
-  else
-    set_error(D, GEOBPE_ECAPACITY, -72);
+  x_put_rec(D, j, r, -72);
 }
 __device__ inline void mid_put_id(const Dev& D, int64_t j, int32_t d, int32_t delta) {
   mid_put(D, j, D.kh1[d], D.kh2[d], D.klen[d], D.krep[3 * (int64_t)d], D.krep[3 * (int64_t)d + 1],
@@ -906,7 +903,7 @@ __device__ __attribute__((always_inline)) inline void mid_append_body(const Dev&
 // workgroups 0..G-1: the find of merge `par` (find = 0: none, a flush; par < 0: the
 // pipelined exchange's device parity); workgroups G..: the posting entries of the previous
 // merge (st->place_par_prev), skipping this merge's winner
-__global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int find) {
+__device__ __attribute__((always_inline)) inline void mid_find_main(const Dev& D, int par, int G, int find) {
   __shared__ union {
     MidFindLds f;
     MidAppLds a;
@@ -932,6 +929,10 @@ __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int 
   if (pp < 0 || !valid) return;
   const int32_t skip = sel.decision == SEL_MERGE ? sel.W : -1;
   mid_append_body(D, pp, skip, blockIdx.x - G, gridDim.x - G, U.a);
+}
+__global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int find) {
+  mid_find_main(D, par, G, find);
+  x_arrive(D);  // (the peer exchange: this launch's records are out, exchange.h)
 }
 
 // ---------------------------------------------------------------------- select + place
@@ -1031,18 +1032,29 @@ __device__ void mid_place_body(const Dev& D, int32_t b, int32_t P) {
 // rewrites of merge st->place_par.  Workgroup 0 records which merge's new pairs the next
 // find's appends take (place_par_prev) and resets its parity's list cursors (nothing else
 // in this launch reads them).
-__global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par, int run_end) {
+// (nimp > 0: the peer exchange's import of the previous launch's records first, in workgroups
+// 1..nimp, which the select waits for; exchange.h)
+__global__ __launch_bounds__(ABLOCK) void k_mid_sel(Dev D, int par, int run_end, int nimp) {
   if (blockIdx.x > 0) {
+    if ((int)blockIdx.x - 1 < nimp) {
+      __shared__ XImpLds X;
+      x_import_share(D, X, blockIdx.x - 1, nimp, false);
+    }
     mid_place_body(D, blockIdx.x - 1, gridDim.x - 1);
     return;
   }
   __shared__ int32_t s_red[SBLOCK / 64];
   __shared__ SelStage S;
   State* st = D.st;
+  const bool xpend = nimp > 0 && st->xpend != 0;  // (read before any workgroup can change it)
   if (threadIdx.x == 0) st->place_par_prev = st->place_par;
   if (par == INT32_MIN) return;
   if (par < 0) {  // pipelined exchange: parity from the device's iteration count; no-op while stalled
-    if (st->stall) return;
+    if (nimp > 0) {
+      if (!x_import_wait(D, xpend, nimp)) return;
+    } else if (st->stall) {
+      return;
+    }
     const int32_t g = st->dgen + 1;
     par = g & 1;
     __syncthreads();  // every thread has read dgen

@@ -128,6 +128,9 @@ def lib():
                                        ctypes.c_int, P]),
         "geobpe_arena_release": (ctypes.c_int, [ctypes.c_int]),
         "geobpe_set_collapse": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_comm_peer": (ctypes.c_int, [P, ctypes.c_int]),
+        "geobpe_run_exchange_log": (ctypes.c_int, [P, I64, pI64, pI64, P, I64]),
+        "geobpe_comm_peer_active": (ctypes.c_int, [P]),
         "geobpe_collapsed": (ctypes.c_int, [P]),
     }
     for name, (res, args) in sig.items():
@@ -152,7 +155,8 @@ EXPORTED_SYMBOLS = [
     "geobpe_comm_unique_id", "geobpe_comm_init_rccl", "geobpe_comm_error", "geobpe_comm_set_callback",
     "geobpe_comm_set_slot", "geobpe_run_exchange", "geobpe_pdb_backbone", "geobpe_pdb_error",
     "geobpe_featurize", "geobpe_rmsd", "geobpe_nerf", "geobpe_glue_opt", "geobpe_arena_release",
-    "geobpe_set_collapse", "geobpe_collapsed",
+    "geobpe_set_collapse", "geobpe_collapsed", "geobpe_comm_peer", "geobpe_comm_peer_active",
+    "geobpe_run_exchange_log",
 ]
 
 

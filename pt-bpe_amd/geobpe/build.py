@@ -9,7 +9,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(os.path.dirname(HERE), "csrc")
 OUT = os.path.join(HERE, "libgeobpe.so")
 SOURCES = [os.path.join(CSRC, "geobpe.hip")]
-DEPS = SOURCES + [os.path.join(CSRC, "keyjson.h"), os.path.join(CSRC, "device.h"), os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "bin_dense.h"), os.path.join(CSRC, "merge.h"), os.path.join(CSRC, "featurize.h"), os.path.join(CSRC, "rmsd.h"), os.path.join(CSRC, "glue.h"), os.path.join(CSRC, "tail.h"), os.path.join(CSRC, "mid.h"),
+DEPS = SOURCES + [os.path.join(CSRC, "keyjson.h"), os.path.join(CSRC, "device.h"), os.path.join(CSRC, "kernels.h"), os.path.join(CSRC, "bin_dense.h"), os.path.join(CSRC, "merge.h"), os.path.join(CSRC, "featurize.h"), os.path.join(CSRC, "rmsd.h"), os.path.join(CSRC, "glue.h"), os.path.join(CSRC, "tail.h"), os.path.join(CSRC, "mid.h"), os.path.join(CSRC, "exchange.h"),
                   os.path.join(os.path.dirname(os.path.dirname(HERE)), "include", "geobpe.h")]
 ARCH = os.environ.get("GEOBPE_ARCH", "gfx950")
 

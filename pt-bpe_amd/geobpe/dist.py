@@ -167,6 +167,9 @@ class TorchGroup:
         fixed = getattr(self, "pipe_cap", None)
         if fixed:
             engine._chk(L.geobpe_comm_set_slot(engine._ctx, int(fixed)))
+        peer = getattr(self, "peer", None)  # (None: the engine's default, the peer exchange up to 8 ranks)
+        if peer is not None:
+            engine._chk(L.geobpe_comm_peer(engine._ctx, 1 if peer else 0))
         engine._x_attached = True
 
     def run_pipelined(self, engine, n_merges: int) -> int:

@@ -308,6 +308,21 @@ class GeoBPEEngine:
         if not self._binned:
             raise RuntimeError("bin() first")
         if self.distributed:
+            if self.pipelined and getattr(self.group, "engine_exchange", False) and hasattr(self.group, "attach"):
+                # the engine's own N > 1 loop; the run's merge records come back with it
+                self.group.attach(self)
+                n, first = ctypes.c_int64(0), ctypes.c_int64(0)
+                buf = np.zeros(3 * max(int(n_merges), 1), dtype=np.int64)
+                self._chk(self.L.geobpe_run_exchange_log(self._ctx, int(n_merges), ctypes.byref(n), ctypes.byref(first),
+                                                         _p(buf), int(n_merges)))
+                self._collapsed = bool(self.L.geobpe_collapsed(self._ctx))
+                if first.value >= 0 and first.value == len(self.merges):
+                    self.merges.extend(tuple(int(x) for x in buf[3 * i:3 * i + 3]) for i in range(n.value))
+                else:
+                    self._refresh_log()
+                if n.value < n_merges:
+                    self._done = True
+                return int(n.value)
             if self.pipelined and hasattr(self.group, "run_pipelined"):
                 done = self.group.run_pipelined(self, int(n_merges))
                 self._collapsed = bool(self.L.geobpe_collapsed(self._ctx))

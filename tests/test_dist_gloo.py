@@ -104,8 +104,10 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
             mid = 1500
         shard = slice_corpus(corpus, lo, hi)
         g = TorchGroup(int(shard["row_off"][-1]), device=0)
-        if mode == "small-slots":  # most merges overflow the fixed slots: the stall / resolve path
+        if mode.endswith("small-slots"):  # most merges overflow the fixed slots: the stall / resolve path
             g.pipe_cap = 16
+        if mode.startswith("allgather"):  # the all-gather of fixed slots instead of the peer exchange
+            g.peer = False
         if mode == "host-loop":  # the Python-driven loop (geobpe.dist) instead of geobpe_run_exchange
             g.engine_exchange = False
         e = GeoBPEEngine(shard, 5, device=0, group=g, mid=mid, collapse=collapse).initialize()
@@ -119,6 +121,8 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
         else:
             done += e.run(80)  # a second pipelined run continues the device parity
         s, ids, off = e.segmentation()
+        if mode not in ("stepwise", "host-loop"):  # (geobpe_run_exchange ran: which exchange it took)
+            assert e.L.geobpe_comm_peer_active(e._ctx) == (0 if mode.startswith("allgather") else 1)
         if mode.startswith("skewed"):
             assert e.merges[0][1] > mid >= e.merges[-1][1], "the run does not cross the middle-regime threshold"
         assert e.collapsed == collapse, "collapse expected" if collapse else "no collapse expected"
@@ -134,14 +138,17 @@ def _engine_worker(rank, world, port, q, mode="pipelined"):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("world, mode", [(2, "pipelined"), (3, "pipelined"), (2, "small-slots"), (2, "stepwise"),
-                                         (3, "mixed"), (4, "small-slots"), (2, "host-loop"),
+                                         (3, "mixed"), (4, "small-slots"), (2, "host-loop"), (2, "allgather"),
+                                         (3, "allgather-small-slots"),
                                          (2, "skewed-nocollapse"), (3, "skewed-nocollapse"), (2, "skewed"),
                                          (3, "skewed"), (2, "collapse"), (4, "collapse"), (2, "mixed-collapse")])
 def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
     """The full N>1 path (TorchGroup exchange, one process per rank) with gloo on
-    one device: the engine's pipelined loop (geobpe_run_exchange over the group's host
-    collective: fixed slots, stall + full re-exchange of an overflowing merge), the same
-    with tiny slots, the Python-driven loop, and the host-synchronised per-merge
+    one device: the engine's pipelined loop (geobpe_run_exchange: the peer exchange -- every
+    rank's receive area IPC-mapped into the others, records stored by the merge kernels, the
+    stream waiting on the peers' headers -- or, "allgather*", the group's host collective over
+    fixed slots; stall + full re-exchange of an overflowing merge), the same with tiny slots,
+    the Python-driven loop, and the host-synchronised per-merge
     exchange; skewed shards whose own merged counts cross the middle-regime threshold far
     apart (the switch follows the replicated count); the collapse at that switch (every
     rank gathers the whole corpus and goes on alone) early, mid-run and before host steps.
