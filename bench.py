@@ -221,6 +221,9 @@ def main():
         sys.exit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
     if args.force_exchange:  # rehearsal of the exchange only: no tables that need per-merge counts
         args.no_profile = args.no_replay = args.no_cpu_baseline = True
+        # (loopback: the rank is its own peer, its records imported by content hash -- what a rank
+        # of N pays for the other ranks' records; GEOBPE_PEER_LOOPBACK=0: the one-rank protocol)
+        os.environ.setdefault("GEOBPE_PEER_LOOPBACK", "1")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0")) if args.dist_backend == "nccl" else 0
@@ -286,6 +289,8 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     done = eng.run(args.steps)
+    if os.environ.get("GEOBPE_XTIME"):
+        print(f"xtime: eng.run returned at +{1e6 * (time.perf_counter() - t0):.1f} us", file=sys.stderr)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -502,7 +507,9 @@ def main():
                    "rank_residues": rank_res, "backend": (args.dist_backend if world > 1 else None),
                    **({"shard_of": args.shard_of} if args.shard_of > 1 else {}),
                    **({"exchange": "rehearsal (world 1)" + (", all-gather" if os.environ.get("GEOBPE_PEER") == "0"
-                                                             else ", peer")} if args.force_exchange else {})},
+                                                             else ", peer" + (", loopback" if os.environ.get(
+                                                                 "GEOBPE_PEER_LOOPBACK") == "1" else ""))}
+                      if args.force_exchange else {})},
         "roofline": roofline,
         "roofline_other": roofline_other,
         "cpu_baseline": cpu,

@@ -243,6 +243,8 @@ struct Dev {
   int64_t xslot, xcapf;  // bytes per source slot (XHDR + xcapf records), records per slot
   int32_t xw, xme;       // ranks, this rank
   int32_t xseq, xpar;    // this launch's sequence number and slot parity
+  int32_t xloop, xpad;   // loopback rehearsal: this rank is also its own peer (records to its own
+                         // slot, imported by content hash; none applied by the producer)
   NewPair* xchk;         // per import workgroup: the keys its import found (not claimed), checked
   int32_t* xchkcnt;      // against their stored content by the next import (EHASH; exchange.h)
   int64_t xchkcap;
@@ -497,11 +499,26 @@ __device__ __attribute__((always_inline)) inline void x_put_rec(const Dev& D, in
     return;
   }
   D.xrec[j] = r;
-  if (D.xw > 1 && j < D.xcapf) {
+  if (D.xw > 0 && !D.xloop && r.pad > 0 && r.delta != 0) {
+    // the peer exchange applies this rank's own change here, where the record is made (the
+    // import takes only the other ranks'); nothing in a producer launch reads the counts, so
+    // this is the import's add moved earlier.  A theta crossing joins the hot list directly.
+    const int32_t d = r.pad - 1;
+    const int32_t old = atomicAdd(&D.count[d], r.delta);
+    const int32_t th = D.st->theta;
+    if (r.delta > 0 && th > 0 && old < th && old + r.delta >= th) {
+      const int64_t k = (int64_t)atomicAdd((unsigned long long*)&D.st->ncl2[D.st->cl_act], 1ULL);
+      if (k < D.KCAP)
+        D.clist[k] = d;
+      else
+        D.st->cl_valid = 0;
+    }
+  }
+  if ((D.xw > 1 || D.xloop) && j < D.xcapf) {
     const unsigned long long* v = reinterpret_cast<const unsigned long long*>(&r);
 #pragma unroll
     for (int q = 0; q < XPEER_MAX; q++) {  // (static indices: a runtime index into the kernel-argument
-      if (q >= D.xw || q == D.xme) continue;  // array copies the whole Dev to scratch)
+      if (q >= D.xw || (q == D.xme && !D.xloop)) continue;  // array copies the whole Dev to scratch)
       // written through to the peer's memory (system-scope stores: no dirty line left in this
       // XCD's L2, so the producer's end needs no L2 write-back before the header)
       unsigned long long* o =

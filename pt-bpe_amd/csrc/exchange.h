@@ -43,20 +43,20 @@ __device__ __attribute__((always_inline)) inline void x_arrive(const Dev& D) {
   // each wave's write-through stores into the peers' memory complete (vmcnt 0) -- no L2
   // write-back per wave: round 6's first form fenced every wave at system scope, a
   // buffer_wbl2 each, and the rehearsal's window fell from 8.8 k to 4.1 k merges/s
-  if (D.xw > 1) __builtin_amdgcn_s_waitcnt(0);
+  if (D.xw > 1 || D.xloop) __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x != 0) return;
   State* st = D.st;
   const int32_t n = __hip_atomic_fetch_add(&st->xarr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (n != (int32_t)gridDim.x - 1) return;
-  if (D.xw > 1) __threadfence_system();  // (one release at system scope before the headers)
+  if (D.xw > 1 || D.xloop) __threadfence_system();  // (one release at system scope before the headers)
   st->xarr = 0;  // (the next producer launch comes after a kernel boundary)
   const bool stalled = __hip_atomic_load(&st->stall, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   const int64_t cnt =
       stalled ? -1 : (int64_t)__hip_atomic_load((unsigned long long*)D.xcnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
   for (int q = 0; q < XPEER_MAX; q++) {  // (static indices into D.xpeer: see x_put_rec)
-    if (q >= D.xw || q == D.xme) continue;
+    if (q >= D.xw || (q == D.xme && !D.xloop)) continue;
     XHdr* h = x_hdr(D.xpeer[q], D.xslot, D.xme);
     __hip_atomic_store(&h->count, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&h->seq, D.xseq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -197,10 +197,12 @@ __device__ void x_import_share(const Dev& D, XImpLds& X, int32_t b, int32_t nb, 
   }
   const int32_t W = D.xw, par = st->xppar, seq = st->xpseq;
   uint8_t* half = D.xrecv + (int64_t)par * W * D.xslot;
-  if (t < W && !X.bad) {  // every rank's count, one thread a rank: this rank's from the state, the others'
-                          // headers (stalled: later no-op launches have overwritten them -- not read)
-    int64_t c = st->xpcnt;
-    if (t != D.xme) {
+  if (t < W && !X.bad) {  // every other rank's count from its header, one thread a rank (stalled:
+                          // later no-op launches have overwritten them -- not read).  This rank's
+                          // own records were applied by the producer (x_put_rec): none to import,
+                          // but a count past the slots stalls every rank, this one included
+    int64_t c = st->xpcnt > D.xcapf ? -1 : 0;
+    if (t != D.xme || D.xloop) {
       XHdr* h = x_hdr(half, D.xslot, t);
       const int32_t sq = __hip_atomic_load(&h->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       c = __hip_atomic_load(&h->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -233,13 +235,8 @@ __device__ void x_import_share(const Dev& D, XImpLds& X, int32_t b, int32_t nb, 
       int r = 0;
       while (j >= X.pre[r + 1]) r++;
       const int64_t k = j - X.pre[r];
-      const DeltaRec rr =
-          r == D.xme ? D.xrec[k] : x_load_rec(reinterpret_cast<const DeltaRec*>(half + (int64_t)r * D.xslot + XHDR) + k);
+      const DeltaRec rr = x_load_rec(reinterpret_cast<const DeltaRec*>(half + (int64_t)r * D.xslot + XHDR) + k);
       if (rr.delta == 0) continue;
-      if (r == D.xme && rr.pad > 0) {  // this rank's own record: its key id, resolved by the producer
-        x_count_add_hot(D, X.hot, rr.pad - 1, rr.delta, th);
-        continue;
-      }
       bool claimed;
       const int32_t d = ht_insert(D, rr.h1, rr.h2, rr.len, &claimed);
       if (d < 0) continue;

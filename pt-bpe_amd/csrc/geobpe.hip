@@ -20,6 +20,7 @@
 #include <rccl/rccl.h>  // types only: the functions are resolved at run time (the process's RCCL)
 
 #include <algorithm>
+#include <chrono>
 #include <climits>
 #include <cmath>
 #include <cstdarg>
@@ -124,7 +125,7 @@ struct geobpe_ctx {
   // peer exchange (exchange.h; geobpe_comm_peer): this rank's receive area (2 parities x
   // x_world slots), every rank's area as mapped here (IPC handles; [x_rank] = x_recv), the
   // host's count of producer launches (each launch's sequence number, the same on every rank)
-  bool x_peer_want = true, x_peer_ready = false, x_pending = false, x_cpwait = true;
+  bool x_peer_want = true, x_peer_ready = false, x_pending = false, x_cpwait = true, x_loop = false;
   uint8_t* x_recv = nullptr;
   uint8_t* x_peers[XPEER_MAX] = {};
   int64_t x_slot = 0, x_rcapf = 0;
@@ -1367,6 +1368,7 @@ Dev x_peer_dev(const geobpe_ctx* c, Dev D, int64_t h) {
   D.xcapf = c->x_rcapf;
   D.xseq = (int32_t)h;
   D.xpar = (int32_t)(h & 1);
+  D.xloop = c->x_loop ? 1 : 0;
   D.xchk = c->x_chk;
   D.xchkcnt = c->x_chkcnt;
   D.xchkcap = c->x_chkcap;
@@ -2394,12 +2396,13 @@ int x_resolve(geobpe_ctx* c) {
   if ((rc = x_allgather(c, c->x_pbuf + REC, c->x_tmp, m * REC))) return rc;
   int64_t off = 0;
   for (int64_t r = 0; r < W; r++) {
+    if (c->x_peer_ready && !c->x_loop && r == c->x_rank) continue;  // (the peer exchange applied this rank's own already)
     if (cnt[r])
       HIPCHK(c, hipMemcpyAsync(c->x_flat + off * REC, c->x_tmp + r * m * REC, cnt[r] * REC, hipMemcpyDeviceToDevice,
                                c->stream));
     off += cnt[r];
   }
-  return geobpe_pipeline_resolve(c, c->x_flat, total);
+  return geobpe_pipeline_resolve(c, c->x_flat, off);
 }
 
 // every rank's `bytes` of host data, rank-major, through the exchange (device staging)
@@ -2518,6 +2521,9 @@ int x_peer_setup(geobpe_ctx* c, int64_t capf) {
     return 0;
   }
   c->x_peers[me] = c->x_recv;
+  // (loopback rehearsal, one rank: its records go to its own slot and are imported by content
+  // hash, as a peer's -- the import cost a rank of N pays, measured on one GPU)
+  if (const char* e = getenv("GEOBPE_PEER_LOOPBACK")) c->x_loop = W == 1 && atoi(e) != 0;
   c->x_hseq = 1;
   c->x_prev_seq = 0;
   c->x_pending = false;
@@ -2760,6 +2766,9 @@ int geobpe_run_exchange_log(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, in
 }  // extern "C"
 namespace {
 int run_exchange_impl(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t* log_first) {
+  static const bool xt = getenv("GEOBPE_XTIME") != nullptr;  // (host phase times to stderr: diagnostics)
+  auto now_us = []() { return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count(); };
+  const double xt0 = xt ? now_us() : 0;
   if (log_first) *log_first = -1;
   if (!c || n_merges < 0) return GEOBPE_EARG;
   if (c->collapsed) return geobpe_run(c, n_merges, n_done);  // (every rank holds the whole corpus)
@@ -2791,7 +2800,10 @@ int run_exchange_impl(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t*
   const int64_t mid_at = c->mid_thresh * W;
   const int64_t collapse_at = peer ? c->x_collapse_at : c->mid_thresh;  // (the all-gather's ~30 us a merge: sooner)
   if (!c->x_hlog) HIPCHK(c, hipHostMalloc((void**)&c->x_hlog, (size_t)(AHEAD_MAX + 2) * sizeof(LogRec), hipHostMallocDefault));
+  const double xt1 = xt ? now_us() : 0;
   if ((rc = pipeline_begin_impl(c, true))) return rc;
+  if (xt) fprintf(stderr, "xtime: preamble %.1f us, begin %.1f us (lite %d)\n", xt1 - xt0, now_us() - xt1,
+                  (int)(c->enq == c->enq_synced));
   int64_t out[4];
   int64_t done = 0;
   if (!peer) rc = geobpe_pipeline_poll(c, out);  // (the slot sizing's largest count starts again)
@@ -2894,9 +2906,16 @@ int run_exchange_impl(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t*
         if (e != hipSuccess) rc = fail(c, GEOBPE_EHIP, "log pull: %s", hipGetErrorString(e));
       }
     }
+    const double xt2 = xt ? now_us() : 0;
     if (rc || (rc = geobpe_pipeline_poll(c, out))) break;
+    if (xt) fprintf(stderr, "xtime: batch of %lld enqueued at +%.1f us, poll %.1f us\n", (long long)k, xt2 - xt0,
+                    now_us() - xt2);
     const bool stalled = out[0] != 0, fin = out[2] != 0;
     const int64_t it = out[1], smax = out[3];
+    if (it - 1 >= lfrom && it - 1 < lfrom + ln) {  // (the next run's first decision needs no copy)
+      c->x_last = c->x_hlog[it - 1 - lfrom];
+      c->x_last_i = it - 1;
+    }
     {  // the winner count's decay over the batch (the next batch's length near a switch)
       const int64_t z = std::min<int64_t>(it - 1, lfrom + ln - 1);
       if (ln > 0 && z > lfrom && c->x_hlog[0].count > 0 && c->x_hlog[z - lfrom].count > 0)
@@ -2937,6 +2956,7 @@ int run_exchange_impl(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t*
   if (rc) return rc;  // (an error in flight is the one to report)
   if (rc_end) return rc_end;
   if (n_done) *n_done = done;
+  if (xt) fprintf(stderr, "xtime: run %.1f us\n", now_us() - xt0);
   return 0;
 }
 
