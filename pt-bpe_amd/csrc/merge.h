@@ -176,7 +176,7 @@ struct FHalf {  // a new neighbour pair of a merged occurrence
 };
 
 struct FindCtx {
-  int32_t W, nid, wl, r, par;
+  int32_t W, nid, wl, ll, r, par;  // (ll: residues of W's left part)
   u64 w1, w2;
   u64 pa1, pb1, pa2, pb2;  // P^(2 wl), P^(2 wl - 1) of both bases (the left key's right part is W)
   bool to_delta;
@@ -290,24 +290,26 @@ __device__ bool find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
                           bool& vr) {
   vl = vr = false;
   const int32_t W = F.W;
+  // round 1: g, b and c together -- an occurrence of W is L at g, R at b = g + len(L), and
+  // c = g + len(W) when b has a right neighbour (the lengths are the winner's)
+  const int32_t b = min(g + F.ll, D.R - 1), cs = min(g + F.wl, D.R - 1);
   const int4 tg = D.tok[g];  // {tid, tlen, tprev, pk}
+  const int2 tb = make_int2(*tok_f(D, b, 1), *tok_f(D, b, 3));  // {.y, .w}: length word, pk
+  const int4 tcs = make_int4(*tok_f(D, cs, 0), *tok_f(D, cs, 1), 0, *tok_f(D, cs, 3));
   if (tg.w != W) return true;
+  if (tok_len(tg.y) != F.ll) set_error(D, GEOBPE_ESTATE, g);
   dbg_stamp(D, 40);
   const int32_t p = tg.z;
-  const int32_t b = g + tok_len(tg.y);
-  // round 2: everything that depends only on (g, p, b)
+  // round 2: the run start's left context
   const int32_t ip = p >= 0 ? p : g;
   const int4 tp = D.tok[ip];
-  const int4 tb = D.tok[b];
   if (p >= 0 && tp.w == W) return true;  // not a run start: its run's start walks it
   dbg_stamp(D, 41);
   const int32_t glL = p >= 0 ? next_glue(D, tp.y, g - 1) : 0;
-  const int32_t glR = next_glue(D, tb.y, g + F.wl - 1);
-  // round 3: c, the run start's left context
-  const int32_t pkb = tb.w;
-  const int32_t c = pkb >= 0 ? b + tok_len(tb.y) : -1;
-  const int32_t ic = c >= 0 ? c : g;
-  const int4 tc = D.tok[ic];
+  const int32_t glR = next_glue(D, tb.x, g + F.wl - 1);
+  const int32_t pkb = tb.y;
+  const int32_t c = pkb >= 0 ? cs : -1;
+  const int4 tc = pkb >= 0 ? tcs : tg;
   const int32_t pp = p >= 0 ? tp.z : -1;
   const int4 tpp = D.tok[pp >= 0 ? pp : g];
   const int32_t vp = p >= 0 ? max(tp.x, 0) : 0;
@@ -333,7 +335,7 @@ __device__ bool find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
   const bool pN = p >= 0 && !pRight;
   dbg_stamp(D, 42);
   // the first occurrence (g, b)
-  emit_occ(D, F, &S.n, g, F.wl | (tb.y & (int32_t)0xFFFF0000), b, c);
+  emit_occ(D, F, &S.n, g, F.wl | (tb.x & (int32_t)0xFFFF0000), b, c);
   if (pkb >= 0) dec_add(D, F, S.u.m.agg, pkb, -1);
   if (pN) {
     dec_add(D, F, S.u.m.agg, tp.w, -1);
@@ -439,6 +441,7 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
   F.W = sel.W;
   F.nid = sel.nid;
   F.wl = sel.wl;
+  F.ll = D.vlen[sel.widL];
   F.r = r;
   F.par = par;
   F.w1 = sel.w1;
