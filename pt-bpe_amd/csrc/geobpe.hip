@@ -499,7 +499,7 @@ int tail_alloc(geobpe_ctx* c) {
 }
 
 // per-key posting lists of the live pairs, after any pending place: a counting build with a
-// global atomic per pair (k_kp_alloc / k_kp_fill).  (Round 4 A/B: a stable radix sort of the
+// global atomic per key and round of a block (k_kp_alloc / k_kp_fill).  (Round 4 A/B: a stable radix sort of the
 // (key, slot) pairs -> runs -> list space -> placement took as long, and its first call loaded
 // the sort's code object inside the loop: 25.3k vs 28.6k merges/s end to end)
 void tail_build(geobpe_ctx* c) {
@@ -512,7 +512,7 @@ void tail_build(geobpe_ctx* c) {
     hipMemsetAsync(&c->D.st->kpool_used, 0, 8, c->stream);
   }
   hipLaunchKernelGGL(k_kp_alloc, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D, c->distributed ? 0 : 1);
-  hipLaunchKernelGGL(k_kp_fill, dim3(c->nb), dim3(BLOCK), 0, c->stream, c->D);
+  hipLaunchKernelGGL(k_kp_fill, dim3(3 * c->nba), dim3(KPF_T), 0, c->stream, c->D);
   hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, c->D);  // (nothing pending)
 }
 
@@ -590,9 +590,11 @@ void tail_check_switch(geobpe_ctx* c) {
 // the middle / late regimes' arrays (per-key lists, pool, merged-occurrence and new-pair
 // lists: ~90 B per residue) reserved with the key arrays, after the bin pass, so that the
 // switch itself allocates nothing (hipMalloc + fill of ~1 GB at C3, inside the merge loop
-// otherwise).  A sharded run reserves at its collapse, for the gathered corpus.
+// otherwise).  A sharded run reserves its shard's here too (round 5 allocated them at the switch,
+// inside the sharded loop: ~1 ms at half of C3, in the N = 2 driver window) and again at its
+// collapse, for the gathered corpus.
 int regime_reserve(geobpe_ctx* c) {
-  if (c->distributed || (c->mid_thresh <= 0 && c->tail_thresh <= 0)) return 0;
+  if (c->mid_thresh <= 0 && c->tail_thresh <= 0) return 0;
   int rc;
   if ((rc = tail_alloc(c))) return rc;
   return sync_state(c);
