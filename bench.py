@@ -224,7 +224,9 @@ def main():
         # (loopback: the rank is its own peer, its records imported by content hash -- what a rank
         # of N pays for the other ranks' records; GEOBPE_PEER_LOOPBACK=0: the one-rank protocol)
         os.environ.setdefault("GEOBPE_PEER_LOOPBACK", "1")
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+        if args.shard_of > 1:  # (one rank's share of an N-way run: the N-way run's regime thresholds)
+            os.environ.setdefault("GEOBPE_XSHARDS", str(args.shard_of))
+    world =int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0")) if args.dist_backend == "nccl" else 0
     import torch

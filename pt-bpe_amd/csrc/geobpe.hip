@@ -140,6 +140,7 @@ struct geobpe_ctx {
   int32_t* x_chkcnt = nullptr;
   int64_t x_chkcap = 0;
   int64_t x_collapse_at = 32768;  // the sharded loop collapses below this count (GEOBPE_COLLAPSE_AT)
+  int64_t x_shards = 1;           // a world-1 rehearsal of one rank's share of an N-way run (GEOBPE_XSHARDS = N): N's thresholds
   // collapse at the middle-regime switch (geobpe_set_collapse): every rank then holds the whole
   // corpus and runs the one-rank loop; its own rows are [own_row0, own_row1) of it
   bool collapse_on = true, collapsed = false;
@@ -661,6 +662,7 @@ int geobpe_create(geobpe_ctx** out, int device, void* stream, int64_t max_vocab)
   if (const char* e = getenv("GEOBPE_TAIL")) c->tail_thresh = atoll(e);  // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_MID")) c->mid_thresh = atoll(e);    // (A/B: 0 = never)
   if (const char* e = getenv("GEOBPE_COLLAPSE_AT")) c->x_collapse_at = atoll(e);  // (A/B: the collapse count)
+  if (const char* e = getenv("GEOBPE_XSHARDS")) c->x_shards = std::max<int64_t>(1, atoll(e));  // (bench --shard-of N)
   if (const char* e = getenv("GEOBPE_SPEC")) c->spec = std::max(0, atoi(e));  // (A/B: 0 = no idle iterations)
   c->nb = 8 * c->nba;
   c->D.NB = c->nb;
@@ -2799,8 +2801,19 @@ int run_exchange_impl(geobpe_ctx* c, int64_t n_merges, int64_t* n_done, int64_t*
   // into the one-rank loop only below x_collapse_at, where one rank's late merge costs about what
   // a sharded merge plus its exchange does.  Both read only replicated data (the winner's global
   // count), so every rank switches at the same poll.
-  const int64_t mid_at = c->mid_thresh * W;
-  const int64_t collapse_at = peer ? c->x_collapse_at : c->mid_thresh;  // (the all-gather's ~30 us a merge: sooner)
+  // A sharded rank switches at 1.5x the one-rank threshold of its share: its full-grid merges pay
+  // the exchange per key record, and the measured crossover of the two regimes moves up (DESIGN 5:
+  // one rank's share of a 2-way run, 50-85 k occurrences, middle regime 93.5 vs full grid 94.0 us a
+  // merge with the exchange, 60 vs 70 without).  A world-1 rehearsal of one rank's share of an
+  // N-way run (x_shards = N) takes N's thresholds: its counts are the share's, the run's are N x.
+  // Two ranks stay in the full grid down to the collapse: there their middle regime does not beat it
+  // (93.5 vs 94.0 us), and the shard's list build (~1.3 ms at half of C3) would be paid again by
+  // the collapse's for the whole corpus.
+  const bool sharded = W > 1 || c->x_shards > 1;
+  const int64_t collapse_at = (peer ? c->x_collapse_at : c->mid_thresh) / (W > 1 ? 1 : c->x_shards);  // (the all-gather's ~30 us a merge: sooner)
+  const int64_t mid_at = (W == 2 || c->x_shards == 2) && c->collapse_on
+                             ? collapse_at
+                             : (sharded ? c->mid_thresh * 3 / 2 : c->mid_thresh) * W;
   if (!c->x_hlog) HIPCHK(c, hipHostMalloc((void**)&c->x_hlog, (size_t)(AHEAD_MAX + 2) * sizeof(LogRec), hipHostMallocDefault));
   const double xt1 = xt ? now_us() : 0;
   if ((rc = pipeline_begin_impl(c, true))) return rc;
