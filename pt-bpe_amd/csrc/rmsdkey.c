@@ -1125,6 +1125,122 @@ done:
   Py_RETURN_NONE;
 }
 
+/* rekey(st, cis, diff) -- the re-keying after a merge's glue re-optimisation (RmsdBPE._merge,
+ * bpe.py:2027-2071): for every chain ci of cis, every token of its btt (insertion order) but the
+ * chain's last, the key of the pair it starts is derived afresh from the re-optimised glues; a
+ * changed key moves the pair between the sets: gd[old].remove((ci, i2)), gd[new].add((ci, i2)),
+ * pk[ci][i2] = new, diff[old] - 1, diff[new] + 1.  st as merge's (its memo unused: the glues inside
+ * the tokens changed).  The Python loop it replaces ran ~45 dict / set / tuple operations a pair
+ * over every pair of every touched chain: ~3/4 of the README setting's host time a step. */
+static PyObject* rekey(PyObject* self, PyObject* args) {
+  PyObject *st, *cis, *diff;
+  (void)self;
+  if (!PyArg_ParseTuple(args, "O!O!O!", &PyTuple_Type, &st, &PyList_Type, &cis, &PyDict_Type, &diff)) return NULL;
+  MSt m;
+  PyObject* memo = NULL;
+  if (!PyArg_ParseTuple(st, "O!OO!O!OO!|O", &PyList_Type, &m.chains, &m.gd, &PyList_Type, &m.pk, &PyDict_Type, &m.edges,
+                        &m.edges_fn, &PyTuple_Type, &m.names, &memo))
+    return NULL;
+  m.memo = NULL;
+  m.diff = diff;
+  m.notes = (Notes){NULL, NULL, 0, 0};
+  int err = 0;
+  for (Py_ssize_t q = 0; q < PyList_GET_SIZE(cis) && !err; q++) {
+    const Py_ssize_t ci = PyLong_AsSsize_t(PyList_GET_ITEM(cis, q));
+    if (ci == -1 && PyErr_Occurred()) {
+      err = 1;
+      break;
+    }
+    if (ci < 0 || ci >= PyList_GET_SIZE(m.chains) || ci >= PyList_GET_SIZE(m.pk)) {
+      PyErr_SetString(PyExc_IndexError, "chain index out of range");
+      err = 1;
+      break;
+    }
+    PyObject* chain = PyList_GET_ITEM(m.chains, ci);
+    PyObject* pkrow = PyList_GET_ITEM(m.pk, ci);
+    PyObject* cols = chain_cols(&m, chain);
+    PyObject* init = PyObject_GetAttr(chain, ATTR[A_INIT]);
+    PyObject* tp = PyObject_GetAttr(chain, ATTR[A_TOKEN_POS]);
+    PyObject* btt = PyObject_GetAttr(chain, ATTR[A_BTT]);
+    PyObject* nres_o = PyObject_GetAttr(chain, ATTR[A_N]);
+    PyObject* items = NULL;
+    if (!cols || !init || !tp || !btt || !nres_o || !PyList_Check(pkrow)) {
+      if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "rmsdkey.rekey: unexpected chain state");
+      err = 1;
+    } else if (!PyList_Check(tp) || !PyDict_Check(btt) || !PyList_Check(init)) {
+      PyErr_SetString(PyExc_TypeError, "rmsdkey.rekey: unexpected chain state");
+      err = 1;
+    } else {
+      items = PyDict_Items(btt);  /* (a snapshot, as list(btt.items())) */
+      if (!items) err = 1;
+    }
+    const Py_ssize_t nres = err ? 0 : PyLong_AsSsize_t(nres_o);
+    if (!err && nres == -1 && PyErr_Occurred()) err = 1;
+    const Py_ssize_t last = 3 * nres - 1;
+    for (Py_ssize_t e = 0; !err && e < PyList_GET_SIZE(items); e++) {
+      PyObject* it = PyList_GET_ITEM(items, e);
+      PyObject* v = PyTuple_GET_ITEM(it, 1);
+      const Py_ssize_t i1 = PyLong_AsSsize_t(PyTuple_GET_ITEM(it, 0));
+      const Py_ssize_t l1 = PyTuple_Check(v) && PyTuple_GET_SIZE(v) == 3 ? PyLong_AsSsize_t(PyTuple_GET_ITEM(v, 2)) : -1;
+      if (PyErr_Occurred() || l1 < 0) {
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "rmsdkey.rekey: btt entries must be 3-tuples");
+        err = 1;
+        break;
+      }
+      if (i1 + l1 == last) continue;
+      const Py_ssize_t i2 = i1 + l1;
+      PyObject* k2 = cint(i2);
+      PyObject* v2 = k2 ? PyDict_GetItemWithError(btt, k2) : NULL;
+      if (!v2) {
+        if (k2 && !PyErr_Occurred()) key_error(k2);
+        Py_XDECREF(k2);
+        err = 1;
+        break;
+      }
+      Py_DECREF(k2);
+      const Py_ssize_t l2 = PyLong_AsSsize_t(PyTuple_GET_ITEM(v2, 2));
+      if (l2 == -1 && PyErr_Occurred()) {
+        err = 1;
+        break;
+      }
+      PyObject* old = pk_get(pkrow, i2);
+      PyObject* t = pair2(ci, i2);
+      if (!t) {
+        err = 1;
+        break;
+      }
+      if (!old) {  /* (_pk_at: KeyError((ci, i2))) */
+        key_error(t);
+        Py_DECREF(t);
+        err = 1;
+        break;
+      }
+      Py_INCREF(old);
+      PyObject* nk = mpair_key(&m, cols, init, tp, btt, nres, i1, l1, l2);
+      const int same = nk ? PyObject_RichCompareBool(nk, old, Py_EQ) : -1;
+      if (same < 0) {
+        err = 1;
+      } else if (!same) {
+        if (set_in(&m, old, t, 0) < 0 || note(&m, old, -1) < 0 || set_in(&m, nk, t, 1) < 0 || pk_set(pkrow, i2, nk) < 0 ||
+            note(&m, nk, 1) < 0)
+          err = 1;
+      }
+      Py_XDECREF(nk);
+      Py_DECREF(old);
+      Py_DECREF(t);
+    }
+    Py_XDECREF(items);
+    Py_XDECREF(cols);
+    Py_XDECREF(init);
+    Py_XDECREF(tp);
+    Py_XDECREF(btt);
+    Py_XDECREF(nres_o);
+  }
+  if (notes_flush(&m.notes, err ? NULL : diff) < 0) err = 1;
+  if (err) return NULL;
+  Py_RETURN_NONE;
+}
+
 /* prio(diff, k2p, heap, push, gd, spheres) -- step 7 of BPE.step (bpe.py:2077-2138) as
  * RmsdBPE._merge runs it: every key whose count changed leaves the priority queue and comes
  * back with its new count (flag = not partitioned, -count, key); a key whose count reached 0
@@ -1499,6 +1615,7 @@ static PyMethodDef METHODS[] = {
                                 {"memo_check", memo_check, METH_VARARGS,
                                  "memo_check(on) -> memo hits compared since the last call (test)"},
                                 {"prio", prio, METH_VARARGS, "the priority updates of a merge (RmsdBPE._merge)"},
+                                {"rekey", rekey, METH_VARARGS, "the re-keying after a glue re-optimisation (RmsdBPE._merge)"},
                                 {"packc", packc, METH_VARARGS, "pack() with spans as (chain, q, r)"},
                                 {"kmed_step", kmed_step, METH_VARARGS, "one k-medoids iteration (algo.py:191-213)"},
                                 {"packa", packa, METH_VARARGS, "pack() with spans as an int64 (n, 3) buffer"},

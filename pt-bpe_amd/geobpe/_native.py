@@ -133,7 +133,10 @@ def lib():
         "geobpe_comm_peer_active": (ctypes.c_int, [P]),
         "geobpe_collapsed": (ctypes.c_int, [P]),
     }
+    ab = bool(os.environ.get("GEOBPE_LIB"))  # (an older A/B build may lack this round's entry points)
     for name, (res, args) in sig.items():
+        if ab and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args

@@ -1063,7 +1063,12 @@ class RmsdBPE:
         if (rmsd and self.glue_opt and not self.rmsd_only and self.glue_opt_method == "all"
                 and self._step % self.glue_opt_every == 0):
             uniq = set(ci for ci, _ in occ)
-            for ci in self._glue_opt(list(uniq)):
+            cis = self._glue_opt(list(uniq))
+            if _KEYC is not None and not self._py_keys:  # (the loop below in C: csrc/rmsdkey.c rekey)
+                _KEYC.rekey((self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T, None),
+                            list(cis), diff)
+                cis = ()
+            for ci in cis:
                 btt = self._chains[ci].btt
                 pk = self._pk[ci]
                 last = 3 * self._chains[ci].n - 1

@@ -152,8 +152,13 @@ def _resolve(pcs, top=40):
 
 
 corpus = synth.make_corpus(synth.make_lengths(n, lo, hi, seed=31), seed=31)
-bpe = BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=0, rmsd_super_res=True,
-          num_partitions={2: 2, 3: 5, 5: 2, 8: 1}, max_num_strucs=500, seed=0)
+if "--readme" in sys.argv:  # (bench.py --config rmsd's setting, README.md:45, without the glue optimisation)
+    bpe = BPE(corpus, bins={1: 50}, bin_strategy="histogram", res_init=True, std_bonds=False,
+              rmsd_partition_min_size=0, rmsd_super_res=True, num_partitions={2: 2, 3: 5, 5: 1, 6: 2, 8: 1},
+              max_num_strucs=500, seed=0)
+else:
+    bpe = BPE(corpus, bins={1: 5}, res_init=True, rmsd_partition_min_size=0, rmsd_super_res=True,
+              num_partitions={2: 2, 3: 5, 5: 2, 8: 1}, max_num_strucs=500, seed=0)
 bpe.initialize()
 bpe.bin()
 bpe.run(WARM)
