@@ -313,7 +313,7 @@ void flush_place(geobpe_ctx* c) {
   Timed t(c, "place");
   if (c->place_mid) {  // token rewrites, then the posting entries, then nothing is pending
     hipLaunchKernelGGL(k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, c->stream, c->D, INT32_MIN, 0, 0);
-    hipLaunchKernelGGL(k_mid_find, dim3(MID_APP), dim3(ABLOCK), 0, c->stream, c->D, (int)(c->gen & 1), 0, 0);
+    hipLaunchKernelGGL(k_mid_find<false>, dim3(MID_APP), dim3(ABLOCK), 0, c->stream, c->D, (int)(c->gen & 1), 0, 0);
     hipLaunchKernelGGL(k_mid_flushed, dim3(1), dim3(64), 0, c->stream, c->D);
   } else {
     hipLaunchKernelGGL(k_place, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D);
@@ -414,7 +414,7 @@ void enqueue_mark(geobpe_ctx* c) {
   LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
 }
 void enqueue_apply(geobpe_ctx* c) {
-  LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
+  LAUNCH_T(c, "commit", k_commit<false>, dim3(c->nba), dim3(ABLOCK), 0, c->D, c->distributed ? 1 : 0, (int)(c->gen & 1));
   c->place_pending = true;
   c->place_mid = false;
   if (c->ev)
@@ -440,7 +440,7 @@ void enqueue_iteration_mid(geobpe_ctx* c) {
   }
   {
     const int G = c->nba - MID_APP;  // (+ the previous merge's posting entries in MID_APP more workgroups)
-    LAUNCH_T(c, "mid_find", k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, c->D, par, G, 1);
+    LAUNCH_T(c, "mid_find", k_mid_find<false>, dim3(c->nba), dim3(ABLOCK), 0, c->D, par, G, 1);
   }
   c->place_pending = true;
   c->place_mid = true;
@@ -538,7 +538,7 @@ int tail_run(geobpe_ctx* c, int64_t n) {
     c->gen += c->h_state->iter - before;  // (one launch parity per merge)
     if (c->h_state->tail_exit > 0) {  // an iteration that is no merge: rebuild / measure / done
       Timed t(c, "commit");
-      hipLaunchKernelGGL(k_commit, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 0, (int)(c->gen & 1));
+      hipLaunchKernelGGL(k_commit<false>, dim3(c->nba), dim3(ABLOCK), 0, c->stream, c->D, 0, (int)(c->gen & 1));
       c->gen++;
       HIPCHK(c, hipGetLastError());
       if ((rc = sync_state(c))) return rc;
@@ -1447,7 +1447,7 @@ int pipeline_iter_impl(geobpe_ctx* c, void* d_buf, int64_t cap_total, bool peer,
     if (c->place_pending && !c->place_mid) flush_place(c);
     c->place_pending = false;
     LAUNCH_T(c, "mid_sel", k_mid_sel, dim3(1 + c->nba), dim3(ABLOCK), 0, D, -1, run_end, nimp);
-    LAUNCH_T(c, "mid_find", k_mid_find, dim3(c->nba), dim3(ABLOCK), 0, D, -1, c->nba - MID_APP, 1);
+    LAUNCH_T(c, "mid_find", k_mid_find<true>, dim3(c->nba), dim3(ABLOCK), 0, D, -1, c->nba - MID_APP, 1);
     c->place_pending = true;
     c->place_mid = true;
     HIPCHK(c, hipGetLastError());
@@ -1461,7 +1461,7 @@ int pipeline_iter_impl(geobpe_ctx* c, void* d_buf, int64_t cap_total, bool peer,
     LAUNCH_T(c, "select", k_select, dim3(grid), dim3(SBLOCK), 0, D, -1, run_end, place ? 1 : 0, nimp);
   }
   LAUNCH_T(c, "find", k_find, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
-  LAUNCH_T(c, "commit", k_commit, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
+  LAUNCH_T(c, "commit", k_commit<true>, dim3(c->nba), dim3(ABLOCK), 0, D, 1, -1);
   c->place_pending = true;
   if (c->ev)
     hipLaunchKernelGGL(k_events, dim3(c->nba), dim3(BLOCK), 0, c->stream, c->D, -1, c->ev, c->ev_cap, c->ev_n);

@@ -810,19 +810,21 @@ __device__ inline KRec commit_key_at(const CommitLds& S, int32_t s) {
 }
 
 // a count change k_commit could not stage: a record (pipelined), the global count or the delta
+template <bool X>
 __device__ inline void commit_add(const Dev& D, int32_t d, int32_t v, bool tod) {
-  if (tod && D.xrec)
+  if (X && tod && D.xrec)
     rec_add(D, d, v);
   else
     global_add(D, d, v, tod);
 }
 
 // a record whose key did not fit the dedupe table: resolved and counted on its own
+template <bool X>
 __device__ __attribute__((always_inline)) inline void commit_fallback(const Dev& D, CommitLds& S, HotApp& hot, const KRec& k, bool tod, int32_t th) {
   const int32_t d = commit_resolve(D, S, k);
   if (d >= 0) {
     atomicAdd(&S.fbn, k.n);
-    if (tod && D.xrec)
+    if (X && tod && D.xrec)
       rec_add(D, d, k.n);
     else if (tod)
       global_add(D, d, k.n, true);
@@ -933,6 +935,7 @@ __device__ __attribute__((always_inline)) inline void commit_export(const Dev& D
   }
 }
 
+template <bool X>
 __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, int to_delta, int par) {
   __shared__ CommitLds S;
   __shared__ HotApp hot;
@@ -1062,7 +1065,7 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
       }                                                           \
       atomicAdd(&S.cn[s_], (k).n);                                \
     } else {                                                      \
-      commit_fallback(D, S, hot, (k), tod, th);                   \
+      commit_fallback<X>(D, S, hot, (k), tod, th);                   \
     }                                                             \
   } while (0)
   const bool mine0 = lane_ok && k0 < min(cK, SK);
@@ -1088,7 +1091,7 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
     x0 = t < nF ? x0r : make_int2(-1, 0);
   }
   if (mine0) COMMIT_INSERT(r0);
-  if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add(D, d0.x, d0.y, tod);
+  if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add<X>(D, d0.x, d0.y, tod);
   dbg_stamp(D, 56);
   if (he && (t < nE || owner_of_key(D, e0.pkey) == j)) COMMIT_INSERT(e0);
   for (int32_t i = t + ABLOCK; i < nE + nKO; i += ABLOCK) {  // (rare: more than ABLOCK extras)
@@ -1097,11 +1100,11 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   }
   dbg_stamp(D, 57);
   dbg_val(D, 59, nF);
-  if (t < nF && !agg_stage(S.u.agg, x0.x, x0.y)) commit_add(D, x0.x, x0.y, tod);
+  if (t < nF && !agg_stage(S.u.agg, x0.x, x0.y)) commit_add<X>(D, x0.x, x0.y, tod);
   for (int32_t i = t + ABLOCK; i < nF; i += ABLOCK) {
     const int32_t ww = seg_of(s_preF, nba, i);
     const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
-    if (!agg_stage(S.u.agg, x.x, x.y)) commit_add(D, x.x, x.y, tod);
+    if (!agg_stage(S.u.agg, x.x, x.y)) commit_add<X>(D, x.x, x.y, tod);
   }
   dbg_stamp(D, 58);
   __syncthreads();
@@ -1183,7 +1186,7 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
     if (d >= 0 && !tod) count_add_hot(D, hot, d, n, th);
     S.cid[s] = d >= 0 ? d : -2;
     if (d >= 0) {
-      if (tod && !D.xrec) touch_add(D, tb, d, n);  // (direct records: written below)
+      if (tod && !(X && D.xrec)) touch_add(D, tb, d, n);  // (direct records: written below)
       nkeys++;
     }
   }
@@ -1242,13 +1245,15 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   }
   dbg_stamp(D, 4);
   // ---- decrements of this owner's keys (multi-rank: into the touched list / the records)
-  if (tod && !D.xrec)
+  if (tod && !(X && D.xrec))
     for (int i = t; i < AggT<12>::N; i += ABLOCK) {
       const int32_t k = S.u.agg.key[i], v = S.u.agg.val[i];
       if (k >= 0 && v != 0) touch_add(D, tb, k, v);
     }
-  if (tod && !D.xrec) touch_flush(D, tb);  // (block-uniform)
-  if (tod && D.xrec) commit_export(D, S);  // (block-uniform)
+  if (tod && !(X && D.xrec)) touch_flush(D, tb);  // (block-uniform)
+  if constexpr (X) {
+    if (tod && D.xrec) commit_export(D, S);  // (block-uniform)
+  }
   hot_flush(D, hot);  // (syncs the workgroup first)
   if (t == 0) {
     D.chkcnt[j] = min(S.chk, (int32_t)D.RC);
@@ -1295,9 +1300,13 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   dbg_stamp(D, 6);
 }
 
+// X: the pipelined exchange's instantiation (the record export, the peer exchange's arrival); the
+// one-rank loop's carries none of that code (round 6's first form: +1.6 us a launch, its SGPR
+// spills 102 -> 276 from the peer pointers held for the export)
+template <bool X>
 __global__ __launch_bounds__(ABLOCK) void k_commit(Dev D, int to_delta, int par) {
-  commit_main(D, to_delta, par);
-  x_arrive(D);  // (the peer exchange: this launch's records are out, exchange.h)
+  commit_main<X>(D, to_delta, par);
+  if constexpr (X) x_arrive(D);  // (the peer exchange: this launch's records are out, exchange.h)
 }
 
 // ---------------------------------------------------------------------- k_place

@@ -250,9 +250,11 @@ __device__ inline int64_t mid_reserve(const Dev& D, int64_t* s_base, int32_t n) 
   __syncthreads();
   return *s_base;
 }
-// -v on key d: a count atomic, or a record (multi-rank)
+// -v on key d: a count atomic, or a record (multi-rank; X: the exchange's instantiation of the
+// kernel -- the one-rank kernels carry none of the record code)
+template <bool X>
 __device__ inline void mid_dec(const Dev& D, int32_t d, int32_t v) {
-  if (D.xrec)
+  if (X && D.xrec)
     mid_emit_id(D, d, v);
   else
     atomicAdd(&D.count[d], v);
@@ -261,9 +263,10 @@ __device__ inline void mid_dec(const Dev& D, int32_t d, int32_t v) {
 // -1 on key d for a destroyed pair, staged in LDS.  One rank: not on W itself -- every pair
 // of W is merged or destroyed by the merge, so the find sets count[W] = 0 once instead of
 // every workgroup decrementing it
+template <bool X>
 __device__ inline void mid_dec_agg(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t d) {
-  if (!D.xrec && d == F.W) return;
-  if (!agg_stage(S.agg, d, -1)) mid_dec(D, d, -1);
+  if (!(X && D.xrec) && d == F.W) return;
+  if (!agg_stage(S.agg, d, -1)) mid_dec<X>(D, d, -1);
 }
 
 // find-or-claim with the CAS as the first probe (an empty first slot is claimed, the key
@@ -279,6 +282,7 @@ __device__ inline int32_t mid_resolve(const Dev& D, u64 h1, u64 h2, int32_t len,
 }
 
 // a new pair resolved on its own (a run's later occurrence, or the round's table is full)
+template <bool X>
 __device__ void mid_single(const Dev& D, MidFindLds& S, const MidCtx& F, u64 h1, u64 h2, int32_t len, int32_t idL,
                            int32_t g, int32_t idR, int32_t target) {
   bool claimed;
@@ -290,7 +294,7 @@ __device__ void mid_single(const Dev& D, MidFindLds& S, const MidCtx& F, u64 h1,
   } else {
     emit_check(D, &S.chk, d, len, h1, h2);
   }
-  if (D.xrec)
+  if (X && D.xrec)
     mid_emit(D, h1, h2, len, idL, g, idR, 1, d);
   else
     count_add_hot(D, S.hot, d, 1, F.th);
@@ -318,6 +322,7 @@ __device__ inline void mid_right(const Dev& D, const MidCtx& F, int32_t t, int32
 
 // the walk of merge.h find_walk: the first occurrence's new pairs are returned (grouped
 // by the caller), a run's later occurrences resolve theirs on their own
+template <bool X>
 __device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g, MidHalf& hl, bool& vl, MidHalf& hr,
                          bool& vr) {
   vl = vr = false;
@@ -358,9 +363,9 @@ __device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g
   }
   const bool pN = p >= 0 && !pRight;
   mid_occ(D, S, F, g, F.wl | (tb.y & (int32_t)0xFFFF0000), b, c);
-  if (pkb >= 0) mid_dec_agg(D, S, F, pkb);
+  if (pkb >= 0) mid_dec_agg<X>(D, S, F, pkb);
   if (pN) {
-    mid_dec_agg(D, S, F, tp.w);
+    mid_dec_agg<X>(D, S, F, tp.w);
     combine_pw(l1, l2, glL, F.w1, F.w2, F.pa1, F.pb1, F.pa2, F.pb2, hl.h1, hl.h2);
     hl.len = tok_len(tp.y) + F.wl;
     hl.pkey = probe_key(hl.h1, hl.h2, hl.len);
@@ -393,11 +398,11 @@ __device__ void mid_walk(const Dev& D, MidFindLds& S, const MidCtx& F, int32_t g
     const int32_t vc2 = c2i >= 0 ? max(tc2.x, 0) : 0;
     const u64 d1 = D.vh1[vc2], d2 = D.vh2[vc2];
     mid_occ(D, S, F, t, F.wl | (tb2.y & (int32_t)0xFFFF0000), b2, c2i);
-    if (pkb2 >= 0) mid_dec_agg(D, S, F, pkb2);
+    if (pkb2 >= 0) mid_dec_agg<X>(D, S, F, pkb2);
     if (c2i >= 0) {
       MidHalf h;
       mid_right(D, F, t, glR2, cL2, tc2.x, tok_len(tc2.y), d1, d2, h);
-      mid_single(D, S, F, h.h1, h.h2, h.len, h.idL, h.g, h.idR, h.target);
+      mid_single<X>(D, S, F, h.h1, h.h2, h.len, h.idL, h.g, h.idR, h.target);
     }
     cur_c = c2i;
     cur_pkb = pkb2;
@@ -473,6 +478,7 @@ __device__ inline MidPre mid_pre(const Dev& D, int32_t w) {
 }
 
 // find workgroup w of G (merge parity par, decision sel)
+template <bool X>
 __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D, const Sel& sel, int par, int32_t w,
                                                                     int32_t G, MidFindLds& S, const MidPre& M) {
   State* st = D.st;
@@ -554,7 +560,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
         const int2 e = i < nl + nsg ? segp[i - nl] : spp[i - nl - nsg];
         if (e.y == F.W) g = e.x;
       }
-      if (g >= 0 && g < D.R) mid_walk(D, S, F, g, hl, vl, hr, vr);  // (a bad list entry: no out-of-range read)
+      if (g >= 0 && g < D.R) mid_walk<X>(D, S, F, g, hl, vl, hr, vr);  // (a bad list entry: no out-of-range read)
     }
     if (c0 == 0) dbg_stamp(D, 15);
     // ---- this round's new keys: LDS dedupe, then one resolve + count update per key
@@ -580,12 +586,12 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       S.rep[sr] = make_int4(hr.len, hr.idL, hr.g, hr.idR);
       S.occ[atomicAdd(&S.nocc, 1)] = sr;
     }
-    if (vl && sl < 0) mid_single(D, S, F, hl.h1, hl.h2, hl.len, hl.idL, hl.g, hl.idR, hl.target);
-    if (vr && sr < 0) mid_single(D, S, F, hr.h1, hr.h2, hr.len, hr.idL, hr.g, hr.idR, hr.target);
+    if (vl && sl < 0) mid_single<X>(D, S, F, hl.h1, hl.h2, hl.len, hl.idL, hl.g, hl.idR, hl.target);
+    if (vr && sr < 0) mid_single<X>(D, S, F, hr.h1, hr.h2, hr.len, hr.idL, hr.g, hr.idR, hr.target);
     __syncthreads();
     if (c0 == 0) dbg_stamp(D, 16);
     const int32_t nocc = S.nocc;
-    const int64_t xb = D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
+    const int64_t xb = X && D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
     for (int32_t q = t; q < nocc; q += ABLOCK) {
       const int32_t s = S.occ[q];
       const int4 rp = S.rep[s];
@@ -596,7 +602,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       const int32_t d = mid_resolve(D, h1, h2, rp.x, &claimed);
       S.did[s] = d;
       if (d < 0) {
-        if (D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, 0, -1);  // (no-op record)
+        if (X && D.xrec) mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, 0, -1);  // (no-op record)
         continue;
       }
       if (claimed) {
@@ -605,7 +611,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       } else {
         emit_check(D, &S.chk, d, rp.x, h1, h2);
       }
-      if (D.xrec)
+      if (X && D.xrec)
         mid_put(D, xb + q, h1, h2, rp.x, rp.y, rp.z, rp.w, S.cnt[s], d);
       else
         count_add_hot(D, S.hot, d, S.cnt[s], F.th);
@@ -614,7 +620,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     // key, in flight under the new pairs' grouping and the list flush (at the launch's end they
     // were the last memory operations to drain; issued before the resolves they queued ahead of
     // the resolves' atomics: merge 100 +2 us, profiles/r5_s6/)
-    if (!D.xrec && c0 + ABLOCK >= ncand)
+    if (!(X && D.xrec) && c0 + ABLOCK >= ncand)
       for (int i = t; i < AggT<11>::N; i += ABLOCK) {
         const int32_t k = S.agg.key[i], v = S.agg.val[i];
         if (k >= 0 && v != 0) atomicAdd(&D.count[k], v);
@@ -641,7 +647,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
   mid_flush_lists(D, S, F.par, w, M.kc0, M.kc1);
   dbg_stamp(D, 12);
   // ---- the decrements (one atomic per key), W's merged pairs, merge count, hot list
-  if (D.xrec) {  // as records: the nonzero slots, compacted behind one reservation
+  if (X && D.xrec) {  // as records: the nonzero slots, compacted behind one reservation
     constexpr int PER = AggT<11>::N / ABLOCK;
     static_assert(AggT<11>::N % ABLOCK == 0, "agg slots per thread");
     int32_t n = 0;
@@ -903,6 +909,7 @@ __device__ __attribute__((always_inline)) inline void mid_append_body(const Dev&
 // workgroups 0..G-1: the find of merge `par` (find = 0: none, a flush; par < 0: the
 // pipelined exchange's device parity); workgroups G..: the posting entries of the previous
 // merge (st->place_par_prev), skipping this merge's winner
+template <bool X>
 __device__ __attribute__((always_inline)) inline void mid_find_main(const Dev& D, int par, int G, int find) {
   __shared__ union {
     MidFindLds f;
@@ -921,7 +928,7 @@ __device__ __attribute__((always_inline)) inline void mid_find_main(const Dev& D
   const bool valid = st->kp_valid != 0;
   if (!find || !valid) sel.decision = SEL_STALL;
   if ((int)blockIdx.x < G) {
-    mid_find_body(D, sel, par, blockIdx.x, G, U.f, pre);
+    mid_find_body<X>(D, sel, par, blockIdx.x, G, U.f, pre);
     return;
   }
   if ((int)blockIdx.x == G && sel.decision == SEL_MERGE) mid_new_token(D, sel);
@@ -930,9 +937,12 @@ __device__ __attribute__((always_inline)) inline void mid_find_main(const Dev& D
   const int32_t skip = sel.decision == SEL_MERGE ? sel.W : -1;
   mid_append_body(D, pp, skip, blockIdx.x - G, gridDim.x - G, U.a);
 }
+// X: the pipelined exchange's instantiation (records, the peer exchange's arrival); the one-rank
+// loop's carries none of that code (round 6's first form: +1.4 us a launch from its registers)
+template <bool X>
 __global__ __launch_bounds__(ABLOCK) void k_mid_find(Dev D, int par, int G, int find) {
-  mid_find_main(D, par, G, find);
-  x_arrive(D);  // (the peer exchange: this launch's records are out, exchange.h)
+  mid_find_main<X>(D, par, G, find);
+  if constexpr (X) x_arrive(D);  // (the peer exchange: this launch's records are out, exchange.h)
 }
 
 // ---------------------------------------------------------------------- select + place

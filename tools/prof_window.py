@@ -16,7 +16,9 @@ MARK = "k_window_mark"
 
 
 def short(n):
-    return n.replace("(anonymous namespace)::", "").replace("gb::", "").split("(")[0].split("::")[-1]
+    # (a template kernel demangles with its return type and arguments: "void gb::k_commit<false>(...)")
+    n = n.replace("(anonymous namespace)::", "").replace("gb::", "").split("(")[0].split("::")[-1]
+    return n.split("<")[0].split(" ")[-1]
 
 
 def _order(r):

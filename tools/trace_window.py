@@ -9,7 +9,9 @@ import sys
 
 
 def short(n):
-    return n.replace("(anonymous namespace)::", "").replace("gb::", "").split("(")[0].split("::")[-1]
+    # (a template kernel demangles with its return type and arguments: "void gb::k_commit<false>(...)")
+    n = n.replace("(anonymous namespace)::", "").replace("gb::", "").split("(")[0].split("::")[-1]
+    return n.split("<")[0].split(" ")[-1]
 
 
 f = glob.glob(sys.argv[1] + "/**/*kernel_trace.csv", recursive=True)[0]
