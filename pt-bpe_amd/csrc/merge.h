@@ -290,14 +290,19 @@ __device__ bool find_walk(const Dev& D, FindCtx& F, FindLds& S, int32_t g, FHalf
                           bool& vr) {
   vl = vr = false;
   const int32_t W = F.W;
-  // round 1: g, b and c together -- an occurrence of W is L at g, R at b = g + len(L), and
-  // c = g + len(W) when b has a right neighbour (the lengths are the winner's)
-  const int32_t b = min(g + F.ll, D.R - 1), cs = min(g + F.wl, D.R - 1);
+  // round 1: g, b and c together -- an occurrence of W is a left part at g and a right part at
+  // b, b = g + len(L) for the winner's own split (L, R), and c = g + len(W) when b has a right
+  // neighbour (whatever the split: the pair's length is the key's)
+  const int32_t bs = min(g + F.ll, D.R - 1), cs = min(g + F.wl, D.R - 1);
   const int4 tg = D.tok[g];  // {tid, tlen, tprev, pk}
-  const int2 tb = make_int2(*tok_f(D, b, 1), *tok_f(D, b, 3));  // {.y, .w}: length word, pk
+  int2 tb = make_int2(*tok_f(D, bs, 1), *tok_f(D, bs, 3));  // {.y, .w}: length word, pk
   const int4 tcs = make_int4(*tok_f(D, cs, 0), *tok_f(D, cs, 1), 0, *tok_f(D, cs, 3));
   if (tg.w != W) return true;
-  if (tok_len(tg.y) != F.ll) set_error(D, GEOBPE_ESTATE, g);
+  int32_t b = bs;
+  if (tok_len(tg.y) != F.ll) {  // another split of W's content (a key is its content, so (AB, C) and
+    b = g + tok_len(tg.y);       // (A, BC) are one key): b from g's record, one more round here only
+    tb = make_int2(*tok_f(D, b, 1), *tok_f(D, b, 3));
+  }
   dbg_stamp(D, 40);
   const int32_t p = tg.z;
   // round 2: the run start's left context
@@ -649,7 +654,12 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
 
 // ---------------------------------------------------------------------- k_commit
 struct CommitLds;
-__device__ __attribute__((always_inline)) inline void commit_export(const Dev& D, CommitLds& S);
+struct XRes {  // an owner's record reservation (commit_export_reserve -> commit_export)
+  int32_t ex;           // this thread's first record within the owner's
+  unsigned long long b;  // the owner's base (thread 0: the returning atomic, consumed late)
+};
+__device__ __attribute__((always_inline)) inline XRes commit_export_reserve(const Dev& D, CommitLds& S);
+__device__ __attribute__((always_inline)) inline void commit_export(const Dev& D, CommitLds& S, const XRes& xr);
 struct CommitLds {
   union {
     AggT<12> agg;  // decrements of this owner's keys
@@ -882,8 +892,9 @@ __device__ __attribute__((always_inline)) inline void commit_publish(const Dev& 
 // k_find's side list -- straight into the rank's slot, one reservation per workgroup on
 // the slot header's count (final when k_commit ends: no header pass).  The import adds
 // every rank's records (this rank's included) to the replicated counts.
-__device__ __attribute__((always_inline)) inline void commit_export(const Dev& D, CommitLds& S) {  // (inlined: a call takes D's address, and the whole Dev goes to scratch)
-  __shared__ unsigned long long s_xb;
+// (two halves: the count and the reservation right after the resolves -- the returning atomic
+// then completes under the publish rounds instead of after them; the stores at the end)
+__device__ __attribute__((always_inline)) inline XRes commit_export_reserve(const Dev& D, CommitLds& S) {
   const int t = threadIdx.x;
   const int64_t nx = min(D.st->nxovf, D.KCAP);  // (k_find's; k_commit adds none)
   const int64_t x0 = nx * blockIdx.x / gridDim.x, x1 = nx * (blockIdx.x + 1) / gridDim.x;
@@ -892,10 +903,19 @@ __device__ __attribute__((always_inline)) inline void commit_export(const Dev& D
   for (int i = t; i < AggT<12>::N; i += ABLOCK) c += S.u.agg.key[i] >= 0 && S.u.agg.val[i] != 0;
   for (int64_t i = x0 + t; i < x1; i += ABLOCK) c++;
   int32_t tot;
-  const int32_t ex = block_excl_scan(c, &tot, S.red);
-  if (t == 0)
-    s_xb = tot ? atomicAdd((unsigned long long*)(D.xcnt ? D.xcnt : &D.st->ntouched), (unsigned long long)tot) : 0ULL;
+  XRes r;
+  r.ex = block_excl_scan(c, &tot, S.red);
+  r.b = t == 0 && tot ? atomicAdd((unsigned long long*)(D.xcnt ? D.xcnt : &D.st->ntouched), (unsigned long long)tot) : 0ULL;
+  return r;
+}
+__device__ __attribute__((always_inline)) inline void commit_export(const Dev& D, CommitLds& S, const XRes& xr) {  // (inlined: a call takes D's address, and the whole Dev goes to scratch)
+  __shared__ unsigned long long s_xb;
+  const int t = threadIdx.x;
+  const int64_t nx = min(D.st->nxovf, D.KCAP);
+  const int64_t x0 = nx * blockIdx.x / gridDim.x, x1 = nx * (blockIdx.x + 1) / gridDim.x;
+  if (t == 0) s_xb = xr.b;
   __syncthreads();
+  const int32_t ex = xr.ex;
   int64_t j = (int64_t)s_xb + ex;
   for (int32_t s = t; s < CKC; s += ABLOCK) {
     if (S.ckey[s] == 0 || S.cid[s] < 0) continue;
@@ -1190,6 +1210,10 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
       nkeys++;
     }
   }
+  XRes xres{0, 0ULL};
+  if constexpr (X) {
+    if (tod && D.xrec) xres = commit_export_reserve(D, S);  // (block-uniform: every key resolved, the decrements staged)
+  }
   // ---- decrements of this owner's keys: one atomic per key, in flight under the log
   // reservation and the publish round (a decrement cannot hide a theta crossing: a positive
   // add that follows sees less; before the resolves they queued ahead of them)
@@ -1252,7 +1276,7 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
     }
   if (tod && !(X && D.xrec)) touch_flush(D, tb);  // (block-uniform)
   if constexpr (X) {
-    if (tod && D.xrec) commit_export(D, S);  // (block-uniform)
+    if (tod && D.xrec) commit_export(D, S, xres);  // (block-uniform)
   }
   hot_flush(D, hot);  // (syncs the workgroup first)
   if (t == 0) {

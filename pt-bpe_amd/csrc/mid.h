@@ -548,6 +548,8 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
   }
   __syncthreads();
   dbg_stamp(D, 11);
+  int64_t xdec_base = -1;  // (X: the decrement records' base, reserved with the last round's)
+  int32_t xdec_ex = 0;
   for (int64_t c0 = 0; c0 < ncand; c0 += ABLOCK) {  // block-uniform rounds, one candidate per thread
     const int64_t i = c0 + t;
     MidHalf hl, hr;
@@ -591,7 +593,29 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
     __syncthreads();
     if (c0 == 0) dbg_stamp(D, 16);
     const int32_t nocc = S.nocc;
-    const int64_t xb = X && D.xrec ? mid_reserve(D, &S.xbase, nocc) : 0;  // (one record per slot)
+    int64_t xb = 0;  // (one record per slot)
+    if constexpr (X) {
+      if (D.xrec) {
+        if (c0 + ABLOCK >= ncand) {  // the last round: the decrement records (every walk is done, so
+          // the staging is final) and W's own record go in the same reservation -- no second
+          // returning atomic at the launch's end
+          constexpr int PER = AggT<11>::N / ABLOCK;
+          int32_t n = 0;
+#pragma unroll
+          for (int u = 0; u < PER; u++) {
+            const int i = t + u * ABLOCK;
+            n += S.agg.key[i] >= 0 && S.agg.val[i] != 0;
+          }
+          const int32_t own = t == 0 && S.nm ? 1 : 0;
+          int32_t tot;
+          xdec_ex = block_excl_scan(n + own, &tot, S.red);
+          xb = mid_reserve(D, &S.xbase, nocc + tot);
+          xdec_base = xb + nocc;
+        } else {
+          xb = mid_reserve(D, &S.xbase, nocc);
+        }
+      }
+    }
     for (int32_t q = t; q < nocc; q += ABLOCK) {
       const int32_t s = S.occ[q];
       const int4 rp = S.rep[s];
@@ -657,9 +681,14 @@ __device__ __attribute__((always_inline)) inline void mid_find_body(const Dev& D
       n += S.agg.key[i] >= 0 && S.agg.val[i] != 0;
     }
     const int32_t own = t == 0 && S.nm ? 1 : 0;
-    int32_t tot;
-    const int32_t ex = block_excl_scan(n + own, &tot, S.red);
-    int64_t j = mid_reserve(D, &S.xbase, tot) + ex;
+    int64_t j;
+    if (xdec_base >= 0) {  // (reserved with the last round's records)
+      j = xdec_base + xdec_ex;
+    } else {  // (no round: no candidate)
+      int32_t tot;
+      const int32_t ex = block_excl_scan(n + own, &tot, S.red);
+      j = mid_reserve(D, &S.xbase, tot) + ex;
+    }
     if (own) mid_put_id(D, j++, F.W, -S.nm);
 #pragma unroll
     for (int u = 0; u < PER; u++) {
