@@ -1125,25 +1125,17 @@ done:
   Py_RETURN_NONE;
 }
 
-/* rekey(st, cis, diff[, masks]) -- the re-keying after a merge's glue re-optimisation (RmsdBPE._merge,
+/* rekey(st, cis, diff) -- the re-keying after a merge's glue re-optimisation (RmsdBPE._merge,
  * bpe.py:2027-2071): for every chain ci of cis, every token of its btt (insertion order) but the
  * chain's last, the key of the pair it starts is derived afresh from the re-optimised glues; a
  * changed key moves the pair between the sets: gd[old].remove((ci, i2)), gd[new].add((ci, i2)),
- * pk[ci][i2] = new, diff[old] - 1, diff[new] + 1.  masks[q]: chain cis[q]'s residues whose glue the
- * re-optimisation changed (_glue_opt's `changed`); a pair with none within one residue of its span
- * keeps its key and is not derived again.  st as merge's (its memo unused: the glues inside
+ * pk[ci][i2] = new, diff[old] - 1, diff[new] + 1.  st as merge's (its memo unused: the glues inside
  * the tokens changed).  The Python loop it replaces ran ~45 dict / set / tuple operations a pair
  * over every pair of every touched chain: ~3/4 of the README setting's host time a step. */
 static PyObject* rekey(PyObject* self, PyObject* args) {
-  PyObject *st, *cis, *diff, *masks = NULL;
+  PyObject *st, *cis, *diff;
   (void)self;
-  if (!PyArg_ParseTuple(args, "O!O!O!|O!", &PyTuple_Type, &st, &PyList_Type, &cis, &PyDict_Type, &diff, &PyList_Type,
-                        &masks))
-    return NULL;
-  if (masks && PyList_GET_SIZE(masks) != PyList_GET_SIZE(cis)) {
-    PyErr_SetString(PyExc_ValueError, "rmsdkey.rekey: one residue mask per chain");
-    return NULL;
-  }
+  if (!PyArg_ParseTuple(args, "O!O!O!", &PyTuple_Type, &st, &PyList_Type, &cis, &PyDict_Type, &diff)) return NULL;
   MSt m;
   PyObject* memo = NULL;
   if (!PyArg_ParseTuple(st, "O!OO!O!OO!|O", &PyList_Type, &m.chains, &m.gd, &PyList_Type, &m.pk, &PyDict_Type, &m.edges,
@@ -1185,25 +1177,6 @@ static PyObject* rekey(PyObject* self, PyObject* args) {
     const Py_ssize_t nres = err ? 0 : PyLong_AsSsize_t(nres_o);
     if (!err && nres == -1 && PyErr_Occurred()) err = 1;
     const Py_ssize_t last = 3 * nres - 1;
-    /* the chain's changed-residue mask as prefix counts (NULL: every pair is derived afresh) */
-    Py_ssize_t* pre = NULL;
-    Py_buffer mb;
-    int have_mb = 0;
-    if (!err && masks) {
-      if (PyObject_GetBuffer(PyList_GET_ITEM(masks, q), &mb, PyBUF_SIMPLE) < 0) {
-        err = 1;
-      } else {
-        have_mb = 1;
-        pre = PyMem_Malloc((size_t)(mb.len + 1) * sizeof *pre);
-        if (!pre) {
-          PyErr_NoMemory();
-          err = 1;
-        } else {
-          pre[0] = 0;
-          for (Py_ssize_t r = 0; r < mb.len; r++) pre[r + 1] = pre[r] + (((const unsigned char*)mb.buf)[r] != 0);
-        }
-      }
-    }
     for (Py_ssize_t e = 0; !err && e < PyList_GET_SIZE(items); e++) {
       PyObject* it = PyList_GET_ITEM(items, e);
       PyObject* v = PyTuple_GET_ITEM(it, 1);
@@ -1229,13 +1202,6 @@ static PyObject* rekey(PyObject* self, PyObject* args) {
       if (l2 == -1 && PyErr_Occurred()) {
         err = 1;
         break;
-      }
-      if (pre) {  /* the key reads the span's bonds [i1, i2 + l2) -- residues i1 / 3 .. (i2 + l2 - 1) / 3
-                   * -- and at most their neighbours: no changed glue there, the same key */
-        Py_ssize_t lo = i1 / 3 - 1, hi = (i2 + l2 - 1) / 3 + 1;
-        lo = lo < 0 ? 0 : lo;
-        hi = hi >= mb.len ? mb.len - 1 : hi;
-        if (hi < lo || pre[hi + 1] - pre[lo] == 0) continue;
       }
       PyObject* old = pk_get(pkrow, i2);
       PyObject* t = pair2(ci, i2);
@@ -1269,8 +1235,6 @@ static PyObject* rekey(PyObject* self, PyObject* args) {
     Py_XDECREF(tp);
     Py_XDECREF(btt);
     Py_XDECREF(nres_o);
-    PyMem_Free(pre);
-    if (have_mb) PyBuffer_Release(&mb);
   }
   if (notes_flush(&m.notes, err ? NULL : diff) < 0) err = 1;
   if (err) return NULL;

@@ -134,9 +134,6 @@ RES_SPHERE_KEY = {3: '{"N:CA": [0], "CA:C": [0], "0C:1N": [0], "tau": [0], "CA:C
 _LEFT = {}
 
 
-_REKEY_VERIFY = os.environ.get("GEOBPE_REKEY_VERIFY") == "1"  # (tests / tools: check the masked re-keying)
-
-
 def _pk_at(pk, ci, i):
     """The stored key of the pair starting at bond i of chain ci (pk: that chain's list);
     KeyError((ci, i)) when no pair starts there, as the reference's dict lookup raises."""
@@ -727,15 +724,12 @@ class RmsdBPE:
             self._glue_prior = G.prior_tables([self._thresholds[s0] for s0 in sizes], [counts[s0] for s0 in sizes])
         return self._glue_prior
 
-    def _glue_opt(self, cis, chains=None, frames=None, changed=None):
+    def _glue_opt(self, cis, chains=None, frames=None):
         """_opt_glue_worker + opt_glue (bpe.py:739-807) for the chains cis (or the given
         chain objects and their cached frames), as one device launch: glue k = (omega_k,
         C:1N:1CA_k, phi_{k+1}) of every initial token but the last, started from the current
         values, aimed at exit frame (start + length) // 3 - 1 of the cached chain; the optimum
-        snapped to grid(3n - 4)'s bins and written back.  Returns cis.  changed (a list): gets, per
-        chain, a uint8 mask over its residues marking those whose written glue differs from the
-        value it replaced (NaN counts as changed) -- a pair key reads only its span's residues and
-        their neighbours, so a pair with no changed residue near it keeps its key (rekey)."""
+        snapped to grid(3n - 4)'s bins and written back.  Returns cis."""
         from . import glue as G
         cis = list(cis)
         if chains is None:
@@ -765,20 +759,11 @@ class RmsdBPE:
         for c, opt, gk in zip(chains, outs, grids):
             thr = self._thresholds[gk]
             om, cn, ph = (G.snap_many(thr[k], opt[:, t]).tolist() for t, k in enumerate(G.GLUE))
-            co, cc, cp = c.cur["omega"], c.cur["C:1N:1CA"], c.cur["phi"]
-            mask = np.zeros(c.n + 1, np.uint8) if changed is not None else None
             for k, (i, _, ln) in enumerate(c.tokens0[:-1]):
                 row = (i + ln) // 3 - 1
-                if mask is not None:
-                    if not (co[row] == om[k] and cc[row] == cn[k]):
-                        mask[row] = 1
-                    if not cp[row + 1] == ph[k]:
-                        mask[row + 1] = 1
-                co[row] = om[k]
-                cc[row] = cn[k]
-                cp[row + 1] = ph[k]
-            if changed is not None:
-                changed.append(mask)
+                c.cur["omega"][row] = om[k]
+                c.cur["C:1N:1CA"][row] = cn[k]
+                c.cur["phi"][row + 1] = ph[k]
         return cis
 
     def _partition_residues(self, n, size, occ):
@@ -1078,17 +1063,10 @@ class RmsdBPE:
         if (rmsd and self.glue_opt and not self.rmsd_only and self.glue_opt_method == "all"
                 and self._step % self.glue_opt_every == 0):
             uniq = set(ci for ci, _ in occ)
-            masks = []
-            cis = self._glue_opt(list(uniq), changed=masks)
-            if _KEYC is not None and not self._py_keys:  # (the loop below in C: csrc/rmsdkey.c rekey,
-                # which derives afresh only the keys of pairs near a residue whose glue changed)
-                st = (self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T, None)
-                _KEYC.rekey(st, list(cis), diff, masks)
-                if _REKEY_VERIFY:  # (every pair derived again, unmasked: no key may have been missed)
-                    d2 = {}
-                    _KEYC.rekey(st, list(cis), d2)
-                    if d2:
-                        raise AssertionError(f"rekey's residue masks missed {len(d2)} key changes")
+            cis = self._glue_opt(list(uniq))
+            if _KEYC is not None and not self._py_keys:  # (the loop below in C: csrc/rmsdkey.c rekey)
+                _KEYC.rekey((self._chains, gd, self._pk, self._key_edges, self._edges_store, _KEY_ORDER_T, None),
+                            list(cis), diff)
                 cis = ()
             for ci in cis:
                 btt = self._chains[ci].btt

@@ -488,15 +488,6 @@ def test_rmsd_mode_glue_opt_host_logic_matches_reference(name, host_glue):
         assert bpe.glue_calls == 1 + len(_load(name)[0].get("induce", []))
 
 
-def test_rekey_residue_masks_miss_no_key(host_glue, monkeypatch):
-    """The re-keying after a glue re-optimisation (rmsdkey.rekey) derives afresh only the pairs
-    within one residue of a glue the re-optimisation changed: every re-keying is followed by an
-    unmasked one, which must find no other key change -- and the run stays the reference's."""
-    from geobpe import rmsd_bpe
-    monkeypatch.setattr(rmsd_bpe, "_REKEY_VERIFY", True)
-    run_and_compare("gl_all_p0")
-
-
 @pytest.mark.skipif(os.environ.get("GEOBPE_SLOW_TESTS") != "1", reason="~20 min on one CPU core (GEOBPE_SLOW_TESTS=1)")
 @pytest.mark.parametrize("name", PARETO + HELD_OUT)
 def test_rmsd_mode_pareto_host_logic_matches_reference(name, host_glue):

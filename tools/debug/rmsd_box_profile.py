@@ -16,8 +16,9 @@ import torch  # noqa: E402,F401  (the HIP runtime shared with torch)
 from geobpe import synth  # noqa: E402
 from geobpe.bpe import BPE  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 2000
-steps = int(sys.argv[2]) if len(sys.argv) > 2 else 60
+argv = [a for a in sys.argv[1:] if not a.startswith("--")]
+n = int(argv[0]) if len(argv) > 0 else 2000
+steps = int(argv[1]) if len(argv) > 1 else 60
 corpus = synth.make_corpus(synth.make_lengths(n, 40, 560, seed=0), seed=0)
 bpe = BPE(corpus, bins={1: 50}, bin_strategy="histogram", res_init=True, std_bonds=False,
           rmsd_partition_min_size=0, rmsd_super_res=True, num_partitions={2: 2, 3: 5, 5: 1, 6: 2, 8: 1},
