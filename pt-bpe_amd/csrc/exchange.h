@@ -112,7 +112,7 @@ __device__ inline void x_claim_payload(const Dev& D, int32_t slot, const DeltaRe
 struct XImpLds {
   HotApp hot;
   int64_t pre[XPEER_MAX + 1];  // record prefix over the ranks
-  int32_t ns, go, bad, chk;
+  int32_t ns, go, bad, chk, half;
 };
 
 // a claimed key of import workgroup b joins klist at the end (region b of D.ns)
@@ -126,7 +126,11 @@ __device__ inline void x_note_claim(const Dev& D, XImpLds& X, int32_t b, int32_t
 
 // a key the import found (not claimed) is checked against its stored content by the next import
 // of the same workgroup index: another import workgroup of this launch may have claimed it and
-// not yet written the content (the deferred check of k_import_fixed's emit_check)
+// not yet written the content (the deferred check of k_import_fixed's emit_check).  The regions
+// come in two halves by the import's producer sequence number (h = seq & 1): an import writes
+// half h and, after its arrival -- off the select's path -- checks half h ^ 1, the last import's
+// (round 6's first form checked first: three dependent rounds before every import's own loads)
+__device__ inline int64_t x_chk_region(const Dev& D, int32_t h, int32_t b) { return (int64_t)h * D.NBA + b; }
 __device__ inline void x_note_found(const Dev& D, XImpLds& X, int32_t b, int32_t d, const DeltaRec& r) {
   const int32_t j = atomicAdd(&X.chk, 1);
   if (j < D.xchkcap) {
@@ -137,18 +141,21 @@ __device__ inline void x_note_found(const Dev& D, XImpLds& X, int32_t b, int32_t
     e.delta = 0;
     e.h1 = r.h1;
     e.h2 = r.h2;
-    D.xchk[(int64_t)b * D.xchkcap + j] = e;
+    D.xchk[x_chk_region(D, X.half, b) * D.xchkcap + j] = e;
   } else {
     atomicAdd((unsigned long long*)&D.st->nunchecked, 1ULL);
   }
 }
-// the previous import's found keys of region b, against the key table (EHASH)
-__device__ inline void x_check_region(const Dev& D, int32_t b) {
-  const int32_t n = min(D.xchkcnt[b], (int32_t)D.xchkcap);
+// an import's found keys (region r = x_chk_region), against the key table (EHASH); the region is
+// then empty (block-uniform)
+__device__ inline void x_check_region(const Dev& D, int64_t r) {
+  const int32_t n = min(D.xchkcnt[r], (int32_t)D.xchkcap);
   for (int32_t i = threadIdx.x; i < n; i += blockDim.x) {
-    const NewPair e = D.xchk[(int64_t)b * D.xchkcap + i];
+    const NewPair e = D.xchk[r * D.xchkcap + i];
     if (!key_is(D, e.target, e.h1, e.h2, e.len)) set_error(D, GEOBPE_EHASH, -81);
   }
+  __syncthreads();  // (every thread has read the count)
+  if (threadIdx.x == 0 && n > 0) D.xchkcnt[r] = 0;
 }
 
 // a relaxed system-scope load (a record another device stored: not through a stale L2 line)
@@ -185,14 +192,17 @@ __device__ void x_import_share(const Dev& D, XImpLds& X, int32_t b, int32_t nb, 
   if (t == 0) {
     X.go = D.xw > 0 && st->xpend != 0;  // (stable for the whole launch: only the finish clears it)
     X.bad = st->stall != 0;
+    X.half = st->xpseq & 1;
     X.ns = 0;
     X.chk = 0;
   }
   hot_init(X.hot);
-  if (D.xw > 0) x_check_region(D, b);  // (the previous import's found keys: their claims are complete)
   __syncthreads();
-  if (!X.go) {
-    if (t == 0 && D.xw > 0) D.xchkcnt[b] = 0;
+  if (!X.go) {  // (no import: both halves' found keys checked now -- their claims are complete)
+    if (D.xw > 0) {
+      x_check_region(D, x_chk_region(D, 0, b));
+      x_check_region(D, x_chk_region(D, 1, b));
+    }
     return;
   }
   const int32_t W = D.xw, par = st->xppar, seq = st->xpseq;
@@ -258,13 +268,16 @@ __device__ void x_import_share(const Dev& D, XImpLds& X, int32_t b, int32_t nb, 
     __syncthreads();
     for (int32_t i = t; i < m; i += ABLOCK) klist_put(D, s_base + i, D.ns[(int64_t)b * D.RC + i]);
   }
-  if (t == 0) D.xchkcnt[b] = min(X.chk, (int32_t)D.xchkcap);
+  if (t == 0) D.xchkcnt[x_chk_region(D, X.half, b)] = min(X.chk, (int32_t)D.xchkcap);
   __builtin_amdgcn_s_waitcnt(0);  // (this wave's stores and atomics complete)
   __syncthreads();
   if (t == 0) {
     const int32_t a = __hip_atomic_fetch_add(&st->xiarr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (last_finishes && a == nb - 1) x_import_finish(D);
   }
+  // the last import's found keys (the other half): their claims are complete since that launch
+  // ended -- checked after the arrival, while the select works
+  x_check_region(D, x_chk_region(D, X.half ^ 1, b));
 }
 
 // the select workgroup: wait for the nb import workgroups of its launch (bounded: a protocol
@@ -298,9 +311,8 @@ __device__ inline bool x_import_wait(const Dev& D, bool pending, int32_t nb) {
 // the end of a peer-exchange run: every import region's found keys checked (the imports of the
 // next run would check them otherwise)
 __global__ __launch_bounds__(ABLOCK) void k_xcheck(Dev D) {
-  x_check_region(D, blockIdx.x);
-  __syncthreads();
-  if (threadIdx.x == 0) D.xchkcnt[blockIdx.x] = 0;
+  x_check_region(D, x_chk_region(D, 0, blockIdx.x));
+  x_check_region(D, x_chk_region(D, 1, blockIdx.x));
 }
 
 // the drain at the end of a batch: the last producer launch's records, imported on their own

@@ -2482,7 +2482,7 @@ int x_peer_setup(geobpe_ctx* c, int64_t capf) {
   memset(&mine, 0, sizeof mine);
   if (ok) ok = hipMalloc((void**)&c->x_recv, (size_t)(2 * W * c->x_slot)) == hipSuccess;
   c->x_chkcap = (W * capf + c->nba - 2) / std::max(1, c->nba - 1) + 64;  // (one import share of every rank's slot)
-  if (ok) ok = !dalloc(c, &c->x_chk, (int64_t)c->nba * c->x_chkcap) && !dalloc(c, &c->x_chkcnt, c->nba, 0);
+  if (ok) ok = !dalloc(c, &c->x_chk, 2 * (int64_t)c->nba * c->x_chkcap) && !dalloc(c, &c->x_chkcnt, 2 * c->nba, 0);  // (two halves, exchange.h)
   if (ok) ok = hipMemsetAsync(c->x_recv, 0, (size_t)(2 * W * c->x_slot), c->stream) == hipSuccess &&
                hipStreamSynchronize(c->stream) == hipSuccess;
   if (ok && W > 1) ok = hipIpcGetMemHandle(&mine, c->x_recv) == hipSuccess;
