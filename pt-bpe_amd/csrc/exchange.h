@@ -6,19 +6,21 @@
 // Round 3-5 moved them with one ncclAllGather of fixed slots per merge plus an import kernel:
 // two more stream operations and their gaps, ~30 us per heavy merge at world 1.  Here the
 // records travel inside the kernels that make them:
-//   producer (k_commit / k_mid_find): record j of this rank is stored into rank q's receive
-//     area at [parity][this rank] for every q != this rank (x_put_rec, device.h) -- IPC-mapped
-//     device memory, xGMI stores on a node, no collective; each workgroup fences its stores at
-//     system scope and arrives on a counter, and the last to arrive stores the slot header
-//     {count, seq} into every peer's area (release, system scope): x_arrive
-//   wait: the host enqueues hipStreamWaitValue32 on every peer's header seq of the previous
-//     launch before the next select launch (the command processor waits; no workgroup spins on
-//     another process, so ranks sharing one GPU cannot starve each other)
-//   import (the next select launch's place workgroups, before their place work): every rank's
-//     records of that launch -- this rank's own from its local list by key id, the others' from
-//     the receive slots, found or claimed by content hash -- added to the counts with the
-//     hot-list check: x_import_share; the select workgroup waits for them (a counter of the
-//     same launch) before its argmax
+//   producer (k_commit / k_mid_find, their exchange instantiations): record j of this rank is
+//     stored into rank q's receive area at [parity][this rank] for every q != this rank
+//     (x_put_rec, device.h) -- IPC-mapped device memory, xGMI stores on a node, write-through
+//     (relaxed system-scope 8-B stores: nothing dirty left in an XCD's L2), no collective; the
+//     rank's own deltas are applied at once by the producer.  Each workgroup waits for its stores
+//     (s_waitcnt 0) and arrives on a counter; the last to arrive issues one system-scope release
+//     and stores the slot header {count, seq} into every peer's area: x_arrive
+//   wait: before the next select launch the host enqueues hipStreamWaitValue32 on the peer's
+//     header seq (two ranks: the command processor waits) or one one-wave k_xwait kernel spinning
+//     on every peer's (three or more: one launch instead of a stream wait per peer); bounded
+//   import (the next select launch's place workgroups, before their place work): the other
+//     ranks' records of that launch, found or claimed by content hash, added to the counts with
+//     the hot-list check: x_import_share; the select workgroup waits for them (a counter of the
+//     same launch) before its argmax.  A world-1 rehearsal (x_loop) stores its own records into
+//     its own slot and imports them the same way
 // A header count past the slot's capacity stalls every rank's pipeline (they all read the same
 // headers); the host then re-exchanges that merge in full (x_resolve) and releases it.
 #pragma once
