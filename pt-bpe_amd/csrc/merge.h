@@ -890,8 +890,8 @@ __device__ __attribute__((always_inline)) inline void commit_publish(const Dev& 
 // pipelined exchange: this owner's delta records -- every resolved key with its
 // occurrence total, every decremented key with its (negative) total, and its share of
 // k_find's side list -- straight into the rank's slot, one reservation per workgroup on
-// the slot header's count (final when k_commit ends: no header pass).  The import adds
-// every rank's records (this rank's included) to the replicated counts.
+// the slot header's count (final when k_commit ends: no header pass).  The producer applies
+// its own rank's deltas at once (x_put_rec); the imports add the other ranks' records.
 // (two halves: the count and the reservation right after the resolves -- the returning atomic
 // then completes under the publish rounds instead of after them; the stores at the end)
 __device__ __attribute__((always_inline)) inline XRes commit_export_reserve(const Dev& D, CommitLds& S) {
@@ -928,7 +928,7 @@ __device__ __attribute__((always_inline)) inline void commit_export(const Dev& D
     r.g = rp.z;
     r.idR = rp.w;
     r.delta = S.cn[s];
-    r.pad = S.cid[s] + 1;  // (the import of this rank's own slot uses it instead of probing)
+    r.pad = S.cid[s] + 1;  // (this rank's key id: x_put_rec applies the delta by it, no probe)
     x_put_rec(D, j, r, -30);
     j++;
   }

@@ -205,8 +205,8 @@ __device__ inline void mid_flush_lists(const Dev& D, MidFindLds& S, int par, int
 }
 
 // multi-rank (D.xrec set, the pipelined exchange): count changes go out as delta records
-// (the import adds every rank's, this rank's included, with the hot-list check); the
-// record carries this rank's key id (pad = id + 1: no probe on import).  Records are
+// (the producer applies its own with the hot-list check, the other ranks' imports probe by
+// content); the record carries this rank's key id (pad = id + 1: the producer's own add).  Records are
 // reserved per workgroup phase (mid_reserve) where the count is known, one wave at a time
 // only on the rare paths (a run's later occurrences, a full LDS table).
 __device__ inline unsigned long long* mid_xcnt(const Dev& D) {
