@@ -316,7 +316,8 @@ int geobpe_comm_set_slot(geobpe_ctx *ctx, int64_t records);
 /* The peer exchange (default on for up to 8 ranks; off: the all-gather of fixed slots): every
  * rank's receive area is IPC-mapped into every other rank once, the merge kernels store their
  * delta records straight into the peers' areas and publish a {count, seq} header, the stream
- * waits for the peers' headers (hipStreamWaitValue32) and the next select launch imports them.
+ * waits for the peers' headers (hipStreamWaitValue32 with two ranks, a one-wave waiter kernel with
+ * more; bounded) and the next select launch imports them.
  * GEOBPE_PEER=0 in the environment turns it off too.  Set before the first geobpe_run_exchange.
  * (No reference counterpart: the reference has no multi-GPU path) */
 int geobpe_comm_peer(geobpe_ctx *ctx, int on);
