@@ -8,8 +8,11 @@ covers the config's 1000 merges.  The prologue (thresholds, quantisation,
 labels) and the initial histogram (BPE.bin) run before the timed region and are
 reported separately.  Inputs are resident in HBM when the timer starts.
 
-N > 1: one rank per GPU (RCCL); the corpus is row-sharded (same 100k chains in
-total: strong scaling), the ranks exchange count deltas once per iteration.
+N > 1: one rank per GPU (RCCL); from geobpe.dist.SHARD_MIN_RANKS ranks the corpus
+is row-sharded (same 100k chains in total: strong scaling) and the ranks exchange
+count deltas once per iteration; below it sharding measured slower than one GPU
+alone, so the ranks run as replicas (the whole corpus each, the same merges,
+checked equal; the value is the job's merge rate, not N times it).
 Launched by torch.distributed.run (WORLD_SIZE set: it must equal --gpus), or as
 plain ``python bench.py --gpus N``: the parent then starts torch.distributed.run
 with N ranks as a child process before anything touches the GPU and exits with
@@ -232,7 +235,7 @@ def main():
     import torch
     import torch.distributed as dist
     from geobpe import synth
-    from geobpe.dist import TorchGroup, shard_rows, slice_corpus
+    from geobpe.dist import TorchGroup, rank_plan, shard_rows, slice_corpus
     from geobpe.engine import GeoBPEEngine
 
     torch.cuda.set_device(local)
@@ -257,7 +260,8 @@ def main():
     if args.shard_of > 1 and world == 1:  # (one rank's share of an N-way run, alone on the GPU)
         lo_r, hi_r = shard_rows(corpus["row_off"], args.shard_of)[0]
         shard = slice_corpus(corpus, lo_r, hi_r)
-    if world > 1 or args.force_exchange:
+    plan = rank_plan(world)  # (below SHARD_MIN_RANKS the ranks are replicas: the whole corpus each)
+    if (world > 1 and plan == "shard") or args.force_exchange:
         if world > 1:
             lo_r, hi_r = shard_rows(corpus["row_off"], world)[rank]
             shard = slice_corpus(corpus, lo_r, hi_r)
@@ -313,6 +317,10 @@ def main():
         rr = [None] * world
         dist.all_gather_object(rr, R_local)
         rank_res = [int(x) for x in rr]
+        if plan == "replicate":  # (replicas: every rank made the same merges, or the line is void)
+            mm = [None] * world
+            dist.all_gather_object(mm, merges_log)
+            assert all(m == merges_log for m in mm), "replica ranks made different merges"
     merge_list = eng.merge_keys() if args.emit_merges else None
     if rank != 0:
         if world > 1:
@@ -505,7 +513,8 @@ def main():
                                 + f": {n} synthetic chains, len U{{{lo}..{hi}}}, {R_total} residues, "
                                 f"bins {{1: {B}}}, merges {args.warmup + 1}..{args.warmup + done}")
                    if args.config in ("c3", "c5") else f"BASELINE configs[1]: {n}x{lo}, bins {{1: {B}}}",
-                   "chains": n, "residues": R_total, "bins": B, "parallelism": f"rows{world}",
+                   "chains": n, "residues": R_total, "bins": B,
+                   "parallelism": f"{'replicas' if world > 1 and plan == 'replicate' else 'rows'}{world}",
                    "rank_residues": rank_res, "backend": (args.dist_backend if world > 1 else None),
                    **({"shard_of": args.shard_of} if args.shard_of > 1 else {}),
                    **({"exchange": "rehearsal (world 1)" + (", all-gather" if os.environ.get("GEOBPE_PEER") == "0"

@@ -27,6 +27,27 @@ from .engine import GeoBPEEngine, ANGLE_TYPES
 
 REC = _native.DELTA_RECORD_BYTES
 
+# The fewest ranks at which row sharding beats every rank running the whole corpus alone.  One
+# rank's share with the peer exchange (loopback), against the whole corpus on the same GPU, on
+# the driver window (profiles/r6_final/suite/fx_w{2,4,8}.json): 1/2 0.81 x, 1/4 1.08 x,
+# 1/8 1.28 x.  Below it the ranks are replicas: each holds the whole corpus and runs the one-rank
+# loop, so the job runs at the one-GPU rate instead of 0.8 x of it.
+SHARD_MIN_RANKS = 4
+
+
+def rank_plan(world: int) -> str:
+    """'shard' (rows split over the ranks, the peer exchange) or 'replicate' (every rank the
+    whole corpus, no exchange) for a run of `world` ranks.  GEOBPE_RANK_PLAN=shard|replicate
+    overrides the measured choice (rehearsals, tests)."""
+    import os
+
+    forced = os.environ.get("GEOBPE_RANK_PLAN")
+    if forced is not None:
+        if forced not in ("shard", "replicate"):
+            raise ValueError(f"GEOBPE_RANK_PLAN must be 'shard' or 'replicate', not {forced!r}")
+        return forced if world > 1 else "replicate"
+    return "shard" if world >= SHARD_MIN_RANKS else "replicate"
+
 
 def shard_rows(row_off: np.ndarray, world: int) -> list:
     """Contiguous chain blocks [(row_lo, row_hi)] with ~equal residue counts."""

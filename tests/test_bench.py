@@ -41,15 +41,19 @@ def test_gpus_must_be_positive():
 
 
 @pytest.mark.gpu
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_gpus2_without_launcher_runs_two_ranks():
     """`bench.py --gpus 2` with no launcher: two rank processes (gloo, both on GPU 0 --
     the one-GPU rehearsal of the RCCL path), n_gpus 2, and the merge list of the
-    1-rank run."""
+    1-rank run -- as replicas (rank_plan's choice at 2 ranks: the whole corpus each) and
+    row-sharded (GEOBPE_RANK_PLAN=shard: the exchange path the plan takes from 4 ranks)."""
     common = ["--config", "c2", "--warmup", "3", "--steps", "5", "--emit-merges", "--no-cpu-baseline", "--no-replay"]
     two = _line(_run(["--gpus", "2", "--dist-backend", "gloo", *common]))
+    rows = _line(_run(["--gpus", "2", "--dist-backend", "gloo", *common], env={"GEOBPE_RANK_PLAN": "shard"}))
     one = _line(_run(["--gpus", "1", *common]))
-    assert two["n_gpus"] == 2 and one["n_gpus"] == 1
-    assert len(two["config"]["rank_residues"]) == 2 and sum(two["config"]["rank_residues"]) == two["config"]["residues"]
-    assert two["steps"] == 5 and len(two["merge_list"]) == 8
-    assert two["merge_list"] == one["merge_list"]
+    assert two["n_gpus"] == 2 and rows["n_gpus"] == 2 and one["n_gpus"] == 1
+    assert two["config"]["parallelism"] == "replicas2" and rows["config"]["parallelism"] == "rows2"
+    assert two["config"]["rank_residues"] == [two["config"]["residues"]] * 2
+    assert len(rows["config"]["rank_residues"]) == 2 and sum(rows["config"]["rank_residues"]) == rows["config"]["residues"]
+    assert two["steps"] == 5 and len(two["merge_list"]) == 8 and rows["steps"] == 5
+    assert two["merge_list"] == one["merge_list"] and rows["merge_list"] == one["merge_list"]

@@ -173,3 +173,21 @@ def test_multirank_engine_on_one_gpu_matches_single(world, mode, oracle_lib):
     assert all(r[2] == o.merges for r in res)
     _, ids, _ = o.segmentation()
     assert sum((r[3] for r in res), []) == ids.tolist()
+
+
+def test_rank_plan_replicates_below_the_measured_crossover(monkeypatch):
+    """bench.py's choice per world size (geobpe.dist.rank_plan): replicas below SHARD_MIN_RANKS,
+    where one rank's share with the exchange measured slower than the whole corpus alone."""
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "pt-bpe_amd"))
+    from geobpe.dist import SHARD_MIN_RANKS, rank_plan
+
+    monkeypatch.delenv("GEOBPE_RANK_PLAN", raising=False)
+    assert SHARD_MIN_RANKS == 4
+    assert [rank_plan(w) for w in (1, 2, 3, 4, 8)] == ["replicate", "replicate", "replicate", "shard", "shard"]
+    monkeypatch.setenv("GEOBPE_RANK_PLAN", "shard")
+    assert rank_plan(2) == "shard" and rank_plan(1) == "replicate"
+    monkeypatch.setenv("GEOBPE_RANK_PLAN", "rows")
+    with pytest.raises(ValueError):
+        rank_plan(2)
