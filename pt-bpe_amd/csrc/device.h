@@ -31,8 +31,8 @@ constexpr int KL_CHUNK = 4096;  // klist entries a commit workgroup reserves at 
 // merge find -> commit hand-off (merge.h): per (owner, find workgroup) fixed record
 // slots, overflow to one global list
 constexpr int NBA_MAX = 256;
-constexpr int SK = 48;      // key records per (owner, find workgroup)
-constexpr int SD = 48;      // decrement records per (owner, find workgroup)
+constexpr int SK = 48;      // key-record slots per (owner, find workgroup); slot 0 holds decrements (below)
+constexpr int SD = 48;      // decrement records per (owner, find workgroup) past the DSH in slot 0
 constexpr int FKC = 2048;   // find: new-key dedupe slots (LDS) per round
 constexpr int CKC = 2048;   // commit: key dedupe slots (LDS) per owner
 constexpr int FMQ = 4096;    // find: candidate queue (LDS) per chunk of posting entries

@@ -170,6 +170,19 @@ __device__ inline void check_found(const Dev& D, int32_t r) {
 }
 
 // ---------------------------------------------------------------------- k_find
+// An (owner, finder) segment of KS is SK 48-B slots.  In the heavy merges a finder sends an owner
+// ~1.5 key records and ~1.5 decrement records, so each segment's writes are a few bytes of one
+// line: the first DSH decrement records therefore go into slot 0, in the line the key records
+// (slots 1..SK-1) dirty anyway, and only the rest into DS.  (Separate DS segments wrote one more
+// 64-B sector per segment: ~4 MB of k_find's ~16 MB written per heavy launch, all written back at
+// the kernel boundary.)
+constexpr int DSH = (int)(sizeof(KRec) / sizeof(int2));  // decrement records in slot 0
+constexpr int SKR = SK - 1;                              // key records per segment
+__device__ inline int64_t krec_at(int64_t seg, int32_t j) { return seg * SK + 1 + j; }
+__device__ inline int2* dec_at(const Dev& D, int64_t seg, int32_t j) {
+  return j < DSH ? reinterpret_cast<int2*>(D.KS + seg * SK) + j : D.DS + seg * SD + (j - DSH);
+}
+
 struct FHalf {  // a new neighbour pair of a merged occurrence
   u64 pkey, h1, h2;
   int32_t len, idL, g, idR, target;
@@ -243,8 +256,8 @@ __device__ inline int32_t emit_krec(const Dev& D, const FindCtx& F, int32_t* cur
   k.tstart = tstart;
   const int o = owner_of_key(D, h.pkey);
   const int32_t j = atomicAdd(&curK[o], 1);
-  if (j < SK) {
-    const int64_t at = ((int64_t)o * D.NBA + F.r) * SK + j;
+  if (j < SKR) {
+    const int64_t at = krec_at((int64_t)o * D.NBA + F.r, j);
     out_store(&D.KS[at], k);
     return (int32_t)at;
   }
@@ -636,14 +649,14 @@ __global__ __launch_bounds__(ABLOCK) void k_find(Dev D, int to_delta, int par) {
     if (k < 0 || v == 0) continue;
     const int ow = owner_of_slot(D, (u64)k);
     const int32_t j = atomicAdd(&S.curD[ow], 1);
-    if (j < SD)
-      out_store(&D.DS[((int64_t)ow * D.NBA + r) * SD + j], make_int2(k, v));
+    if (j < DSH + SD)
+      out_store(dec_at(D, (int64_t)ow * D.NBA + r, j), make_int2(k, v));
     else
       global_add(D, k, v, F.to_delta);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < D.NBA; i += ABLOCK) {
-    out_store(reinterpret_cast<int2*>(D.cntK) + cnt_at(D, i, r), make_int2(min(S.curK[i], SK), min(S.curD[i], SD)));
+    out_store(reinterpret_cast<int2*>(D.cntK) + cnt_at(D, i, r), make_int2(min(S.curK[i], SKR), min(S.curD[i], DSH + SD)));
   }
   if (threadIdx.x == 0) {
     out_store(&D.Lcnt[r], min(S.n, (int32_t)D.LC));
@@ -697,7 +710,7 @@ __device__ inline bool commit_rec(const Dev& D, const CommitLds& S, int32_t j, i
   const int32_t totK = S.preK[D.NBA];
   if (i < totK) {
     const int32_t w = seg_of(S.preK, D.NBA, i);
-    *at = ((int64_t)j * D.NBA + w) * SK + (i - S.preK[w]);
+    *at = krec_at((int64_t)j * D.NBA + w, i - S.preK[w]);
     k = D.KS[*at];
     return true;
   }
@@ -765,7 +778,7 @@ __device__ inline int64_t extra_at(const Dev& D, const int32_t* preE, int32_t nb
                                    int32_t i) {
   if (i < nE) {
     const int32_t ww = seg_of(preE, nba, i);
-    return ((int64_t)j * nba + ww) * SK + PER + (i - preE[ww]);
+    return krec_at((int64_t)j * nba + ww, PER + (i - preE[ww]));
   }
   return (int64_t)nba * nba * SK + (i - nE);
 }
@@ -1038,8 +1051,8 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   if (t == 0) tb.n = 0;
   dbg_stamp(D, 51);
   {  // records past the first PER of a finder's slot: prefix sums
-    const int32_t eK = t < nba ? max(0, min(cK, SK) - PER) : 0;
-    const int32_t eD = t < nba ? max(0, min(cD, SD) - PER) : 0;
+    const int32_t eK = t < nba ? max(0, min(cK, SKR) - PER) : 0;
+    const int32_t eD = t < nba ? max(0, min(cD, DSH + SD) - PER) : 0;
     int32_t totE, totF;
     const int32_t xE = block_excl_scan(eK, &totE, S.red);
     const int32_t xF = block_excl_scan(eD, &totF, S.red);
@@ -1067,9 +1080,9 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   // (unconditional loads from clamped slots, all of this round's loads issued before any wait: a
   // load inside `if` made the compiler wait for it at the join, r0 / d0 / e0 / x0 one after another)
   {
-    const bool hk = lane_ok && k0 < min(cK, SK), hd = lane_ok && k0 < min(cD, SD);
-    r0 = ld_rec(&D.KS[seg * SK + (hk ? k0 : 0)]);
-    const int2 d0r = ld_now(&D.DS[seg * SD + (hd ? k0 : 0)]);
+    const bool hk = lane_ok && k0 < min(cK, SKR), hd = lane_ok && k0 < min(cD, DSH + SD);
+    r0 = ld_rec(&D.KS[krec_at(seg, hk ? k0 : 0)]);
+    const int2 d0r = ld_now(dec_at(D, seg, hd ? k0 : 0));
     d0 = hd ? d0r : make_int2(0, 0);
   }
   // ---- round 1: key records -> LDS dedupe (occurrence totals per key); decrements -> LDS
@@ -1088,7 +1101,7 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
       commit_fallback<X>(D, S, hot, (k), tod, th);                   \
     }                                                             \
   } while (0)
-  const bool mine0 = lane_ok && k0 < min(cK, SK);
+  const bool mine0 = lane_ok && k0 < min(cK, SKR);
   const int32_t nE = s_preE[nba], nF = s_preF[nba], nKO = S.nKO;
   // this thread's first record past a slot's first PER (extras, then the overflow list) and
   // its first extra decrement record go out in the same round as r0 / d0: the owners with
@@ -1101,17 +1114,17 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   int2 x0 = make_int2(-1, 0);
   {
     if (he) at0 = extra_at(D, s_preE, nba, j, PER, nE, t);
-    int64_t xa = 0;
+    const int2* xa = D.DS;
     if (t < nF) {
       const int32_t ww = seg_of(s_preF, nba, t);
-      xa = ((int64_t)j * nba + ww) * SD + PER + (t - s_preF[ww]);
+      xa = dec_at(D, (int64_t)j * nba + ww, PER + (t - s_preF[ww]));
     }
     e0 = ld_rec(&D.KS[at0]);
-    const int2 x0r = ld_now(&D.DS[xa]);
+    const int2 x0r = ld_now(xa);
     x0 = t < nF ? x0r : make_int2(-1, 0);
   }
   if (mine0) COMMIT_INSERT(r0);
-  if (lane_ok && k0 < min(cD, SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add<X>(D, d0.x, d0.y, tod);
+  if (lane_ok && k0 < min(cD, DSH + SD) && !agg_stage(S.u.agg, d0.x, d0.y)) commit_add<X>(D, d0.x, d0.y, tod);
   dbg_stamp(D, 56);
   if (he && (t < nE || owner_of_key(D, e0.pkey) == j)) COMMIT_INSERT(e0);
   for (int32_t i = t + ABLOCK; i < nE + nKO; i += ABLOCK) {  // (rare: more than ABLOCK extras)
@@ -1123,14 +1136,14 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   if (t < nF && !agg_stage(S.u.agg, x0.x, x0.y)) commit_add<X>(D, x0.x, x0.y, tod);
   for (int32_t i = t + ABLOCK; i < nF; i += ABLOCK) {
     const int32_t ww = seg_of(s_preF, nba, i);
-    const int2 x = D.DS[((int64_t)j * nba + ww) * SD + PER + (i - s_preF[ww])];
+    const int2 x = *dec_at(D, (int64_t)j * nba + ww, PER + (i - s_preF[ww]));
     if (!agg_stage(S.u.agg, x.x, x.y)) commit_add<X>(D, x.x, x.y, tod);
   }
   dbg_stamp(D, 58);
   __syncthreads();
   dbg_stamp(D, 2);
   if (D.dbg) {  // (debug timeline: this owner's work, block-uniform)
-    const int32_t nr = __syncthreads_count(mine0), nd = __syncthreads_count(lane_ok && k0 < min(cD, SD));
+    const int32_t nr = __syncthreads_count(mine0), nd = __syncthreads_count(lane_ok && k0 < min(cD, DSH + SD));
     dbg_val(D, 7, nr + nE + nKO);
     dbg_val(D, 8, nd + nF);
   }
@@ -1231,7 +1244,7 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
     int32_t tk, tr, td;
     block_excl_scan(nkeys, &tk, S.red);
     block_excl_scan(mine0 ? 1 : 0, &tr, S.red);
-    block_excl_scan(lane_ok && k0 < min(cD, SD) ? 1 : 0, &td, S.red);
+    block_excl_scan(lane_ok && k0 < min(cD, DSH + SD) ? 1 : 0, &td, S.red);
     if (t == 0) {
       atomicAdd((unsigned long long*)&st->stat_keys, (unsigned long long)tk);
       atomicAdd((unsigned long long*)&st->stat_krec, (unsigned long long)(tr + nE + nKO));
@@ -1251,7 +1264,7 @@ __device__ __attribute__((always_inline)) inline void commit_main(const Dev& D, 
   // ---- round 2: every record's key id and posting-log position (k_place writes pk
   // and the log entries of its occurrence slots); the first PER records per finder
   // are still in registers
-  commit_publish2(D, S, mine0, r0, seg * SK + k0, he && (t < nE || owner_of_key(D, e0.pkey) == j), e0, at0);
+  commit_publish2(D, S, mine0, r0, krec_at(seg, k0),he && (t < nE || owner_of_key(D, e0.pkey) == j), e0, at0);
   dbg_stamp(D, 53);
   dbg_val(D, 54, nE);
   dbg_val(D, 55, nKO);
@@ -1356,7 +1369,7 @@ __device__ inline int32_t place_owner(const Dev& D, int32_t at) {
 __device__ inline int32_t place_rec_at(const Dev& D, const PlaceLds& S, int32_t j, int32_t i, int32_t nk, int64_t k_lo) {
   if (i < nk) {
     const int32_t ow = seg_of(S.pre, D.NBA, i);
-    return (int32_t)(((int64_t)ow * D.NBA + j) * SK + (i - S.pre[ow]));
+    return (int32_t)krec_at((int64_t)ow * D.NBA + j, i - S.pre[ow]);
   }
   return (int32_t)((int64_t)D.NBA * D.NBA * SK + k_lo + (i - nk));
 }
