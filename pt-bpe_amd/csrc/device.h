@@ -219,7 +219,6 @@ struct Dev {
   int32_t* cntD;
   KRec* KO;         // overflow: key records past their fixed slots
   int64_t KO_cap;
-  int2 *KSid, *KOid;  // k_commit -> k_place: (key id, posting-log position) per record
   int2* T;          // [find wg][TC]: {occurrence slot, its key record (KS index)} grouped by new key
   int32_t* Tcnt;    // [find wg]: T entries
   int64_t TC;

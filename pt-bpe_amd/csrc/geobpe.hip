@@ -759,11 +759,9 @@ int geobpe_load_angles(geobpe_ctx* c, int64_t n_rows, const int64_t* h_row_off, 
       (rc = dalloc(c, &D.pnch, c->nba, 0)) || (rc = dalloc(c, &D.pfill, c->nba, 0)) ||
       (rc = dalloc(c, &D.KS, (int64_t)c->nba * c->nba * SK + D.KO_cap)) || (rc = dalloc(c, &D.cntK, 2 * (int64_t)c->nba * c->nba, 0)) ||
       (rc = dalloc(c, &D.DS, (int64_t)c->nba * c->nba * SD)) || (rc = dalloc(c, &D.cntD, (int64_t)c->nba * c->nba, 0)) ||
-      (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) || (rc = dalloc(c, &D.Tcnt, c->nba, 0)) ||
-      (rc = dalloc(c, &D.KSid, (int64_t)c->nba * c->nba * SK + D.KO_cap)))
+      (rc = dalloc(c, &D.T, (int64_t)c->nba * D.TC)) || (rc = dalloc(c, &D.Tcnt, c->nba, 0)))
     return rc;
   D.KO = D.KS + (int64_t)c->nba * c->nba * SK;  // (one allocation: a record index into KS covers both)
-  D.KOid = D.KSid + (int64_t)c->nba * c->nba * SK;
   const int need[6] = {GEOBPE_COL_PHI, GEOBPE_COL_PSI, GEOBPE_COL_OMEGA, GEOBPE_COL_TAU, GEOBPE_COL_CAC1N,
                        GEOBPE_COL_C1NCA};
   for (int q = 0; q < 6; q++) {

@@ -176,12 +176,23 @@ __device__ inline void check_found(const Dev& D, int32_t r) {
 // (slots 1..SK-1) dirty anyway, and only the rest into DS.  (Separate DS segments wrote one more
 // 64-B sector per segment: ~4 MB of k_find's ~16 MB written per heavy launch, all written back at
 // the kernel boundary.)
+// (The segment's record counts in slot 0 too, so that k_commit's first round found them in the
+// line of its records, measured no faster: k_find's 256 more scattered stores cost what the
+// commit saved, profiles/r6_ab/dsh/.)
 constexpr int DSH = (int)(sizeof(KRec) / sizeof(int2));  // decrement records in slot 0
 constexpr int SKR = SK - 1;                              // key records per segment
 __device__ inline int64_t krec_at(int64_t seg, int32_t j) { return seg * SK + 1 + j; }
 __device__ inline int2* dec_at(const Dev& D, int64_t seg, int32_t j) {
   return j < DSH ? reinterpret_cast<int2*>(D.KS + seg * SK) + j : D.DS + seg * SD + (j - DSH);
 }
+// k_commit -> k_place: a published record's {key id, posting-log position} overwrites its {g, idR}
+// (read only by the commit's resolve, before the publish), so k_place's one 16-B load of the
+// record's tail {id, log position, n, tstart} is one line (a separate id array was a second
+// line per record, and one more dirty sector per segment at the commit's end)
+static_assert(offsetof(KRec, g) == 32 && offsetof(KRec, idR) == 36 && offsetof(KRec, n) == 40 &&
+                  offsetof(KRec, tstart) == 44, "a record's 16-B tail");
+__device__ inline int2* rec_id(const Dev& D, int64_t at) { return reinterpret_cast<int2*>(&D.KS[at].g); }
+__device__ inline int4 rec_tail(const Dev& D, int64_t at) { return ld_now_t(reinterpret_cast<const int4*>(&D.KS[at].g)); }
 
 struct FHalf {  // a new neighbour pair of a merged occurrence
   u64 pkey, h1, h2;
@@ -880,8 +891,8 @@ __device__ __attribute__((always_inline)) inline void commit_publish2(const Dev&
   const int32_t n0 = m0 && d0 >= 0 ? k0.n : 0, n1 = m1 && d1 >= 0 ? k1.n : 0;
   int32_t tot;
   const int32_t ex = block_excl_scan(n0 + n1, &tot, S.red);
-  if (m0) D.KSid[at0] = make_int2(d0 >= 0 ? d0 : -1, S.logok && d0 >= 0 ? (int32_t)(S.logpos + ex) : -1);
-  if (m1) D.KSid[at1] = make_int2(d1 >= 0 ? d1 : -1, S.logok && d1 >= 0 ? (int32_t)(S.logpos + ex + n0) : -1);
+  if (m0) *rec_id(D, at0) = make_int2(d0 >= 0 ? d0 : -1, S.logok && d0 >= 0 ? (int32_t)(S.logpos + ex) : -1);
+  if (m1) *rec_id(D, at1) = make_int2(d1 >= 0 ? d1 : -1, S.logok && d1 >= 0 ? (int32_t)(S.logpos + ex + n0) : -1);
   __syncthreads();
   if (threadIdx.x == 0) S.logpos += tot;
 }
@@ -894,7 +905,7 @@ __device__ __attribute__((always_inline)) inline void commit_publish(const Dev& 
   const int32_t ex = block_excl_scan(n, &tot, S.red);
   if (mine) {
     const int2 v = make_int2(d >= 0 ? d : -1, S.logok && d >= 0 ? (int32_t)(S.logpos + ex) : -1);
-    D.KSid[at] = v;
+    *rec_id(D, at) = v;
   }
   __syncthreads();
   if (threadIdx.x == 0) S.logpos += tot;
@@ -1441,10 +1452,9 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   // sets made the compiler wait for it at the join, one group after the other)
   const bool h0 = t < nT && te0.y >= 0, h1 = t + ABLOCK < nT && te1.y >= 0;
   const int32_t a0 = h0 ? te0.y : 0, a1 = h1 ? te1.y : 0;
-  const int2 v0r = ld_now(&D.KSid[a0]), v1r = ld_now(&D.KSid[a1]);
-  const int32_t ts0r = ld_now(&D.KS[a0].tstart), ts1r = ld_now(&D.KS[a1].tstart);
-  const int2 v0 = h0 ? v0r : make_int2(-1, -1), v1 = h1 ? v1r : make_int2(-1, -1);
-  const int32_t ts0 = h0 ? ts0r : 0, ts1 = h1 ? ts1r : 0;
+  const int4 q0 = rec_tail(D, a0), q1 = rec_tail(D, a1);
+  const int2 v0 = h0 ? make_int2(q0.x, q0.y) : make_int2(-1, -1), v1 = h1 ? make_int2(q1.x, q1.y) : make_int2(-1, -1);
+  const int32_t ts0 = h0 ? q0.w : 0, ts1 = h1 ? q1.w : 0;
   const int64_t oper = (novf + D.NBA - 1) / D.NBA;
   const int64_t o_lo = (int64_t)j * oper, o_n = max((int64_t)0, min(novf, o_lo + oper) - o_lo);
   const int64_t kper = (nko + D.NBA - 1) / D.NBA;
@@ -1462,8 +1472,8 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   // ---- round 2, part 2: the records of this finder's slots (their ranges need the scan)
   const bool hr = t < nrec;
   const int32_t ra = hr ? place_rec_at(D, S, j, t, nk, k_lo) : 0;
-  const int2 rnt_r = ld_now(reinterpret_cast<const int2*>(&D.KS[ra].n)), rv_r = ld_now(&D.KSid[ra]);
-  const int2 rnt = hr ? rnt_r : make_int2(0, 0), rv = hr ? rv_r : make_int2(-1, -1);
+  const int4 rq = rec_tail(D, ra);
+  const int2 rnt = hr ? make_int2(rq.z, rq.w) : make_int2(0, 0), rv = hr ? make_int2(rq.x, rq.y) : make_int2(-1, -1);
   dbg_stamp(D, 37);
   // ---- the token rewrites of find region j (round 1's data).  The thread's first entry comes from
   // registers with no load on its path (a conditional load there made the compiler wait for every
@@ -1480,11 +1490,15 @@ __device__ void place_body(const Dev& D, int32_t j, PlaceLds& S) {
   if (h1) place_tentry(D, qbase + t + ABLOCK, te1, v1, ts1);
   for (int32_t i = t + ABLOCK; i < nrec; i += ABLOCK) {  // (rare: more records than threads)
     const int32_t at = place_rec_at(D, S, j, i, nk, k_lo);
-    place_single(D, at, *reinterpret_cast<const int2*>(&D.KS[at].n), D.KSid[at]);
+    const int4 q = rec_tail(D, at);
+    place_single(D, at, make_int2(q.z, q.w), make_int2(q.x, q.y));
   }
   for (int32_t q = t + 2 * ABLOCK; q < nT; q += ABLOCK) {  // (rare: more than 2 per thread)
     const int2 e = Tj[q];
-    if (e.y >= 0) place_tentry(D, qbase + q, e, D.KSid[e.y], D.KS[e.y].tstart);
+    if (e.y >= 0) {
+      const int4 r = rec_tail(D, e.y);
+      place_tentry(D, qbase + q, e, make_int2(r.x, r.y), r.w);
+    }
   }
   dbg_stamp(D, 32);
 }
